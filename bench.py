@@ -1,0 +1,301 @@
+#!/usr/bin/env python3
+"""Benchmark of the hot path: hypergraph-conv fwd+bwd M-edges/s at emb_dim=64, % HBM roofline.
+
+A step is one forward + backward of the HGNN-normalised 2-hop conv
+``Y = D_v^-1/2·H·D_e^-1·Hᵀ·D_v^-1/2·X`` (data/graph.py:28-42 of the reference) over one
+synthetic user×item incidence H, i.e. four hgd_spmm hops: CSC (into items) + CSR (into users)
+forward, the same pair backward. Unit of work = one nonzero of H.
+
+    python bench.py [--gpus N --steps K --warmup W --workload synthetic|ml1m|yelp|amazon|zipf]
+
+N > 1 runs one process per GPU under torch.distributed.run (RCCL): every rank owns its own
+block of users (weak scaling: fixed users/edges per GPU, items shared) and the item sums are
+all-reduced over xGMI in each hop (hypergraph_diffusion_for_recommendation_amd/sharded.py).
+
+Rank 0 prints ONE JSON line. ``roofline`` prices the dominant kernel (hgd_spmm) from HIP events
+recorded around every hop launch on its stream during the timed steps; ``cpu_baseline`` times the
+reference's own library calls (torch.sparse.mm + autograd on CPU, oracle/ref_cpu.py) on a bounded
+sample of the same generator, on this box's host cores.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+METRIC = "hypergraph-conv fwd+bwd M-edges/sec at emb_dim=64; % HBM roofline"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+# users, items, edges per GPU (SURVEY.md §8 config sizes; dataset shapes are public statistics
+# with the reference's 75 % train split, not shipped data)
+WORKLOADS = {
+    "synthetic": (10_000_000, 1_000_000, 100_000_000, None),
+    "zipf": (10_000_000, 1_000_000, 100_000_000, 1.0),
+    "ml1m": (6_040, 3_706, 750_000, None),
+    "yelp": (31_668, 38_048, 1_170_000, None),
+    "amazon": (52_643, 91_599, 2_240_000, None),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="synthetic", choices=sorted(WORKLOADS))
+    ap.add_argument("--dim", type=int, default=64)
+    ap.add_argument("--users", type=int, default=None)
+    ap.add_argument("--items", type=int, default=None)
+    ap.add_argument("--edges", type=int, default=None)
+    ap.add_argument("--chunks", type=int, default=4, help="item chunks for the overlapped all-reduce")
+    ap.add_argument("--cpu-sample-edges", type=int, default=10_000_000)
+    ap.add_argument("--cpu-budget-s", type=float, default=25.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc", default="auto", choices=["auto", "on", "off"],
+                    help="measure HBM traffic with rocprofv3 PMC passes in a child process")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    return ap.parse_args()
+
+
+def make_graph(U, I, E, seed, zipf, device):
+    """Synthetic incidence on the device: uniform users, uniform (or Zipf) items, deduplicated,
+    row-major sorted (torch generator seeded per rank; the bench's data, not the product)."""
+    import torch
+    g = torch.Generator(device=device).manual_seed(seed)
+    u = torch.randint(0, U, (E,), device=device, generator=g, dtype=torch.int64)
+    if zipf is None:
+        i = torch.randint(0, I, (E,), device=device, generator=g, dtype=torch.int64)
+    else:
+        ranks = torch.arange(1, I + 1, device=device, dtype=torch.float64)
+        p = ranks.pow(-float(zipf))
+        i = torch.multinomial((p / p.sum()).float(), E, replacement=True, generator=g)
+    key = torch.unique(u * I + i)
+    del u, i
+    return torch.stack([key // I, key % I])
+
+
+def cpu_baseline(U, I, E, zipf, sample_edges, budget_s, d):
+    """oracle/ref_cpu.py (torch.sparse.mm + autograd, the reference's own calls) on a bounded,
+    proportionally scaled sample of the same generator; median M-edges/s."""
+    import numpy as np
+    import torch
+
+    from oracle import hgd_oracle as O
+    from oracle import ref_cpu
+
+    f = min(1.0, sample_edges / E)
+    u_s, i_s, e_s = max(1, int(U * f)), max(1, int(I * f)), max(1, int(E * f))
+    rows, cols = O.synthetic_incidence(u_s, i_s, e_s, seed=0, zipf=zipf)
+    H = ref_cpu.coo_tensor(rows, cols, None, (u_s, i_s))
+    g = torch.Generator().manual_seed(1)
+    X = torch.empty(u_s, d)
+    torch.nn.init.xavier_uniform_(X, generator=g)
+    dY = torch.randn(u_s, d, generator=g)
+    times = []
+    t_start = time.perf_counter()
+    ref_cpu.hgconv2_fwd_bwd(H, X, dY)  # warm-up
+    while len(times) < 5 and (time.perf_counter() - t_start) < budget_s or len(times) < 1:
+        t0 = time.perf_counter()
+        ref_cpu.hgconv2_fwd_bwd(H, X, dY)
+        times.append(time.perf_counter() - t0)
+    t = statistics.median(times)
+    return {
+        "value": round(len(rows) / t / 1e6, 3),
+        "unit": "M-edges/s",
+        "cores": torch.get_num_threads(),
+        "kind": "port",
+        "sample": (f"{u_s}x{i_s} graph, {len(rows)} edges (same generator scaled by {f:.3g}), "
+                   f"d={d}, torch.sparse.mm fwd+bwd (oracle/ref_cpu.py), median of "
+                   f"{len(times)} runs, {t:.3f} s/run"),
+    }
+
+
+def pmc_traffic(args, U, I, E):
+    """Runs this script under rocprofv3 twice (FETCH_SIZE, WRITE_SIZE) as a child process and
+    returns HBM bytes per hgd_spmm launch: (FETCH_SIZE·2 + WRITE_SIZE)·1024 (gfx950 FETCH_SIZE
+    reads half the bytes of wide streaming reads: MI355X_MICROARCH.md §HBM)."""
+    import csv
+    import glob
+    import shutil
+    import tempfile
+    rp = shutil.which("rocprofv3")
+    if not rp:
+        return None, "rocprofv3 not found"
+    out = {}
+    tmp = tempfile.mkdtemp(prefix="hgd_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = os.path.join(tmp, ctr)
+        cmd = [rp, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "run", "--",
+               sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "2",
+               "--warmup", "1", "--workload", args.workload, "--dim", str(args.dim),
+               "--users", str(U), "--items", str(I), "--edges", str(E)]
+        try:
+            subprocess.run(cmd, check=True, timeout=600, stdout=subprocess.DEVNULL,
+                           stderr=subprocess.DEVNULL)
+        except Exception as exc:  # noqa: BLE001 — report, never fail the bench
+            return None, f"rocprofv3 {ctr} pass failed: {exc}"
+        files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+        if not files:
+            return None, f"no counter csv for {ctr}"
+        vals = []
+        with open(files[0]) as fh:
+            for row in csv.DictReader(fh):
+                if "spmm_kernel" in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
+                    vals.append(float(row["Counter_Value"]))
+        if not vals:
+            return None, f"no spmm_kernel rows for {ctr}"
+        out[ctr] = statistics.mean(vals)
+    shutil.rmtree(tmp, ignore_errors=True)
+    traffic = (out["FETCH_SIZE"] * 2.0 + out["WRITE_SIZE"]) * 1024.0
+    return traffic, f"FETCH_SIZE={out['FETCH_SIZE']:.0f}KB WRITE_SIZE={out['WRITE_SIZE']:.0f}KB per launch"
+
+
+def main():
+    args = parse()
+    U0, I0, E0, zipf = WORKLOADS[args.workload]
+    U = args.users or U0
+    I = args.items or I0
+    E = args.edges or E0
+    d = args.dim
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    pmc = None
+    pmc_note = None
+    want_pmc = (args.pmc == "on" or (args.pmc == "auto" and world == 1 and args.gpus == 1
+                                     and args.workload in ("synthetic", "zipf")))
+    if want_pmc and not args.pmc_child:
+        # child profiler processes run BEFORE this process touches the GPU
+        pmc, pmc_note = pmc_traffic(args, U, I, E)
+
+    import torch
+    import torch.distributed as dist
+
+    from hypergraph_diffusion_for_recommendation_amd import Incidence, profiling
+    from hypergraph_diffusion_for_recommendation_amd.sharded import (ShardedIncidence,
+                                                                       sharded_two_hop)
+
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+    device = torch.device(f"cuda:{local_rank}")
+
+    idx = make_graph(U, I, E, seed=rank, zipf=zipf, device=device)
+    nnz = int(idx.shape[1])
+    inc = Incidence.from_coo(idx, None, (U, I), device=device, validate=False, rows_sorted=True)
+    del idx
+    sh = ShardedIncidence(inc, n_chunks=args.chunks, P="sym", Q="mean", R="sym")
+    g = torch.Generator(device=device).manual_seed(1000 + rank)
+    X = torch.empty(U, d, device=device)
+    bound = (6.0 / (U + d)) ** 0.5  # xavier_uniform_ on [U, d] (HCCF.py:164-169)
+    X.uniform_(-bound, bound, generator=g)
+    X.requires_grad_(True)
+    dY = torch.randn(U, d, device=device, generator=g)
+    # warm the scale / edge-value caches outside the timed region
+    inc.scale("row", "sym"), inc.edge_values("csc", "sym")
+
+    def step():
+        Y = sharded_two_hop(sh, X)
+        (dX,) = torch.autograd.grad(Y, X, dY)
+        return dX
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    timer = profiling.HopTimer()
+    t0 = time.perf_counter()
+    with timer:
+        for _ in range(args.steps):
+            step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        tot = torch.tensor([nnz], dtype=torch.float64, device=device)
+        dist.all_reduce(tot)
+        total_edges = float(tot.item())
+    else:
+        total_edges = float(nnz)
+
+    if args.pmc_child:
+        return
+    hop = timer.summary()
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    value = total_edges * args.steps / elapsed / 1e6
+    achieved = hop["avg_bytes"] / (hop["avg_ms"] * 1e-3) / 1e9 if hop["avg_ms"] > 0 else 0.0
+    roofline = {
+        "bound": "hbm",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBPS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBPS, 4),
+        "traffic": None if pmc is None else round(pmc / 1.0),
+        "kernel": "hgd::spmm_kernel (hgd_spmm hop)",
+        "algorithmic_bytes_per_launch": round(hop["avg_bytes"]),
+        "avg_launch_ms": round(hop["avg_ms"], 4),
+        "launches_timed": hop["launches"],
+    }
+    if pmc_note:
+        roofline["traffic_note"] = pmc_note
+    if pmc is not None:
+        roofline["traffic_over_algorithmic"] = round(pmc / hop["avg_bytes"], 3)
+
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        cpu = cpu_baseline(U, I, E, zipf, args.cpu_sample_edges, args.cpu_budget_s, d)
+
+    out = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "M-edges/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": ("synthetic: per-GPU uniform user x item incidence (torch generator seed=rank, "
+                 "dedup), xavier_uniform X, N(0,1) dY"),
+        "config": {
+            "workload": f"{args.workload}-{U}x{I}x{E}-d{d}",
+            "users_per_gpu": U, "items": I, "edges_per_gpu_requested": E,
+            "edges_per_gpu": nnz, "emb_dim": d,
+            "op": "hgconv2 fwd+bwd: D_v^-1/2 H D_e^-1 H^T D_v^-1/2 X, 4 hgd_spmm hops",
+            "parallelism": (f"user-row shards x{world}, RCCL all-reduce of item sums "
+                            f"({args.chunks} chunks)" if world > 1 else "single GPU"),
+        },
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,128 @@
+"""ctypes binding of libhgd.so (the C ABI declared in include/hgd.h).
+
+The product path goes through this module only: there is no CPU or PyTorch fallback. If the
+shared library is missing the first call raises ``HGDNativeError`` telling how to build it
+(``python -c "import __graft_entry__ as g; g.build()"`` or ``make -C .../csrc``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("HGD_LIB_PATH", os.path.join(_HERE, "_lib", "libhgd.so"))
+
+c_void_p = ctypes.c_void_p
+c_i64 = ctypes.c_int64
+c_i32 = ctypes.c_int32
+c_f32 = ctypes.c_float
+c_f64 = ctypes.c_double
+c_size = ctypes.c_size_t
+
+HGD_OK = 0
+EPI_NONE, EPI_LEAKY_RELU, EPI_RELU = 0, 1, 2
+_STATUS_NAMES = {0: "HGD_OK", 1: "HGD_ERR_INVALID_ARG", 2: "HGD_ERR_HIP",
+                 3: "HGD_ERR_UNSUPPORTED", 4: "HGD_ERR_WORKSPACE"}
+
+
+class HGDNativeError(RuntimeError):
+    """Raised when libhgd is missing or a call returns a non-OK hgd_status."""
+
+
+class SplitPlan(ctypes.Structure):
+    """Mirror of ``hgd_split_plan`` (include/hgd.h)."""
+
+    _fields_ = [
+        ("threshold", c_i64),
+        ("chunk", c_i32),
+        ("_pad", c_i32),
+        ("n_heavy", c_i64),
+        ("n_chunks", c_i64),
+        ("heavy_rows", c_void_p),
+        ("heavy_cptr", c_void_p),
+        ("chunk_heavy", c_void_p),
+    ]
+
+
+# name -> (restype, argtypes); every symbol of include/hgd.h appears here.
+_SIGNATURES = {
+    "hgd_version": (c_i32, []),
+    "hgd_get_last_error_string": (ctypes.c_char_p, []),
+    "hgd_split_plan_count": (c_i32, [c_void_p, c_i64, c_i64, c_i32, c_void_p, c_void_p]),
+    "hgd_split_plan_workspace_size": (c_size, [c_i64]),
+    "hgd_split_plan_build": (c_i32, [c_void_p, c_i64, c_i64, c_i32, c_void_p, c_void_p, c_void_p,
+                                     c_i64, c_i64, c_void_p, c_size, c_void_p]),
+    "hgd_spmm_workspace_size": (c_size, [ctypes.POINTER(SplitPlan), c_i32]),
+    "hgd_spmm": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_i64, c_i64, c_i64,
+                         c_void_p, c_i64, c_void_p, c_i64, c_i32, c_i32, c_f32,
+                         ctypes.POINTER(SplitPlan), c_void_p, c_size, c_void_p]),
+    "hgd_index_narrow": (c_i32, [c_void_p, c_i64, c_i64, c_void_p, c_void_p, c_void_p]),
+    "hgd_sort_perm_workspace_size": (c_size, [c_i64]),
+    "hgd_sort_perm": (c_i32, [c_void_p, c_i64, c_i64, c_void_p, c_void_p, c_void_p, c_size,
+                              c_void_p]),
+    "hgd_rowptr_from_sorted": (c_i32, [c_void_p, c_i64, c_i64, c_void_p, c_void_p]),
+    "hgd_check_sorted": (c_i32, [c_void_p, c_i64, c_i64, c_void_p, c_void_p]),
+    "hgd_expand_rows": (c_i32, [c_void_p, c_i64, c_i64, c_void_p, c_void_p]),
+    "hgd_gather32": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p, c_void_p]),
+    "hgd_degree_scale": (c_i32, [c_void_p, c_void_p, c_i64, c_f64, c_void_p, c_void_p]),
+    "hgd_edge_values": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_void_p,
+                                c_void_p]),
+    "hgd_dropedge_workspace_size": (c_size, [c_i64]),
+    "hgd_dropedge_compact": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_f32,
+                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size,
+                                     c_void_p]),
+    "hgd_dense_threshold_workspace_size": (c_size, [c_i64]),
+    "hgd_dense_threshold_rowptr": (c_i32, [c_void_p, c_i64, c_i64, c_i64, c_f32, c_void_p,
+                                           c_void_p, c_size, c_void_p]),
+    "hgd_dense_threshold_fill": (c_i32, [c_void_p, c_i64, c_i64, c_i64, c_f32, c_void_p,
+                                         c_void_p, c_void_p]),
+    "hgd_epilogue_apply": (c_i32, [c_void_p, c_i64, c_i32, c_f32, c_void_p, c_void_p]),
+    "hgd_epilogue_backward": (c_i32, [c_void_p, c_void_p, c_i64, c_i32, c_f32, c_void_p,
+                                      c_void_p]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load() -> ctypes.CDLL:
+    """Loads libhgd.so once and binds every ABI symbol; raises HGDNativeError if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise HGDNativeError(
+                f"libhgd.so not found at {LIB_PATH}; build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` "
+                "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def symbols():
+    return list(_SIGNATURES)
+
+
+def check(status: int, what: str) -> None:
+    if status != HGD_OK:
+        msg = load().hgd_get_last_error_string().decode(errors="replace")
+        raise HGDNativeError(f"{what}: {_STATUS_NAMES.get(status, status)}: {msg}")
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a tensor (None for None)."""
+    return None if t is None else t.data_ptr()
+
+
+def stream_handle(device=None) -> int:
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream

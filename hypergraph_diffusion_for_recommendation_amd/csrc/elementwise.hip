@@ -1,0 +1,82 @@
+// Elementwise epilogue kernels around the SpMM hops (HBM streaming, float4 vectorised).
+//   forward : nn.LeakyReLU / nn.ReLU applied after the second hop (HGCNConv act=True,
+//             model/graph/HGNN_HD4.py:459-460, model/graph/HGCN.py:171-173) when it cannot be
+//             fused into hgd_spmm's store (negative slope).
+//   backward: dZ = dY * (ref > 0 ? 1 : slope) — torch's leaky_relu_backward on the saved
+//             pre-activation, or on the output when slope >= 0 (same sign).
+#include "hgd_internal.h"
+
+namespace hgd {
+
+__device__ __forceinline__ float epi_fwd(float z, int epi, float slope) {
+  if (epi == HGD_EPI_LEAKY_RELU) return z > 0.f ? z : z * slope;
+  if (epi == HGD_EPI_RELU) return z > 0.f ? z : 0.f;
+  return z;
+}
+
+__device__ __forceinline__ float epi_bwd(float ref, float dy, int epi, float slope) {
+  if (epi == HGD_EPI_LEAKY_RELU) return ref > 0.f ? dy : dy * slope;
+  if (epi == HGD_EPI_RELU) return ref > 0.f ? dy : 0.f;
+  return dy;
+}
+
+__global__ void k_epi_apply(const float* __restrict__ z, int64_t n, int epi, float slope,
+                            float* __restrict__ y) {
+  const int64_t i4 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) * 4;
+  if (i4 + 3 < n) {
+    float4 v = *reinterpret_cast<const float4*>(z + i4);
+    v.x = epi_fwd(v.x, epi, slope);
+    v.y = epi_fwd(v.y, epi, slope);
+    v.z = epi_fwd(v.z, epi, slope);
+    v.w = epi_fwd(v.w, epi, slope);
+    *reinterpret_cast<float4*>(y + i4) = v;
+  } else {
+    for (int64_t i = i4; i < n; ++i) y[i] = epi_fwd(z[i], epi, slope);
+  }
+}
+
+__global__ void k_epi_backward(const float* __restrict__ ref, const float* __restrict__ dy,
+                               int64_t n, int epi, float slope, float* __restrict__ dz) {
+  const int64_t i4 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) * 4;
+  if (i4 + 3 < n) {
+    const float4 r = *reinterpret_cast<const float4*>(ref + i4);
+    float4 g = *reinterpret_cast<const float4*>(dy + i4);
+    g.x = epi_bwd(r.x, g.x, epi, slope);
+    g.y = epi_bwd(r.y, g.y, epi, slope);
+    g.z = epi_bwd(r.z, g.z, epi, slope);
+    g.w = epi_bwd(r.w, g.w, epi, slope);
+    *reinterpret_cast<float4*>(dz + i4) = g;
+  } else {
+    for (int64_t i = i4; i < n; ++i) dz[i] = epi_bwd(ref[i], dy[i], epi, slope);
+  }
+}
+
+inline bool aligned16(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
+
+}  // namespace hgd
+
+using namespace hgd;
+
+extern "C" hgd_status hgd_epilogue_apply(const float* z, int64_t n, int32_t epilogue, float slope,
+                                         float* y, void* stream) {
+  clear_error();
+  HGD_REQUIRE(n >= 0, "hgd_epilogue_apply: n < 0");
+  if (n == 0) return HGD_OK;
+  HGD_REQUIRE(z && y && aligned16(z) && aligned16(y), "hgd_epilogue_apply: null/unaligned");
+  hipLaunchKernelGGL(k_epi_apply, dim3(grid_for((n + 3) / 4)), dim3(kBlock), 0,
+                     as_stream(stream), z, n, epilogue, slope, y);
+  return check_launch("hgd_epilogue_apply");
+}
+
+extern "C" hgd_status hgd_epilogue_backward(const float* ref, const float* dy, int64_t n,
+                                            int32_t epilogue, float slope, float* dz,
+                                            void* stream) {
+  clear_error();
+  HGD_REQUIRE(n >= 0, "hgd_epilogue_backward: n < 0");
+  if (n == 0) return HGD_OK;
+  HGD_REQUIRE(ref && dy && dz && aligned16(ref) && aligned16(dy) && aligned16(dz),
+              "hgd_epilogue_backward: null/unaligned");
+  hipLaunchKernelGGL(k_epi_backward, dim3(grid_for((n + 3) / 4)), dim3(kBlock), 0,
+                     as_stream(stream), ref, dy, n, epilogue, slope, dz);
+  return check_launch("hgd_epilogue_backward");
+}

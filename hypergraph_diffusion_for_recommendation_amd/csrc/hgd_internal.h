@@ -1,0 +1,58 @@
+// Internal helpers shared by the libhgd translation units (not part of the ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+
+#include "../../include/hgd.h"
+
+namespace hgd {
+
+// Thread-local last-error text returned by hgd_get_last_error_string().
+extern thread_local char g_last_error[512];
+
+inline hgd_status fail(hgd_status st, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_last_error, sizeof(g_last_error), fmt, ap);
+  va_end(ap);
+  return st;
+}
+
+inline void clear_error() { g_last_error[0] = '\0'; }
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Checks the most recent launch; turns a HIP error into HGD_ERR_HIP with context.
+inline hgd_status check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(HGD_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+  return HGD_OK;
+}
+
+#define HGD_REQUIRE(cond, ...)                                   \
+  do {                                                           \
+    if (!(cond)) return ::hgd::fail(HGD_ERR_INVALID_ARG, __VA_ARGS__); \
+  } while (0)
+
+#define HGD_HIP(call)                                                              \
+  do {                                                                             \
+    hipError_t _e = (call);                                                        \
+    if (_e != hipSuccess)                                                          \
+      return ::hgd::fail(HGD_ERR_HIP, "%s failed: %s", #call, hipGetErrorString(_e)); \
+  } while (0)
+
+constexpr int kBlock = 256;
+
+inline unsigned grid_for(int64_t n, int per_block = kBlock) {
+  int64_t g = (n + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  return static_cast<unsigned>(g);
+}
+
+inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
+
+}  // namespace hgd

@@ -1,0 +1,318 @@
+// CSR row-gather SpMM hop for gfx950 (CDNA4, wave64).
+//
+// Replaces torch.sparse.mm(adj, X) / torch.sparse.mm(adj.t(), X) (HCCF.py:199, HGNN_HD4.py:459-462,
+// HGCN.py:173-175) and the torch_scatter mean pair (layers2/EquivSetConv2.py:88-93) of the
+// reference (paths relative to /root/reference/HD_SELFRec).
+//
+// Work mapping (HBM-bound gather, ~0.5 flop/B; no MFMA):
+//   * one row of Y per group of G lanes; each lane owns VEC contiguous columns, so a group moves
+//     one gathered X row per load instruction (d=64: G=16 lanes × float4 = 256 B, 4 rows per wave);
+//   * the group loads G column indices (and weights) with one coalesced load and broadcasts them
+//     with __shfl, then issues U independent row gathers before consuming any of them, so every
+//     lane keeps U×16 B in flight (U=8: 8 KB per wave at d=64);
+//   * the sum runs in edge order in fp32 (single accumulator, fmaf), so results are deterministic;
+//   * rows longer than the split plan's threshold are cut into fixed-size chunks handled by extra
+//     blocks placed FIRST in the grid (they are the longest work items); a fix-up kernel sums the
+//     chunk partials in chunk order — no float atomics anywhere.
+#include "hgd_internal.h"
+
+namespace hgd {
+
+struct SpmmArgs {
+  const int64_t* rowptr;
+  const int32_t* col;
+  const float* val;
+  const float* row_scale;
+  int64_t row_begin, row_end;
+  const float* X;
+  int64_t ldx;
+  float* Y;
+  int64_t ldy;
+  int32_t d;
+  int32_t col0;  // first column handled by this launch (column passes for wide/odd d)
+  int32_t epi;
+  float slope;
+  // split plan
+  int64_t heavy_threshold;
+  int64_t n_chunks;
+  int64_t n_heavy;
+  int32_t chunk;
+  int32_t _pad;
+  const int32_t* chunk_heavy;
+  const int32_t* heavy_rows;
+  const int64_t* heavy_cptr;
+  float* partial;  // [n_chunks, d]
+  int64_t heavy_blocks;
+};
+
+__device__ __forceinline__ float epilogue(float y, int epi, float slope) {
+  if (epi == HGD_EPI_LEAKY_RELU) return y > 0.f ? y : y * slope;
+  if (epi == HGD_EPI_RELU) return y > 0.f ? y : 0.f;
+  return y;
+}
+
+template <int VEC>
+__device__ __forceinline__ void load_vec(const float* p, float (&v)[VEC]) {
+  if constexpr (VEC == 4) {
+    const float4 t = *reinterpret_cast<const float4*>(p);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  } else {
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) v[i] = p[i];
+  }
+}
+
+template <int VEC>
+__device__ __forceinline__ void store_vec(float* p, const float (&v)[VEC]) {
+  if constexpr (VEC == 4) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) p[i] = v[i];
+  }
+}
+
+// Σ_{e in [e0,e1)} val[e] * X[col[e], cols of this lane], in edge order.
+template <int G, int VEC, int U, bool HAS_VAL>
+__device__ __forceinline__ void gather_sum(const SpmmArgs& a, int64_t e0, int64_t e1, int l,
+                                           bool col_ok, float (&acc)[VEC]) {
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) acc[i] = 0.f;
+  const int64_t coff = static_cast<int64_t>(a.col0) + static_cast<int64_t>(l) * VEC;
+  for (int64_t eb = e0; eb < e1; eb += G) {
+    const int n = static_cast<int>(min(static_cast<int64_t>(G), e1 - eb));
+    int myc = 0;
+    float myw = 1.f;
+    if (l < n) {
+      myc = a.col[eb + l];
+      if constexpr (HAS_VAL) myw = a.val[eb + l];
+    }
+    for (int k = 0; k < n; k += U) {
+      float xv[U][VEC];
+      float w[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int kk = k + u;
+        const int c = (G == 1) ? myc : __shfl(myc, kk, G);
+        if constexpr (HAS_VAL) w[u] = (G == 1) ? myw : __shfl(myw, kk, G);
+        if (kk < n && col_ok) {
+          load_vec<VEC>(a.X + static_cast<int64_t>(c) * a.ldx + coff, xv[u]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < VEC; ++i) xv[u][i] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (k + u < n) {
+#pragma unroll
+          for (int i = 0; i < VEC; ++i) {
+            if constexpr (HAS_VAL)
+              acc[i] = fmaf(w[u], xv[u][i], acc[i]);
+            else
+              acc[i] += xv[u][i];
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int G, int VEC, int U, bool HAS_VAL>
+__global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
+  constexpr int GPB = kBlock / G;
+  const int g = threadIdx.x / G;
+  const int l = threadIdx.x % G;
+  const int64_t coff = static_cast<int64_t>(a.col0) + static_cast<int64_t>(l) * VEC;
+  const bool col_ok = coff < a.d;
+  float acc[VEC];
+
+  if (static_cast<int64_t>(blockIdx.x) < a.heavy_blocks) {
+    const int64_t t = static_cast<int64_t>(blockIdx.x) * GPB + g;
+    if (t >= a.n_chunks) return;
+    const int h = a.chunk_heavy[t];
+    const int64_t r = a.heavy_rows[h];
+    if (r < a.row_begin || r >= a.row_end) return;
+    const int64_t k = t - a.heavy_cptr[h];
+    const int64_t re = a.rowptr[r + 1];
+    const int64_t e0 = a.rowptr[r] + k * a.chunk;
+    const int64_t e1 = min(e0 + static_cast<int64_t>(a.chunk), re);
+    gather_sum<G, VEC, U, HAS_VAL>(a, e0, e1, l, col_ok, acc);
+    if (col_ok) store_vec<VEC>(a.partial + t * a.d + coff, acc);
+    return;
+  }
+
+  const int64_t r =
+      a.row_begin + (static_cast<int64_t>(blockIdx.x) - a.heavy_blocks) * GPB + g;
+  if (r >= a.row_end) return;
+  const int64_t e0 = a.rowptr[r];
+  const int64_t e1 = a.rowptr[r + 1];
+  if (a.heavy_threshold > 0 && e1 - e0 > a.heavy_threshold) return;  // split-plan row
+  gather_sum<G, VEC, U, HAS_VAL>(a, e0, e1, l, col_ok, acc);
+  const float s = a.row_scale ? a.row_scale[r] : 1.f;
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) acc[i] = epilogue(acc[i] * s, a.epi, a.slope);
+  if (col_ok) store_vec<VEC>(a.Y + r * a.ldy + coff, acc);
+}
+
+// Sums the chunk partials of each split row in chunk order, then scale + epilogue.
+template <int G, int VEC>
+__global__ __launch_bounds__(kBlock) void spmm_fixup_kernel(SpmmArgs a) {
+  constexpr int GPB = kBlock / G;
+  const int g = threadIdx.x / G;
+  const int l = threadIdx.x % G;
+  const int64_t h = static_cast<int64_t>(blockIdx.x) * GPB + g;
+  if (h >= a.n_heavy) return;
+  const int64_t r = a.heavy_rows[h];
+  if (r < a.row_begin || r >= a.row_end) return;
+  const int64_t coff = static_cast<int64_t>(a.col0) + static_cast<int64_t>(l) * VEC;
+  if (coff >= a.d) return;
+  float acc[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) acc[i] = 0.f;
+  for (int64_t t = a.heavy_cptr[h]; t < a.heavy_cptr[h + 1]; ++t) {
+    float v[VEC];
+    load_vec<VEC>(a.partial + t * a.d + coff, v);
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) acc[i] += v[i];
+  }
+  const float s = a.row_scale ? a.row_scale[r] : 1.f;
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) acc[i] = epilogue(acc[i] * s, a.epi, a.slope);
+  store_vec<VEC>(a.Y + r * a.ldy + coff, acc);
+}
+
+namespace {
+
+constexpr int kUnroll = 8;
+
+template <int G, int VEC>
+hgd_status launch_g(SpmmArgs a, bool has_val, hipStream_t st) {
+  constexpr int GPB = kBlock / G;
+  const int64_t rows = a.row_end - a.row_begin;
+  const int64_t light_blocks = (rows + GPB - 1) / GPB;
+  a.heavy_blocks = (a.n_chunks + GPB - 1) / GPB;
+  const int64_t blocks = light_blocks + a.heavy_blocks;
+  if (blocks > 0) {
+    if (blocks > 0x7fffffffLL) return fail(HGD_ERR_UNSUPPORTED, "hgd_spmm: grid too large");
+    if (has_val)
+      hipLaunchKernelGGL((spmm_kernel<G, VEC, kUnroll, true>), dim3(blocks), dim3(kBlock), 0,
+                         st, a);
+    else
+      hipLaunchKernelGGL((spmm_kernel<G, VEC, kUnroll, false>), dim3(blocks), dim3(kBlock), 0,
+                         st, a);
+    hgd_status s = check_launch("hgd_spmm kernel");
+    if (s != HGD_OK) return s;
+  }
+  if (a.n_heavy > 0) {
+    const int64_t fblocks = (a.n_heavy + GPB - 1) / GPB;
+    hipLaunchKernelGGL((spmm_fixup_kernel<G, VEC>), dim3(fblocks), dim3(kBlock), 0, st, a);
+    return check_launch("hgd_spmm fixup");
+  }
+  return HGD_OK;
+}
+
+template <int VEC>
+hgd_status launch_vec(int G, const SpmmArgs& a, bool has_val, hipStream_t st) {
+  switch (G) {
+    case 1: return launch_g<1, VEC>(a, has_val, st);
+    case 2: return launch_g<2, VEC>(a, has_val, st);
+    case 4: return launch_g<4, VEC>(a, has_val, st);
+    case 8: return launch_g<8, VEC>(a, has_val, st);
+    case 16: return launch_g<16, VEC>(a, has_val, st);
+    case 32: return launch_g<32, VEC>(a, has_val, st);
+    case 64: return launch_g<64, VEC>(a, has_val, st);
+    default: return fail(HGD_ERR_UNSUPPORTED, "hgd_spmm: unsupported group size %d", G);
+  }
+}
+
+int next_pow2(int x) {
+  int p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+}  // namespace
+}  // namespace hgd
+
+extern "C" size_t hgd_spmm_workspace_size(const hgd_split_plan* plan, int32_t d) {
+  if (!plan || plan->n_heavy <= 0 || plan->threshold <= 0 || d <= 0) return 0;
+  return hgd::align_up(static_cast<size_t>(plan->n_chunks) * static_cast<size_t>(d) * 4);
+}
+
+extern "C" hgd_status hgd_spmm(const int64_t* rowptr, const int32_t* col, const float* val,
+                               const float* row_scale, int64_t n_rows, int64_t n_src_rows,
+                               int64_t row_begin, int64_t row_end, const float* X, int64_t ldx,
+                               float* Y, int64_t ldy, int32_t d, int32_t epilogue, float slope,
+                               const hgd_split_plan* plan, void* workspace,
+                               size_t workspace_bytes, void* stream) {
+  using namespace hgd;
+  clear_error();
+  HGD_REQUIRE(d > 0, "hgd_spmm: d must be > 0 (got %d)", d);
+  HGD_REQUIRE(n_rows >= 0 && n_src_rows >= 0, "hgd_spmm: negative sizes");
+  HGD_REQUIRE(row_begin >= 0 && row_begin <= row_end && row_end <= n_rows,
+              "hgd_spmm: row range [%lld,%lld) outside [0,%lld)", (long long)row_begin,
+              (long long)row_end, (long long)n_rows);
+  HGD_REQUIRE(ldx >= d && ldy >= d, "hgd_spmm: ldx/ldy must be >= d");
+  HGD_REQUIRE(epilogue >= HGD_EPI_NONE && epilogue <= HGD_EPI_RELU, "hgd_spmm: bad epilogue %d",
+              epilogue);
+  if (row_end == row_begin) return HGD_OK;
+  // col / X may be NULL for a structure without nonzeros (never dereferenced then).
+  HGD_REQUIRE(rowptr && Y, "hgd_spmm: null rowptr/Y");
+  HGD_REQUIRE(X || n_src_rows == 0, "hgd_spmm: null X");
+
+  SpmmArgs a{};
+  a.rowptr = rowptr;
+  a.col = col;
+  a.val = val;
+  a.row_scale = row_scale;
+  a.row_begin = row_begin;
+  a.row_end = row_end;
+  a.X = X;
+  a.ldx = ldx;
+  a.Y = Y;
+  a.ldy = ldy;
+  a.d = d;
+  a.epi = epilogue;
+  a.slope = slope;
+  if (plan && plan->threshold > 0 && plan->n_heavy > 0) {
+    HGD_REQUIRE(plan->chunk > 0 && plan->heavy_rows && plan->heavy_cptr && plan->chunk_heavy,
+                "hgd_spmm: incomplete split plan");
+    const size_t need = hgd_spmm_workspace_size(plan, d);
+    if (workspace_bytes < need || (need && !workspace))
+      return fail(HGD_ERR_WORKSPACE, "hgd_spmm: workspace %zu < required %zu", workspace_bytes,
+                  need);
+    a.heavy_threshold = plan->threshold;
+    a.chunk = plan->chunk;
+    a.n_chunks = plan->n_chunks;
+    a.n_heavy = plan->n_heavy;
+    a.chunk_heavy = plan->chunk_heavy;
+    a.heavy_rows = plan->heavy_rows;
+    a.heavy_cptr = plan->heavy_cptr;
+    a.partial = static_cast<float*>(workspace);
+  }
+
+  hipStream_t st = as_stream(stream);
+  const bool has_val = val != nullptr;
+  const bool aligned = (reinterpret_cast<uintptr_t>(X) % 16 == 0) &&
+                       (reinterpret_cast<uintptr_t>(Y) % 16 == 0) && (ldx % 4 == 0) &&
+                       (ldy % 4 == 0) && (d % 4 == 0);
+  if (aligned) {
+    // float4 path: one pass when d/4 <= 64 lanes, else 256-column passes.
+    const int lanes = d / 4;
+    const int G = lanes >= 64 ? 64 : next_pow2(lanes);
+    for (int c0 = 0; c0 < d; c0 += 4 * G) {
+      a.col0 = c0;
+      hgd_status s = launch_vec<4>(G, a, has_val, st);
+      if (s != HGD_OK) return s;
+    }
+  } else {
+    const int G = d >= 64 ? 64 : next_pow2(d);
+    for (int c0 = 0; c0 < d; c0 += G) {
+      a.col0 = c0;
+      hgd_status s = launch_vec<1>(G, a, has_val, st);
+      if (s != HGD_OK) return s;
+    }
+  }
+  return HGD_OK;
+}

@@ -1,0 +1,543 @@
+// Structure primitives feeding the SpMM hops: COO→CSR ordering, CSR→CSC transpose support,
+// degree scales, per-nonzero weights, drop-edge compaction and dense-threshold nonzero.
+// All outputs are deterministic and bit-exact with the CPU restatement in oracle/.
+//
+// Reference behaviour restated (paths relative to /root/reference/HD_SELFRec):
+//   rowptr / sort      base/torch_interface.py:8-12 (row-major COO), cuSPARSE coalesce inside
+//                      torch.sparse.mm and the `adj.t()` transpose of HGCNConv (HGNN_HD4.py:459)
+//   degree scale       data/graph.py:11-25 (D^-1/2 A D^-1/2, D^-1 A, inf→0), data/graph.py:28-42
+//   drop-edge          model/graph/HCCF.py:213-226 (mask → idxs[:,mask], vals[mask]/keepRate)
+//   dense threshold    model/layers/layers2/EquivSetGNN2.py:105-133 (torch.nonzero(H > 0))
+#include <hipcub/hipcub.hpp>
+
+#include "hgd_internal.h"
+
+namespace hgd {
+
+thread_local char g_last_error[512] = {0};
+
+// ------------------------------------------------------------------------------------------
+__global__ void k_plan_count(const int64_t* __restrict__ rowptr, int64_t n_rows,
+                             int64_t threshold, int32_t chunk,
+                             unsigned long long* __restrict__ counts) {
+  __shared__ unsigned long long s_h[kBlock / 64], s_c[kBlock / 64];
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  unsigned long long h = 0, c = 0;
+  if (r < n_rows) {
+    const int64_t deg = rowptr[r + 1] - rowptr[r];
+    if (deg > threshold) {
+      h = 1;
+      c = static_cast<unsigned long long>((deg + chunk - 1) / chunk);
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    h += __shfl_down(h, off, 64);
+    c += __shfl_down(c, off, 64);
+  }
+  const int w = threadIdx.x / 64;
+  if ((threadIdx.x & 63) == 0) {
+    s_h[w] = h;
+    s_c[w] = c;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long th = 0, tc = 0;
+    for (int i = 0; i < kBlock / 64; ++i) {
+      th += s_h[i];
+      tc += s_c[i];
+    }
+    if (th) atomicAdd(&counts[0], th);
+    if (tc) atomicAdd(&counts[1], tc);
+  }
+}
+
+__global__ void k_plan_flags(const int64_t* __restrict__ rowptr, int64_t n_rows,
+                             int64_t threshold, int32_t chunk, int64_t* __restrict__ flag,
+                             int64_t* __restrict__ nch) {
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (r > n_rows) return;
+  int64_t f = 0, c = 0;
+  if (r < n_rows) {
+    const int64_t deg = rowptr[r + 1] - rowptr[r];
+    if (deg > threshold) {
+      f = 1;
+      c = (deg + chunk - 1) / chunk;
+    }
+  }
+  flag[r] = f;  // entry n_rows is 0 so the exclusive scan leaves the total there
+  nch[r] = c;
+}
+
+__global__ void k_plan_scatter(const int64_t* __restrict__ rowptr, int64_t n_rows,
+                               int64_t threshold, const int64_t* __restrict__ pos,
+                               const int64_t* __restrict__ cpos, int32_t* __restrict__ heavy_rows,
+                               int64_t* __restrict__ heavy_cptr, int64_t n_heavy) {
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (r > n_rows) return;
+  if (r == n_rows) {
+    heavy_cptr[n_heavy] = cpos[n_rows];
+    return;
+  }
+  if (rowptr[r + 1] - rowptr[r] > threshold) {
+    const int64_t p = pos[r];
+    heavy_rows[p] = static_cast<int32_t>(r);
+    heavy_cptr[p] = cpos[r];
+  }
+}
+
+__global__ void k_plan_chunks(const int64_t* __restrict__ heavy_cptr, int64_t n_heavy,
+                              int64_t n_chunks, int32_t* __restrict__ chunk_heavy) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (t >= n_chunks) return;
+  // largest h with heavy_cptr[h] <= t
+  int64_t lo = 0, hi = n_heavy;  // invariant: heavy_cptr[lo] <= t < heavy_cptr[hi]
+  while (hi - lo > 1) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (heavy_cptr[mid] <= t)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  chunk_heavy[t] = static_cast<int32_t>(lo);
+}
+
+// ------------------------------------------------------------------------------------------
+__global__ void k_index_narrow(const int64_t* __restrict__ in, int64_t n, int64_t upper,
+                               int32_t* __restrict__ out, unsigned long long* err) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const int64_t v = in[i];
+  const bool bad = v < 0 || v >= upper;
+  out[i] = bad ? 0 : static_cast<int32_t>(v);
+  if (bad) atomicAdd(err, 1ull);
+}
+
+__global__ void k_iota(int32_t* __restrict__ out, int64_t n) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (i < n) out[i] = static_cast<int32_t>(i);
+}
+
+__global__ void k_rowptr_from_sorted(const int32_t* __restrict__ rows, int64_t nnz,
+                                     int64_t n_rows, int64_t* __restrict__ rowptr) {
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (r > n_rows) return;
+  int64_t lo = 0, hi = nnz;  // first p with rows[p] >= r
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (rows[mid] < r)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  rowptr[r] = lo;
+}
+
+__global__ void k_check_sorted(const int32_t* __restrict__ rows, int64_t nnz, int64_t n_rows,
+                               unsigned long long* bad) {
+  const int64_t e = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (e >= nnz) return;
+  const int32_t v = rows[e];
+  bool b = v < 0 || v >= n_rows;
+  if (e > 0 && rows[e - 1] > v) b = true;
+  if (b) atomicAdd(bad, 1ull);
+}
+
+__global__ void k_expand_rows(const int64_t* __restrict__ rowptr, int64_t n_rows,
+                              int32_t* __restrict__ rows_out, int64_t nnz) {
+  const int64_t e = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (e >= nnz) return;
+  int64_t lo = 0, hi = n_rows;  // last r with rowptr[r] <= e
+  while (hi - lo > 1) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (rowptr[mid] <= e)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  rows_out[e] = static_cast<int32_t>(lo);
+}
+
+__global__ void k_gather32(const uint32_t* __restrict__ src, const int32_t* __restrict__ perm,
+                           int64_t n, uint32_t* __restrict__ out) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (i < n) out[i] = src[perm[i]];
+}
+
+__global__ void k_degree_scale(const int64_t* __restrict__ rowptr, const float* __restrict__ val,
+                               int64_t n_rows, double power, float* __restrict__ out) {
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (r >= n_rows) return;
+  double deg;
+  if (val) {
+    float s = 0.f;  // fp32 row sum in edge order (scipy sums the float32 matrix in float32)
+    for (int64_t e = rowptr[r]; e < rowptr[r + 1]; ++e) s += val[e];
+    deg = static_cast<double>(s);
+  } else {
+    deg = static_cast<double>(rowptr[r + 1] - rowptr[r]);
+  }
+  float res;
+  if (deg == 0.0) {
+    res = 0.f;  // np.power(0, -p) = inf → 0 (data/graph.py:16)
+  } else if (power == -1.0) {
+    res = static_cast<float>(1.0 / deg);
+  } else if (power == -0.5) {
+    res = static_cast<float>(1.0 / sqrt(deg));
+  } else {
+    res = static_cast<float>(pow(deg, power));
+  }
+  out[r] = res;
+}
+
+__global__ void k_edge_values(const float* __restrict__ base, const int32_t* __restrict__ perm,
+                              const float* __restrict__ src_scale,
+                              const int32_t* __restrict__ src_idx, int64_t n,
+                              float* __restrict__ out) {
+  const int64_t e = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (e >= n) return;
+  float v = 1.f;
+  if (base) v = base[perm ? perm[e] : e];
+  if (src_scale) v *= src_scale[src_idx[e]];
+  out[e] = v;
+}
+
+__global__ void k_mask_to_i64(const uint8_t* __restrict__ mask, int64_t n,
+                              int64_t* __restrict__ flags) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (i > n) return;
+  flags[i] = (i < n && mask[i]) ? 1 : 0;
+}
+
+__global__ void k_dropedge_scatter(const int64_t* __restrict__ rows,
+                                   const int64_t* __restrict__ cols,
+                                   const float* __restrict__ val,
+                                   const uint8_t* __restrict__ mask,
+                                   const int64_t* __restrict__ pos, int64_t nnz, float keep,
+                                   int64_t* __restrict__ out_rows, int64_t* __restrict__ out_cols,
+                                   float* __restrict__ out_val, int64_t* __restrict__ out_count) {
+  const int64_t e = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (e == nnz) *out_count = pos[nnz];
+  if (e >= nnz || !mask[e]) return;
+  const int64_t p = pos[e];
+  out_rows[p] = rows[e];
+  out_cols[p] = cols[e];
+  out_val[p] = __fdiv_rn(val[e], keep);  // vals[mask] / keepRate, IEEE fp32 division
+}
+
+// One wavefront per row: number of entries > thresh.
+__global__ void k_dense_count(const float* __restrict__ H, int64_t n_rows, int64_t n_cols,
+                              int64_t ld, float thresh, int64_t* __restrict__ counts) {
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * (kBlock / 64) + threadIdx.x / 64;
+  const int lane = threadIdx.x & 63;
+  if (r > n_rows) return;
+  int64_t cnt = 0;
+  if (r < n_rows) {
+    const float* row = H + r * ld;
+    for (int64_t c0 = 0; c0 < n_cols; c0 += 64) {
+      const int64_t c = c0 + lane;
+      const bool f = c < n_cols && row[c] > thresh;
+      cnt += __popcll(__ballot(f));
+    }
+  }
+  if (lane == 0) counts[r] = cnt;  // counts[n_rows] = 0 → exclusive scan total
+}
+
+__global__ void k_dense_fill(const float* __restrict__ H, int64_t n_rows, int64_t n_cols,
+                             int64_t ld, float thresh, const int64_t* __restrict__ rowptr,
+                             int32_t* __restrict__ cols) {
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * (kBlock / 64) + threadIdx.x / 64;
+  const int lane = threadIdx.x & 63;
+  if (r >= n_rows) return;
+  const float* row = H + r * ld;
+  int64_t p = rowptr[r];
+  const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int64_t c0 = 0; c0 < n_cols; c0 += 64) {
+    const int64_t c = c0 + lane;
+    const bool f = c < n_cols && row[c] > thresh;
+    const unsigned long long b = __ballot(f);
+    if (f) cols[p + __popcll(b & lt_mask)] = static_cast<int32_t>(c);
+    p += __popcll(b);
+  }
+}
+
+template <typename T>
+size_t excl_scan_bytes(int64_t n) {
+  size_t bytes = 0;
+  if (hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, static_cast<const T*>(nullptr),
+                                       static_cast<T*>(nullptr), n) != hipSuccess)
+    return 0;
+  return bytes;
+}
+
+}  // namespace hgd
+
+using namespace hgd;
+
+extern "C" int hgd_version(void) { return 100; }  // 0.1.0
+
+extern "C" const char* hgd_get_last_error_string(void) { return g_last_error; }
+
+// ------------------------------------------------------------------------------------------
+extern "C" hgd_status hgd_split_plan_count(const int64_t* rowptr, int64_t n_rows,
+                                           int64_t threshold, int32_t chunk, int64_t* counts,
+                                           void* stream) {
+  clear_error();
+  HGD_REQUIRE(rowptr && counts, "hgd_split_plan_count: null pointer");
+  HGD_REQUIRE(chunk > 0 && threshold > 0, "hgd_split_plan_count: chunk/threshold must be > 0");
+  hipStream_t st = as_stream(stream);
+  HGD_HIP(hipMemsetAsync(counts, 0, 2 * sizeof(int64_t), st));
+  if (n_rows <= 0) return HGD_OK;
+  hipLaunchKernelGGL(k_plan_count, dim3(grid_for(n_rows)), dim3(kBlock), 0, st, rowptr, n_rows,
+                     threshold, chunk, reinterpret_cast<unsigned long long*>(counts));
+  return check_launch("hgd_split_plan_count");
+}
+
+extern "C" size_t hgd_split_plan_workspace_size(int64_t n_rows) {
+  const size_t arr = align_up(static_cast<size_t>(n_rows + 1) * sizeof(int64_t));
+  return 4 * arr + align_up(excl_scan_bytes<int64_t>(n_rows + 1));
+}
+
+extern "C" hgd_status hgd_split_plan_build(const int64_t* rowptr, int64_t n_rows,
+                                           int64_t threshold, int32_t chunk, int32_t* heavy_rows,
+                                           int64_t* heavy_cptr, int32_t* chunk_heavy,
+                                           int64_t n_heavy, int64_t n_chunks, void* workspace,
+                                           size_t workspace_bytes, void* stream) {
+  clear_error();
+  HGD_REQUIRE(rowptr && heavy_cptr, "hgd_split_plan_build: null pointer");
+  HGD_REQUIRE(chunk > 0 && threshold > 0, "hgd_split_plan_build: chunk/threshold must be > 0");
+  const size_t need = hgd_split_plan_workspace_size(n_rows);
+  if (workspace_bytes < need || !workspace)
+    return fail(HGD_ERR_WORKSPACE, "hgd_split_plan_build: workspace %zu < %zu", workspace_bytes,
+                need);
+  hipStream_t st = as_stream(stream);
+  if (n_heavy == 0) {
+    HGD_HIP(hipMemsetAsync(heavy_cptr, 0, sizeof(int64_t), st));
+    return HGD_OK;
+  }
+  HGD_REQUIRE(heavy_rows && chunk_heavy, "hgd_split_plan_build: null output arrays");
+  const size_t arr = align_up(static_cast<size_t>(n_rows + 1) * sizeof(int64_t));
+  char* ws = static_cast<char*>(workspace);
+  int64_t* flag = reinterpret_cast<int64_t*>(ws);
+  int64_t* nch = reinterpret_cast<int64_t*>(ws + arr);
+  int64_t* pos = reinterpret_cast<int64_t*>(ws + 2 * arr);
+  int64_t* cpos = reinterpret_cast<int64_t*>(ws + 3 * arr);
+  void* tmp = ws + 4 * arr;
+  size_t tmp_bytes = workspace_bytes - 4 * arr;
+  hipLaunchKernelGGL(k_plan_flags, dim3(grid_for(n_rows + 1)), dim3(kBlock), 0, st, rowptr,
+                     n_rows, threshold, chunk, flag, nch);
+  hgd_status s = check_launch("hgd_split_plan_build flags");
+  if (s != HGD_OK) return s;
+  size_t b = tmp_bytes;
+  HGD_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, b, flag, pos, n_rows + 1, st));
+  b = tmp_bytes;
+  HGD_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, b, nch, cpos, n_rows + 1, st));
+  hipLaunchKernelGGL(k_plan_scatter, dim3(grid_for(n_rows + 1)), dim3(kBlock), 0, st, rowptr,
+                     n_rows, threshold, pos, cpos, heavy_rows, heavy_cptr, n_heavy);
+  s = check_launch("hgd_split_plan_build scatter");
+  if (s != HGD_OK) return s;
+  if (n_chunks > 0) {
+    hipLaunchKernelGGL(k_plan_chunks, dim3(grid_for(n_chunks)), dim3(kBlock), 0, st, heavy_cptr,
+                       n_heavy, n_chunks, chunk_heavy);
+    return check_launch("hgd_split_plan_build chunks");
+  }
+  return HGD_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+extern "C" hgd_status hgd_index_narrow(const int64_t* in, int64_t n, int64_t upper, int32_t* out,
+                                       int64_t* err_count, void* stream) {
+  clear_error();
+  HGD_REQUIRE(n >= 0, "hgd_index_narrow: n < 0");
+  HGD_REQUIRE(upper <= 0x7fffffffLL + 1, "hgd_index_narrow: upper bound exceeds int32");
+  if (n == 0) return HGD_OK;
+  HGD_REQUIRE(in && out && err_count, "hgd_index_narrow: null pointer");
+  hipLaunchKernelGGL(k_index_narrow, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), in,
+                     n, upper, out, reinterpret_cast<unsigned long long*>(err_count));
+  return check_launch("hgd_index_narrow");
+}
+
+extern "C" size_t hgd_sort_perm_workspace_size(int64_t n) {
+  size_t bytes = 0;
+  if (n <= 0) return 0;
+  if (hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, static_cast<const int32_t*>(nullptr),
+                                         static_cast<int32_t*>(nullptr),
+                                         static_cast<const int32_t*>(nullptr),
+                                         static_cast<int32_t*>(nullptr), n, 0, 32) != hipSuccess)
+    return 0;
+  return align_up(static_cast<size_t>(n) * sizeof(int32_t)) + align_up(bytes);
+}
+
+extern "C" hgd_status hgd_sort_perm(const int32_t* keys, int64_t n, int64_t n_keys,
+                                    int32_t* keys_out, int32_t* perm_out, void* workspace,
+                                    size_t workspace_bytes, void* stream) {
+  clear_error();
+  HGD_REQUIRE(n >= 0 && n < 0x7fffffffLL, "hgd_sort_perm: n out of range");
+  if (n == 0) return HGD_OK;
+  HGD_REQUIRE(keys && keys_out && perm_out, "hgd_sort_perm: null pointer");
+  HGD_REQUIRE(n_keys > 0 && n_keys <= 0x7fffffffLL + 1, "hgd_sort_perm: bad n_keys");
+  const size_t need = hgd_sort_perm_workspace_size(n);
+  if (need == 0 || workspace_bytes < need || !workspace)
+    return fail(HGD_ERR_WORKSPACE, "hgd_sort_perm: workspace %zu < %zu", workspace_bytes, need);
+  hipStream_t st = as_stream(stream);
+  char* ws = static_cast<char*>(workspace);
+  int32_t* iota = reinterpret_cast<int32_t*>(ws);
+  const size_t off = align_up(static_cast<size_t>(n) * sizeof(int32_t));
+  hipLaunchKernelGGL(k_iota, dim3(grid_for(n)), dim3(kBlock), 0, st, iota, n);
+  hgd_status s = check_launch("hgd_sort_perm iota");
+  if (s != HGD_OK) return s;
+  int end_bit = 1;
+  while (end_bit < 32 && (1LL << end_bit) < n_keys) ++end_bit;
+  size_t b = workspace_bytes - off;
+  HGD_HIP(hipcub::DeviceRadixSort::SortPairs(ws + off, b, keys, keys_out, iota, perm_out, n, 0,
+                                             end_bit, st));
+  return HGD_OK;
+}
+
+extern "C" hgd_status hgd_rowptr_from_sorted(const int32_t* sorted_rows, int64_t nnz,
+                                             int64_t n_rows, int64_t* rowptr, void* stream) {
+  clear_error();
+  HGD_REQUIRE(nnz >= 0 && n_rows >= 0, "hgd_rowptr_from_sorted: negative size");
+  HGD_REQUIRE(rowptr && (sorted_rows || nnz == 0), "hgd_rowptr_from_sorted: null pointer");
+  hipLaunchKernelGGL(k_rowptr_from_sorted, dim3(grid_for(n_rows + 1)), dim3(kBlock), 0,
+                     as_stream(stream), sorted_rows, nnz, n_rows, rowptr);
+  return check_launch("hgd_rowptr_from_sorted");
+}
+
+extern "C" hgd_status hgd_check_sorted(const int32_t* rows, int64_t nnz, int64_t n_rows,
+                                       int64_t* bad, void* stream) {
+  clear_error();
+  HGD_REQUIRE(bad && (rows || nnz == 0), "hgd_check_sorted: null pointer");
+  hipStream_t st = as_stream(stream);
+  HGD_HIP(hipMemsetAsync(bad, 0, sizeof(int64_t), st));
+  if (nnz == 0) return HGD_OK;
+  hipLaunchKernelGGL(k_check_sorted, dim3(grid_for(nnz)), dim3(kBlock), 0, st, rows, nnz, n_rows,
+                     reinterpret_cast<unsigned long long*>(bad));
+  return check_launch("hgd_check_sorted");
+}
+
+extern "C" hgd_status hgd_expand_rows(const int64_t* rowptr, int64_t n_rows, int64_t nnz,
+                                      int32_t* rows_out, void* stream) {
+  clear_error();
+  HGD_REQUIRE(rowptr && n_rows >= 0 && nnz >= 0, "hgd_expand_rows: bad arguments");
+  if (nnz == 0) return HGD_OK;
+  HGD_REQUIRE(rows_out && n_rows > 0, "hgd_expand_rows: null rows_out or no rows");
+  hipLaunchKernelGGL(k_expand_rows, dim3(grid_for(nnz)), dim3(kBlock), 0, as_stream(stream),
+                     rowptr, n_rows, rows_out, nnz);
+  return check_launch("hgd_expand_rows");
+}
+
+extern "C" hgd_status hgd_gather32(const void* src, const int32_t* perm, int64_t n, void* out,
+                                   void* stream) {
+  clear_error();
+  if (n == 0) return HGD_OK;
+  HGD_REQUIRE(src && perm && out && n > 0, "hgd_gather32: bad arguments");
+  hipLaunchKernelGGL(k_gather32, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream),
+                     static_cast<const uint32_t*>(src), perm, n, static_cast<uint32_t*>(out));
+  return check_launch("hgd_gather32");
+}
+
+extern "C" hgd_status hgd_degree_scale(const int64_t* rowptr, const float* val, int64_t n_rows,
+                                       double power, float* scale_out, void* stream) {
+  clear_error();
+  HGD_REQUIRE(n_rows >= 0, "hgd_degree_scale: n_rows < 0");
+  if (n_rows == 0) return HGD_OK;
+  HGD_REQUIRE(rowptr && scale_out, "hgd_degree_scale: null pointer");
+  hipLaunchKernelGGL(k_degree_scale, dim3(grid_for(n_rows)), dim3(kBlock), 0, as_stream(stream),
+                     rowptr, val, n_rows, power, scale_out);
+  return check_launch("hgd_degree_scale");
+}
+
+extern "C" hgd_status hgd_edge_values(const float* base, const int32_t* perm,
+                                      const float* src_scale, const int32_t* src_idx, int64_t n,
+                                      float* out, void* stream) {
+  clear_error();
+  HGD_REQUIRE(n >= 0, "hgd_edge_values: n < 0");
+  if (n == 0) return HGD_OK;
+  HGD_REQUIRE(out, "hgd_edge_values: null out");
+  HGD_REQUIRE(!src_scale || src_idx, "hgd_edge_values: src_scale needs src_idx");
+  HGD_REQUIRE(!perm || base, "hgd_edge_values: perm needs base");
+  hipLaunchKernelGGL(k_edge_values, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream), base,
+                     perm, src_scale, src_idx, n, out);
+  return check_launch("hgd_edge_values");
+}
+
+extern "C" size_t hgd_dropedge_workspace_size(int64_t nnz) {
+  return 2 * align_up(static_cast<size_t>(nnz + 1) * sizeof(int64_t)) +
+         align_up(excl_scan_bytes<int64_t>(nnz + 1));
+}
+
+extern "C" hgd_status hgd_dropedge_compact(const int64_t* rows, const int64_t* cols,
+                                           const float* val, const uint8_t* mask, int64_t nnz,
+                                           float keep, int64_t* out_rows, int64_t* out_cols,
+                                           float* out_val, int64_t* out_count, void* workspace,
+                                           size_t workspace_bytes, void* stream) {
+  clear_error();
+  HGD_REQUIRE(nnz >= 0 && out_count, "hgd_dropedge_compact: bad arguments");
+  HGD_REQUIRE(keep > 0.f, "hgd_dropedge_compact: keep must be > 0");
+  hipStream_t st = as_stream(stream);
+  if (nnz == 0) {
+    HGD_HIP(hipMemsetAsync(out_count, 0, sizeof(int64_t), st));
+    return HGD_OK;
+  }
+  HGD_REQUIRE(rows && cols && val && mask && out_rows && out_cols && out_val,
+              "hgd_dropedge_compact: null pointer");
+  const size_t need = hgd_dropedge_workspace_size(nnz);
+  if (workspace_bytes < need || !workspace)
+    return fail(HGD_ERR_WORKSPACE, "hgd_dropedge_compact: workspace %zu < %zu", workspace_bytes,
+                need);
+  const size_t arr = align_up(static_cast<size_t>(nnz + 1) * sizeof(int64_t));
+  char* ws = static_cast<char*>(workspace);
+  int64_t* flags = reinterpret_cast<int64_t*>(ws);
+  int64_t* pos = reinterpret_cast<int64_t*>(ws + arr);
+  hipLaunchKernelGGL(k_mask_to_i64, dim3(grid_for(nnz + 1)), dim3(kBlock), 0, st, mask, nnz,
+                     flags);
+  hgd_status s = check_launch("hgd_dropedge_compact flags");
+  if (s != HGD_OK) return s;
+  size_t b = workspace_bytes - 2 * arr;
+  HGD_HIP(hipcub::DeviceScan::ExclusiveSum(ws + 2 * arr, b, flags, pos, nnz + 1, st));
+  hipLaunchKernelGGL(k_dropedge_scatter, dim3(grid_for(nnz + 1)), dim3(kBlock), 0, st, rows, cols,
+                     val, mask, pos, nnz, keep, out_rows, out_cols, out_val, out_count);
+  return check_launch("hgd_dropedge_compact scatter");
+}
+
+extern "C" size_t hgd_dense_threshold_workspace_size(int64_t n_rows) {
+  return align_up(static_cast<size_t>(n_rows + 1) * sizeof(int64_t)) +
+         align_up(excl_scan_bytes<int64_t>(n_rows + 1));
+}
+
+extern "C" hgd_status hgd_dense_threshold_rowptr(const float* H, int64_t n_rows, int64_t n_cols,
+                                                 int64_t ld, float thresh, int64_t* rowptr,
+                                                 void* workspace, size_t workspace_bytes,
+                                                 void* stream) {
+  clear_error();
+  HGD_REQUIRE(n_rows >= 0 && n_cols >= 0 && (ld >= n_cols || n_rows == 0),
+              "hgd_dense_threshold_rowptr: sizes");
+  HGD_REQUIRE(rowptr && (H || n_rows == 0 || n_cols == 0), "hgd_dense_threshold_rowptr: null");
+  const size_t need = hgd_dense_threshold_workspace_size(n_rows);
+  if (workspace_bytes < need || !workspace)
+    return fail(HGD_ERR_WORKSPACE, "hgd_dense_threshold_rowptr: workspace %zu < %zu",
+                workspace_bytes, need);
+  hipStream_t st = as_stream(stream);
+  const size_t arr = align_up(static_cast<size_t>(n_rows + 1) * sizeof(int64_t));
+  char* ws = static_cast<char*>(workspace);
+  int64_t* counts = reinterpret_cast<int64_t*>(ws);
+  hipLaunchKernelGGL(k_dense_count, dim3(grid_for(n_rows + 1, kBlock / 64)), dim3(kBlock), 0, st,
+                     H, n_rows, n_cols, ld, thresh, counts);
+  hgd_status s = check_launch("hgd_dense_threshold_rowptr count");
+  if (s != HGD_OK) return s;
+  size_t b = workspace_bytes - arr;
+  HGD_HIP(hipcub::DeviceScan::ExclusiveSum(ws + arr, b, counts, rowptr, n_rows + 1, st));
+  return HGD_OK;
+}
+
+extern "C" hgd_status hgd_dense_threshold_fill(const float* H, int64_t n_rows, int64_t n_cols,
+                                               int64_t ld, float thresh, const int64_t* rowptr,
+                                               int32_t* cols, void* stream) {
+  clear_error();
+  HGD_REQUIRE(n_rows >= 0 && n_cols >= 0 && (ld >= n_cols || n_rows == 0),
+              "hgd_dense_threshold_fill: sizes");
+  if (n_rows == 0 || n_cols == 0) return HGD_OK;
+  HGD_REQUIRE(H && rowptr && cols, "hgd_dense_threshold_fill: null pointer");
+  hipLaunchKernelGGL(k_dense_fill, dim3(grid_for(n_rows, kBlock / 64)), dim3(kBlock), 0,
+                     as_stream(stream), H, n_rows, n_cols, ld, thresh, rowptr, cols);
+  return check_launch("hgd_dense_threshold_fill");
+}

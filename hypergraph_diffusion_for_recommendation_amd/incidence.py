@@ -1,0 +1,456 @@
+"""Device-resident incidence structures for the propagation hops.
+
+An :class:`Incidence` holds one sparse matrix ``A`` of shape ``[n_rows, n_cols]`` twice:
+
+* ``csr``  — rows of ``A`` (the hop ``Y = A·X``, ``torch.sparse.mm(adj, X)``), and
+* ``csc``  — rows of ``Aᵀ`` (the hop ``M = Aᵀ·X``, ``torch.sparse.mm(adj.t(), X)``),
+
+plus the per-nonzero weights in both orders and cached degree scales. Everything is built on
+the GPU by libhgd (``include/hgd.h``); this module only allocates buffers with the PyTorch
+caching allocator and sequences the C-ABI calls. It replaces the per-call COO handling of the
+reference (``base/torch_interface.py:8-12`` builds the COO; ``torch.sparse.mm`` coalesces it and
+``HGCNConv`` rebuilds ``adj.t()`` on every call, ``model/graph/HGNN_HD4.py:459-462``).
+
+Layout in HBM (N rows, E nonzeros): rowptr int64[N+1], col int32[E], val fp32[E] (optional),
+for each orientation; split plans for rows longer than ``split_threshold`` nonzeros.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from . import _native as nat
+from . import profiling
+
+DEFAULT_SPLIT_THRESHOLD = 2048
+DEFAULT_SPLIT_CHUNK = 512
+
+
+def _ws(nbytes: int, device) -> torch.Tensor:
+    return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+
+
+def _stream(device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+class CSR:
+    """One orientation: ``rowptr`` int64 [n_rows+1], ``col`` int32 [nnz] (device tensors),
+    and the long-row split plan used by :func:`spmm_csr`."""
+
+    def __init__(self, rowptr: torch.Tensor, col: torch.Tensor, n_rows: int, n_cols: int,
+                 split_threshold: int = DEFAULT_SPLIT_THRESHOLD,
+                 split_chunk: int = DEFAULT_SPLIT_CHUNK, plan_counts: Optional[Tuple] = None):
+        self.rowptr = rowptr
+        self.col = col
+        self.n_rows = int(n_rows)
+        self.n_cols = int(n_cols)
+        self.nnz = int(col.numel())
+        self.device = rowptr.device
+        self.split_threshold = int(split_threshold)
+        self.split_chunk = int(split_chunk)
+        self._plan_arrays = ()
+        self.plan = nat.SplitPlan()
+        self.plan.threshold = 0
+        if plan_counts is not None:
+            self._build_plan(*plan_counts)
+
+    # -- split plan ---------------------------------------------------------------------
+    def plan_count_async(self) -> Optional[torch.Tensor]:
+        """Queues the (n_heavy, n_chunks) count; returns the device tensor to read later."""
+        if self.split_threshold <= 0 or self.n_rows == 0 or self.nnz <= self.split_threshold:
+            return None
+        counts = torch.empty(2, dtype=torch.int64, device=self.device)
+        nat.check(nat.load().hgd_split_plan_count(
+            self.rowptr.data_ptr(), self.n_rows, self.split_threshold, self.split_chunk,
+            counts.data_ptr(), _stream(self.device)), "hgd_split_plan_count")
+        return counts
+
+    def _build_plan(self, n_heavy: int, n_chunks: int) -> None:
+        n_heavy, n_chunks = int(n_heavy), int(n_chunks)
+        if n_heavy == 0:
+            self.plan.threshold = 0
+            return
+        dev = self.device
+        heavy_rows = torch.empty(n_heavy, dtype=torch.int32, device=dev)
+        heavy_cptr = torch.empty(n_heavy + 1, dtype=torch.int64, device=dev)
+        chunk_heavy = torch.empty(n_chunks, dtype=torch.int32, device=dev)
+        lib = nat.load()
+        ws = _ws(lib.hgd_split_plan_workspace_size(self.n_rows), dev)
+        nat.check(lib.hgd_split_plan_build(
+            self.rowptr.data_ptr(), self.n_rows, self.split_threshold, self.split_chunk,
+            heavy_rows.data_ptr(), heavy_cptr.data_ptr(), chunk_heavy.data_ptr(), n_heavy,
+            n_chunks, ws.data_ptr(), ws.numel(), _stream(dev)), "hgd_split_plan_build")
+        self._plan_arrays = (heavy_rows, heavy_cptr, chunk_heavy)
+        p = self.plan
+        p.threshold = self.split_threshold
+        p.chunk = self.split_chunk
+        p.n_heavy = n_heavy
+        p.n_chunks = n_chunks
+        p.heavy_rows = heavy_rows.data_ptr()
+        p.heavy_cptr = heavy_cptr.data_ptr()
+        p.chunk_heavy = chunk_heavy.data_ptr()
+
+    @property
+    def n_heavy(self) -> int:
+        return int(self.plan.n_heavy) if self.plan.threshold > 0 else 0
+
+    def degrees(self) -> torch.Tensor:
+        return self.rowptr[1:] - self.rowptr[:-1]
+
+
+def spmm_csr(csr: CSR, X: torch.Tensor, val: Optional[torch.Tensor] = None,
+             row_scale: Optional[torch.Tensor] = None, epilogue: int = nat.EPI_NONE,
+             slope: float = 0.0, out: Optional[torch.Tensor] = None,
+             row_begin: int = 0, row_end: Optional[int] = None) -> torch.Tensor:
+    """``Y[r] = epi(row_scale[r] * Σ_e val[e] * X[col[e]])`` for r in [row_begin, row_end)."""
+    if X.dim() != 2:
+        raise ValueError(f"spmm: X must be 2-D, got {tuple(X.shape)}")
+    if X.dtype != torch.float32:
+        raise TypeError(f"spmm: X must be float32, got {X.dtype}")
+    if X.device.type != "cuda":
+        raise RuntimeError("spmm: X must be a device (cuda/hip) tensor; there is no CPU path")
+    if X.shape[0] != csr.n_cols:
+        raise ValueError(f"spmm: X has {X.shape[0]} rows, structure expects {csr.n_cols}")
+    if X.stride(1) != 1:
+        X = X.contiguous()
+    d = X.shape[1]
+    if out is None:
+        out = torch.empty((csr.n_rows, d), dtype=torch.float32, device=X.device)
+    if row_end is None:
+        row_end = csr.n_rows
+    if d == 0 or row_end <= row_begin:
+        return out
+    if val is not None and val.numel() != csr.nnz:
+        raise ValueError("spmm: val size mismatch")
+    if row_scale is not None and row_scale.numel() != csr.n_rows:
+        raise ValueError("spmm: row_scale size mismatch")
+    lib = nat.load()
+    plan_ptr = ctypes.byref(csr.plan)
+    wsb = lib.hgd_spmm_workspace_size(plan_ptr, d)
+    ws = _ws(wsb, X.device) if wsb else None
+    timer = profiling.active()
+    if timer is not None:
+        t0 = timer.begin()
+    nat.check(lib.hgd_spmm(
+        csr.rowptr.data_ptr(), csr.col.data_ptr() if csr.nnz else None, nat.ptr(val),
+        nat.ptr(row_scale), csr.n_rows, csr.n_cols, int(row_begin), int(row_end),
+        X.data_ptr(), X.stride(0), out.data_ptr(), out.stride(0), d, int(epilogue),
+        float(slope), plan_ptr, nat.ptr(ws), wsb, _stream(X.device)), "hgd_spmm")
+    if timer is not None:
+        rb, re_ = int(row_begin), int(row_end)
+        full = rb == 0 and re_ == csr.n_rows
+
+        def nbytes(csr=csr, rb=rb, re_=re_, full=full, d=d, hv=val is not None,
+                   hs=row_scale is not None):
+            nnz = csr.nnz if full else int(csr.rowptr[re_].item() - csr.rowptr[rb].item())
+            return profiling.hop_bytes(nnz, re_ - rb, d, hv, hs)
+
+        timer.end(t0, nbytes)
+    return out
+
+
+class Incidence:
+    """Sparse ``A [n_rows, n_cols]`` as CSR + CSC on the device (see module docstring)."""
+
+    def __init__(self, csr: CSR, csc: CSR, val: Optional[torch.Tensor],
+                 val_t: Optional[torch.Tensor]):
+        self.csr = csr
+        self.csc = csc
+        self.val = val          # per-nonzero weights in CSR order (None = binary)
+        self.val_t = val_t      # the same weights in CSC order
+        self.n_rows = csr.n_rows
+        self.n_cols = csr.n_cols
+        self.nnz = csr.nnz
+        self.device = csr.device
+        self._scales: Dict[Tuple[str, str], torch.Tensor] = {}
+        self._edge_vals: Dict[Tuple[str, str, str], Optional[torch.Tensor]] = {}
+
+    @property
+    def shape(self):
+        return (self.n_rows, self.n_cols)
+
+    # -- construction ------------------------------------------------------------------
+    @classmethod
+    def from_coo(cls, indices: torch.Tensor, values: Optional[torch.Tensor], shape,
+                 device=None, validate: bool = True, rows_sorted: Optional[bool] = None,
+                 split_threshold: int = DEFAULT_SPLIT_THRESHOLD,
+                 split_chunk: int = DEFAULT_SPLIT_CHUNK) -> "Incidence":
+        """Builds from COO ``indices`` int64 [2, nnz] (+ fp32 ``values`` or None = ones).
+
+        Entries keep their order within a row (duplicates stay separate nonzeros, which is the
+        same linear map as torch's coalesced sum). Raises ValueError on out-of-range indices.
+        """
+        n_rows, n_cols = int(shape[0]), int(shape[1])
+        if n_rows >= 2 ** 31 or n_cols >= 2 ** 31:
+            raise ValueError("Incidence: dimensions must be < 2^31")
+        device = torch.device(device) if device is not None else indices.device
+        if device.type != "cuda":
+            raise RuntimeError("Incidence: needs a device (cuda/hip) target; there is no CPU path")
+        lib = nat.load()
+        st = _stream(device)
+        indices = indices.to(device=device, dtype=torch.int64)
+        nnz = int(indices.shape[1])
+        if values is not None:
+            values = values.to(device=device, dtype=torch.float32).contiguous()
+            if values.numel() != nnz:
+                raise ValueError("Incidence: values/indices size mismatch")
+        rows64 = indices[0].contiguous()
+        cols64 = indices[1].contiguous()
+        rows = torch.empty(nnz, dtype=torch.int32, device=device)
+        cols = torch.empty(nnz, dtype=torch.int32, device=device)
+        flags = torch.zeros(3, dtype=torch.int64, device=device)
+        if nnz:
+            nat.check(lib.hgd_index_narrow(rows64.data_ptr(), nnz, n_rows, rows.data_ptr(),
+                                           flags[0:1].data_ptr(), st), "hgd_index_narrow(rows)")
+            nat.check(lib.hgd_index_narrow(cols64.data_ptr(), nnz, n_cols, cols.data_ptr(),
+                                           flags[1:2].data_ptr(), st), "hgd_index_narrow(cols)")
+            if rows_sorted is None:
+                nat.check(lib.hgd_check_sorted(rows.data_ptr(), nnz, n_rows,
+                                               flags[2:3].data_ptr(), st), "hgd_check_sorted")
+        if validate or rows_sorted is None:
+            f = flags.tolist()
+            if f[0] or f[1]:
+                raise ValueError(f"Incidence: {f[0]} row / {f[1]} col indices out of range "
+                                 f"for shape {(n_rows, n_cols)}")
+            if rows_sorted is None:
+                rows_sorted = f[2] == 0
+        if nnz and not rows_sorted:
+            perm = torch.empty(nnz, dtype=torch.int32, device=device)
+            rows_s = torch.empty_like(rows)
+            ws = _ws(lib.hgd_sort_perm_workspace_size(nnz), device)
+            nat.check(lib.hgd_sort_perm(rows.data_ptr(), nnz, n_rows, rows_s.data_ptr(),
+                                        perm.data_ptr(), ws.data_ptr(), ws.numel(), st),
+                      "hgd_sort_perm(rows)")
+            rows = rows_s
+            cols = _gather32(cols, perm)
+            if values is not None:
+                values = _gather32(values, perm)
+        return cls._from_sorted(rows, cols, values, n_rows, n_cols, split_threshold,
+                                split_chunk)
+
+    @classmethod
+    def _from_sorted(cls, rows: torch.Tensor, cols: torch.Tensor, values: Optional[torch.Tensor],
+                     n_rows: int, n_cols: int, split_threshold: int,
+                     split_chunk: int) -> "Incidence":
+        device = rows.device
+        lib = nat.load()
+        st = _stream(device)
+        nnz = int(rows.numel())
+        rowptr = torch.empty(n_rows + 1, dtype=torch.int64, device=device)
+        nat.check(lib.hgd_rowptr_from_sorted(rows.data_ptr() if nnz else None, nnz, n_rows,
+                                             rowptr.data_ptr(), st), "hgd_rowptr_from_sorted")
+        # CSC: stable sort of the column ids keeps rows ascending inside each column.
+        colptr = torch.empty(n_cols + 1, dtype=torch.int64, device=device)
+        csc_col = torch.empty(nnz, dtype=torch.int32, device=device)
+        val_t = None
+        if nnz:
+            keys = torch.empty(nnz, dtype=torch.int32, device=device)
+            perm = torch.empty(nnz, dtype=torch.int32, device=device)
+            ws = _ws(lib.hgd_sort_perm_workspace_size(nnz), device)
+            nat.check(lib.hgd_sort_perm(cols.data_ptr(), nnz, n_cols, keys.data_ptr(),
+                                        perm.data_ptr(), ws.data_ptr(), ws.numel(), st),
+                      "hgd_sort_perm(cols)")
+            del ws
+            nat.check(lib.hgd_rowptr_from_sorted(keys.data_ptr(), nnz, n_cols,
+                                                 colptr.data_ptr(), st),
+                      "hgd_rowptr_from_sorted(csc)")
+            del keys
+            csc_col = _gather32(rows, perm)
+            if values is not None:
+                val_t = _gather32(values, perm)
+            del perm
+        else:
+            colptr.zero_()
+        csr = CSR(rowptr, cols, n_rows, n_cols, split_threshold, split_chunk)
+        csc = CSR(colptr, csc_col, n_cols, n_rows, split_threshold, split_chunk)
+        c1, c2 = csr.plan_count_async(), csc.plan_count_async()
+        if c1 is not None:
+            csr._build_plan(*c1.tolist())
+        if c2 is not None:
+            csc._build_plan(*c2.tolist())
+        return cls(csr, csc, values, val_t)
+
+    @classmethod
+    def from_torch_sparse(cls, adj: torch.Tensor, device=None, **kw) -> "Incidence":
+        """From a torch sparse COO tensor as built by ``convert_sparse_mat_to_tensor``."""
+        if adj.layout != torch.sparse_coo:
+            raise TypeError("Incidence.from_torch_sparse expects a sparse COO tensor")
+        if device is None:
+            device = adj.device if adj.device.type == "cuda" else torch.device("cuda")
+        return cls.from_coo(adj._indices(), adj._values(), adj.shape, device=device, **kw)
+
+    @classmethod
+    def from_scipy(cls, mat, device="cuda", binary: bool = False, **kw) -> "Incidence":
+        """From a scipy sparse matrix (row-major COO order of ``tocoo()``, like the reference)."""
+        coo = mat.tocoo()
+        idx = torch.stack([torch.from_numpy(coo.row.astype("int64")),
+                           torch.from_numpy(coo.col.astype("int64"))])
+        vals = None if binary else torch.from_numpy(coo.data.astype("float32"))
+        return cls.from_coo(idx, vals, coo.shape, device=device, **kw)
+
+    @classmethod
+    def from_index_lists(cls, vertex: torch.Tensor, edges: torch.Tensor, n_vertices: int,
+                         n_edges: Optional[int] = None, device=None, **kw) -> "Incidence":
+        """Binary incidence B[vertex[k], edges[k]] (ED-HNN's V/E lists, EquivSetConv2.py:85-93).
+
+        ``n_edges`` defaults to max(edges)+1, the row count torch_scatter gives the edge means.
+        """
+        device = torch.device(device) if device is not None else vertex.device
+        if device.type != "cuda":
+            device = torch.device("cuda")
+        if n_edges is None:
+            n_edges = int(edges.max().item()) + 1 if edges.numel() else 0
+        idx = torch.stack([vertex.to(device=device, dtype=torch.int64),
+                           edges.to(device=device, dtype=torch.int64)])
+        return cls.from_coo(idx, None, (int(n_vertices), int(n_edges)), device=device, **kw)
+
+    # -- derived per-row / per-nonzero quantities --------------------------------------
+    def scale(self, side: str, kind: Optional[str]) -> Optional[torch.Tensor]:
+        """Degree scale over rows ('row') or columns ('col') of A.
+
+        kind: None → no scale; 'mean' → 1/deg (torch_scatter mean; 0 for empty);
+        'sym' → deg^-1/2 (data/graph.py:15-16, inf→0); 'wmean'/'wsym' use the weighted
+        degree Σ val (normalize_graph_mat's rowsum of a weighted matrix).
+        """
+        if kind is None:
+            return None
+        key = (side, kind)
+        s = self._scales.get(key)
+        if s is not None:
+            return s
+        o = self.csr if side == "row" else self.csc
+        weighted = kind.startswith("w")
+        power = {"mean": -1.0, "sym": -0.5}[kind[1:] if weighted else kind]
+        w = None
+        if weighted:
+            w = self.val if side == "row" else self.val_t
+        s = torch.empty(o.n_rows, dtype=torch.float32, device=self.device)
+        nat.check(nat.load().hgd_degree_scale(o.rowptr.data_ptr(), nat.ptr(w), o.n_rows, power,
+                                              s.data_ptr(), _stream(self.device)),
+                  "hgd_degree_scale")
+        self._scales[key] = s
+        return s
+
+    def edge_values(self, orient: str, src_kind: Optional[str]) -> Optional[torch.Tensor]:
+        """Per-nonzero weights for a hop over ``orient`` ('csr' or 'csc') with the SOURCE-side
+        diagonal folded in: w[e] = a[e] * S[src(e)], S = scale over the gathered side."""
+        key = (orient, src_kind or "")
+        if key in self._edge_vals:
+            return self._edge_vals[key]
+        o = self.csr if orient == "csr" else self.csc
+        base = self.val if orient == "csr" else self.val_t
+        src_side = "col" if orient == "csr" else "row"
+        s = self.scale(src_side, src_kind)
+        if s is None:
+            out = base
+        else:
+            out = torch.empty(o.nnz, dtype=torch.float32, device=self.device)
+            nat.check(nat.load().hgd_edge_values(
+                nat.ptr(base), None, s.data_ptr(), o.col.data_ptr() if o.nnz else None, o.nnz,
+                out.data_ptr(), _stream(self.device)), "hgd_edge_values")
+        self._edge_vals[key] = out
+        return out
+
+    def to_dense_cpu(self) -> torch.Tensor:
+        """Debug helper: the matrix as a dense CPU tensor (test use)."""
+        rp = self.csr.rowptr.cpu()
+        rows = torch.repeat_interleave(torch.arange(self.n_rows), rp[1:] - rp[:-1])
+        out = torch.zeros(self.n_rows, self.n_cols)
+        v = self.val.cpu() if self.val is not None else torch.ones(self.nnz)
+        out.index_put_((rows, self.csr.col.cpu().long()), v, accumulate=True)
+        return out
+
+
+def drop_edges(indices: torch.Tensor, values: torch.Tensor, mask: torch.Tensor,
+               keep_rate: float, count: Optional[int] = None):
+    """Device compaction of SpAdjDropEdge (model/graph/HCCF.py:217-226): keeps the COO entries
+    whose ``mask`` is set, in order, with ``values / keep_rate`` (IEEE fp32 division).
+    Returns (indices int64 [2, kept], values fp32 [kept]). ``count`` (kept entries) avoids a
+    device→host read when the caller already knows it (e.g. a host-drawn mask)."""
+    device = values.device
+    lib = nat.load()
+    st = _stream(device)
+    nnz = int(values.numel())
+    indices = indices.to(device=device, dtype=torch.int64)
+    rows = indices[0].contiguous()
+    cols = indices[1].contiguous()
+    m = mask.to(device=device, dtype=torch.uint8).contiguous()
+    if m.numel() != nnz:
+        raise ValueError("drop_edges: mask size mismatch")
+    n_out = torch.empty(1, dtype=torch.int64, device=device)
+    if count is None:
+        count = int(m.sum().item()) if nnz else 0
+    out_idx = torch.empty((2, count), dtype=torch.int64, device=device)
+    out_val = torch.empty(count, dtype=torch.float32, device=device)
+    ws = _ws(lib.hgd_dropedge_workspace_size(nnz), device)
+    nat.check(lib.hgd_dropedge_compact(
+        rows.data_ptr() if nnz else None, cols.data_ptr() if nnz else None,
+        values.contiguous().data_ptr() if nnz else None, m.data_ptr() if nnz else None, nnz,
+        float(keep_rate), out_idx[0].data_ptr() if count else None,
+        out_idx[1].data_ptr() if count else None, out_val.data_ptr() if count else None,
+        n_out.data_ptr(), ws.data_ptr(), ws.numel(), st), "hgd_dropedge_compact")
+    return out_idx, out_val
+
+
+def dense_threshold(H: torch.Tensor, thresh: float = 0.0):
+    """``torch.nonzero(H > thresh)`` of a dense 2-D fp32 device matrix as CSR
+    (rowptr int64 [n+1], cols int32 [nnz]) in row-major order
+    (EquivSetGNN.generate_V_E, model/layers/layers2/EquivSetGNN2.py:105-133)."""
+    if H.dim() != 2 or H.dtype != torch.float32:
+        raise TypeError("dense_threshold: expects a 2-D float32 matrix")
+    if H.stride(1) != 1:
+        H = H.contiguous()
+    device = H.device
+    lib = nat.load()
+    st = _stream(device)
+    n, k = H.shape
+    rowptr = torch.empty(n + 1, dtype=torch.int64, device=device)
+    ws = _ws(lib.hgd_dense_threshold_workspace_size(n), device)
+    nat.check(lib.hgd_dense_threshold_rowptr(H.data_ptr(), n, k, H.stride(0), float(thresh),
+                                             rowptr.data_ptr(), ws.data_ptr(), ws.numel(), st),
+              "hgd_dense_threshold_rowptr")
+    nnz = int(rowptr[n].item())
+    cols = torch.empty(nnz, dtype=torch.int32, device=device)
+    if nnz:
+        nat.check(lib.hgd_dense_threshold_fill(H.data_ptr(), n, k, H.stride(0), float(thresh),
+                                               rowptr.data_ptr(), cols.data_ptr(), st),
+                  "hgd_dense_threshold_fill")
+    return rowptr, cols
+
+
+def expand_rows(rowptr: torch.Tensor, nnz: int) -> torch.Tensor:
+    """Row id of every CSR nonzero (int32)."""
+    n_rows = rowptr.numel() - 1
+    out = torch.empty(nnz, dtype=torch.int32, device=rowptr.device)
+    if nnz:
+        nat.check(nat.load().hgd_expand_rows(rowptr.data_ptr(), n_rows, nnz, out.data_ptr(),
+                                             _stream(rowptr.device)), "hgd_expand_rows")
+    return out
+
+
+def _gather32(src: torch.Tensor, perm: torch.Tensor) -> torch.Tensor:
+    out = torch.empty_like(src)
+    n = perm.numel()
+    if n:
+        nat.check(nat.load().hgd_gather32(src.data_ptr(), perm.data_ptr(), n, out.data_ptr(),
+                                          _stream(src.device)), "hgd_gather32")
+    return out
+
+
+def incidence_of(adj, cache: bool = True) -> Incidence:
+    """The Incidence behind a torch sparse COO tensor (cached on the tensor object), or the
+    argument itself when it already is one."""
+    if isinstance(adj, Incidence):
+        return adj
+    inc = getattr(adj, "_hgd_incidence", None) if cache else None
+    if inc is None:
+        inc = Incidence.from_torch_sparse(adj)
+        if cache:
+            try:
+                adj._hgd_incidence = inc
+            except (AttributeError, RuntimeError):
+                pass
+    return inc

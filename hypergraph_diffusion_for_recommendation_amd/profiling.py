@@ -1,0 +1,73 @@
+"""Per-hop timing with HIP events plus the algorithmic-byte model of SURVEY.md §8(d).
+
+While a :class:`HopTimer` is active every :func:`incidence.spmm_csr` call records a start and
+an end event on the stream the hop is launched on (the current torch stream, which is the
+stream handed to ``hgd_spmm``) and remembers the hop's algorithmic bytes:
+
+    B_hop = nnz·(4 [col] + 4·[val] + 4d [gathered row]) + R·(4d [Y row] + 4·[row_scale])
+            + (R+1)·8 [int64 rowptr]
+
+i.e. what one launch must move at minimum: every index once, one d-wide fp32 row gathered per
+nonzero, every output row written once.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+
+_ACTIVE: Optional["HopTimer"] = None
+
+
+def hop_bytes(nnz: int, rows: int, d: int, has_val: bool, has_scale: bool) -> int:
+    return (nnz * (4 + (4 if has_val else 0) + 4 * d)
+            + rows * (4 * d + (4 if has_scale else 0)) + (rows + 1) * 8)
+
+
+class HopTimer:
+    def __init__(self):
+        self.records: List[tuple] = []
+
+    def __enter__(self):
+        global _ACTIVE
+        self._prev = _ACTIVE
+        _ACTIVE = self
+        return self
+
+    def __exit__(self, *exc):
+        global _ACTIVE
+        _ACTIVE = self._prev
+        return False
+
+    def begin(self):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+
+    def end(self, start, nbytes_fn):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        self.records.append((start, ev, nbytes_fn))
+
+    def summary(self) -> dict:
+        """Synchronises, then returns launches, total ms, total algorithmic bytes, GB/s."""
+        torch.cuda.synchronize()
+        ms = [s.elapsed_time(e) for s, e, _ in self.records]
+        nbytes = [f() for _, _, f in self.records]
+        tot_ms = float(sum(ms))
+        tot_b = int(sum(nbytes))
+        n = len(ms)
+        return {
+            "launches": n,
+            "total_ms": tot_ms,
+            "avg_ms": tot_ms / n if n else 0.0,
+            "bytes": tot_b,
+            "avg_bytes": tot_b / n if n else 0.0,
+            "gbps": (tot_b / (tot_ms * 1e-3) / 1e9) if tot_ms > 0 else 0.0,
+            "per_launch_ms": ms,
+            "per_launch_bytes": nbytes,
+        }
+
+
+def active() -> Optional[HopTimer]:
+    return _ACTIVE

@@ -1,0 +1,171 @@
+/*
+ * hgd.h — C ABI of libhgd, the MI355X (gfx950) hypergraph-propagation library.
+ *
+ * This is the drop-in boundary for the hot path named by BASELINE.json `north_star`:
+ * the incidence SpMM hops (Hᵀ·X then H·M, with degree normalisation) that sit under
+ * SELFRec's model/graph plugins, plus the per-step structure work feeding them.
+ * Every entry point replaces one implicit device-op call site of the reference
+ * (paths relative to /root/reference/HD_SELFRec):
+ *
+ *   hgd_spmm                 torch.sparse.mm(adj, X)            model/graph/HCCF.py:199,
+ *                            torch.sparse.mm(adj.t(), X)        model/graph/HGNN_HD4.py:459-462,
+ *                                                               model/graph/HGCN.py:173-175,
+ *                            torch_scatter.scatter(.., 'mean')  model/layers/layers2/EquivSetConv2.py:88-93
+ *                            (row_scale = 1/count is the scatter-mean; val = per-nonzero weight)
+ *   hgd_sort_perm            COO→CSR / CSR→CSC ordering that cuSPARSE re-derives per call
+ *                            (`adj.t()` in HGCNConv.forward, HGNN_HD4.py:459; coalesce in torch.sparse.mm)
+ *   hgd_rowptr_from_sorted   row pointer of a row-sorted COO  base/torch_interface.py:8-12
+ *   hgd_degree_scale         D^-1/2 and D^-1 of data/graph.py:11-25 (inf→0) and data/graph.py:28-42
+ *   hgd_edge_values          per-nonzero weights with a source-side diagonal folded in
+ *   hgd_dropedge_compact     SpAdjDropEdge.forward, model/graph/HCCF.py:213-226 (vals[mask]/keep, idxs[:,mask])
+ *   hgd_dense_threshold_*    torch.nonzero(hypergraph > 0), model/layers/layers2/EquivSetGNN2.py:105-133
+ *                            (row-major order identical to torch.nonzero)
+ *
+ * Conventions:
+ *   - All pointers are DEVICE pointers unless a parameter says "host".
+ *   - The caller owns every buffer; the library never allocates or frees caller memory.
+ *     Scratch comes from a caller-provided workspace sized by the matching *_workspace_size.
+ *   - Every call is stream-ordered on `stream` (a hipStream_t passed as void*; NULL = legacy
+ *     default stream) and performs no host synchronisation, so it can be graph-captured.
+ *   - Errors come back as hgd_status; hgd_get_last_error_string() describes the last failure
+ *     on the calling thread. No C++ exception crosses the ABI.
+ *   - Indices: row pointers are int64, column/row indices are int32 (rows, cols < 2^31).
+ *   - Floating point is fp32 in and out; sums run in fp32 in edge order (deterministic).
+ */
+#ifndef HGD_H
+#define HGD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum hgd_status {
+  HGD_OK = 0,
+  HGD_ERR_INVALID_ARG = 1,
+  HGD_ERR_HIP = 2,
+  HGD_ERR_UNSUPPORTED = 3,
+  HGD_ERR_WORKSPACE = 4
+} hgd_status;
+
+typedef enum hgd_epilogue {
+  HGD_EPI_NONE = 0,
+  HGD_EPI_LEAKY_RELU = 1, /* nn.LeakyReLU(negative_slope=slope): HGCNConv act=True */
+  HGD_EPI_RELU = 2
+} hgd_epilogue;
+
+/* Library ABI version (major*10000 + minor*100 + patch). */
+int hgd_version(void);
+/* Human-readable description of the last error on this thread ("" if none). */
+const char* hgd_get_last_error_string(void);
+
+/* ------------------------------------------------------------------------------------------
+ * Split plan for long rows. Rows whose degree exceeds `threshold` are cut into chunks of
+ * `chunk` nonzeros, summed by separate wavefront groups into a workspace, then combined in
+ * chunk order (deterministic, no atomics). All arrays are device arrays built by
+ * hgd_split_plan_build; a NULL plan or n_heavy == 0 means no row is split.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct hgd_split_plan {
+  int64_t threshold;           /* rows with degree > threshold are split (<=0: none)   */
+  int32_t chunk;               /* nonzeros per chunk                                    */
+  int32_t _pad;
+  int64_t n_heavy;             /* number of split rows                                  */
+  int64_t n_chunks;            /* total chunks over all split rows                      */
+  const int32_t* heavy_rows;   /* [n_heavy]   split row ids, ascending                  */
+  const int64_t* heavy_cptr;   /* [n_heavy+1] chunk range of each split row             */
+  const int32_t* chunk_heavy;  /* [n_chunks]  split-row index owning each chunk         */
+} hgd_split_plan;
+
+/* Counts (n_heavy, n_chunks) for a plan into device int64[2] `counts`. */
+hgd_status hgd_split_plan_count(const int64_t* rowptr, int64_t n_rows, int64_t threshold,
+                                int32_t chunk, int64_t* counts, void* stream);
+size_t hgd_split_plan_workspace_size(int64_t n_rows);
+/* Fills plan->heavy_rows / heavy_cptr / chunk_heavy (caller-allocated, sized from counts). */
+hgd_status hgd_split_plan_build(const int64_t* rowptr, int64_t n_rows, int64_t threshold,
+                                int32_t chunk, int32_t* heavy_rows, int64_t* heavy_cptr,
+                                int32_t* chunk_heavy, int64_t n_heavy, int64_t n_chunks,
+                                void* workspace, size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * One SpMM hop over a CSR structure (the CSC of H is the CSR of Hᵀ):
+ *   for r in [row_begin, row_end):
+ *     Y[r, 0:d] = epi( row_scale[r] * Σ_{e=rowptr[r]}^{rowptr[r+1]-1} val[e] * X[col[e], 0:d] )
+ * val == NULL means all ones; row_scale == NULL means 1. X rows are n_src_rows × ldx floats.
+ * Rows outside [row_begin,row_end) are not written. Workspace: hgd_spmm_workspace_size.
+ * ---------------------------------------------------------------------------------------- */
+size_t hgd_spmm_workspace_size(const hgd_split_plan* plan, int32_t d);
+hgd_status hgd_spmm(const int64_t* rowptr, const int32_t* col, const float* val,
+                    const float* row_scale, int64_t n_rows, int64_t n_src_rows,
+                    int64_t row_begin, int64_t row_end, const float* X, int64_t ldx, float* Y,
+                    int64_t ldy, int32_t d, int32_t epilogue, float slope,
+                    const hgd_split_plan* plan, void* workspace, size_t workspace_bytes,
+                    void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Structure primitives (all deterministic; indices bit-exact with the CPU restatement).
+ * ---------------------------------------------------------------------------------------- */
+/* int64 indices → int32, checking 0 <= v < upper; err_count (device int64) += #violations. */
+hgd_status hgd_index_narrow(const int64_t* in, int64_t n, int64_t upper, int32_t* out,
+                            int64_t* err_count, void* stream);
+/* Stable sort of int32 keys in [0, n_keys): keys_out = sorted keys, perm_out[i] = source position. */
+size_t hgd_sort_perm_workspace_size(int64_t n);
+hgd_status hgd_sort_perm(const int32_t* keys, int64_t n, int64_t n_keys, int32_t* keys_out,
+                         int32_t* perm_out, void* workspace, size_t workspace_bytes,
+                         void* stream);
+/* rowptr[r] = first position p with sorted_rows[p] >= r, r in [0, n_rows]. */
+hgd_status hgd_rowptr_from_sorted(const int32_t* sorted_rows, int64_t nnz, int64_t n_rows,
+                                  int64_t* rowptr, void* stream);
+/* Counts positions where sorted_rows decreases or leaves [0,n_rows) into device int64 *bad. */
+hgd_status hgd_check_sorted(const int32_t* rows, int64_t nnz, int64_t n_rows, int64_t* bad,
+                            void* stream);
+/* rows_out[e] = r for e in [rowptr[r], rowptr[r+1]), nnz = rowptr[n_rows]. */
+hgd_status hgd_expand_rows(const int64_t* rowptr, int64_t n_rows, int64_t nnz, int32_t* rows_out,
+                           void* stream);
+/* out[i] = src[perm[i]] (4-byte elements: int32 or fp32 bit patterns). */
+hgd_status hgd_gather32(const void* src, const int32_t* perm, int64_t n, void* out,
+                        void* stream);
+/* s[r] = deg(r)^power with deg = rowptr diff (val == NULL) or Σ val over the row; deg == 0 → 0.
+ * power is -1.0 (D^-1) or -0.5 (D^-1/2) or any other exponent. */
+hgd_status hgd_degree_scale(const int64_t* rowptr, const float* val, int64_t n_rows,
+                            double power, float* scale_out, void* stream);
+/* out[e] = (base ? base[perm ? perm[e] : e] : 1) * (src_scale ? src_scale[src_idx[e]] : 1). */
+hgd_status hgd_edge_values(const float* base, const int32_t* perm, const float* src_scale,
+                           const int32_t* src_idx, int64_t n, float* out, void* stream);
+
+/* Drop-edge compaction (SpAdjDropEdge): keeps entries with mask[e] != 0 in order,
+ * out_val = val[e] / keep. Writes the kept count to device int64 *out_count. */
+size_t hgd_dropedge_workspace_size(int64_t nnz);
+hgd_status hgd_dropedge_compact(const int64_t* rows, const int64_t* cols, const float* val,
+                                const uint8_t* mask, int64_t nnz, float keep,
+                                int64_t* out_rows, int64_t* out_cols, float* out_val,
+                                int64_t* out_count, void* workspace, size_t workspace_bytes,
+                                void* stream);
+
+/* torch.nonzero(H > thresh) of a dense row-major [n_rows, n_cols] fp32 matrix (leading dim ld),
+ * in two passes: rowptr (n_rows+1, int64) then the column list (rowptr[n_rows] int32 entries). */
+size_t hgd_dense_threshold_workspace_size(int64_t n_rows);
+hgd_status hgd_dense_threshold_rowptr(const float* H, int64_t n_rows, int64_t n_cols, int64_t ld,
+                                      float thresh, int64_t* rowptr, void* workspace,
+                                      size_t workspace_bytes, void* stream);
+hgd_status hgd_dense_threshold_fill(const float* H, int64_t n_rows, int64_t n_cols, int64_t ld,
+                                    float thresh, const int64_t* rowptr, int32_t* cols,
+                                    void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Elementwise epilogues around the hops (contiguous fp32, 16-byte aligned).
+ *   apply:    y = epi(z)                                   (nn.LeakyReLU / nn.ReLU forward)
+ *   backward: dz = dy * (ref > 0 ? 1 : slope) for LEAKY, dy * (ref > 0) for RELU, where ref is
+ *             the pre-activation (or the output when slope >= 0, which has the same sign).
+ * ---------------------------------------------------------------------------------------- */
+hgd_status hgd_epilogue_apply(const float* z, int64_t n, int32_t epilogue, float slope, float* y,
+                              void* stream);
+hgd_status hgd_epilogue_backward(const float* ref, const float* dy, int64_t n, int32_t epilogue,
+                                 float slope, float* dz, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HGD_H */

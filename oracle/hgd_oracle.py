@@ -1,0 +1,341 @@
+"""CPU oracle for the hypergraph-propagation hot path — TEST INFRASTRUCTURE ONLY.
+
+This module is a plain numpy restatement of the reference's algorithm for the path named by
+BASELINE.json ``north_star``. Only ``tests/``, ``__graft_entry__.smoke()`` and the
+``cpu_baseline`` leg of ``bench.py`` may import it, and only as the checker; the product path
+(``hypergraph_diffusion_for_recommendation_amd``) never calls it and fails loudly without its
+HIP library.
+
+Parity status: **parity unpinned by the reference itself.** The reference ships no tests, golden
+vectors or fixtures for this path, and importing/running the reference in
+this container was denied by the environment, so no reference outputs exist.
+The restatement is pinned instead by (i) hand-derived known-answer cases, (ii) cross-checks
+against the torch-CPU library calls the reference itself makes (``oracle/ref_cpu.py``:
+``torch.sparse.mm``, ``index_reduce_('mean')`` for torch_scatter's mean), and (iii) algebraic
+properties (adjointness, row-stochastic means).
+
+Floating point is float64 here; integer/index results (orders, masks, row pointers) are exact.
+Every function cites the reference file:line it restates (relative to
+/root/reference/HD_SELFRec).
+"""
+from __future__ import annotations
+
+import numpy as np
+import scipy.sparse as sp
+
+
+# ---------------------------------------------------------------------------------------------
+# Graph construction — data/ui_graph.py, data/graph.py, base/torch_interface.py
+# ---------------------------------------------------------------------------------------------
+def remap_ids(pairs):
+    """Id maps in first-appearance order of the training file (data/ui_graph.py:107-125)."""
+    user, item = {}, {}
+    for u, i in pairs:
+        if u not in user:
+            user[u] = len(user)
+        if i not in item:
+            item[i] = len(item)
+    return user, item
+
+
+def bipartite_adjacency(user_idx, item_idx, n_users, n_items):
+    """ui_adj = [[0, R], [Rᵀ, 0]] as float32 CSR, duplicates summed
+    (Interaction.__create_sparse_bipartite_adjacency, data/ui_graph.py:134-148)."""
+    n = n_users + n_items
+    user_idx = np.asarray(user_idx)
+    item_idx = np.asarray(item_idx)
+    ratings = np.ones_like(user_idx, dtype=np.float32)
+    tmp = sp.csr_matrix((ratings, (user_idx, item_idx + n_users)), shape=(n, n),
+                        dtype=np.float32)
+    return tmp + tmp.T
+
+
+def normalize_graph_mat(adj):
+    """D^-1/2·A·D^-1/2 for square, D^-1·A otherwise, inf→0 (Graph.normalize_graph_mat,
+    data/graph.py:11-25). Float32 like the reference (rowsum of a float32 matrix)."""
+    shape = adj.get_shape()
+    rowsum = np.array(adj.sum(1))
+    with np.errstate(divide="ignore"):
+        if shape[0] == shape[1]:
+            d_inv = np.power(rowsum, -0.5).flatten()
+            d_inv[np.isinf(d_inv)] = 0.0
+            d = sp.diags(d_inv)
+            return d.dot(adj).dot(d)
+        d_inv = np.power(rowsum, -1).flatten()
+        d_inv[np.isinf(d_inv)] = 0.0
+        return sp.diags(d_inv).dot(adj)
+
+
+def normalize_graph_mat_hyper(H):
+    """D_v^-1/2·H·D_e^-1·Hᵀ·D_v^-1/2 (Graph.normalize_graph_mat_hyper, data/graph.py:28-42) —
+    the operator the benchmark's hgconv2 applies without forming it."""
+    colsum = np.array(H.sum(0))
+    rowsum = np.array(H.sum(1))
+    with np.errstate(divide="ignore"):
+        de = np.power(colsum, -1.0).flatten()
+        de[np.isinf(de)] = 0.0
+        dv = np.power(rowsum, -0.5).flatten()
+        dv[np.isinf(dv)] = 0.0
+    Dv, De = sp.diags(dv), sp.diags(de)
+    return Dv.dot(H).dot(De).dot(H.T).dot(Dv)
+
+
+def coo_of(mat):
+    """(indices int64 [2,nnz], values float32) in ``tocoo()`` order
+    (TorchGraphInterface.convert_sparse_mat_to_tensor, base/torch_interface.py:8-12)."""
+    coo = mat.tocoo()
+    idx = np.stack([coo.row.astype(np.int64), coo.col.astype(np.int64)])
+    return idx, coo.data.astype(np.float32)
+
+
+# ---------------------------------------------------------------------------------------------
+# Structure (integer, bit-exact)
+# ---------------------------------------------------------------------------------------------
+def csr_from_coo(rows, cols, n_rows, vals=None):
+    """Stable row ordering of a COO (entries keep their order inside a row), row pointer."""
+    rows = np.asarray(rows, dtype=np.int64)
+    cols = np.asarray(cols, dtype=np.int64)
+    perm = np.argsort(rows, kind="stable")
+    rowptr = np.zeros(n_rows + 1, dtype=np.int64)
+    np.add.at(rowptr, rows + 1, 1)
+    rowptr = np.cumsum(rowptr)
+    v = None if vals is None else np.asarray(vals)[perm]
+    return rowptr, cols[perm].astype(np.int32), v, perm
+
+
+def transpose_csr(rowptr, col, n_cols, vals=None):
+    """CSC of a CSR via a stable counting sort on the column id: inside every column the rows
+    stay ascending (the order ``adj.t()`` + coalesce produces for a row-sorted COO)."""
+    n_rows = len(rowptr) - 1
+    rows = np.repeat(np.arange(n_rows, dtype=np.int64), np.diff(rowptr))
+    perm = np.argsort(col, kind="stable")
+    colptr = np.zeros(n_cols + 1, dtype=np.int64)
+    np.add.at(colptr, np.asarray(col, dtype=np.int64) + 1, 1)
+    colptr = np.cumsum(colptr)
+    v = None if vals is None else np.asarray(vals)[perm]
+    return colptr, rows[perm].astype(np.int32), v, perm
+
+
+def split_plan(rowptr, threshold, chunk):
+    """Rows with degree > threshold, their chunk ranges and each chunk's owner
+    (the deterministic long-row split of hgd_spmm; not a reference concept)."""
+    deg = np.diff(rowptr)
+    heavy = np.nonzero(deg > threshold)[0].astype(np.int32)
+    nch = (deg[heavy] + chunk - 1) // chunk
+    cptr = np.concatenate([[0], np.cumsum(nch)]).astype(np.int64)
+    chunk_heavy = np.repeat(np.arange(len(heavy), dtype=np.int32), nch)
+    return heavy, cptr, chunk_heavy
+
+
+def dropedge(indices, values, mask, keep_rate):
+    """SpAdjDropEdge.forward (model/graph/HCCF.py:217-226): keep entries where mask is set,
+    in order, values divided by keepRate in float32. ``mask`` is
+    ``((torch.rand(nnz) + keepRate).floor()).type(torch.bool)`` drawn by the caller."""
+    mask = np.asarray(mask, dtype=bool)
+    new_idx = np.asarray(indices)[:, mask]
+    new_vals = (np.asarray(values, dtype=np.float32)[mask] / np.float32(keep_rate)).astype(
+        np.float32)
+    return new_idx, new_vals
+
+
+def nonzero_threshold(dense, thresh=0.0):
+    """torch.nonzero(H > thresh) row-major (EquivSetGNN.generate_V_E,
+    model/layers/layers2/EquivSetGNN2.py:105-133): V = rows, E = cols."""
+    r, c = np.nonzero(np.asarray(dense) > thresh)
+    return r.astype(np.int64), c.astype(np.int64)
+
+
+# ---------------------------------------------------------------------------------------------
+# Propagation (float64)
+# ---------------------------------------------------------------------------------------------
+def spmm_coo(rows, cols, vals, n_rows, X):
+    """Y = A·X for COO A (torch.sparse.mm(adj, X), HCCF.py:199); float64, duplicates summed."""
+    X = np.asarray(X, dtype=np.float64)
+    Y = np.zeros((n_rows, X.shape[1]), dtype=np.float64)
+    w = np.ones(len(rows)) if vals is None else np.asarray(vals, dtype=np.float64)
+    np.add.at(Y, np.asarray(rows), w[:, None] * X[np.asarray(cols)])
+    return Y
+
+
+def spmm_csr(rowptr, col, X, val=None, row_scale=None, epi=None, slope=0.0, absolute=False):
+    """The hgd_spmm contract in float64: Y[r] = epi(s[r]·Σ val[e]·X[col[e]]).
+    ``absolute=True`` returns Σ|s·val·X| (the magnitude the fp32 tolerance is scaled by)."""
+    X = np.asarray(X, dtype=np.float64)
+    n_rows = len(rowptr) - 1
+    rows = np.repeat(np.arange(n_rows), np.diff(rowptr))
+    w = np.ones(len(col)) if val is None else np.asarray(val, dtype=np.float64)
+    s = np.ones(n_rows) if row_scale is None else np.asarray(row_scale, dtype=np.float64)
+    terms = w[:, None] * X[np.asarray(col, dtype=np.int64)]
+    if absolute:
+        terms = np.abs(terms)
+    Y = np.zeros((n_rows, X.shape[1]))
+    np.add.at(Y, rows, terms)
+    Y *= (np.abs(s) if absolute else s)[:, None]
+    if not absolute:
+        Y = epilogue(Y, epi, slope)
+    return Y
+
+
+def epilogue(Y, epi, slope):
+    """nn.LeakyReLU(negative_slope) / nn.ReLU (HGCNConv act=True, HGNN_HD4.py:459-460)."""
+    if epi == "leaky_relu":
+        return np.where(Y > 0, Y, Y * slope)
+    if epi == "relu":
+        return np.where(Y > 0, Y, 0.0)
+    return Y
+
+
+def degree_scale(deg, power):
+    """deg^power with 0 → 0 (np.power(.., -p) then inf→0, data/graph.py:15-16)."""
+    deg = np.asarray(deg, dtype=np.float64)
+    out = np.zeros_like(deg)
+    nz = deg != 0
+    out[nz] = np.power(deg[nz], power)
+    return out
+
+
+def scatter_mean(src, index, dim_size=None):
+    """torch_scatter.scatter(src, index, dim=-2, reduce='mean') (pytorch-scatter 2.1.0,
+    selfrec.yml:181): out size dim_size or max(index)+1, sum / clamp(count, min=1)."""
+    src = np.asarray(src, dtype=np.float64)
+    index = np.asarray(index, dtype=np.int64)
+    n = dim_size if dim_size is not None else (int(index.max()) + 1 if len(index) else 0)
+    out = np.zeros((n, src.shape[1]))
+    np.add.at(out, index, src)
+    cnt = np.bincount(index, minlength=n).astype(np.float64)
+    return out / np.maximum(cnt, 1.0)[:, None]
+
+
+def equivset_mean_2hop(X, V, E, N):
+    """EquivSetConv.forward core with W1 = Identity, W2 = the Xev slice (mlp2_layers = 0),
+    alpha = 0 (layers2/EquivSetConv2.py:85-97; args HGNN_HD4.py:371-388):
+    Xe = scatter_mean(X[V], E); Xv = scatter_mean(Xe[E], V, dim_size=N)."""
+    X = np.asarray(X, dtype=np.float64)
+    Xe = scatter_mean(X[V], E)
+    return scatter_mean(Xe[E], V, dim_size=N)
+
+
+def two_hop(rows, cols, vals, shape, X, P=None, Q=None, R=None, epi=None, slope=0.0):
+    """epi(P·A·Q·Aᵀ·R·X) for COO A with named diagonal scales (None/'mean'/'sym'/'wmean'/
+    'wsym'); HGCNConv is P=Q=R=None (HGNN_HD4.py:455-462), hgconv2 is P=R='sym', Q='mean'
+    (data/graph.py:28-42), the ED-HNN mean pair is P=Q='mean' (EquivSetConv2.py:88-93)."""
+    n_r, n_c = shape
+    rows = np.asarray(rows, dtype=np.int64)
+    cols = np.asarray(cols, dtype=np.int64)
+    w = np.ones(len(rows)) if vals is None else np.asarray(vals, dtype=np.float64)
+    Ps = _scale(rows, w, n_r, P)
+    Qs = _scale(cols, w, n_c, Q)
+    Rs = _scale(rows, w, n_r, R)
+    X = np.asarray(X, dtype=np.float64) * Rs[:, None]
+    M = spmm_coo(cols, rows, w, n_c, X) * Qs[:, None]
+    Y = spmm_coo(rows, cols, w, n_r, M) * Ps[:, None]
+    return epilogue(Y, epi, slope)
+
+
+def two_hop_backward(rows, cols, vals, shape, Y_out, dY, P=None, Q=None, R=None, epi=None,
+                     slope=0.0):
+    """dX of :func:`two_hop`: dZ = dY·epi'(Z); dX = R·A·Q·Aᵀ·P·dZ."""
+    n_r, n_c = shape
+    rows = np.asarray(rows, dtype=np.int64)
+    cols = np.asarray(cols, dtype=np.int64)
+    w = np.ones(len(rows)) if vals is None else np.asarray(vals, dtype=np.float64)
+    dZ = np.asarray(dY, dtype=np.float64)
+    if epi == "leaky_relu":
+        dZ = np.where(np.asarray(Y_out) > 0, dZ, dZ * slope)
+    elif epi == "relu":
+        dZ = np.where(np.asarray(Y_out) > 0, dZ, 0.0)
+    Ps = _scale(rows, w, n_r, P)
+    Qs = _scale(cols, w, n_c, Q)
+    Rs = _scale(rows, w, n_r, R)
+    dM = spmm_coo(cols, rows, w, n_c, dZ * Ps[:, None]) * Qs[:, None]
+    return spmm_coo(rows, cols, w, n_r, dM) * Rs[:, None]
+
+
+def _scale(idx, w, n, kind):
+    if kind is None:
+        return np.ones(n)
+    weighted = kind.startswith("w")
+    base = kind[1:] if weighted else kind
+    deg = np.zeros(n)
+    np.add.at(deg, idx, w if weighted else 1.0)
+    return degree_scale(deg, {"mean": -1.0, "sym": -0.5}[base])
+
+
+def hgconv2(H, X):
+    """D_v^-1/2·H·D_e^-1·Hᵀ·D_v^-1/2·X for a scipy incidence H [V,E] (data/graph.py:28-42)."""
+    H = H.tocoo()
+    return two_hop(H.row, H.col, None, H.shape, X, P="sym", Q="mean", R="sym")
+
+
+def layer_norm(X, weight=None, bias=None, eps=1e-5):
+    """nn.LayerNorm(d) over the last dim (MLP InputNorm, model/layers/MLP.py:65-71)."""
+    X = np.asarray(X, dtype=np.float64)
+    mu = X.mean(-1, keepdims=True)
+    var = X.var(-1, keepdims=True)
+    Y = (X - mu) / np.sqrt(var + eps)
+    if weight is not None:
+        Y = Y * weight
+    if bias is not None:
+        Y = Y + bias
+    return Y
+
+
+def linear(X, W, b=None):
+    """nn.Linear: X·Wᵀ + b."""
+    Y = np.asarray(X, dtype=np.float64) @ np.asarray(W, dtype=np.float64).T
+    return Y if b is None else Y + b
+
+
+def equivset_conv(X, V, E, X0, alpha, ln_w, ln_b, lin_w, lin_b):
+    """EquivSetConv2.forward with the HGNN_HD4 configuration (W1 = Identity, W2 = slice,
+    W = MLP('ln', InputNorm, 1 layer) = Linear(LayerNorm(·))), layers2/EquivSetConv2.py:85-100,
+    model/layers/MLP.py:65-72,109-117."""
+    N = X.shape[0]
+    Xv = equivset_mean_2hop(X, V, E, N)
+    Xv = (1 - alpha) * Xv + alpha * np.asarray(X0, dtype=np.float64)
+    return linear(layer_norm(Xv, ln_w, ln_b), lin_w, lin_b)
+
+
+# ---------------------------------------------------------------------------------------------
+# HCCF encoder (dense learned hypergraph) — model/graph/HCCF.py:173-211
+# ---------------------------------------------------------------------------------------------
+def hccf_forward(norm_adj_rows, norm_adj_cols, norm_adj_vals, N, E_u, E_i, W_u, W_i, n_layers):
+    """HCCFEncoder.forward with keep_rate = 1 and dropout off (HCCF.py:173-191): per layer
+    gcn = Â·h, hyper_u = H_u·(H_uᵀ·h_u) with H_u = E_u·W_u (same for items); h += gcn + hyper."""
+    E_u = np.asarray(E_u, dtype=np.float64)
+    E_i = np.asarray(E_i, dtype=np.float64)
+    Hu = E_u @ np.asarray(W_u, dtype=np.float64)
+    Hi = E_i @ np.asarray(W_i, dtype=np.float64)
+    U = E_u.shape[0]
+    h = np.concatenate([E_u, E_i], 0)
+    hidden = [h]
+    gcns, hyps = [], []
+    for _ in range(n_layers):
+        g = spmm_coo(norm_adj_rows, norm_adj_cols, norm_adj_vals, N, hidden[-1])
+        hu = Hu @ (Hu.T @ hidden[-1][:U])
+        hi = Hi @ (Hi.T @ hidden[-1][U:])
+        hyp = np.concatenate([hu, hi], 0)
+        gcns.append(g)
+        hyps.append(hyp)
+        hidden.append(g + hyp)
+    emb = sum(hidden)
+    return emb[:U], emb[U:], gcns, hyps
+
+
+# ---------------------------------------------------------------------------------------------
+# Synthetic graphs (SURVEY.md §8d generator)
+# ---------------------------------------------------------------------------------------------
+def synthetic_incidence(n_users, n_items, nnz, seed=0, zipf=None):
+    """U×I binary incidence: PCG64(seed) uniform users and items (or Zipf(zipf) items,
+    truncated to I), deduplicated, row-major sorted. Returns (rows, cols) int64."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    u = rng.integers(0, n_users, size=nnz, dtype=np.int64)
+    if zipf is None:
+        i = rng.integers(0, n_items, size=nnz, dtype=np.int64)
+    else:
+        ranks = np.arange(1, n_items + 1, dtype=np.float64)
+        p = ranks ** (-float(zipf))
+        p /= p.sum()
+        i = rng.choice(n_items, size=nnz, p=p).astype(np.int64)
+    key = np.unique(u * n_items + i)
+    return key // n_items, key % n_items

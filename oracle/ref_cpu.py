@@ -1,0 +1,73 @@
+"""torch-CPU restatement of the reference path — TEST INFRASTRUCTURE / CPU BASELINE ONLY.
+
+Uses the very library calls the reference makes (paths relative to
+/root/reference/HD_SELFRec), so it doubles as the ``cpu_baseline`` (kind "port") of bench.py
+and as a second, independent cross-check of ``oracle/hgd_oracle.py``:
+
+* COO built like TorchGraphInterface.convert_sparse_mat_to_tensor (base/torch_interface.py:8-12)
+* hops with ``torch.sparse.mm`` (GCNLayer HCCF.py:199; HGCNConv HGNN_HD4.py:459-462, which
+  re-derives ``adj.t()`` per call)
+* torch_scatter's mean restated as ``index_reduce_(..., 'mean', include_self=False)``
+  (EquivSetConv2.py:89,93 — torch_scatter itself is not installed here)
+* backward by autograd, as in the reference training loop (HCCF.py:93-96).
+
+Never imported by the product package.
+"""
+from __future__ import annotations
+
+import torch
+
+
+def coo_tensor(rows, cols, vals, shape):
+    i = torch.stack([torch.as_tensor(rows, dtype=torch.int64),
+                     torch.as_tensor(cols, dtype=torch.int64)])
+    v = (torch.ones(i.shape[1], dtype=torch.float32) if vals is None
+         else torch.as_tensor(vals, dtype=torch.float32))
+    return torch.sparse_coo_tensor(i, v, tuple(shape))
+
+
+def degree_scale(idx, n, power, weights=None):
+    deg = torch.zeros(n, dtype=torch.float32)
+    deg.index_add_(0, torch.as_tensor(idx, dtype=torch.int64),
+                   torch.ones(len(idx)) if weights is None else weights)
+    s = torch.pow(deg, power)
+    s[torch.isinf(s)] = 0.0
+    return s
+
+
+def hgconv2(H: torch.Tensor, X: torch.Tensor, dv=None, de=None) -> torch.Tensor:
+    """D_v^-1/2·H·D_e^-1·Hᵀ·D_v^-1/2·X with torch.sparse.mm (data/graph.py:28-42 operator);
+    H is a sparse COO [V, E]. Autograd flows to X."""
+    Hi = H._indices()
+    if dv is None:
+        dv = degree_scale(Hi[0], H.shape[0], -0.5)
+    if de is None:
+        de = degree_scale(Hi[1], H.shape[1], -1.0)
+    M = torch.sparse.mm(H.t(), X * dv[:, None]) * de[:, None]
+    return torch.sparse.mm(H, M) * dv[:, None]
+
+
+def hgcn_conv(adj: torch.Tensor, X: torch.Tensor, act=True, slope=0.5) -> torch.Tensor:
+    """HGCNConv.forward (HGNN_HD4.py:455-462): leaky(A·(Aᵀ·X)) or no activation."""
+    Y = torch.sparse.mm(adj, torch.sparse.mm(adj.t(), X))
+    return torch.nn.functional.leaky_relu(Y, slope) if act else Y
+
+
+def scatter_mean(src: torch.Tensor, index: torch.Tensor, dim_size=None) -> torch.Tensor:
+    n = dim_size if dim_size is not None else int(index.max()) + 1
+    out = torch.zeros((n, src.shape[1]), dtype=src.dtype)
+    return out.index_reduce_(0, index, src, "mean", include_self=False)
+
+
+def equivset_mean_2hop(X: torch.Tensor, V: torch.Tensor, E: torch.Tensor, N: int):
+    """EquivSetConv2.forward core (layers2/EquivSetConv2.py:88-93)."""
+    Xe = scatter_mean(X[V], E)
+    return scatter_mean(Xe[E], V, dim_size=N)
+
+
+def hgconv2_fwd_bwd(H: torch.Tensor, X: torch.Tensor, dY: torch.Tensor):
+    """One fwd+bwd of the benchmarked op on CPU; returns (Y, dX)."""
+    X = X.detach().requires_grad_(True)
+    Y = hgconv2(H, X)
+    (dX,) = torch.autograd.grad(Y, X, dY)
+    return Y.detach(), dX

@@ -1,0 +1,147 @@
+"""Parity of the hgd_spmm hop (HIP, gfx950) against the float64 oracle.
+
+Every case goes through the C ABI (libhgd.so via ctypes). Tolerance: |got - ref| <= 1e-5·Σ|terms|
+element-wise (tests/_util.py).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import hgd_oracle as O
+from tests._util import assert_close, random_coo
+
+pytestmark = pytest.mark.gpu
+
+
+def _build(rows, cols, vals, shape, dev, **kw):
+    from hypergraph_diffusion_for_recommendation_amd import Incidence
+    idx = torch.from_numpy(np.stack([rows, cols]))
+    v = None if vals is None else torch.from_numpy(vals.astype(np.float32))
+    return Incidence.from_coo(idx, v, shape, device=dev, **kw)
+
+
+@pytest.mark.parametrize("d", [1, 3, 4, 8, 16, 32, 48, 64, 96, 128, 256, 320])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_spmm_dims(dev, d, weighted):
+    from hypergraph_diffusion_for_recommendation_amd import spmm_csr
+    rng = np.random.default_rng(d * 7 + weighted)
+    R, C = 173, 129
+    r, c = random_coo(rng, R, C, 2500)
+    vals = rng.standard_normal(len(r)).astype(np.float32) if weighted else None
+    inc = _build(r, c, vals, (R, C), dev)
+    X = rng.standard_normal((C, d)).astype(np.float32)
+    scale = rng.random(R).astype(np.float32) if weighted else None
+    Y = spmm_csr(inc.csr, torch.from_numpy(X).to(dev), val=inc.val,
+                 row_scale=None if scale is None else torch.from_numpy(scale).to(dev))
+    rowptr, col, v, _ = O.csr_from_coo(r, c, R, vals)
+    ref = O.spmm_csr(rowptr, col, X, v, scale)
+    mag = O.spmm_csr(rowptr, col, X, v, scale, absolute=True)
+    assert_close(Y.cpu().numpy(), ref, mag, what=f"spmm d={d}")
+
+
+@pytest.mark.parametrize("d", [8, 64, 128])
+def test_spmm_transpose_hop(dev, d):
+    from hypergraph_diffusion_for_recommendation_amd import spmm_csr
+    rng = np.random.default_rng(11 + d)
+    R, C = 300, 77
+    r, c = random_coo(rng, R, C, 4000)
+    vals = rng.random(len(r)).astype(np.float32)
+    inc = _build(r, c, vals, (R, C), dev)
+    X = rng.standard_normal((R, d)).astype(np.float32)
+    Y = spmm_csr(inc.csc, torch.from_numpy(X).to(dev), val=inc.val_t)
+    ref = O.spmm_coo(c, r, vals, C, X)
+    mag = O.spmm_coo(c, r, np.abs(vals), C, np.abs(X))
+    assert_close(Y.cpu().numpy(), ref, mag, what="Aᵀ·X")
+
+
+@pytest.mark.parametrize("d", [4, 32, 64, 256, 7])
+@pytest.mark.parametrize("epi", [None, "leaky_relu", "relu"])
+def test_spmm_split_rows_and_epilogue(dev, d, epi):
+    """Long rows through the deterministic chunk split (threshold 16, chunk 8)."""
+    from hypergraph_diffusion_for_recommendation_amd import spmm_csr
+    from hypergraph_diffusion_for_recommendation_amd import _native as nat
+    rng = np.random.default_rng(5 + d)
+    R, C = 64, 500
+    degs = np.array([0, 1, 15, 16, 17, 24, 400, 3] + list(rng.integers(0, 40, R - 8)))
+    rows = np.repeat(np.arange(R), degs)
+    cols = np.concatenate([rng.choice(C, size=k, replace=False) for k in degs])
+    vals = rng.standard_normal(len(rows)).astype(np.float32)
+    inc = _build(rows, cols, vals, (R, C), dev, split_threshold=16, split_chunk=8)
+    heavy, cptr, ch = O.split_plan(np.concatenate([[0], np.cumsum(degs)]), 16, 8)
+    assert inc.csr.n_heavy == len(heavy)
+    ha, hc, chh = inc.csr._plan_arrays
+    np.testing.assert_array_equal(ha.cpu().numpy(), heavy)
+    np.testing.assert_array_equal(hc.cpu().numpy(), cptr)
+    np.testing.assert_array_equal(chh.cpu().numpy(), ch)
+    X = rng.standard_normal((C, d)).astype(np.float32)
+    scale = rng.random(R).astype(np.float32)
+    code = {None: nat.EPI_NONE, "leaky_relu": nat.EPI_LEAKY_RELU, "relu": nat.EPI_RELU}[epi]
+    Y = spmm_csr(inc.csr, torch.from_numpy(X).to(dev), val=inc.val,
+                 row_scale=torch.from_numpy(scale).to(dev), epilogue=code, slope=0.2)
+    rowptr, col, v, _ = O.csr_from_coo(rows, cols, R, vals)
+    ref = O.spmm_csr(rowptr, col, X, v, scale, epi=epi, slope=0.2)
+    mag = O.spmm_csr(rowptr, col, X, v, scale, absolute=True)
+    assert_close(Y.cpu().numpy(), ref, mag, what=f"split d={d} epi={epi}")
+
+
+def test_spmm_row_range_and_empty(dev):
+    from hypergraph_diffusion_for_recommendation_amd import spmm_csr
+    rng = np.random.default_rng(3)
+    R, C, d = 100, 40, 64
+    r, c = random_coo(rng, R, C, 600)
+    inc = _build(r, c, None, (R, C), dev)
+    X = torch.from_numpy(rng.standard_normal((C, d)).astype(np.float32)).to(dev)
+    out = torch.full((R, d), 7.0, device=dev)
+    spmm_csr(inc.csr, X, out=out, row_begin=30, row_end=55)
+    rowptr, col, _, _ = O.csr_from_coo(r, c, R)
+    ref = O.spmm_csr(rowptr, col, X.cpu().numpy())
+    mag = O.spmm_csr(rowptr, col, X.cpu().numpy(), absolute=True)
+    got = out.cpu().numpy()
+    assert (got[:30] == 7.0).all() and (got[55:] == 7.0).all()
+    assert_close(got[30:55], ref[30:55], mag[30:55], what="row range")
+    # empty structure: all-zero output, no launch problems
+    inc0 = _build(np.zeros(0, np.int64), np.zeros(0, np.int64), None, (5, 9), dev)
+    Y0 = spmm_csr(inc0.csr, torch.ones(9, 16, device=dev))
+    assert Y0.shape == (5, 16) and float(Y0.abs().sum()) == 0.0
+
+
+def test_spmm_unaligned_view(dev):
+    """A column slice (16-byte misaligned base) takes the scalar path and still matches."""
+    from hypergraph_diffusion_for_recommendation_amd import spmm_csr
+    rng = np.random.default_rng(9)
+    R, C = 50, 60
+    r, c = random_coo(rng, R, C, 700)
+    inc = _build(r, c, None, (R, C), dev)
+    big = torch.from_numpy(rng.standard_normal((C, 70)).astype(np.float32)).to(dev)
+    X = big[:, 1:65]
+    Y = spmm_csr(inc.csr, X)
+    rowptr, col, _, _ = O.csr_from_coo(r, c, R)
+    Xn = X.cpu().numpy()
+    assert_close(Y.cpu().numpy(), O.spmm_csr(rowptr, col, Xn),
+                 O.spmm_csr(rowptr, col, Xn, absolute=True), what="unaligned")
+
+
+def test_spmm_deterministic(dev):
+    from hypergraph_diffusion_for_recommendation_amd import spmm_csr
+    rng = np.random.default_rng(21)
+    R, C, d = 2000, 300, 64
+    r, c = random_coo(rng, R, C, 60000)
+    inc = _build(r, c, rng.random(len(r)).astype(np.float32), (R, C), dev, split_threshold=64,
+                 split_chunk=16)
+    X = torch.from_numpy(rng.standard_normal((C, d)).astype(np.float32)).to(dev)
+    a = spmm_csr(inc.csc, torch.randn(R, d, device=dev), val=inc.val_t)
+    Y1 = spmm_csr(inc.csr, X, val=inc.val)
+    Y2 = spmm_csr(inc.csr, X, val=inc.val)
+    assert torch.equal(Y1, Y2)
+    assert a.shape == (C, d)
+
+
+def test_spmm_rejects_bad_input(dev):
+    from hypergraph_diffusion_for_recommendation_amd import spmm_csr
+    inc = _build(np.array([0, 1]), np.array([1, 0]), None, (2, 2), dev)
+    with pytest.raises(ValueError):
+        spmm_csr(inc.csr, torch.ones(3, 4, device=dev))
+    with pytest.raises(TypeError):
+        spmm_csr(inc.csr, torch.ones(2, 4, device=dev, dtype=torch.float64))
+    with pytest.raises(RuntimeError):
+        spmm_csr(inc.csr, torch.ones(2, 4))

@@ -1,0 +1,107 @@
+"""Bit-exact parity of the structure primitives (CSR/CSC, degree scales, drop-edge, nonzero)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import hgd_oracle as O
+from tests._util import random_coo
+
+pytestmark = pytest.mark.gpu
+
+
+def _inc(rows, cols, vals, shape, dev, **kw):
+    from hypergraph_diffusion_for_recommendation_amd import Incidence
+    idx = torch.from_numpy(np.stack([rows, cols]).astype(np.int64))
+    v = None if vals is None else torch.from_numpy(np.asarray(vals, dtype=np.float32))
+    return Incidence.from_coo(idx, v, shape, device=dev, **kw)
+
+
+@pytest.mark.parametrize("sort", [True, False])
+def test_csr_csc_bit_exact(dev, sort):
+    rng = np.random.default_rng(1 + sort)
+    R, C = 1000, 700
+    r, c = random_coo(rng, R, C, 20000, sort=sort, dup=not sort)
+    vals = rng.standard_normal(len(r)).astype(np.float32)
+    inc = _inc(r, c, vals, (R, C), dev)
+    rowptr, col, v, _ = O.csr_from_coo(r, c, R, vals)
+    np.testing.assert_array_equal(inc.csr.rowptr.cpu().numpy(), rowptr)
+    np.testing.assert_array_equal(inc.csr.col.cpu().numpy(), col)
+    np.testing.assert_array_equal(inc.val.cpu().numpy().view(np.uint32), v.view(np.uint32))
+    colptr, rows_t, vt, _ = O.transpose_csr(rowptr, col, C, v)
+    np.testing.assert_array_equal(inc.csc.rowptr.cpu().numpy(), colptr)
+    np.testing.assert_array_equal(inc.csc.col.cpu().numpy(), rows_t)
+    np.testing.assert_array_equal(inc.val_t.cpu().numpy().view(np.uint32), vt.view(np.uint32))
+
+
+def test_out_of_range_indices_raise(dev):
+    with pytest.raises(ValueError):
+        _inc(np.array([0, 5]), np.array([0, 1]), None, (3, 3), dev)
+    with pytest.raises(ValueError):
+        _inc(np.array([0, 1]), np.array([0, -1]), None, (3, 3), dev)
+
+
+def test_degree_scales(dev):
+    rng = np.random.default_rng(4)
+    R, C = 300, 200
+    r, c = random_coo(rng, R, C, 3000)
+    vals = rng.random(len(r)).astype(np.float32) + 0.5
+    inc = _inc(r, c, vals, (R, C), dev)
+    deg_r = np.bincount(r, minlength=R)
+    deg_c = np.bincount(c, minlength=C)
+    for side, deg in (("row", deg_r), ("col", deg_c)):
+        for kind, p in (("mean", -1.0), ("sym", -0.5)):
+            got = inc.scale(side, kind).cpu().numpy()
+            ref = O.degree_scale(deg, p).astype(np.float32)
+            np.testing.assert_array_equal(got, ref)  # correctly rounded from float64
+    wdeg = np.zeros(R, np.float32)
+    rowptr, col, v, _ = O.csr_from_coo(r, c, R, vals)
+    for i in range(R):  # fp32 sequential row sum, as the kernel (and scipy's float32 sum)
+        s = np.float32(0)
+        for e in range(rowptr[i], rowptr[i + 1]):
+            s = np.float32(s + v[e])
+        wdeg[i] = s
+    np.testing.assert_array_equal(inc.scale("row", "wsym").cpu().numpy(),
+                                  O.degree_scale(wdeg.astype(np.float64), -0.5).astype(np.float32))
+
+
+def test_dropedge_bit_exact(dev):
+    """SpAdjDropEdge: mask from torch.rand(nnz) on CPU exactly like HCCF.py:223."""
+    from hypergraph_diffusion_for_recommendation_amd.incidence import drop_edges
+    rng = np.random.default_rng(8)
+    N = 400
+    r, c = random_coo(rng, N, N, 5000)
+    vals = rng.random(len(r)).astype(np.float32)
+    keep = 0.7
+    torch.manual_seed(123)
+    mask = ((torch.rand(len(r)) + keep).floor()).type(torch.bool)
+    idx, v = drop_edges(torch.from_numpy(np.stack([r, c])).to(dev),
+                        torch.from_numpy(vals).to(dev), mask.to(dev), keep)
+    ref_idx, ref_v = O.dropedge(np.stack([r, c]), vals, mask.numpy(), keep)
+    np.testing.assert_array_equal(idx.cpu().numpy(), ref_idx)
+    np.testing.assert_array_equal(v.cpu().numpy().view(np.uint32), ref_v.view(np.uint32))
+    # and equals the torch CPU expression of the reference itself
+    t_idx = torch.from_numpy(np.stack([r, c]))[:, mask]
+    t_v = torch.from_numpy(vals)[mask] / keep
+    assert torch.equal(idx.cpu(), t_idx) and torch.equal(v.cpu(), t_v)
+
+
+@pytest.mark.parametrize("shape", [(37, 53), (64, 64), (130, 1), (1, 300), (0, 5)])
+def test_dense_threshold_order(dev, shape):
+    from hypergraph_diffusion_for_recommendation_amd.incidence import dense_threshold
+    rng = np.random.default_rng(sum(shape))
+    H = (rng.random(shape) > 0.6).astype(np.float32) * rng.random(shape).astype(np.float32)
+    rowptr, cols = dense_threshold(torch.from_numpy(H).to(dev), 0.0)
+    V, E = O.nonzero_threshold(H, 0.0)
+    got_rows = np.repeat(np.arange(shape[0]), np.diff(rowptr.cpu().numpy()))
+    np.testing.assert_array_equal(got_rows, V)
+    np.testing.assert_array_equal(cols.cpu().numpy(), E)
+    tv = torch.nonzero(torch.from_numpy(H) > 0)
+    np.testing.assert_array_equal(tv[:, 1].numpy(), cols.cpu().numpy())
+
+
+def test_expand_rows(dev):
+    from hypergraph_diffusion_for_recommendation_amd.incidence import expand_rows
+    rng = np.random.default_rng(2)
+    r, c = random_coo(rng, 90, 80, 1500)
+    inc = _inc(r, c, None, (90, 80), dev)
+    np.testing.assert_array_equal(expand_rows(inc.csr.rowptr, inc.nnz).cpu().numpy(), r)
