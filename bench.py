@@ -257,6 +257,16 @@ def main():
         "avg_launch_ms": round(hop["avg_ms"], 4),
         "launches_timed": hop["launches"],
     }
+    # per-hop breakdown: launches cycle fwd-CSC (into items), fwd-CSR (into users), bwd-CSC, bwd-CSR
+    names = ["fwd_items", "fwd_users", "bwd_items", "bwd_users"]
+    if world == 1 and hop["launches"] % 4 == 0:
+        per = {}
+        for k, nm in enumerate(names):
+            ms = hop["per_launch_ms"][k::4]
+            by = hop["per_launch_bytes"][k::4]
+            per[nm] = {"ms": round(statistics.mean(ms), 4),
+                       "GBps": round(statistics.mean(by) / (statistics.mean(ms) * 1e-3) / 1e9, 1)}
+        roofline["per_hop"] = per
     if pmc_note:
         roofline["traffic_note"] = pmc_note
     if pmc is not None:

@@ -155,27 +155,53 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
   if (col_ok) store_vec<VEC>(a.Y + r * a.ldy + coff, acc);
 }
 
-// Sums the chunk partials of each split row in chunk order, then scale + epilogue.
+// One block per split row: each of the GPB lane groups sums the chunk partials
+// t = first + g, first + g + GPB, ... (FU independent loads in flight), then group 0 adds the
+// GPB group sums in group order. The combine order is fixed by (chunk count, GPB), so the result
+// is deterministic run to run; a popular item with ~10^4 chunks is reduced by GPB·FU loads in
+// flight instead of one serial chain.
 template <int G, int VEC>
 __global__ __launch_bounds__(kBlock) void spmm_fixup_kernel(SpmmArgs a) {
   constexpr int GPB = kBlock / G;
+  constexpr int FU = 4;
+  __shared__ float s_acc[GPB][G * VEC];
   const int g = threadIdx.x / G;
   const int l = threadIdx.x % G;
-  const int64_t h = static_cast<int64_t>(blockIdx.x) * GPB + g;
-  if (h >= a.n_heavy) return;
+  const int64_t h = blockIdx.x;
   const int64_t r = a.heavy_rows[h];
-  if (r < a.row_begin || r >= a.row_end) return;
+  if (r < a.row_begin || r >= a.row_end) return;  // block-uniform
   const int64_t coff = static_cast<int64_t>(a.col0) + static_cast<int64_t>(l) * VEC;
-  if (coff >= a.d) return;
+  const bool col_ok = coff < a.d;
   float acc[VEC];
 #pragma unroll
   for (int i = 0; i < VEC; ++i) acc[i] = 0.f;
-  for (int64_t t = a.heavy_cptr[h]; t < a.heavy_cptr[h + 1]; ++t) {
-    float v[VEC];
-    load_vec<VEC>(a.partial + t * a.d + coff, v);
+  const int64_t t0 = a.heavy_cptr[h], t1 = a.heavy_cptr[h + 1];
+  for (int64_t t = t0 + g; t < t1; t += GPB * FU) {
+    float v[FU][VEC];
 #pragma unroll
-    for (int i = 0; i < VEC; ++i) acc[i] += v[i];
+    for (int u = 0; u < FU; ++u) {
+      const int64_t tt = t + static_cast<int64_t>(u) * GPB;
+      if (tt < t1 && col_ok) {
+        load_vec<VEC>(a.partial + tt * a.d + coff, v[u]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) v[u][i] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < FU; ++u)
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) acc[i] += v[u][i];
   }
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) s_acc[g][l * VEC + i] = acc[i];
+  __syncthreads();
+  if (g != 0 || !col_ok) return;
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) acc[i] = s_acc[0][l * VEC + i];
+  for (int k = 1; k < GPB; ++k)
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) acc[i] += s_acc[k][l * VEC + i];
   const float s = a.row_scale ? a.row_scale[r] : 1.f;
 #pragma unroll
   for (int i = 0; i < VEC; ++i) acc[i] = epilogue(acc[i] * s, a.epi, a.slope);
@@ -205,8 +231,8 @@ hgd_status launch_g(SpmmArgs a, bool has_val, hipStream_t st) {
     if (s != HGD_OK) return s;
   }
   if (a.n_heavy > 0) {
-    const int64_t fblocks = (a.n_heavy + GPB - 1) / GPB;
-    hipLaunchKernelGGL((spmm_fixup_kernel<G, VEC>), dim3(fblocks), dim3(kBlock), 0, st, a);
+    if (a.n_heavy > 0x7fffffffLL) return fail(HGD_ERR_UNSUPPORTED, "hgd_spmm: too many split rows");
+    hipLaunchKernelGGL((spmm_fixup_kernel<G, VEC>), dim3(a.n_heavy), dim3(kBlock), 0, st, a);
     return check_launch("hgd_spmm fixup");
   }
   return HGD_OK;

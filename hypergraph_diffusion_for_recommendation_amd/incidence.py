@@ -93,6 +93,11 @@ class CSR:
         p.heavy_cptr = heavy_cptr.data_ptr()
         p.chunk_heavy = chunk_heavy.data_ptr()
 
+    def __deepcopy__(self, memo):
+        # immutable device structure: copies of a module share it (the ctypes plan struct
+        # holding raw device pointers cannot be pickled or duplicated meaningfully)
+        return self
+
     @property
     def n_heavy(self) -> int:
         return int(self.plan.n_heavy) if self.plan.threshold > 0 else 0
@@ -171,6 +176,9 @@ class Incidence:
     @property
     def shape(self):
         return (self.n_rows, self.n_cols)
+
+    def __deepcopy__(self, memo):
+        return self  # immutable once built (scale / edge-value caches are derived data)
 
     # -- construction ------------------------------------------------------------------
     @classmethod

@@ -71,3 +71,25 @@ def hgconv2_fwd_bwd(H: torch.Tensor, X: torch.Tensor, dY: torch.Tensor):
     Y = hgconv2(H, X)
     (dX,) = torch.autograd.grad(Y, X, dY)
     return Y.detach(), dX
+
+
+def equivset_conv(X, vertex, edges, X0, W1, W2, W, alpha, aggr="mean"):
+    """EquivSetConv.forward (layers2/EquivSetConv2.py:85-100) with torch ops on CPU; W1/W2/W are
+    callables (W2 None = the ``X[..., in_features:]`` slice of mlp2_layers = 0)."""
+    N = X.shape[-2]
+
+    def scatter(src, index, dim_size=None):
+        n = dim_size if dim_size is not None else int(index.max()) + 1
+        out = torch.zeros((n, src.shape[1]), dtype=src.dtype)
+        if aggr == "mean":
+            return out.index_reduce_(0, index, src, "mean", include_self=False)
+        return out.index_add_(0, index, src)
+
+    Xve = W1(X)[..., vertex, :]
+    Xe = scatter(Xve, edges)
+    Xev = Xe[..., edges, :]
+    cat = torch.cat([X[..., vertex, :], Xev], -1)
+    Xev = cat[..., X.shape[-1]:] if W2 is None else W2(cat)
+    Xv = scatter(Xev, vertex, dim_size=N)
+    X = (1 - alpha) * Xv + alpha * X0
+    return W(X)

@@ -1,0 +1,141 @@
+"""CPU: the oracle against its committed golden vectors, hand-derived known answers and the
+torch-CPU library calls the reference makes (oracle/ref_cpu.py)."""
+import os
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import torch
+
+from oracle import hgd_oracle as O
+from oracle import ref_cpu
+from tests._util import assert_close
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def load(name):
+    return dict(np.load(os.path.join(GOLDEN, f"{name}.npz"), allow_pickle=False))
+
+
+def test_golden_regenerates_exactly():
+    """make_golden.py is deterministic and the committed vectors are what it produces."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("mg", os.path.join(GOLDEN, "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    rng = np.random.default_rng(2024)
+    fresh = {"toy_hgconv2": mg.toy_hgconv2(), "hgcn_conv": mg.hgcn_fixture(rng),
+             "edhnn": mg.edhnn_fixture(rng), "dropedge": mg.dropedge_fixture(rng),
+             "structure": mg.structure_fixture(rng), "hgconv2": mg.hgconv2_fixture(),
+             "hccf": mg.hccf_fixture(rng)}
+    for name, arrs in fresh.items():
+        gold = load(name)
+        assert set(gold) == set(arrs), name
+        for k, v in arrs.items():
+            np.testing.assert_array_equal(np.asarray(v), gold[k], err_msg=f"{name}.{k}")
+
+
+def test_toy_known_answer():
+    g = load("toy_hgconv2")
+    s = 1.0 / (2.0 * np.sqrt(2.0))
+    T = np.array([[0.5, s, 0.0], [s, 0.5, s], [0.0, s, 0.5]])
+    np.testing.assert_allclose(g["Y"], T @ g["X"].astype(np.float64), rtol=0, atol=1e-15)
+
+
+def test_normalize_graph_mat_known_answer():
+    """2 users, 1 item, both connected: degrees (1,1,2) → entries 1/√2 (data/graph.py:11-25)."""
+    A = O.bipartite_adjacency([0, 1], [0, 0], 2, 1)
+    N = O.normalize_graph_mat(A).toarray()
+    r = np.float32(1.0) / np.sqrt(np.float32(2.0))
+    exp = np.array([[0, 0, r], [0, 0, r], [r, r, 0]], dtype=np.float32)
+    np.testing.assert_allclose(N, exp, rtol=1e-7)
+    assert N.dtype == np.float32
+    # empty node: inf → 0
+    A2 = sp.csr_matrix(np.array([[0, 1, 0], [1, 0, 0], [0, 0, 0]], dtype=np.float32))
+    assert np.isfinite(O.normalize_graph_mat(A2).toarray()).all()
+
+
+def test_duplicates_summed_in_bipartite_adjacency():
+    A = O.bipartite_adjacency([0, 0, 1], [0, 0, 1], 2, 2).toarray()
+    assert A[0, 2] == 2.0 and A[2, 0] == 2.0 and A[1, 3] == 1.0
+
+
+def test_mean_pair_row_stochastic():
+    """Means of a constant signal are that constant on every non-isolated vertex."""
+    g = load("edhnn")
+    X = np.ones((int(g["N"]), 3))
+    Y = O.equivset_mean_2hop(X, g["V"], g["E"], int(g["N"]))
+    has = np.bincount(g["V"], minlength=int(g["N"])) > 0
+    np.testing.assert_allclose(Y[has], 1.0, rtol=1e-14)
+    assert (Y[~has] == 0).all()
+
+
+def test_hgconv2_adjoint():
+    g = load("hgconv2")
+    rng = np.random.default_rng(0)
+    X2 = rng.standard_normal(g["X"].shape)
+    a = np.sum(g["Y"] * X2)
+    b = np.sum(g["X"] * O.two_hop(g["rows"], g["cols"], None, tuple(g["shape"]), X2, "sym",
+                                   "mean", "sym"))
+    assert abs(a - b) < 1e-9 * (abs(a) + abs(b))
+
+
+def test_oracle_vs_torch_sparse_mm():
+    g = load("hgcn_conv")
+    idx, vals = g["indices"], g["values"]
+    N = int(g["n_users"] + g["n_items"])
+    adj = ref_cpu.coo_tensor(idx[0], idx[1], vals, (N, N))
+    Xt = torch.from_numpy(g["X"]).requires_grad_(True)
+    Yt = ref_cpu.hgcn_conv(adj, Xt, act=True, slope=0.5)
+    (dXt,) = torch.autograd.grad(Yt, Xt, torch.from_numpy(g["dY"]))
+    mag = O.two_hop(idx[0], idx[1], np.abs(vals), (N, N), np.abs(g["X"]))
+    assert_close(Yt.detach().numpy(), g["Y"], mag, what="HGCNConv fwd")
+    dmag = O.two_hop(idx[0], idx[1], np.abs(vals), (N, N), np.abs(g["dY"]))
+    assert_close(dXt.numpy(), g["dX"], dmag, what="HGCNConv bwd")
+
+
+def test_scatter_mean_semantics():
+    src = np.array([[1.0], [2.0], [4.0]])
+    idx = np.array([0, 0, 2])
+    out = O.scatter_mean(src, idx)
+    np.testing.assert_array_equal(out, [[1.5], [0.0], [4.0]])
+    out = O.scatter_mean(src, idx, dim_size=5)
+    assert out.shape == (5, 1)
+    t = ref_cpu.scatter_mean(torch.tensor(src, dtype=torch.float32), torch.tensor(idx))
+    np.testing.assert_allclose(t.numpy(), [[1.5], [0.0], [4.0]])
+
+
+def test_structure_fixture_consistency():
+    g = load("structure")
+    # CSR reproduces the COO as a multiset per row, in input order
+    for r in range(len(g["rowptr"]) - 1):
+        sel = np.nonzero(g["rows"] == r)[0]
+        np.testing.assert_array_equal(g["col"][g["rowptr"][r]:g["rowptr"][r + 1]], g["cols"][sel])
+    # CSC rows ascending inside every column
+    for c in range(len(g["colptr"]) - 1):
+        seg = g["rows_t"][g["colptr"][c]:g["colptr"][c + 1]]
+        assert np.all(np.diff(seg) >= 0)
+
+
+def test_dropedge_fixture_matches_reference_expression():
+    g = load("dropedge")
+    t_idx = torch.from_numpy(g["indices"])[:, torch.from_numpy(g["mask"])]
+    t_val = torch.from_numpy(g["values"])[torch.from_numpy(g["mask"])] / float(g["keep"])
+    np.testing.assert_array_equal(t_idx.numpy(), g["new_indices"])
+    np.testing.assert_array_equal(t_val.numpy().view(np.uint32), g["new_values"].view(np.uint32))
+
+
+def test_nonzero_order_matches_torch():
+    g = load("edhnn")
+    nz = torch.nonzero(torch.from_numpy(g["dense"]) > 0)
+    np.testing.assert_array_equal(nz[:, 0].numpy(), g["V"])
+    np.testing.assert_array_equal(nz[:, 1].numpy(), g["E"])
+
+
+@pytest.mark.parametrize("zipf", [None, 1.0])
+def test_synthetic_generator_dedup_sorted(zipf):
+    r, c = O.synthetic_incidence(1000, 200, 20000, seed=0, zipf=zipf)
+    key = r * 200 + c
+    assert np.all(np.diff(key) > 0)
+    assert r.max() < 1000 and c.max() < 200

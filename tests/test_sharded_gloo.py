@@ -1,0 +1,115 @@
+"""CPU, world_size 2 over gloo: the user-row sharded 2-hop conv (sharded.py) — global item-degree
+all-reduce, chunked async all-reduce of item partial sums, local second hop — reproduces the
+unsharded operator. The per-shard hop itself is replaced by a CPU stand-in built on the oracle
+(only this test does that; the product path has no CPU hop)."""
+import os
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import hgd_oracle as O
+
+U_PER, I, NNZ_PER, D = 60, 25, 500, 8
+
+
+class _CPUCsr:
+    def __init__(self, rowptr, col, n_rows, n_cols):
+        self.rowptr = torch.from_numpy(rowptr)
+        self.col = torch.from_numpy(col.astype(np.int32))
+        self.n_rows, self.n_cols, self.nnz = n_rows, n_cols, len(col)
+
+
+class _CPUIncidence:
+    """Interface-compatible stand-in for Incidence (scale / edge_values / csr / csc)."""
+
+    def __init__(self, rows, cols, n_rows, n_cols):
+        rowptr, col, _, _ = O.csr_from_coo(rows, cols, n_rows)
+        colptr, rows_t, _, _ = O.transpose_csr(rowptr, col, n_cols)
+        self.csr = _CPUCsr(rowptr, col, n_rows, n_cols)
+        self.csc = _CPUCsr(colptr, rows_t, n_cols, n_rows)
+        self.n_rows, self.n_cols, self.val = n_rows, n_cols, None
+
+    def scale(self, side, kind):
+        if kind is None:
+            return None
+        o = self.csr if side == "row" else self.csc
+        deg = (o.rowptr[1:] - o.rowptr[:-1]).numpy()
+        return torch.from_numpy(O.degree_scale(deg, {"mean": -1.0, "sym": -0.5}[kind])).float()
+
+    def edge_values(self, orient, kind):
+        s = self.scale("col" if orient == "csr" else "row", kind)
+        if s is None:
+            return None
+        o = self.csr if orient == "csr" else self.csc
+        return s[o.col.long()]
+
+
+def _cpu_spmm(csr, X, val=None, row_scale=None, epilogue=0, slope=0.0, out=None, row_begin=0,
+              row_end=None):
+    row_end = csr.n_rows if row_end is None else row_end
+    Y = O.spmm_csr(csr.rowptr.numpy(), csr.col.numpy(), X.detach().numpy(),
+                   None if val is None else val.numpy(),
+                   None if row_scale is None else row_scale.numpy())
+    if out is None:
+        out = torch.zeros(csr.n_rows, X.shape[1])
+    out[row_begin:row_end] = torch.from_numpy(Y[row_begin:row_end]).float()
+    return out
+
+
+def _graph(rank):
+    rows, cols = O.synthetic_incidence(U_PER, I, NNZ_PER, seed=100 + rank)
+    return rows, cols
+
+
+def _worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from hypergraph_diffusion_for_recommendation_amd import sharded
+    sharded.spmm_csr = _cpu_spmm  # CPU stand-in for the HIP hop (test only)
+    rows, cols = _graph(rank)
+    sh = sharded.ShardedIncidence(_CPUIncidence(rows, cols, U_PER, I), n_chunks=3)
+    rng = np.random.default_rng(rank)
+    X = torch.from_numpy(rng.standard_normal((U_PER, D)).astype(np.float32))
+    dY = torch.from_numpy(rng.standard_normal((U_PER, D)).astype(np.float32))
+    X.requires_grad_(True)
+    Y = sharded.sharded_two_hop(sh, X)
+    (dX,) = torch.autograd.grad(Y, X, dY)
+    np.savez(os.path.join(outdir, f"r{rank}.npz"), X=X.detach().numpy(), dY=dY.numpy(),
+             Y=Y.detach().numpy(), dX=dX.numpy(), n_chunks=len(sh.bounds))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world", [2])
+def test_sharded_two_hop_matches_global(world):
+    with tempfile.TemporaryDirectory() as td:
+        mp.start_processes(_worker, args=(world, _free_port(), td), nprocs=world, join=True,
+                           start_method="spawn")
+        parts = [np.load(os.path.join(td, f"r{r}.npz")) for r in range(world)]
+    assert all(int(p["n_chunks"]) == 3 for p in parts)
+    rows = np.concatenate([_graph(r)[0] + r * U_PER for r in range(world)])
+    cols = np.concatenate([_graph(r)[1] for r in range(world)])
+    shape = (world * U_PER, I)
+    X = np.concatenate([p["X"] for p in parts])
+    dY = np.concatenate([p["dY"] for p in parts])
+    Y = O.two_hop(rows, cols, None, shape, X, "sym", "mean", "sym")
+    dX = O.two_hop_backward(rows, cols, None, shape, Y, dY, "sym", "mean", "sym")
+    got_Y = np.concatenate([p["Y"] for p in parts])
+    got_dX = np.concatenate([p["dX"] for p in parts])
+    mag = O.two_hop(rows, cols, None, shape, np.abs(X), "sym", "mean", "sym")
+    dmag = O.two_hop(rows, cols, None, shape, np.abs(dY), "sym", "mean", "sym")
+    assert np.all(np.abs(got_Y - Y) <= 1e-5 * mag + 1e-12)
+    assert np.all(np.abs(got_dX - dX) <= 1e-5 * dmag + 1e-12)
