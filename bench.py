@@ -185,10 +185,16 @@ def main():
     from hypergraph_diffusion_for_recommendation_amd.sharded import (ShardedIncidence,
                                                                        sharded_two_hop)
 
+    # one rank per GPU; the modulo only matters for rehearsing N ranks on fewer GPUs (gloo)
+    dev_index = local_rank % max(1, torch.cuda.device_count())
+    device = torch.device(f"cuda:{dev_index}")
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
-    device = torch.device(f"cuda:{local_rank}")
+        torch.cuda.set_device(device)
+        backend = os.environ.get("HGD_DIST_BACKEND", "nccl")  # nccl == RCCL on ROCm
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
 
     idx = make_graph(U, I, E, seed=rank, zipf=zipf, device=device)
     nnz = int(idx.shape[1])

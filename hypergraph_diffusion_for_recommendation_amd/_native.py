@@ -48,6 +48,7 @@ class SplitPlan(ctypes.Structure):
 # name -> (restype, argtypes); every symbol of include/hgd.h appears here.
 _SIGNATURES = {
     "hgd_version": (c_i32, []),
+    "hgd_set_tuning": (c_i32, [c_i32, c_i32]),
     "hgd_get_last_error_string": (ctypes.c_char_p, []),
     "hgd_split_plan_count": (c_i32, [c_void_p, c_i64, c_i64, c_i32, c_void_p, c_void_p]),
     "hgd_split_plan_workspace_size": (c_size, [c_i64]),
@@ -104,6 +105,13 @@ def load() -> ctypes.CDLL:
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        # optional process-wide tuning overrides (hgd_set_tuning keys 1 / 2)
+        for key, env in ((1, "HGD_SPMM_UNROLL"), (2, "HGD_SPMM_POLICY")):
+            if os.environ.get(env):
+                st = lib.hgd_set_tuning(key, int(os.environ[env]))
+                if st != HGD_OK:
+                    raise HGDNativeError(f"{env}={os.environ[env]}: "
+                                         f"{lib.hgd_get_last_error_string().decode()}")
         _lib = lib
     return _lib
 

@@ -51,10 +51,21 @@ __device__ __forceinline__ float epilogue(float y, int epi, float slope) {
   return y;
 }
 
-template <int VEC>
+// Cache-policy bits of the tuned variants (hgd_set_tuning(HGD_TUNE_SPMM_POLICY, bits)):
+constexpr int kPolNtStore = 1;   // Y rows: non-temporal stores (written once, never re-read here)
+constexpr int kPolNtIndex = 2;   // col / val streams: non-temporal loads (read exactly once)
+constexpr int kPolNtGather = 4;  // gathered X rows: non-temporal loads
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int VEC, bool NT = false>
 __device__ __forceinline__ void load_vec(const float* p, float (&v)[VEC]) {
   if constexpr (VEC == 4) {
-    const float4 t = *reinterpret_cast<const float4*>(p);
+    f32x4 t;
+    if constexpr (NT)
+      t = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+    else
+      t = *reinterpret_cast<const f32x4*>(p);
     v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
   } else {
 #pragma unroll
@@ -62,10 +73,14 @@ __device__ __forceinline__ void load_vec(const float* p, float (&v)[VEC]) {
   }
 }
 
-template <int VEC>
+template <int VEC, bool NT = false>
 __device__ __forceinline__ void store_vec(float* p, const float (&v)[VEC]) {
   if constexpr (VEC == 4) {
-    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    const f32x4 t = {v[0], v[1], v[2], v[3]};
+    if constexpr (NT)
+      __builtin_nontemporal_store(t, reinterpret_cast<f32x4*>(p));
+    else
+      *reinterpret_cast<f32x4*>(p) = t;
   } else {
 #pragma unroll
     for (int i = 0; i < VEC; ++i) p[i] = v[i];
@@ -73,7 +88,7 @@ __device__ __forceinline__ void store_vec(float* p, const float (&v)[VEC]) {
 }
 
 // Σ_{e in [e0,e1)} val[e] * X[col[e], cols of this lane], in edge order.
-template <int G, int VEC, int U, bool HAS_VAL>
+template <int G, int VEC, int U, bool HAS_VAL, int POL>
 __device__ __forceinline__ void gather_sum(const SpmmArgs& a, int64_t e0, int64_t e1, int l,
                                            bool col_ok, float (&acc)[VEC]) {
 #pragma unroll
@@ -84,8 +99,13 @@ __device__ __forceinline__ void gather_sum(const SpmmArgs& a, int64_t e0, int64_
     int myc = 0;
     float myw = 1.f;
     if (l < n) {
-      myc = a.col[eb + l];
-      if constexpr (HAS_VAL) myw = a.val[eb + l];
+      if constexpr (POL & kPolNtIndex) {
+        myc = __builtin_nontemporal_load(a.col + eb + l);
+        if constexpr (HAS_VAL) myw = __builtin_nontemporal_load(a.val + eb + l);
+      } else {
+        myc = a.col[eb + l];
+        if constexpr (HAS_VAL) myw = a.val[eb + l];
+      }
     }
     for (int k = 0; k < n; k += U) {
       float xv[U][VEC];
@@ -96,7 +116,8 @@ __device__ __forceinline__ void gather_sum(const SpmmArgs& a, int64_t e0, int64_
         const int c = (G == 1) ? myc : __shfl(myc, kk, G);
         if constexpr (HAS_VAL) w[u] = (G == 1) ? myw : __shfl(myw, kk, G);
         if (kk < n && col_ok) {
-          load_vec<VEC>(a.X + static_cast<int64_t>(c) * a.ldx + coff, xv[u]);
+          load_vec<VEC, (POL & kPolNtGather) != 0>(a.X + static_cast<int64_t>(c) * a.ldx + coff,
+                                                   xv[u]);
         } else {
 #pragma unroll
           for (int i = 0; i < VEC; ++i) xv[u][i] = 0.f;
@@ -118,7 +139,7 @@ __device__ __forceinline__ void gather_sum(const SpmmArgs& a, int64_t e0, int64_
   }
 }
 
-template <int G, int VEC, int U, bool HAS_VAL>
+template <int G, int VEC, int U, bool HAS_VAL, int POL>
 __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
   constexpr int GPB = kBlock / G;
   const int g = threadIdx.x / G;
@@ -137,7 +158,7 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
     const int64_t re = a.rowptr[r + 1];
     const int64_t e0 = a.rowptr[r] + k * a.chunk;
     const int64_t e1 = min(e0 + static_cast<int64_t>(a.chunk), re);
-    gather_sum<G, VEC, U, HAS_VAL>(a, e0, e1, l, col_ok, acc);
+    gather_sum<G, VEC, U, HAS_VAL, POL>(a, e0, e1, l, col_ok, acc);
     if (col_ok) store_vec<VEC>(a.partial + t * a.d + coff, acc);
     return;
   }
@@ -148,11 +169,11 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
   const int64_t e0 = a.rowptr[r];
   const int64_t e1 = a.rowptr[r + 1];
   if (a.heavy_threshold > 0 && e1 - e0 > a.heavy_threshold) return;  // split-plan row
-  gather_sum<G, VEC, U, HAS_VAL>(a, e0, e1, l, col_ok, acc);
+  gather_sum<G, VEC, U, HAS_VAL, POL>(a, e0, e1, l, col_ok, acc);
   const float s = a.row_scale ? a.row_scale[r] : 1.f;
 #pragma unroll
   for (int i = 0; i < VEC; ++i) acc[i] = epilogue(acc[i] * s, a.epi, a.slope);
-  if (col_ok) store_vec<VEC>(a.Y + r * a.ldy + coff, acc);
+  if (col_ok) store_vec<VEC, (POL & kPolNtStore) != 0>(a.Y + r * a.ldy + coff, acc);
 }
 
 // One block per split row: each of the GPB lane groups sums the chunk partials
@@ -210,7 +231,41 @@ __global__ __launch_bounds__(kBlock) void spmm_fixup_kernel(SpmmArgs a) {
 
 namespace {
 
-constexpr int kUnroll = 8;
+// Tuning knobs (hgd_set_tuning); defaults are the measured best on MI355X.
+int g_unroll = 8;
+int g_policy = 0;
+
+template <int G, int VEC, int U, int POL>
+void launch_main(const SpmmArgs& a, bool has_val, int64_t blocks, hipStream_t st) {
+  if (has_val)
+    hipLaunchKernelGGL((spmm_kernel<G, VEC, U, true, POL>), dim3(blocks), dim3(kBlock), 0, st, a);
+  else
+    hipLaunchKernelGGL((spmm_kernel<G, VEC, U, false, POL>), dim3(blocks), dim3(kBlock), 0, st, a);
+}
+
+template <int G, int VEC>
+void launch_tuned(const SpmmArgs& a, bool has_val, int64_t blocks, hipStream_t st) {
+  if constexpr (G == 16 && VEC == 4) {
+    // the d = 64 path carries the full tuning matrix (unroll × cache policy)
+#define HGD_POL_CASES(U)                                                       \
+    switch (g_policy & 7) {                                                    \
+      case 0: return launch_main<G, VEC, U, 0>(a, has_val, blocks, st);        \
+      case 1: return launch_main<G, VEC, U, 1>(a, has_val, blocks, st);        \
+      case 2: return launch_main<G, VEC, U, 2>(a, has_val, blocks, st);        \
+      case 3: return launch_main<G, VEC, U, 3>(a, has_val, blocks, st);        \
+      case 4: return launch_main<G, VEC, U, 4>(a, has_val, blocks, st);        \
+      case 5: return launch_main<G, VEC, U, 5>(a, has_val, blocks, st);        \
+      case 6: return launch_main<G, VEC, U, 6>(a, has_val, blocks, st);        \
+      default: return launch_main<G, VEC, U, 7>(a, has_val, blocks, st);      \
+    }
+    if (g_unroll <= 4) { HGD_POL_CASES(4) }
+    if (g_unroll >= 16) { HGD_POL_CASES(16) }
+    HGD_POL_CASES(8)
+#undef HGD_POL_CASES
+  } else {
+    launch_main<G, VEC, 8, 0>(a, has_val, blocks, st);
+  }
+}
 
 template <int G, int VEC>
 hgd_status launch_g(SpmmArgs a, bool has_val, hipStream_t st) {
@@ -221,12 +276,7 @@ hgd_status launch_g(SpmmArgs a, bool has_val, hipStream_t st) {
   const int64_t blocks = light_blocks + a.heavy_blocks;
   if (blocks > 0) {
     if (blocks > 0x7fffffffLL) return fail(HGD_ERR_UNSUPPORTED, "hgd_spmm: grid too large");
-    if (has_val)
-      hipLaunchKernelGGL((spmm_kernel<G, VEC, kUnroll, true>), dim3(blocks), dim3(kBlock), 0,
-                         st, a);
-    else
-      hipLaunchKernelGGL((spmm_kernel<G, VEC, kUnroll, false>), dim3(blocks), dim3(kBlock), 0,
-                         st, a);
+    launch_tuned<G, VEC>(a, has_val, blocks, st);
     hgd_status s = check_launch("hgd_spmm kernel");
     if (s != HGD_OK) return s;
   }
@@ -341,4 +391,21 @@ extern "C" hgd_status hgd_spmm(const int64_t* rowptr, const int32_t* col, const 
     }
   }
   return HGD_OK;
+}
+
+extern "C" hgd_status hgd_set_tuning(int32_t key, int32_t value) {
+  using namespace hgd;
+  clear_error();
+  switch (key) {
+    case HGD_TUNE_SPMM_UNROLL:
+      HGD_REQUIRE(value == 4 || value == 8 || value == 16, "hgd_set_tuning: unroll must be 4/8/16");
+      g_unroll = value;
+      return HGD_OK;
+    case HGD_TUNE_SPMM_POLICY:
+      HGD_REQUIRE(value >= 0 && value <= 7, "hgd_set_tuning: policy bits 0..7");
+      g_policy = value;
+      return HGD_OK;
+    default:
+      return fail(HGD_ERR_INVALID_ARG, "hgd_set_tuning: unknown key %d", key);
+  }
 }

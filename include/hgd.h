@@ -56,6 +56,13 @@ typedef enum hgd_epilogue {
   HGD_EPI_RELU = 2
 } hgd_epilogue;
 
+/* Tuning knobs of the SpMM hop (process-wide; defaults are the measured best on MI355X).
+ *   HGD_TUNE_SPMM_UNROLL: independent row gathers in flight per lane (4, 8 or 16)
+ *   HGD_TUNE_SPMM_POLICY: cache-policy bits, 1 = non-temporal Y stores,
+ *                         2 = non-temporal index/weight loads, 4 = non-temporal row gathers */
+typedef enum hgd_tune_key { HGD_TUNE_SPMM_UNROLL = 1, HGD_TUNE_SPMM_POLICY = 2 } hgd_tune_key;
+hgd_status hgd_set_tuning(int32_t key, int32_t value);
+
 /* Library ABI version (major*10000 + minor*100 + patch). */
 int hgd_version(void);
 /* Human-readable description of the last error on this thread ("" if none). */
