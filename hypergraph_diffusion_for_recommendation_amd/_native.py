@@ -36,7 +36,7 @@ class SplitPlan(ctypes.Structure):
     _fields_ = [
         ("threshold", c_i64),
         ("chunk", c_i32),
-        ("_pad", c_i32),
+        ("flags", c_i32),
         ("n_heavy", c_i64),
         ("n_chunks", c_i64),
         ("heavy_rows", c_void_p),

@@ -37,7 +37,7 @@ struct SpmmArgs {
   int64_t n_chunks;
   int64_t n_heavy;
   int32_t chunk;
-  int32_t _pad;
+  int32_t seg;  // 1: segmented short-row kernel (plan flag HGD_PLAN_SEGMENTED)
   const int32_t* chunk_heavy;
   const int32_t* heavy_rows;
   const int64_t* heavy_cptr;
@@ -55,6 +55,7 @@ __device__ __forceinline__ float epilogue(float y, int epi, float slope) {
 constexpr int kPolNtStore = 1;   // Y rows: non-temporal stores (written once, never re-read here)
 constexpr int kPolNtIndex = 2;   // col / val streams: non-temporal loads (read exactly once)
 constexpr int kPolNtGather = 4;  // gathered X rows: non-temporal loads
+constexpr int kPolPrefetch = 8;  // software-pipelined index batches (see gather_sum)
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -87,25 +88,53 @@ __device__ __forceinline__ void store_vec(float* p, const float (&v)[VEC]) {
   }
 }
 
-// Σ_{e in [e0,e1)} val[e] * X[col[e], cols of this lane], in edge order.
+// Lane l's share of a batch of G column indices (and weights) starting at nonzero eb.
+template <bool HAS_VAL, int POL>
+__device__ __forceinline__ void load_index(const SpmmArgs& a, int64_t eb, int n, int l, int& c,
+                                           float& w) {
+  c = 0;
+  w = 1.f;
+  if (l < n) {
+    if constexpr (POL & kPolNtIndex) {
+      c = __builtin_nontemporal_load(a.col + eb + l);
+      if constexpr (HAS_VAL) w = __builtin_nontemporal_load(a.val + eb + l);
+    } else {
+      c = a.col[eb + l];
+      if constexpr (HAS_VAL) w = a.val[eb + l];
+    }
+  }
+}
+
+// Σ_{e in [e0,e1)} val[e] * X[col[e], cols of this lane], in edge order. With kPolPrefetch the
+// index batch b+1 is loaded before the gathers of batch b are issued, so the dependent
+// index → gather round trip is paid once per row instead of once per batch of G nonzeros.
 template <int G, int VEC, int U, bool HAS_VAL, int POL>
 __device__ __forceinline__ void gather_sum(const SpmmArgs& a, int64_t e0, int64_t e1, int l,
                                            bool col_ok, float (&acc)[VEC]) {
 #pragma unroll
   for (int i = 0; i < VEC; ++i) acc[i] = 0.f;
   const int64_t coff = static_cast<int64_t>(a.col0) + static_cast<int64_t>(l) * VEC;
+  constexpr bool PF = (POL & kPolPrefetch) != 0;
+  int nxc = 0;
+  float nxw = 1.f;
+  if constexpr (PF) {
+    if (e0 < e1)
+      load_index<HAS_VAL, POL>(a, e0, static_cast<int>(min(static_cast<int64_t>(G), e1 - e0)), l,
+                               nxc, nxw);
+  }
   for (int64_t eb = e0; eb < e1; eb += G) {
     const int n = static_cast<int>(min(static_cast<int64_t>(G), e1 - eb));
-    int myc = 0;
-    float myw = 1.f;
-    if (l < n) {
-      if constexpr (POL & kPolNtIndex) {
-        myc = __builtin_nontemporal_load(a.col + eb + l);
-        if constexpr (HAS_VAL) myw = __builtin_nontemporal_load(a.val + eb + l);
-      } else {
-        myc = a.col[eb + l];
-        if constexpr (HAS_VAL) myw = a.val[eb + l];
-      }
+    int myc;
+    float myw;
+    if constexpr (PF) {
+      myc = nxc;
+      myw = nxw;
+      const int64_t en = eb + G;
+      if (en < e1)
+        load_index<HAS_VAL, POL>(a, en, static_cast<int>(min(static_cast<int64_t>(G), e1 - en)),
+                                 l, nxc, nxw);
+    } else {
+      load_index<HAS_VAL, POL>(a, eb, n, l, myc, myw);
     }
     for (int k = 0; k < n; k += U) {
       float xv[U][VEC];
@@ -176,6 +205,107 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
   if (col_ok) store_vec<VEC, (POL & kPolNtStore) != 0>(a.Y + r * a.ldy + coff, acc);
 }
 
+// Segmented variant for short rows (hgd_split_plan.flags & HGD_PLAN_SEGMENTED): a group owns
+// G consecutive rows and walks their nonzeros as ONE flat stream [rowptr[r0], rowptr[r0+G]) in
+// batches of G indices, so every gather batch is full whatever the row lengths, the row pointers
+// and row scales of all G rows arrive in one coalesced load, and the accumulator is flushed
+// (scale, epilogue, store) at each row boundary. Sums stay in edge order per row.
+template <int G, int VEC, int U, bool HAS_VAL, int POL>
+__global__ __launch_bounds__(kBlock) void spmm_seg_kernel(SpmmArgs a) {
+  constexpr int GPB = kBlock / G;
+  const int g = threadIdx.x / G;
+  const int l = threadIdx.x % G;
+  const int64_t r0 = a.row_begin + (static_cast<int64_t>(blockIdx.x) * GPB + g) * G;
+  if (r0 >= a.row_end) return;
+  const int nr = static_cast<int>(min(static_cast<int64_t>(G), a.row_end - r0));
+  int64_t my_end = 0;  // lane j: end of local row j
+  float my_s = 1.f;    // lane j: scale of local row j
+  if (l < nr) {
+    my_end = a.rowptr[r0 + l + 1];
+    if (a.row_scale) my_s = a.row_scale[r0 + l];
+  }
+  const int64_t e_begin = a.rowptr[r0];
+  const int64_t e_end = __shfl(my_end, nr - 1, G);
+  const int64_t coff = static_cast<int64_t>(a.col0) + static_cast<int64_t>(l) * VEC;
+  const bool col_ok = coff < a.d;
+  float acc[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) acc[i] = 0.f;
+  int cur = 0;
+  int64_t next_b = __shfl(my_end, 0, G);
+
+  auto flush = [&]() {
+    const float s = __shfl(my_s, cur, G);
+    float y[VEC];
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      y[i] = epilogue(acc[i] * s, a.epi, a.slope);
+      acc[i] = 0.f;
+    }
+    if (col_ok) store_vec<VEC, (POL & kPolNtStore) != 0>(a.Y + (r0 + cur) * a.ldy + coff, y);
+    ++cur;
+    const int64_t nb = __shfl(my_end, cur < nr ? cur : 0, G);
+    next_b = cur < nr ? nb : INT64_MAX;
+  };
+
+  constexpr bool PF = (POL & kPolPrefetch) != 0;
+  int nxc = 0;
+  float nxw = 1.f;
+  if constexpr (PF) {
+    if (e_begin < e_end)
+      load_index<HAS_VAL, POL>(
+          a, e_begin, static_cast<int>(min(static_cast<int64_t>(G), e_end - e_begin)), l, nxc,
+          nxw);
+  }
+  for (int64_t eb = e_begin; eb < e_end; eb += G) {
+    const int n = static_cast<int>(min(static_cast<int64_t>(G), e_end - eb));
+    int myc;
+    float myw;
+    if constexpr (PF) {
+      myc = nxc;
+      myw = nxw;
+      const int64_t en = eb + G;
+      if (en < e_end)
+        load_index<HAS_VAL, POL>(
+            a, en, static_cast<int>(min(static_cast<int64_t>(G), e_end - en)), l, nxc, nxw);
+    } else {
+      load_index<HAS_VAL, POL>(a, eb, n, l, myc, myw);
+    }
+    for (int k = 0; k < n; k += U) {
+      float xv[U][VEC];
+      float w[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int kk = k + u;
+        const int c = __shfl(myc, kk, G);
+        if constexpr (HAS_VAL) w[u] = __shfl(myw, kk, G);
+        if (kk < n && col_ok) {
+          load_vec<VEC, (POL & kPolNtGather) != 0>(a.X + static_cast<int64_t>(c) * a.ldx + coff,
+                                                   xv[u]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < VEC; ++i) xv[u][i] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (k + u < n) {
+          const int64_t e = eb + k + u;
+          while (e >= next_b) flush();  // group-uniform; also emits empty rows
+#pragma unroll
+          for (int i = 0; i < VEC; ++i) {
+            if constexpr (HAS_VAL)
+              acc[i] = fmaf(w[u], xv[u][i], acc[i]);
+            else
+              acc[i] += xv[u][i];
+          }
+        }
+      }
+    }
+  }
+  while (cur < nr) flush();
+}
+
 // One block per split row: each of the GPB lane groups sums the chunk partials
 // t = first + g, first + g + GPB, ... (FU independent loads in flight), then group 0 adds the
 // GPB group sums in group order. The combine order is fixed by (chunk count, GPB), so the result
@@ -232,11 +362,23 @@ __global__ __launch_bounds__(kBlock) void spmm_fixup_kernel(SpmmArgs a) {
 namespace {
 
 // Tuning knobs (hgd_set_tuning); defaults are the measured best on MI355X.
+constexpr int kDefaultPolicy = kPolPrefetch;
 int g_unroll = 8;
-int g_policy = 0;
+int g_policy = kDefaultPolicy;
 
 template <int G, int VEC, int U, int POL>
-void launch_main(const SpmmArgs& a, bool has_val, int64_t blocks, hipStream_t st) {
+void launch_kernel(const SpmmArgs& a, bool has_val, bool seg, int64_t blocks, hipStream_t st) {
+  if constexpr (G >= 8) {
+    if (seg) {
+      if (has_val)
+        hipLaunchKernelGGL((spmm_seg_kernel<G, VEC, U, true, POL>), dim3(blocks), dim3(kBlock),
+                           0, st, a);
+      else
+        hipLaunchKernelGGL((spmm_seg_kernel<G, VEC, U, false, POL>), dim3(blocks), dim3(kBlock),
+                           0, st, a);
+      return;
+    }
+  }
   if (has_val)
     hipLaunchKernelGGL((spmm_kernel<G, VEC, U, true, POL>), dim3(blocks), dim3(kBlock), 0, st, a);
   else
@@ -244,26 +386,21 @@ void launch_main(const SpmmArgs& a, bool has_val, int64_t blocks, hipStream_t st
 }
 
 template <int G, int VEC>
-void launch_tuned(const SpmmArgs& a, bool has_val, int64_t blocks, hipStream_t st) {
+void launch_tuned(const SpmmArgs& a, bool has_val, bool seg, int64_t blocks, hipStream_t st) {
   if constexpr (G == 16 && VEC == 4) {
-    // the d = 64 path carries the full tuning matrix (unroll × cache policy)
-#define HGD_POL_CASES(U)                                                       \
-    switch (g_policy & 7) {                                                    \
-      case 0: return launch_main<G, VEC, U, 0>(a, has_val, blocks, st);        \
-      case 1: return launch_main<G, VEC, U, 1>(a, has_val, blocks, st);        \
-      case 2: return launch_main<G, VEC, U, 2>(a, has_val, blocks, st);        \
-      case 3: return launch_main<G, VEC, U, 3>(a, has_val, blocks, st);        \
-      case 4: return launch_main<G, VEC, U, 4>(a, has_val, blocks, st);        \
-      case 5: return launch_main<G, VEC, U, 5>(a, has_val, blocks, st);        \
-      case 6: return launch_main<G, VEC, U, 6>(a, has_val, blocks, st);        \
-      default: return launch_main<G, VEC, U, 7>(a, has_val, blocks, st);      \
+    // the d = 64 path carries the tuning matrix (unroll × {plain, nt-store, prefetch, both})
+#define HGD_POL_CASES(U)                                                            \
+    switch (g_policy) {                                                             \
+      case 0: return launch_kernel<G, VEC, U, 0>(a, has_val, seg, blocks, st);      \
+      case 1: return launch_kernel<G, VEC, U, 1>(a, has_val, seg, blocks, st);      \
+      case 9: return launch_kernel<G, VEC, U, 9>(a, has_val, seg, blocks, st);      \
+      default: return launch_kernel<G, VEC, U, 8>(a, has_val, seg, blocks, st);     \
     }
-    if (g_unroll <= 4) { HGD_POL_CASES(4) }
     if (g_unroll >= 16) { HGD_POL_CASES(16) }
     HGD_POL_CASES(8)
 #undef HGD_POL_CASES
   } else {
-    launch_main<G, VEC, 8, 0>(a, has_val, blocks, st);
+    launch_kernel<G, VEC, 8, kDefaultPolicy>(a, has_val, seg, blocks, st);
   }
 }
 
@@ -271,12 +408,21 @@ template <int G, int VEC>
 hgd_status launch_g(SpmmArgs a, bool has_val, hipStream_t st) {
   constexpr int GPB = kBlock / G;
   const int64_t rows = a.row_end - a.row_begin;
+  if constexpr (G >= 8) {
+    if (a.seg) {
+      const int64_t sblocks = (rows + static_cast<int64_t>(GPB) * G - 1) / (GPB * G);
+      if (sblocks <= 0) return HGD_OK;
+      if (sblocks > 0x7fffffffLL) return fail(HGD_ERR_UNSUPPORTED, "hgd_spmm: grid too large");
+      launch_tuned<G, VEC>(a, has_val, true, sblocks, st);
+      return check_launch("hgd_spmm segmented kernel");
+    }
+  }
   const int64_t light_blocks = (rows + GPB - 1) / GPB;
   a.heavy_blocks = (a.n_chunks + GPB - 1) / GPB;
   const int64_t blocks = light_blocks + a.heavy_blocks;
   if (blocks > 0) {
     if (blocks > 0x7fffffffLL) return fail(HGD_ERR_UNSUPPORTED, "hgd_spmm: grid too large");
-    launch_tuned<G, VEC>(a, has_val, blocks, st);
+    launch_tuned<G, VEC>(a, has_val, false, blocks, st);
     hgd_status s = check_launch("hgd_spmm kernel");
     if (s != HGD_OK) return s;
   }
@@ -366,6 +512,8 @@ extern "C" hgd_status hgd_spmm(const int64_t* rowptr, const int32_t* col, const 
     a.heavy_rows = plan->heavy_rows;
     a.heavy_cptr = plan->heavy_cptr;
     a.partial = static_cast<float*>(workspace);
+  } else if (plan && (plan->flags & HGD_PLAN_SEGMENTED)) {
+    a.seg = 1;  // only without split rows: the segmented walk covers every nonzero of its rows
   }
 
   hipStream_t st = as_stream(stream);
@@ -398,11 +546,12 @@ extern "C" hgd_status hgd_set_tuning(int32_t key, int32_t value) {
   clear_error();
   switch (key) {
     case HGD_TUNE_SPMM_UNROLL:
-      HGD_REQUIRE(value == 4 || value == 8 || value == 16, "hgd_set_tuning: unroll must be 4/8/16");
+      HGD_REQUIRE(value == 8 || value == 16, "hgd_set_tuning: unroll must be 8 or 16");
       g_unroll = value;
       return HGD_OK;
     case HGD_TUNE_SPMM_POLICY:
-      HGD_REQUIRE(value >= 0 && value <= 7, "hgd_set_tuning: policy bits 0..7");
+      HGD_REQUIRE(value == 0 || value == 1 || value == 8 || value == 9,
+                  "hgd_set_tuning: policy must be 0, 1 (nt stores), 8 (index prefetch) or 9");
       g_policy = value;
       return HGD_OK;
     default:

@@ -57,9 +57,9 @@ typedef enum hgd_epilogue {
 } hgd_epilogue;
 
 /* Tuning knobs of the SpMM hop (process-wide; defaults are the measured best on MI355X).
- *   HGD_TUNE_SPMM_UNROLL: independent row gathers in flight per lane (4, 8 or 16)
- *   HGD_TUNE_SPMM_POLICY: cache-policy bits, 1 = non-temporal Y stores,
- *                         2 = non-temporal index/weight loads, 4 = non-temporal row gathers */
+ *   HGD_TUNE_SPMM_UNROLL: independent row gathers in flight per lane (8 or 16)
+ *   HGD_TUNE_SPMM_POLICY: 0 plain, 1 non-temporal Y stores, 8 software-pipelined index
+ *                         batches (default), 9 both */
 typedef enum hgd_tune_key { HGD_TUNE_SPMM_UNROLL = 1, HGD_TUNE_SPMM_POLICY = 2 } hgd_tune_key;
 hgd_status hgd_set_tuning(int32_t key, int32_t value);
 
@@ -77,13 +77,17 @@ const char* hgd_get_last_error_string(void);
 typedef struct hgd_split_plan {
   int64_t threshold;           /* rows with degree > threshold are split (<=0: none)   */
   int32_t chunk;               /* nonzeros per chunk                                    */
-  int32_t _pad;
+  int32_t flags;               /* HGD_PLAN_SEGMENTED: short rows, use the segmented kernel */
   int64_t n_heavy;             /* number of split rows                                  */
   int64_t n_chunks;            /* total chunks over all split rows                      */
   const int32_t* heavy_rows;   /* [n_heavy]   split row ids, ascending                  */
   const int64_t* heavy_cptr;   /* [n_heavy+1] chunk range of each split row             */
   const int32_t* chunk_heavy;  /* [n_chunks]  split-row index owning each chunk         */
 } hgd_split_plan;
+
+/* plan.flags bit: the structure has short rows (average degree ≲ 32) and no split rows —
+ * hgd_spmm then walks groups of consecutive rows as one nonzero stream (segmented kernel). */
+#define HGD_PLAN_SEGMENTED 1
 
 /* Counts (n_heavy, n_chunks) for a plan into device int64[2] `counts`. */
 hgd_status hgd_split_plan_count(const int64_t* rowptr, int64_t n_rows, int64_t threshold,

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--zipf", type=float, default=None)
     ap.add_argument("--unrolls", default="4,8,16")
     ap.add_argument("--policies", default="0,1,2,3,4,5,6,7")
+    ap.add_argument("--segmented", default="0,1", help="user-hop kernel variants to A/B")
     args = ap.parse_args()
 
     import torch
@@ -46,11 +47,13 @@ def main():
     Yu = torch.empty(args.users, args.dim, device=dev)
     lib = _native.load()
     variants = list(itertools.product([int(u) for u in args.unrolls.split(",")],
-                                      [int(x) for x in args.policies.split(",")]))
+                                      [int(x) for x in args.policies.split(",")],
+                                      [int(x) for x in args.segmented.split(",")]))
     res = {v: {"items": [], "users": []} for v in variants}
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
     for _ in range(args.rounds):
-        for u, pol in variants:
+        for u, pol, seg in variants:
+            inc.csr.configure_kernel(segmented=bool(seg))
             _native.check(lib.hgd_set_tuning(1, u), "unroll")
             _native.check(lib.hgd_set_tuning(2, pol), "policy")
             ev[0].record()
@@ -59,16 +62,16 @@ def main():
             spmm_csr(inc.csr, M, row_scale=p, out=Yu)
             ev[2].record()
             torch.cuda.synchronize()
-            res[(u, pol)]["items"].append(ev[0].elapsed_time(ev[1]))
-            res[(u, pol)]["users"].append(ev[1].elapsed_time(ev[2]))
+            res[(u, pol, seg)]["items"].append(ev[0].elapsed_time(ev[1]))
+            res[(u, pol, seg)]["users"].append(ev[1].elapsed_time(ev[2]))
     print(f"graph {args.users}x{args.items}x{inc.nnz} d={args.dim} zipf={args.zipf}")
-    print("unroll policy  items_ms(med/min)  users_ms(med/min)  sum")
+    print("unroll policy seg  items_ms(med/min)  users_ms(med/min)  sum")
     rows = []
     for v in variants:
         it, us = res[v]["items"], res[v]["users"]
         rows.append((statistics.median(it) + statistics.median(us), v, it, us))
     for s, v, it, us in sorted(rows):
-        print(f"{v[0]:6d} {v[1]:6d}  {statistics.median(it):7.4f}/{min(it):7.4f}  "
+        print(f"{v[0]:6d} {v[1]:6d} {v[2]:3d}  {statistics.median(it):7.4f}/{min(it):7.4f}  "
               f"{statistics.median(us):7.4f}/{min(us):7.4f}  {s:7.4f}")
 
 
