@@ -62,6 +62,9 @@ def parse():
     ap.add_argument("--pmc", default="auto", choices=["auto", "on", "off"],
                     help="measure HBM traffic with rocprofv3 PMC passes in a child process")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--graph", default="off", choices=["on", "off"],
+                    help="replay the fwd+bwd step as one captured hipGraph (measured: no gain "
+                         "once the per-hop events are out of the timed loop)")
     return ap.parse_args()
 
 
@@ -210,10 +213,31 @@ def main():
     # warm the scale / edge-value caches outside the timed region
     inc.scale("row", "sym"), inc.edge_values("csc", "sym")
 
-    def step():
+    def eager_step():
         Y = sharded_two_hop(sh, X)
         (dX,) = torch.autograd.grad(Y, X, dY)
         return dX
+
+    step = eager_step
+    use_graph = args.graph == "on"
+    if use_graph:
+        # whole-step capture: fwd + autograd bwd (4 hgd_spmm launches and their allocations) as
+        # one hipGraph over the static X / dY — replay removes the host launch overhead that
+        # dominates dataset-sized graphs, with no input copies (make_graphed_callables would
+        # copy X and dY into placeholders every replay: 2 × 2.56 GB at the 100 M-edge shape)
+        side = torch.cuda.Stream(device)
+        side.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(side):
+            for _ in range(3):
+                eager_step()
+        torch.cuda.current_stream(device).wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            static_dX = eager_step()
+
+        def step():
+            graph.replay()
+            return static_dX
 
     for _ in range(args.warmup):
         step()
@@ -221,15 +245,20 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    timer = profiling.HopTimer()
     t0 = time.perf_counter()
-    with timer:
-        for _ in range(args.steps):
-            step()
+    for _ in range(args.steps):
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # roofline pass: the same steps again, eager, with HIP events around every hop launch on
+    # its stream (kept out of the timed loop above so the events cannot inflate ms_per_step)
+    timer = profiling.HopTimer()
+    with timer:
+        for _ in range(args.steps):
+            eager_step()
+    torch.cuda.synchronize()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -303,6 +332,7 @@ def main():
             "op": "hgconv2 fwd+bwd: D_v^-1/2 H D_e^-1 H^T D_v^-1/2 X, 4 hgd_spmm hops",
             "parallelism": (f"user-row shards x{world}, RCCL all-reduce of item sums "
                             f"({args.chunks} chunks)" if world > 1 else "single GPU"),
+            "hip_graph": use_graph,
         },
         "roofline": roofline,
         "cpu_baseline": cpu,

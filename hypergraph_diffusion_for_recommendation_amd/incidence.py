@@ -28,6 +28,22 @@ from . import profiling
 DEFAULT_SPLIT_THRESHOLD = 2048
 DEFAULT_SPLIT_CHUNK = 512
 SEGMENTED_MAX_AVG_DEGREE = 32
+# lane-group tasks needed to fill MI355X: 256 CUs × 16 waves × 4 groups of 16 lanes (d = 64)
+TARGET_GROUPS = 16384
+
+
+def auto_split(n_rows: int, nnz: int) -> Tuple[int, int]:
+    """(threshold, chunk) for the long-row split. Large structures keep 2048 / 512 (split only
+    the popular outliers). A structure with fewer rows than TARGET_GROUPS (e.g. ML-1M's 3,706
+    items × ~200 nonzeros) would leave most CUs idle with one group per row, so its rows are cut
+    into chunks of ≈ nnz / TARGET_GROUPS nonzeros (power of two in [32, 512])."""
+    if n_rows >= TARGET_GROUPS or nnz == 0:
+        return DEFAULT_SPLIT_THRESHOLD, DEFAULT_SPLIT_CHUNK
+    want = max(1, nnz // TARGET_GROUPS)
+    chunk = 32
+    while chunk < want and chunk < DEFAULT_SPLIT_CHUNK:
+        chunk *= 2
+    return 2 * chunk, chunk
 
 
 def _ws(nbytes: int, device) -> torch.Tensor:
@@ -204,9 +220,11 @@ class Incidence:
     @classmethod
     def from_coo(cls, indices: torch.Tensor, values: Optional[torch.Tensor], shape,
                  device=None, validate: bool = True, rows_sorted: Optional[bool] = None,
-                 split_threshold: int = DEFAULT_SPLIT_THRESHOLD,
-                 split_chunk: int = DEFAULT_SPLIT_CHUNK) -> "Incidence":
+                 split_threshold: Optional[int] = None,
+                 split_chunk: Optional[int] = None) -> "Incidence":
         """Builds from COO ``indices`` int64 [2, nnz] (+ fp32 ``values`` or None = ones).
+
+        ``split_threshold`` / ``split_chunk`` default to :func:`auto_split` per orientation.
 
         Entries keep their order within a row (duplicates stay separate nonzeros, which is the
         same linear map as torch's coalesced sum). Raises ValueError on out-of-range indices.
@@ -261,8 +279,8 @@ class Incidence:
 
     @classmethod
     def _from_sorted(cls, rows: torch.Tensor, cols: torch.Tensor, values: Optional[torch.Tensor],
-                     n_rows: int, n_cols: int, split_threshold: int,
-                     split_chunk: int) -> "Incidence":
+                     n_rows: int, n_cols: int, split_threshold: Optional[int] = None,
+                     split_chunk: Optional[int] = None) -> "Incidence":
         device = rows.device
         lib = nat.load()
         st = _stream(device)
@@ -292,8 +310,13 @@ class Incidence:
             del perm
         else:
             colptr.zero_()
-        csr = CSR(rowptr, cols, n_rows, n_cols, split_threshold, split_chunk)
-        csc = CSR(colptr, csc_col, n_cols, n_rows, split_threshold, split_chunk)
+        def split(n):
+            if split_threshold is None:
+                return auto_split(n, nnz)
+            return split_threshold, split_chunk or DEFAULT_SPLIT_CHUNK
+
+        csr = CSR(rowptr, cols, n_rows, n_cols, *split(n_rows))
+        csc = CSR(colptr, csc_col, n_cols, n_rows, *split(n_cols))
         c1, c2 = csr.plan_count_async(), csc.plan_count_async()
         if c1 is not None:
             csr._build_plan(*c1.tolist())

@@ -326,8 +326,7 @@ class EquivSetGNN(nn.Module):
         if inc is None:
             n_e = int(hypergraph.shape[1])
             csr_rows = V.to(torch.int32)
-            inc = Incidence._from_sorted(csr_rows, cols, None, int(hypergraph.shape[0]), n_e,
-                                         split_threshold=2048, split_chunk=512)
+            inc = Incidence._from_sorted(csr_rows, cols, None, int(hypergraph.shape[0]), n_e)
         # E spans max(E)+1 hyperedges in the reference (torch_scatter's output size); extra empty
         # columns of the incidence contribute nothing, so the cached incidence is reused as is.
         V._hgd_incidence = inc
