@@ -1,0 +1,152 @@
+"""Encoders of the hot-path carriers, rebuilt on the drop-in layers (the callers of the path).
+
+They keep the reference's constructor arguments (the argparse ``kwargs`` dict and the
+``Interaction`` data object with ``n_users``, ``n_items``, ``norm_adj``, ``ui_adj``), parameter
+names (so ``state_dict``s load either way) and forward outputs, so a plugin can swap the whole
+encoder (paths relative to /root/reference/HD_SELFRec):
+
+* :class:`HCCFEncoder`       model/graph/HCCF.py:136-191
+* :class:`LocalAwareEncoder` model/graph/HGNN_HD4.py:336-405 (``--mode=local_only``)
+
+Everything sparse runs on libhgd; dropout, the dense ``E·W`` products and LayerNorm stay torch.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from .incidence import Incidence
+from .layers import EquivSetGNN, GCNLayer, HGCNConv, HGNNLayer, SpAdjDropEdge
+
+
+def sparse_tensor_of(mat, device) -> torch.Tensor:
+    """TorchGraphInterface.convert_sparse_mat_to_tensor (base/torch_interface.py:8-12) on the
+    device, with its Incidence built once and cached on the tensor."""
+    coo = mat.tocoo()
+    i = torch.from_numpy(np.stack([coo.row, coo.col]).astype(np.int64))
+    v = torch.from_numpy(coo.data.astype(np.float32))
+    t = torch.sparse_coo_tensor(i, v, coo.shape).to(device)
+    t._hgd_incidence = Incidence.from_coo(t._indices(), t._values(), coo.shape, device=device)
+    return t
+
+
+class HCCFEncoder(nn.Module):
+    """HCCF propagation: per layer a GCN hop on the (edge-dropped) normalised bipartite graph plus
+    the dense learned-hypergraph hop for users and items; outputs the layer sum and the per-layer
+    GCN / hypergraph embeddings for the InfoNCE terms (HCCF.py:173-191)."""
+
+    def __init__(self, conf, data, device=None):
+        super().__init__()
+        self.data = data
+        self._parse_config(conf)
+        self.device = torch.device(device) if device is not None else torch.device("cuda")
+        self.gcnlayer = GCNLayer(self.leaky)
+        self.hgnnlayer = HGNNLayer(self.leaky)
+        self.norm_adj = data.norm_adj
+        self.sparse_norm_adj = sparse_tensor_of(self.norm_adj, self.device)
+        self.embedding_dict = self._init_model()
+        self.drop_out = nn.Dropout(self.drop_rate)
+        self.edgeDropper = SpAdjDropEdge()
+
+    def _parse_config(self, config):
+        self.lRate = float(config['lrate'])
+        self.lr_decay = float(config['lr_decay'])
+        self.maxEpoch = int(config['max_epoch'])
+        self.batchSize = int(config['batch_size'])
+        self.reg = float(config['reg'])
+        self.latent_size = int(config['embedding_size'])
+        self.hyperDim = int(config['hyper_dim'])
+        self.drop_rate = float(config['drop_rate'])
+        self.leaky = float(config['p'])
+        self.n_layers = int(config['n_layers'])
+        self.n_edges = int(config['hyper_dim'])
+
+    def _init_model(self):
+        init = nn.init.xavier_uniform_
+        dev = self.device
+        return nn.ParameterDict({
+            'user_emb': nn.Parameter(init(torch.empty(self.data.n_users, self.latent_size)).to(dev)),
+            'item_emb': nn.Parameter(init(torch.empty(self.data.n_items, self.latent_size)).to(dev)),
+            'user_w': nn.Parameter(init(torch.empty(self.latent_size, self.n_edges)).to(dev)),
+            'item_w': nn.Parameter(init(torch.empty(self.latent_size, self.n_edges)).to(dev)),
+        })
+
+    def forward(self, keep_rate=0.5):
+        nu = self.data.n_users
+        embeddings = torch.cat([self.embedding_dict['user_emb'], self.embedding_dict['item_emb']], 0)
+        hidden = [embeddings]
+        gcn_hidden, hgnn_hidden = [], []
+        hyper_uu = self.embedding_dict['user_emb'] @ self.embedding_dict['user_w']
+        hyper_ii = self.embedding_dict['item_emb'] @ self.embedding_dict['item_w']
+        for _ in range(self.n_layers):
+            gcn_emb = self.gcnlayer(self.edgeDropper(self.sparse_norm_adj, keep_rate), hidden[-1])
+            hyper_uemb = self.hgnnlayer(self.drop_out(hyper_uu), hidden[-1][:nu])
+            hyper_iemb = self.hgnnlayer(self.drop_out(hyper_ii), hidden[-1][nu:])
+            gcn_hidden += [gcn_emb]
+            hgnn_hidden += [torch.cat([hyper_uemb, hyper_iemb], 0)]
+            hidden += [gcn_emb + hgnn_hidden[-1]]
+        embeddings = sum(hidden)
+        return embeddings[:nu], embeddings[nu:], gcn_hidden, hgnn_hidden
+
+
+def edhnn_config(hyper_size):
+    """LocalAwareEncoder.init_edhnn_config (HGNN_HD4.py:371-388)."""
+    return {
+        'MLP_hidden': hyper_size, 'MLP1_num_layers': 0, 'MLP2_num_layers': 0,
+        'MLP3_num_layers': 1, 'MLP_num_layers': 0, 'restart_alpha': 0.0, 'aggregate': 'mean',
+        'dropout': 0.5, 'normalization': 'ln', 'input_norm': True, 'All_num_layers': 1,
+        'activation': 'relu', 'input_dropout': 0.6, 'AllSet_input_norm': True,
+    }
+
+
+class LocalAwareEncoder(nn.Module):
+    """HGNN_HD4's local encoder: layers 0..L-2 are ED-HNN blocks on V/E = nonzero(ui_adj > 0),
+    the last is LayerNorm(HGCNConv(Â, ·, act=False)); every layer adds the layer-0 residual
+    (HGNN_HD4.py:390-405).
+
+    The reference densifies ``ui_adj`` on the CPU (``torch.tensor(ui_adj.todense())``,
+    HGNN_HD4.py:367-369: 83 GB at Amazon-Book) and scans it twice per block per step; here the
+    same V/E (row-major nonzero order) come from the sparse matrix, once.
+    """
+
+    def __init__(self, data, emb_size, hyper_size, n_layers, leaky, drop_rate, device=None,
+                 use_self_att=False):
+        super().__init__()
+        self.data = data
+        self.latent_size = emb_size
+        self.hyper_size = hyper_size
+        self.layers = n_layers
+        self.norm_adj = data.norm_adj
+        self.ui_adj = data.ui_adj
+        self.device = torch.device(device) if device is not None else torch.device("cuda")
+        self.relu = nn.ReLU()
+        self.act = nn.LeakyReLU(leaky)
+        self.dropout = nn.Dropout(drop_rate)
+        self.edgeDropper = SpAdjDropEdge()
+        self.sparse_norm_adj = sparse_tensor_of(data.norm_adj, self.device)
+        self.edhnn_args = edhnn_config(self.hyper_size)
+        self.hgcn_layers = nn.ModuleList([HGCNConv(leaky=0.5) for _ in range(self.layers)])
+        self.edhnn_layers = nn.ModuleList(
+            [EquivSetGNN(hyper_size, self.edhnn_args, None, data) for _ in range(self.layers)])
+        self.lns = nn.ModuleList([nn.LayerNorm(hyper_size) for _ in range(self.layers)])
+        self.edhnn_ui_n = data.n_items + data.n_users
+        ui = data.ui_adj.tocsr().copy()
+        ui.sort_indices()  # nonzero(dense > 0) order: rows, then ascending columns
+        ui.eliminate_zeros()
+        self.hypergraph = sparse_tensor_of(ui, self.device)
+        self.to(self.device)  # the reference moves it with HGNNModel.to(device)
+
+    def forward(self, ego_embeddings, sparse_norm_adj):
+        res = ego_embeddings
+        all_embeddings = []
+        for k in range(self.layers):
+            if k != self.layers - 1:
+                ego_embeddings = self.edhnn_layers[k](ego_embeddings, self.hypergraph,
+                                                      self.edhnn_ui_n) + res
+            else:
+                ego_embeddings = self.lns[0](self.hgcn_layers[0](sparse_norm_adj, ego_embeddings,
+                                                                 act=False)) + res
+            all_embeddings += [ego_embeddings]
+        nu = self.data.n_users
+        return all_embeddings[-1][:nu], all_embeddings[-1][nu:]
