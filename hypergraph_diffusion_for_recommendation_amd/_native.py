@@ -73,6 +73,12 @@ _SIGNATURES = {
     "hgd_dropedge_compact": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_f32,
                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size,
                                      c_void_p]),
+    "hgd_bernoulli_mask": (c_i32, [ctypes.c_uint64, c_i64, c_f32, c_void_p, c_void_p]),
+    "hgd_dropedge_structure_workspace_size": (c_size, [c_i64]),
+    "hgd_dropedge_structure": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_void_p, c_void_p, c_i64, c_i64, c_i64, c_void_p, c_f32,
+                                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_void_p, c_void_p, c_size, c_void_p]),
     "hgd_dense_threshold_workspace_size": (c_size, [c_i64]),
     "hgd_dense_threshold_rowptr": (c_i32, [c_void_p, c_i64, c_i64, c_i64, c_f32, c_void_p,
                                            c_void_p, c_size, c_void_p]),

@@ -223,6 +223,50 @@ __global__ void k_dropedge_scatter(const int64_t* __restrict__ rows,
   out_val[p] = __fdiv_rn(val[e], keep);  // vals[mask] / keepRate, IEEE fp32 division
 }
 
+// Counter-based keep-mask: u = 24-bit uniform in [0,1) from a splitmix64 hash of (seed, i);
+// keep iff floor(u + keep) != 0, the expression of SpAdjDropEdge (HCCF.py:223) on a device RNG.
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__global__ void k_bernoulli_mask(uint64_t seed, int64_t n, float keep,
+                                 uint8_t* __restrict__ mask) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t h = splitmix64(seed ^ splitmix64(static_cast<uint64_t>(i)));
+  const float u = static_cast<float>(h >> 40) * (1.0f / 16777216.0f);
+  mask[i] = floorf(u + keep) != 0.f ? 1 : 0;
+}
+
+// flags[i] = mask[perm ? perm[i] : i] (0/1), flags[n] = 0 for the exclusive-scan total.
+__global__ void k_mask_flags(const uint8_t* __restrict__ mask, const int32_t* __restrict__ perm,
+                             int64_t n, int64_t* __restrict__ flags) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (i > n) return;
+  flags[i] = (i < n && mask[perm ? perm[i] : i]) ? 1 : 0;
+}
+
+// Order-preserving compaction of one orientation + its row pointer:
+// idx_out[pos[e]] = idx[e], val_out[pos[e]] = val[e] / keep for kept e; rowptr_out[r] = pos[rowptr[r]].
+__global__ void k_compact_orientation(const int64_t* __restrict__ rowptr, int64_t n_rows,
+                                      const int32_t* __restrict__ idx,
+                                      const float* __restrict__ val,
+                                      const int64_t* __restrict__ flags,
+                                      const int64_t* __restrict__ pos, int64_t nnz, float keep,
+                                      int64_t* __restrict__ rowptr_out,
+                                      int32_t* __restrict__ idx_out,
+                                      float* __restrict__ val_out) {
+  const int64_t e = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (e <= n_rows) rowptr_out[e] = pos[rowptr[e]];
+  if (e >= nnz || !flags[e]) return;
+  const int64_t p = pos[e];
+  idx_out[p] = idx[e];
+  if (val && val_out) val_out[p] = __fdiv_rn(val[e], keep);
+}
+
 // One wavefront per row: number of entries > thresh.
 __global__ void k_dense_count(const float* __restrict__ H, int64_t n_rows, int64_t n_cols,
                               int64_t ld, float thresh, int64_t* __restrict__ counts) {
@@ -497,6 +541,66 @@ extern "C" hgd_status hgd_dropedge_compact(const int64_t* rows, const int64_t* c
   hipLaunchKernelGGL(k_dropedge_scatter, dim3(grid_for(nnz + 1)), dim3(kBlock), 0, st, rows, cols,
                      val, mask, pos, nnz, keep, out_rows, out_cols, out_val, out_count);
   return check_launch("hgd_dropedge_compact scatter");
+}
+
+extern "C" hgd_status hgd_bernoulli_mask(uint64_t seed, int64_t n, float keep, uint8_t* mask,
+                                         void* stream) {
+  clear_error();
+  HGD_REQUIRE(n >= 0 && (mask || n == 0), "hgd_bernoulli_mask: bad arguments");
+  if (n == 0) return HGD_OK;
+  hipLaunchKernelGGL(k_bernoulli_mask, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream),
+                     seed, n, keep, mask);
+  return check_launch("hgd_bernoulli_mask");
+}
+
+extern "C" size_t hgd_dropedge_structure_workspace_size(int64_t nnz) {
+  return 2 * align_up(static_cast<size_t>(nnz + 1) * sizeof(int64_t)) +
+         align_up(excl_scan_bytes<int64_t>(nnz + 1));
+}
+
+extern "C" hgd_status hgd_dropedge_structure(
+    const int64_t* rowptr, const int32_t* col, const float* val, const int64_t* colptr,
+    const int32_t* row_t, const float* val_t, const int32_t* perm_t, int64_t n_rows,
+    int64_t n_cols, int64_t nnz, const uint8_t* mask, float keep, int64_t* rowptr_out,
+    int32_t* col_out, float* val_out, int64_t* colptr_out, int32_t* row_t_out,
+    float* val_t_out, void* workspace, size_t workspace_bytes, void* stream) {
+  clear_error();
+  HGD_REQUIRE(n_rows >= 0 && n_cols >= 0 && nnz >= 0, "hgd_dropedge_structure: sizes");
+  HGD_REQUIRE(keep > 0.f, "hgd_dropedge_structure: keep must be > 0");
+  HGD_REQUIRE(rowptr && colptr && rowptr_out && colptr_out, "hgd_dropedge_structure: null ptr");
+  HGD_REQUIRE(nnz == 0 || (col && row_t && perm_t && mask && col_out && row_t_out),
+              "hgd_dropedge_structure: null index arrays");
+  HGD_REQUIRE(!val == !val_t && (!val || (val_out && val_t_out)),
+              "hgd_dropedge_structure: values must be given for both orientations or neither");
+  const size_t need = hgd_dropedge_structure_workspace_size(nnz);
+  if (workspace_bytes < need || !workspace)
+    return fail(HGD_ERR_WORKSPACE, "hgd_dropedge_structure: workspace %zu < %zu",
+                workspace_bytes, need);
+  hipStream_t st = as_stream(stream);
+  const size_t arr = align_up(static_cast<size_t>(nnz + 1) * sizeof(int64_t));
+  char* ws = static_cast<char*>(workspace);
+  int64_t* flags = reinterpret_cast<int64_t*>(ws);
+  int64_t* pos = reinterpret_cast<int64_t*>(ws + arr);
+  void* tmp = ws + 2 * arr;
+  const size_t tmp_bytes = workspace_bytes - 2 * arr;
+  // CSR: the mask is in CSR order
+  for (int side = 0; side < 2; ++side) {
+    const bool csc = side == 1;
+    const int64_t nr = csc ? n_cols : n_rows;
+    hipLaunchKernelGGL(k_mask_flags, dim3(grid_for(nnz + 1)), dim3(kBlock), 0, st, mask,
+                       csc ? perm_t : nullptr, nnz, flags);
+    hgd_status s = check_launch("hgd_dropedge_structure flags");
+    if (s != HGD_OK) return s;
+    size_t b = tmp_bytes;
+    HGD_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, b, flags, pos, nnz + 1, st));
+    hipLaunchKernelGGL(k_compact_orientation, dim3(grid_for(std::max(nnz, nr + 1))),
+                       dim3(kBlock), 0, st, csc ? colptr : rowptr, nr, csc ? row_t : col,
+                       csc ? val_t : val, flags, pos, nnz, keep, csc ? colptr_out : rowptr_out,
+                       csc ? row_t_out : col_out, csc ? val_t_out : val_out);
+    s = check_launch("hgd_dropedge_structure compact");
+    if (s != HGD_OK) return s;
+  }
+  return HGD_OK;
 }
 
 extern "C" size_t hgd_dense_threshold_workspace_size(int64_t n_rows) {

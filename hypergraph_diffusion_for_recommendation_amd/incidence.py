@@ -208,6 +208,8 @@ class Incidence:
         self.device = csr.device
         self._scales: Dict[Tuple[str, str], torch.Tensor] = {}
         self._edge_vals: Dict[Tuple[str, str, str], Optional[torch.Tensor]] = {}
+        self.perm_t: Optional[torch.Tensor] = None  # CSC position → CSR position
+        self.coo_sorted = False  # True when built from a row-sorted COO (COO order = CSR order)
 
     @property
     def shape(self):
@@ -274,8 +276,9 @@ class Incidence:
             cols = _gather32(cols, perm)
             if values is not None:
                 values = _gather32(values, perm)
-        return cls._from_sorted(rows, cols, values, n_rows, n_cols, split_threshold,
-                                split_chunk)
+        inc = cls._from_sorted(rows, cols, values, n_rows, n_cols, split_threshold, split_chunk)
+        inc.coo_sorted = bool(rows_sorted) or nnz == 0
+        return inc
 
     @classmethod
     def _from_sorted(cls, rows: torch.Tensor, cols: torch.Tensor, values: Optional[torch.Tensor],
@@ -307,9 +310,10 @@ class Incidence:
             csc_col = _gather32(rows, perm)
             if values is not None:
                 val_t = _gather32(values, perm)
-            del perm
         else:
             colptr.zero_()
+            perm = torch.empty(0, dtype=torch.int32, device=device)
+
         def split(n):
             if split_threshold is None:
                 return auto_split(n, nnz)
@@ -324,7 +328,54 @@ class Incidence:
             csc._build_plan(*c2.tolist())
         csr.configure_kernel()
         csc.configure_kernel()
-        return cls(csr, csc, values, val_t)
+        inc = cls(csr, csc, values, val_t)
+        inc.perm_t = perm  # CSC position → CSR position (sort-free drop-edge rebuilds)
+        return inc
+
+    def drop(self, mask: torch.Tensor, keep: float) -> "Incidence":
+        """The incidence of SpAdjDropEdge's output (HCCF.py:217-226) built from this one without
+        any sort: ``mask`` (uint8/bool, CSR order) keeps nonzeros in order and values are divided
+        by ``keep``; the CSC comes from compacting this CSC through ``perm_t``
+        (hgd_dropedge_structure). One device→host read (the kept count)."""
+        lib = nat.load()
+        dev = self.device
+        st = _stream(dev)
+        nnz, R, C = self.nnz, self.n_rows, self.n_cols
+        m = mask.to(device=dev, dtype=torch.uint8).contiguous()
+        if m.numel() != nnz:
+            raise ValueError("Incidence.drop: mask size mismatch")
+        rowptr = torch.empty(R + 1, dtype=torch.int64, device=dev)
+        colptr = torch.empty(C + 1, dtype=torch.int64, device=dev)
+        col = torch.empty(nnz, dtype=torch.int32, device=dev)
+        row_t = torch.empty(nnz, dtype=torch.int32, device=dev)
+        weighted = self.val is not None
+        val = torch.empty(nnz, dtype=torch.float32, device=dev) if weighted else None
+        val_t = torch.empty(nnz, dtype=torch.float32, device=dev) if weighted else None
+        ws = _ws(lib.hgd_dropedge_structure_workspace_size(nnz), dev)
+        nat.check(lib.hgd_dropedge_structure(
+            self.csr.rowptr.data_ptr(), nat.ptr(self.csr.col) if nnz else None, nat.ptr(self.val),
+            self.csc.rowptr.data_ptr(), nat.ptr(self.csc.col) if nnz else None,
+            nat.ptr(self.val_t), nat.ptr(self.perm_t) if nnz else None, R, C, nnz,
+            m.data_ptr() if nnz else None, float(keep), rowptr.data_ptr(),
+            col.data_ptr() if nnz else None, nat.ptr(val), colptr.data_ptr(),
+            row_t.data_ptr() if nnz else None, nat.ptr(val_t), ws.data_ptr(), ws.numel(), st),
+            "hgd_dropedge_structure")
+        kept = int(rowptr[R].item()) if R else 0
+        col, row_t = col[:kept], row_t[:kept]
+        if weighted:
+            val, val_t = val[:kept], val_t[:kept]
+        csr = CSR(rowptr, col, R, C, self.csr.split_threshold, self.csr.split_chunk)
+        csc = CSR(colptr, row_t, C, R, self.csc.split_threshold, self.csc.split_chunk)
+        # degrees only shrink: a parent without split rows has none after dropping (no count)
+        for child, parent in ((csr, self.csr), (csc, self.csc)):
+            if parent.n_heavy:
+                cnt = child.plan_count_async()
+                if cnt is not None:
+                    child._build_plan(*cnt.tolist())
+            child.plan.flags = parent.plan.flags if child.n_heavy == 0 else 0
+        out = Incidence(csr, csc, val, val_t)
+        out.perm_t = None  # a dropped structure is not dropped again (the reference drops the base)
+        return out
 
     @classmethod
     def from_torch_sparse(cls, adj: torch.Tensor, device=None, **kw) -> "Incidence":

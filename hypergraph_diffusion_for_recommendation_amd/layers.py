@@ -77,13 +77,18 @@ class HGCNConv(nn.Module):
 class SpAdjDropEdge(nn.Module):
     """Edge dropout on a sparse COO adjacency (HCCF.py:213-226).
 
-    The keep-mask is drawn exactly as the reference does — ``torch.rand(nnz)`` on the CPU
-    generator, ``floor(rand + keepRate)`` — so it is bit-identical for the same seed; the
-    compaction (``idxs[:, mask]``, ``vals[mask] / keepRate``) runs on the device.
+    By default the keep-mask is drawn exactly as the reference does — ``torch.rand(nnz)`` on the
+    CPU generator, ``floor(rand + keepRate)`` — so it is bit-identical for the same seed.
+    ``device_rng=True`` draws it on the GPU instead (hgd_bernoulli_mask, seeded from the CPU
+    generator so ``torch.manual_seed`` still fixes it): same distribution, no host RNG / H2D.
+    The compaction (``idxs[:, mask]``, ``vals[mask] / keepRate``) and the CSR/CSC of the result
+    are built on the device; for the row-major COO of ``convert_sparse_mat_to_tensor`` the
+    structure is derived from the parent's without sorting (Incidence.drop).
     """
 
-    def __init__(self):
+    def __init__(self, device_rng: bool = False):
         super().__init__()
+        self.device_rng = device_rng
 
     def forward(self, adj, keepRate):
         if keepRate == 1.0:
@@ -91,16 +96,28 @@ class SpAdjDropEdge(nn.Module):
         vals = adj._values()
         idxs = adj._indices()
         edgeNum = vals.size()
-        mask = ((torch.rand(edgeNum) + keepRate).floor()).type(torch.bool)
-        count = int(mask.sum())
         device = vals.device if vals.device.type == "cuda" else torch.device("cuda")
-        new_idx, new_vals = drop_edges(idxs.to(device), vals.to(device),
-                                       mask.to(device, non_blocking=True), keepRate, count)
+        parent = incidence_of(adj) if vals.device.type == "cuda" else None
+        if self.device_rng:
+            from . import _native as nat
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+            mask = torch.empty(edgeNum, dtype=torch.uint8, device=device)
+            if mask.numel():
+                nat.check(nat.load().hgd_bernoulli_mask(
+                    seed, mask.numel(), float(keepRate), mask.data_ptr(),
+                    torch.cuda.current_stream(device).cuda_stream), "hgd_bernoulli_mask")
+            count = None
+        else:
+            mask = ((torch.rand(edgeNum) + keepRate).floor()).type(torch.bool)
+            count = int(mask.sum())
+            mask = mask.to(device, non_blocking=True)
+        new_idx, new_vals = drop_edges(idxs.to(device), vals.to(device), mask, keepRate, count)
         out = torch.sparse_coo_tensor(new_idx, new_vals, adj.shape)
-        # the compaction is order preserving; sortedness is re-checked on the device (no sort
-        # happens for the row-major COO of convert_sparse_mat_to_tensor)
-        out._hgd_incidence = Incidence.from_coo(new_idx, new_vals, adj.shape, device=device,
-                                                validate=False)
+        if parent is not None and parent.coo_sorted and parent.perm_t is not None:
+            out._hgd_incidence = parent.drop(mask, keepRate)  # COO order == CSR order
+        else:
+            out._hgd_incidence = Incidence.from_coo(new_idx, new_vals, adj.shape, device=device,
+                                                    validate=False)
         return out
 
 

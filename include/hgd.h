@@ -154,6 +154,24 @@ hgd_status hgd_dropedge_compact(const int64_t* rows, const int64_t* cols, const 
                                 int64_t* out_count, void* workspace, size_t workspace_bytes,
                                 void* stream);
 
+/* Device keep-mask for drop-edge: mask[i] = floor(u_i + keep) != 0 with u_i a 24-bit uniform
+ * from a counter-based hash of (seed, i) — the SpAdjDropEdge expression (HCCF.py:223) without
+ * the host RNG round trip (statistically, not bitwise, equal to torch's CPU stream). */
+hgd_status hgd_bernoulli_mask(uint64_t seed, int64_t n, float keep, uint8_t* mask, void* stream);
+
+/* Sort-free rebuild of a drop-edge'd structure from its parent: compacts the parent CSR with the
+ * mask (CSR order) and the parent CSC with mask[perm_t[e']] (perm_t: CSC position → CSR
+ * position), dividing values by keep; row pointers are remapped through the prefix sums.
+ * Outputs are sized for nnz (upper bound); the kept count is rowptr_out[n_rows]. No host sync. */
+size_t hgd_dropedge_structure_workspace_size(int64_t nnz);
+hgd_status hgd_dropedge_structure(const int64_t* rowptr, const int32_t* col, const float* val,
+                                  const int64_t* colptr, const int32_t* row_t, const float* val_t,
+                                  const int32_t* perm_t, int64_t n_rows, int64_t n_cols,
+                                  int64_t nnz, const uint8_t* mask, float keep,
+                                  int64_t* rowptr_out, int32_t* col_out, float* val_out,
+                                  int64_t* colptr_out, int32_t* row_t_out, float* val_t_out,
+                                  void* workspace, size_t workspace_bytes, void* stream);
+
 /* torch.nonzero(H > thresh) of a dense row-major [n_rows, n_cols] fp32 matrix (leading dim ld),
  * in two passes: rowptr (n_rows+1, int64) then the column list (rowptr[n_rows] int32 entries). */
 size_t hgd_dense_threshold_workspace_size(int64_t n_rows);

@@ -105,3 +105,70 @@ def test_expand_rows(dev):
     r, c = random_coo(rng, 90, 80, 1500)
     inc = _inc(r, c, None, (90, 80), dev)
     np.testing.assert_array_equal(expand_rows(inc.csr.rowptr, inc.nnz).cpu().numpy(), r)
+
+
+@pytest.mark.parametrize("weighted", [True, False])
+def test_incidence_drop_is_sort_free_rebuild(dev, weighted):
+    """Incidence.drop (hgd_dropedge_structure) equals building the dropped COO from scratch."""
+    from hypergraph_diffusion_for_recommendation_amd import Incidence
+    rng = np.random.default_rng(12 + weighted)
+    R, C = 700, 500
+    r, c = random_coo(rng, R, C, 9000)
+    vals = rng.random(len(r)).astype(np.float32) if weighted else None
+    inc = _inc(r, c, vals, (R, C), dev)
+    assert inc.coo_sorted and inc.perm_t is not None
+    torch.manual_seed(3)
+    mask = ((torch.rand(len(r)) + 0.6).floor()).type(torch.bool)
+    d = inc.drop(mask.to(dev), 0.6)
+    keep = mask.numpy()
+    v2 = None if vals is None else (vals[keep] / np.float32(0.6)).astype(np.float32)
+    rowptr, col, vv, _ = O.csr_from_coo(r[keep], c[keep], R, v2)
+    colptr, rows_t, vt, _ = O.transpose_csr(rowptr, col, C, vv)
+    np.testing.assert_array_equal(d.csr.rowptr.cpu().numpy(), rowptr)
+    np.testing.assert_array_equal(d.csr.col.cpu().numpy(), col)
+    np.testing.assert_array_equal(d.csc.rowptr.cpu().numpy(), colptr)
+    np.testing.assert_array_equal(d.csc.col.cpu().numpy(), rows_t)
+    if weighted:
+        np.testing.assert_array_equal(d.val.cpu().numpy().view(np.uint32), vv.view(np.uint32))
+        np.testing.assert_array_equal(d.val_t.cpu().numpy().view(np.uint32), vt.view(np.uint32))
+    assert d.nnz == int(keep.sum())
+
+
+def test_device_mask_statistics_and_seed(dev):
+    from hypergraph_diffusion_for_recommendation_amd import _native as nat
+    lib = nat.load()
+    n = 1_000_000
+    st = torch.cuda.current_stream().cuda_stream
+    m1 = torch.empty(n, dtype=torch.uint8, device=dev)
+    m2 = torch.empty(n, dtype=torch.uint8, device=dev)
+    m3 = torch.empty(n, dtype=torch.uint8, device=dev)
+    for m, s in ((m1, 7), (m2, 7), (m3, 8)):
+        nat.check(lib.hgd_bernoulli_mask(s, n, 0.7, m.data_ptr(), st), "mask")
+    assert torch.equal(m1, m2) and not torch.equal(m1, m3)
+    frac = m1.float().mean().item()
+    assert abs(frac - 0.7) < 3e-3  # ~6.5 sigma at n = 1e6
+    # keep = 1.0 keeps everything (floor(u + 1) = 1 for u in [0, 1))
+    nat.check(lib.hgd_bernoulli_mask(9, n, 1.0, m1.data_ptr(), st), "mask")
+    assert int(m1.sum()) == n
+
+
+def test_spadj_dropedge_device_rng(dev):
+    from hypergraph_diffusion_for_recommendation_amd.layers import SpAdjDropEdge
+    rng = np.random.default_rng(4)
+    A = O.normalize_graph_mat(O.bipartite_adjacency(*random_coo(rng, 80, 60, 700), 80, 60))
+    idx, vals = O.coo_of(A)
+    adj = torch.sparse_coo_tensor(torch.from_numpy(idx), torch.from_numpy(vals), A.shape).to(dev)
+    torch.manual_seed(5)
+    a = SpAdjDropEdge(device_rng=True)(adj, 0.7)
+    torch.manual_seed(5)
+    b = SpAdjDropEdge(device_rng=True)(adj, 0.7)
+    assert torch.equal(a._indices(), b._indices()) and torch.equal(a._values(), b._values())
+    # the result is a subset of the parent, in order, values / keep
+    ai = a._indices().cpu().numpy()
+    key = idx[0] * A.shape[1] + idx[1]
+    sel = np.searchsorted(key, ai[0] * A.shape[1] + ai[1])
+    assert np.all(np.diff(sel) > 0)
+    np.testing.assert_array_equal(a._values().cpu().numpy(),
+                                  (vals[sel] / np.float32(0.7)).astype(np.float32))
+    inc = a._hgd_incidence
+    assert inc.nnz == a._values().numel()
