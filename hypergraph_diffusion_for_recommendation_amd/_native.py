@@ -84,6 +84,10 @@ _SIGNATURES = {
                                            c_void_p, c_size, c_void_p]),
     "hgd_dense_threshold_fill": (c_i32, [c_void_p, c_i64, c_i64, c_i64, c_f32, c_void_p,
                                          c_void_p, c_void_p]),
+    "hgd_mask_scores": (c_i32, [c_void_p, c_i64, c_i64, c_void_p, c_void_p, c_void_p, c_f32,
+                                c_void_p]),
+    "hgd_topk_rows": (c_i32, [c_void_p, c_i64, c_i64, c_i64, c_i32, c_void_p, c_void_p,
+                              c_void_p]),
     "hgd_epilogue_apply": (c_i32, [c_void_p, c_i64, c_i32, c_f32, c_void_p, c_void_p]),
     "hgd_epilogue_backward": (c_i32, [c_void_p, c_void_p, c_i64, c_i32, c_f32, c_void_p,
                                       c_void_p]),

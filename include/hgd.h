@@ -183,6 +183,21 @@ hgd_status hgd_dense_threshold_fill(const float* H, int64_t n_rows, int64_t n_co
                                     void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * Evaluation (GraphRecommender.test, base/graph_recommender.py:61-92).
+ *   hgd_mask_scores: scores[r, cols[rowptr[m]:rowptr[m+1]]] = value, m = row_map ? row_map[r] : r
+ *                    (rated items → -10e8, :79-80).
+ *   hgd_topk_rows:   per row, the K entries find_k_largest (util/algorithm.py:143-173) returns —
+ *                    first K of {(c_j, j): j < K} ∪ {(c_i, i)} by score desc, seed first, index
+ *                    asc (so top items among the first K appear twice, as in the reference).
+ *                    1 <= k <= 256, n_cols >= k; out_ids int32 [n_rows, k], out_scores fp32.
+ * ---------------------------------------------------------------------------------------- */
+hgd_status hgd_mask_scores(float* scores, int64_t n_rows, int64_t ld, const int64_t* rowptr,
+                           const int32_t* cols, const int32_t* row_map, float value,
+                           void* stream);
+hgd_status hgd_topk_rows(const float* scores, int64_t n_rows, int64_t n_cols, int64_t ld,
+                         int32_t k, int32_t* out_ids, float* out_scores, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Elementwise epilogues around the hops (contiguous fp32, 16-byte aligned).
  *   apply:    y = epi(z)                                   (nn.LeakyReLU / nn.ReLU forward)
  *   backward: dz = dy * (ref > 0 ? 1 : slope) for LEAKY, dy * (ref > 0) for RELU, where ref is

@@ -339,3 +339,57 @@ def synthetic_incidence(n_users, n_items, nnz, seed=0, zipf=None):
         i = rng.choice(n_items, size=nnz, p=p).astype(np.int64)
     key = np.unique(u * n_items + i)
     return key // n_items, key % n_items
+
+
+# ---------------------------------------------------------------------------------------------
+# Evaluation top-K — base/graph_recommender.py:61-92, util/algorithm.py:143-173
+# ---------------------------------------------------------------------------------------------
+def find_k_largest(K, candidates):
+    """Literal restatement of the numba find_k_largest (util/algorithm.py:143-173), including
+    its re-scan of the first K candidates (so a top item among them is listed twice)."""
+    cand = list(candidates)
+    n = [(iid, s) for iid, s in enumerate(cand[:K])]
+    n.sort(key=lambda d: d[1], reverse=True)
+    scores = [x[1] for x in n]
+    ids = [x[0] for x in n]
+    for iid, score in enumerate(cand):
+        ind = K
+        l, r = 0, K - 1
+        if scores[r] < score:
+            while r >= l:
+                mid = int((r - l) / 2) + l
+                if scores[mid] >= score:
+                    l = mid + 1
+                elif scores[mid] < score:
+                    r = mid - 1
+                if r < l:
+                    ind = r
+                    break
+        if ind < K - 2:
+            scores[ind + 2:] = scores[ind + 1:-1]
+            ids[ind + 2:] = ids[ind + 1:-1]
+        if ind < K - 1:
+            scores[ind + 1] = score
+            ids[ind + 1] = iid
+    return ids, scores
+
+
+def topk_closed_form(K, candidates):
+    """The same result as :func:`find_k_largest`: the first K of {(c_j, j): j < K} (seed) ∪
+    {(c_i, i)} ordered by score desc, seed first, index asc (vectorised, for large rows)."""
+    c = np.asarray(candidates)
+    n = len(c)
+    sc = np.concatenate([c[:K], c])
+    seed = np.concatenate([np.ones(K, np.int64), np.zeros(n, np.int64)])
+    idx = np.concatenate([np.arange(K), np.arange(n)])
+    order = np.lexsort((idx, -seed, -sc.astype(np.float64)))[:K]
+    return idx[order].tolist(), sc[order].tolist()
+
+
+def masked_scores(user_emb, item_emb, users, rated, mask_value=-10e8):
+    """score = user_emb[u]·item_embᵀ with every rated item set to -10e8
+    (GraphRecommender.test, base/graph_recommender.py:73-80); float64 scores."""
+    S = np.asarray(user_emb, np.float64)[users] @ np.asarray(item_emb, np.float64).T
+    for r, u in enumerate(users):
+        S[r, list(rated[u])] = mask_value
+    return S

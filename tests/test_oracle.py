@@ -139,3 +139,23 @@ def test_synthetic_generator_dedup_sorted(zipf):
     key = r * 200 + c
     assert np.all(np.diff(key) > 0)
     assert r.max() < 1000 and c.max() < 200
+
+
+@pytest.mark.parametrize("K", [1, 3, 10, 40])
+def test_find_k_largest_closed_form(K):
+    """The literal find_k_largest equals the closed form (seed ∪ stream ordering), incl. ties
+    and the duplicated first-K entries."""
+    rng = np.random.default_rng(K)
+    for trial in range(30):
+        n = int(rng.integers(K, 200))
+        c = rng.integers(-5, 6, size=n).astype(np.float32)  # heavy ties
+        if trial % 3 == 0:
+            c[: min(K, n)] += 10  # top items inside the seed window → duplicates
+        ids, sc = O.find_k_largest(K, c)
+        ids2, sc2 = O.topk_closed_form(K, c)
+        assert ids == ids2 and np.allclose(sc, sc2), (trial, ids, ids2)
+
+
+def test_find_k_largest_duplicates_seed_items():
+    ids, sc = O.find_k_largest(3, np.array([5.0, 4.0, 3.0, 10.0, 1.0]))
+    assert ids == [3, 0, 0] and sc == [10.0, 5.0, 5.0]
