@@ -80,10 +80,10 @@ _SIGNATURES = {
                                        c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                        c_void_p, c_void_p, c_size, c_void_p]),
     "hgd_dense_threshold_workspace_size": (c_size, [c_i64]),
-    "hgd_dense_threshold_rowptr": (c_i32, [c_void_p, c_i64, c_i64, c_i64, c_f32, c_void_p,
-                                           c_void_p, c_size, c_void_p]),
-    "hgd_dense_threshold_fill": (c_i32, [c_void_p, c_i64, c_i64, c_i64, c_f32, c_void_p,
-                                         c_void_p, c_void_p]),
+    "hgd_dense_threshold_rowptr": (c_i32, [c_void_p, c_i64, c_i64, c_i64, c_f32, c_i32,
+                                           c_void_p, c_void_p, c_size, c_void_p]),
+    "hgd_dense_threshold_fill": (c_i32, [c_void_p, c_i64, c_i64, c_i64, c_f32, c_i32, c_void_p,
+                                         c_void_p, c_void_p, c_void_p]),
     "hgd_mask_scores": (c_i32, [c_void_p, c_i64, c_i64, c_void_p, c_void_p, c_void_p, c_f32,
                                 c_void_p]),
     "hgd_topk_rows": (c_i32, [c_void_p, c_i64, c_i64, c_i64, c_i32, c_void_p, c_void_p,

@@ -267,9 +267,16 @@ __global__ void k_compact_orientation(const int64_t* __restrict__ rowptr, int64_
   if (val && val_out) val_out[p] = __fdiv_rn(val[e], keep);
 }
 
-// One wavefront per row: number of entries > thresh.
+// HGD_DENSE_GREATER: v > thresh (torch.nonzero(H > thresh)); HGD_DENSE_NONZERO: v != 0
+// (torch.nonzero(H), the pattern of a dense adjacency such as DHCF's, DHCF.py:140).
+__device__ __forceinline__ bool dense_keep(float v, float thresh, int mode) {
+  return mode == HGD_DENSE_NONZERO ? v != 0.f : v > thresh;
+}
+
+// One wavefront per row: number of kept entries.
 __global__ void k_dense_count(const float* __restrict__ H, int64_t n_rows, int64_t n_cols,
-                              int64_t ld, float thresh, int64_t* __restrict__ counts) {
+                              int64_t ld, float thresh, int mode,
+                              int64_t* __restrict__ counts) {
   const int64_t r = static_cast<int64_t>(blockIdx.x) * (kBlock / 64) + threadIdx.x / 64;
   const int lane = threadIdx.x & 63;
   if (r > n_rows) return;
@@ -278,7 +285,7 @@ __global__ void k_dense_count(const float* __restrict__ H, int64_t n_rows, int64
     const float* row = H + r * ld;
     for (int64_t c0 = 0; c0 < n_cols; c0 += 64) {
       const int64_t c = c0 + lane;
-      const bool f = c < n_cols && row[c] > thresh;
+      const bool f = c < n_cols && dense_keep(row[c], thresh, mode);
       cnt += __popcll(__ballot(f));
     }
   }
@@ -286,8 +293,9 @@ __global__ void k_dense_count(const float* __restrict__ H, int64_t n_rows, int64
 }
 
 __global__ void k_dense_fill(const float* __restrict__ H, int64_t n_rows, int64_t n_cols,
-                             int64_t ld, float thresh, const int64_t* __restrict__ rowptr,
-                             int32_t* __restrict__ cols) {
+                             int64_t ld, float thresh, int mode,
+                             const int64_t* __restrict__ rowptr, int32_t* __restrict__ cols,
+                             float* __restrict__ vals) {
   const int64_t r = static_cast<int64_t>(blockIdx.x) * (kBlock / 64) + threadIdx.x / 64;
   const int lane = threadIdx.x & 63;
   if (r >= n_rows) return;
@@ -296,9 +304,14 @@ __global__ void k_dense_fill(const float* __restrict__ H, int64_t n_rows, int64_
   const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   for (int64_t c0 = 0; c0 < n_cols; c0 += 64) {
     const int64_t c = c0 + lane;
-    const bool f = c < n_cols && row[c] > thresh;
+    const float v = c < n_cols ? row[c] : 0.f;
+    const bool f = c < n_cols && dense_keep(v, thresh, mode);
     const unsigned long long b = __ballot(f);
-    if (f) cols[p + __popcll(b & lt_mask)] = static_cast<int32_t>(c);
+    if (f) {
+      const int64_t q = p + __popcll(b & lt_mask);
+      cols[q] = static_cast<int32_t>(c);
+      if (vals) vals[q] = v;
+    }
     p += __popcll(b);
   }
 }
@@ -609,12 +622,14 @@ extern "C" size_t hgd_dense_threshold_workspace_size(int64_t n_rows) {
 }
 
 extern "C" hgd_status hgd_dense_threshold_rowptr(const float* H, int64_t n_rows, int64_t n_cols,
-                                                 int64_t ld, float thresh, int64_t* rowptr,
-                                                 void* workspace, size_t workspace_bytes,
-                                                 void* stream) {
+                                                 int64_t ld, float thresh, int32_t mode,
+                                                 int64_t* rowptr, void* workspace,
+                                                 size_t workspace_bytes, void* stream) {
   clear_error();
   HGD_REQUIRE(n_rows >= 0 && n_cols >= 0 && (ld >= n_cols || n_rows == 0),
               "hgd_dense_threshold_rowptr: sizes");
+  HGD_REQUIRE(mode == HGD_DENSE_GREATER || mode == HGD_DENSE_NONZERO,
+              "hgd_dense_threshold_rowptr: bad mode %d", mode);
   HGD_REQUIRE(rowptr && (H || n_rows == 0 || n_cols == 0), "hgd_dense_threshold_rowptr: null");
   const size_t need = hgd_dense_threshold_workspace_size(n_rows);
   if (workspace_bytes < need || !workspace)
@@ -625,7 +640,7 @@ extern "C" hgd_status hgd_dense_threshold_rowptr(const float* H, int64_t n_rows,
   char* ws = static_cast<char*>(workspace);
   int64_t* counts = reinterpret_cast<int64_t*>(ws);
   hipLaunchKernelGGL(k_dense_count, dim3(grid_for(n_rows + 1, kBlock / 64)), dim3(kBlock), 0, st,
-                     H, n_rows, n_cols, ld, thresh, counts);
+                     H, n_rows, n_cols, ld, thresh, mode, counts);
   hgd_status s = check_launch("hgd_dense_threshold_rowptr count");
   if (s != HGD_OK) return s;
   size_t b = workspace_bytes - arr;
@@ -634,14 +649,17 @@ extern "C" hgd_status hgd_dense_threshold_rowptr(const float* H, int64_t n_rows,
 }
 
 extern "C" hgd_status hgd_dense_threshold_fill(const float* H, int64_t n_rows, int64_t n_cols,
-                                               int64_t ld, float thresh, const int64_t* rowptr,
-                                               int32_t* cols, void* stream) {
+                                               int64_t ld, float thresh, int32_t mode,
+                                               const int64_t* rowptr, int32_t* cols, float* vals,
+                                               void* stream) {
   clear_error();
   HGD_REQUIRE(n_rows >= 0 && n_cols >= 0 && (ld >= n_cols || n_rows == 0),
               "hgd_dense_threshold_fill: sizes");
+  HGD_REQUIRE(mode == HGD_DENSE_GREATER || mode == HGD_DENSE_NONZERO,
+              "hgd_dense_threshold_fill: bad mode %d", mode);
   if (n_rows == 0 || n_cols == 0) return HGD_OK;
   HGD_REQUIRE(H && rowptr && cols, "hgd_dense_threshold_fill: null pointer");
   hipLaunchKernelGGL(k_dense_fill, dim3(grid_for(n_rows, kBlock / 64)), dim3(kBlock), 0,
-                     as_stream(stream), H, n_rows, n_cols, ld, thresh, rowptr, cols);
+                     as_stream(stream), H, n_rows, n_cols, ld, thresh, mode, rowptr, cols, vals);
   return check_launch("hgd_dense_threshold_fill");
 }

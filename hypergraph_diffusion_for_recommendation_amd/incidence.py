@@ -378,6 +378,19 @@ class Incidence:
         return out
 
     @classmethod
+    def from_dense(cls, A: torch.Tensor, device=None, **kw) -> "Incidence":
+        """The nonzero pattern and values of a dense matrix (``torch.nonzero(A)`` order), e.g.
+        DHCF's dense interaction matrix fed to HGCNConv (DHCF.py:140, :131-133)."""
+        device = torch.device(device) if device is not None else (
+            A.device if A.device.type == "cuda" else torch.device("cuda"))
+        A = A.to(device=device, dtype=torch.float32)
+        rowptr, cols, vals = dense_threshold(A, 0.0, nonzero=True, values=True)
+        rows = expand_rows(rowptr, cols.numel())
+        inc = cls._from_sorted(rows, cols, vals, A.shape[0], A.shape[1], **kw)
+        inc.coo_sorted = True
+        return inc
+
+    @classmethod
     def from_torch_sparse(cls, adj: torch.Tensor, device=None, **kw) -> "Incidence":
         """From a torch sparse COO tensor as built by ``convert_sparse_mat_to_tensor``."""
         if adj.layout != torch.sparse_coo:
@@ -499,10 +512,11 @@ def drop_edges(indices: torch.Tensor, values: torch.Tensor, mask: torch.Tensor,
     return out_idx, out_val
 
 
-def dense_threshold(H: torch.Tensor, thresh: float = 0.0):
-    """``torch.nonzero(H > thresh)`` of a dense 2-D fp32 device matrix as CSR
-    (rowptr int64 [n+1], cols int32 [nnz]) in row-major order
-    (EquivSetGNN.generate_V_E, model/layers/layers2/EquivSetGNN2.py:105-133)."""
+def dense_threshold(H: torch.Tensor, thresh: float = 0.0, nonzero: bool = False,
+                    values: bool = False):
+    """``torch.nonzero(H > thresh)`` (or ``torch.nonzero(H)`` with ``nonzero=True``) of a dense
+    2-D fp32 device matrix as CSR (rowptr int64 [n+1], cols int32 [nnz][, values fp32]) in
+    row-major order (EquivSetGNN.generate_V_E, model/layers/layers2/EquivSetGNN2.py:105-133)."""
     if H.dim() != 2 or H.dtype != torch.float32:
         raise TypeError("dense_threshold: expects a 2-D float32 matrix")
     if H.stride(1) != 1:
@@ -511,17 +525,21 @@ def dense_threshold(H: torch.Tensor, thresh: float = 0.0):
     lib = nat.load()
     st = _stream(device)
     n, k = H.shape
+    mode = 1 if nonzero else 0
     rowptr = torch.empty(n + 1, dtype=torch.int64, device=device)
     ws = _ws(lib.hgd_dense_threshold_workspace_size(n), device)
     nat.check(lib.hgd_dense_threshold_rowptr(H.data_ptr(), n, k, H.stride(0), float(thresh),
-                                             rowptr.data_ptr(), ws.data_ptr(), ws.numel(), st),
-              "hgd_dense_threshold_rowptr")
+                                             mode, rowptr.data_ptr(), ws.data_ptr(), ws.numel(),
+                                             st), "hgd_dense_threshold_rowptr")
     nnz = int(rowptr[n].item())
     cols = torch.empty(nnz, dtype=torch.int32, device=device)
+    vals = torch.empty(nnz, dtype=torch.float32, device=device) if values else None
     if nnz:
         nat.check(lib.hgd_dense_threshold_fill(H.data_ptr(), n, k, H.stride(0), float(thresh),
-                                               rowptr.data_ptr(), cols.data_ptr(), st),
-                  "hgd_dense_threshold_fill")
+                                               mode, rowptr.data_ptr(), cols.data_ptr(),
+                                               nat.ptr(vals), st), "hgd_dense_threshold_fill")
+    if values:
+        return rowptr, cols, vals
     return rowptr, cols
 
 
@@ -551,7 +569,12 @@ def incidence_of(adj, cache: bool = True) -> Incidence:
         return adj
     inc = getattr(adj, "_hgd_incidence", None) if cache else None
     if inc is None:
-        inc = Incidence.from_torch_sparse(adj)
+        if adj.layout == torch.sparse_coo:
+            inc = Incidence.from_torch_sparse(adj)
+        elif adj.layout == torch.strided and adj.dim() == 2:
+            inc = Incidence.from_dense(adj)  # the pattern of a dense adjacency (DHCF)
+        else:
+            raise TypeError(f"incidence_of: unsupported adjacency layout {adj.layout}")
         if cache:
             try:
                 adj._hgd_incidence = inc

@@ -172,15 +172,19 @@ hgd_status hgd_dropedge_structure(const int64_t* rowptr, const int32_t* col, con
                                   int64_t* colptr_out, int32_t* row_t_out, float* val_t_out,
                                   void* workspace, size_t workspace_bytes, void* stream);
 
-/* torch.nonzero(H > thresh) of a dense row-major [n_rows, n_cols] fp32 matrix (leading dim ld),
- * in two passes: rowptr (n_rows+1, int64) then the column list (rowptr[n_rows] int32 entries). */
+/* torch.nonzero(H > thresh) (mode HGD_DENSE_GREATER) or torch.nonzero(H) (HGD_DENSE_NONZERO)
+ * of a dense row-major [n_rows, n_cols] fp32 matrix (leading dim ld), in two passes: rowptr
+ * (n_rows+1, int64), then the column list (rowptr[n_rows] int32 entries) and, if vals != NULL,
+ * the kept values in the same order. */
+#define HGD_DENSE_GREATER 0
+#define HGD_DENSE_NONZERO 1
 size_t hgd_dense_threshold_workspace_size(int64_t n_rows);
 hgd_status hgd_dense_threshold_rowptr(const float* H, int64_t n_rows, int64_t n_cols, int64_t ld,
-                                      float thresh, int64_t* rowptr, void* workspace,
-                                      size_t workspace_bytes, void* stream);
+                                      float thresh, int32_t mode, int64_t* rowptr,
+                                      void* workspace, size_t workspace_bytes, void* stream);
 hgd_status hgd_dense_threshold_fill(const float* H, int64_t n_rows, int64_t n_cols, int64_t ld,
-                                    float thresh, const int64_t* rowptr, int32_t* cols,
-                                    void* stream);
+                                    float thresh, int32_t mode, const int64_t* rowptr,
+                                    int32_t* cols, float* vals, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Evaluation (GraphRecommender.test, base/graph_recommender.py:61-92).
