@@ -45,6 +45,29 @@ class SplitPlan(ctypes.Structure):
     ]
 
 
+class RowEpilogue(ctypes.Structure):
+    """Mirror of ``hgd_row_epilogue`` (include/hgd.h)."""
+
+    _fields_ = [
+        ("act", c_i32),
+        ("slope", c_f32),
+        ("layer_norm", c_i32),
+        ("ln_eps", c_f32),
+        ("ln_gamma", c_void_p),
+        ("ln_beta", c_void_p),
+        ("out_scale", c_f32),
+        ("res1", c_void_p),
+        ("ld_res1", c_i64),
+        ("res1_scale", c_f32),
+        ("res2", c_void_p),
+        ("ld_res2", c_i64),
+        ("res2_scale", c_f32),
+        ("act_out", c_void_p),
+        ("ld_act", c_i64),
+        ("stats", c_void_p),
+    ]
+
+
 # name -> (restype, argtypes); every symbol of include/hgd.h appears here.
 _SIGNATURES = {
     "hgd_version": (c_i32, []),
@@ -58,6 +81,15 @@ _SIGNATURES = {
     "hgd_spmm": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_i64, c_i64, c_i64,
                          c_void_p, c_i64, c_void_p, c_i64, c_i32, c_i32, c_f32,
                          ctypes.POINTER(SplitPlan), c_void_p, c_size, c_void_p]),
+    "hgd_spmm_fused": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_i64, c_i64,
+                               c_i64, c_void_p, c_i64, c_void_p, c_i64, c_i32,
+                               ctypes.POINTER(RowEpilogue), ctypes.POINTER(SplitPlan), c_void_p,
+                               c_size, c_void_p]),
+    "hgd_row_epilogue_backward_workspace_size": (c_size, [c_i64, c_i32]),
+    "hgd_row_epilogue_backward": (c_i32, [c_void_p, c_i64, c_void_p, c_i64, c_void_p, c_void_p,
+                                          c_i64, c_i32, c_i32, c_f32, c_i32, c_f32, c_void_p,
+                                          c_i64, c_void_p, c_void_p, c_void_p, c_size,
+                                          c_void_p]),
     "hgd_index_narrow": (c_i32, [c_void_p, c_i64, c_i64, c_void_p, c_void_p, c_void_p]),
     "hgd_sort_perm_workspace_size": (c_size, [c_i64]),
     "hgd_sort_perm": (c_i32, [c_void_p, c_i64, c_i64, c_void_p, c_void_p, c_void_p, c_size,

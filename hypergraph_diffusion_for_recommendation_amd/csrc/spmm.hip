@@ -43,12 +43,21 @@ struct SpmmArgs {
   const int64_t* heavy_cptr;
   float* partial;  // [n_chunks, d]
   int64_t heavy_blocks;
+  hgd_row_epilogue ex;  // used by the EX (hgd_spmm_fused) instantiations only
 };
 
 __device__ __forceinline__ float epilogue(float y, int epi, float slope) {
   if (epi == HGD_EPI_LEAKY_RELU) return y > 0.f ? y : y * slope;
   if (epi == HGD_EPI_RELU) return y > 0.f ? y : 0.f;
   return y;
+}
+
+// Sum of v over the G lanes of this lane group (xor butterfly; every lane gets the total).
+template <int G>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int m = G / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, G);
+  return v;
 }
 
 // Cache-policy bits of the tuned variants (hgd_set_tuning(HGD_TUNE_SPMM_POLICY, bits)):
@@ -86,6 +95,61 @@ __device__ __forceinline__ void store_vec(float* p, const float (&v)[VEC]) {
 #pragma unroll
     for (int i = 0; i < VEC; ++i) p[i] = v[i];
   }
+}
+
+// Scale, epilogue and store of one finished row r (all G lanes of the group call it together).
+// With EX the hgd_row_epilogue runs in registers: the group holds the whole row (single column
+// pass, checked on the host), so the LayerNorm statistics are two group_sum butterflies.
+template <int G, int VEC, bool EX, bool NT_STORE>
+__device__ __forceinline__ void finish_row(const SpmmArgs& a, int64_t r, float s, int l,
+                                           int64_t coff, bool col_ok, float (&acc)[VEC]) {
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) acc[i] = epilogue(acc[i] * s, a.epi, a.slope);
+  if constexpr (EX) {
+    const hgd_row_epilogue& e = a.ex;
+    if (e.act_out && col_ok) store_vec<VEC>(e.act_out + r * e.ld_act + coff, acc);
+    if (e.layer_norm) {
+      float t = 0.f;
+      if (col_ok) {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) t += acc[i];
+      }
+      const float mu = group_sum<G>(t) / static_cast<float>(a.d);
+      t = 0.f;
+      if (col_ok) {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) t += (acc[i] - mu) * (acc[i] - mu);
+      }
+      const float rstd = 1.f / sqrtf(group_sum<G>(t) / static_cast<float>(a.d) + e.ln_eps);
+      if (e.stats && l == 0) {
+        e.stats[2 * r] = mu;
+        e.stats[2 * r + 1] = rstd;
+      }
+      if (col_ok) {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+          const float gm = e.ln_gamma ? e.ln_gamma[coff + i] : 1.f;
+          const float bt = e.ln_beta ? e.ln_beta[coff + i] : 0.f;
+          acc[i] = fmaf((acc[i] - mu) * rstd, gm, bt);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) acc[i] *= e.out_scale;
+    if (e.res1 && col_ok) {
+      float rv[VEC];
+      load_vec<VEC>(e.res1 + r * e.ld_res1 + coff, rv);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) acc[i] = fmaf(e.res1_scale, rv[i], acc[i]);
+    }
+    if (e.res2 && col_ok) {
+      float rv[VEC];
+      load_vec<VEC>(e.res2 + r * e.ld_res2 + coff, rv);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) acc[i] = fmaf(e.res2_scale, rv[i], acc[i]);
+    }
+  }
+  if (col_ok) store_vec<VEC, NT_STORE>(a.Y + r * a.ldy + coff, acc);
 }
 
 // Lane l's share of a batch of G column indices (and weights) starting at nonzero eb.
@@ -168,7 +232,7 @@ __device__ __forceinline__ void gather_sum(const SpmmArgs& a, int64_t e0, int64_
   }
 }
 
-template <int G, int VEC, int U, bool HAS_VAL, int POL>
+template <int G, int VEC, int U, bool HAS_VAL, int POL, bool EX>
 __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
   constexpr int GPB = kBlock / G;
   const int g = threadIdx.x / G;
@@ -200,9 +264,7 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
   if (a.heavy_threshold > 0 && e1 - e0 > a.heavy_threshold) return;  // split-plan row
   gather_sum<G, VEC, U, HAS_VAL, POL>(a, e0, e1, l, col_ok, acc);
   const float s = a.row_scale ? a.row_scale[r] : 1.f;
-#pragma unroll
-  for (int i = 0; i < VEC; ++i) acc[i] = epilogue(acc[i] * s, a.epi, a.slope);
-  if (col_ok) store_vec<VEC, (POL & kPolNtStore) != 0>(a.Y + r * a.ldy + coff, acc);
+  finish_row<G, VEC, EX, (POL & kPolNtStore) != 0>(a, r, s, l, coff, col_ok, acc);
 }
 
 // Segmented variant for short rows (hgd_split_plan.flags & HGD_PLAN_SEGMENTED): a group owns
@@ -210,7 +272,7 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
 // batches of G indices, so every gather batch is full whatever the row lengths, the row pointers
 // and row scales of all G rows arrive in one coalesced load, and the accumulator is flushed
 // (scale, epilogue, store) at each row boundary. Sums stay in edge order per row.
-template <int G, int VEC, int U, bool HAS_VAL, int POL>
+template <int G, int VEC, int U, bool HAS_VAL, int POL, bool EX>
 __global__ __launch_bounds__(kBlock) void spmm_seg_kernel(SpmmArgs a) {
   constexpr int GPB = kBlock / G;
   const int g = threadIdx.x / G;
@@ -239,10 +301,10 @@ __global__ __launch_bounds__(kBlock) void spmm_seg_kernel(SpmmArgs a) {
     float y[VEC];
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
-      y[i] = epilogue(acc[i] * s, a.epi, a.slope);
+      y[i] = acc[i];
       acc[i] = 0.f;
     }
-    if (col_ok) store_vec<VEC, (POL & kPolNtStore) != 0>(a.Y + (r0 + cur) * a.ldy + coff, y);
+    finish_row<G, VEC, EX, (POL & kPolNtStore) != 0>(a, r0 + cur, s, l, coff, col_ok, y);
     ++cur;
     const int64_t nb = __shfl(my_end, cur < nr ? cur : 0, G);
     next_b = cur < nr ? nb : INT64_MAX;
@@ -311,7 +373,7 @@ __global__ __launch_bounds__(kBlock) void spmm_seg_kernel(SpmmArgs a) {
 // GPB group sums in group order. The combine order is fixed by (chunk count, GPB), so the result
 // is deterministic run to run; a popular item with ~10^4 chunks is reduced by GPB·FU loads in
 // flight instead of one serial chain.
-template <int G, int VEC>
+template <int G, int VEC, bool EX>
 __global__ __launch_bounds__(kBlock) void spmm_fixup_kernel(SpmmArgs a) {
   constexpr int GPB = kBlock / G;
   constexpr int FU = 4;
@@ -347,16 +409,14 @@ __global__ __launch_bounds__(kBlock) void spmm_fixup_kernel(SpmmArgs a) {
 #pragma unroll
   for (int i = 0; i < VEC; ++i) s_acc[g][l * VEC + i] = acc[i];
   __syncthreads();
-  if (g != 0 || !col_ok) return;
+  if (g != 0) return;  // group 0 (all of its lanes: finish_row reduces over the group)
 #pragma unroll
   for (int i = 0; i < VEC; ++i) acc[i] = s_acc[0][l * VEC + i];
   for (int k = 1; k < GPB; ++k)
 #pragma unroll
     for (int i = 0; i < VEC; ++i) acc[i] += s_acc[k][l * VEC + i];
   const float s = a.row_scale ? a.row_scale[r] : 1.f;
-#pragma unroll
-  for (int i = 0; i < VEC; ++i) acc[i] = epilogue(acc[i] * s, a.epi, a.slope);
-  store_vec<VEC>(a.Y + r * a.ldy + coff, acc);
+  finish_row<G, VEC, EX, false>(a, r, s, l, coff, col_ok, acc);
 }
 
 namespace {
@@ -366,28 +426,32 @@ constexpr int kDefaultPolicy = kPolPrefetch;
 int g_unroll = 8;
 int g_policy = kDefaultPolicy;
 
-template <int G, int VEC, int U, int POL>
+template <int G, int VEC, int U, int POL, bool EX = false>
 void launch_kernel(const SpmmArgs& a, bool has_val, bool seg, int64_t blocks, hipStream_t st) {
   if constexpr (G >= 8) {
     if (seg) {
       if (has_val)
-        hipLaunchKernelGGL((spmm_seg_kernel<G, VEC, U, true, POL>), dim3(blocks), dim3(kBlock),
-                           0, st, a);
+        hipLaunchKernelGGL((spmm_seg_kernel<G, VEC, U, true, POL, EX>), dim3(blocks),
+                           dim3(kBlock), 0, st, a);
       else
-        hipLaunchKernelGGL((spmm_seg_kernel<G, VEC, U, false, POL>), dim3(blocks), dim3(kBlock),
-                           0, st, a);
+        hipLaunchKernelGGL((spmm_seg_kernel<G, VEC, U, false, POL, EX>), dim3(blocks),
+                           dim3(kBlock), 0, st, a);
       return;
     }
   }
   if (has_val)
-    hipLaunchKernelGGL((spmm_kernel<G, VEC, U, true, POL>), dim3(blocks), dim3(kBlock), 0, st, a);
+    hipLaunchKernelGGL((spmm_kernel<G, VEC, U, true, POL, EX>), dim3(blocks), dim3(kBlock), 0,
+                       st, a);
   else
-    hipLaunchKernelGGL((spmm_kernel<G, VEC, U, false, POL>), dim3(blocks), dim3(kBlock), 0, st, a);
+    hipLaunchKernelGGL((spmm_kernel<G, VEC, U, false, POL, EX>), dim3(blocks), dim3(kBlock), 0,
+                       st, a);
 }
 
-template <int G, int VEC>
+template <int G, int VEC, bool EX>
 void launch_tuned(const SpmmArgs& a, bool has_val, bool seg, int64_t blocks, hipStream_t st) {
-  if constexpr (G == 16 && VEC == 4) {
+  if constexpr (EX) {
+    launch_kernel<G, VEC, 8, kDefaultPolicy, true>(a, has_val, seg, blocks, st);
+  } else if constexpr (G == 16 && VEC == 4) {
     // the d = 64 path carries the tuning matrix (unroll × {plain, nt-store, prefetch, both})
 #define HGD_POL_CASES(U)                                                            \
     switch (g_policy) {                                                             \
@@ -404,7 +468,7 @@ void launch_tuned(const SpmmArgs& a, bool has_val, bool seg, int64_t blocks, hip
   }
 }
 
-template <int G, int VEC>
+template <int G, int VEC, bool EX>
 hgd_status launch_g(SpmmArgs a, bool has_val, hipStream_t st) {
   constexpr int GPB = kBlock / G;
   const int64_t rows = a.row_end - a.row_begin;
@@ -413,7 +477,7 @@ hgd_status launch_g(SpmmArgs a, bool has_val, hipStream_t st) {
       const int64_t sblocks = (rows + static_cast<int64_t>(GPB) * G - 1) / (GPB * G);
       if (sblocks <= 0) return HGD_OK;
       if (sblocks > 0x7fffffffLL) return fail(HGD_ERR_UNSUPPORTED, "hgd_spmm: grid too large");
-      launch_tuned<G, VEC>(a, has_val, true, sblocks, st);
+      launch_tuned<G, VEC, EX>(a, has_val, true, sblocks, st);
       return check_launch("hgd_spmm segmented kernel");
     }
   }
@@ -422,28 +486,29 @@ hgd_status launch_g(SpmmArgs a, bool has_val, hipStream_t st) {
   const int64_t blocks = light_blocks + a.heavy_blocks;
   if (blocks > 0) {
     if (blocks > 0x7fffffffLL) return fail(HGD_ERR_UNSUPPORTED, "hgd_spmm: grid too large");
-    launch_tuned<G, VEC>(a, has_val, false, blocks, st);
+    launch_tuned<G, VEC, EX>(a, has_val, false, blocks, st);
     hgd_status s = check_launch("hgd_spmm kernel");
     if (s != HGD_OK) return s;
   }
   if (a.n_heavy > 0) {
     if (a.n_heavy > 0x7fffffffLL) return fail(HGD_ERR_UNSUPPORTED, "hgd_spmm: too many split rows");
-    hipLaunchKernelGGL((spmm_fixup_kernel<G, VEC>), dim3(a.n_heavy), dim3(kBlock), 0, st, a);
+    hipLaunchKernelGGL((spmm_fixup_kernel<G, VEC, EX>), dim3(a.n_heavy), dim3(kBlock), 0, st,
+                       a);
     return check_launch("hgd_spmm fixup");
   }
   return HGD_OK;
 }
 
-template <int VEC>
+template <int VEC, bool EX = false>
 hgd_status launch_vec(int G, const SpmmArgs& a, bool has_val, hipStream_t st) {
   switch (G) {
-    case 1: return launch_g<1, VEC>(a, has_val, st);
-    case 2: return launch_g<2, VEC>(a, has_val, st);
-    case 4: return launch_g<4, VEC>(a, has_val, st);
-    case 8: return launch_g<8, VEC>(a, has_val, st);
-    case 16: return launch_g<16, VEC>(a, has_val, st);
-    case 32: return launch_g<32, VEC>(a, has_val, st);
-    case 64: return launch_g<64, VEC>(a, has_val, st);
+    case 1: return launch_g<1, VEC, EX>(a, has_val, st);
+    case 2: return launch_g<2, VEC, EX>(a, has_val, st);
+    case 4: return launch_g<4, VEC, EX>(a, has_val, st);
+    case 8: return launch_g<8, VEC, EX>(a, has_val, st);
+    case 16: return launch_g<16, VEC, EX>(a, has_val, st);
+    case 32: return launch_g<32, VEC, EX>(a, has_val, st);
+    case 64: return launch_g<64, VEC, EX>(a, has_val, st);
     default: return fail(HGD_ERR_UNSUPPORTED, "hgd_spmm: unsupported group size %d", G);
   }
 }
@@ -462,26 +527,35 @@ extern "C" size_t hgd_spmm_workspace_size(const hgd_split_plan* plan, int32_t d)
   return hgd::align_up(static_cast<size_t>(plan->n_chunks) * static_cast<size_t>(d) * 4);
 }
 
-extern "C" hgd_status hgd_spmm(const int64_t* rowptr, const int32_t* col, const float* val,
-                               const float* row_scale, int64_t n_rows, int64_t n_src_rows,
-                               int64_t row_begin, int64_t row_end, const float* X, int64_t ldx,
-                               float* Y, int64_t ldy, int32_t d, int32_t epilogue, float slope,
-                               const hgd_split_plan* plan, void* workspace,
-                               size_t workspace_bytes, void* stream) {
-  using namespace hgd;
-  clear_error();
-  HGD_REQUIRE(d > 0, "hgd_spmm: d must be > 0 (got %d)", d);
-  HGD_REQUIRE(n_rows >= 0 && n_src_rows >= 0, "hgd_spmm: negative sizes");
+namespace hgd {
+namespace {
+
+hgd_status spmm_impl(const int64_t* rowptr, const int32_t* col, const float* val,
+                     const float* row_scale, int64_t n_rows, int64_t n_src_rows, int64_t row_begin,
+                     int64_t row_end, const float* X, int64_t ldx, float* Y, int64_t ldy,
+                     int32_t d, int32_t epilogue, float slope, const hgd_row_epilogue* ex,
+                     const hgd_split_plan* plan, void* workspace, size_t workspace_bytes,
+                     void* stream, const char* fn) {
+  HGD_REQUIRE(d > 0, "%s: d must be > 0 (got %d)", fn, d);
+  HGD_REQUIRE(n_rows >= 0 && n_src_rows >= 0, "%s: negative sizes", fn);
   HGD_REQUIRE(row_begin >= 0 && row_begin <= row_end && row_end <= n_rows,
-              "hgd_spmm: row range [%lld,%lld) outside [0,%lld)", (long long)row_begin,
+              "%s: row range [%lld,%lld) outside [0,%lld)", fn, (long long)row_begin,
               (long long)row_end, (long long)n_rows);
-  HGD_REQUIRE(ldx >= d && ldy >= d, "hgd_spmm: ldx/ldy must be >= d");
-  HGD_REQUIRE(epilogue >= HGD_EPI_NONE && epilogue <= HGD_EPI_RELU, "hgd_spmm: bad epilogue %d",
+  HGD_REQUIRE(ldx >= d && ldy >= d, "%s: ldx/ldy must be >= d", fn);
+  HGD_REQUIRE(epilogue >= HGD_EPI_NONE && epilogue <= HGD_EPI_RELU, "%s: bad epilogue %d", fn,
               epilogue);
+  if (ex) {
+    HGD_REQUIRE(epilogue == HGD_EPI_NONE || slope >= 0.f,
+                "%s: a fused activation needs slope >= 0 (got %g)", fn, (double)slope);
+    HGD_REQUIRE(ex->layer_norm == 0 || ex->layer_norm == 1, "%s: layer_norm must be 0/1", fn);
+    HGD_REQUIRE(!ex->res1 || ex->ld_res1 >= d, "%s: ld_res1 < d", fn);
+    HGD_REQUIRE(!ex->res2 || ex->ld_res2 >= d, "%s: ld_res2 < d", fn);
+    HGD_REQUIRE(!ex->act_out || ex->ld_act >= d, "%s: ld_act < d", fn);
+  }
   if (row_end == row_begin) return HGD_OK;
   // col / X may be NULL for a structure without nonzeros (never dereferenced then).
-  HGD_REQUIRE(rowptr && Y, "hgd_spmm: null rowptr/Y");
-  HGD_REQUIRE(X || n_src_rows == 0, "hgd_spmm: null X");
+  HGD_REQUIRE(rowptr && Y, "%s: null rowptr/Y", fn);
+  HGD_REQUIRE(X || n_src_rows == 0, "%s: null X", fn);
 
   SpmmArgs a{};
   a.rowptr = rowptr;
@@ -497,12 +571,13 @@ extern "C" hgd_status hgd_spmm(const int64_t* rowptr, const int32_t* col, const 
   a.d = d;
   a.epi = epilogue;
   a.slope = slope;
+  if (ex) a.ex = *ex;
   if (plan && plan->threshold > 0 && plan->n_heavy > 0) {
     HGD_REQUIRE(plan->chunk > 0 && plan->heavy_rows && plan->heavy_cptr && plan->chunk_heavy,
-                "hgd_spmm: incomplete split plan");
+                "%s: incomplete split plan", fn);
     const size_t need = hgd_spmm_workspace_size(plan, d);
     if (workspace_bytes < need || (need && !workspace))
-      return fail(HGD_ERR_WORKSPACE, "hgd_spmm: workspace %zu < required %zu", workspace_bytes,
+      return fail(HGD_ERR_WORKSPACE, "%s: workspace %zu < required %zu", fn, workspace_bytes,
                   need);
     a.heavy_threshold = plan->threshold;
     a.chunk = plan->chunk;
@@ -518,27 +593,65 @@ extern "C" hgd_status hgd_spmm(const int64_t* rowptr, const int32_t* col, const 
 
   hipStream_t st = as_stream(stream);
   const bool has_val = val != nullptr;
-  const bool aligned = (reinterpret_cast<uintptr_t>(X) % 16 == 0) &&
-                       (reinterpret_cast<uintptr_t>(Y) % 16 == 0) && (ldx % 4 == 0) &&
-                       (ldy % 4 == 0) && (d % 4 == 0);
+  auto al16 = [](const void* p, int64_t ld) {
+    return p == nullptr || (reinterpret_cast<uintptr_t>(p) % 16 == 0 && ld % 4 == 0);
+  };
+  bool aligned = al16(X, ldx) && al16(Y, ldy) && (d % 4 == 0);
+  if (ex)
+    aligned = aligned && al16(ex->res1, ex->ld_res1) && al16(ex->res2, ex->ld_res2) &&
+              al16(ex->act_out, ex->ld_act);
+  if (ex && ex->layer_norm && (aligned ? d > 256 : d > 64))
+    return fail(HGD_ERR_UNSUPPORTED,
+                "%s: layer_norm needs d <= 256 (16-byte aligned rows) or d <= 64 (got d=%d%s)",
+                fn, d, aligned ? "" : ", unaligned");
   if (aligned) {
     // float4 path: one pass when d/4 <= 64 lanes, else 256-column passes.
     const int lanes = d / 4;
     const int G = lanes >= 64 ? 64 : next_pow2(lanes);
     for (int c0 = 0; c0 < d; c0 += 4 * G) {
       a.col0 = c0;
-      hgd_status s = launch_vec<4>(G, a, has_val, st);
+      hgd_status s = ex ? launch_vec<4, true>(G, a, has_val, st)
+                        : launch_vec<4>(G, a, has_val, st);
       if (s != HGD_OK) return s;
     }
   } else {
     const int G = d >= 64 ? 64 : next_pow2(d);
     for (int c0 = 0; c0 < d; c0 += G) {
       a.col0 = c0;
-      hgd_status s = launch_vec<1>(G, a, has_val, st);
+      hgd_status s = ex ? launch_vec<1, true>(G, a, has_val, st)
+                        : launch_vec<1>(G, a, has_val, st);
       if (s != HGD_OK) return s;
     }
   }
   return HGD_OK;
+}
+
+}  // namespace
+}  // namespace hgd
+
+extern "C" hgd_status hgd_spmm(const int64_t* rowptr, const int32_t* col, const float* val,
+                               const float* row_scale, int64_t n_rows, int64_t n_src_rows,
+                               int64_t row_begin, int64_t row_end, const float* X, int64_t ldx,
+                               float* Y, int64_t ldy, int32_t d, int32_t epilogue, float slope,
+                               const hgd_split_plan* plan, void* workspace,
+                               size_t workspace_bytes, void* stream) {
+  hgd::clear_error();
+  return hgd::spmm_impl(rowptr, col, val, row_scale, n_rows, n_src_rows, row_begin, row_end, X,
+                        ldx, Y, ldy, d, epilogue, slope, nullptr, plan, workspace,
+                        workspace_bytes, stream, "hgd_spmm");
+}
+
+extern "C" hgd_status hgd_spmm_fused(const int64_t* rowptr, const int32_t* col, const float* val,
+                                     const float* row_scale, int64_t n_rows, int64_t n_src_rows,
+                                     int64_t row_begin, int64_t row_end, const float* X,
+                                     int64_t ldx, float* Y, int64_t ldy, int32_t d,
+                                     const hgd_row_epilogue* epi, const hgd_split_plan* plan,
+                                     void* workspace, size_t workspace_bytes, void* stream) {
+  hgd::clear_error();
+  HGD_REQUIRE(epi != nullptr, "hgd_spmm_fused: null epilogue descriptor");
+  return hgd::spmm_impl(rowptr, col, val, row_scale, n_rows, n_src_rows, row_begin, row_end, X,
+                        ldx, Y, ldy, d, epi->act, epi->slope, epi, plan, workspace,
+                        workspace_bytes, stream, "hgd_spmm_fused");
 }
 
 extern "C" hgd_status hgd_set_tuning(int32_t key, int32_t value) {

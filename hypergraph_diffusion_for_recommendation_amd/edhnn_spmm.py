@@ -10,8 +10,9 @@ aggregation steps are HGCNConv two-hops over ``norm_adj`` instead of scatter-mea
 * :class:`EquivSetGNN` — model/layers/EquivSetGNN.py:32-101: dropout → ReLU(lin_in) → x0 →
   [dropout → conv → act] × All_num_layers → dropout.
 
-Both two-hops run as fused hgd_spmm pairs with the LeakyReLU in the second hop's store
-(functional.two_hop); the LayerNorm / Linear / residual stay torch. The wavelet (HWNN) layers
+Both two-hops run as hgd_spmm pairs whose second store also applies the LeakyReLU, the LayerNorm,
+the residual and the restart blend (hgd_spmm_fused, functional.two_hop_fused; SURVEY.md §8f
+rank 1); only the Linear layers stay torch (rocBLAS). The wavelet (HWNN) layers
 the reference constructs but never calls are not built.
 """
 from __future__ import annotations
@@ -20,6 +21,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .functional import two_hop_fused
+from .incidence import incidence_of
 from .layers import MLP, HGCNConv
 
 
@@ -47,6 +50,7 @@ class EquivSetConv(nn.Module):
         self.hgcn_layers = nn.ModuleList([HGCNConv(leaky) for _ in range(2)])
         self.mean_pooling = nn.AdaptiveAvgPool1d(out_features)
         self.lns = nn.ModuleList([nn.LayerNorm(out_features) for _ in range(2)])
+        self.fused_epilogue = True  # False: the reference's separate LN / add / blend ops
 
     def reset_parameters(self):
         for m in (self.W1, self.W2, self.W):
@@ -55,15 +59,30 @@ class EquivSetConv(nn.Module):
 
     def forward(self, X, sparse_norm_adj, X0, *ui_adj, act=True):
         Xve = self.W1(X)
-        Xe = self.lns[0](self.hgcn_layers[0](sparse_norm_adj, Xve, act=True)) + Xve
+        fused = self.fused_epilogue and torch.is_tensor(X0) and tuple(X0.shape) == tuple(Xve.shape)
+        if fused:
+            inc = incidence_of(sparse_norm_adj)
+            slope0 = self.hgcn_layers[0].act.negative_slope
+            # Xe = LN0(leaky(A·(Aᵀ·Xve))) + Xve in one store
+            Xe = two_hop_fused(inc, Xve, epilogue="leaky_relu", slope=slope0, norm=self.lns[0],
+                               res1=Xve, res1_scale=1.0)
+        else:
+            Xe = self.lns[0](self.hgcn_layers[0](sparse_norm_adj, Xve, act=True)) + Xve
         if self.W2 is None:
             Xev = Xe  # W2 = X[..., in_features:] of cat([X, Xe])
         else:
             Xev = self.W2(torch.cat([X, Xe], -1))
         if Xev.shape[-1] != self.out_features:  # AdaptiveAvgPool1d is the identity otherwise
             Xev = self.mean_pooling(Xev)
-        X_v = self.lns[1](self.hgcn_layers[1](sparse_norm_adj, Xev, act=True)) + Xev
-        X = (1 - self.alpha) * X_v + self.alpha * X0
+        if fused and tuple(Xev.shape) == tuple(X0.shape):
+            slope1 = self.hgcn_layers[1].act.negative_slope
+            # (1-α)·(LN1(leaky(A·(Aᵀ·Xev))) + Xev) + α·X0 in one store
+            X = two_hop_fused(inc, Xev, epilogue="leaky_relu", slope=slope1, norm=self.lns[1],
+                              out_scale=1 - self.alpha, res1=Xev, res1_scale=1 - self.alpha,
+                              res2=X0, res2_scale=self.alpha)
+        else:
+            X_v = self.lns[1](self.hgcn_layers[1](sparse_norm_adj, Xev, act=True)) + Xev
+            X = (1 - self.alpha) * X_v + self.alpha * X0
         return self.W(X)
 
 

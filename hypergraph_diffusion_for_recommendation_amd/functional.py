@@ -135,3 +135,113 @@ def hgconv2(inc: Incidence, X: torch.Tensor) -> torch.Tensor:
 def mean2hop(inc: Incidence, X: torch.Tensor) -> torch.Tensor:
     """ED-HNN edge-mean then vertex-mean ``D_v^-1·B·D_e^-1·Bᵀ·X`` (EquivSetConv2.py:88-93)."""
     return two_hop(inc, X, P="mean", Q="mean", R=None)
+
+
+def _ln_supported(d: int) -> bool:
+    # hgd_spmm_fused / hgd_row_epilogue_backward keep a whole row in one lane group
+    return d <= 256 if d % 4 == 0 else d <= 64
+
+
+class _FusedTwoHop(torch.autograd.Function):
+    """``Y = out_scale·LN(epi(P·A·Q·Aᵀ·R·X)) + s1·res1 + s2·res2`` — the second hop's store runs
+    the activation, LayerNorm and residual blend (hgd_spmm_fused); the backward runs their
+    gradient in one pass (hgd_row_epilogue_backward) before the two backward hops."""
+
+    @staticmethod
+    def forward(ctx, X, gamma, beta, res1, res2, inc: Incidence, cfg):
+        P, Q, R, epi, slope, ln, eps, out_scale, s1, s2 = cfg
+        X = X.contiguous()
+        dev = X.device
+        n, d = inc.n_rows, X.shape[1]
+        q = inc.scale("col", Q)
+        M = spmm_csr(inc.csc, X, val=inc.edge_values("csc", R), row_scale=q)
+        p = inc.scale("row", P)
+        need_a = ln or epi != nat.EPI_NONE
+        A = torch.empty((n, d), dtype=torch.float32, device=dev) if need_a else None
+        stats = torch.empty((n, 2), dtype=torch.float32, device=dev) if ln else None
+        res1 = None if res1 is None else res1.contiguous()
+        res2 = None if res2 is None else res2.contiguous()
+        ex = nat.RowEpilogue(
+            act=epi, slope=slope, layer_norm=int(ln), ln_eps=eps,
+            ln_gamma=nat.ptr(gamma) if ln else None, ln_beta=nat.ptr(beta) if ln else None,
+            out_scale=out_scale,
+            res1=nat.ptr(res1), ld_res1=0 if res1 is None else res1.stride(0), res1_scale=s1,
+            res2=nat.ptr(res2), ld_res2=0 if res2 is None else res2.stride(0), res2_scale=s2,
+            act_out=nat.ptr(A), ld_act=0 if A is None else A.stride(0), stats=nat.ptr(stats))
+        Y = spmm_csr(inc.csr, M, val=inc.val, row_scale=p, ex=ex)
+        ctx.inc = inc
+        ctx.cfg = cfg
+        ctx.has_res = (res1 is not None, res2 is not None)
+        ctx.save_for_backward(A, stats, gamma if ln else None)
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        inc = ctx.inc
+        P, Q, R, epi, slope, ln, eps, out_scale, s1, s2 = ctx.cfg
+        A, stats, gamma = ctx.saved_tensors
+        dY = dY.contiguous()
+        n, d = dY.shape
+        dev = dY.device
+        want_g = ln and ctx.needs_input_grad[1]
+        want_b = ln and ctx.needs_input_grad[2]
+        dgamma = torch.empty(d, dtype=torch.float32, device=dev) if want_g else None
+        dbeta = torch.empty(d, dtype=torch.float32, device=dev) if want_b else None
+        lib = nat.load()
+        wsb = lib.hgd_row_epilogue_backward_workspace_size(n, d) if (want_g or want_b) else 0
+        ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev) if wsb else None
+        dZ = torch.empty_like(dY)
+        nat.check(lib.hgd_row_epilogue_backward(
+            dY.data_ptr(), dY.stride(0), nat.ptr(A), 0 if A is None else A.stride(0),
+            nat.ptr(stats), nat.ptr(gamma), n, d, epi, float(slope), int(ln), float(out_scale),
+            dZ.data_ptr(), dZ.stride(0), nat.ptr(dgamma), nat.ptr(dbeta), nat.ptr(ws), wsb,
+            torch.cuda.current_stream(dev).cuda_stream), "hgd_row_epilogue_backward")
+        dX = None
+        if ctx.needs_input_grad[0]:
+            q = inc.scale("col", Q)
+            dM = spmm_csr(inc.csc, dZ, val=inc.edge_values("csc", P), row_scale=q)
+            dX = spmm_csr(inc.csr, dM, val=inc.val, row_scale=inc.scale("row", R))
+
+        def res_grad(k, s):
+            if not ctx.has_res[k] or not ctx.needs_input_grad[3 + k]:
+                return None
+            return dY if s == 1.0 else dY * s
+
+        return dX, dgamma, dbeta, res_grad(0, s1), res_grad(1, s2), None, None
+
+
+def two_hop_fused(inc: Incidence, X: torch.Tensor, P: Optional[str] = None,
+                  Q: Optional[str] = None, R: Optional[str] = None,
+                  epilogue: Optional[str] = None, slope: float = 0.0,
+                  norm: Optional[torch.nn.LayerNorm] = None, out_scale: float = 1.0,
+                  res1: Optional[torch.Tensor] = None, res1_scale: float = 1.0,
+                  res2: Optional[torch.Tensor] = None, res2_scale: float = 1.0) -> torch.Tensor:
+    """``out_scale·norm(epi(P·A·Q·Aᵀ·R·X)) + res1_scale·res1 + res2_scale·res2`` with autograd.
+
+    One fused hgd_spmm_fused store replaces the reference's separate LayerNorm, residual add and
+    restart blend kernels. ``norm`` is an ``nn.LayerNorm`` over the last
+    dim (its weight/bias get gradients). Shapes the fused store cannot hold (LayerNorm with
+    d > 256, or a negative slope) run the same math as separate device ops."""
+    epi = _EPI[epilogue]
+    d = X.shape[1]
+    ln = norm is not None
+    if ln and (tuple(norm.normalized_shape) != (d,)):
+        raise ValueError(f"two_hop_fused: LayerNorm over {tuple(norm.normalized_shape)}, d={d}")
+    for r in (res1, res2):
+        if r is not None and tuple(r.shape) != (inc.n_rows, d):
+            raise ValueError(f"two_hop_fused: residual {tuple(r.shape)} != {(inc.n_rows, d)}")
+    if (ln and not _ln_supported(d)) or (epi != nat.EPI_NONE and slope < 0):
+        y = two_hop(inc, X, P=P, Q=Q, R=R, epilogue=epilogue, slope=slope)
+        if ln:
+            y = norm(y)
+        y = out_scale * y
+        if res1 is not None:
+            y = y + res1_scale * res1
+        if res2 is not None:
+            y = y + res2_scale * res2
+        return y
+    gamma = norm.weight if ln and norm.weight is not None else None
+    beta = norm.bias if ln and norm.bias is not None else None
+    cfg = (P, Q, R, epi, float(slope), ln, float(norm.eps) if ln else 0.0, float(out_scale),
+           float(res1_scale), float(res2_scale))
+    return _FusedTwoHop.apply(X, gamma, beta, res1, res2, inc, cfg)

@@ -145,8 +145,12 @@ class CSR:
 def spmm_csr(csr: CSR, X: torch.Tensor, val: Optional[torch.Tensor] = None,
              row_scale: Optional[torch.Tensor] = None, epilogue: int = nat.EPI_NONE,
              slope: float = 0.0, out: Optional[torch.Tensor] = None,
-             row_begin: int = 0, row_end: Optional[int] = None) -> torch.Tensor:
-    """``Y[r] = epi(row_scale[r] * Σ_e val[e] * X[col[e]])`` for r in [row_begin, row_end)."""
+             row_begin: int = 0, row_end: Optional[int] = None,
+             ex: Optional[nat.RowEpilogue] = None) -> torch.Tensor:
+    """``Y[r] = epi(row_scale[r] * Σ_e val[e] * X[col[e]])`` for r in [row_begin, row_end).
+
+    With ``ex`` (an ``hgd_row_epilogue``) the call is ``hgd_spmm_fused``: ``ex.act``/``ex.slope``
+    replace ``epilogue``/``slope`` and the LayerNorm / residual epilogue runs in the store."""
     if X.dim() != 2:
         raise ValueError(f"spmm: X must be 2-D, got {tuple(X.shape)}")
     if X.dtype != torch.float32:
@@ -175,11 +179,18 @@ def spmm_csr(csr: CSR, X: torch.Tensor, val: Optional[torch.Tensor] = None,
     timer = profiling.active()
     if timer is not None:
         t0 = timer.begin()
-    nat.check(lib.hgd_spmm(
-        csr.rowptr.data_ptr(), csr.col.data_ptr() if csr.nnz else None, nat.ptr(val),
-        nat.ptr(row_scale), csr.n_rows, csr.n_cols, int(row_begin), int(row_end),
-        X.data_ptr(), X.stride(0), out.data_ptr(), out.stride(0), d, int(epilogue),
-        float(slope), plan_ptr, nat.ptr(ws), wsb, _stream(X.device)), "hgd_spmm")
+    if ex is None:
+        nat.check(lib.hgd_spmm(
+            csr.rowptr.data_ptr(), csr.col.data_ptr() if csr.nnz else None, nat.ptr(val),
+            nat.ptr(row_scale), csr.n_rows, csr.n_cols, int(row_begin), int(row_end),
+            X.data_ptr(), X.stride(0), out.data_ptr(), out.stride(0), d, int(epilogue),
+            float(slope), plan_ptr, nat.ptr(ws), wsb, _stream(X.device)), "hgd_spmm")
+    else:
+        nat.check(lib.hgd_spmm_fused(
+            csr.rowptr.data_ptr(), csr.col.data_ptr() if csr.nnz else None, nat.ptr(val),
+            nat.ptr(row_scale), csr.n_rows, csr.n_cols, int(row_begin), int(row_end),
+            X.data_ptr(), X.stride(0), out.data_ptr(), out.stride(0), d, ctypes.byref(ex),
+            plan_ptr, nat.ptr(ws), wsb, _stream(X.device)), "hgd_spmm_fused")
     if timer is not None:
         rb, re_ = int(row_begin), int(row_end)
         full = rb == 0 and re_ == csr.n_rows

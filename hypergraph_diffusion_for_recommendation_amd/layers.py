@@ -29,7 +29,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .functional import spmm, two_hop
+from .functional import spmm, two_hop, two_hop_fused
 from .incidence import (CSR, Incidence, dense_threshold, drop_edges, expand_rows,
                         incidence_of)
 
@@ -216,6 +216,7 @@ class EquivSetConv(nn.Module):
         self.dropout = dropout
         self.data = data
         self._cache = None
+        self.fused_epilogue = True  # False: the reference's separate blend ops (A/B benches)
 
     def reset_parameters(self):
         for m in (self.W1, self.W2, self.W):
@@ -239,6 +240,10 @@ class EquivSetConv(nn.Module):
         scale = "mean" if self.aggr == "mean" else None
         Xs = self.W1(X)
         if self.W2 is None:
+            if self.fused_epilogue and torch.is_tensor(X0) and tuple(X0.shape) == (N, Xs.shape[1]):
+                # restart blend (1-α)·Xv + α·X0 fused into the second hop's store
+                return self.W(two_hop_fused(inc, Xs, P=scale, Q=scale, out_scale=1 - self.alpha,
+                                            res1=X0, res1_scale=self.alpha))
             Xv = two_hop(inc, Xs, P=scale, Q=scale, R=None)
         else:
             # general path: Xe = aggr(W1(X)[V], E); Xv = aggr(W2([X[V], Xe[E]]), V)

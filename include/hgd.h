@@ -115,6 +115,61 @@ hgd_status hgd_spmm(const int64_t* rowptr, const int32_t* col, const float* val,
                     void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * Fused row epilogue of an ED-HNN / HGCN layer. Replaces the torch ops
+ * the reference runs on the hop output, each an extra [N,d] HBM round trip and launch:
+ *   LayerNorm + residual     Xe = LN0(HGCNConv(adj, Xve)) + Xve   model/layers/EquivSetConv.py:86-107,
+ *                                                                 model/graph/HGNN_HD3.py:705-720
+ *   restart blend            X = (1-α)·Xv + α·X0                   model/layers/layers2/EquivSetConv2.py:96
+ * For every row r written by the hop (z = row_scale[r]·Σ of hgd_spmm):
+ *   a = act(z)                         (act_out[r] = a when act_out != NULL)
+ *   b = layer_norm ? (a - μ_r)·rstd_r·γ + β : a      (biased variance, rstd = 1/sqrt(var+eps);
+ *                                                      stats[2r] = μ_r, stats[2r+1] = rstd_r)
+ *   Y[r] = out_scale·b + res1_scale·res1[r] + res2_scale·res2[r]    (NULL residuals skipped)
+ * layer_norm needs the whole row in one lane group: d <= 256 with 16-byte aligned rows (X, Y,
+ * residuals, act_out, leading dims % 4 == 0), or d <= 64 otherwise (HGD_ERR_UNSUPPORTED beyond).
+ * act must be NONE or have slope >= 0, so that act'(z) can be read from the sign of a.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct hgd_row_epilogue {
+  int32_t act;            /* hgd_epilogue */
+  float slope;
+  int32_t layer_norm;     /* 0 / 1 */
+  float ln_eps;
+  const float* ln_gamma;  /* [d] or NULL (= 1) */
+  const float* ln_beta;   /* [d] or NULL (= 0) */
+  float out_scale;
+  const float* res1;      /* [n_rows, ld_res1] or NULL */
+  int64_t ld_res1;
+  float res1_scale;
+  const float* res2;
+  int64_t ld_res2;
+  float res2_scale;
+  float* act_out;         /* [n_rows, ld_act] or NULL */
+  int64_t ld_act;
+  float* stats;           /* [n_rows, 2] or NULL */
+} hgd_row_epilogue;
+
+/* hgd_spmm with the fused row epilogue `epi` (which replaces hgd_spmm's epilogue/slope). */
+hgd_status hgd_spmm_fused(const int64_t* rowptr, const int32_t* col, const float* val,
+                          const float* row_scale, int64_t n_rows, int64_t n_src_rows,
+                          int64_t row_begin, int64_t row_end, const float* X, int64_t ldx,
+                          float* Y, int64_t ldy, int32_t d, const hgd_row_epilogue* epi,
+                          const hgd_split_plan* plan, void* workspace, size_t workspace_bytes,
+                          void* stream);
+
+/* Backward of the row epilogue up to z (the residual gradients are res_scale·dY, left to the
+ * caller): dZ = act'(a) ⊙ LN_bwd(out_scale·dY), with LN_bwd the LayerNorm input gradient
+ * rstd·(ĝ - mean(ĝ) - â·mean(ĝ⊙â)), ĝ = γ⊙dy, â = (a-μ)·rstd recomputed from act_out and stats.
+ * dgamma = Σ_r dy⊙â, dbeta = Σ_r dy (written, not accumulated; summed in a fixed order, so the
+ * result is deterministic). act_out is required when act != NONE or layer_norm. */
+size_t hgd_row_epilogue_backward_workspace_size(int64_t n_rows, int32_t d);
+hgd_status hgd_row_epilogue_backward(const float* dY, int64_t ldy, const float* act_out,
+                                     int64_t ld_act, const float* stats, const float* ln_gamma,
+                                     int64_t n_rows, int32_t d, int32_t act, float slope,
+                                     int32_t layer_norm, float out_scale, float* dZ, int64_t ldz,
+                                     float* dgamma, float* dbeta, void* workspace,
+                                     size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Structure primitives (all deterministic; indices bit-exact with the CPU restatement).
  * ---------------------------------------------------------------------------------------- */
 /* int64 indices → int32, checking 0 <= v < upper; err_count (device int64) += #violations. */

@@ -280,6 +280,49 @@ def layer_norm(X, weight=None, bias=None, eps=1e-5):
     return Y
 
 
+def row_epilogue(Z, act=None, slope=0.0, ln=False, gamma=None, beta=None, eps=1e-5,
+                 out_scale=1.0, res1=None, s1=1.0, res2=None, s2=1.0):
+    """The torch op chain after an HGCNConv two-hop that hgd_spmm_fused runs in its store:
+    ``Xe = LN0(leaky(Z)) + Xve`` (model/layers/EquivSetConv.py:86-92, HGNN_HD3.py:705-712) and
+    ``(1-α)·(LN1(leaky(Z')) + Xev) + α·X0`` (EquivSetConv.py:100-104), or the restart blend
+    ``(1-α)·Xv + α·X0`` of layers2/EquivSetConv2.py:96. Returns (Y, a) with a = act(Z)."""
+    a = epilogue(np.asarray(Z, dtype=np.float64), act, slope)
+    b = layer_norm(a, gamma, beta, eps) if ln else a
+    Y = out_scale * b
+    if res1 is not None:
+        Y = Y + s1 * np.asarray(res1, dtype=np.float64)
+    if res2 is not None:
+        Y = Y + s2 * np.asarray(res2, dtype=np.float64)
+    return Y, a
+
+
+def row_epilogue_backward(Z, dY, act=None, slope=0.0, ln=False, gamma=None, eps=1e-5,
+                          out_scale=1.0):
+    """Gradient of :func:`row_epilogue` w.r.t. Z, γ and β (the autograd of nn.LayerNorm and
+    nn.LeakyReLU as torch defines them): returns (dZ, dgamma, dbeta)."""
+    Z = np.asarray(Z, dtype=np.float64)
+    a = epilogue(Z, act, slope)
+    dy = out_scale * np.asarray(dY, dtype=np.float64)
+    dgamma = dbeta = None
+    if ln:
+        d = a.shape[-1]
+        mu = a.mean(-1, keepdims=True)
+        rstd = 1.0 / np.sqrt(a.var(-1, keepdims=True) + eps)
+        ah = (a - mu) * rstd
+        g = np.ones(d) if gamma is None else np.asarray(gamma, dtype=np.float64)
+        gh = dy * g
+        da = rstd * (gh - gh.mean(-1, keepdims=True) - ah * (gh * ah).mean(-1, keepdims=True))
+        dgamma = (dy * ah).sum(0)
+        dbeta = dy.sum(0)
+    else:
+        da = dy
+    if act == "leaky_relu":
+        da = np.where(Z > 0, da, da * slope)
+    elif act == "relu":
+        da = np.where(Z > 0, da, 0.0)
+    return da, dgamma, dbeta
+
+
 def linear(X, W, b=None):
     """nn.Linear: X·Wᵀ + b."""
     Y = np.asarray(X, dtype=np.float64) @ np.asarray(W, dtype=np.float64).T

@@ -159,3 +159,35 @@ def test_find_k_largest_closed_form(K):
 def test_find_k_largest_duplicates_seed_items():
     ids, sc = O.find_k_largest(3, np.array([5.0, 4.0, 3.0, 10.0, 1.0]))
     assert ids == [3, 0, 0] and sc == [10.0, 5.0, 5.0]
+
+
+@pytest.mark.parametrize("act,slope,ln", [(None, 0.0, True), ("leaky_relu", 0.2, True),
+                                          ("relu", 0.0, False), ("leaky_relu", 0.5, False)])
+def test_row_epilogue_backward_matches_torch_autograd(act, slope, ln):
+    """The LN / LeakyReLU / blend gradient restatement against torch autograd in float64."""
+    import torch
+    rng = np.random.default_rng(5)
+    Z = rng.standard_normal((40, 24))
+    dY = rng.standard_normal((40, 24))
+    g = rng.random(24) + 0.5
+    b = rng.standard_normal(24)
+    R1 = rng.standard_normal((40, 24))
+    Y, _ = O.row_epilogue(Z, act, slope, ln, g, b, 1e-5, 0.7, R1, 0.4)
+    Zt = torch.tensor(Z, requires_grad=True)
+    gt = torch.tensor(g, requires_grad=True)
+    bt = torch.tensor(b, requires_grad=True)
+    a = Zt
+    if act == "leaky_relu":
+        a = torch.nn.functional.leaky_relu(Zt, slope)
+    elif act == "relu":
+        a = torch.relu(Zt)
+    if ln:
+        a = torch.nn.functional.layer_norm(a, (24,), gt, bt, 1e-5)
+    Yt = 0.7 * a + 0.4 * torch.tensor(R1)
+    np.testing.assert_allclose(Y, Yt.detach().numpy(), rtol=1e-12, atol=1e-12)
+    Yt.backward(torch.tensor(dY))
+    dZ, dg, db = O.row_epilogue_backward(Z, dY, act, slope, ln, g, 1e-5, 0.7)
+    np.testing.assert_allclose(dZ, Zt.grad.numpy(), rtol=1e-10, atol=1e-12)
+    if ln:
+        np.testing.assert_allclose(dg, gt.grad.numpy(), rtol=1e-10, atol=1e-12)
+        np.testing.assert_allclose(db, bt.grad.numpy(), rtol=1e-10, atol=1e-12)
