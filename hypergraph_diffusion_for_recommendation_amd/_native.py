@@ -85,11 +85,22 @@ _SIGNATURES = {
                                c_i64, c_void_p, c_i64, c_void_p, c_i64, c_i32,
                                ctypes.POINTER(RowEpilogue), ctypes.POINTER(SplitPlan), c_void_p,
                                c_size, c_void_p]),
+    "hgd_row_epilogue_forward": (c_i32, [c_void_p, c_i64, c_i64, c_i32,
+                                         ctypes.POINTER(RowEpilogue), c_void_p, c_i64,
+                                         c_void_p]),
     "hgd_row_epilogue_backward_workspace_size": (c_size, [c_i64, c_i32]),
     "hgd_row_epilogue_backward": (c_i32, [c_void_p, c_i64, c_void_p, c_i64, c_void_p, c_void_p,
                                           c_i64, c_i32, c_i32, c_f32, c_i32, c_f32, c_void_p,
                                           c_i64, c_void_p, c_void_p, c_void_p, c_size,
                                           c_void_p]),
+    "hgd_linear_forward": (c_i32, [c_void_p, c_i64, c_i64, c_i32, c_void_p, c_i64, c_i32,
+                                   c_void_p, c_i32, c_void_p, c_i64, c_void_p]),
+    "hgd_linear_backward_data": (c_i32, [c_void_p, c_i64, c_void_p, c_i64, c_i64, c_i32,
+                                         c_void_p, c_i64, c_i32, c_void_p, c_i64, c_void_p]),
+    "hgd_linear_backward_weight_workspace_size": (c_size, [c_i64, c_i32, c_i32]),
+    "hgd_linear_backward_weight": (c_i32, [c_void_p, c_i64, c_void_p, c_i64, c_void_p, c_i64,
+                                           c_i64, c_i32, c_i32, c_void_p, c_void_p, c_void_p,
+                                           c_size, c_void_p]),
     "hgd_index_narrow": (c_i32, [c_void_p, c_i64, c_i64, c_void_p, c_void_p, c_void_p]),
     "hgd_sort_perm_workspace_size": (c_size, [c_i64]),
     "hgd_sort_perm": (c_i32, [c_void_p, c_i64, c_i64, c_void_p, c_void_p, c_void_p, c_size,

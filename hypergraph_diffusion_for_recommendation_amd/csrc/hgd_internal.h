@@ -55,4 +55,9 @@ inline unsigned grid_for(int64_t n, int per_block = kBlock) {
 
 inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 
+// out[c] = Σ_{s < S} P[s·W + c] for c < W, summed in a fixed order (deterministic): 16 waves per
+// block each sum a contiguous slice of s for 64 columns, then the slices are added in order
+// (reduce.hip). Used for split-K and per-block partials.
+hgd_status sum_rows(const float* P, int64_t S, int64_t W, float* out, hipStream_t st);
+
 }  // namespace hgd

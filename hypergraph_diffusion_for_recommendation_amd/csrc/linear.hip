@@ -1,0 +1,475 @@
+// The skinny Linear layers around the ED-HNN hops ("lin_in GEMM + ReLU …
+// Linear (MFMA at d ≥ 64)"): nn.Linear(d, d) over N ≫ d rows — lin_in (EquivSetGNN2.py:93-94,
+// EquivSetGNN.py:88-89) and the MLP layers (model/layers/MLP.py:109-117). The library GEMMs the
+// reference gets for these shapes are tiled for square problems: the profile of the Yelp-shaped
+// block (profiles/r01_edhnn_yelp) shows the weight gradient [64 × 64] = dYᵀ·X with K = 69,716
+// rows taking 0.20 ms (4 workgroups on a 256-CU chip) and the forward 30 µs for 36 MB.
+//
+// All three products run on the f32-input MFMA v_mfma_f32_16x16x4_f32 (exact f32 products and
+// sums, at the f32 vector rate) with operands loaded straight from HBM as float4 rows:
+//
+//  * row GEMM (forward Y = relu?(X·Wᵀ + b), backward-data dX = (dY ⊙ [Y > 0])·W): W's 64-column
+//    slice is staged once per workgroup through LDS into registers (K/16 × 16 floats per lane),
+//    then each wave streams 16-row tiles (grid-stride, next tile's loads in flight during the
+//    current tile's MFMAs), so every input row is read once and every output row written once
+//    (≈ 16 flop per byte at d = 64, where the f32 MFMA and HBM rates meet). Lane l loads float4
+//    X[r0 + (l&15)][4(l>>4) + 16q]; MFMA step (q, c) then multiplies k = 4(l>>4) + 16q + c — a
+//    fixed permutation of k that the W fragments follow, so the rows need no LDS or shuffles.
+//  * split-K weight GEMM (dW = (dY ⊙ mask)ᵀ·X, db = Σ dY ⊙ mask): the rows are cut into S slices
+//    (one workgroup each, ≤ 1024); lane l loads float4 row fragments of both operands and the 16
+//    MFMAs of a 4-row step produce the whole 64 × 64 tile with (m, n) = (4i + t, 4j + u)
+//    permuted; the 4 waves are combined in LDS in wave order, the S slice partials by sum_rows in
+//    slice order. No atomics: results are bitwise reproducible.
+#include "hgd_internal.h"
+
+namespace hgd {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+
+__device__ __forceinline__ f32x4 relu_mask(f32x4 v, f32x4 m) {
+  return f32x4{m.x > 0.f ? v.x : 0.f, m.y > 0.f ? v.y : 0.f, m.z > 0.f ? v.z : 0.f,
+               m.w > 0.f ? v.w : 0.f};
+}
+
+constexpr int kRowGemmMaxBlocks = 512;
+constexpr int kMaxSplits = 1024;
+
+struct RowGemm {
+  const float* A;     // [rows, K]
+  int64_t lda;
+  const float* mask;  // optional [rows, K]: A ⊙ (mask > 0)
+  int64_t ldm;
+  const float* B;     // Bm[k][n] = B[k * bsk + n * bsn]
+  int64_t bsk, bsn;
+  const float* bias;  // [N] or NULL
+  int32_t relu;
+  float* Y;
+  int64_t ldy;
+  int64_t rows;
+  int32_t K, N;
+};
+
+template <int KQ, bool MASK>  // K = 16·KQ; MASK: A ⊙ (mask > 0)
+__global__ __launch_bounds__(256) void k_row_gemm(RowGemm p) {
+  constexpr int K = 16 * KQ;
+  constexpr int LDB = 65;           // padded row: the k-contiguous staging writes spread banks
+  constexpr int PER = K * 64 / 256;  // staged floats per thread
+  constexpr int SUB = 2;             // 16-row sub-tiles per wave iteration
+  __shared__ float sB[K * LDB];      // Bm[k][n0 + nl], zero past N
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int i16 = lane & 15;
+  const int h = lane >> 4;
+  const int n0 = blockIdx.y * 64;
+  const int nt = min(4, (p.N - n0) / 16);  // live 16-column tiles of this slice (uniform)
+  {
+    // all loads first (independent, in flight together), then the LDS writes
+    float tmp[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int e = threadIdx.x + 256 * j;
+      const int k = p.bsk == 1 ? e % K : e / 64;
+      const int nl = p.bsk == 1 ? e / K : e % 64;
+      const int n = n0 + nl < p.N ? n0 + nl : p.N - 1;
+      tmp[j] = p.B[static_cast<int64_t>(k) * p.bsk + static_cast<int64_t>(n) * p.bsn];
+      if (n0 + nl >= p.N) tmp[j] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int e = threadIdx.x + 256 * j;
+      const int k = p.bsk == 1 ? e % K : e / 64;
+      const int nl = p.bsk == 1 ? e / K : e % 64;
+      sB[k * LDB + nl] = tmp[j];
+    }
+  }
+  __syncthreads();
+  float bf[KQ][4][4];
+#pragma unroll
+  for (int q = 0; q < KQ; ++q)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) bf[q][c][t] = sB[(4 * h + 16 * q + c) * LDB + 16 * t + i16];
+  float bias_v[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) bias_v[t] = (p.bias && t < nt) ? p.bias[n0 + 16 * t + i16] : 0.f;
+
+  const int64_t tiles = (p.rows + 16 * SUB - 1) / (16 * SUB);  // 32-row super-tiles
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * 4;
+  // Unconditional raw loads (the compiler then counts them exactly in its vmcnt waits): rows
+  // past the end are clamped to the last row and their results never stored; the ReLU mask is
+  // applied when the tile is consumed.
+  auto load = [&](int64_t tile, f32x4 (&a)[SUB][KQ], f32x4 (&m)[SUB][KQ]) {
+    tile = tile < tiles ? tile : tiles - 1;
+#pragma unroll
+    for (int s = 0; s < SUB; ++s) {
+      int64_t ra = tile * 16 * SUB + 16 * s + i16;
+      ra = ra < p.rows ? ra : p.rows - 1;
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) a[s][q] = ld4(p.A + ra * p.lda + 4 * h + 16 * q);
+      if constexpr (MASK) {
+#pragma unroll
+        for (int q = 0; q < KQ; ++q) m[s][q] = ld4(p.mask + ra * p.ldm + 4 * h + 16 * q);
+      }
+    }
+  };
+  auto compute = [&](int64_t tile, f32x4 (&a)[SUB][KQ], const f32x4 (&m)[SUB][KQ]) {
+#pragma unroll
+    for (int s = 0; s < SUB; ++s) {
+      if constexpr (MASK) {
+#pragma unroll
+        for (int q = 0; q < KQ; ++q) a[s][q] = relu_mask(a[s][q], m[s][q]);
+      }
+      f32x4 acc[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < KQ; ++q)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) acc[t] = mfma4(a[s][q][c], bf[q][c][t], acc[t]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = acc[t][r] + bias_v[t];
+          acc[t][r] = (p.relu && v < 0.f) ? 0.f : v;
+        }
+      const int64_t r0 = tile * 16 * SUB + 16 * s;
+      float* yb = p.Y + n0 + i16;
+      if (nt == 4 && r0 + 16 <= p.rows) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) yb[(r0 + 4 * h + r) * p.ldy + 16 * t] = acc[t][r];
+      } else {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (t < nt && r0 + 4 * h + r < p.rows)
+              yb[(r0 + 4 * h + r) * p.ldy + 16 * t] = acc[t][r];
+      }
+    }
+  };
+  int64_t tile = static_cast<int64_t>(blockIdx.x) * 4 + wave;
+  if (tile >= tiles) return;
+  // ping-pong buffers: the next super-tile's loads are in flight during this one's MFMAs
+  f32x4 a0[SUB][KQ], a1[SUB][KQ], m0v[SUB][KQ], m1v[SUB][KQ];
+  load(tile, a0, m0v);
+  while (tile < tiles) {
+    load(tile + stride, a1, m1v);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(tile, a0, m0v);
+    __builtin_amdgcn_sched_barrier(0);
+    tile += stride;
+    if (tile >= tiles) break;
+    load(tile + stride, a0, m0v);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(tile, a1, m1v);
+    __builtin_amdgcn_sched_barrier(0);
+    tile += stride;
+  }
+}
+
+struct SplitK {
+  const float* A;  // [rows, M] (dY)
+  int64_t lda;
+  const float* mask;
+  int64_t ldm;
+  const float* B;  // [rows, N] (X)
+  int64_t ldb;
+  int64_t rows;
+  int32_t M, N;
+  int64_t rows_per_split;
+  float* part;       // [S, M·N]
+  float* part_bias;  // [S, M] or NULL
+};
+
+template <bool MASK>
+__global__ __launch_bounds__(256) void k_splitk_tn(SplitK p) {
+  __shared__ float s_acc[4][64 * 64];
+  __shared__ float s_bias[4][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int i16 = lane & 15;
+  const int h = lane >> 4;
+  const int m0 = blockIdx.y * 64;
+  const int n0 = blockIdx.z * 64;
+  const int64_t k_begin = static_cast<int64_t>(blockIdx.x) * p.rows_per_split;
+  const int64_t k_end = min(p.rows, k_begin + p.rows_per_split);
+  const bool mcol = m0 + 4 * i16 < p.M;
+  const bool ncol = n0 + 4 * i16 < p.N;
+  const int mc = mcol ? m0 + 4 * i16 : m0;  // clamped (valid) columns; zeroed at consume
+  const int nc = ncol ? n0 + 4 * i16 : n0;
+  const bool want_bias = p.part_bias != nullptr && blockIdx.z == 0;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[t][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bsum[4] = {0.f, 0.f, 0.f, 0.f};
+
+  constexpr int U = 8;  // 4-row steps per wave per batch (loads of batch b+1 overlap b's MFMAs)
+  // Unconditional loads from clamped rows (exact vmcnt accounting by the compiler); rows past
+  // k_end and columns past M / N are zeroed when consumed.
+  auto load = [&](int64_t kb, f32x4 (&a)[U], f32x4 (&b)[U], f32x4 (&m)[U]) {
+#pragma unroll
+    for (int s = 0; s < U; ++s) {
+      int64_t kr = kb + 16 * s + h;
+      kr = kr < k_end ? kr : k_begin;
+      a[s] = ld4(p.A + kr * p.lda + mc);
+      if constexpr (MASK) m[s] = ld4(p.mask + kr * p.ldm + mc);
+      b[s] = ld4(p.B + kr * p.ldb + nc);
+    }
+  };
+  auto compute = [&](int64_t kb, const f32x4 (&ca)[U], const f32x4 (&cb)[U],
+                     const f32x4 (&cm)[U]) {
+#pragma unroll
+    for (int s = 0; s < U; ++s) {
+      const bool ok = kb + 16 * s + h < k_end;
+      f32x4 av = ca[s], bv = cb[s];
+      if constexpr (MASK) av = relu_mask(av, cm[s]);
+      if (!(ok && mcol)) av = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (!(ok && ncol)) bv = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[t][u] = mfma4(av[t], bv[u], acc[t][u]);
+      if (want_bias) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) bsum[t] += av[t];
+      }
+    }
+  };
+  // ping-pong buffers (no loop-carried copies, which the compiler would hoist into the MFMA
+  // stream together with a full vmcnt wait)
+  f32x4 a0[U], b0[U], m0v[U], a1[U], b1[U], m1v[U];
+  int64_t kb = k_begin + 4 * wave;
+  load(kb, a0, b0, m0v);
+  while (kb < k_end) {
+    load(kb + 16 * U, a1, b1, m1v);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(kb, a0, b0, m0v);
+    __builtin_amdgcn_sched_barrier(0);
+    kb += 16 * U;
+    if (kb >= k_end) break;
+    load(kb + 16 * U, a0, b0, m0v);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(kb, a1, b1, m1v);
+    __builtin_amdgcn_sched_barrier(0);
+    kb += 16 * U;
+  }
+  // acc[t][u] lane (i16, h) reg r: m_local = 4·(4h + r) + t, n_local = 4·i16 + u
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        s_acc[wave][(4 * (4 * h + r) + t) * 64 + 4 * i16 + u] = acc[t][u][r];
+  if (want_bias) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      bsum[t] += __shfl_xor(bsum[t], 16);
+      bsum[t] += __shfl_xor(bsum[t], 32);
+      if (h == 0) s_bias[wave][4 * i16 + t] = bsum[t];
+    }
+  }
+  __syncthreads();
+  const int64_t MN = static_cast<int64_t>(p.M) * p.N;
+  for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+    const int ml = e >> 6, nl = e & 63;
+    if (m0 + ml < p.M && n0 + nl < p.N) {
+      const float v = ((s_acc[0][e] + s_acc[1][e]) + s_acc[2][e]) + s_acc[3][e];
+      p.part[static_cast<int64_t>(blockIdx.x) * MN + static_cast<int64_t>(m0 + ml) * p.N + n0 +
+             nl] = v;
+    }
+  }
+  if (want_bias && threadIdx.x < 64 && m0 + static_cast<int>(threadIdx.x) < p.M) {
+    const int ml = threadIdx.x;
+    p.part_bias[static_cast<int64_t>(blockIdx.x) * p.M + m0 + ml] =
+        ((s_bias[0][ml] + s_bias[1][ml]) + s_bias[2][ml]) + s_bias[3][ml];
+  }
+}
+
+bool al16(const void* p, int64_t ld) {
+  return p == nullptr || (reinterpret_cast<uintptr_t>(p) % 16 == 0 && ld % 4 == 0);
+}
+
+hgd_status row_gemm(const RowGemm& p, hipStream_t st, const char* fn) {
+  if (p.rows == 0) return HGD_OK;
+  const int64_t tiles = (p.rows + 31) / 32;
+  int64_t bx = (tiles + 3) / 4;
+  if (bx > kRowGemmMaxBlocks) bx = kRowGemmMaxBlocks;
+  const dim3 grid(static_cast<unsigned>(bx), static_cast<unsigned>((p.N + 63) / 64));
+  switch (p.K / 16) {
+#define HGD_CASE(Q)                                                                \
+    case Q:                                                                        \
+      if (p.mask)                                                                  \
+        hipLaunchKernelGGL((k_row_gemm<Q, true>), grid, dim3(256), 0, st, p);      \
+      else                                                                         \
+        hipLaunchKernelGGL((k_row_gemm<Q, false>), grid, dim3(256), 0, st, p);     \
+      break;
+    HGD_CASE(1) HGD_CASE(2) HGD_CASE(3) HGD_CASE(4) HGD_CASE(5) HGD_CASE(6) HGD_CASE(7)
+    HGD_CASE(8)
+#undef HGD_CASE
+    default:
+      return fail(HGD_ERR_UNSUPPORTED, "%s: K = %d (needs 16..128, multiple of 16)", fn, p.K);
+  }
+  return check_launch(fn);
+}
+
+int64_t splits_for(int64_t rows) {
+  int64_t s = (rows + 511) / 512;
+  if (s > kMaxSplits) s = kMaxSplits;
+  return s < 1 ? 1 : s;
+}
+
+}  // namespace
+}  // namespace hgd
+
+extern "C" hgd_status hgd_linear_forward(const float* X, int64_t ldx, int64_t n_rows,
+                                         int32_t in_features, const float* W, int64_t ldw,
+                                         int32_t out_features, const float* bias, int32_t relu,
+                                         float* Y, int64_t ldy, void* stream) {
+  using namespace hgd;
+  clear_error();
+  HGD_REQUIRE(n_rows >= 0, "hgd_linear_forward: negative rows");
+  HGD_REQUIRE(in_features % 16 == 0 && in_features >= 16 && in_features <= 128,
+              "hgd_linear_forward: in_features %d must be a multiple of 16 in [16, 128]",
+              in_features);
+  HGD_REQUIRE(out_features % 16 == 0 && out_features >= 16,
+              "hgd_linear_forward: out_features %d must be a positive multiple of 16",
+              out_features);
+  HGD_REQUIRE(ldx >= in_features && ldy >= out_features && ldw >= in_features,
+              "hgd_linear_forward: leading dimension too small");
+  if (n_rows == 0) return HGD_OK;
+  HGD_REQUIRE(X && W && Y, "hgd_linear_forward: null pointer");
+  HGD_REQUIRE(al16(X, ldx), "hgd_linear_forward: X rows must be 16-byte aligned");
+  RowGemm p{};
+  p.A = X;
+  p.lda = ldx;
+  p.B = W;  // Bm[k][n] = W[n][k]
+  p.bsk = 1;
+  p.bsn = ldw;
+  p.bias = bias;
+  p.relu = relu != 0;
+  p.Y = Y;
+  p.ldy = ldy;
+  p.rows = n_rows;
+  p.K = in_features;
+  p.N = out_features;
+  return row_gemm(p, as_stream(stream), "hgd_linear_forward");
+}
+
+extern "C" hgd_status hgd_linear_backward_data(const float* dY, int64_t ldy, const float* relu_out,
+                                               int64_t ldr, int64_t n_rows, int32_t out_features,
+                                               const float* W, int64_t ldw, int32_t in_features,
+                                               float* dX, int64_t ldx, void* stream) {
+  using namespace hgd;
+  clear_error();
+  HGD_REQUIRE(n_rows >= 0, "hgd_linear_backward_data: negative rows");
+  HGD_REQUIRE(out_features % 16 == 0 && out_features >= 16 && out_features <= 128,
+              "hgd_linear_backward_data: out_features %d must be a multiple of 16 in [16, 128]",
+              out_features);
+  HGD_REQUIRE(in_features % 16 == 0 && in_features >= 16,
+              "hgd_linear_backward_data: in_features %d must be a positive multiple of 16",
+              in_features);
+  HGD_REQUIRE(ldy >= out_features && ldx >= in_features && ldw >= in_features &&
+                  (!relu_out || ldr >= out_features),
+              "hgd_linear_backward_data: leading dimension too small");
+  if (n_rows == 0) return HGD_OK;
+  HGD_REQUIRE(dY && W && dX, "hgd_linear_backward_data: null pointer");
+  HGD_REQUIRE(al16(dY, ldy) && al16(relu_out, ldr),
+              "hgd_linear_backward_data: dY / relu_out rows must be 16-byte aligned");
+  RowGemm p{};
+  p.A = dY;
+  p.lda = ldy;
+  p.mask = relu_out;
+  p.ldm = ldr;
+  p.B = W;  // Bm[k][n] = W[k][n]  (k = output feature, n = input feature)
+  p.bsk = ldw;
+  p.bsn = 1;
+  p.Y = dX;
+  p.ldy = ldx;
+  p.rows = n_rows;
+  p.K = out_features;
+  p.N = in_features;
+  return row_gemm(p, as_stream(stream), "hgd_linear_backward_data");
+}
+
+extern "C" size_t hgd_linear_backward_weight_workspace_size(int64_t n_rows, int32_t out_features,
+                                                           int32_t in_features) {
+  if (n_rows <= 0 || out_features <= 0 || in_features <= 0) return 0;
+  const size_t S = static_cast<size_t>(hgd::splits_for(n_rows));
+  return hgd::align_up(S * out_features * in_features * 4) + hgd::align_up(S * out_features * 4);
+}
+
+extern "C" hgd_status hgd_linear_backward_weight(const float* dY, int64_t ldy,
+                                                 const float* relu_out, int64_t ldr,
+                                                 const float* X, int64_t ldx, int64_t n_rows,
+                                                 int32_t out_features, int32_t in_features,
+                                                 float* dW, float* db, void* workspace,
+                                                 size_t workspace_bytes, void* stream) {
+  using namespace hgd;
+  clear_error();
+  HGD_REQUIRE(n_rows >= 0, "hgd_linear_backward_weight: negative rows");
+  HGD_REQUIRE(out_features % 16 == 0 && out_features >= 16 && in_features % 16 == 0 &&
+                  in_features >= 16,
+              "hgd_linear_backward_weight: features (%d, %d) must be positive multiples of 16",
+              out_features, in_features);
+  HGD_REQUIRE(ldy >= out_features && ldx >= in_features && (!relu_out || ldr >= out_features),
+              "hgd_linear_backward_weight: leading dimension too small");
+  HGD_REQUIRE(dW, "hgd_linear_backward_weight: null dW");
+  hipStream_t st = as_stream(stream);
+  if (n_rows == 0) {
+    HGD_HIP(hipMemsetAsync(dW, 0, static_cast<size_t>(out_features) * in_features * 4, st));
+    if (db) HGD_HIP(hipMemsetAsync(db, 0, static_cast<size_t>(out_features) * 4, st));
+    return HGD_OK;
+  }
+  HGD_REQUIRE(dY && X, "hgd_linear_backward_weight: null dY / X");
+  HGD_REQUIRE(al16(dY, ldy) && al16(X, ldx) && al16(relu_out, ldr),
+              "hgd_linear_backward_weight: rows must be 16-byte aligned");
+  const size_t need = hgd_linear_backward_weight_workspace_size(n_rows, out_features, in_features);
+  if (workspace_bytes < need || !workspace)
+    return fail(HGD_ERR_WORKSPACE, "hgd_linear_backward_weight: workspace %zu < required %zu",
+                workspace_bytes, need);
+  const int64_t S = splits_for(n_rows);
+  int64_t per = (n_rows + S - 1) / S;
+  per = (per + 15) / 16 * 16;
+  SplitK p{};
+  p.A = dY;
+  p.lda = ldy;
+  p.mask = relu_out;
+  p.ldm = ldr;
+  p.B = X;
+  p.ldb = ldx;
+  p.rows = n_rows;
+  p.M = out_features;
+  p.N = in_features;
+  p.rows_per_split = per;
+  p.part = static_cast<float*>(workspace);
+  const size_t part_bytes = align_up(static_cast<size_t>(S) * out_features * in_features * 4);
+  p.part_bias = db ? reinterpret_cast<float*>(static_cast<char*>(workspace) + part_bytes) : nullptr;
+  const int64_t S_used = (n_rows + per - 1) / per;
+  const dim3 grid(static_cast<unsigned>(S_used), static_cast<unsigned>((out_features + 63) / 64),
+                  static_cast<unsigned>((in_features + 63) / 64));
+  if (relu_out)
+    hipLaunchKernelGGL((k_splitk_tn<true>), grid, dim3(256), 0, st, p);
+  else
+    hipLaunchKernelGGL((k_splitk_tn<false>), grid, dim3(256), 0, st, p);
+  hgd_status s = check_launch("hgd_linear_backward_weight");
+  if (s != HGD_OK) return s;
+  s = sum_rows(p.part, S_used, static_cast<int64_t>(out_features) * in_features, dW, st);
+  if (s != HGD_OK || !db) return s;
+  return sum_rows(p.part_bias, S_used, out_features, db, st);
+}

@@ -147,17 +147,83 @@ __global__ __launch_bounds__(kBlock) void k_rowepi_bwd(RowEpiBwd p) {
   }
 }
 
-__global__ void k_colsum(const float* pg, const float* pb, int64_t blocks, int32_t d, float* dg,
-                         float* db) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= d) return;
-  float sg = 0.f, sb = 0.f;
-  for (int64_t b = 0; b < blocks; ++b) {
-    sg += pg[b * d + c];
-    sb += pb[b * d + c];
+// Forward of the row epilogue on an existing matrix Z (hgd_row_epilogue_forward): the same math
+// as hgd_spmm_fused's store, for the LayerNorms that do not follow a hop (the MLP InputNorm of
+// model/layers/MLP.py:65-71,109-110). One lane group per row; statistics by group_sum.
+struct RowEpiFwd {
+  const float* Z;
+  int64_t ldz;
+  int64_t n;
+  int32_t d;
+  hgd_row_epilogue e;
+  float* Y;
+  int64_t ldy;
+};
+
+template <int G, int VEC>
+__global__ __launch_bounds__(kBlock) void k_rowepi_fwd(RowEpiFwd p) {
+  constexpr int GPB = kBlock / G;
+  const int g = threadIdx.x / G;
+  const int l = threadIdx.x % G;
+  const int64_t coff = static_cast<int64_t>(l) * VEC;
+  const bool col_ok = coff < p.d;
+  const hgd_row_epilogue& e = p.e;
+  const float inv_d = 1.f / static_cast<float>(p.d);
+  for (int64_t r = static_cast<int64_t>(blockIdx.x) * GPB + g; r < p.n;
+       r += static_cast<int64_t>(gridDim.x) * GPB) {
+    float v[VEC];
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) v[i] = 0.f;
+    if (col_ok) ld<VEC>(p.Z + r * p.ldz + coff, v);
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      if (e.act == HGD_EPI_LEAKY_RELU) v[i] = v[i] > 0.f ? v[i] : v[i] * e.slope;
+      else if (e.act == HGD_EPI_RELU) v[i] = v[i] > 0.f ? v[i] : 0.f;
+    }
+    if (e.act_out && col_ok) st<VEC>(e.act_out + r * e.ld_act + coff, v);
+    if (e.layer_norm) {
+      float t = 0.f;
+      if (col_ok) {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) t += v[i];
+      }
+      const float mu = group_sum<G>(t) * inv_d;
+      t = 0.f;
+      if (col_ok) {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) t += (v[i] - mu) * (v[i] - mu);
+      }
+      const float rstd = 1.f / sqrtf(group_sum<G>(t) * inv_d + e.ln_eps);
+      if (e.stats && l == 0) {
+        e.stats[2 * r] = mu;
+        e.stats[2 * r + 1] = rstd;
+      }
+      if (col_ok) {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+          const float gm = e.ln_gamma ? e.ln_gamma[coff + i] : 1.f;
+          const float bt = e.ln_beta ? e.ln_beta[coff + i] : 0.f;
+          v[i] = fmaf((v[i] - mu) * rstd, gm, bt);
+        }
+      }
+    }
+    if (!col_ok) continue;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) v[i] *= e.out_scale;
+    if (e.res1) {
+      float rv[VEC];
+      ld<VEC>(e.res1 + r * e.ld_res1 + coff, rv);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) v[i] = fmaf(e.res1_scale, rv[i], v[i]);
+    }
+    if (e.res2) {
+      float rv[VEC];
+      ld<VEC>(e.res2 + r * e.ld_res2 + coff, rv);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) v[i] = fmaf(e.res2_scale, rv[i], v[i]);
+    }
+    st<VEC>(p.Y + r * p.ldy + coff, v);
   }
-  if (dg) dg[c] = sg;
-  if (db) db[c] = sb;
 }
 
 int next_pow2(int x) {
@@ -177,6 +243,20 @@ hgd_status launch(int G, const RowEpiBwd& p, int64_t blocks, hipStream_t st) {
 #undef HGD_CASE
     default:
       return fail(HGD_ERR_UNSUPPORTED, "hgd_row_epilogue_backward: group size %d", G);
+  }
+}
+
+template <int VEC>
+hgd_status launch_fwd(int G, const RowEpiFwd& p, int64_t blocks, hipStream_t st) {
+  switch (G) {
+#define HGD_CASE(GG)                                                                      \
+    case GG:                                                                              \
+      hipLaunchKernelGGL((k_rowepi_fwd<GG, VEC>), dim3(blocks), dim3(kBlock), 0, st, p);  \
+      return check_launch("hgd_row_epilogue_forward");
+    HGD_CASE(1) HGD_CASE(2) HGD_CASE(4) HGD_CASE(8) HGD_CASE(16) HGD_CASE(32) HGD_CASE(64)
+#undef HGD_CASE
+    default:
+      return fail(HGD_ERR_UNSUPPORTED, "hgd_row_epilogue_forward: group size %d", G);
   }
 }
 
@@ -267,9 +347,56 @@ extern "C" hgd_status hgd_row_epilogue_backward(const float* dY, int64_t ldy, co
     if (s != HGD_OK) return s;
   }
   if (want_gb) {
-    hipLaunchKernelGGL(k_colsum, dim3((d + kBlock - 1) / kBlock), dim3(kBlock), 0, st, p.part_g,
-                       p.part_b, blocks, d, dgamma, dbeta);
-    return check_launch("hgd_row_epilogue_backward colsum");
+    if (dgamma) {
+      hgd_status s = sum_rows(p.part_g, blocks, d, dgamma, st);
+      if (s != HGD_OK) return s;
+    }
+    if (dbeta) return sum_rows(p.part_b, blocks, d, dbeta, st);
   }
   return HGD_OK;
+}
+
+extern "C" hgd_status hgd_row_epilogue_forward(const float* Z, int64_t ldz, int64_t n_rows,
+                                               int32_t d, const hgd_row_epilogue* epi, float* Y,
+                                               int64_t ldy, void* stream) {
+  using namespace hgd;
+  clear_error();
+  HGD_REQUIRE(epi != nullptr, "hgd_row_epilogue_forward: null epilogue descriptor");
+  HGD_REQUIRE(d > 0 && n_rows >= 0, "hgd_row_epilogue_forward: bad sizes");
+  HGD_REQUIRE(epi->act >= HGD_EPI_NONE && epi->act <= HGD_EPI_RELU,
+              "hgd_row_epilogue_forward: bad act");
+  HGD_REQUIRE(epi->act == HGD_EPI_NONE || epi->slope >= 0.f,
+              "hgd_row_epilogue_forward: activation needs slope >= 0");
+  HGD_REQUIRE(epi->layer_norm == 0 || epi->layer_norm == 1,
+              "hgd_row_epilogue_forward: layer_norm 0/1");
+  HGD_REQUIRE(ldz >= d && ldy >= d, "hgd_row_epilogue_forward: ldz/ldy < d");
+  HGD_REQUIRE((!epi->res1 || epi->ld_res1 >= d) && (!epi->res2 || epi->ld_res2 >= d) &&
+                  (!epi->act_out || epi->ld_act >= d),
+              "hgd_row_epilogue_forward: leading dimension < d");
+  if (n_rows == 0) return HGD_OK;
+  HGD_REQUIRE(Z && Y, "hgd_row_epilogue_forward: null Z/Y");
+  auto al16 = [](const void* p, int64_t ld) {
+    return p == nullptr || (reinterpret_cast<uintptr_t>(p) % 16 == 0 && ld % 4 == 0);
+  };
+  const bool aligned = d % 4 == 0 && al16(Z, ldz) && al16(Y, ldy) &&
+                       al16(epi->res1, epi->ld_res1) && al16(epi->res2, epi->ld_res2) &&
+                       al16(epi->act_out, epi->ld_act);
+  const int G = aligned ? (d / 4 >= 64 ? 64 : next_pow2(d / 4)) : (d >= 64 ? 64 : next_pow2(d));
+  const int span = aligned ? 4 * G : G;
+  if (span < d)
+    return fail(HGD_ERR_UNSUPPORTED,
+                "hgd_row_epilogue_forward: needs d <= 256 (aligned rows) or d <= 64 (got %d)", d);
+  RowEpiFwd p{};
+  p.Z = Z;
+  p.ldz = ldz;
+  p.n = n_rows;
+  p.d = d;
+  p.e = *epi;
+  p.Y = Y;
+  p.ldy = ldy;
+  const int64_t gpb = kBlock / G;
+  int64_t blocks = (n_rows + gpb - 1) / gpb;
+  if (blocks > 4096) blocks = 4096;
+  return aligned ? launch_fwd<4>(G, p, blocks, as_stream(stream))
+                 : launch_fwd<1>(G, p, blocks, as_stream(stream));
 }

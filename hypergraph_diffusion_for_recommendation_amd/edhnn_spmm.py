@@ -23,7 +23,7 @@ import torch.nn.functional as F
 
 from .functional import two_hop_fused
 from .incidence import incidence_of
-from .layers import MLP, HGCNConv
+from .layers import MLP, HGCNConv, LayerNorm, Linear
 
 
 class EquivSetConv(nn.Module):
@@ -49,7 +49,7 @@ class EquivSetConv(nn.Module):
         self.data = data
         self.hgcn_layers = nn.ModuleList([HGCNConv(leaky) for _ in range(2)])
         self.mean_pooling = nn.AdaptiveAvgPool1d(out_features)
-        self.lns = nn.ModuleList([nn.LayerNorm(out_features) for _ in range(2)])
+        self.lns = nn.ModuleList([LayerNorm(out_features) for _ in range(2)])
         self.fused_epilogue = True  # False: the reference's separate LN / add / blend ops
 
     def reset_parameters(self):
@@ -103,7 +103,7 @@ class EquivSetGNN(nn.Module):
         self.mlp3_layers = (args['MLP_num_layers'] if args['MLP3_num_layers'] < 0
                             else args['MLP3_num_layers'])
         self.nlayer = args['All_num_layers']
-        self.lin_in = nn.Linear(num_features, args['MLP_hidden'])
+        self.lin_in = Linear(num_features, args['MLP_hidden'])
         self.conv = EquivSetConv(args['MLP_hidden'], args['MLP_hidden'], ncount, mcount,
                                  mlp1_layers=self.mlp1_layers, mlp2_layers=self.mlp2_layers,
                                  mlp3_layers=self.mlp3_layers, alpha=args['restart_alpha'],
@@ -118,7 +118,7 @@ class EquivSetGNN(nn.Module):
 
     def forward(self, x, sparse_norm_adj, n_nodes, act=True):
         x = self.dropout(x)
-        x = F.relu(self.lin_in(x))
+        x = self.lin_in(x, relu=True)  # F.relu(lin_in(x)) fused
         x0 = x
         for _ in range(self.nlayer):
             x = self.dropout(x)

@@ -8,7 +8,8 @@ encoder (paths relative to /root/reference/HD_SELFRec):
 * :class:`HCCFEncoder`       model/graph/HCCF.py:136-191
 * :class:`LocalAwareEncoder` model/graph/HGNN_HD4.py:336-405 (``--mode=local_only``)
 
-Everything sparse runs on libhgd; dropout, the dense ``E·W`` products and LayerNorm stay torch.
+Everything sparse runs on libhgd, with the LayerNorm / residual after a hop fused into its store;
+dropout and HCCF's dense ``E·W`` products stay torch.
 """
 from __future__ import annotations
 
@@ -16,8 +17,9 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from .incidence import Incidence
-from .layers import EquivSetGNN, GCNLayer, HGCNConv, HGNNLayer, SpAdjDropEdge
+from .functional import two_hop_fused
+from .incidence import Incidence, incidence_of
+from .layers import EquivSetGNN, GCNLayer, HGCNConv, HGNNLayer, LayerNorm, SpAdjDropEdge
 
 
 def sparse_tensor_of(mat, device) -> torch.Tensor:
@@ -129,7 +131,7 @@ class LocalAwareEncoder(nn.Module):
         self.hgcn_layers = nn.ModuleList([HGCNConv(leaky=0.5) for _ in range(self.layers)])
         self.edhnn_layers = nn.ModuleList(
             [EquivSetGNN(hyper_size, self.edhnn_args, None, data) for _ in range(self.layers)])
-        self.lns = nn.ModuleList([nn.LayerNorm(hyper_size) for _ in range(self.layers)])
+        self.lns = nn.ModuleList([LayerNorm(hyper_size) for _ in range(self.layers)])
         self.edhnn_ui_n = data.n_items + data.n_users
         ui = data.ui_adj.tocsr().copy()
         ui.sort_indices()  # nonzero(dense > 0) order: rows, then ascending columns
@@ -145,8 +147,9 @@ class LocalAwareEncoder(nn.Module):
                 ego_embeddings = self.edhnn_layers[k](ego_embeddings, self.hypergraph,
                                                       self.edhnn_ui_n) + res
             else:
-                ego_embeddings = self.lns[0](self.hgcn_layers[0](sparse_norm_adj, ego_embeddings,
-                                                                 act=False)) + res
+                # LN0(HGCNConv(Â, x, act=False)) + res in one fused hop store
+                ego_embeddings = two_hop_fused(incidence_of(sparse_norm_adj), ego_embeddings,
+                                               norm=self.lns[0], res1=res, res1_scale=1.0)
             all_embeddings += [ego_embeddings]
         nu = self.data.n_users
         return all_embeddings[-1][:nu], all_embeddings[-1][nu:]

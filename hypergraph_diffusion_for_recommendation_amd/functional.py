@@ -23,6 +23,7 @@ diagonals swapped.
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Optional
 
 import torch
@@ -245,3 +246,168 @@ def two_hop_fused(inc: Incidence, X: torch.Tensor, P: Optional[str] = None,
     cfg = (P, Q, R, epi, float(slope), ln, float(norm.eps) if ln else 0.0, float(out_scale),
            float(res1_scale), float(res2_scale))
     return _FusedTwoHop.apply(X, gamma, beta, res1, res2, inc, cfg)
+
+
+def _linear_native_ok(X: torch.Tensor, weight: torch.Tensor) -> bool:
+    out_f, in_f = weight.shape
+    return (X.is_cuda and X.dtype == torch.float32 and weight.dtype == torch.float32
+            and in_f % 16 == 0 and out_f % 16 == 0 and 16 <= in_f <= 128 and 16 <= out_f <= 128)
+
+
+class _Linear(torch.autograd.Function):
+    """``relu?(X·Wᵀ + b)`` on hgd_linear_* (f32 MFMA; forward, backward-data, split-K
+    backward-weight with the bias gradient folded in)."""
+
+    @staticmethod
+    def forward(ctx, X, weight, bias, relu: bool):
+        lib = nat.load()
+        X = X.contiguous()
+        W = weight.contiguous()
+        n, in_f = X.shape
+        out_f = W.shape[0]
+        Y = torch.empty((n, out_f), dtype=torch.float32, device=X.device)
+        st = torch.cuda.current_stream(X.device).cuda_stream
+        nat.check(lib.hgd_linear_forward(X.data_ptr(), X.stride(0), n, in_f, W.data_ptr(),
+                                         W.stride(0), out_f, nat.ptr(bias), int(relu),
+                                         Y.data_ptr(), Y.stride(0), st), "hgd_linear_forward")
+        ctx.relu = relu
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(X, W, Y if relu else None)
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        lib = nat.load()
+        X, W, Y = ctx.saved_tensors
+        dY = dY.contiguous()
+        n, in_f = X.shape
+        out_f = W.shape[0]
+        st = torch.cuda.current_stream(dY.device).cuda_stream
+        dX = dW = db = None
+        if ctx.needs_input_grad[0]:
+            dX = torch.empty_like(X)
+            nat.check(lib.hgd_linear_backward_data(
+                dY.data_ptr(), dY.stride(0), nat.ptr(Y), 0 if Y is None else Y.stride(0), n,
+                out_f, W.data_ptr(), W.stride(0), in_f, dX.data_ptr(), dX.stride(0), st),
+                "hgd_linear_backward_data")
+        want_b = ctx.has_bias and ctx.needs_input_grad[2]
+        if ctx.needs_input_grad[1] or want_b:
+            dW = torch.empty((out_f, in_f), dtype=torch.float32, device=dY.device)
+            db = torch.empty(out_f, dtype=torch.float32, device=dY.device) if want_b else None
+            wsb = lib.hgd_linear_backward_weight_workspace_size(n, out_f, in_f)
+            ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dY.device)
+            nat.check(lib.hgd_linear_backward_weight(
+                dY.data_ptr(), dY.stride(0), nat.ptr(Y), 0 if Y is None else Y.stride(0),
+                X.data_ptr(), X.stride(0), n, out_f, in_f, dW.data_ptr(), nat.ptr(db),
+                ws.data_ptr(), wsb, st), "hgd_linear_backward_weight")
+            if not ctx.needs_input_grad[1]:
+                dW = None
+        return dX, dW, db, None
+
+
+def linear(X: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None,
+           relu: bool = False) -> torch.Tensor:
+    """``F.linear`` (optionally followed by ``F.relu``) for the skinny ED-HNN shapes: features
+    multiples of 16 up to 128 run on hgd_linear_*; other shapes use the library GEMM."""
+    if not _linear_native_ok(X, weight):
+        Y = torch.nn.functional.linear(X, weight, bias)
+        return torch.relu(Y) if relu else Y
+    lead = X.shape[:-1]
+    Y = _Linear.apply(X.reshape(-1, X.shape[-1]), weight, bias, bool(relu))
+    return Y.reshape(*lead, weight.shape[0])
+
+
+class _RowEpilogue(torch.autograd.Function):
+    """``out_scale·LN(act(Z)) + s1·res1 + s2·res2`` on an existing matrix
+    (hgd_row_epilogue_forward / hgd_row_epilogue_backward)."""
+
+    @staticmethod
+    def forward(ctx, Z, gamma, beta, res1, res2, cfg):
+        epi, slope, ln, eps, out_scale, s1, s2 = cfg
+        Z = Z.contiguous()
+        n, d = Z.shape
+        dev = Z.device
+        need_a = ln or epi != nat.EPI_NONE
+        A = (Z if epi == nat.EPI_NONE else torch.empty_like(Z)) if need_a else None
+        stats = torch.empty((n, 2), dtype=torch.float32, device=dev) if ln else None
+        res1 = None if res1 is None else res1.contiguous()
+        res2 = None if res2 is None else res2.contiguous()
+        ex = nat.RowEpilogue(
+            act=epi, slope=slope, layer_norm=int(ln), ln_eps=eps,
+            ln_gamma=nat.ptr(gamma) if ln else None, ln_beta=nat.ptr(beta) if ln else None,
+            out_scale=out_scale,
+            res1=nat.ptr(res1), ld_res1=0 if res1 is None else res1.stride(0), res1_scale=s1,
+            res2=nat.ptr(res2), ld_res2=0 if res2 is None else res2.stride(0), res2_scale=s2,
+            act_out=nat.ptr(A) if (A is not None and A is not Z) else None,
+            ld_act=0 if A is None else A.stride(0), stats=nat.ptr(stats))
+        Y = torch.empty_like(Z)
+        nat.check(nat.load().hgd_row_epilogue_forward(
+            Z.data_ptr(), Z.stride(0), n, d, ctypes.byref(ex), Y.data_ptr(), Y.stride(0),
+            torch.cuda.current_stream(dev).cuda_stream), "hgd_row_epilogue_forward")
+        ctx.cfg = cfg
+        ctx.has_res = (res1 is not None, res2 is not None)
+        ctx.save_for_backward(A, stats, gamma if ln else None)
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        epi, slope, ln, eps, out_scale, s1, s2 = ctx.cfg
+        A, stats, gamma = ctx.saved_tensors
+        dY = dY.contiguous()
+        n, d = dY.shape
+        dev = dY.device
+        lib = nat.load()
+        want_g = ln and ctx.needs_input_grad[1]
+        want_b = ln and ctx.needs_input_grad[2]
+        dgamma = torch.empty(d, dtype=torch.float32, device=dev) if want_g else None
+        dbeta = torch.empty(d, dtype=torch.float32, device=dev) if want_b else None
+        wsb = lib.hgd_row_epilogue_backward_workspace_size(n, d) if (want_g or want_b) else 0
+        ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev) if wsb else None
+        dZ = None
+        if ctx.needs_input_grad[0] or want_g or want_b:
+            dZ = torch.empty_like(dY)
+            nat.check(lib.hgd_row_epilogue_backward(
+                dY.data_ptr(), dY.stride(0), nat.ptr(A), 0 if A is None else A.stride(0),
+                nat.ptr(stats), nat.ptr(gamma), n, d, epi, float(slope), int(ln),
+                float(out_scale), dZ.data_ptr(), dZ.stride(0), nat.ptr(dgamma), nat.ptr(dbeta),
+                nat.ptr(ws), wsb, torch.cuda.current_stream(dev).cuda_stream),
+                "hgd_row_epilogue_backward")
+
+        def res_grad(k, s):
+            if not ctx.has_res[k] or not ctx.needs_input_grad[3 + k]:
+                return None
+            return dY if s == 1.0 else dY * s
+
+        return (dZ if ctx.needs_input_grad[0] else None, dgamma, dbeta, res_grad(0, s1),
+                res_grad(1, s2), None)
+
+
+def row_epilogue(Z: torch.Tensor, epilogue: Optional[str] = None, slope: float = 0.0,
+                 norm: Optional[torch.nn.LayerNorm] = None, out_scale: float = 1.0,
+                 res1: Optional[torch.Tensor] = None, res1_scale: float = 1.0,
+                 res2: Optional[torch.Tensor] = None, res2_scale: float = 1.0) -> torch.Tensor:
+    """The fused store of :func:`two_hop_fused` applied to an existing [n, d] matrix."""
+    epi = _EPI[epilogue]
+    d = Z.shape[-1]
+    ln = norm is not None
+    if (Z.dim() != 2 or not Z.is_cuda or Z.dtype != torch.float32 or not _ln_supported(d)
+            or (epi != nat.EPI_NONE and slope < 0)):
+        raise ValueError("row_epilogue: needs a 2-D float32 device matrix with d <= 256 "
+                         "(d <= 64 when d % 4 != 0) and slope >= 0")
+    gamma = norm.weight if ln and norm.weight is not None else None
+    beta = norm.bias if ln and norm.bias is not None else None
+    cfg = (epi, float(slope), ln, float(norm.eps) if ln else 0.0, float(out_scale),
+           float(res1_scale), float(res2_scale))
+    return _RowEpilogue.apply(Z, gamma, beta, res1, res2, cfg)
+
+
+def layer_norm(x: torch.Tensor, norm: torch.nn.LayerNorm) -> torch.Tensor:
+    """``norm(x)`` for a LayerNorm over the last dim: hgd_row_epilogue_* on device float32 rows
+    that fit one lane group, the library op otherwise."""
+    d = x.shape[-1]
+    if (x.is_cuda and x.dtype == torch.float32 and tuple(norm.normalized_shape) == (d,)
+            and _ln_supported(d) and x.numel() > 0):
+        lead = x.shape[:-1]
+        return row_epilogue(x.reshape(-1, d), norm=norm).reshape(*lead, d)
+    return torch.nn.functional.layer_norm(x, norm.normalized_shape, norm.weight, norm.bias,
+                                          norm.eps)

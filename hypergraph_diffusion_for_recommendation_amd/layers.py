@@ -29,7 +29,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .functional import spmm, two_hop, two_hop_fused
+from .functional import layer_norm, linear, spmm, two_hop, two_hop_fused
 from .incidence import (CSR, Incidence, dense_threshold, drop_edges, expand_rows,
                         incidence_of)
 
@@ -121,6 +121,24 @@ class SpAdjDropEdge(nn.Module):
         return out
 
 
+class Linear(nn.Linear):
+    """nn.Linear (same parameters and state_dict) whose forward runs hgd_linear_* for the skinny
+    shapes of the ED-HNN block (functional.linear); ``forward(x, relu=True)`` fuses the ReLU
+    that follows lin_in and the hidden MLP layers."""
+
+    def forward(self, x, relu: bool = False):
+        return linear(x, self.weight, self.bias, relu)
+
+
+class LayerNorm(nn.LayerNorm):
+    """nn.LayerNorm (same parameters and state_dict) running hgd_row_epilogue_* for device fp32
+    rows of up to 256 features (functional.layer_norm): one pass forward, one pass backward
+    with the γ/β gradients, instead of the library's three kernels."""
+
+    def forward(self, x):
+        return layer_norm(x, self)
+
+
 class MLP(nn.Module):
     """Same parameter layout and forward as model/layers/MLP.py:29-117 (adapted from
     CorrectAndSmooth): [norm] → (Linear → ReLU → norm → dropout)* → Linear."""
@@ -135,7 +153,7 @@ class MLP(nn.Module):
         self.normalizations = nn.ModuleList()
         self.InputNorm = InputNorm
         assert Normalization in ['bn', 'ln', 'None']
-        norm = {'bn': nn.BatchNorm1d, 'ln': nn.LayerNorm, 'None': None}[Normalization]
+        norm = {'bn': nn.BatchNorm1d, 'ln': LayerNorm, 'None': None}[Normalization]
 
         def mk(c):
             return norm(c) if norm is not None else nn.Identity()
@@ -143,14 +161,14 @@ class MLP(nn.Module):
         first = mk(in_channels) if (InputNorm and norm is not None) else nn.Identity()
         self.normalizations.append(first)
         if num_layers == 1:
-            self.lins.append(nn.Linear(in_channels, out_channels))
+            self.lins.append(Linear(in_channels, out_channels))
         else:
-            self.lins.append(nn.Linear(in_channels, hidden_channels))
+            self.lins.append(Linear(in_channels, hidden_channels))
             self.normalizations.append(mk(hidden_channels))
             for _ in range(num_layers - 2):
-                self.lins.append(nn.Linear(hidden_channels, hidden_channels))
+                self.lins.append(Linear(hidden_channels, hidden_channels))
                 self.normalizations.append(mk(hidden_channels))
-            self.lins.append(nn.Linear(hidden_channels, out_channels))
+            self.lins.append(Linear(hidden_channels, out_channels))
         self.dropout = dropout
 
     def reset_parameters(self):
@@ -163,8 +181,7 @@ class MLP(nn.Module):
     def forward(self, x):
         x = self.normalizations[0](x)
         for i, lin in enumerate(self.lins[:-1]):
-            x = lin(x)
-            x = F.relu(x, inplace=True)
+            x = lin(x, relu=True)  # Linear → ReLU fused
             x = self.normalizations[i + 1](x)
             x = F.dropout(x, p=self.dropout, training=self.training)
         return self.lins[-1](x)
@@ -298,7 +315,7 @@ class EquivSetGNN(nn.Module):
         self.mlp3_layers = (args['MLP_num_layers'] if args['MLP3_num_layers'] < 0
                             else args['MLP3_num_layers'])
         self.nlayer = args['All_num_layers']
-        self.lin_in = nn.Linear(num_features, args['MLP_hidden'])
+        self.lin_in = Linear(num_features, args['MLP_hidden'])
         self.conv = EquivSetConv(args['MLP_hidden'], args['MLP_hidden'],
                                  mlp1_layers=self.mlp1_layers, mlp2_layers=self.mlp2_layers,
                                  mlp3_layers=self.mlp3_layers, alpha=args['restart_alpha'],
@@ -315,7 +332,7 @@ class EquivSetGNN(nn.Module):
     def forward(self, x, hypergraph, n_nodes):
         V, E = self.generate_V_E(n_nodes, hypergraph)
         x = self.dropout(x)
-        x = F.relu(self.lin_in(x))
+        x = self.lin_in(x, relu=True)  # F.relu(lin_in(x)) fused
         x0 = x
         for _ in range(self.nlayer):
             x = self.dropout(x)

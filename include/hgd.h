@@ -156,6 +156,13 @@ hgd_status hgd_spmm_fused(const int64_t* rowptr, const int32_t* col, const float
                           const hgd_split_plan* plan, void* workspace, size_t workspace_bytes,
                           void* stream);
 
+/* The same row epilogue applied to an existing matrix Z [n_rows, ldz] (z = Z[r], no hop): the
+ * LayerNorms that do not follow a hop, e.g. the MLP InputNorm of model/layers/MLP.py:65-71,109-110.
+ * Needs d <= 256 with 16-byte aligned rows, or d <= 64. Y may alias Z. */
+hgd_status hgd_row_epilogue_forward(const float* Z, int64_t ldz, int64_t n_rows, int32_t d,
+                                    const hgd_row_epilogue* epi, float* Y, int64_t ldy,
+                                    void* stream);
+
 /* Backward of the row epilogue up to z (the residual gradients are res_scale·dY, left to the
  * caller): dZ = act'(a) ⊙ LN_bwd(out_scale·dY), with LN_bwd the LayerNorm input gradient
  * rstd·(ĝ - mean(ĝ) - â·mean(ĝ⊙â)), ĝ = γ⊙dy, â = (a-μ)·rstd recomputed from act_out and stats.
@@ -168,6 +175,34 @@ hgd_status hgd_row_epilogue_backward(const float* dY, int64_t ldy, const float* 
                                      int32_t layer_norm, float out_scale, float* dZ, int64_t ldz,
                                      float* dgamma, float* dbeta, void* workspace,
                                      size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Skinny Linear layers on the f32 MFMA: nn.Linear(in, out) over
+ * n_rows ≫ in, out — lin_in of model/layers/EquivSetGNN.py:88-89 /
+ * layers2/EquivSetGNN2.py:93-94 (with its F.relu) and the MLP layers of
+ * model/layers/MLP.py:109-117. W is [out_features, ldw] row-major (nn.Linear.weight); features
+ * are multiples of 16, rows 16-byte aligned. Forward: in_features <= 128; backward-data:
+ * out_features <= 128. Exact f32 products and sums (order differs from a library GEMM).
+ *   forward          Y = relu?(X·Wᵀ + bias)
+ *   backward_data    dX = (dY ⊙ [relu_out > 0])·W        (relu_out = the forward Y, or NULL)
+ *   backward_weight  dW = (dY ⊙ [relu_out > 0])ᵀ·X, db = Σ_rows dY ⊙ [relu_out > 0]
+ *                    (dW written contiguous [out, in]; split-K partials summed in a fixed order)
+ * ---------------------------------------------------------------------------------------- */
+hgd_status hgd_linear_forward(const float* X, int64_t ldx, int64_t n_rows, int32_t in_features,
+                              const float* W, int64_t ldw, int32_t out_features,
+                              const float* bias, int32_t relu, float* Y, int64_t ldy,
+                              void* stream);
+hgd_status hgd_linear_backward_data(const float* dY, int64_t ldy, const float* relu_out,
+                                    int64_t ldr, int64_t n_rows, int32_t out_features,
+                                    const float* W, int64_t ldw, int32_t in_features, float* dX,
+                                    int64_t ldx, void* stream);
+size_t hgd_linear_backward_weight_workspace_size(int64_t n_rows, int32_t out_features,
+                                                 int32_t in_features);
+hgd_status hgd_linear_backward_weight(const float* dY, int64_t ldy, const float* relu_out,
+                                      int64_t ldr, const float* X, int64_t ldx, int64_t n_rows,
+                                      int32_t out_features, int32_t in_features, float* dW,
+                                      float* db, void* workspace, size_t workspace_bytes,
+                                      void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Structure primitives (all deterministic; indices bit-exact with the CPU restatement).

@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Microbenchmark of the skinny Linear kernels (hgd_linear_*) against the library GEMMs torch
+uses for the same products, at ED-HNN shapes: rows × d → d. Prints one JSON line per case with
+device times from HIP events (median of --reps) and the achieved HBM rate on the algorithmic
+bytes (inputs read once, outputs written once)."""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, nargs="+", default=[69_716, 2_200_000])
+    ap.add_argument("--dim", type=int, default=64)
+    ap.add_argument("--reps", type=int, default=50)
+    args = ap.parse_args()
+    import torch
+
+    from hypergraph_diffusion_for_recommendation_amd import _native as nat
+
+    lib = nat.load()
+    dev = torch.device("cuda")
+    d = args.dim
+
+    def timed(fn):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(args.reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1e3)
+        return statistics.median(ts)
+
+    for n in args.rows:
+        X = torch.randn(n, d, device=dev)
+        W = torch.randn(d, d, device=dev)
+        b = torch.randn(d, device=dev)
+        dY = torch.randn(n, d, device=dev)
+        Y = torch.empty(n, d, device=dev)
+        dX = torch.empty(n, d, device=dev)
+        dW = torch.empty(d, d, device=dev)
+        db = torch.empty(d, device=dev)
+        wsb = lib.hgd_linear_backward_weight_workspace_size(n, d, d)
+        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        st = torch.cuda.current_stream().cuda_stream
+        cases = {
+            "fwd_hgd": lambda: lib.hgd_linear_forward(X.data_ptr(), d, n, d, W.data_ptr(), d, d,
+                                                      b.data_ptr(), 1, Y.data_ptr(), d, st),
+            "fwd_torch": lambda: torch.relu(torch.nn.functional.linear(X, W, b)),
+            "bwd_data_hgd": lambda: lib.hgd_linear_backward_data(
+                dY.data_ptr(), d, Y.data_ptr(), d, n, d, W.data_ptr(), d, d, dX.data_ptr(), d,
+                st),
+            "bwd_data_torch": lambda: torch.mm(dY * (Y > 0), W),
+            "bwd_weight_hgd": lambda: lib.hgd_linear_backward_weight(
+                dY.data_ptr(), d, None, 0, X.data_ptr(), d, n, d, d, dW.data_ptr(),
+                db.data_ptr(), ws.data_ptr(), wsb, st),
+            "bwd_weight_torch": lambda: (torch.mm(dY.t(), X), dY.sum(0)),
+        }
+        algo = {"fwd": 2 * n * d * 4, "bwd_data": 3 * n * d * 4, "bwd_weight": 2 * n * d * 4}
+        for name, fn in cases.items():
+            us = timed(fn)
+            kind = name.rsplit("_", 1)[0]
+            print(json.dumps({"case": name, "rows": n, "d": d, "us": round(us, 2),
+                              "alg_GBps": round(algo[kind] / us / 1e3, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

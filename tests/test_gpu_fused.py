@@ -195,3 +195,51 @@ def test_fused_rejects_bad_descriptor(dev):
     st = lib.hgd_spmm_fused(rowptr.data_ptr(), None, None, None, 2, 0, 0, 2, None, 300,
                             Y.data_ptr(), 300, 300, ctypes.byref(ex), None, None, 0, None)
     assert st == 3
+
+
+@pytest.mark.parametrize("d", [3, 16, 64, 100, 256])
+def test_layer_norm_module_matches_torch(dev, d):
+    """layers.LayerNorm (hgd_row_epilogue_forward/backward) vs nn.LayerNorm: output and the
+    input / γ / β gradients."""
+    from hypergraph_diffusion_for_recommendation_amd.layers import LayerNorm
+    torch.manual_seed(d)
+    ref = torch.nn.LayerNorm(d).to(dev)
+    with torch.no_grad():
+        ref.weight.uniform_(0.5, 1.5)
+        ref.bias.normal_()
+    ours = LayerNorm(d).to(dev)
+    ours.load_state_dict(ref.state_dict())
+    x = (torch.randn(5003, d, device=dev) * 3 + 1)
+    dY = torch.randn(5003, d, device=dev)
+    outs = []
+    for m in (ours, ref):
+        xx = x.clone().requires_grad_(True)
+        y = m(xx)
+        g = torch.autograd.grad(y, (xx, m.weight, m.bias), dY)
+        outs.append((y.detach(),) + tuple(g))
+    for name, a, b in zip(("y", "dx", "dgamma", "dbeta"), *outs):
+        s = b.abs().max().item()
+        tol = 2e-5 if name in ("y", "dx") else 2e-5 * 50
+        assert (a - b).abs().max().item() <= tol * s, name
+
+
+def test_row_epilogue_standalone_vs_oracle(dev):
+    from hypergraph_diffusion_for_recommendation_amd.functional import row_epilogue
+    rng = np.random.default_rng(8)
+    n, d = 777, 64
+    Z = rng.standard_normal((n, d)).astype(np.float32)
+    R1 = rng.standard_normal((n, d)).astype(np.float32)
+    dY = rng.standard_normal((n, d)).astype(np.float32)
+    norm = torch.nn.LayerNorm(d).to(dev)
+    with torch.no_grad():
+        norm.weight.uniform_(0.5, 1.5)
+        norm.bias.normal_()
+    Zt = torch.from_numpy(Z).to(dev).requires_grad_(True)
+    Y = row_epilogue(Zt, "leaky_relu", 0.2, norm, 0.6, torch.from_numpy(R1).to(dev), 0.4)
+    (gZ,) = torch.autograd.grad(Y, Zt, torch.from_numpy(dY).to(dev))
+    g = norm.weight.detach().cpu().numpy()
+    b = norm.bias.detach().cpu().numpy()
+    Yref, a = O.row_epilogue(Z, "leaky_relu", 0.2, True, g, b, 1e-5, 0.6, R1, 0.4)
+    np.testing.assert_allclose(Y.detach().cpu().numpy(), Yref, rtol=0, atol=2e-5 * np.abs(Yref).max())
+    dZ, _, _ = O.row_epilogue_backward(Z, dY, "leaky_relu", 0.2, True, g, 1e-5, 0.6)
+    np.testing.assert_allclose(gZ.cpu().numpy(), dZ, rtol=0, atol=2e-5 * np.abs(dZ).max())
