@@ -101,6 +101,13 @@ _SIGNATURES = {
     "hgd_linear_backward_weight": (c_i32, [c_void_p, c_i64, c_void_p, c_i64, c_void_p, c_i64,
                                            c_i64, c_i32, c_i32, c_void_p, c_void_p, c_void_p,
                                            c_size, c_void_p]),
+    "hgd_infonce_workspace_size": (c_size, [c_i64, c_i32]),
+    "hgd_infonce_forward": (c_i32, [c_void_p, c_i64, c_void_p, c_i64, c_i64, c_void_p, c_i64,
+                                    c_i32, c_f32, c_void_p, c_void_p, c_void_p, c_void_p,
+                                    c_void_p, c_void_p, c_void_p, c_void_p, c_size, c_void_p]),
+    "hgd_infonce_backward": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_i64,
+                                     c_i32, c_f32, c_void_p, c_void_p, c_void_p, c_void_p,
+                                     c_size, c_void_p]),
     "hgd_index_narrow": (c_i32, [c_void_p, c_i64, c_i64, c_void_p, c_void_p, c_void_p]),
     "hgd_sort_perm_workspace_size": (c_size, [c_i64]),
     "hgd_sort_perm": (c_i32, [c_void_p, c_i64, c_i64, c_void_p, c_void_p, c_void_p, c_size,

@@ -411,3 +411,72 @@ def layer_norm(x: torch.Tensor, norm: torch.nn.LayerNorm) -> torch.Tensor:
         return row_epilogue(x.reshape(-1, d), norm=norm).reshape(*lead, d)
     return torch.nn.functional.layer_norm(x, norm.normalized_shape, norm.weight, norm.bias,
                                           norm.eps)
+
+
+class _ContrastLoss(torch.autograd.Function):
+    """hgd_infonce_forward / hgd_infonce_backward (see contrast_loss)."""
+
+    @staticmethod
+    def forward(ctx, E1, E2, nodes, temp: float):
+        lib = nat.load()
+        dev = E1.device
+        E1c = E1 if E1.stride(1) == 1 else E1.contiguous()
+        E2c = E2 if E2.stride(1) == 1 else E2.contiguous()
+        nodes = nodes.to(device=dev, dtype=torch.int64).contiguous()
+        B, d = nodes.numel(), E1.shape[1]
+        f = dict(dtype=torch.float32, device=dev)
+        P1, P2 = torch.empty((B, d), **f), torch.empty((B, d), **f)
+        inv1, inv2, pos, deno = (torch.empty(B, **f) for _ in range(4))
+        loss = torch.empty((), **f)
+        wsb = lib.hgd_infonce_workspace_size(B, d)
+        ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+        st = torch.cuda.current_stream(dev).cuda_stream
+        nat.check(lib.hgd_infonce_forward(
+            E1c.data_ptr(), E1c.stride(0), E2c.data_ptr(), E2c.stride(0), E1.shape[0],
+            nodes.data_ptr(), B, d, float(temp), P1.data_ptr(), P2.data_ptr(), inv1.data_ptr(),
+            inv2.data_ptr(), pos.data_ptr(), deno.data_ptr(), loss.data_ptr(), ws.data_ptr(), wsb,
+            st), "hgd_infonce_forward")
+        ctx.temp = float(temp)
+        ctx.shapes = (E1.shape, E2.shape)
+        ctx.save_for_backward(P1, P2, inv1, inv2, deno, nodes)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        lib = nat.load()
+        P1, P2, inv1, inv2, deno, nodes = ctx.saved_tensors
+        B, d = P1.shape
+        dev = P1.device
+        g = g.to(dtype=torch.float32).reshape(1).contiguous()
+        dX1, dX2 = torch.empty_like(P1), torch.empty_like(P2)
+        wsb = lib.hgd_infonce_workspace_size(B, d)
+        ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+        nat.check(lib.hgd_infonce_backward(
+            P1.data_ptr(), P2.data_ptr(), inv1.data_ptr(), inv2.data_ptr(), deno.data_ptr(), B, d,
+            ctx.temp, g.data_ptr(), dX1.data_ptr(), dX2.data_ptr(), ws.data_ptr(), wsb,
+            torch.cuda.current_stream(dev).cuda_stream), "hgd_infonce_backward")
+        dE1 = dE2 = None
+        if ctx.needs_input_grad[0]:
+            dE1 = torch.zeros(ctx.shapes[0], dtype=torch.float32, device=dev)
+            dE1.index_add_(0, nodes, dX1)
+        if ctx.needs_input_grad[1]:
+            dE2 = torch.zeros(ctx.shapes[1], dtype=torch.float32, device=dev)
+            dE2.index_add_(0, nodes, dX2)
+        return dE1, dE2, None, None
+
+
+def contrast_loss(embeds1: torch.Tensor, embeds2: torch.Tensor, nodes: torch.Tensor,
+                  temp: float) -> torch.Tensor:
+    """``contrastLoss(embeds1, embeds2, nodes, temp)`` of util/loss_torch.py:103-110 (InfoNCE over
+    the batch rows ``nodes``), fused: only the B batch rows are normalised and the [B, B]
+    logits are never materialised. Device float32 tables with d a multiple of 16 up to 256;
+    other inputs are rejected (the reference formula is three lines of torch for those)."""
+    d = embeds1.shape[-1]
+    if (embeds1.dim() != 2 or embeds2.shape != embeds1.shape or not embeds1.is_cuda
+            or embeds1.dtype != torch.float32 or embeds2.dtype != torch.float32
+            or d % 16 != 0 or not 16 <= d <= 256):
+        raise ValueError("contrast_loss: needs two float32 device tables [N, d] with d a "
+                         "multiple of 16 in [16, 256]")
+    if nodes.numel() == 0:
+        raise ValueError("contrast_loss: empty batch")
+    return _ContrastLoss.apply(embeds1, embeds2, nodes, float(temp))

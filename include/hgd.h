@@ -205,6 +205,29 @@ hgd_status hgd_linear_backward_weight(const float* dY, int64_t ldy, const float*
                                       void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * Fused InfoNCE, contrastLoss of util/loss_torch.py:103-110:
+ *   p1 = normalize(E1[nodes] + 1e-8), p2 = normalize(E2[nodes] + 1e-8)   (eps 1e-12)
+ *   loss = -(1/B) Σ_b log( exp(<p1_b,p2_b>/τ) / (Σ_j exp(<p1_b,p2_j>/τ) + 1e-8) )
+ * Only the B batch rows are gathered and normalised; the [B, B] exp-sum is never materialised.
+ * Forward writes P1, P2 [B, d] (contiguous), inv_norm1/2 [B], pos_logit [B], deno [B] and the
+ * scalar loss (all device). Backward recomputes the logits and writes dX1, dX2 [B, d] =
+ * dloss/d(E1[nodes]), dloss/d(E2[nodes]) scaled by the device scalar *grad_loss; scattering
+ * them into the [N, d] table gradients (duplicate nodes add) is the caller's. d: multiple of 16
+ * in [16, 256]. Deterministic (fixed-order reductions). Workspace: hgd_infonce_workspace_size.
+ * ---------------------------------------------------------------------------------------- */
+size_t hgd_infonce_workspace_size(int64_t batch, int32_t d);
+hgd_status hgd_infonce_forward(const float* E1, int64_t ld1, const float* E2, int64_t ld2,
+                               int64_t n_rows, const int64_t* nodes, int64_t batch, int32_t d,
+                               float temp, float* P1, float* P2, float* inv_norm1,
+                               float* inv_norm2, float* pos_logit, float* deno, float* loss,
+                               void* workspace, size_t workspace_bytes, void* stream);
+hgd_status hgd_infonce_backward(const float* P1, const float* P2, const float* inv_norm1,
+                                const float* inv_norm2, const float* deno, int64_t batch,
+                                int32_t d, float temp, const float* grad_loss, float* dX1,
+                                float* dX2, void* workspace, size_t workspace_bytes,
+                                void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Structure primitives (all deterministic; indices bit-exact with the CPU restatement).
  * ---------------------------------------------------------------------------------------- */
 /* int64 indices → int32, checking 0 <= v < upper; err_count (device int64) += #violations. */

@@ -323,6 +323,21 @@ def row_epilogue_backward(Z, dY, act=None, slope=0.0, ln=False, gamma=None, eps=
     return da, dgamma, dbeta
 
 
+def contrast_loss(E1, E2, nodes, temp):
+    """contrastLoss, util/loss_torch.py:103-110: InfoNCE between the batch rows of two
+    row-normalised tables (F.normalize(x + 1e-8), eps 1e-12), float64."""
+    def normalize(X):
+        X = np.asarray(X, dtype=np.float64) + 1e-8
+        n = np.sqrt((X * X).sum(-1, keepdims=True))
+        return X / np.maximum(n, 1e-12)
+    nodes = np.asarray(nodes, dtype=np.int64)
+    P1 = normalize(E1)[nodes]
+    P2 = normalize(E2)[nodes]
+    nume = np.exp((P1 * P2).sum(-1) / temp)
+    deno = np.exp(P1 @ P2.T / temp).sum(-1) + 1e-8
+    return float(-np.log(nume / deno).mean())
+
+
 def linear(X, W, b=None):
     """nn.Linear: X·Wᵀ + b."""
     Y = np.asarray(X, dtype=np.float64) @ np.asarray(W, dtype=np.float64).T

@@ -93,3 +93,16 @@ def equivset_conv(X, vertex, edges, X0, W1, W2, W, alpha, aggr="mean"):
     Xv = scatter(Xev, vertex, dim_size=N)
     X = (1 - alpha) * Xv + alpha * X0
     return W(X)
+
+
+def contrast_loss(embeds1: torch.Tensor, embeds2: torch.Tensor, nodes: torch.Tensor, temp):
+    """contrastLoss (util/loss_torch.py:103-110) with the reference's own torch calls; run in
+    float64 on the host it is the oracle for hgd_infonce_* (values and, via autograd, grads)."""
+    F = torch.nn.functional
+    embeds1 = F.normalize(embeds1 + 1e-8, p=2)
+    embeds2 = F.normalize(embeds2 + 1e-8, p=2)
+    pck1 = embeds1[nodes]
+    pck2 = embeds2[nodes]
+    nume = torch.exp(torch.sum(pck1 * pck2, dim=-1) / temp)
+    deno = torch.exp(pck1 @ pck2.T / temp).sum(-1) + 1e-8
+    return -torch.log(nume / deno).mean()

@@ -29,6 +29,65 @@ ARGS = {  # LocalAwareEncoder.init_edhnn_config, HGNN_HD4.py:371-388 (hidden = e
     'input_dropout': 0.6, 'AllSet_input_norm': True}
 
 
+def make_reference_step(m, form, A, ui, N, d, dev, X, dY):
+    """One fwd+bwd of the block with the reference's torch ops on the device: torch.sparse.mm
+    hops (model/layers/EquivSetConv.py:86-107) or torch_scatter-style means (sum / count,
+    layers2/EquivSetConv2.py:88-93), F.layer_norm / F.linear / F.dropout."""
+    import torch
+    import torch.nn.functional as F
+    from oracle import hgd_oracle as O
+
+    c = m.conv
+    p_drop = m.dropout.p
+    alpha = c.alpha
+    lin_in = (m.lin_in.weight, m.lin_in.bias)
+    Wn, Wl = c.W.normalizations[0], c.W.lins[0]
+
+    def tail(Xv, x0):
+        Xb = (1 - alpha) * Xv + alpha * x0
+        Xb = F.layer_norm(Xb, (d,), Wn.weight, Wn.bias, Wn.eps)
+        y = torch.relu(F.linear(Xb, Wl.weight, Wl.bias))
+        return F.dropout(y, p_drop, True)
+
+    if form == "spmm":
+        idx, vals = O.coo_of(A)
+        adj = torch.sparse_coo_tensor(torch.from_numpy(idx), torch.from_numpy(vals),
+                                      A.shape).coalesce().to(dev)
+        ln0, ln1 = c.lns[0], c.lns[1]
+
+        def hop(x):
+            return F.leaky_relu(torch.sparse.mm(adj, torch.sparse.mm(adj.t(), x)), 0.2)
+
+        def step():
+            xx = X.detach().requires_grad_(True)
+            h = F.dropout(xx, p_drop, True)
+            h = torch.relu(F.linear(h, *lin_in))
+            x0 = h
+            h = F.dropout(h, p_drop, True)
+            Xe = F.layer_norm(hop(h), (d,), ln0.weight, ln0.bias, ln0.eps) + h
+            Xv = F.layer_norm(hop(Xe), (d,), ln1.weight, ln1.bias, ln1.eps) + Xe
+            tail(Xv, x0).backward(dY)
+        return step
+
+    coo = ui.tocoo()
+    V = torch.from_numpy(coo.row.astype("int64")).to(dev)
+    E = torch.from_numpy(coo.col.astype("int64")).to(dev)
+    ones = torch.ones(len(V), device=dev)
+    cnt_e = torch.zeros(N, device=dev).index_add_(0, E, ones).clamp_(min=1)[:, None]
+    cnt_v = torch.zeros(N, device=dev).index_add_(0, V, ones).clamp_(min=1)[:, None]
+
+    def step():
+        xx = X.detach().requires_grad_(True)
+        h = F.dropout(xx, p_drop, True)
+        h = torch.relu(F.linear(h, *lin_in))
+        x0 = h
+        h = F.dropout(h, p_drop, True)
+        Xe = torch.zeros(N, d, device=dev).index_add(0, E, h[V]) / cnt_e
+        Xv = torch.zeros(N, d, device=dev).index_add(0, V, Xe[E]) / cnt_v
+        tail(Xv, x0).backward(dY)
+    return step
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--users", type=int, default=31_668)
@@ -38,6 +97,8 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--cpu-reps", type=int, default=3)
     ap.add_argument("--tag", default="yelp")
+    ap.add_argument("--variants", default="gpu_fused,gpu_unfused,gpu_reference_ops,cpu_reference_ops",
+                    help="comma list of variants to run")
     args = ap.parse_args()
     import numpy as np
     import scipy.sparse as sp
@@ -85,7 +146,10 @@ def main():
         else:
             m = EquivSetGNN(d, cfg, H).to(dev).train()
             call = lambda xx: m(xx, H, N)  # noqa: E731
+        want = set(args.variants.split(","))
         for fused in (True, False):
+            if ("gpu_fused" if fused else "gpu_unfused") not in want:
+                continue
             m.conv.fused_epilogue = fused
 
             def step():
@@ -96,7 +160,13 @@ def main():
             ms = gpu_time(step, args.reps)
             out.append({"form": form, "variant": "gpu_fused" if fused else "gpu_unfused",
                         "ms_per_step": round(ms, 4)})
-        if form == "spmm":
+        # the reference's own op chain on the same GPU (torch.sparse.mm / index_add means,
+        # nn.functional LayerNorm / Linear / dropout), same parameters
+        if "gpu_reference_ops" in want:
+            ref_step = make_reference_step(m, form, A, ui, N, d, dev, X, dY)
+            out.append({"form": form, "variant": "gpu_reference_ops",
+                        "ms_per_step": round(gpu_time(ref_step, args.reps), 4)})
+        if form == "spmm" and "cpu_reference_ops" in want:
             # the reference's CPU path: same parameters, torch.sparse.mm + host ops
             mc = edhnn_spmm.EquivSetGNN(d, cfg).train()
             mc.load_state_dict({k: v.cpu() for k, v in m.state_dict().items()})

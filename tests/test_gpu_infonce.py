@@ -1,0 +1,89 @@
+"""Fused InfoNCE (hgd_infonce_*, contrastLoss of util/loss_torch.py:103-110; SURVEY.md §8f
+rank 4) against the reference's own torch formula run in float64 on the host
+(oracle/ref_cpu.contrast_loss): the loss and the gradients of both tables, with duplicate batch
+nodes, ragged batch sizes, zero rows and several widths / temperatures."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import hgd_oracle as O
+from oracle import ref_cpu
+
+pytestmark = pytest.mark.gpu
+
+CASES = [(1000, 64, 256, 0.2), (300, 16, 37, 1.0), (5000, 128, 2048, 0.1), (64, 256, 64, 0.5),
+         (2000, 48, 2, 0.3), (40_000, 64, 4096, 0.2)]
+
+
+@pytest.mark.parametrize("N,d,B,temp", CASES)
+def test_infonce_matches_reference_formula(dev, N, d, B, temp):
+    from hypergraph_diffusion_for_recommendation_amd.functional import contrast_loss
+    rng = np.random.default_rng(N + d + B)
+    E1 = rng.standard_normal((N, d)).astype(np.float32)
+    E2 = rng.standard_normal((N, d)).astype(np.float32)
+    # a zero row (‖x + 1e-8‖ ≈ 7e-8: its gradient is the 1/‖x‖-amplified dp, fine as long as
+    # dp does not cancel) in the batch once, and duplicated batch nodes
+    E1[0] = 0.0
+    nodes = rng.integers(1, N, size=B)
+    nodes[: min(B, 3)] = 1
+    if B > 3:
+        nodes[3] = 0
+    g1 = torch.from_numpy(E1).to(dev).requires_grad_(True)
+    g2 = torch.from_numpy(E2).to(dev).requires_grad_(True)
+    loss = contrast_loss(g1, g2, torch.from_numpy(nodes).to(dev), temp)
+    loss.backward()
+    c1 = torch.tensor(E1, dtype=torch.float64, requires_grad=True)
+    c2 = torch.tensor(E2, dtype=torch.float64, requires_grad=True)
+    ref = ref_cpu.contrast_loss(c1, c2, torch.from_numpy(nodes), temp)
+    ref.backward()
+    assert abs(ref.item() - O.contrast_loss(E1, E2, nodes, temp)) < 1e-9 * max(1, abs(ref.item()))
+    # loss: a mean of B log-ratios of sums of B exps (|logit| <= 1/temp): fp32 rounding bound
+    assert abs(loss.item() - ref.item()) <= 1e-5 * (abs(ref.item()) + 1.0 / temp)
+    for got, want in ((g1.grad, c1.grad), (g2.grad, c2.grad)):
+        got = got.double().cpu()
+        scale = want.abs().max().item() + 1e-30
+        err = (got - want).abs().max().item()
+        # relative to the largest gradient, with a floor at fp32 resolution of the per-row
+        # softmax weights (coef = 1/(B·τ)): a batch of one repeated node has a true gradient
+        # of O(1e-8·coef) that fp32 rounds to 0, in the reference's fp32 run too
+        assert err <= 1e-4 * scale + 1e-7 / (B * temp), (err, scale)
+        # rows outside the batch get exactly zero gradient
+        outside = torch.ones(N, dtype=torch.bool)
+        outside[torch.from_numpy(nodes)] = False
+        assert got[outside].abs().max().item() == 0.0 if outside.any() else True
+
+
+def test_infonce_single_row_batch(dev):
+    """B = 1: the loss is log(1 + 1e-8·e^{-s/τ}) ≈ 0 and its gradient is below fp32 resolution
+    (in the reference's fp32 run as well); only finiteness and the ≈ 0 loss are checked."""
+    from hypergraph_diffusion_for_recommendation_amd.functional import contrast_loss
+    E1 = torch.randn(100, 32, device=dev, requires_grad=True)
+    E2 = torch.randn(100, 32, device=dev, requires_grad=True)
+    loss = contrast_loss(E1, E2, torch.tensor([7], device=dev), 0.3)
+    loss.backward()
+    assert abs(loss.item()) < 1e-6
+    assert torch.isfinite(E1.grad).all() and torch.isfinite(E2.grad).all()
+
+
+def test_infonce_deterministic_and_sync_free(dev):
+    from hypergraph_diffusion_for_recommendation_amd.functional import contrast_loss
+    torch.manual_seed(0)
+    E1 = torch.randn(10_000, 64, device=dev, requires_grad=True)
+    E2 = torch.randn(10_000, 64, device=dev, requires_grad=True)
+    nodes = torch.randint(0, 10_000, (2048,), device=dev)
+    outs = []
+    for _ in range(2):
+        E1.grad = E2.grad = None
+        loss = contrast_loss(E1, E2, nodes, 0.2) * 3.0  # upstream grad 3 via the device scalar
+        loss.backward()
+        outs.append((loss.detach().clone(), E1.grad.clone(), E2.grad.clone()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    # the fused loss / dX are bitwise stable; the scatter into the table is index_add_ (atomics)
+    assert torch.allclose(outs[0][1], outs[1][1], rtol=0, atol=1e-7)
+
+
+def test_infonce_rejects_bad_shapes(dev):
+    from hypergraph_diffusion_for_recommendation_amd.functional import contrast_loss
+    with pytest.raises(ValueError):
+        contrast_loss(torch.randn(10, 20, device=dev), torch.randn(10, 20, device=dev),
+                      torch.arange(4, device=dev), 0.2)

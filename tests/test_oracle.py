@@ -191,3 +191,17 @@ def test_row_epilogue_backward_matches_torch_autograd(act, slope, ln):
     if ln:
         np.testing.assert_allclose(dg, gt.grad.numpy(), rtol=1e-10, atol=1e-12)
         np.testing.assert_allclose(db, bt.grad.numpy(), rtol=1e-10, atol=1e-12)
+
+
+def test_contrast_loss_restatements_agree():
+    """numpy restatement vs the reference's torch calls (oracle/ref_cpu.contrast_loss), float64."""
+    import torch
+    from oracle import ref_cpu
+    rng = np.random.default_rng(4)
+    E1 = rng.standard_normal((50, 16))
+    E2 = rng.standard_normal((50, 16))
+    E1[3] = 0.0  # a zero row: normalize(0 + 1e-8) stays finite
+    nodes = rng.integers(0, 50, size=20)
+    a = O.contrast_loss(E1, E2, nodes, 0.2)
+    b = ref_cpu.contrast_loss(torch.tensor(E1), torch.tensor(E2), torch.tensor(nodes), 0.2)
+    assert abs(a - b.item()) <= 1e-12 * max(1.0, abs(a))
