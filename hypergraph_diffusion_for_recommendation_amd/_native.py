@@ -108,6 +108,18 @@ _SIGNATURES = {
     "hgd_infonce_backward": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_i64,
                                      c_i32, c_f32, c_void_p, c_void_p, c_void_p, c_void_p,
                                      c_size, c_void_p]),
+    "hgd_ingest_read": (c_i32, [ctypes.c_char_p, c_i32, c_i32, ctypes.POINTER(c_void_p)]),
+    "hgd_ingest_count": (c_i64, [c_void_p]),
+    "hgd_ingest_copy": (c_i32, [c_void_p, c_void_p, c_void_p]),
+    "hgd_ingest_free": (None, [c_void_p]),
+    "hgd_remap_workspace_size": (c_size, [c_i64]),
+    "hgd_remap_first_appearance": (c_i32, [c_void_p, c_i64, c_void_p, c_void_p, c_void_p,
+                                           c_void_p, c_size, c_void_p]),
+    "hgd_coo_coalesce_workspace_size": (c_size, [c_i64]),
+    "hgd_coo_coalesce": (c_i32, [c_void_p, c_void_p, c_i64, c_i64, c_i64, c_void_p, c_void_p,
+                                 c_void_p, c_void_p, c_void_p, c_size, c_void_p]),
+    "hgd_normalize_values": (c_i32, [c_void_p, c_void_p, c_void_p, c_i64, c_void_p, c_void_p,
+                                     c_void_p, c_void_p]),
     "hgd_index_narrow": (c_i32, [c_void_p, c_i64, c_i64, c_void_p, c_void_p, c_void_p]),
     "hgd_sort_perm_workspace_size": (c_size, [c_i64]),
     "hgd_sort_perm": (c_i32, [c_void_p, c_i64, c_i64, c_void_p, c_void_p, c_void_p, c_size,

@@ -228,6 +228,48 @@ hgd_status hgd_infonce_backward(const float* P1, const float* P2, const float* i
                                 void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * Ingest and graph build — the data path producing the hot path's
+ * input matrices (data/loader.py:24-38, data/ui_graph.py:43-112, data/graph.py:11-25).
+ *
+ * Host (no GPU needed): hgd_ingest_read parses a "user<sep>item[<sep>…]" file exactly like
+ * FileIO.load_data_set — first line skipped; a line with a tab splits on tabs, else on commas,
+ * after stripping; fields 0/1 parsed like Python int(); other fields ignored; "\n", "\r\n" and
+ * "\r" end lines — with n_threads parser threads (<= 0: all cores). Lines the reference would
+ * reject fail the call (the message names the line). The handle owns the parsed arrays.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct hgd_ingest hgd_ingest;
+hgd_status hgd_ingest_read(const char* path, int32_t skip_header, int32_t n_threads,
+                           hgd_ingest** out);
+int64_t hgd_ingest_count(const hgd_ingest* h);  /* records, -1 for NULL */
+/* Copies the raw user / item ids (host int64 arrays of hgd_ingest_count entries, file order). */
+hgd_status hgd_ingest_copy(const hgd_ingest* h, int64_t* user_raw, int64_t* item_raw);
+void hgd_ingest_free(hgd_ingest* h);
+
+/* Device: ids[i] = rank of keys[i] among the distinct keys ordered by first appearance (the
+ * `if user not in self.user: self.user[user] = len(self.user)` loop, data/ui_graph.py:43-56);
+ * uniq[r] = the key with id r (first *n_unique entries); *n_unique on the device. */
+size_t hgd_remap_workspace_size(int64_t n);
+hgd_status hgd_remap_first_appearance(const int64_t* keys, int64_t n, int32_t* ids,
+                                      int64_t* uniq, int64_t* n_unique, void* workspace,
+                                      size_t workspace_bytes, void* stream);
+
+/* Device: canonical CSR (rows ascending, columns ascending, duplicates summed into float32
+ * counts) of the COO (rows, cols) [n] — scipy csr_matrix((ones, (row, col))), ui_graph.py:70-84.
+ * col_out / val_out need n entries; the nonzero count lands in device *nnz_out. */
+size_t hgd_coo_coalesce_workspace_size(int64_t n);
+hgd_status hgd_coo_coalesce(const int32_t* rows, const int32_t* cols, int64_t n, int64_t n_rows,
+                            int64_t n_cols, int64_t* rowptr, int32_t* col_out, float* val_out,
+                            int64_t* nnz_out, void* workspace, size_t workspace_bytes,
+                            void* stream);
+
+/* Device: out[e] = (row_scale[r]·val[e])·col_scale[col[e]] (col_scale NULL: no second factor) —
+ * d_mat_inv.dot(adj).dot(d_mat_inv) of Graph.normalize_graph_mat with the scales of
+ * hgd_degree_scale (power -0.5 square, -1 rectangular). */
+hgd_status hgd_normalize_values(const int64_t* rowptr, const int32_t* col, const float* val,
+                                int64_t n_rows, const float* row_scale, const float* col_scale,
+                                float* out, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Structure primitives (all deterministic; indices bit-exact with the CPU restatement).
  * ---------------------------------------------------------------------------------------- */
 /* int64 indices → int32, checking 0 <= v < upper; err_count (device int64) += #violations. */

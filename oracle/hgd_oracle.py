@@ -27,6 +27,21 @@ import scipy.sparse as sp
 # ---------------------------------------------------------------------------------------------
 # Graph construction — data/ui_graph.py, data/graph.py, base/torch_interface.py
 # ---------------------------------------------------------------------------------------------
+def load_data_set(path):
+    """FileIO.load_data_set (data/loader.py:24-38): skip the header line; a line containing a
+    tab splits on tabs, otherwise on commas, after strip(); int() of fields 0 and 1; weight 1.
+    Python's own exceptions propagate where the reference's would."""
+    import re
+    data = []
+    with open(path) as f:
+        next(f)
+        for line in f:
+            sep = "\t" if "\t" in line else ","
+            items = re.split(sep, line.strip())
+            data.append([int(items[0]), int(items[1]), 1.0])
+    return data
+
+
 def remap_ids(pairs):
     """Id maps in first-appearance order of the training file (data/ui_graph.py:107-125)."""
     user, item = {}, {}

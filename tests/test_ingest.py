@@ -1,0 +1,100 @@
+"""Host ingest (hgd_ingest_read, FileIO.load_data_set of data/loader.py:24-38) against the
+oracle restatement on the same files: separators, whitespace, signs / underscores, line endings,
+multi-threaded chunking, and the lines the reference rejects. CPU only (no device calls)."""
+import numpy as np
+import pytest
+
+from oracle import hgd_oracle as O
+
+
+def _write(tmp_path, name, text, mode="w"):
+    p = tmp_path / name
+    if mode == "wb":
+        p.write_bytes(text)
+    else:
+        p.write_text(text)
+    return str(p)
+
+
+def _check_same(path, **kw):
+    from hypergraph_diffusion_for_recommendation_amd.ingest import load_data_set
+    u, i = load_data_set(path, **kw)
+    ref = O.load_data_set(path)
+    assert u.tolist() == [r[0] for r in ref]
+    assert i.tolist() == [r[1] for r in ref]
+    return u, i
+
+
+CASES = {
+    "tab": "user\titem\trating\n1\t2\t5\n3\t4\t1\n1\t4\t0\n",
+    "comma": "u,i\n10,20\n30,40,1.5\n10,40\n",
+    "whitespace": "h\n 1 , 2 \n\t7\t8\t\n+3,-4\n0007,9\n",
+    "underscore": "h\n1_000,2\n-5,+6\n",
+    "header_only": "user,item\n",
+    "no_trailing_newline": "h\n1,2\n3,4",
+    "mixed": "h\n1,2\n3\t4\n5,6\n",
+    "big_ids": "h\n9223372036854775807,-9223372036854775808\n",
+}
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_ingest_matches_load_data_set(tmp_path, name):
+    _check_same(_write(tmp_path, name, CASES[name]))
+
+
+def test_ingest_line_endings(tmp_path):
+    for ending in (b"\r\n", b"\r"):
+        body = ending.join([b"u,i", b"1,2", b"3,4", b"5,6"]) + ending
+        p = _write(tmp_path, "le.csv", body, mode="wb")
+        from hypergraph_diffusion_for_recommendation_amd.ingest import load_data_set
+        u, i = load_data_set(p)
+        assert u.tolist() == [1, 3, 5] and i.tolist() == [2, 4, 6]
+        # Python's universal newlines agree
+        ref = O.load_data_set(p)
+        assert [r[0] for r in ref] == [1, 3, 5]
+
+
+def test_ingest_multithreaded_chunks_agree(tmp_path):
+    """A 3 MB file parsed with 1 and 7 threads (chunk cuts inside lines, CRLF across a cut)."""
+    rng = np.random.default_rng(0)
+    n = 200_000
+    us = rng.integers(-10**12, 10**12, size=n)
+    its = rng.integers(0, 10**6, size=n)
+    lines = ["user,item,rating"]
+    for k, (a, b) in enumerate(zip(us, its)):
+        lines.append(f"{a}\t{b}\t1" if k % 3 == 0 else f"{a},{b}")
+    p = _write(tmp_path, "big.csv", "\r\n".join(lines) + "\r\n", mode="w")
+    from hypergraph_diffusion_for_recommendation_amd.ingest import load_data_set
+    u1, i1 = load_data_set(p, n_threads=1)
+    u7, i7 = load_data_set(p, n_threads=7)
+    assert np.array_equal(u1, us) and np.array_equal(i1, its)
+    assert np.array_equal(u7, us) and np.array_equal(i7, its)
+
+
+@pytest.mark.parametrize("text,line", [
+    ("h\n1,2\n\n3,4\n", 3),          # empty line: int('') raises in the reference
+    ("h\n1,2\n3 4\n", 3),            # no separator: one field
+    ("h\n1,2\n1.0,2\n", 3),          # int('1.0') raises
+    ("h\n1,x\n", 2),
+    ("h\n1,2\n1__0,2\n", 3),         # int('1__0') raises
+    ("h\n1,2\n99999999999999999999,1\n", 3),  # beyond int64
+])
+def test_ingest_rejects_what_the_reference_rejects(tmp_path, text, line):
+    from hypergraph_diffusion_for_recommendation_amd import _native as nat
+    from hypergraph_diffusion_for_recommendation_amd.ingest import load_data_set
+    p = _write(tmp_path, "bad.csv", text)
+    with pytest.raises(nat.HGDNativeError, match=f"line {line}"):
+        load_data_set(p)
+    if "9999999999" not in text:  # Python ints are unbounded: only the int64 limit differs
+        with pytest.raises((ValueError, IndexError)):
+            O.load_data_set(p)
+
+
+def test_ingest_empty_file_and_missing(tmp_path):
+    from hypergraph_diffusion_for_recommendation_amd import _native as nat
+    from hypergraph_diffusion_for_recommendation_amd.ingest import load_data_set
+    p = _write(tmp_path, "empty.csv", "")
+    with pytest.raises(nat.HGDNativeError, match="empty"):
+        load_data_set(p)
+    with pytest.raises(nat.HGDNativeError, match="cannot open"):
+        load_data_set(str(tmp_path / "nope.csv"))
