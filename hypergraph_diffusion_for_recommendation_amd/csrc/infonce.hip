@@ -77,43 +77,74 @@ __global__ __launch_bounds__(256) void k_nce_gather(const float* __restrict__ E1
   }
 }
 
-// A / B fragment of rows [r0, r0+16) of a [B, d] matrix for k-step q: lane l holds
-// M[r0 + (l & 15)][4q + (l >> 4)] (rows past B are clamped; their contributions are masked).
+// Fragments of rows [r0, r0+16) of a [B, d] matrix as float4 loads: lane l holds
+// M[r0 + (l&15)][4(l>>4) + 16q' .. +3] for q' < d/16, i.e. MFMA step (q', c) multiplies
+// k = 4(l>>4) + 16q' + c — a fixed permutation of k that every operand loaded this way shares.
+// Rows past B are clamped (their contributions are masked by the callers).
 template <int DQ>
-__device__ __forceinline__ void load_frag(const float* M, int64_t B, int d, int64_t r0, int lane,
-                                          float (&f)[DQ]) {
+__device__ __forceinline__ void load_frag4(const float* M, int64_t B, int d, int64_t r0, int lane,
+                                           f32x4 (&f)[DQ / 4]) {
   int64_t r = r0 + (lane & 15);
   r = r < B ? r : B - 1;
+  const float* row = M + r * d + 4 * (lane >> 4);
 #pragma unroll
-  for (int q = 0; q < DQ; ++q) f[q] = M[r * d + 4 * q + (lane >> 4)];
+  for (int q = 0; q < DQ / 4; ++q) f[q] = *reinterpret_cast<const f32x4*>(row + 16 * q);
 }
 
 // ---- forward exp-sums: partial[s][b] = Σ_{j in slice s} exp(<p1_b, p2_j>/τ) ----
+// A wave owns 16 rows of p1; the slice's p2 rows stream in 64-row super-tiles (4 MFMA tiles)
+// through a copy-free ping-pong, so a super-tile's loads are in flight behind the previous
+// one's MFMAs and exps.
 template <int DQ>  // d = 4·DQ
 __global__ __launch_bounds__(256) void k_nce_rowsum(const float* __restrict__ P1,
                                                     const float* __restrict__ P2, int64_t B,
                                                     float inv_temp, int64_t j_per_slice,
                                                     float* partial) {
+  constexpr int Q4 = DQ / 4;
+  constexpr int SUB = 4;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int64_t b0 = static_cast<int64_t>(blockIdx.x) * 64 + 16 * wave;
   if (b0 >= B) return;
   const int d = 4 * DQ;
-  float a[DQ];
-  load_frag<DQ>(P1, B, d, b0, lane, a);
+  f32x4 a[Q4];
+  load_frag4<DQ>(P1, B, d, b0, lane, a);
   const int64_t j_begin = static_cast<int64_t>(blockIdx.y) * j_per_slice;
   const int64_t j_end = min(B, j_begin + j_per_slice);
   float psum[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int64_t j0 = j_begin; j0 < j_end; j0 += 16) {
-    float bf[DQ];
-    load_frag<DQ>(P2, B, d, j0, lane, bf);
-    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  auto load = [&](int64_t j0, f32x4 (&f)[SUB][Q4]) {
 #pragma unroll
-    for (int q = 0; q < DQ; ++q) s = mfma4(a[q], bf[q], s);
-    // s[r] = <p1_{b0 + 4(l>>4) + r}, p2_{j0 + (l&15)}>
-    const bool jok = j0 + (lane & 15) < j_end;
+    for (int t = 0; t < SUB; ++t) load_frag4<DQ>(P2, B, d, j0 + 16 * t, lane, f[t]);
+  };
+  auto compute = [&](int64_t j0, const f32x4 (&f)[SUB][Q4]) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) psum[r] += jok ? expf(s[r] * inv_temp) : 0.f;
+    for (int t = 0; t < SUB; ++t) {
+      f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < Q4; ++q)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) s = mfma4(a[q][c], f[t][q][c], s);
+      // s[r] = <p1_{b0 + 4(l>>4) + r}, p2_{j0 + 16t + (l&15)}>
+      const bool jok = j0 + 16 * t + (lane & 15) < j_end;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) psum[r] += jok ? expf(s[r] * inv_temp) : 0.f;
+    }
+  };
+  f32x4 f0[SUB][Q4], f1[SUB][Q4];
+  int64_t j0 = j_begin;
+  load(j0, f0);
+  while (j0 < j_end) {
+    load(j0 + 16 * SUB, f1);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(j0, f0);
+    __builtin_amdgcn_sched_barrier(0);
+    j0 += 16 * SUB;
+    if (j0 >= j_end) break;
+    load(j0 + 16 * SUB, f0);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(j0, f1);
+    __builtin_amdgcn_sched_barrier(0);
+    j0 += 16 * SUB;
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) psum[r] = group_sum<16>(psum[r]);
@@ -159,17 +190,19 @@ __global__ __launch_bounds__(256) void k_nce_bwd(const float* __restrict__ P1,
                                                  float inv_temp, const float* __restrict__ deno,
                                                  const float* __restrict__ grad, float coef_base,
                                                  int64_t k_per_slice, float* part) {
+  constexpr int Q4 = DQ / 4;
+  constexpr int SUB = 2;  // 16-row tiles of the streamed matrix per ping-pong stage
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int d = 4 * DQ;
-  // "own" rows: b (ROWS) or j (!ROWS); "other" rows are streamed in 16-row tiles
   const float coef = grad[0] * coef_base;  // upstream dL/dloss (device scalar: no host sync)
+  // "own" rows: b (ROWS) or j (!ROWS); "other" rows are streamed in 16-row tiles
   const float* own_m = ROWS ? P1 : P2;
   const float* oth_m = ROWS ? P2 : P1;
   const int64_t o0 = static_cast<int64_t>(blockIdx.x) * 64 + 16 * wave;
   if (o0 >= B) return;
-  float own[DQ];
-  load_frag<DQ>(own_m, B, d, o0, lane, own);
+  f32x4 own[Q4];
+  load_frag4<DQ>(own_m, B, d, o0, lane, own);
   const int64_t o_lane = o0 + (lane & 15);  // own row of this lane in the logit tile below
   float deno_own = 1.f;
   if (ROWS) deno_own = deno[o_lane < B ? o_lane : B - 1];
@@ -178,36 +211,71 @@ __global__ __launch_bounds__(256) void k_nce_bwd(const float* __restrict__ P1,
   f32x4 acc[DQ / 4];
 #pragma unroll
   for (int t = 0; t < DQ / 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int64_t k0 = k_begin; k0 < k_end; k0 += 16) {
-    float of[DQ];
-    load_frag<DQ>(oth_m, B, d, k0, lane, of);
-    // logit tile with the OTHER index on the output rows: T[r'][c] = <oth_{k0+4(l>>4)+r}, own_{o0+(l&15)}>
-    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  // per 16-row tile: the other rows as logit fragments (row on the lane) and as the B operand of
+  // the accumulation (feature on the lane): bv[r][t] = oth[k0 + 4(l>>4) + r][16t + (l&15)]
+  struct Tile {
+    f32x4 of[Q4];
+    float bv[4][DQ / 4];
+  };
+  auto load = [&](int64_t k0, Tile (&T)[SUB]) {
 #pragma unroll
-    for (int q = 0; q < DQ; ++q) s = mfma4(of[q], own[q], s);
-    float gk[4];
+    for (int u = 0; u < SUB; ++u) {
+      const int64_t kt = k0 + 16 * u;
+      load_frag4<DQ>(oth_m, B, d, kt, lane, T[u].of);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t k = k0 + 4 * (lane >> 4) + r;  // other index of register r
-      const bool kok = k < k_end;
-      const int64_t kc = k < B ? k : B - 1;
-      const float e = expf(s[r] * inv_temp);
-      const float den = ROWS ? deno_own : deno[kc];
-      const float delta = (k == o_lane) ? 1.f : 0.f;
-      gk[r] = (kok && o_lane < B) ? coef * (e / den - delta) : 0.f;
-    }
-    // acc[own row (l&15)][n] += Σ_k G[own][k] · oth_k[n]: A operand = gk (i = own on the lane,
-    // k-step r covers other rows {4(l>>4) + r}), B operand = oth rows in the same order.
+      for (int r = 0; r < 4; ++r) {
+        int64_t k = kt + 4 * (lane >> 4) + r;
+        k = k < B ? k : B - 1;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      int64_t k = k0 + 4 * (lane >> 4) + r;
-      k = k < B ? k : B - 1;
-#pragma unroll
-      for (int t = 0; t < DQ / 4; ++t) {
-        const float bv = oth_m[k * d + 16 * t + (lane & 15)];
-        acc[t] = mfma4(gk[r], bv, acc[t]);
+        for (int t = 0; t < DQ / 4; ++t) T[u].bv[r][t] = oth_m[k * d + 16 * t + (lane & 15)];
       }
     }
+  };
+  auto compute = [&](int64_t k0, const Tile (&T)[SUB]) {
+#pragma unroll
+    for (int u = 0; u < SUB; ++u) {
+      const int64_t kt = k0 + 16 * u;
+      // logit tile with the OTHER index on the output rows:
+      // s[r] = <oth_{kt + 4(l>>4) + r}, own_{o0 + (l&15)}>
+      f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < Q4; ++q)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) s = mfma4(T[u].of[q][c], own[q][c], s);
+      float gk[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t k = kt + 4 * (lane >> 4) + r;  // other index of register r
+        const bool kok = k < k_end;
+        const int64_t kc = k < B ? k : B - 1;
+        const float e = expf(s[r] * inv_temp);
+        const float den = ROWS ? deno_own : deno[kc];
+        const float delta = (k == o_lane) ? 1.f : 0.f;
+        gk[r] = (kok && o_lane < B) ? coef * (e / den - delta) : 0.f;
+      }
+      // acc[own row][n] += Σ_k G[own][k]·oth_k[n]: A operand = gk (own row on the lane, k-step
+      // r covers other rows {4(l>>4) + r}), B operand = those rows' features (bv).
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int t = 0; t < DQ / 4; ++t) acc[t] = mfma4(gk[r], T[u].bv[r][t], acc[t]);
+    }
+  };
+  Tile t0[SUB], t1[SUB];
+  int64_t k0 = k_begin;
+  load(k0, t0);
+  while (k0 < k_end) {
+    load(k0 + 16 * SUB, t1);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(k0, t0);
+    __builtin_amdgcn_sched_barrier(0);
+    k0 += 16 * SUB;
+    if (k0 >= k_end) break;
+    load(k0 + 16 * SUB, t0);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(k0, t1);
+    __builtin_amdgcn_sched_barrier(0);
+    k0 += 16 * SUB;
   }
   // acc[t] reg r: own row o0 + 4(l>>4) + r, feature 16t + (l&15)
 #pragma unroll
@@ -264,7 +332,7 @@ int64_t slices_for(int64_t B) {
 
 int64_t per_slice(int64_t B, int64_t S) {
   int64_t p = (B + S - 1) / S;
-  return (p + 15) / 16 * 16;
+  return (p + 63) / 64 * 64;  // whole 64-row super-tiles
 }
 
 }  // namespace
