@@ -480,3 +480,86 @@ def contrast_loss(embeds1: torch.Tensor, embeds2: torch.Tensor, nodes: torch.Ten
     if nodes.numel() == 0:
         raise ValueError("contrast_loss: empty batch")
     return _ContrastLoss.apply(embeds1, embeds2, nodes, float(temp))
+
+
+def _mm_ok(H: torch.Tensor, X: torch.Tensor) -> bool:
+    n, K = H.shape
+    d = X.shape[1]
+    return (H.is_cuda and X.is_cuda and H.dtype == torch.float32 and X.dtype == torch.float32
+            and K % 16 == 0 and d % 16 == 0 and 16 <= K <= 128 and 16 <= d <= 128
+            and X.shape[0] == n)
+
+
+def _tn(A: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
+    """Aᵀ·B for tall A [n, m], B [n, k] (split-K hgd_linear_backward_weight)."""
+    lib = nat.load()
+    n, m = A.shape
+    k = B.shape[1]
+    C = torch.empty((m, k), dtype=torch.float32, device=A.device)
+    wsb = lib.hgd_linear_backward_weight_workspace_size(n, m, k)
+    ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=A.device)
+    nat.check(lib.hgd_linear_backward_weight(
+        A.data_ptr(), A.stride(0), None, 0, B.data_ptr(), B.stride(0), n, m, k, C.data_ptr(),
+        None, ws.data_ptr(), wsb, torch.cuda.current_stream(A.device).cuda_stream),
+        "hgd_linear_backward_weight")
+    return C
+
+
+def _nn(A: torch.Tensor, M: torch.Tensor) -> torch.Tensor:
+    """A·M for tall A [n, m] and small M [m, k] (hgd_linear_backward_data)."""
+    lib = nat.load()
+    n, m = A.shape
+    k = M.shape[1]
+    Y = torch.empty((n, k), dtype=torch.float32, device=A.device)
+    nat.check(lib.hgd_linear_backward_data(
+        A.data_ptr(), A.stride(0), None, 0, n, m, M.data_ptr(), M.stride(0), k, Y.data_ptr(),
+        Y.stride(0), torch.cuda.current_stream(A.device).cuda_stream), "hgd_linear_backward_data")
+    return Y
+
+
+def _nt(A: torch.Tensor, M: torch.Tensor) -> torch.Tensor:
+    """A·Mᵀ for tall A [n, k] and small M [m, k] (hgd_linear_forward without bias)."""
+    lib = nat.load()
+    n, k = A.shape
+    m = M.shape[0]
+    Y = torch.empty((n, m), dtype=torch.float32, device=A.device)
+    nat.check(lib.hgd_linear_forward(A.data_ptr(), A.stride(0), n, k, M.data_ptr(), M.stride(0),
+                                     m, None, 0, Y.data_ptr(), Y.stride(0),
+                                     torch.cuda.current_stream(A.device).cuda_stream),
+              "hgd_linear_forward")
+    return Y
+
+
+class _DenseTwoHop(torch.autograd.Function):
+    """``H·(Hᵀ·X)`` with H [n, K] dense (HGNNLayer, HCCF.py:201-211) on the skinny MFMA kernels:
+    Hᵀ·X is a split-K product, H·M a row GEMM; the backward reuses the same three kernels."""
+
+    @staticmethod
+    def forward(ctx, H, X):
+        H = H.contiguous()
+        X = X.contiguous()
+        M = _tn(H, X)             # [K, d] = Hᵀ·X
+        Y = _nn(H, M)             # [n, d] = H·M
+        ctx.save_for_backward(H, X, M)
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        H, X, M = ctx.saved_tensors
+        dY = dY.contiguous()
+        dM = _tn(H, dY)           # Hᵀ·dY
+        dH = dX = None
+        if ctx.needs_input_grad[1]:
+            dX = _nn(H, dM)       # H·dM
+        if ctx.needs_input_grad[0]:
+            dH = _nt(dY, M)       # dY·Mᵀ
+            dH += _nt(X, dM)      # + X·dMᵀ
+        return dH, dX
+
+
+def dense_two_hop(H: torch.Tensor, X: torch.Tensor) -> torch.Tensor:
+    """``torch.mm(H, torch.mm(H.T, X))`` for the learned dense hypergraph; features (K, d)
+    multiples of 16 up to 128 run on hgd_linear_*, others on the library GEMM."""
+    if not _mm_ok(H, X):
+        return torch.mm(H, torch.mm(H.T, X))
+    return _DenseTwoHop.apply(H, X)

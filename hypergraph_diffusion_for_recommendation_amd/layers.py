@@ -29,7 +29,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .functional import layer_norm, linear, spmm, two_hop, two_hop_fused
+from .functional import dense_two_hop, layer_norm, linear, spmm, two_hop, two_hop_fused
 from .incidence import (CSR, Incidence, dense_threshold, drop_edges, expand_rows,
                         incidence_of)
 
@@ -48,15 +48,15 @@ class GCNLayer(nn.Module):
 
 class HGNNLayer(nn.Module):
     """Dense learned hypergraph: ``adj·(adjᵀ·embeds)`` with adj = dropout(E·W) [n, K]
-    (HCCF.py:201-211). K = hyper_dim (32) so both products are skinny library GEMMs."""
+    (HCCF.py:201-211). K = hyper_dim (32): both products are skinny — the split-K and row
+    MFMA kernels of hgd_linear_* (functional.dense_two_hop), forward and backward."""
 
     def __init__(self, leaky):
         super().__init__()
         self.act = nn.LeakyReLU(negative_slope=leaky)
 
     def forward(self, adj, embeds):
-        edge_embeds = torch.mm(adj.T, embeds)
-        return torch.mm(adj, edge_embeds)
+        return dense_two_hop(adj, embeds)
 
 
 class HGCNConv(nn.Module):

@@ -188,3 +188,24 @@ def test_equivset_fused_epilogue_matches_unfused(dev):
         for a, b in zip(*outs):
             s = b.abs().max().item() + 1e-6
             assert (a - b).abs().max().item() <= 5e-5 * s
+
+
+@pytest.mark.parametrize("n,K,d", [(31_668, 32, 64), (1000, 16, 32), (77, 48, 128)])
+def test_hgnn_layer_dense_two_hop(dev, n, K, d):
+    """HGNNLayer (HCCF.py:201-211) on the MFMA kernels vs float64: output and grads of H, X."""
+    from hypergraph_diffusion_for_recommendation_amd.layers import HGNNLayer
+    torch.manual_seed(n)
+    H = (torch.randn(n, K) * 0.2).to(dev).requires_grad_(True)
+    X = torch.randn(n, d).to(dev).requires_grad_(True)
+    dY = torch.randn(n, d).to(dev)
+    Y = HGNNLayer(0.5)(H, X)
+    gH, gX = torch.autograd.grad(Y, (H, X), dY)
+    Hd = H.detach().double().cpu().requires_grad_(True)
+    Xd = X.detach().double().cpu().requires_grad_(True)
+    Yd = Hd @ (Hd.T @ Xd)
+    rH, rX = torch.autograd.grad(Yd, (Hd, Xd), dY.double().cpu())
+    # |err| <= 1e-5 · Σ|terms| (magnitude from the same products on |·|)
+    mag = Hd.abs() @ (Hd.abs().T @ Xd.abs())
+    assert ((Y.detach().double().cpu() - Yd.detach()).abs() <= 1e-5 * mag + 1e-12).all()
+    for g, r in ((gH, rH), (gX, rX)):
+        assert (g.double().cpu() - r).abs().max().item() <= 1e-5 * r.abs().max().item() * 50
