@@ -97,7 +97,8 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--cpu-reps", type=int, default=3)
     ap.add_argument("--tag", default="yelp")
-    ap.add_argument("--variants", default="gpu_fused,gpu_unfused,gpu_reference_ops,cpu_reference_ops",
+    ap.add_argument("--variants",
+                    default="gpu_fused,gpu_fused_graph,gpu_unfused,gpu_reference_ops,cpu_reference_ops",
                     help="comma list of variants to run")
     args = ap.parse_args()
     import numpy as np
@@ -162,6 +163,28 @@ def main():
                         "ms_per_step": round(ms, 4)})
         # the reference's own op chain on the same GPU (torch.sparse.mm / index_add means,
         # nn.functional LayerNorm / Linear / dropout), same parameters
+        if "gpu_fused_graph" in want:
+            # the same fused step captured once in a HIP graph (static X / dY; dropout masks are
+            # drawn from the graph-safe philox state, fresh every replay)
+            m.conv.fused_epilogue = True
+            xs = X.detach().clone().requires_grad_(True)
+
+            def body():
+                m.zero_grad(set_to_none=False)
+                xs.grad = None
+                call(xs).backward(dY)
+
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                for _ in range(3):
+                    body()
+            torch.cuda.current_stream().wait_stream(side)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                call(xs).backward(dY)
+            ms = gpu_time(graph.replay, args.reps)
+            out.append({"form": form, "variant": "gpu_fused_graph", "ms_per_step": round(ms, 4)})
         if "gpu_reference_ops" in want:
             ref_step = make_reference_step(m, form, A, ui, N, d, dev, X, dY)
             out.append({"form": form, "variant": "gpu_reference_ops",
