@@ -161,6 +161,41 @@ def pmc_traffic(args, U, I, E):
     return traffic, f"FETCH_SIZE={out['FETCH_SIZE']:.0f}KB WRITE_SIZE={out['WRITE_SIZE']:.0f}KB per launch"
 
 
+def copy_peak_gbps(device, n_bytes=1 << 30, reps=10):
+    """Streaming ceiling of this box: a 1 GiB device-to-device copy (one read + one write
+    stream), timed as torch's copy_ and as a float4-per-thread copy kernel (hgd_epilogue_apply
+    with no activation); median of `reps` launches each, returns (best GB/s, {name: GB/s})."""
+    import torch
+
+    from hypergraph_diffusion_for_recommendation_amd import _native as nat
+    n = n_bytes // 4
+    a = torch.ones(n, device=device)
+    b = torch.empty_like(a)
+    lib = nat.load()
+
+    def hgd_copy():
+        nat.check(lib.hgd_epilogue_apply(a.data_ptr(), n, nat.EPI_NONE, 0.0, b.data_ptr(),
+                                         torch.cuda.current_stream(device).cuda_stream),
+                  "hgd_epilogue_apply")
+
+    rates = {}
+    for name, fn in (("torch_copy_", lambda: b.copy_(a)), ("float4_copy_kernel", hgd_copy)):
+        for _ in range(3):
+            fn()
+        ts = []
+        for _ in range(reps):
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        rates[name] = round(2.0 * n_bytes / (statistics.median(ts) * 1e-3) / 1e9, 1)
+    del a, b
+    return max(rates.values()), rates
+
+
 def main():
     args = parse()
     U0, I0, E0, zipf = WORKLOADS[args.workload]
@@ -302,6 +337,12 @@ def main():
             per[nm] = {"ms": round(statistics.mean(ms), 4),
                        "GBps": round(statistics.mean(by) / (statistics.mean(ms) * 1e-3) / 1e9, 1)}
         roofline["per_hop"] = per
+    if world == 1:
+        # also report a measured stream-copy peak on this box (read + write bytes)
+        cp, cp_detail = copy_peak_gbps(device)
+        roofline["measured_copy_GBps"] = round(cp, 1)
+        roofline["measured_copy_detail"] = cp_detail
+        roofline["frac_of_measured_copy"] = round(achieved / cp, 4) if cp > 0 else None
     if pmc_note:
         roofline["traffic_note"] = pmc_note
     if pmc is not None:
