@@ -44,7 +44,8 @@ template <int G>
 __global__ __launch_bounds__(256) void k_nce_gather(const float* __restrict__ E1, int64_t ld1,
                                                     const float* __restrict__ E2, int64_t ld2,
                                                     const int64_t* __restrict__ nodes, int64_t B,
-                                                    int32_t d, float inv_temp, float* P1,
+                                                    int64_t n_rows, int32_t d, float inv_temp,
+                                                    float* P1,
                                                     float* P2, float* inv1, float* inv2,
                                                     float* pos_logit) {
   constexpr int GPB = 256 / G;
@@ -52,7 +53,12 @@ __global__ __launch_bounds__(256) void k_nce_gather(const float* __restrict__ E1
   const int l = threadIdx.x % G;
   const int64_t b = static_cast<int64_t>(blockIdx.x) * GPB + g;
   if (b >= B) return;
-  const int64_t node = nodes[b];
+  // torch indexing semantics: negative ids count from the end (the reference passes
+  // torch.unique(emb.long()), HCCF.py:65-66, which yields -1 / 0 / 1); out-of-range ids are
+  // rejected by the caller — clamped here only so that no load leaves the table
+  int64_t node = nodes[b];
+  if (node < 0) node += n_rows;
+  node = node < 0 ? 0 : (node >= n_rows ? n_rows - 1 : node);
   const int c0 = 4 * l;
   const bool ok = c0 < d;
   f32x4 x1 = {0.f, 0.f, 0.f, 0.f}, x2 = {0.f, 0.f, 0.f, 0.f};
@@ -375,11 +381,11 @@ extern "C" hgd_status hgd_infonce_forward(const float* E1, int64_t ld1, const fl
   const int64_t gpb = 256 / G;
   const dim3 gg(static_cast<unsigned>((batch + gpb - 1) / gpb));
   switch (G) {
-    case 4: hipLaunchKernelGGL((k_nce_gather<4>), gg, dim3(256), 0, st, E1, ld1, E2, ld2, nodes, batch, d, inv_temp, P1, P2, inv_norm1, inv_norm2, pos_logit); break;
-    case 8: hipLaunchKernelGGL((k_nce_gather<8>), gg, dim3(256), 0, st, E1, ld1, E2, ld2, nodes, batch, d, inv_temp, P1, P2, inv_norm1, inv_norm2, pos_logit); break;
-    case 16: hipLaunchKernelGGL((k_nce_gather<16>), gg, dim3(256), 0, st, E1, ld1, E2, ld2, nodes, batch, d, inv_temp, P1, P2, inv_norm1, inv_norm2, pos_logit); break;
-    case 32: hipLaunchKernelGGL((k_nce_gather<32>), gg, dim3(256), 0, st, E1, ld1, E2, ld2, nodes, batch, d, inv_temp, P1, P2, inv_norm1, inv_norm2, pos_logit); break;
-    default: hipLaunchKernelGGL((k_nce_gather<64>), gg, dim3(256), 0, st, E1, ld1, E2, ld2, nodes, batch, d, inv_temp, P1, P2, inv_norm1, inv_norm2, pos_logit); break;
+    case 4: hipLaunchKernelGGL((k_nce_gather<4>), gg, dim3(256), 0, st, E1, ld1, E2, ld2, nodes, batch, n_rows, d, inv_temp, P1, P2, inv_norm1, inv_norm2, pos_logit); break;
+    case 8: hipLaunchKernelGGL((k_nce_gather<8>), gg, dim3(256), 0, st, E1, ld1, E2, ld2, nodes, batch, n_rows, d, inv_temp, P1, P2, inv_norm1, inv_norm2, pos_logit); break;
+    case 16: hipLaunchKernelGGL((k_nce_gather<16>), gg, dim3(256), 0, st, E1, ld1, E2, ld2, nodes, batch, n_rows, d, inv_temp, P1, P2, inv_norm1, inv_norm2, pos_logit); break;
+    case 32: hipLaunchKernelGGL((k_nce_gather<32>), gg, dim3(256), 0, st, E1, ld1, E2, ld2, nodes, batch, n_rows, d, inv_temp, P1, P2, inv_norm1, inv_norm2, pos_logit); break;
+    default: hipLaunchKernelGGL((k_nce_gather<64>), gg, dim3(256), 0, st, E1, ld1, E2, ld2, nodes, batch, n_rows, d, inv_temp, P1, P2, inv_norm1, inv_norm2, pos_logit); break;
   }
   hgd_status s = check_launch("hgd_infonce_forward gather");
   if (s != HGD_OK) return s;

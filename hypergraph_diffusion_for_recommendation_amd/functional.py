@@ -479,6 +479,12 @@ def contrast_loss(embeds1: torch.Tensor, embeds2: torch.Tensor, nodes: torch.Ten
                          "multiple of 16 in [16, 256]")
     if nodes.numel() == 0:
         raise ValueError("contrast_loss: empty batch")
+    n = embeds1.shape[0]
+    # torch indexing semantics (negative ids wrap; HCCF passes torch.unique(emb.long()), which
+    # holds -1 / 0 / 1); out of range raises like embeds[nodes] would
+    if bool(((nodes < -n) | (nodes >= n)).any()):
+        raise IndexError(f"contrast_loss: node index out of range for a table of {n} rows")
+    nodes = torch.where(nodes < 0, nodes + n, nodes)  # the gradient scatter needs [0, n)
     return _ContrastLoss.apply(embeds1, embeds2, nodes, float(temp))
 
 

@@ -209,6 +209,8 @@ hgd_status hgd_linear_backward_weight(const float* dY, int64_t ldy, const float*
  *   p1 = normalize(E1[nodes] + 1e-8), p2 = normalize(E2[nodes] + 1e-8)   (eps 1e-12)
  *   loss = -(1/B) Σ_b log( exp(<p1_b,p2_b>/τ) / (Σ_j exp(<p1_b,p2_j>/τ) + 1e-8) )
  * Only the B batch rows are gathered and normalised; the [B, B] exp-sum is never materialised.
+ * nodes follow torch indexing: negative ids count from the end of the table (HCCF.py:65-66 passes
+ * torch.unique(emb.long())); ids outside [-n_rows, n_rows) are the caller's error (clamped here).
  * Forward writes P1, P2 [B, d] (contiguous), inv_norm1/2 [B], pos_logit [B], deno [B] and the
  * scalar loss (all device). Backward recomputes the logits and writes dX1, dX2 [B, d] =
  * dloss/d(E1[nodes]), dloss/d(E2[nodes]) scaled by the device scalar *grad_loss; scattering

@@ -87,3 +87,26 @@ def test_infonce_rejects_bad_shapes(dev):
     with pytest.raises(ValueError):
         contrast_loss(torch.randn(10, 20, device=dev), torch.randn(10, 20, device=dev),
                       torch.arange(4, device=dev), 0.2)
+
+
+def test_infonce_torch_index_semantics(dev):
+    """HCCF passes torch.unique(emb.long()) (HCCF.py:65-66): ids like -1 / 0 / 1 index like torch
+    (negative from the end); out-of-range ids raise IndexError as embeds[nodes] would."""
+    from hypergraph_diffusion_for_recommendation_amd.functional import contrast_loss
+    torch.manual_seed(3)
+    E1 = torch.randn(50, 32, device=dev, requires_grad=True)
+    E2 = torch.randn(50, 32, device=dev, requires_grad=True)
+    emb = torch.randn(64, 32, device=dev) * 1.5
+    nodes = torch.unique(emb.long())
+    loss = contrast_loss(E1, E2, nodes, 0.2)
+    loss.backward()
+    c1 = E1.detach().double().cpu().requires_grad_(True)
+    c2 = E2.detach().double().cpu().requires_grad_(True)
+    ref = ref_cpu.contrast_loss(c1, c2, nodes.cpu(), 0.2)
+    ref.backward()
+    assert abs(loss.item() - ref.item()) <= 1e-5 * (abs(ref.item()) + 5.0)
+    assert (E1.grad.double().cpu() - c1.grad).abs().max().item() <= 1e-4 * c1.grad.abs().max().item()
+    with pytest.raises(IndexError):
+        contrast_loss(E1, E2, torch.tensor([0, 50], device=dev), 0.2)
+    with pytest.raises(IndexError):
+        contrast_loss(E1, E2, torch.tensor([-51], device=dev), 0.2)
