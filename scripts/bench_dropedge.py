@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-step cost of HCCF's edge dropout + GCN hop (SpAdjDropEdge → GCNLayer, HCCF.py:182) on a
-dataset-shaped normalised bipartite graph, for: the reference's CPU path (oracle/ref_cpu-style
+dataset-shaped normalised bipartite graph, for: the reference's CPU path (scripts/refops-style
 torch CPU ops), the GPU with the reference's CPU mask + from-scratch rebuild, the sort-free
 rebuild, and the device mask. Prints one JSON line per variant."""
 import argparse
@@ -29,7 +29,7 @@ def main():
     from hypergraph_diffusion_for_recommendation_amd import Incidence
     from hypergraph_diffusion_for_recommendation_amd.encoders import sparse_tensor_of
     from hypergraph_diffusion_for_recommendation_amd.layers import GCNLayer, SpAdjDropEdge
-    from oracle import hgd_oracle as O
+    import refops as O
 
     u, i = O.synthetic_incidence(args.users, args.items, args.edges, seed=0)
     A = O.normalize_graph_mat(O.bipartite_adjacency(u, i, args.users, args.items))

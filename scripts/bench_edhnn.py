@@ -9,7 +9,7 @@ normalised bipartite graph, for both forms:
 
 each with the fused row epilogue (hgd_spmm_fused) and with the reference's separate torch ops
 (``fused_epilogue = False``), plus the reference's CPU path for the SpMM form (torch.sparse.mm +
-nn.LayerNorm on the host, oracle/ref_cpu.hgcn_conv) on the same graph. Training mode (dropout
+nn.LayerNorm on the host, scripts/refops.hgcn_conv) on the same graph. Training mode (dropout
 on), synthetic graph and random weights. Prints one JSON line per variant.
 """
 import argparse
@@ -35,7 +35,7 @@ def make_reference_step(m, form, A, ui, N, d, dev, X, dY):
     layers2/EquivSetConv2.py:88-93), F.layer_norm / F.linear / F.dropout."""
     import torch
     import torch.nn.functional as F
-    from oracle import hgd_oracle as O
+    import refops as O
 
     c = m.conv
     p_drop = m.dropout.p
@@ -108,8 +108,8 @@ def main():
     from hypergraph_diffusion_for_recommendation_amd import edhnn_spmm
     from hypergraph_diffusion_for_recommendation_amd.encoders import sparse_tensor_of
     from hypergraph_diffusion_for_recommendation_amd.layers import EquivSetGNN
-    from oracle import hgd_oracle as O
-    from oracle import ref_cpu
+    import refops as O
+    import refops as ref_cpu
 
     u, i = O.synthetic_incidence(args.users, args.items, args.edges, seed=0)
     ui = O.bipartite_adjacency(u, i, args.users, args.items)

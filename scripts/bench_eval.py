@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Time the batched scoring + top-K evaluation (evaluation.rank_users) for every user of a
 dataset-shaped graph, beside the reference's per-user CPU formulation (score row, mask rated
-items, find_k_largest ordering via the oracle's closed form; numba is not installed, so the
+items, find_k_largest ordering via the closed form (scripts/refops); numba is not installed, so the
 CPU figure is a numpy port, timed on a user sample and scaled). One JSON line per variant."""
 import argparse
 import json
@@ -27,7 +27,7 @@ def main():
     import torch
 
     from hypergraph_diffusion_for_recommendation_amd.evaluation import rank_users, rated_csr
-    from oracle import hgd_oracle as O
+    import refops as O
 
     u, i = O.synthetic_incidence(args.users, args.items, args.edges, seed=0)
     R = sp.csr_matrix((np.ones(len(u), np.float32), (u, i)), shape=(args.users, args.items))

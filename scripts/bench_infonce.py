@@ -19,7 +19,7 @@ def main():
     import torch
 
     from hypergraph_diffusion_for_recommendation_amd.functional import contrast_loss
-    from oracle import ref_cpu
+    import refops as ref_cpu
     dev = torch.device("cuda")
     for N, d, B in ((31_668, 64, 2048), (1_000_000, 64, 2048), (10_000_000, 64, 4096)):
         E1 = torch.randn(N, d, device=dev, requires_grad=True)

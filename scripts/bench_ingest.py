@@ -2,7 +2,7 @@
 """Ingest + graph build on a synthetic "user\\titem\\t1" training file:
 the native path (hgd_ingest_read with N host threads → device id remap, coalesce, normalisation,
 CSR/CSC incidences) against the reference's Python path (FileIO.load_data_set's line loop, the
-Interaction dict loop, scipy csr_matrix + normalize_graph_mat; restated in oracle/) on a
+Interaction dict loop, scipy csr_matrix + normalize_graph_mat; restated in scripts/refops) on a
 bounded sample. Prints one JSON line per measurement."""
 import argparse
 import json
@@ -28,7 +28,7 @@ def main():
     import torch
 
     from hypergraph_diffusion_for_recommendation_amd.ingest import InteractionGraph, load_data_set
-    from oracle import hgd_oracle as O
+    import refops as O
 
     rng = np.random.default_rng(0)
     users = rng.integers(0, args.users, size=args.lines) * 7 + 3  # sparse raw id space
