@@ -9,7 +9,8 @@ encoder (paths relative to /root/reference/HD_SELFRec):
 * :class:`LocalAwareEncoder` model/graph/HGNN_HD4.py:336-405 (``--mode=local_only``)
 
 Everything sparse runs on libhgd, with the LayerNorm / residual after a hop fused into its store;
-dropout and HCCF's dense ``E·W`` products stay torch.
+HCCF's dense ``E·W`` and learned-hypergraph products run on the skinny MFMA kernels; dropout
+stays torch.
 """
 from __future__ import annotations
 
@@ -17,7 +18,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from .functional import two_hop_fused
+from .functional import linear, two_hop_fused
 from .incidence import Incidence, incidence_of
 from .layers import EquivSetGNN, GCNLayer, HGCNConv, HGNNLayer, LayerNorm, SpAdjDropEdge
 
@@ -79,8 +80,9 @@ class HCCFEncoder(nn.Module):
         embeddings = torch.cat([self.embedding_dict['user_emb'], self.embedding_dict['item_emb']], 0)
         hidden = [embeddings]
         gcn_hidden, hgnn_hidden = [], []
-        hyper_uu = self.embedding_dict['user_emb'] @ self.embedding_dict['user_w']
-        hyper_ii = self.embedding_dict['item_emb'] @ self.embedding_dict['item_w']
+        # E·W [n, d]·[d, K] on the skinny MFMA Linear (functional.linear takes W as [out, in])
+        hyper_uu = linear(self.embedding_dict['user_emb'], self.embedding_dict['user_w'].t())
+        hyper_ii = linear(self.embedding_dict['item_emb'], self.embedding_dict['item_w'].t())
         for _ in range(self.n_layers):
             gcn_emb = self.gcnlayer(self.edgeDropper(self.sparse_norm_adj, keep_rate), hidden[-1])
             hyper_uemb = self.hgnnlayer(self.drop_out(hyper_uu), hidden[-1][:nu])

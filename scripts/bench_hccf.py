@@ -1,0 +1,114 @@
+#!/usr/bin/env python3
+"""One HCCF training step (BASELINE configs[2]: Yelp2018-shaped, 3 layers, d = 64, InfoNCE SSL;
+HCCF.py:56-106) on one MI355X: forward (edge-dropped GCN hop + learned-hypergraph hops per
+layer), BPR + per-layer contrastLoss on users and items, backward, clip_grad_norm_ (where the
+reference calls it) and Adam. Variants:
+
+* hgd_cpu_mask     — encoders.HCCFEncoder: hops, drop-edge compaction / sort-free rebuild,
+                     HGNNLayer and InfoNCE on this library; the drop-edge mask drawn by the
+                     reference's CPU torch.rand (bit-identical masks for a seed);
+* hgd_device_mask  — the same with SpAdjDropEdge(device_rng=True);
+* reference_ops    — scripts/refops.HCCFEncoderRef + the reference's losses (torch.sparse.mm,
+                     torch.mm, F.normalize …) on the same GPU, same parameters.
+
+Synthetic graph (SURVEY.md §8d generator), random batches drawn on the device (the reference's
+Python sampler is outside the path). Prints one JSON line per variant."""
+import argparse
+import json
+import os
+import statistics
+import sys
+import types
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--users", type=int, default=31_668)
+    ap.add_argument("--items", type=int, default=38_048)
+    ap.add_argument("--edges", type=int, default=1_237_259)
+    ap.add_argument("--dim", type=int, default=64)
+    ap.add_argument("--layers", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--variants", default="hgd_cpu_mask,hgd_device_mask,reference_ops")
+    args = ap.parse_args()
+    import torch
+
+    import refops as R
+    from hypergraph_diffusion_for_recommendation_amd.encoders import HCCFEncoder
+    from hypergraph_diffusion_for_recommendation_amd.functional import contrast_loss
+
+    dev = torch.device("cuda")
+    u, i = R.synthetic_incidence(args.users, args.items, args.edges, seed=0)
+    A = R.normalize_graph_mat(R.bipartite_adjacency(u, i, args.users, args.items))
+    nu, ni = args.users, args.items
+    data = types.SimpleNamespace(n_users=nu, n_items=ni, norm_adj=A)
+    conf = dict(lrate=0.001, lr_decay=0.7, max_epoch=1, batch_size=args.batch, reg=0.1,
+                embedding_size=args.dim, hyper_dim=32, drop_rate=0.5, p=0.1,
+                n_layers=args.layers)
+    temp, cl_rate, keep = 0.2, 1e-4, 0.5
+    g = torch.Generator(device=dev).manual_seed(0)
+    batches = [(torch.randint(0, nu, (args.batch,), device=dev, generator=g),
+                torch.randint(0, ni, (args.batch,), device=dev, generator=g),
+                torch.randint(0, ni, (args.batch,), device=dev, generator=g)) for _ in range(8)]
+
+    def make_step(model, loss_fn):
+        opt = torch.optim.Adam(model.parameters(), lr=conf["lrate"])
+        state = {"k": 0}
+
+        def step():
+            uid, pid, nid = batches[state["k"] % len(batches)]
+            state["k"] += 1
+            ue, ie, gcn, hyp = model(keep_rate=keep)
+            anc, pos, neg = ue[uid], ie[pid], ie[nid]
+            ssl = 0
+            for layer in range(args.layers):
+                e1, e2 = gcn[layer].detach(), hyp[layer]
+                ssl = ssl + loss_fn(e1[:nu], e2[:nu], torch.unique(anc.long()), temp) \
+                    + loss_fn(e1[nu:], e2[nu:], torch.unique(pos.long()), temp)
+            loss = R.bpr_loss(anc, pos, neg) + cl_rate * ssl
+            opt.zero_grad()
+            torch.nn.utils.clip_grad_norm_(model.parameters(), 4)  # before backward, as HCCF.py:95
+            loss.backward()
+            opt.step()
+        return step
+
+    def timed(step):
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(args.reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            step()
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        return statistics.median(ts)
+
+    torch.manual_seed(0)
+    ours = HCCFEncoder(conf, data, dev)
+    ref = R.HCCFEncoderRef(nu, ni, args.dim, 32, args.layers, conf["drop_rate"],
+                           ours.sparse_norm_adj.detach().clone().coalesce())
+    ref.load_state_dict(ours.state_dict(), strict=False)
+    out = []
+    want = args.variants.split(",")
+    if "hgd_cpu_mask" in want:
+        out.append(("hgd_cpu_mask", timed(make_step(ours, contrast_loss))))
+    if "hgd_device_mask" in want:
+        ours.edgeDropper.device_rng = True
+        out.append(("hgd_device_mask", timed(make_step(ours, contrast_loss))))
+    if "reference_ops" in want:
+        out.append(("reference_ops", timed(make_step(ref, R.contrast_loss))))
+    for name, ms in out:
+        print(json.dumps({"variant": name, "ms_per_step": round(ms, 3), "users": nu,
+                          "items": ni, "edges": len(u), "d": args.dim, "layers": args.layers,
+                          "batch": args.batch}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -107,3 +107,61 @@ def find_k_largest(K, candidates):
 
 
 topk_closed_form = find_k_largest
+
+
+# ---- HCCF with the reference's torch ops (HCCF.py:136-226, loss_torch.py:5-9,103-110) -------
+def bpr_loss(user_emb, pos_item_emb, neg_item_emb):
+    """util/loss_torch.py:5-9."""
+    pos_score = torch.mul(user_emb, pos_item_emb).sum(dim=1)
+    neg_score = torch.mul(user_emb, neg_item_emb).sum(dim=1)
+    return torch.mean(-torch.log(10e-6 + torch.sigmoid(pos_score - neg_score)))
+
+
+def sp_adj_drop_edge(adj, keep_rate):
+    """SpAdjDropEdge.forward (HCCF.py:213-226): CPU torch.rand mask, device compaction."""
+    if keep_rate == 1.0:
+        return adj
+    vals = adj._values()
+    idxs = adj._indices()
+    mask = ((torch.rand(vals.size()) + keep_rate).floor()).type(torch.bool)
+    return torch.sparse_coo_tensor(idxs[:, mask.to(idxs.device)],
+                                   vals[mask.to(vals.device)] / keep_rate, adj.shape)
+
+
+class HCCFEncoderRef(torch.nn.Module):
+    """HCCFEncoder (HCCF.py:136-191) with the reference's ops: torch.sparse.mm GCN hop on the
+    edge-dropped norm_adj, torch.mm learned-hypergraph hops. Same parameter names as
+    encoders.HCCFEncoder, so a state_dict moves between them."""
+
+    def __init__(self, n_users, n_items, latent, hyper_dim, n_layers, drop_rate, sparse_adj):
+        super().__init__()
+        self.n_users, self.n_layers = n_users, n_layers
+        self.adj = sparse_adj
+        init = torch.nn.init.xavier_uniform_
+        dev = sparse_adj.device
+        self.embedding_dict = torch.nn.ParameterDict({
+            'user_emb': torch.nn.Parameter(init(torch.empty(n_users, latent)).to(dev)),
+            'item_emb': torch.nn.Parameter(init(torch.empty(n_items, latent)).to(dev)),
+            'user_w': torch.nn.Parameter(init(torch.empty(latent, hyper_dim)).to(dev)),
+            'item_w': torch.nn.Parameter(init(torch.empty(latent, hyper_dim)).to(dev)),
+        })
+        self.drop_out = torch.nn.Dropout(drop_rate)
+
+    def forward(self, keep_rate=0.5):
+        nu = self.n_users
+        e = self.embedding_dict
+        hidden = [torch.cat([e['user_emb'], e['item_emb']], 0)]
+        gcn_hidden, hgnn_hidden = [], []
+        hyper_uu = e['user_emb'] @ e['user_w']
+        hyper_ii = e['item_emb'] @ e['item_w']
+        for _ in range(self.n_layers):
+            gcn = torch.sparse.mm(sp_adj_drop_edge(self.adj, keep_rate), hidden[-1])
+            hu = self.drop_out(hyper_uu)
+            hi = self.drop_out(hyper_ii)
+            hyper_u = torch.mm(hu, torch.mm(hu.T, hidden[-1][:nu]))
+            hyper_i = torch.mm(hi, torch.mm(hi.T, hidden[-1][nu:]))
+            gcn_hidden.append(gcn)
+            hgnn_hidden.append(torch.cat([hyper_u, hyper_i], 0))
+            hidden.append(gcn + hgnn_hidden[-1])
+        emb = sum(hidden)
+        return emb[:nu], emb[nu:], gcn_hidden, hgnn_hidden
