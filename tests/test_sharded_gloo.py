@@ -65,13 +65,14 @@ def _graph(rank):
     return rows, cols
 
 
-def _worker(rank, world, port, outdir):
+def _worker(rank, world, port, outdir, scales):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from hypergraph_diffusion_for_recommendation_amd import sharded
     sharded.spmm_csr = _cpu_spmm  # CPU stand-in for the HIP hop (test only)
     rows, cols = _graph(rank)
-    sh = sharded.ShardedIncidence(_CPUIncidence(rows, cols, U_PER, I), n_chunks=3)
+    P, Q, R = scales
+    sh = sharded.ShardedIncidence(_CPUIncidence(rows, cols, U_PER, I), n_chunks=3, P=P, Q=Q, R=R)
     rng = np.random.default_rng(rank)
     X = torch.from_numpy(rng.standard_normal((U_PER, D)).astype(np.float32))
     dY = torch.from_numpy(rng.standard_normal((U_PER, D)).astype(np.float32))
@@ -93,23 +94,29 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2])
-def test_sharded_two_hop_matches_global(world):
+SCALES = [("sym", "mean", "sym"),   # hgconv2 (data/graph.py:28-42)
+          ("mean", "mean", None)]   # the ED-HNN vertex/edge means (layers2/EquivSetConv2.py:88-93)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("scales", SCALES, ids=["hgconv2", "mean2hop"])
+def test_sharded_two_hop_matches_global(world, scales):
     with tempfile.TemporaryDirectory() as td:
-        mp.start_processes(_worker, args=(world, _free_port(), td), nprocs=world, join=True,
-                           start_method="spawn")
+        mp.start_processes(_worker, args=(world, _free_port(), td, scales), nprocs=world,
+                           join=True, start_method="spawn")
         parts = [np.load(os.path.join(td, f"r{r}.npz")) for r in range(world)]
     assert all(int(p["n_chunks"]) == 3 for p in parts)
+    P, Q, R = scales
     rows = np.concatenate([_graph(r)[0] + r * U_PER for r in range(world)])
     cols = np.concatenate([_graph(r)[1] for r in range(world)])
     shape = (world * U_PER, I)
     X = np.concatenate([p["X"] for p in parts])
     dY = np.concatenate([p["dY"] for p in parts])
-    Y = O.two_hop(rows, cols, None, shape, X, "sym", "mean", "sym")
-    dX = O.two_hop_backward(rows, cols, None, shape, Y, dY, "sym", "mean", "sym")
+    Y = O.two_hop(rows, cols, None, shape, X, P, Q, R)
+    dX = O.two_hop_backward(rows, cols, None, shape, Y, dY, P, Q, R)
     got_Y = np.concatenate([p["Y"] for p in parts])
     got_dX = np.concatenate([p["dX"] for p in parts])
-    mag = O.two_hop(rows, cols, None, shape, np.abs(X), "sym", "mean", "sym")
-    dmag = O.two_hop(rows, cols, None, shape, np.abs(dY), "sym", "mean", "sym")
+    mag = O.two_hop(rows, cols, None, shape, np.abs(X), P, Q, R)
+    dmag = O.two_hop_backward(rows, cols, None, shape, Y, np.abs(dY), P, Q, R)
     assert np.all(np.abs(got_Y - Y) <= 1e-5 * mag + 1e-12)
     assert np.all(np.abs(got_dX - dX) <= 1e-5 * dmag + 1e-12)
