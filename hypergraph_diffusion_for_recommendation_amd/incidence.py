@@ -579,6 +579,9 @@ def incidence_of(adj, cache: bool = True) -> Incidence:
     if isinstance(adj, Incidence):
         return adj
     inc = getattr(adj, "_hgd_incidence", None) if cache else None
+    if (inc is not None and adj.layout == torch.strided
+            and getattr(adj, "_hgd_incidence_version", None) != adj._version):
+        inc = None  # a dense adjacency modified in place since its structure was taken
     if inc is None:
         if adj.layout == torch.sparse_coo:
             inc = Incidence.from_torch_sparse(adj)
@@ -589,6 +592,7 @@ def incidence_of(adj, cache: bool = True) -> Incidence:
         if cache:
             try:
                 adj._hgd_incidence = inc
+                adj._hgd_incidence_version = adj._version
             except (AttributeError, RuntimeError):
                 pass
     return inc

@@ -23,6 +23,7 @@ device :class:`~.incidence.Incidence` (also accepted directly).
 """
 from __future__ import annotations
 
+import weakref
 from typing import Optional
 
 import torch
@@ -241,14 +242,19 @@ class EquivSetConv(nn.Module):
                 m.reset_parameters()
 
     def _incidence(self, vertex, edges, N) -> Incidence:
-        key = (vertex.data_ptr(), edges.data_ptr(), vertex.numel(), int(N),
-               getattr(vertex, "_version", 0), getattr(edges, "_version", 0))
-        if self._cache is not None and self._cache[0] == key:
-            return self._cache[1]
+        # V from EquivSetGNN.generate_V_E carries its incidence; otherwise cache by tensor
+        # identity (weakrefs: an address or id() can be reused by a NEW tensor, e.g. the
+        # per-step learned hypergraph of HCCF_diffusion.py:205-206, and must not hit)
         inc = getattr(vertex, "_hgd_incidence", None)
-        if inc is None or inc.n_rows != N:
-            inc = Incidence.from_index_lists(vertex, edges, N)
-        self._cache = (key, inc)
+        if inc is not None and inc.n_rows == N:
+            return inc
+        c = self._cache
+        if (c is not None and c[0]() is vertex and c[1]() is edges
+                and c[2] == (int(N), vertex._version, edges._version)):
+            return c[3]
+        inc = Incidence.from_index_lists(vertex, edges, N)
+        self._cache = (weakref.ref(vertex), weakref.ref(edges),
+                       (int(N), vertex._version, edges._version), inc)
         return inc
 
     def forward(self, X, vertex, edges, X0):
@@ -281,12 +287,11 @@ class EquivSetConv(nn.Module):
     def _pos(self, index, n_out, tag):
         attr = f"_pos_{tag}"
         c = getattr(self, attr, None)
-        key = (index.data_ptr(), index.numel(), n_out)
-        if c is not None and c[0] == key:
-            return c[1]
+        if c is not None and c[0]() is index and c[1] == (index._version, n_out):
+            return c[2]
         inc = _position_incidence(index.to(torch.device("cuda") if index.device.type != "cuda"
                                            else index.device), n_out)
-        setattr(self, attr, (key, inc))
+        setattr(self, attr, (weakref.ref(index), (index._version, n_out), inc))
         return inc
 
 
@@ -342,9 +347,13 @@ class EquivSetGNN(nn.Module):
 
     def generate_V_E(self, n_nodes, hypergraph):
         """V = rows, E = cols of nonzero(hypergraph > 0), row-major (EquivSetGNN2.py:105-133)."""
-        key = (id(hypergraph), getattr(hypergraph, "_version", 0))
-        if self._ve_cache is not None and self._ve_cache[0] == key:
-            return self._ve_cache[1]
+        # cached per hypergraph OBJECT (weakref identity + version): the reference rebuilds V/E
+        # on every call, and a learned hypergraph (HCCF_diffusion.py:205-206) is a new tensor
+        # each step, whose id() may equal a dead predecessor's
+        version = getattr(hypergraph, "_version", 0)
+        c = self._ve_cache
+        if c is not None and c[0]() is hypergraph and c[1] == version:
+            return c[2]
         device = torch.device("cuda")
         if isinstance(hypergraph, Incidence):
             inc = hypergraph
@@ -369,5 +378,5 @@ class EquivSetGNN(nn.Module):
         # E spans max(E)+1 hyperedges in the reference (torch_scatter's output size); extra empty
         # columns of the incidence contribute nothing, so the cached incidence is reused as is.
         V._hgd_incidence = inc
-        self._ve_cache = (key, (V, E))
+        self._ve_cache = (weakref.ref(hypergraph), version, (V, E))
         return V, E
