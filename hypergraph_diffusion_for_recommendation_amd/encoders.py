@@ -155,3 +155,40 @@ class LocalAwareEncoder(nn.Module):
             all_embeddings += [ego_embeddings]
         nu = self.data.n_users
         return all_embeddings[-1][:nu], all_embeddings[-1][nu:]
+
+
+class HCCFDiffusionEncoder(HCCFEncoder):
+    """HCCF_diffusion's encoder (model/graph/HCCF_diffusion.py:131-215): HCCF with the learned
+    hypergraph hop replaced by one shared ED-HNN block (EquivSetGNN, mean aggregation) run on the
+    dense learned hypergraph dropout(E·W) [n, K] of users and of items — the repo's "hypergraph
+    diffusion". The V/E of that hypergraph (nonzero(H > 0)) change every call; they are taken on
+    the device (hgd_dense_threshold_*) and the two scatter-means run as one fused two-hop.
+    ``edhnn_user_n`` / ``edhnn_item_n`` (n + K) are the reference's E offsets, which do not
+    change the result (the extra hyperedge slots are empty)."""
+
+    def __init__(self, conf, data, device=None):
+        super().__init__(conf, data, device)
+        self.edhnn_user_n = self.data.n_users + self.n_edges
+        self.edhnn_item_n = self.data.n_items + self.n_edges
+        self.edhnn_args = dict(edhnn_config(self.latent_size))
+        self.edhnnlayer = EquivSetGNN(self.latent_size, self.edhnn_args).to(self.device)
+        del self.hgnnlayer
+
+    def forward(self, keep_rate=0.5):
+        nu = self.data.n_users
+        e = self.embedding_dict
+        hidden = [torch.cat([e['user_emb'], e['item_emb']], 0)]
+        gcn_hidden, hgnn_hidden = [], []
+        hyper_uu = linear(e['user_emb'], e['user_w'].t())
+        hyper_ii = linear(e['item_emb'], e['item_w'].t())
+        for _ in range(self.n_layers):
+            gcn_emb = self.gcnlayer(self.edgeDropper(self.sparse_norm_adj, keep_rate), hidden[-1])
+            hyper_uemb = self.edhnnlayer(hidden[-1][:nu], self.drop_out(hyper_uu),
+                                         self.edhnn_user_n)
+            hyper_iemb = self.edhnnlayer(hidden[-1][nu:], self.drop_out(hyper_ii),
+                                         self.edhnn_item_n)
+            gcn_hidden += [gcn_emb]
+            hgnn_hidden += [torch.cat([hyper_uemb, hyper_iemb], 0)]
+            hidden += [gcn_emb + hgnn_hidden[-1]]
+        emb = sum(hidden)
+        return emb[:nu], emb[nu:], gcn_hidden, hgnn_hidden

@@ -90,3 +90,46 @@ def test_local_aware_encoder_eval(dev):
     ref = x.numpy()
     got = torch.cat([ue, ie]).cpu().numpy()
     assert np.abs(got - ref).max() <= 2e-5 * max(1.0, np.abs(ref).max())
+
+
+def test_hccf_diffusion_encoder_eval(dev):
+    """HCCF_diffusion's encoder (HCCF_diffusion.py:131-215) in eval mode against a CPU
+    restatement with the reference's ops: torch.sparse.mm GCN hop, nonzero(H > 0) of the learned
+    hypergraph E·W with the n + K offset on E, scatter means (index_reduce), Linear(LN(·))."""
+    from hypergraph_diffusion_for_recommendation_amd.encoders import HCCFDiffusionEncoder
+    rng = np.random.default_rng(2)
+    U, I = 70, 55
+    u, i = random_coo(rng, U, I, 500)
+    A = O.normalize_graph_mat(O.bipartite_adjacency(u, i, U, I))
+    data = SimpleNamespace(n_users=U, n_items=I, norm_adj=A)
+    torch.manual_seed(0)
+    enc = HCCFDiffusionEncoder(HCCF_KW, data, device=dev).eval()
+    with torch.no_grad():
+        ue, ie, gcns, hyps = enc(keep_rate=1)
+    ec = copy.deepcopy(enc).cpu().eval()
+    e = {k: v.detach().cpu() for k, v in ec.embedding_dict.items()}
+    idx, vals = O.coo_of(A)
+    adj_c = ref_cpu.coo_tensor(idx[0], idx[1], vals, A.shape)
+    K = e["user_w"].shape[1]
+    blk = ec.edhnnlayer
+
+    def edhnn(x, H, n_nodes):
+        nz = torch.nonzero(H > 0)
+        V, E = nz[:, 0], nz[:, 1] + n_nodes
+        h = torch.relu(blk.lin_in(x))
+        h = ref_cpu.equivset_conv(h, V, E, h, blk.conv.W1, None, blk.conv.W, 0.0, "mean")
+        return torch.relu(h)
+
+    with torch.no_grad():
+        hidden = [torch.cat([e["user_emb"], e["item_emb"]], 0)]
+        huu, hii = e["user_emb"] @ e["user_w"], e["item_emb"] @ e["item_w"]
+        for layer in range(HCCF_KW["n_layers"]):
+            gcn = torch.sparse.mm(adj_c, hidden[-1])
+            hyp = torch.cat([edhnn(hidden[-1][:U], huu, U + K), edhnn(hidden[-1][U:], hii, I + K)])
+            for got, ref in ((gcns[layer], gcn), (hyps[layer], hyp)):
+                assert np.abs(got.cpu().numpy() - ref.numpy()).max() <= 2e-5 * max(
+                    1.0, ref.abs().max().item()), layer
+            hidden.append(gcn + hyp)
+        emb = sum(hidden)
+    assert np.abs(torch.cat([ue, ie]).cpu().numpy() - emb.numpy()).max() <= 2e-5 * max(
+        1.0, emb.abs().max().item())
