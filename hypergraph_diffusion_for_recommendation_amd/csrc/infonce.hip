@@ -17,23 +17,11 @@
 //     4 registers = the k index, in a permuted order the B operand follows); the split-j partials
 //     are summed in order and the F.normalize backward (dx = (dp − p<p,dp>)/‖x‖) is fused into
 //     that final pass. The scatter into the [N, d] table gradients is left to the caller.
+#include "device_util.h"
 #include "hgd_internal.h"
 
 namespace hgd {
 namespace {
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
-
-template <int G>
-__device__ __forceinline__ float group_sum(float v) {
-#pragma unroll
-  for (int m = G / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, G);
-  return v;
-}
 
 constexpr float kShift = 1e-8f;   // embeds + 1e-8 (loss_torch.py:104-105)
 constexpr float kNormEps = 1e-12f;  // F.normalize eps

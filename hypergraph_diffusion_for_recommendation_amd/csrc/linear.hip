@@ -20,18 +20,11 @@
 //    MFMAs of a 4-row step produce the whole 64 × 64 tile with (m, n) = (4i + t, 4j + u)
 //    permuted; the 4 waves are combined in LDS in wave order, the S slice partials by sum_rows in
 //    slice order. No atomics: results are bitwise reproducible.
+#include "device_util.h"
 #include "hgd_internal.h"
 
 namespace hgd {
 namespace {
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
-
-__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 
 __device__ __forceinline__ f32x4 relu_mask(f32x4 v, f32x4 m) {
   return f32x4{m.x > 0.f ? v.x : 0.f, m.y > 0.f ? v.y : 0.f, m.z > 0.f ? v.z : 0.f,

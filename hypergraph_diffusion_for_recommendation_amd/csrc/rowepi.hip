@@ -9,14 +9,13 @@
 // combines its lane groups in LDS in group order and writes one partial row; a second kernel sums
 // the partials in block order. The grid size depends only on (n_rows, d), so the result is
 // deterministic run to run.
+#include "device_util.h"
 #include "hgd_internal.h"
 
 namespace hgd {
 namespace {
 
 constexpr int kMaxBlocks = 1024;
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 struct RowEpiBwd {
   const float* dY;
@@ -37,34 +36,6 @@ struct RowEpiBwd {
   float* part_g;  // [gridDim.x, d] or NULL
   float* part_b;
 };
-
-template <int VEC>
-__device__ __forceinline__ void ld(const float* p, float (&v)[VEC]) {
-  if constexpr (VEC == 4) {
-    const f32x4 t = *reinterpret_cast<const f32x4*>(p);
-    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
-  } else {
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) v[i] = p[i];
-  }
-}
-
-template <int VEC>
-__device__ __forceinline__ void st(float* p, const float (&v)[VEC]) {
-  if constexpr (VEC == 4) {
-    *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
-  } else {
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) p[i] = v[i];
-  }
-}
-
-template <int G>
-__device__ __forceinline__ float group_sum(float v) {
-#pragma unroll
-  for (int m = G / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, G);
-  return v;
-}
 
 template <int G, int VEC>
 __global__ __launch_bounds__(kBlock) void k_rowepi_bwd(RowEpiBwd p) {
@@ -90,8 +61,8 @@ __global__ __launch_bounds__(kBlock) void k_rowepi_bwd(RowEpiBwd p) {
 #pragma unroll
     for (int i = 0; i < VEC; ++i) dy[i] = a[i] = 0.f;
     if (col_ok) {
-      ld<VEC>(p.dY + r * p.ldy + coff, dy);
-      if (need_a) ld<VEC>(p.A + r * p.lda + coff, a);
+      load_vec<VEC>(p.dY + r * p.ldy + coff, dy);
+      if (need_a) load_vec<VEC>(p.A + r * p.lda + coff, a);
     }
 #pragma unroll
     for (int i = 0; i < VEC; ++i) dy[i] *= p.out_scale;
@@ -127,7 +98,7 @@ __global__ __launch_bounds__(kBlock) void k_rowepi_bwd(RowEpiBwd p) {
 #pragma unroll
       for (int i = 0; i < VEC; ++i) da[i] = a[i] > 0.f ? da[i] : 0.f;
     }
-    if (col_ok) st<VEC>(p.dZ + r * p.ldz + coff, da);
+    if (col_ok) store_vec<VEC>(p.dZ + r * p.ldz + coff, da);
   }
   if (!p.part_g) return;  // block-uniform
 #pragma unroll
@@ -174,13 +145,13 @@ __global__ __launch_bounds__(kBlock) void k_rowepi_fwd(RowEpiFwd p) {
     float v[VEC];
 #pragma unroll
     for (int i = 0; i < VEC; ++i) v[i] = 0.f;
-    if (col_ok) ld<VEC>(p.Z + r * p.ldz + coff, v);
+    if (col_ok) load_vec<VEC>(p.Z + r * p.ldz + coff, v);
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
       if (e.act == HGD_EPI_LEAKY_RELU) v[i] = v[i] > 0.f ? v[i] : v[i] * e.slope;
       else if (e.act == HGD_EPI_RELU) v[i] = v[i] > 0.f ? v[i] : 0.f;
     }
-    if (e.act_out && col_ok) st<VEC>(e.act_out + r * e.ld_act + coff, v);
+    if (e.act_out && col_ok) store_vec<VEC>(e.act_out + r * e.ld_act + coff, v);
     if (e.layer_norm) {
       float t = 0.f;
       if (col_ok) {
@@ -212,24 +183,18 @@ __global__ __launch_bounds__(kBlock) void k_rowepi_fwd(RowEpiFwd p) {
     for (int i = 0; i < VEC; ++i) v[i] *= e.out_scale;
     if (e.res1) {
       float rv[VEC];
-      ld<VEC>(e.res1 + r * e.ld_res1 + coff, rv);
+      load_vec<VEC>(e.res1 + r * e.ld_res1 + coff, rv);
 #pragma unroll
       for (int i = 0; i < VEC; ++i) v[i] = fmaf(e.res1_scale, rv[i], v[i]);
     }
     if (e.res2) {
       float rv[VEC];
-      ld<VEC>(e.res2 + r * e.ld_res2 + coff, rv);
+      load_vec<VEC>(e.res2 + r * e.ld_res2 + coff, rv);
 #pragma unroll
       for (int i = 0; i < VEC; ++i) v[i] = fmaf(e.res2_scale, rv[i], v[i]);
     }
-    st<VEC>(p.Y + r * p.ldy + coff, v);
+    store_vec<VEC>(p.Y + r * p.ldy + coff, v);
   }
-}
-
-int next_pow2(int x) {
-  int p = 1;
-  while (p < x) p <<= 1;
-  return p;
 }
 
 template <int VEC>

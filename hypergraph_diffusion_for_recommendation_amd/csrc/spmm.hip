@@ -14,6 +14,7 @@
 //   * rows longer than the split plan's threshold are cut into fixed-size chunks handled by extra
 //     blocks placed FIRST in the grid (they are the longest work items); a fix-up kernel sums the
 //     chunk partials in chunk order — no float atomics anywhere.
+#include "device_util.h"
 #include "hgd_internal.h"
 
 namespace hgd {
@@ -52,50 +53,11 @@ __device__ __forceinline__ float epilogue(float y, int epi, float slope) {
   return y;
 }
 
-// Sum of v over the G lanes of this lane group (xor butterfly; every lane gets the total).
-template <int G>
-__device__ __forceinline__ float group_sum(float v) {
-#pragma unroll
-  for (int m = G / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, G);
-  return v;
-}
-
 // Cache-policy bits of the tuned variants (hgd_set_tuning(HGD_TUNE_SPMM_POLICY, bits)):
 constexpr int kPolNtStore = 1;   // Y rows: non-temporal stores (written once, never re-read here)
 constexpr int kPolNtIndex = 2;   // col / val streams: non-temporal loads (read exactly once)
 constexpr int kPolNtGather = 4;  // gathered X rows: non-temporal loads
 constexpr int kPolPrefetch = 8;  // software-pipelined index batches (see gather_sum)
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-template <int VEC, bool NT = false>
-__device__ __forceinline__ void load_vec(const float* p, float (&v)[VEC]) {
-  if constexpr (VEC == 4) {
-    f32x4 t;
-    if constexpr (NT)
-      t = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
-    else
-      t = *reinterpret_cast<const f32x4*>(p);
-    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
-  } else {
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) v[i] = p[i];
-  }
-}
-
-template <int VEC, bool NT = false>
-__device__ __forceinline__ void store_vec(float* p, const float (&v)[VEC]) {
-  if constexpr (VEC == 4) {
-    const f32x4 t = {v[0], v[1], v[2], v[3]};
-    if constexpr (NT)
-      __builtin_nontemporal_store(t, reinterpret_cast<f32x4*>(p));
-    else
-      *reinterpret_cast<f32x4*>(p) = t;
-  } else {
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) p[i] = v[i];
-  }
-}
 
 // Scale, epilogue and store of one finished row r (all G lanes of the group call it together).
 // With EX the hgd_row_epilogue runs in registers: the group holds the whole row (single column
@@ -511,12 +473,6 @@ hgd_status launch_vec(int G, const SpmmArgs& a, bool has_val, hipStream_t st) {
     case 64: return launch_g<64, VEC, EX>(a, has_val, st);
     default: return fail(HGD_ERR_UNSUPPORTED, "hgd_spmm: unsupported group size %d", G);
   }
-}
-
-int next_pow2(int x) {
-  int p = 1;
-  while (p < x) p <<= 1;
-  return p;
 }
 
 }  // namespace
