@@ -200,27 +200,176 @@ __global__ void k_edge_values(const float* __restrict__ base, const int32_t* __r
   out[e] = v;
 }
 
-__global__ void k_mask_to_i64(const uint8_t* __restrict__ mask, int64_t n,
-                              int64_t* __restrict__ flags) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
-  if (i > n) return;
-  flags[i] = (i < n && mask[i]) ? 1 : 0;
+// ---- ordered stream compaction, reduce-then-scan over tiles ----------------------------------
+// The drop-edge paths keep the entries whose flag is set, in order. A device-wide scan of one
+// flag per entry (hipcub DeviceScan, decoupled lookback over ~n/2048 blocks) costs a serial
+// chain of block-to-block handoffs — 27 µs for 2.3 M entries, 20x the bytes it moves. Here:
+// k_tile_count counts each 2,048-entry tile, k_tile_scan (one block) turns the counts into tile
+// offsets, and k_tile_compact recomputes the flags and writes every kept entry at
+// tile offset + its in-tile prefix (wave ballots + a 4-wave LDS prefix per 256-entry round).
+constexpr int kTileThreads = 256;
+constexpr int kTileIter = 8;
+constexpr int64_t kTile = static_cast<int64_t>(kTileThreads) * kTileIter;
+
+struct MaskFlag {  // entry e kept iff mask[perm ? perm[e] : e] != 0
+  const uint8_t* mask;
+  const int32_t* perm;
+  __device__ bool operator()(int64_t e) const { return mask[perm ? perm[e] : e] != 0; }
+};
+
+struct StructWriter {  // one orientation: idx_out[p] = idx[e], val_out[p] = val[e] / keep
+  const int32_t* idx;
+  const float* val;
+  float keep;
+  int32_t* idx_out;
+  float* val_out;
+  __device__ void operator()(int64_t e, int64_t p) const {
+    idx_out[p] = idx[e];
+    if (val) val_out[p] = __fdiv_rn(val[e], keep);  // IEEE fp32 division like vals / keepRate
+  }
+};
+
+struct CooWriter {  // idxs[:, mask], vals[mask] / keepRate
+  const int64_t* rows;
+  const int64_t* cols;
+  const float* val;
+  float keep;
+  int64_t* out_rows;
+  int64_t* out_cols;
+  float* out_val;
+  __device__ void operator()(int64_t e, int64_t p) const {
+    out_rows[p] = rows[e];
+    out_cols[p] = cols[e];
+    out_val[p] = __fdiv_rn(val[e], keep);
+  }
+};
+
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
 }
 
-__global__ void k_dropedge_scatter(const int64_t* __restrict__ rows,
-                                   const int64_t* __restrict__ cols,
-                                   const float* __restrict__ val,
-                                   const uint8_t* __restrict__ mask,
-                                   const int64_t* __restrict__ pos, int64_t nnz, float keep,
-                                   int64_t* __restrict__ out_rows, int64_t* __restrict__ out_cols,
-                                   float* __restrict__ out_val, int64_t* __restrict__ out_count) {
-  const int64_t e = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
-  if (e == nnz) *out_count = pos[nnz];
-  if (e >= nnz || !mask[e]) return;
-  const int64_t p = pos[e];
-  out_rows[p] = rows[e];
-  out_cols[p] = cols[e];
-  out_val[p] = __fdiv_rn(val[e], keep);  // vals[mask] / keepRate, IEEE fp32 division
+template <class F>
+__global__ __launch_bounds__(kTileThreads) void k_tile_count(F flag, int64_t n,
+                                                            int32_t* __restrict__ tile_cnt) {
+  __shared__ int s_w[kTileThreads / 64];
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kTile;
+  int c = 0;
+#pragma unroll
+  for (int j = 0; j < kTileIter; ++j) {
+    const int64_t e = base + j * kTileThreads + threadIdx.x;
+    c += (e < n && flag(e)) ? 1 : 0;
+  }
+  c = wave_sum_i(c);
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int w = 0; w < kTileThreads / 64; ++w) t += s_w[w];
+    tile_cnt[blockIdx.x] = t;
+  }
+}
+
+// One block: off[t] = Σ_{t' < t} cnt[t'] for t <= n_tiles (off[n_tiles] = total).
+__global__ __launch_bounds__(1024) void k_tile_scan(const int32_t* __restrict__ cnt,
+                                                   int64_t n_tiles, int64_t* __restrict__ off) {
+  __shared__ int64_t s[1024];
+  const int64_t per = (n_tiles + 1023) / 1024;
+  const int64_t t0 = static_cast<int64_t>(threadIdx.x) * per;
+  const int64_t t1 = t0 + per < n_tiles ? t0 + per : n_tiles;
+  int64_t sum = 0;
+  for (int64_t t = t0; t < t1; ++t) sum += cnt[t];
+  s[threadIdx.x] = sum;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {
+    const int64_t v = static_cast<int>(threadIdx.x) >= d ? s[threadIdx.x - d] : 0;
+    __syncthreads();
+    s[threadIdx.x] += v;
+    __syncthreads();
+  }
+  int64_t run = s[threadIdx.x] - sum;
+  for (int64_t t = t0; t < t1; ++t) {
+    off[t] = run;
+    run += cnt[t];
+  }
+  if (threadIdx.x == 1023) off[n_tiles] = s[1023];
+}
+
+template <class F, class W>
+__global__ __launch_bounds__(kTileThreads) void k_tile_compact(F flag, W write, int64_t n,
+                                                              const int64_t* __restrict__ tile_off,
+                                                              int32_t* __restrict__ pos_in_tile) {
+  __shared__ int s_w[kTileThreads / 64];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kTile;
+  const int64_t off = tile_off[blockIdx.x];
+  int in_tile = 0;
+  for (int j = 0; j < kTileIter; ++j) {
+    const int64_t e = base + j * kTileThreads + threadIdx.x;
+    const bool f = e < n && flag(e);
+    const unsigned long long ball = __ballot(f);
+    const int before = __popcll(ball & ((1ull << lane) - 1ull));
+    if (lane == 0) s_w[wave] = __popcll(ball);
+    __syncthreads();
+    int wave_off = 0, round = 0;
+#pragma unroll
+    for (int w = 0; w < kTileThreads / 64; ++w) {
+      wave_off += w < wave ? s_w[w] : 0;
+      round += s_w[w];
+    }
+    const int my = in_tile + wave_off + before;  // kept entries of this tile before e
+    if (pos_in_tile && e < n) pos_in_tile[e] = my;
+    if (f) write(e, off + my);
+    in_tile += round;
+    __syncthreads();
+  }
+}
+
+// rowptr_out[r] = number of kept entries before rowptr[r].
+__global__ void k_rowptr_tiles(const int64_t* __restrict__ rowptr, int64_t n_rows, int64_t n,
+                               const int64_t* __restrict__ tile_off,
+                               const int32_t* __restrict__ pos_in_tile, int64_t n_tiles,
+                               int64_t* __restrict__ rowptr_out) {
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (r > n_rows) return;
+  const int64_t e0 = rowptr[r];
+  rowptr_out[r] = e0 < n ? tile_off[e0 / kTile] + pos_in_tile[e0] : tile_off[n_tiles];
+}
+
+__global__ void k_copy_i64(const int64_t* __restrict__ src, int64_t* __restrict__ dst) {
+  *dst = *src;
+}
+
+int64_t n_tiles_for(int64_t n) { return (n + kTile - 1) / kTile; }
+
+size_t tile_ws_bytes(int64_t n, bool with_pos) {
+  const int64_t t = n_tiles_for(n);
+  return align_up(static_cast<size_t>(t + 1) * sizeof(int32_t)) +
+         align_up(static_cast<size_t>(t + 1) * sizeof(int64_t)) +
+         (with_pos ? align_up(static_cast<size_t>(n + 1) * sizeof(int32_t)) : 0);
+}
+
+// Launches count → scan → compact (+ optional in-tile positions) on `ws`.
+template <class F, class W>
+hgd_status tile_compact(F flag, W write, int64_t n, char* ws, bool with_pos, hipStream_t st,
+                        int64_t** tile_off_out, int32_t** pos_out, const char* what) {
+  const int64_t t = n_tiles_for(n);
+  int32_t* cnt = reinterpret_cast<int32_t*>(ws);
+  int64_t* off = reinterpret_cast<int64_t*>(ws + align_up(static_cast<size_t>(t + 1) * 4));
+  int32_t* pos = with_pos ? reinterpret_cast<int32_t*>(
+                                ws + align_up(static_cast<size_t>(t + 1) * 4) +
+                                align_up(static_cast<size_t>(t + 1) * 8))
+                          : nullptr;
+  if (t > 0x7fffffffLL) return fail(HGD_ERR_UNSUPPORTED, "%s: too many tiles", what);
+  hipLaunchKernelGGL((k_tile_count<F>), dim3(t), dim3(kTileThreads), 0, st, flag, n, cnt);
+  hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, st, cnt, t, off);
+  hipLaunchKernelGGL((k_tile_compact<F, W>), dim3(t), dim3(kTileThreads), 0, st, flag, write, n,
+                     off, pos);
+  *tile_off_out = off;
+  if (pos_out) *pos_out = pos;
+  return check_launch(what);
 }
 
 // Counter-based keep-mask: u = 24-bit uniform in [0,1) from a splitmix64 hash of (seed, i);
@@ -239,32 +388,6 @@ __global__ void k_bernoulli_mask(uint64_t seed, int64_t n, float keep,
   const uint64_t h = splitmix64(seed ^ splitmix64(static_cast<uint64_t>(i)));
   const float u = static_cast<float>(h >> 40) * (1.0f / 16777216.0f);
   mask[i] = floorf(u + keep) != 0.f ? 1 : 0;
-}
-
-// flags[i] = mask[perm ? perm[i] : i] (0/1), flags[n] = 0 for the exclusive-scan total.
-__global__ void k_mask_flags(const uint8_t* __restrict__ mask, const int32_t* __restrict__ perm,
-                             int64_t n, int64_t* __restrict__ flags) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
-  if (i > n) return;
-  flags[i] = (i < n && mask[perm ? perm[i] : i]) ? 1 : 0;
-}
-
-// Order-preserving compaction of one orientation + its row pointer:
-// idx_out[pos[e]] = idx[e], val_out[pos[e]] = val[e] / keep for kept e; rowptr_out[r] = pos[rowptr[r]].
-__global__ void k_compact_orientation(const int64_t* __restrict__ rowptr, int64_t n_rows,
-                                      const int32_t* __restrict__ idx,
-                                      const float* __restrict__ val,
-                                      const int64_t* __restrict__ flags,
-                                      const int64_t* __restrict__ pos, int64_t nnz, float keep,
-                                      int64_t* __restrict__ rowptr_out,
-                                      int32_t* __restrict__ idx_out,
-                                      float* __restrict__ val_out) {
-  const int64_t e = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
-  if (e <= n_rows) rowptr_out[e] = pos[rowptr[e]];
-  if (e >= nnz || !flags[e]) return;
-  const int64_t p = pos[e];
-  idx_out[p] = idx[e];
-  if (val && val_out) val_out[p] = __fdiv_rn(val[e], keep);
 }
 
 // HGD_DENSE_GREATER: v > thresh (torch.nonzero(H > thresh)); HGD_DENSE_NONZERO: v != 0
@@ -518,8 +641,7 @@ extern "C" hgd_status hgd_edge_values(const float* base, const int32_t* perm,
 }
 
 extern "C" size_t hgd_dropedge_workspace_size(int64_t nnz) {
-  return 2 * align_up(static_cast<size_t>(nnz + 1) * sizeof(int64_t)) +
-         align_up(excl_scan_bytes<int64_t>(nnz + 1));
+  return tile_ws_bytes(nnz, false);
 }
 
 extern "C" hgd_status hgd_dropedge_compact(const int64_t* rows, const int64_t* cols,
@@ -541,19 +663,14 @@ extern "C" hgd_status hgd_dropedge_compact(const int64_t* rows, const int64_t* c
   if (workspace_bytes < need || !workspace)
     return fail(HGD_ERR_WORKSPACE, "hgd_dropedge_compact: workspace %zu < %zu", workspace_bytes,
                 need);
-  const size_t arr = align_up(static_cast<size_t>(nnz + 1) * sizeof(int64_t));
-  char* ws = static_cast<char*>(workspace);
-  int64_t* flags = reinterpret_cast<int64_t*>(ws);
-  int64_t* pos = reinterpret_cast<int64_t*>(ws + arr);
-  hipLaunchKernelGGL(k_mask_to_i64, dim3(grid_for(nnz + 1)), dim3(kBlock), 0, st, mask, nnz,
-                     flags);
-  hgd_status s = check_launch("hgd_dropedge_compact flags");
+  int64_t* off = nullptr;
+  hgd_status s = tile_compact(MaskFlag{mask, nullptr},
+                              CooWriter{rows, cols, val, keep, out_rows, out_cols, out_val}, nnz,
+                              static_cast<char*>(workspace), false, st, &off, nullptr,
+                              "hgd_dropedge_compact");
   if (s != HGD_OK) return s;
-  size_t b = workspace_bytes - 2 * arr;
-  HGD_HIP(hipcub::DeviceScan::ExclusiveSum(ws + 2 * arr, b, flags, pos, nnz + 1, st));
-  hipLaunchKernelGGL(k_dropedge_scatter, dim3(grid_for(nnz + 1)), dim3(kBlock), 0, st, rows, cols,
-                     val, mask, pos, nnz, keep, out_rows, out_cols, out_val, out_count);
-  return check_launch("hgd_dropedge_compact scatter");
+  hipLaunchKernelGGL(k_copy_i64, dim3(1), dim3(1), 0, st, off + n_tiles_for(nnz), out_count);
+  return check_launch("hgd_dropedge_compact count");
 }
 
 extern "C" hgd_status hgd_bernoulli_mask(uint64_t seed, int64_t n, float keep, uint8_t* mask,
@@ -567,8 +684,7 @@ extern "C" hgd_status hgd_bernoulli_mask(uint64_t seed, int64_t n, float keep, u
 }
 
 extern "C" size_t hgd_dropedge_structure_workspace_size(int64_t nnz) {
-  return 2 * align_up(static_cast<size_t>(nnz + 1) * sizeof(int64_t)) +
-         align_up(excl_scan_bytes<int64_t>(nnz + 1));
+  return tile_ws_bytes(nnz, true);
 }
 
 extern "C" hgd_status hgd_dropedge_structure(
@@ -590,28 +706,31 @@ extern "C" hgd_status hgd_dropedge_structure(
     return fail(HGD_ERR_WORKSPACE, "hgd_dropedge_structure: workspace %zu < %zu",
                 workspace_bytes, need);
   hipStream_t st = as_stream(stream);
-  const size_t arr = align_up(static_cast<size_t>(nnz + 1) * sizeof(int64_t));
-  char* ws = static_cast<char*>(workspace);
-  int64_t* flags = reinterpret_cast<int64_t*>(ws);
-  int64_t* pos = reinterpret_cast<int64_t*>(ws + arr);
-  void* tmp = ws + 2 * arr;
-  const size_t tmp_bytes = workspace_bytes - 2 * arr;
-  // CSR: the mask is in CSR order
+  const int64_t nt = n_tiles_for(nnz);
+  // the two orientations run one after the other on the same workspace (stream-ordered)
   for (int side = 0; side < 2; ++side) {
     const bool csc = side == 1;
     const int64_t nr = csc ? n_cols : n_rows;
-    hipLaunchKernelGGL(k_mask_flags, dim3(grid_for(nnz + 1)), dim3(kBlock), 0, st, mask,
-                       csc ? perm_t : nullptr, nnz, flags);
-    hgd_status s = check_launch("hgd_dropedge_structure flags");
-    if (s != HGD_OK) return s;
-    size_t b = tmp_bytes;
-    HGD_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, b, flags, pos, nnz + 1, st));
-    hipLaunchKernelGGL(k_compact_orientation, dim3(grid_for(std::max(nnz, nr + 1))),
-                       dim3(kBlock), 0, st, csc ? colptr : rowptr, nr, csc ? row_t : col,
-                       csc ? val_t : val, flags, pos, nnz, keep, csc ? colptr_out : rowptr_out,
-                       csc ? row_t_out : col_out, csc ? val_t_out : val_out);
-    s = check_launch("hgd_dropedge_structure compact");
-    if (s != HGD_OK) return s;
+    const int64_t* ptr = csc ? colptr : rowptr;
+    int64_t* ptr_out = csc ? colptr_out : rowptr_out;
+    int64_t* off = nullptr;
+    int32_t* pos = nullptr;
+    if (nnz > 0) {
+      // CSR: the mask is in CSR order; CSC: entry e is CSR entry perm_t[e]
+      hgd_status s = tile_compact(
+          MaskFlag{mask, csc ? perm_t : nullptr},
+          StructWriter{csc ? row_t : col, csc ? val_t : val, keep, csc ? row_t_out : col_out,
+                       csc ? val_t_out : val_out},
+          nnz, static_cast<char*>(workspace), true, st, &off, &pos,
+          "hgd_dropedge_structure compact");
+      if (s != HGD_OK) return s;
+      hipLaunchKernelGGL(k_rowptr_tiles, dim3(grid_for(nr + 1)), dim3(kBlock), 0, st, ptr, nr,
+                         nnz, off, pos, nt, ptr_out);
+      s = check_launch("hgd_dropedge_structure rowptr");
+      if (s != HGD_OK) return s;
+    } else {
+      HGD_HIP(hipMemsetAsync(ptr_out, 0, static_cast<size_t>(nr + 1) * sizeof(int64_t), st));
+    }
   }
   return HGD_OK;
 }
