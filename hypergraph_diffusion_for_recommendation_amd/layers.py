@@ -112,13 +112,16 @@ class SpAdjDropEdge(nn.Module):
             mask = ((torch.rand(edgeNum) + keepRate).floor()).type(torch.bool)
             count = int(mask.sum())
             mask = mask.to(device, non_blocking=True)
+        child = None
+        if parent is not None and parent.coo_sorted and parent.perm_t is not None:
+            # COO order == CSR order: the structure first, its kept count (the one device→host
+            # read of the step) then sizes the COO compaction
+            child = parent.drop(mask, keepRate)
+            count = child.nnz
         new_idx, new_vals = drop_edges(idxs.to(device), vals.to(device), mask, keepRate, count)
         out = torch.sparse_coo_tensor(new_idx, new_vals, adj.shape)
-        if parent is not None and parent.coo_sorted and parent.perm_t is not None:
-            out._hgd_incidence = parent.drop(mask, keepRate)  # COO order == CSR order
-        else:
-            out._hgd_incidence = Incidence.from_coo(new_idx, new_vals, adj.shape, device=device,
-                                                    validate=False)
+        out._hgd_incidence = child if child is not None else Incidence.from_coo(
+            new_idx, new_vals, adj.shape, device=device, validate=False)
         return out
 
 
