@@ -86,3 +86,15 @@ def test_struct_layouts_match_header(tmp_path):
         assert got[(cname, "size")] == __import__("ctypes").sizeof(py), cname
         for f, _ in py._fields_:
             assert got[(cname, f)] == getattr(py, f).offset, (cname, f)
+
+
+def test_c_host_example_compiles_against_the_header(tmp_path):
+    """include/hgd.h is valid C11 and every call of examples/hgconv2_host.c links against
+    libhgd.so (compile + link only: no device here)."""
+    if not os.path.exists("/opt/rocm/include/hip/hip_runtime_api.h"):
+        pytest.skip("ROCm headers not available")
+    from tests._native_host import build
+    exe = build(tmp_path / "hgconv2_host")
+    if exe is None:
+        pytest.skip("gcc not available")
+    assert os.path.exists(exe)
