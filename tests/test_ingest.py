@@ -98,3 +98,55 @@ def test_ingest_empty_file_and_missing(tmp_path):
         load_data_set(p)
     with pytest.raises(nat.HGDNativeError, match="cannot open"):
         load_data_set(str(tmp_path / "nope.csv"))
+
+
+def _field(draw, st):
+    sign = draw(st.sampled_from(["", "", "+", "-"]))
+    digits = draw(st.text(alphabet="0123456789", min_size=1, max_size=12))
+    if draw(st.booleans()) and len(digits) > 1:  # one '_' between digits (valid for int())
+        k = draw(st.integers(1, len(digits) - 1))
+        digits = digits[:k] + "_" + digits[k:]
+    pad = st.sampled_from(["", " ", "  ", "\x0b", "\x0c"])
+    return draw(pad) + sign + digits + draw(pad)
+
+
+def test_ingest_fuzz_against_restated_loader(tmp_path):
+    """Random well-formed and malformed lines: the native parser returns exactly what the
+    restated FileIO.load_data_set returns, and fails exactly where it raises."""
+    hypothesis = pytest.importorskip("hypothesis")
+    st = hypothesis.strategies
+    from hypergraph_diffusion_for_recommendation_amd import _native as nat
+    from hypergraph_diffusion_for_recommendation_amd.ingest import load_data_set
+
+    @st.composite
+    def line(draw):
+        kind = draw(st.sampled_from(["tab", "comma", "comma", "tab_extra", "bad"]))
+        a, b = _field(draw, st), _field(draw, st)
+        if kind == "tab":
+            return a + "\t" + b
+        if kind == "comma":
+            return a + "," + b
+        if kind == "tab_extra":
+            return a + "\t" + b + "\t" + draw(st.sampled_from(["1", "0.5", "x", ""]))
+        return draw(st.sampled_from(["", " ", a, a + " " + b, a + ",", "1.5,2", "x,1"]))
+
+    @hypothesis.settings(max_examples=150, deadline=None,
+                         suppress_health_check=list(hypothesis.HealthCheck))
+    @hypothesis.given(st.lists(line(), min_size=0, max_size=12),
+                      st.sampled_from(["\n", "\r\n"]))
+    def check(lines, nl):
+        path = tmp_path / "f.txt"
+        path.write_bytes(("hdr" + nl + nl.join(lines) + (nl if lines else "")).encode())
+        try:
+            ref = O.load_data_set(str(path))
+        except (ValueError, IndexError):
+            with pytest.raises(nat.HGDNativeError):
+                load_data_set(str(path))
+            return
+        if any(abs(r[0]) >= 2 ** 63 or abs(r[1]) >= 2 ** 63 for r in ref):
+            return  # Python ints are unbounded; the native ids are int64
+        u, i = load_data_set(str(path))
+        assert u.tolist() == [r[0] for r in ref]
+        assert i.tolist() == [r[1] for r in ref]
+
+    check()
