@@ -68,6 +68,30 @@ class RowEpilogue(ctypes.Structure):
     ]
 
 
+class IncidenceView(ctypes.Structure):
+    """Mirror of ``hgd_incidence_view`` (include/hgd.h)."""
+
+    _fields_ = [
+        ("n_rows", c_i64),
+        ("n_cols", c_i64),
+        ("nnz", c_i64),
+        ("rowptr", c_void_p),
+        ("col", c_void_p),
+        ("val", c_void_p),
+        ("colptr", c_void_p),
+        ("row_t", c_void_p),
+        ("val_t", c_void_p),
+        ("perm_t", c_void_p),
+    ]
+
+
+SCALE_NONE, SCALE_MEAN, SCALE_SYM, SCALE_WMEAN, SCALE_WSYM = 0, 1, 2, 3, 4
+SCALE_KINDS = {None: SCALE_NONE, "mean": SCALE_MEAN, "sym": SCALE_SYM, "wmean": SCALE_WMEAN,
+               "wsym": SCALE_WSYM}
+SIDE_ROWS, SIDE_COLS = 0, 1
+COMM_ID_BYTES = 128
+_PP = ctypes.POINTER(c_void_p)
+
 # name -> (restype, argtypes); every symbol of include/hgd.h appears here.
 _SIGNATURES = {
     "hgd_version": (c_i32, []),
@@ -153,6 +177,32 @@ _SIGNATURES = {
     "hgd_epilogue_apply": (c_i32, [c_void_p, c_i64, c_i32, c_f32, c_void_p, c_void_p]),
     "hgd_epilogue_backward": (c_i32, [c_void_p, c_void_p, c_i64, c_i32, c_f32, c_void_p,
                                       c_void_p]),
+    # incidence objects, conv2hop, RCCL exchange
+    "hgd_incidence_create": (c_i32, [c_void_p, c_void_p, c_void_p, c_i64, c_i64, c_i64, _PP,
+                                     c_void_p]),
+    "hgd_incidence_from_dense": (c_i32, [c_void_p, c_i64, c_i64, c_i64, c_f32, c_i32, c_i32,
+                                         _PP, c_void_p]),
+    "hgd_incidence_dropedge": (c_i32, [c_void_p, c_void_p, c_f32, _PP, c_void_p]),
+    "hgd_incidence_destroy": (None, [c_void_p]),
+    "hgd_incidence_get_view": (c_i32, [c_void_p, ctypes.POINTER(IncidenceView)]),
+    "hgd_incidence_scale": (c_i32, [c_void_p, c_i32, c_i32, _PP]),
+    "hgd_incidence_prepare": (c_i32, [c_void_p, ctypes.c_uint32, c_void_p]),
+    "hgd_incidence_workspace_size": (c_size, [c_void_p, c_i32]),
+    "hgd_incidence_spmm": (c_i32, [c_void_p, c_i32, c_void_p, c_i64, c_void_p, c_i64, c_i32,
+                                   c_void_p, c_i32, c_f32, c_void_p, c_size, c_void_p]),
+    "hgd_comm_get_unique_id": (c_i32, [c_void_p]),
+    "hgd_comm_create": (c_i32, [c_void_p, c_i32, c_i32, _PP]),
+    "hgd_comm_destroy": (None, [c_void_p]),
+    "hgd_comm_set_chunks": (c_i32, [c_void_p, c_i32]),
+    "hgd_exchange_allreduce": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p]),
+    "hgd_incidence_globalize_columns": (c_i32, [c_void_p, c_void_p, c_void_p]),
+    "hgd_conv2hop_workspace_size": (c_size, [c_void_p, c_i32, c_i32]),
+    "hgd_conv2hop_forward": (c_i32, [c_void_p, c_i32, c_i32, c_i32, c_void_p, c_i64, c_i32,
+                                     c_void_p, c_i64, c_i32, c_f32, c_void_p, c_void_p, c_void_p,
+                                     c_void_p, c_size, c_void_p]),
+    "hgd_conv2hop_backward": (c_i32, [c_void_p, c_i32, c_i32, c_i32, c_void_p, c_i64, c_i32,
+                                      c_void_p, c_i32, c_f32, c_void_p, c_i64, c_void_p,
+                                      c_void_p, c_size, c_void_p]),
 }
 
 _lib = None

@@ -369,6 +369,139 @@ hgd_status hgd_epilogue_apply(const float* z, int64_t n, int32_t epilogue, float
 hgd_status hgd_epilogue_backward(const float* ref, const float* dy, int64_t n, int32_t epilogue,
                                  float slope, float* dz, void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * Incidence objects (SURVEY.md §8b "C ABI libhgd"): the library-owned form of the structure the
+ * flat calls above take as loose arrays. One object holds H's CSR (rows = vertices / users,
+ * columns = hyperedges / items), its CSC, the CSC→CSR permutation, the degree scales of both
+ * sides and the split plans — what the reference's torch.sparse COO `adj` plus cuSPARSE's
+ * per-call coalesce/transpose stand for (base/torch_interface.py:8-12, HGNN_HD4.py:455-462).
+ *
+ *   hgd_incidence_create      convert_sparse_mat_to_tensor + the per-call adj.t() / coalesce
+ *   hgd_incidence_from_dense  torch.nonzero(H > 0) of EquivSetGNN2.generate_V_E
+ *                             (layers2/EquivSetGNN2.py:105-133) and DHCF's dense adjacency
+ *   hgd_incidence_dropedge    SpAdjDropEdge.forward (HCCF.py:213-226) without a sort
+ *   hgd_incidence_spmm        torch.sparse.mm(adj, X) / torch.sparse.mm(adj.t(), X)
+ *   hgd_conv2hop_forward/     HGCNConv.forward (HGNN_HD4.py:455-462), the ED-HNN scatter-mean
+ *   hgd_conv2hop_backward     pair (layers2/EquivSetConv2.py:88-93), HGNN normalisation
+ *                             (data/graph.py:28-42) and their autograd backward
+ *
+ * Creation and drop-edge are setup calls: they allocate device memory (hipMalloc) and
+ * synchronise `stream` once (split-plan and kept counts). The object is then immutable apart
+ * from lazily built per-nonzero weights (guarded by an internal mutex; hgd_incidence_prepare
+ * builds them ahead of graph capture), so it may be used from several threads and streams
+ * at once. The object owns its arrays; callers' buffers are only read.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct hgd_incidence hgd_incidence;
+
+/* Degree scales of one side of H (torch_scatter 'mean' = 1/deg, data/graph.py:11-25 and :28-42
+ * D^-1/2 / D^-1 with inf→0; the W-variants use the weighted degree Σ val). */
+typedef enum hgd_scale {
+  HGD_SCALE_NONE = 0,
+  HGD_SCALE_MEAN = 1,  /* deg^-1   */
+  HGD_SCALE_SYM = 2,   /* deg^-1/2 */
+  HGD_SCALE_WMEAN = 3, /* (Σ val)^-1   */
+  HGD_SCALE_WSYM = 4   /* (Σ val)^-1/2 */
+} hgd_scale;
+#define HGD_SIDE_ROWS 0
+#define HGD_SIDE_COLS 1
+
+/* Copies the CSR (rowptr [n_rows+1] int64, col [nnz] int32, val [nnz] or NULL = binary; device
+ * pointers) into a new object, validates it (rowptr monotone from 0 to nnz, 0 <= col < n_cols;
+ * columns need not be sorted within a row) and derives the CSC (stable: rows ascending within a
+ * column), scales and split plans. */
+hgd_status hgd_incidence_create(const int64_t* rowptr, const int32_t* col, const float* val,
+                                int64_t n_rows, int64_t n_cols, int64_t nnz,
+                                hgd_incidence** out, void* stream);
+/* The object of torch.nonzero(H > thresh) (HGD_DENSE_GREATER) or torch.nonzero(H)
+ * (HGD_DENSE_NONZERO) of a dense [n_rows, n_cols] matrix (leading dim ld); keep_values != 0
+ * keeps H's entries as values, otherwise the incidence is binary. */
+hgd_status hgd_incidence_from_dense(const float* H, int64_t n_rows, int64_t n_cols, int64_t ld,
+                                    float thresh, int32_t mode, int32_t keep_values,
+                                    hgd_incidence** out, void* stream);
+/* SpAdjDropEdge: the child keeps the nonzeros with keep_mask[e] != 0 (CSR order, nnz bytes) and
+ * carries values val[e]/keep (a binary parent's values are 1, so the child's are 1/keep).
+ * Built by compaction of the parent's CSR and CSC (no sort). A child cannot be dropped again
+ * (the reference always drops the base adjacency). */
+hgd_status hgd_incidence_dropedge(const hgd_incidence* parent, const uint8_t* keep_mask,
+                                  float keep, hgd_incidence** out, void* stream);
+void hgd_incidence_destroy(hgd_incidence* inc);
+
+/* Read-only view of the object's device arrays (valid until destroy). */
+typedef struct hgd_incidence_view {
+  int64_t n_rows, n_cols, nnz;
+  const int64_t* rowptr;  /* CSR */
+  const int32_t* col;
+  const float* val;       /* NULL: binary */
+  const int64_t* colptr;  /* CSC */
+  const int32_t* row_t;
+  const float* val_t;
+  const int32_t* perm_t;  /* CSC position → CSR position (NULL for a drop-edge child) */
+} hgd_incidence_view;
+hgd_status hgd_incidence_get_view(const hgd_incidence* inc, hgd_incidence_view* out);
+/* Device pointer to the object's degree scale of one side (HGD_SIDE_ROWS / HGD_SIDE_COLS);
+ * NULL for HGD_SCALE_NONE. The column scales are the global ones after
+ * hgd_incidence_globalize_columns. */
+hgd_status hgd_incidence_scale(const hgd_incidence* inc, int32_t side, int32_t kind,
+                               const float** out);
+/* Builds the per-nonzero weights conv2hop needs for source-side scales `kinds_mask`
+ * (bit k = hgd_scale k) now, so that later calls allocate nothing (graph capture). */
+hgd_status hgd_incidence_prepare(const hgd_incidence* inc, uint32_t kinds_mask, void* stream);
+
+/* Workspace of hgd_incidence_spmm for width d (the split-plan partials). */
+size_t hgd_incidence_workspace_size(const hgd_incidence* inc, int32_t d);
+/* Y = epi(row_scale ⊙ (A·X)) (transpose = 0, Y has n_rows rows) or epi(row_scale ⊙ (Aᵀ·X))
+ * (transpose = 1, served by the CSC, Y has n_cols rows); values are A's. row_scale: NULL or a
+ * device array over Y's rows (e.g. from hgd_incidence_scale). */
+hgd_status hgd_incidence_spmm(const hgd_incidence* inc, int32_t transpose, const float* X,
+                              int64_t ldx, float* Y, int64_t ldy, int32_t d,
+                              const float* row_scale, int32_t epilogue, float slope,
+                              void* workspace, size_t workspace_bytes, void* stream);
+
+/* Multi-GPU exchange: one process per GPU, users (rows of H) sharded in
+ * contiguous ranges, items (columns) replicated; RCCL over xGMI. The communicator owns a side
+ * stream for the chunked, overlapped all-reduce of the item sums. */
+typedef struct hgd_comm hgd_comm;
+#define HGD_COMM_ID_BYTES 128
+/* Rank 0 creates the id (host buffer of HGD_COMM_ID_BYTES) and distributes it out of band. */
+hgd_status hgd_comm_get_unique_id(void* id_out);
+/* Collective over the nranks processes; binds the communicator to the current HIP device. */
+hgd_status hgd_comm_create(const void* id, int32_t nranks, int32_t rank, hgd_comm** out);
+void hgd_comm_destroy(hgd_comm* comm);
+/* Item chunks per exchange for the overlapped hop (default 4, 1..64). */
+hgd_status hgd_comm_set_chunks(hgd_comm* comm, int32_t n_chunks);
+/* In-place sum of a device fp32 buffer over the ranks, ordered on `stream`. */
+hgd_status hgd_exchange_allreduce(hgd_comm* comm, float* buf, int64_t count, void* stream);
+/* Replaces the object's column degrees by their sum over the ranks (each rank holds a user
+ * shard of the same item set), so column scales — the Q of conv2hop — are global. Collective;
+ * synchronises `stream`. */
+hgd_status hgd_incidence_globalize_columns(hgd_incidence* inc, hgd_comm* comm, void* stream);
+
+/* The two-hop conv over the object, Y = epi(P·A·Q·Aᵀ·R·X) with P, R row scales and Q a column
+ * scale (hgd_scale each):
+ *   HGCNConv (HGNN_HD4.py:455-462)        P = Q = R = NONE on the weighted norm_adj
+ *   ED-HNN mean pair (EquivSetConv2:88-93) P = MEAN, Q = MEAN, R = NONE on the binary V/E incidence
+ *   HGNN normalisation (graph.py:28-42)    P = SYM, Q = MEAN, R = SYM (the benchmarked op)
+ * Forward: hop 1 M = Q·Aᵀ·(R·X) over the CSC into the workspace (copied to saved_M when not
+ * NULL), hop 2 Y = epi(P·A·M) over the CSR. An activation with slope >= 0 is fused into hop 2;
+ * with slope < 0, pre_act [n_rows, d] (contiguous) receives P·A·M and Y = epi(pre_act).
+ * Backward: dZ = epi'(dY) (act_ref = the forward Y when slope >= 0, else pre_act; NULL without
+ * an epilogue), dM = Q·Aᵀ·(P·dZ), dX = R·A·dM — the same hops with P and R swapped.
+ * comm != NULL: this rank's A is a user shard; hop 1's item sums are all-reduced (chunked and
+ * overlapped on the communicator's stream) before hop 2; Q must be NONE or the global
+ * MEAN / SYM of hgd_incidence_globalize_columns. Epilogues with slope < 0 or dY with ldy != d
+ * need contiguous rows. Workspace: hgd_conv2hop_workspace_size. */
+size_t hgd_conv2hop_workspace_size(const hgd_incidence* inc, int32_t d, int32_t epilogue);
+hgd_status hgd_conv2hop_forward(const hgd_incidence* inc, int32_t P, int32_t Q, int32_t R,
+                                const float* X, int64_t ldx, int32_t d, float* Y, int64_t ldy,
+                                int32_t epilogue, float slope, float* saved_M, float* pre_act,
+                                hgd_comm* comm, void* workspace, size_t workspace_bytes,
+                                void* stream);
+hgd_status hgd_conv2hop_backward(const hgd_incidence* inc, int32_t P, int32_t Q, int32_t R,
+                                 const float* dY, int64_t ldy, int32_t d, const float* act_ref,
+                                 int32_t epilogue, float slope, float* dX, int64_t ldx,
+                                 hgd_comm* comm, void* workspace, size_t workspace_bytes,
+                                 void* stream);
+
 #ifdef __cplusplus
 }
 #endif

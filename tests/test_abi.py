@@ -68,7 +68,8 @@ def test_struct_layouts_match_header(tmp_path):
     from hypergraph_diffusion_for_recommendation_amd import _native
     if shutil.which("gcc") is None:
         pytest.skip("gcc not available")
-    structs = {"hgd_split_plan": _native.SplitPlan, "hgd_row_epilogue": _native.RowEpilogue}
+    structs = {"hgd_split_plan": _native.SplitPlan, "hgd_row_epilogue": _native.RowEpilogue,
+               "hgd_incidence_view": _native.IncidenceView}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "hgd.h"', 'int main(void) {']
     for cname, py in structs.items():
         lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
@@ -89,12 +90,13 @@ def test_struct_layouts_match_header(tmp_path):
 
 
 def test_c_host_example_compiles_against_the_header(tmp_path):
-    """include/hgd.h is valid C11 and every call of examples/hgconv2_host.c links against
-    libhgd.so (compile + link only: no device here)."""
+    """include/hgd.h is valid C11 and every call of the examples/ hosts (flat ABI and incidence
+    objects + RCCL exchange) links against libhgd.so (compile + link only: no device here)."""
     if not os.path.exists("/opt/rocm/include/hip/hip_runtime_api.h"):
         pytest.skip("ROCm headers not available")
     from tests._native_host import build
-    exe = build(tmp_path / "hgconv2_host")
-    if exe is None:
-        pytest.skip("gcc not available")
-    assert os.path.exists(exe)
+    for src in ("hgconv2_host.c", "conv2hop_objects.c"):
+        exe = build(tmp_path / src[:-2], src)
+        if exe is None:
+            pytest.skip("gcc not available")
+        assert os.path.exists(exe)

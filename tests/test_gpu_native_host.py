@@ -16,3 +16,17 @@ def test_c_host_hgconv2(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr + r.stdout
     assert "hgconv2_host ok" in r.stdout
+
+
+def test_c_host_conv2hop_objects(tmp_path):
+    """examples/conv2hop_objects.c: incidence object, one-rank RCCL communicator, sharded conv
+    forward + backward against the host float64 computation."""
+    import os
+    from tests._native_host import build
+    exe = build(tmp_path / "conv2hop_objects", "conv2hop_objects.c")
+    if exe is None:
+        pytest.skip("gcc not available")
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=180, env=env)
+    assert r.returncode == 0, r.stderr + r.stdout
+    assert "conv2hop_objects ok" in r.stdout
