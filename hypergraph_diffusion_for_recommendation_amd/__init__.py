@@ -13,8 +13,8 @@ with the reference's operator signatures:
 """
 from . import _native
 from .incidence import CSR, Incidence, incidence_of, spmm_csr
-from .functional import hgconv2, mean2hop, spmm, two_hop
+from .functional import contrast_loss, hgconv2, mean2hop, spmm, two_hop, unique_long
 
 __all__ = ["CSR", "Incidence", "incidence_of", "spmm_csr", "spmm", "two_hop", "hgconv2",
-           "mean2hop", "_native"]
+           "mean2hop", "contrast_loss", "unique_long", "_native"]
 __version__ = "0.1.0"

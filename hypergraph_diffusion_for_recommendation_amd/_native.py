@@ -177,6 +177,14 @@ _SIGNATURES = {
     "hgd_epilogue_apply": (c_i32, [c_void_p, c_i64, c_i32, c_f32, c_void_p, c_void_p]),
     "hgd_epilogue_backward": (c_i32, [c_void_p, c_void_p, c_i64, c_i32, c_f32, c_void_p,
                                       c_void_p]),
+    "hgd_unique_workspace_size": (c_size, [c_i64]),
+    "hgd_unique_i64": (c_i32, [c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_size, c_void_p]),
+    "hgd_unique_trunc_f32": (c_i32, [c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_size,
+                                     c_void_p]),
+    "hgd_unique_sort_i64": (c_i32, [c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_size,
+                                    c_void_p]),
+    "hgd_unique_sort_trunc_f32": (c_i32, [c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_size,
+                                          c_void_p]),
     # incidence objects, conv2hop, RCCL exchange
     "hgd_incidence_create": (c_i32, [c_void_p, c_void_p, c_void_p, c_i64, c_i64, c_i64, _PP,
                                      c_void_p]),

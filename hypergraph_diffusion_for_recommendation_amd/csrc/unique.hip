@@ -1,0 +1,359 @@
+// Sorted unique of integer keys: torch.unique(x.long()) as HCCF's loss calls it on every step,
+// `contrastLoss(..., torch.unique(ancs.long()), ...)` (model/graph/HCCF.py:65-66), over a
+// [batch, d] float embedding block (262,144 values at batch 4096, d = 64). torch runs a device
+// merge sort for it — ~20 launches per call, ~0.7 ms of an HCCF step (profiles/r01_hccf) —
+// although the truncated values span a handful of integers.
+//
+// Here: a range bitmap. One pass finds min / max; if the range fits kCapBits, every key sets its
+// bit (block-private LDS bitmap first when the range is small, so the hot words see one global
+// atomicOr per block — OR is idempotent, so the result does not depend on the order), then a
+// tile count / one-block scan / emit pass writes the set bits in ascending order: exactly
+// torch.unique's sorted output. No host synchronisation: a range beyond the bitmap writes
+// *n_out = -1 and the caller runs hgd_unique_sort (radix sort + unique, same result).
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <climits>
+
+#include "device_util.h"
+#include "hgd_internal.h"
+
+namespace hgd {
+namespace {
+
+constexpr int64_t kCapBits = int64_t(1) << 24;  // 2 MB bitmap
+constexpr int64_t kCapWords = kCapBits / 32;
+constexpr int kEmitThreads = 256;
+constexpr int kWordsPerThread = 8;
+constexpr int64_t kTileWords = kEmitThreads * kWordsPerThread;  // 2048 words = 65,536 bits
+constexpr int64_t kMaxTiles = kCapWords / kTileWords;           // 256
+constexpr int kLdsWords = 1024;                                 // block-private bitmap
+constexpr unsigned kGrid = 512;
+
+struct State {
+  long long lo, hi;  // min / max key
+  int overflow;
+  int pad;
+};
+
+struct I64Src {
+  const int64_t* p;
+  __device__ int64_t operator()(int64_t i) const { return p[i]; }
+};
+
+// float → int64 like Tensor.long(): truncation toward zero; NaN / ±inf / |x| >= 2^63 (undefined
+// in C++) map to INT64_MIN, the x86 "integer indefinite" torch's CPU cast produces.
+struct TruncSrc {
+  const float* p;
+  __device__ int64_t operator()(int64_t i) const {
+    const float x = p[i];
+    if (!(fabsf(x) < 9.2233720368547758e18f)) return INT64_MIN;
+    return static_cast<int64_t>(x);
+  }
+};
+
+__device__ __forceinline__ long long wave_min(long long v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    const long long w = __shfl_xor(v, o);
+    v = w < v ? w : v;
+  }
+  return v;
+}
+__device__ __forceinline__ long long wave_max(long long v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    const long long w = __shfl_xor(v, o);
+    v = w > v ? w : v;
+  }
+  return v;
+}
+
+__global__ void k_uq_init(State* st) {
+  st->lo = LLONG_MAX;
+  st->hi = LLONG_MIN;
+  st->overflow = 0;
+}
+
+template <class Src>
+__global__ __launch_bounds__(256) void k_uq_minmax(Src src, int64_t n, State* st) {
+  long long lo = LLONG_MAX, hi = LLONG_MIN;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += stride) {
+    const long long k = src(i);
+    lo = k < lo ? k : lo;
+    hi = k > hi ? k : hi;
+  }
+  lo = wave_min(lo);
+  hi = wave_max(hi);
+  if ((threadIdx.x & 63) == 0 && lo <= hi) {
+    atomicMin(&st->lo, lo);
+    atomicMax(&st->hi, hi);
+  }
+}
+
+__device__ __forceinline__ bool range_words(const State* st, int64_t* words) {
+  const long long lo = st->lo, hi = st->hi;
+  if (lo > hi) {  // no keys
+    *words = 0;
+    return true;
+  }
+  // hi - lo may overflow int64: compare in unsigned
+  const unsigned long long span = static_cast<unsigned long long>(hi) -
+                                  static_cast<unsigned long long>(lo);
+  if (span >= static_cast<unsigned long long>(kCapBits)) return false;
+  *words = static_cast<int64_t>((span + 1 + 31) / 32);
+  return true;
+}
+
+__global__ __launch_bounds__(256) void k_uq_zero(uint32_t* bitmap, State* st) {
+  int64_t words;
+  if (!range_words(st, &words)) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->overflow = 1;
+    return;
+  }
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t w = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; w < words;
+       w += stride)
+    bitmap[w] = 0u;
+}
+
+template <class Src>
+__global__ __launch_bounds__(256) void k_uq_mark(Src src, int64_t n, uint32_t* bitmap,
+                                                 const State* st) {
+  __shared__ uint32_t s_bits[kLdsWords];
+  int64_t words;
+  if (!range_words(st, &words) || words == 0) return;  // uniform over the grid
+  const long long lo = st->lo;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  const int64_t i0 = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  if (words <= kLdsWords) {
+    for (int w = threadIdx.x; w < words; w += blockDim.x) s_bits[w] = 0u;
+    __syncthreads();
+    for (int64_t i = i0; i < n; i += stride) {
+      const uint64_t b = static_cast<uint64_t>(src(i)) - static_cast<uint64_t>(lo);
+      atomicOr(&s_bits[b >> 5], 1u << (b & 31));
+    }
+    __syncthreads();
+    for (int w = threadIdx.x; w < words; w += blockDim.x)
+      if (s_bits[w]) atomicOr(&bitmap[w], s_bits[w]);
+  } else {
+    for (int64_t i = i0; i < n; i += stride) {
+      const uint64_t b = static_cast<uint64_t>(src(i)) - static_cast<uint64_t>(lo);
+      atomicOr(&bitmap[b >> 5], 1u << (b & 31));
+    }
+  }
+}
+
+__device__ __forceinline__ int block_exclusive_scan(int v, int* total) {
+  __shared__ int s_wave[kEmitThreads / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int incl = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(incl, o);
+    if (lane >= o) incl += u;
+  }
+  if (lane == 63) s_wave[wave] = incl;
+  __syncthreads();
+  int base = 0, all = 0;
+#pragma unroll
+  for (int w = 0; w < kEmitThreads / 64; ++w) {
+    base += w < wave ? s_wave[w] : 0;
+    all += s_wave[w];
+  }
+  *total = all;
+  return base + incl - v;
+}
+
+__global__ __launch_bounds__(kEmitThreads) void k_uq_count(const uint32_t* bitmap,
+                                                           const State* st, int* tile_cnt) {
+  int64_t words;
+  if (!range_words(st, &words)) return;
+  const int64_t tiles = (words + kTileWords - 1) / kTileWords;
+  if (blockIdx.x >= tiles) return;
+  const int64_t w0 = blockIdx.x * kTileWords + threadIdx.x * kWordsPerThread;
+  int c = 0;
+#pragma unroll
+  for (int j = 0; j < kWordsPerThread; ++j)
+    if (w0 + j < words) c += __popc(bitmap[w0 + j]);
+  int total;
+  (void)block_exclusive_scan(c, &total);
+  if (threadIdx.x == 0) tile_cnt[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kMaxTiles) void k_uq_scan(const int* tile_cnt, const State* st,
+                                                       int64_t* tile_off, int64_t* n_out) {
+  __shared__ int64_t s[kMaxTiles];
+  int64_t words;
+  if (!range_words(st, &words)) {
+    if (threadIdx.x == 0) *n_out = -1;  // the caller runs hgd_unique_sort
+    return;
+  }
+  const int64_t tiles = (words + kTileWords - 1) / kTileWords;
+  const int64_t v = threadIdx.x < tiles ? tile_cnt[threadIdx.x] : 0;
+  s[threadIdx.x] = v;
+  __syncthreads();
+  for (int d = 1; d < kMaxTiles; d <<= 1) {
+    const int64_t u = static_cast<int>(threadIdx.x) >= d ? s[threadIdx.x - d] : 0;
+    __syncthreads();
+    s[threadIdx.x] += u;
+    __syncthreads();
+  }
+  if (threadIdx.x < tiles) tile_off[threadIdx.x] = s[threadIdx.x] - v;
+  if (threadIdx.x == kMaxTiles - 1) *n_out = s[threadIdx.x];
+}
+
+__global__ __launch_bounds__(kEmitThreads) void k_uq_emit(const uint32_t* bitmap, const State* st,
+                                                          const int64_t* tile_off, int64_t* out) {
+  int64_t words;
+  if (!range_words(st, &words)) return;
+  const int64_t tiles = (words + kTileWords - 1) / kTileWords;
+  if (blockIdx.x >= tiles) return;
+  const long long lo = st->lo;
+  const int64_t w0 = blockIdx.x * kTileWords + threadIdx.x * kWordsPerThread;
+  uint32_t bits[kWordsPerThread];
+  int c = 0;
+#pragma unroll
+  for (int j = 0; j < kWordsPerThread; ++j) {
+    bits[j] = w0 + j < words ? bitmap[w0 + j] : 0u;
+    c += __popc(bits[j]);
+  }
+  int total;
+  int64_t pos = tile_off[blockIdx.x] + block_exclusive_scan(c, &total);
+#pragma unroll
+  for (int j = 0; j < kWordsPerThread; ++j) {
+    uint32_t b = bits[j];
+    while (b) {
+      const int k = __ffs(b) - 1;
+      b &= b - 1;
+      out[pos++] = static_cast<int64_t>(static_cast<unsigned long long>(lo) +
+                                        static_cast<unsigned long long>((w0 + j) * 32 + k));
+    }
+  }
+}
+
+template <class Src>
+__global__ void k_uq_materialize(Src src, int64_t n, int64_t* keys) {
+  const int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  if (i < n) keys[i] = src(i);
+}
+
+// workspace layout of the bitmap path
+constexpr size_t kOffState = 0;
+constexpr size_t kOffCnt = 256;
+constexpr size_t kOffTileOff = kOffCnt + kMaxTiles * sizeof(int);
+constexpr size_t kOffBitmap = kOffTileOff + kMaxTiles * sizeof(int64_t);
+constexpr size_t kBitmapPathBytes = kOffBitmap + kCapWords * sizeof(uint32_t);
+
+size_t sort_path_bytes(int64_t n) {
+  size_t a = 0, b = 0;
+  if (hipcub::DeviceRadixSort::SortKeys(nullptr, a, static_cast<const int64_t*>(nullptr),
+                                        static_cast<int64_t*>(nullptr), static_cast<int>(n)) !=
+      hipSuccess)
+    return 0;
+  if (hipcub::DeviceSelect::Unique(nullptr, b, static_cast<const int64_t*>(nullptr),
+                                   static_cast<int64_t*>(nullptr), static_cast<int64_t*>(nullptr),
+                                   static_cast<int>(n)) != hipSuccess)
+    return 0;
+  return 2 * align_up(static_cast<size_t>(n) * 8) + align_up(a > b ? a : b);
+}
+
+template <class Src>
+hgd_status unique_bitmap(Src src, int64_t n, int64_t* out, int64_t* n_out, void* ws, size_t wsb,
+                         hipStream_t st, const char* fn) {
+  HGD_REQUIRE(n >= 0 && n < (int64_t(1) << 31), "%s: n must be in [0, 2^31)", fn);
+  HGD_REQUIRE(n_out && (n == 0 || out), "%s: null output", fn);
+  if (wsb < kBitmapPathBytes || !ws)
+    return fail(HGD_ERR_WORKSPACE, "%s: workspace %zu < required %zu", fn, wsb, kBitmapPathBytes);
+  char* w = static_cast<char*>(ws);
+  State* s = reinterpret_cast<State*>(w + kOffState);
+  int* cnt = reinterpret_cast<int*>(w + kOffCnt);
+  int64_t* toff = reinterpret_cast<int64_t*>(w + kOffTileOff);
+  uint32_t* bitmap = reinterpret_cast<uint32_t*>(w + kOffBitmap);
+  hipLaunchKernelGGL(k_uq_init, dim3(1), dim3(1), 0, st, s);
+  if (n > 0) {
+    const unsigned g = static_cast<unsigned>(std::min<int64_t>(kGrid, (n + 255) / 256));
+    hipLaunchKernelGGL(k_uq_minmax<Src>, dim3(g), dim3(256), 0, st, src, n, s);
+  }
+  hipLaunchKernelGGL(k_uq_zero, dim3(kGrid), dim3(256), 0, st, bitmap, s);
+  if (n > 0) {
+    const unsigned g = static_cast<unsigned>(std::min<int64_t>(kGrid, (n + 255) / 256));
+    hipLaunchKernelGGL(k_uq_mark<Src>, dim3(g), dim3(256), 0, st, src, n, bitmap, s);
+  }
+  hipLaunchKernelGGL(k_uq_count, dim3(kMaxTiles), dim3(kEmitThreads), 0, st, bitmap, s, cnt);
+  hipLaunchKernelGGL(k_uq_scan, dim3(1), dim3(kMaxTiles), 0, st, cnt, s, toff, n_out);
+  hipLaunchKernelGGL(k_uq_emit, dim3(kMaxTiles), dim3(kEmitThreads), 0, st, bitmap, s, toff, out);
+  return check_launch(fn);
+}
+
+template <class Src>
+hgd_status unique_sort(Src src, const int64_t* keys_in, int64_t n, int64_t* out, int64_t* n_out,
+                       void* ws, size_t wsb, hipStream_t st, const char* fn) {
+  HGD_REQUIRE(n >= 0 && n < (int64_t(1) << 31), "%s: n must be in [0, 2^31)", fn);
+  HGD_REQUIRE(n_out && (n == 0 || out), "%s: null output", fn);
+  if (n == 0) {
+    HGD_HIP(hipMemsetAsync(n_out, 0, sizeof(int64_t), st));
+    return HGD_OK;
+  }
+  const size_t need = sort_path_bytes(n);
+  if (need == 0) return fail(HGD_ERR_HIP, "%s: hipcub workspace query failed", fn);
+  if (wsb < need || !ws)
+    return fail(HGD_ERR_WORKSPACE, "%s: workspace %zu < required %zu", fn, wsb, need);
+  char* w = static_cast<char*>(ws);
+  int64_t* keys = reinterpret_cast<int64_t*>(w);
+  int64_t* sorted = reinterpret_cast<int64_t*>(w + align_up(static_cast<size_t>(n) * 8));
+  char* tmp = w + 2 * align_up(static_cast<size_t>(n) * 8);
+  size_t tb = wsb - 2 * align_up(static_cast<size_t>(n) * 8);
+  if (!keys_in) {
+    hipLaunchKernelGGL(k_uq_materialize<Src>, dim3(grid_for(n)), dim3(kBlock), 0, st, src, n,
+                       keys);
+    hgd_status r = check_launch(fn);
+    if (r != HGD_OK) return r;
+    keys_in = keys;
+  }
+  HGD_HIP(hipcub::DeviceRadixSort::SortKeys(tmp, tb, keys_in, sorted, static_cast<int>(n), 0, 64,
+                                            st));
+  HGD_HIP(hipcub::DeviceSelect::Unique(tmp, tb, sorted, out, n_out, static_cast<int>(n), st));
+  return HGD_OK;
+}
+
+}  // namespace
+}  // namespace hgd
+
+using namespace hgd;
+
+extern "C" size_t hgd_unique_workspace_size(int64_t n) {
+  const size_t s = n > 0 ? sort_path_bytes(n) : 0;
+  return s > kBitmapPathBytes ? s : kBitmapPathBytes;
+}
+
+extern "C" hgd_status hgd_unique_i64(const int64_t* keys, int64_t n, int64_t* out,
+                                     int64_t* n_out, void* ws, size_t wsb, void* stream) {
+  clear_error();
+  HGD_REQUIRE(n == 0 || keys, "hgd_unique_i64: null keys");
+  return unique_bitmap(I64Src{keys}, n, out, n_out, ws, wsb, as_stream(stream), "hgd_unique_i64");
+}
+
+extern "C" hgd_status hgd_unique_trunc_f32(const float* x, int64_t n, int64_t* out,
+                                           int64_t* n_out, void* ws, size_t wsb, void* stream) {
+  clear_error();
+  HGD_REQUIRE(n == 0 || x, "hgd_unique_trunc_f32: null x");
+  return unique_bitmap(TruncSrc{x}, n, out, n_out, ws, wsb, as_stream(stream),
+                       "hgd_unique_trunc_f32");
+}
+
+extern "C" hgd_status hgd_unique_sort_i64(const int64_t* keys, int64_t n, int64_t* out,
+                                          int64_t* n_out, void* ws, size_t wsb, void* stream) {
+  clear_error();
+  HGD_REQUIRE(n == 0 || keys, "hgd_unique_sort_i64: null keys");
+  return unique_sort(I64Src{keys}, keys, n, out, n_out, ws, wsb, as_stream(stream),
+                     "hgd_unique_sort_i64");
+}
+
+extern "C" hgd_status hgd_unique_sort_trunc_f32(const float* x, int64_t n, int64_t* out,
+                                                int64_t* n_out, void* ws, size_t wsb,
+                                                void* stream) {
+  clear_error();
+  HGD_REQUIRE(n == 0 || x, "hgd_unique_sort_trunc_f32: null x");
+  return unique_sort(TruncSrc{x}, nullptr, n, out, n_out, ws, wsb, as_stream(stream),
+                     "hgd_unique_sort_trunc_f32");
+}

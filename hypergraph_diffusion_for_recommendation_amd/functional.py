@@ -186,6 +186,19 @@ class _FusedTwoHop(torch.autograd.Function):
         dev = dY.device
         want_g = ln and ctx.needs_input_grad[1]
         want_b = ln and ctx.needs_input_grad[2]
+        if not ln and epi == nat.EPI_NONE:
+            # a pure blend: dZ = out_scale·dY, folded into the item-side row scale of the first
+            # backward hop (n_cols multiplies instead of an [n, d] pass)
+            dX = None
+            if ctx.needs_input_grad[0]:
+                q = inc.scale("col", Q)
+                if out_scale != 1.0:
+                    q = (torch.full((inc.n_cols,), out_scale, dtype=torch.float32, device=dev)
+                         if q is None else q * out_scale)
+                dM = spmm_csr(inc.csc, dY, val=inc.edge_values("csc", P), row_scale=q)
+                dX = spmm_csr(inc.csr, dM, val=inc.val, row_scale=inc.scale("row", R))
+            return (dX, None, None, _res_grad(ctx, dY, 0, s1), _res_grad(ctx, dY, 1, s2), None,
+                    None)
         dgamma = torch.empty(d, dtype=torch.float32, device=dev) if want_g else None
         dbeta = torch.empty(d, dtype=torch.float32, device=dev) if want_b else None
         lib = nat.load()
@@ -202,13 +215,14 @@ class _FusedTwoHop(torch.autograd.Function):
             q = inc.scale("col", Q)
             dM = spmm_csr(inc.csc, dZ, val=inc.edge_values("csc", P), row_scale=q)
             dX = spmm_csr(inc.csr, dM, val=inc.val, row_scale=inc.scale("row", R))
+        return (dX, dgamma, dbeta, _res_grad(ctx, dY, 0, s1), _res_grad(ctx, dY, 1, s2), None,
+                None)
 
-        def res_grad(k, s):
-            if not ctx.has_res[k] or not ctx.needs_input_grad[3 + k]:
-                return None
-            return dY if s == 1.0 else dY * s
 
-        return dX, dgamma, dbeta, res_grad(0, s1), res_grad(1, s2), None, None
+def _res_grad(ctx, dY, k, s):
+    if not ctx.has_res[k] or not ctx.needs_input_grad[3 + k]:
+        return None
+    return dY if s == 1.0 else dY * s
 
 
 def two_hop_fused(inc: Incidence, X: torch.Tensor, P: Optional[str] = None,
@@ -486,6 +500,36 @@ def contrast_loss(embeds1: torch.Tensor, embeds2: torch.Tensor, nodes: torch.Ten
         raise IndexError(f"contrast_loss: node index out of range for a table of {n} rows")
     nodes = torch.where(nodes < 0, nodes + n, nodes)  # the gradient scatter needs [0, n)
     return _ContrastLoss.apply(embeds1, embeds2, nodes, float(temp))
+
+
+def unique_long(x: torch.Tensor) -> torch.Tensor:
+    """``torch.unique(x.long())`` (sorted, int64) of a device float32 or int64 tensor — the node
+    list HCCF's loss builds every step, ``torch.unique(ancs.long())`` (model/graph/HCCF.py:65-66).
+    Floats truncate toward zero like ``Tensor.long()``. Range-bitmap kernels (hgd_unique_*);
+    a key range beyond 2^24 takes the device radix-sort path. One device→host read (the count),
+    as torch.unique."""
+    if not x.is_cuda or x.dtype not in (torch.float32, torch.int64):
+        raise ValueError("unique_long: needs a float32 or int64 device tensor")
+    x = x.contiguous().view(-1)
+    n = x.numel()
+    lib = nat.load()
+    dev = x.device
+    out = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    cnt = torch.empty(1, dtype=torch.int64, device=dev)
+    wsb = lib.hgd_unique_workspace_size(n)
+    ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    f = x.dtype == torch.float32
+    fast = lib.hgd_unique_trunc_f32 if f else lib.hgd_unique_i64
+    nat.check(fast(x.data_ptr(), n, out.data_ptr(), cnt.data_ptr(), ws.data_ptr(), wsb, st),
+              "hgd_unique")
+    k = int(cnt.item())
+    if k < 0:  # key range beyond the bitmap
+        slow = lib.hgd_unique_sort_trunc_f32 if f else lib.hgd_unique_sort_i64
+        nat.check(slow(x.data_ptr(), n, out.data_ptr(), cnt.data_ptr(), ws.data_ptr(), wsb, st),
+                  "hgd_unique_sort")
+        k = int(cnt.item())
+    return out[:k]
 
 
 def _mm_ok(H: torch.Tensor, X: torch.Tensor) -> bool:

@@ -359,6 +359,26 @@ hgd_status hgd_topk_rows(const float* scores, int64_t n_rows, int64_t n_cols, in
                          int32_t k, int32_t* out_ids, float* out_scores, void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * Sorted unique of integer keys — torch.unique(t.long()) as HCCF's loss calls it every step on
+ * [batch, d] embedding blocks: contrastLoss(..., torch.unique(ancs.long()), ...),
+ * model/graph/HCCF.py:65-66 (the truncated embedding values become the node list).
+ *   hgd_unique_i64 / hgd_unique_trunc_f32: range-bitmap path, no host sync. out [n] receives the
+ *     distinct keys ascending (the trunc variant truncates floats toward zero like Tensor.long();
+ *     NaN / ±inf / |x| >= 2^63 become INT64_MIN), device *n_out their count — or -1 when the
+ *     key range exceeds 2^24, in which case the caller runs the matching hgd_unique_sort_* (device
+ *     radix sort + unique, same output). n < 2^31. Workspace: hgd_unique_workspace_size(n).
+ * ---------------------------------------------------------------------------------------- */
+size_t hgd_unique_workspace_size(int64_t n);
+hgd_status hgd_unique_i64(const int64_t* keys, int64_t n, int64_t* out, int64_t* n_out,
+                          void* workspace, size_t workspace_bytes, void* stream);
+hgd_status hgd_unique_trunc_f32(const float* x, int64_t n, int64_t* out, int64_t* n_out,
+                                void* workspace, size_t workspace_bytes, void* stream);
+hgd_status hgd_unique_sort_i64(const int64_t* keys, int64_t n, int64_t* out, int64_t* n_out,
+                               void* workspace, size_t workspace_bytes, void* stream);
+hgd_status hgd_unique_sort_trunc_f32(const float* x, int64_t n, int64_t* out, int64_t* n_out,
+                                     void* workspace, size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Elementwise epilogues around the hops (contiguous fp32, 16-byte aligned).
  *   apply:    y = epi(z)                                   (nn.LeakyReLU / nn.ReLU forward)
  *   backward: dz = dy * (ref > 0 ? 1 : slope) for LEAKY, dy * (ref > 0) for RELU, where ref is

@@ -1,0 +1,63 @@
+"""hgd_unique_* / functional.unique_long: torch.unique(x.long()) as HCCF's loss calls it every
+step (model/graph/HCCF.py:65-66) — bit-exact (sorted int64 keys) against torch.unique on the
+same tensor, over the range-bitmap path (LDS-private and global bitmaps) and the radix-sort path
+taken beyond a 2^24 key range."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(x):
+    return torch.unique(x.cpu().long())
+
+
+@pytest.mark.parametrize("shape,scale", [((4096, 64), 1.0), ((4096, 64), 3.0), ((1, 1), 1.0),
+                                         ((513, 7), 40.0), ((2048, 32), 5000.0)])
+def test_unique_of_truncated_embeddings(dev, shape, scale):
+    from hypergraph_diffusion_for_recommendation_amd import unique_long
+    g = torch.Generator(device=dev).manual_seed(int(scale * 10) + shape[0])
+    x = torch.randn(shape, device=dev, generator=g) * scale
+    got = unique_long(x)
+    assert got.dtype == torch.int64
+    assert torch.equal(got.cpu(), _ref(x))
+
+
+def test_unique_int64_paths(dev):
+    from hypergraph_diffusion_for_recommendation_amd import unique_long
+    rng = np.random.default_rng(0)
+    cases = {
+        "small_range": rng.integers(-5, 6, size=100_000),
+        "lds_boundary": rng.integers(0, 1024 * 32, size=50_000),       # exactly 1024 words
+        "global_bitmap": rng.integers(-10**6, 10**6, size=300_000),    # > 1024 words
+        "cap_minus_one": np.array([7, 7 + (1 << 24) - 1, 100, 7]),     # widest bitmap range
+        "cap": np.array([7, 7 + (1 << 24), 100]),                      # one past: sort path
+        "wide": rng.integers(-2**62, 2**62, size=200_000),             # sort path
+        "extremes": np.array([-2**63, 2**63 - 1, 0, -2**63, 5]),       # span overflows int64
+        "single": np.array([42]),
+        "dups": np.full(1000, -3),
+    }
+    for name, a in cases.items():
+        t = torch.from_numpy(a.astype(np.int64)).to(dev)
+        got = unique_long(t)
+        assert torch.equal(got.cpu(), torch.unique(t.cpu())), name
+
+
+def test_unique_empty_and_special_floats(dev):
+    from hypergraph_diffusion_for_recommendation_amd import unique_long
+    assert unique_long(torch.empty(0, device=dev)).numel() == 0
+    assert unique_long(torch.empty(0, dtype=torch.int64, device=dev)).numel() == 0
+    x = torch.tensor([1.9, -1.9, -0.5, 0.5, 2.0, -2.0, 3e9, -3e9], device=dev)
+    assert unique_long(x).cpu().tolist() == sorted({1, -1, 0, 2, -2, 3000000000, -3000000000})
+    # NaN / inf / out of int64 range → INT64_MIN (documented; C++ leaves the cast undefined)
+    y = torch.tensor([float("nan"), float("inf"), -float("inf"), 1e30, 4.0], device=dev)
+    assert unique_long(y).cpu().tolist() == [-2**63, 4]
+
+
+def test_unique_rejects_other_dtypes(dev):
+    from hypergraph_diffusion_for_recommendation_amd import unique_long
+    with pytest.raises(ValueError):
+        unique_long(torch.zeros(4, dtype=torch.int32, device=dev))
+    with pytest.raises(ValueError):
+        unique_long(torch.zeros(4))
