@@ -496,7 +496,12 @@ def contrast_loss(embeds1: torch.Tensor, embeds2: torch.Tensor, nodes: torch.Ten
     n = embeds1.shape[0]
     # torch indexing semantics (negative ids wrap; HCCF passes torch.unique(emb.long()), which
     # holds -1 / 0 / 1); out of range raises like embeds[nodes] would
-    if bool(((nodes < -n) | (nodes >= n)).any()):
+    rng = getattr(nodes, "_hgd_range", None)  # set by unique_long: no device read needed
+    if rng is not None and rng[2] != nodes._version:
+        rng = None  # modified in place since
+    bad = (rng[0] < -n or rng[1] >= n) if rng is not None else bool(
+        ((nodes < -n) | (nodes >= n)).any())
+    if bad:
         raise IndexError(f"contrast_loss: node index out of range for a table of {n} rows")
     nodes = torch.where(nodes < 0, nodes + n, nodes)  # the gradient scatter needs [0, n)
     return _ContrastLoss.apply(embeds1, embeds2, nodes, float(temp))
@@ -506,30 +511,41 @@ def unique_long(x: torch.Tensor) -> torch.Tensor:
     """``torch.unique(x.long())`` (sorted, int64) of a device float32 or int64 tensor — the node
     list HCCF's loss builds every step, ``torch.unique(ancs.long())`` (model/graph/HCCF.py:65-66).
     Floats truncate toward zero like ``Tensor.long()``. Range-bitmap kernels (hgd_unique_*);
-    a key range beyond 2^24 takes the device radix-sort path. One device→host read (the count),
-    as torch.unique."""
+    a key range beyond 2^24 takes the device radix-sort path. One device→host read, as
+    torch.unique: the count together with the key range, which is attached to the result
+    (``_hgd_range``) so that :func:`contrast_loss` checks its bounds without another read."""
     if not x.is_cuda or x.dtype not in (torch.float32, torch.int64):
         raise ValueError("unique_long: needs a float32 or int64 device tensor")
-    x = x.contiguous().view(-1)
+    x = x.detach().contiguous().view(-1)
     n = x.numel()
     lib = nat.load()
     dev = x.device
     out = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
-    cnt = torch.empty(1, dtype=torch.int64, device=dev)
     wsb = lib.hgd_unique_workspace_size(n)
-    ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+    # [count | pad | workspace]: the workspace starts with the kernels' (min, max) state, so one
+    # 272-byte copy returns the count and the range
+    buf = torch.empty(_UQ_HEAD + max(wsb, 1), dtype=torch.uint8, device=dev)
     st = torch.cuda.current_stream(dev).cuda_stream
     f = x.dtype == torch.float32
     fast = lib.hgd_unique_trunc_f32 if f else lib.hgd_unique_i64
-    nat.check(fast(x.data_ptr(), n, out.data_ptr(), cnt.data_ptr(), ws.data_ptr(), wsb, st),
+    base = buf.data_ptr()
+    nat.check(fast(x.data_ptr(), n, out.data_ptr(), base, base + _UQ_HEAD, wsb, st),
               "hgd_unique")
-    k = int(cnt.item())
+    head = buf[:_UQ_HEAD + 16].cpu().view(torch.int64)
+    k = int(head[0])
     if k < 0:  # key range beyond the bitmap
         slow = lib.hgd_unique_sort_trunc_f32 if f else lib.hgd_unique_sort_i64
-        nat.check(slow(x.data_ptr(), n, out.data_ptr(), cnt.data_ptr(), ws.data_ptr(), wsb, st),
+        nat.check(slow(x.data_ptr(), n, out.data_ptr(), base, base + _UQ_HEAD, wsb, st),
                   "hgd_unique_sort")
-        k = int(cnt.item())
-    return out[:k]
+        k = int(buf[:8].cpu().view(torch.int64)[0])
+        return out[:k]
+    res = out[:k]
+    if k:
+        res._hgd_range = (int(head[_UQ_HEAD // 8]), int(head[_UQ_HEAD // 8 + 1]), res._version)
+    return res
+
+
+_UQ_HEAD = 256  # bytes before the unique workspace (count at 0; 256-byte aligned workspace)
 
 
 def _mm_ok(H: torch.Tensor, X: torch.Tensor) -> bool:

@@ -61,3 +61,21 @@ def test_unique_rejects_other_dtypes(dev):
         unique_long(torch.zeros(4, dtype=torch.int32, device=dev))
     with pytest.raises(ValueError):
         unique_long(torch.zeros(4))
+
+
+def test_unique_range_feeds_contrast_loss_bounds(dev):
+    """unique_long attaches the key range; contrast_loss uses it for its IndexError check (and
+    falls back to reading the nodes when they were modified in place)."""
+    from hypergraph_diffusion_for_recommendation_amd import contrast_loss, unique_long
+    E = torch.randn(10, 16, device=dev)
+    nodes = unique_long(torch.tensor([-3.5, 2.2, 9.9, 0.1], device=dev))
+    assert nodes._hgd_range[:2] == (-3, 9)
+    loss = contrast_loss(E, E.clone(), nodes, 0.2)
+    assert torch.isfinite(loss)
+    bad = unique_long(torch.tensor([1.0, 10.0], device=dev))
+    with pytest.raises(IndexError):
+        contrast_loss(E, E.clone(), bad, 0.2)
+    ok = unique_long(torch.tensor([1.0, 2.0], device=dev))
+    ok[1] = 12  # in-place change: the cached range is ignored, the check reads the values
+    with pytest.raises(IndexError):
+        contrast_loss(E, E.clone(), ok, 0.2)
