@@ -110,7 +110,7 @@ def cpu_baseline(U, I, E, zipf, sample_edges, budget_s, d):
         ref_cpu.hgconv2_fwd_bwd(H, X, dY)
         times.append(time.perf_counter() - t0)
     t = statistics.median(times)
-    return {
+    out = {
         "value": round(len(rows) / t / 1e6, 3),
         "unit": "M-edges/s",
         "cores": torch.get_num_threads(),
@@ -119,6 +119,30 @@ def cpu_baseline(U, I, E, zipf, sample_edges, budget_s, d):
                    f"d={d}, torch.sparse.mm fwd+bwd (oracle/ref_cpu.py), median of "
                    f"{len(times)} runs, {t:.3f} s/run"),
     }
+    # also a 1-thread figure, on a 10x smaller sample of the same generator
+    f1 = f / 10
+    u1, i1, e1 = max(1, int(U * f1)), max(1, int(I * f1)), max(1, int(E * f1))
+    r1, c1 = O.synthetic_incidence(u1, i1, e1, seed=0, zipf=zipf)
+    H1 = ref_cpu.coo_tensor(r1, c1, None, (u1, i1))
+    X1 = torch.empty(u1, d)
+    torch.nn.init.xavier_uniform_(X1, generator=g)
+    dY1 = torch.randn(u1, d, generator=g)
+    threads = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        ref_cpu.hgconv2_fwd_bwd(H1, X1, dY1)  # warm-up
+        t1s = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            ref_cpu.hgconv2_fwd_bwd(H1, X1, dY1)
+            t1s.append(time.perf_counter() - t0)
+    finally:
+        torch.set_num_threads(threads)
+    t1 = statistics.median(t1s)
+    out["single_thread"] = {"value": round(len(r1) / t1 / 1e6, 3), "cores": 1,
+                            "sample": f"{u1}x{i1} graph, {len(r1)} edges, median of 3, "
+                                      f"{t1:.3f} s/run"}
+    return out
 
 
 def pmc_traffic(args, U, I, E):
