@@ -9,12 +9,12 @@ outputs (fp32, 1e-5 relative) with every sparse hop on libhgd's gfx950 kernels:
 class                  reference                                        hot op here
 =====================  ==============================================  =========================
 GCNLayer               model/graph/HCCF.py:193-199                      hgd_spmm (CSR, + CSC bwd)
-HGNNLayer              model/graph/HCCF.py:201-211                      dense GEMMs (rocBLAS)
+HGNNLayer              model/graph/HCCF.py:201-211                      hgd_linear_* (f32 MFMA)
 HGCNConv               model/graph/HGNN_HD4.py:450-462 (and copies)     2 hops, fused LeakyReLU
 SpAdjDropEdge          model/graph/HCCF.py:213-226                      hgd_dropedge_compact
 EquivSetConv           model/layers/layers2/EquivSetConv2.py:38-100     mean/sum 2-hop (V/E)
 EquivSetGNN            model/layers/layers2/EquivSetGNN2.py:32-155      hgd_dense_threshold_*
-MLP                    model/layers/MLP.py:29-117                       nn.Linear / nn.LayerNorm
+MLP                    model/layers/MLP.py:29-117                       hgd_linear_* / row epi
 =====================  ==============================================  =========================
 
 Sparse adjacencies are accepted exactly as the reference passes them — torch sparse COO tensors
