@@ -89,3 +89,345 @@ class _ShardedHGConv(torch.autograd.Function):
 def sharded_two_hop(sh: ShardedIncidence, X_local: torch.Tensor) -> torch.Tensor:
     """P·H·Q·Hᵀ·R·X on user-row shards (X_local = this rank's user rows)."""
     return _ShardedHGConv.apply(X_local, sh)
+
+
+# ---------------------------------------------------------------------------------------------
+# The model-side operators on user-row shards (SURVEY.md §8e "HCCF specifics"): the bipartite
+# node graph of HCCF / HGCNConv / ED-HNN and HCCF's learned dense hypergraph.
+#
+# Convention for replicated tensors (item rows, the [K, d] hyperedge messages): every rank holds
+# the same VALUE, and the gradient a rank computes for it is that rank's PARTIAL gradient (its own
+# loss terms); the true gradient is the sum over ranks. So an all-reduce in the forward has an
+# all-reduce as its backward, a replicated tensor consumed by a local op needs no exchange, and
+# replicated parameters (item embeddings, W) get their partial gradients summed once before the
+# optimizer step (:func:`allreduce_replicated_grads`, what DDP does for every parameter).
+# ---------------------------------------------------------------------------------------------
+
+from . import _native as nat  # noqa: E402
+from .functional import _epilogue_apply, _epilogue_backward, _nn, _nt, _tn  # noqa: E402,F401
+
+
+class _AllReduceSum(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, group):
+        ctx.group = group
+        y = x.contiguous().clone()
+        dist.all_reduce(y, group=group)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous().clone()
+        dist.all_reduce(g, group=ctx.group)
+        return g, None
+
+
+def all_reduce_sum(x: torch.Tensor, group=None) -> torch.Tensor:
+    """Σ over ranks of per-rank partials, differentiable (backward = the same sum)."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return x
+    return _AllReduceSum.apply(x, group)
+
+
+def allreduce_replicated_grads(params, group=None) -> None:
+    """Sums the partial gradients of replicated parameters over ranks (call before step())."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return
+    for p in params:
+        if p.grad is not None:
+            dist.all_reduce(p.grad, group=group)
+
+
+def block_coo(indices: torch.Tensor, values: Optional[torch.Tensor], n_users: int, u0: int,
+              u1: int):
+    """The two blocks of a bipartite [N, N] COO (users first) that user rows [u0, u1) own:
+    ``B = A[u0:u1, U:]`` (local users → items) and ``C = A[U:, u0:u1]`` (items → local users),
+    re-indexed locally, in the input's order (row-major stays row-major), with the positions of
+    their entries in the input (to slice a global drop-edge mask the same way)."""
+    r, c = indices[0], indices[1]
+    sel_b = ((r >= u0) & (r < u1) & (c >= n_users)).nonzero().flatten()
+    sel_c = ((r >= n_users) & (c >= u0) & (c < u1)).nonzero().flatten()
+    b_idx = torch.stack([r[sel_b] - u0, c[sel_b] - n_users])
+    c_idx = torch.stack([r[sel_c] - n_users, c[sel_c] - u0])
+    b_val = None if values is None else values[sel_b]
+    c_val = None if values is None else values[sel_c]
+    return b_idx, b_val, c_idx, c_val, sel_b, sel_c
+
+
+def _transposed(inc):
+    """Aᵀ of an Incidence as an Incidence sharing its arrays (CSR and CSC swap roles)."""
+    t = Incidence(inc.csc, inc.csr, inc.val_t, inc.val)
+    if inc.perm_t is not None:
+        inv = torch.empty_like(inc.perm_t)
+        inv[inc.perm_t.long()] = torch.arange(inc.nnz, dtype=inv.dtype, device=inv.device)
+        t.perm_t = inv
+    t.coo_sorted = True
+    return t
+
+
+def _fold(base: Optional[torch.Tensor], scale: torch.Tensor, col: torch.Tensor, nnz: int):
+    """w[e] = base[e] · scale[col[e]] (hgd_edge_values): a source-side diagonal folded into the
+    per-nonzero weights of a hop."""
+    out = torch.empty(nnz, dtype=torch.float32, device=scale.device)
+    if nnz:
+        nat.check(nat.load().hgd_edge_values(
+            nat.ptr(base), None, scale.data_ptr(), col.data_ptr(), nnz, out.data_ptr(),
+            torch.cuda.current_stream(scale.device).cuda_stream), "hgd_edge_values")
+    return out
+
+
+class ShardedBipartite:
+    """One rank's share of a bipartite node operator ``A [N, N] = [[0, B], [C, 0]]`` (users
+    first: ``Interaction.__create_sparse_bipartite_adjacency`` / ``normalize_graph_mat``,
+    data/ui_graph.py:70-84, data/graph.py:11-25) under user-row sharding.
+
+    The rank owns users [u0, u1) and holds ``B_g = A[u0:u1, U:]`` and ``C_g = A[U:, u0:u1]`` as
+    incidences; for a symmetric A (norm_adj, ui_adj) ``C_g = B_gᵀ`` is B_g's own CSC. A hop
+    ``Y = S·A·X`` on the local layout ``[X_u[u0:u1]; X_i]`` is
+
+        Y_i = Σ_g S_i·C_g·X_u,g    CSR hop of C_g into the item rows, chunked, RCCL all-reduce
+        Y_u = S_u·B_g·X_i          local CSR hop, issued while the item chunks are in flight
+
+    and its backward (partial dY_i per rank) is dY_i ← Σ_g dY_i (all-reduce, overlapped with
+    dX_i = B_gᵀ·S_u·dY_u, a partial), then dX_u = C_gᵀ·S_i·dY_i. S is an optional row scale of
+    the GLOBAL degrees ('mean' 1/deg, the ED-HNN means; 'sym' deg^-1/2); item degrees are
+    all-reduced once per kind."""
+
+    def __init__(self, B, C=None, group=None, n_chunks: int = 4):
+        self.B = B
+        self.C = C if C is not None else _transposed(B)
+        self.symmetric = C is None
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.n_local = B.n_rows
+        self.n_items = B.n_cols
+        if self.C.n_rows != self.n_items or self.C.n_cols != self.n_local:
+            raise ValueError("ShardedBipartite: C must be [items, local users]")
+        self.n_chunks = max(1, int(n_chunks)) if self.world > 1 else 1
+        step = -(-self.n_items // self.n_chunks) if self.n_items else 0
+        self.bounds = [(k * step, min((k + 1) * step, self.n_items))
+                       for k in range(self.n_chunks) if k * step < self.n_items] or [(0, 0)]
+        self.sel_b = self.sel_c = None
+        self._scales = {}
+        self._folded = {}
+
+    @classmethod
+    def from_global(cls, adj, n_users: int, n_items: int, u0: int, u1: int, device=None,
+                    group=None, n_chunks: int = 4, symmetric: Optional[bool] = None):
+        """Slices a global bipartite adjacency — a torch sparse COO as
+        ``convert_sparse_mat_to_tensor`` builds it (base/torch_interface.py:8-12), or
+        (indices, values) — into this rank's blocks. ``symmetric=None`` checks C_g == B_gᵀ on
+        the device and then keeps only B_g."""
+        if isinstance(adj, torch.Tensor):
+            idx, val = adj._indices(), adj._values()
+            if tuple(adj.shape) != (n_users + n_items, n_users + n_items):
+                raise ValueError("ShardedBipartite: adjacency must be [U+I, U+I]")
+        else:
+            idx, val = adj
+        device = torch.device(device) if device is not None else torch.device("cuda")
+        idx = idx.to(device)
+        val = None if val is None else val.to(device=device, dtype=torch.float32)
+        b_idx, b_val, c_idx, c_val, sel_b, sel_c = block_coo(idx, val, n_users, u0, u1)
+        n_loc = u1 - u0
+        B = Incidence.from_coo(b_idx, b_val, (n_loc, n_items), device=device)
+        C = None
+        if symmetric is not True:
+            C = Incidence.from_coo(c_idx, c_val, (n_items, n_loc), device=device)
+            if symmetric is None and _same_transpose(B, C):
+                C = None
+        sh = cls(B, C, group=group, n_chunks=n_chunks)
+        sh.sel_b, sh.sel_c = sel_b, sel_c
+        return sh
+
+    # -- scales ------------------------------------------------------------------------------
+    def scale(self, side: str, kind: Optional[str]) -> Optional[torch.Tensor]:
+        """Global-degree row scale of the user ('user') or item ('item') rows of A."""
+        if kind is None:
+            return None
+        key = (side, kind)
+        if key in self._scales:
+            return self._scales[key]
+        if kind not in ("mean", "sym"):
+            raise ValueError(f"ShardedBipartite: unsupported scale {kind!r}")
+        o = self.B.csr if side == "user" else self.C.csr
+        deg = (o.rowptr[1:] - o.rowptr[:-1]).to(torch.float64)
+        if side == "item" and self.world > 1:
+            dist.all_reduce(deg, group=self.group)
+        p = -1.0 if kind == "mean" else -0.5
+        s = torch.where(deg > 0, deg.pow(p), torch.zeros_like(deg)).to(torch.float32)
+        self._scales[key] = s
+        return s
+
+    def _src_folded(self, which: str, kind: Optional[str]):
+        """Backward-hop weights with the forward's output scale folded in as a source scale:
+        'c_t' = C_gᵀ·S_i (into users), 'b_t' = B_gᵀ·S_u (into items)."""
+        inc = self.C if which == "c_t" else self.B
+        if kind is None:
+            return inc.val_t
+        key = (which, kind)
+        if key not in self._folded:
+            s = self.scale("item" if which == "c_t" else "user", kind)
+            self._folded[key] = _fold(inc.val_t, s, inc.csc.col, inc.nnz)
+        return self._folded[key]
+
+    # -- drop-edge (SpAdjDropEdge, HCCF.py:213-226) ------------------------------------------
+    def drop(self, keep: float, mask_b: torch.Tensor, mask_c: torch.Tensor) -> "ShardedBipartite":
+        """The shard of the edge-dropped adjacency: ``mask_b`` / ``mask_c`` select B_g's and C_g's
+        nonzeros in CSR order (for parity with the reference's global ``torch.rand(nnz)`` mask,
+        :meth:`drop_global`). The result is never symmetric (the blocks drop independently)."""
+        B = self.B.drop(mask_b, keep)
+        C = self.C.drop(mask_c, keep)
+        return ShardedBipartite(B, C, group=self.group, n_chunks=self.n_chunks)
+
+    def drop_global(self, keep: float, mask: torch.Tensor) -> "ShardedBipartite":
+        """:meth:`drop` with the reference's mask over the GLOBAL COO (same draw on every rank)."""
+        if self.sel_b is None:
+            raise RuntimeError("drop_global needs a shard built by from_global")
+        mask = mask.to(self.sel_b.device)
+        return self.drop(keep, mask[self.sel_b], mask[self.sel_c])
+
+    def drop_device(self, keep: float, seed: int) -> "ShardedBipartite":
+        """:meth:`drop` with device keep-masks (hgd_bernoulli_mask): every global nonzero lies in
+        exactly one rank's B_g or C_g, so per-rank draws are one independent Bernoulli per
+        entry, as the reference's. ``seed`` should differ per rank."""
+        lib = nat.load()
+        masks = []
+        for k, inc in enumerate((self.B, self.C)):
+            m = torch.empty(inc.nnz, dtype=torch.uint8, device=inc.device)
+            if inc.nnz:
+                nat.check(lib.hgd_bernoulli_mask(
+                    (int(seed) * 2 + k) & ((1 << 62) - 1), inc.nnz, float(keep), m.data_ptr(),
+                    torch.cuda.current_stream(inc.device).cuda_stream), "hgd_bernoulli_mask")
+            masks.append(m)
+        return self.drop(keep, masks[0], masks[1])
+
+
+def _same_transpose(B, C) -> bool:
+    """C == Bᵀ exactly (structure and values): C's CSR against B's CSC."""
+    if B.nnz != C.nnz:
+        return False
+    if not torch.equal(B.csc.rowptr, C.csr.rowptr) or not torch.equal(B.csc.col, C.csr.col):
+        return False
+    if (B.val is None) != (C.val is None):
+        return False
+    return B.val is None or torch.equal(B.val_t, C.val)
+
+
+class _BipartiteHop(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, X, sh: ShardedBipartite, kind):
+        ctx.sh, ctx.kind = sh, kind
+        n = sh.n_local
+        X = X.contiguous()
+        Y = torch.empty_like(X)
+        Yi = Y[n:]
+        works: List = []
+        for a, b in sh.bounds:
+            if b > a:
+                spmm_csr(sh.C.csr, X[:n], val=sh.C.val, row_scale=sh.scale("item", kind),
+                         out=Yi, row_begin=a, row_end=b)
+            if sh.world > 1:
+                works.append(dist.all_reduce(Yi[a:b], group=sh.group, async_op=True))
+        spmm_csr(sh.B.csr, X[n:], val=sh.B.val, row_scale=sh.scale("user", kind), out=Y[:n])
+        for w in works:
+            w.wait()
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        sh, kind = ctx.sh, ctx.kind
+        n = sh.n_local
+        dY = dY.contiguous()
+        w_b, w_c = sh._src_folded("b_t", kind), sh._src_folded("c_t", kind)  # before the async
+        dYi = dY[n:].clone()
+        work = dist.all_reduce(dYi, group=sh.group, async_op=True) if sh.world > 1 else None
+        dX = torch.empty_like(dY)
+        # partial dX_i = B_gᵀ·S_u·dY_u while the item gradient is summed
+        spmm_csr(sh.B.csc, dY[:n], val=w_b, out=dX[n:])
+        if work is not None:
+            work.wait()
+        spmm_csr(sh.C.csc, dYi, val=w_c, out=dX[:n])
+        return dX, None, None
+
+
+def bipartite_hop(sh: ShardedBipartite, X_local: torch.Tensor,
+                  scale: Optional[str] = None) -> torch.Tensor:
+    """``S·A·X`` on this rank's layout ``[X_u[u0:u1]; X_i]`` (see :class:`ShardedBipartite`)."""
+    if X_local.shape[0] != sh.n_local + sh.n_items:
+        raise ValueError(f"bipartite_hop: X has {X_local.shape[0]} rows, shard expects "
+                         f"{sh.n_local} users + {sh.n_items} items")
+    return _BipartiteHop.apply(X_local, sh, scale)
+
+
+class _Epilogue(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, Z, epi: int, slope: float):
+        Y = _epilogue_apply(Z.contiguous(), epi, slope)
+        ctx.save_for_backward(Y)
+        ctx.epi, ctx.slope = epi, slope
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        (Y,) = ctx.saved_tensors
+        return _epilogue_backward(Y, dY, ctx.epi, ctx.slope), None, None
+
+
+def sharded_gcn_hop(sh: ShardedBipartite, X_local: torch.Tensor) -> torch.Tensor:
+    """GCNLayer (``torch.sparse.mm(adj, embeds)``, HCCF.py:193-199) on user-row shards."""
+    return bipartite_hop(sh, X_local)
+
+
+def sharded_hgcn_conv(sh: ShardedBipartite, X_local: torch.Tensor, act: bool = True,
+                      slope: float = 0.5) -> torch.Tensor:
+    """HGCNConv (``leaky(A·(Aᵀ·X))``, HGNN_HD4.py:450-462) on user-row shards of a symmetric A
+    (norm_adj: Aᵀ = A as a matrix, whichever order its blocks are stored in): two hops, the
+    LeakyReLU after the second exchange (it is not linear)."""
+    Z = bipartite_hop(sh, bipartite_hop(sh, X_local))
+    if not act:
+        return Z
+    return _Epilogue.apply(Z, nat.EPI_LEAKY_RELU, float(slope))
+
+
+def sharded_mean_two_hop(sh: ShardedBipartite, X_local: torch.Tensor) -> torch.Tensor:
+    """The ED-HNN scatter-mean pair over V/E = nonzero(ui_adj) (EquivSetConv2.py:88-93:
+    Xe = mean of X over each hyperedge's vertices, then Xv = mean of Xe over each vertex's
+    hyperedges) on user-row shards. ui_adj is symmetric, so both means are D^-1·A with the
+    global degrees."""
+    return bipartite_hop(sh, bipartite_hop(sh, X_local, "mean"), "mean")
+
+
+class _ShardedDenseTwoHop(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, H, X, group):
+        H = H.contiguous()
+        X = X.contiguous()
+        M = _tn(H, X)                      # this rank's Hᵀ·X [K, d]
+        dist.all_reduce(M, group=group)    # K·d·4 bytes: 8 KB at K = 32, d = 64
+        ctx.save_for_backward(H, X, M)
+        ctx.group = group
+        return _nn(H, M)
+
+    @staticmethod
+    def backward(ctx, dY):
+        H, X, M = ctx.saved_tensors
+        dY = dY.contiguous()
+        dM = _tn(H, dY)
+        dist.all_reduce(dM, group=ctx.group)
+        dH = dX = None
+        if ctx.needs_input_grad[1]:
+            dX = _nn(H, dM)
+        if ctx.needs_input_grad[0]:
+            dH = _nt(dY, M)
+            dH += _nt(X, dM)
+        return dH, dX, None
+
+
+def sharded_dense_two_hop(H_local: torch.Tensor, X_local: torch.Tensor,
+                          group=None) -> torch.Tensor:
+    """HGNNLayer's ``H·(Hᵀ·X)`` (HCCF.py:201-211) over user rows split across ranks: the [K, d]
+    hyperedge messages Hᵀ·X are all-reduced (forward and backward), the rest is local."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        from .functional import dense_two_hop
+        return dense_two_hop(H_local, X_local)
+    return _ShardedDenseTwoHop.apply(H_local, X_local, group)

@@ -1,0 +1,222 @@
+"""The hot-path carriers on user-row shards (BASELINE configs[3]: hypergraph
+diffusion, user-row sharded on the GPUs of one node). Paths relative to
+/root/reference/HD_SELFRec.
+
+Rank g owns users [u0, u1): their embedding rows, their rows of the bipartite graphs (and the
+item rows' entries in their columns, :class:`~.sharded.ShardedBipartite`) and their rows of the
+learned user hypergraph. Items, the item hypergraph and every weight matrix are replicated.
+The local node layout is ``[users u0..u1-1; all items]`` — the reference's ``[users; items]``
+restricted to this rank's users. Exchanges (RCCL over xGMI with backend "nccl"):
+
+* every bipartite hop: one all-reduce of the item rows forward, one backward (chunked, overlapped
+  with the local user hop / the item partial);
+* HCCF's learned user hypergraph: one [K, d] all-reduce forward and one backward.
+
+Replicated tensors follow :mod:`.sharded`'s convention (same value on every rank, per-rank
+partial gradients): call :func:`~.sharded.allreduce_replicated_grads` on the replicated
+parameters (:meth:`replicated_parameters`) before the optimizer step. Dropout on replicated rows
+draws from a generator seeded identically on every rank (``seed``), so the replicas stay equal.
+"""
+from __future__ import annotations
+
+from typing import Iterator, Optional
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .encoders import edhnn_config
+from .functional import dense_two_hop, layer_norm, linear
+from .layers import EquivSetGNN, LayerNorm
+from .sharded import (ShardedBipartite, bipartite_hop, sharded_dense_two_hop,
+                      sharded_hgcn_conv, sharded_mean_two_hop)
+
+
+def shard_bounds(n_users: int, world: int, rank: int):
+    """Contiguous user range of ``rank`` (sizes differ by at most one)."""
+    cuts = np.linspace(0, n_users, world + 1).astype(np.int64)
+    return int(cuts[rank]), int(cuts[rank + 1])
+
+
+def _coo_tensor(mat, binary: bool = False):
+    """(indices int64 [2, nnz], values fp32 or None) of a scipy matrix. Weighted: ``tocoo()``
+    order, exactly as ``convert_sparse_mat_to_tensor`` (base/torch_interface.py:8-12) — the
+    order the reference's drop-edge mask indexes. Binary: the V/E order of
+    ``nonzero(ui_adj > 0)`` (sorted rows, ascending columns, zeros dropped; HGNN_HD4.py:367-369)."""
+    if binary:
+        csr = mat.tocsr().copy()
+        csr.sort_indices()
+        csr.eliminate_zeros()
+        coo = csr.tocoo()
+    else:
+        coo = mat.tocoo()
+    idx = torch.from_numpy(np.stack([coo.row, coo.col]).astype(np.int64))
+    val = None if binary else torch.from_numpy(coo.data.astype(np.float32))
+    return idx, val
+
+
+class _SplitDropout(nn.Module):
+    """nn.Dropout over the local layout: local rows draw from the default generator, replicated
+    rows (``start`` onward) from ``gen`` (identical on every rank)."""
+
+    def __init__(self, p: float, gen: torch.Generator):
+        super().__init__()
+        self.p, self.gen = float(p), gen
+
+    def forward(self, x: torch.Tensor, start: int) -> torch.Tensor:
+        if not self.training or self.p == 0.0:
+            return x
+        if self.p == 1.0:
+            return torch.zeros_like(x)
+        loc = F.dropout(x[:start], self.p, True)
+        keep = torch.empty_like(x[start:]).bernoulli_(1.0 - self.p, generator=self.gen)
+        return torch.cat([loc, x[start:] * keep / (1.0 - self.p)])
+
+
+class ShardedHCCFEncoder(nn.Module):
+    """HCCFEncoder (HCCF.py:136-191) on user-row shards, same parameter names: ``user_emb``
+    holds this rank's rows. Per layer: the edge-dropped GCN hop (:func:`bipartite_hop` on the
+    dropped shard), the user hypergraph hop over the split users (:func:`sharded_dense_two_hop`)
+    and the replicated item hypergraph hop (:func:`dense_two_hop`).
+
+    ``device_rng=False`` draws the reference's global CPU ``torch.rand(nnz)`` mask per layer (the
+    same bits as the single-GPU encoder for a seed; every rank draws it); ``True`` draws each
+    rank's blocks on the device (independent Bernoulli per nonzero, as the reference's)."""
+
+    def __init__(self, conf, data, u0: int, u1: int, group=None, device=None, n_chunks: int = 4,
+                 device_rng: bool = True, seed: int = 0):
+        super().__init__()
+        from .encoders import HCCFEncoder
+        HCCFEncoder._parse_config(self, conf)
+        self.data = data
+        self.u0, self.u1, self.n_local = int(u0), int(u1), int(u1) - int(u0)
+        self.device = torch.device(device) if device is not None else torch.device("cuda")
+        self.group = group
+        self.device_rng = device_rng
+        U, I = data.n_users, data.n_items
+        self.adj = ShardedBipartite.from_global(_coo_tensor(data.norm_adj), U, I, u0, u1,
+                                                device=self.device, group=group,
+                                                n_chunks=n_chunks)
+        self.nnz_global = int(data.norm_adj.nnz)
+        d, K = self.latent_size, self.n_edges
+        bu = (6.0 / (U + d)) ** 0.5  # xavier_uniform_ bound of the GLOBAL [U, d] table
+        self.embedding_dict = nn.ParameterDict({
+            'user_emb': nn.Parameter(torch.empty(self.n_local, d, device=self.device)
+                                     .uniform_(-bu, bu)),
+            'item_emb': nn.Parameter(nn.init.xavier_uniform_(torch.empty(I, d)).to(self.device)),
+            'user_w': nn.Parameter(nn.init.xavier_uniform_(torch.empty(d, K)).to(self.device)),
+            'item_w': nn.Parameter(nn.init.xavier_uniform_(torch.empty(d, K)).to(self.device)),
+        })
+        self.rep_gen = torch.Generator(device=self.device).manual_seed(int(seed))
+        self.drop_out = nn.Dropout(self.drop_rate)
+        self.rep_drop = _SplitDropout(self.drop_rate, self.rep_gen)
+
+    @torch.no_grad()
+    def load_global(self, embedding_dict) -> None:
+        """Takes this rank's slice of a single-GPU HCCFEncoder's parameters."""
+        e = self.embedding_dict
+        e['user_emb'].copy_(embedding_dict['user_emb'][self.u0:self.u1])
+        for k in ('item_emb', 'user_w', 'item_w'):
+            e[k].copy_(embedding_dict[k])
+
+    def replicated_parameters(self) -> Iterator[nn.Parameter]:
+        e = self.embedding_dict
+        return iter([e['item_emb'], e['user_w'], e['item_w']])
+
+    def _dropped(self, keep_rate: float) -> ShardedBipartite:
+        if keep_rate == 1.0:
+            return self.adj
+        if self.device_rng:
+            seed = int(torch.randint(0, 2 ** 40, (1,)).item())  # same draw on every rank
+            rank = torch.distributed.get_rank(self.group) if self.adj.world > 1 else 0
+            return self.adj.drop_device(keep_rate, seed * 4096 + rank)
+        mask = ((torch.rand(self.nnz_global) + keep_rate).floor()).type(torch.bool)
+        return self.adj.drop_global(keep_rate, mask)
+
+    def forward(self, keep_rate=0.5):
+        nl = self.n_local
+        e = self.embedding_dict
+        embeddings = torch.cat([e['user_emb'], e['item_emb']], 0)
+        hidden = [embeddings]
+        gcn_hidden, hgnn_hidden = [], []
+        hyper_uu = linear(e['user_emb'], e['user_w'].t())
+        hyper_ii = linear(e['item_emb'], e['item_w'].t())
+        for _ in range(self.n_layers):
+            gcn_emb = bipartite_hop(self._dropped(keep_rate), hidden[-1])
+            hyper_u = sharded_dense_two_hop(self.drop_out(hyper_uu), hidden[-1][:nl], self.group)
+            hyper_i = dense_two_hop(self.rep_drop(hyper_ii, 0), hidden[-1][nl:])
+            gcn_hidden += [gcn_emb]
+            hgnn_hidden += [torch.cat([hyper_u, hyper_i], 0)]
+            hidden += [gcn_emb + hgnn_hidden[-1]]
+        embeddings = sum(hidden)
+        return embeddings[:nl], embeddings[nl:], gcn_hidden, hgnn_hidden
+
+
+class ShardedLocalAwareEncoder(nn.Module):
+    """LocalAwareEncoder (HGNN_HD4.py:336-405, ``--mode=local_only``) on user-row shards, same
+    submodules and parameter names (``state_dict``s load either way): layers 0..L-2 are ED-HNN
+    blocks whose vertex/edge mean pair over V/E = nonzero(ui_adj) runs as
+    :func:`sharded_mean_two_hop`; the last layer is LN0(HGCNConv(Â, ·, act=False)) with the
+    two hops as :func:`sharded_hgcn_conv`; every layer adds the layer-0 residual. All other
+    ops are row-wise, so they run on the local layout unchanged."""
+
+    def __init__(self, data, emb_size, hyper_size, n_layers, leaky, drop_rate, u0: int, u1: int,
+                 group=None, device=None, n_chunks: int = 4, seed: int = 0):
+        super().__init__()
+        self.data = data
+        self.latent_size = emb_size
+        self.hyper_size = hyper_size
+        self.layers = n_layers
+        self.u0, self.u1, self.n_local = int(u0), int(u1), int(u1) - int(u0)
+        self.device = torch.device(device) if device is not None else torch.device("cuda")
+        self.group = group
+        U, I = data.n_users, data.n_items
+        self.edhnn_args = edhnn_config(hyper_size)
+        self.edhnn_layers = nn.ModuleList(
+            [EquivSetGNN(hyper_size, self.edhnn_args, None, data) for _ in range(n_layers)])
+        self.lns = nn.ModuleList([LayerNorm(hyper_size) for _ in range(n_layers)])
+        self.ui = ShardedBipartite.from_global(_coo_tensor(data.ui_adj, binary=True), U, I, u0,
+                                               u1, device=self.device, group=group,
+                                               n_chunks=n_chunks)
+        self.norm = ShardedBipartite.from_global(_coo_tensor(data.norm_adj), U, I, u0, u1,
+                                                 device=self.device, group=group,
+                                                 n_chunks=n_chunks)
+        self.rep_gen = torch.Generator(device=self.device).manual_seed(int(seed))
+        self._drops = {}
+        self.to(self.device)
+
+    def replicated_parameters(self) -> Iterator[nn.Parameter]:
+        return self.parameters()  # every weight is replicated; embeddings come from the caller
+
+    def _drop(self, module: nn.Dropout, x: torch.Tensor) -> torch.Tensor:
+        d = self._drops.get(id(module))
+        if d is None:
+            d = self._drops[id(module)] = _SplitDropout(module.p, self.rep_gen)
+        d.training = self.training
+        return d(x, self.n_local)
+
+    def _edhnn(self, blk: EquivSetGNN, x: torch.Tensor) -> torch.Tensor:
+        """EquivSetGNN.forward (EquivSetGNN2.py:83-103) with the sharded aggregation."""
+        x = self._drop(blk.dropout, x)
+        x = blk.lin_in(x, relu=True)
+        x0 = x
+        conv = blk.conv
+        for _ in range(blk.nlayer):
+            x = self._drop(blk.dropout, x)
+            xv = sharded_mean_two_hop(self.ui, conv.W1(x))
+            if conv.alpha:
+                xv = (1 - conv.alpha) * xv + conv.alpha * x0
+            x = blk.act(conv.W(xv))
+        return self._drop(blk.dropout, x)
+
+    def forward(self, ego_embeddings, sparse_norm_adj=None):
+        res = ego_embeddings
+        for k in range(self.layers):
+            if k != self.layers - 1:
+                ego_embeddings = self._edhnn(self.edhnn_layers[k], ego_embeddings) + res
+            else:
+                z = sharded_hgcn_conv(self.norm, ego_embeddings, act=False)
+                ego_embeddings = layer_norm(z, self.lns[0]) + res
+        nl = self.n_local
+        return ego_embeddings[:nl], ego_embeddings[nl:]

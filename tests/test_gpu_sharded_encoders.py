@@ -1,0 +1,125 @@
+"""GPU, 2 and 3 ranks (gloo between processes sharing cuda:0; RCCL cannot put two ranks on one
+device): the user-row sharded encoders (sharded_encoders.py) against the single-GPU encoders
+on the same graph and parameters — outputs, the embedding gradient, and the parameter gradients
+once the replicated ones are summed (allreduce_replicated_grads). HCCF runs with the
+reference's global CPU drop-edge mask (same seed, same bits) and dropout off; LocalAwareEncoder
+in eval mode. Bound: max |sharded − single| ≤ 1e-5 · max |single| per tensor (the sharded item
+sums are added in a different order)."""
+import os
+import socket
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import hgd_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+U, I, NNZ, D = 257, 131, 4000, 32
+HCCF_KW = dict(lrate=0.001, lr_decay=0.9, max_epoch=1, batch_size=32, reg=0.01,
+               embedding_size=D, hyper_dim=16, drop_rate=0.0, p=0.5, n_layers=3)
+
+
+def _data():
+    u, i = O.synthetic_incidence(U, I, NNZ, seed=3)
+    ui = O.bipartite_adjacency(u, i, U, I).tocsr()
+    return SimpleNamespace(n_users=U, n_items=I, ui_adj=ui, norm_adj=O.normalize_graph_mat(ui).tocsr())
+
+
+def _check(what, got, ref):
+    err = (got.double() - ref.double()).abs().max().item()
+    scale = max(ref.double().abs().max().item(), 1e-30)
+    assert err <= 1e-5 * scale, f"{what}: max err {err:.3e} vs max |ref| {scale:.3e}"
+
+
+def _grads(world, rank, dev):
+    g = torch.Generator().manual_seed(7)
+    Gu = torch.randn(U, D, generator=g)
+    Gi = [torch.randn(I, D, generator=g) for _ in range(world)]
+    return Gu.to(dev), torch.stack(Gi).sum(0).to(dev), Gi[rank].to(dev)
+
+
+def _worker(rank, world, port, which):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        from hypergraph_diffusion_for_recommendation_amd import sharded_encoders as SE
+        from hypergraph_diffusion_for_recommendation_amd.encoders import (HCCFEncoder,
+                                                                          LocalAwareEncoder)
+        from hypergraph_diffusion_for_recommendation_amd.sharded import \
+            allreduce_replicated_grads
+        data = _data()
+        u0, u1 = SE.shard_bounds(U, world, rank)
+        Gu, Gi_tot, Gi_mine = _grads(world, rank, dev)
+        if which == "hccf":
+            torch.manual_seed(0)
+            ref = HCCFEncoder(HCCF_KW, data, device=dev)
+            sh = SE.ShardedHCCFEncoder(HCCF_KW, data, u0, u1, device=dev, n_chunks=3,
+                                       device_rng=False)
+            sh.load_global(ref.embedding_dict)
+            torch.manual_seed(123)
+            ue, ie, _, _ = ref(keep_rate=0.7)
+            ((ue * Gu).sum() + (ie * Gi_tot).sum()).backward()
+            torch.manual_seed(123)
+            se, si, _, _ = sh(keep_rate=0.7)
+            ((se * Gu[u0:u1]).sum() + (si * Gi_mine).sum()).backward()
+            _check("user rows", se, ue[u0:u1])
+            _check("item rows", si, ie)
+            allreduce_replicated_grads(sh.replicated_parameters())
+            rd, sd = ref.embedding_dict, sh.embedding_dict
+            _check("d user_emb", sd['user_emb'].grad, rd['user_emb'].grad[u0:u1])
+            for k in ('item_emb', 'user_w', 'item_w'):
+                _check(f"d {k}", sd[k].grad, rd[k].grad)
+        else:
+            torch.manual_seed(0)
+            ref = LocalAwareEncoder(data, D, D, 3, 0.3, 0.2, device=dev).eval()
+            sh = SE.ShardedLocalAwareEncoder(data, D, D, 3, 0.3, 0.2, u0, u1, device=dev,
+                                             n_chunks=3).eval()
+            missing, unexpected = sh.load_state_dict(ref.state_dict(), strict=False)
+            assert not missing, missing
+            ego = torch.randn(U + I, D, generator=torch.Generator().manual_seed(5)).to(dev)
+            x = ego.clone().requires_grad_(True)
+            ue, ie = ref(x, ref.sparse_norm_adj)
+            ((ue * Gu).sum() + (ie * Gi_tot).sum()).backward()
+            xl = torch.cat([ego[u0:u1], ego[U:]]).requires_grad_(True)
+            se, si = sh(xl)
+            ((se * Gu[u0:u1]).sum() + (si * Gi_mine).sum()).backward()
+            _check("user rows", se, ue[u0:u1])
+            _check("item rows", si, ie)
+            n = u1 - u0
+            _check("d ego users", xl.grad[:n], x.grad[u0:u1])
+            gi = xl.grad[n:].contiguous()
+            dist.all_reduce(gi)
+            _check("d ego items", gi, x.grad[U:])
+            allreduce_replicated_grads(sh.replicated_parameters())
+            rp = dict(ref.named_parameters())
+            for name, p in sh.named_parameters():
+                if rp[name].grad is None:  # unused by the reference too (lns[1:])
+                    assert p.grad is None, name
+                    continue
+                _check(f"d {name}", p.grad, rp[name].grad)
+        torch.cuda.synchronize()
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("which", ["hccf", "local_aware"])
+def test_sharded_encoder_matches_single_gpu(dev, world, which):
+    mp.start_processes(_worker, args=(world, _free_port(), which), nprocs=world, join=True,
+                       start_method="spawn")
