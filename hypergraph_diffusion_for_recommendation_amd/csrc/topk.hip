@@ -12,10 +12,13 @@
 // item among the first K with a top score is listed twice by the reference, and is here too.
 //
 // GPU mapping (one 256-thread workgroup per score row, rows are HBM-streamed):
-//   1. radix select of the K-th largest stream key (4 passes of 8-bit digits, LDS histogram);
-//   2. ordered compaction: every key above the threshold plus the lowest-index ties, giving
-//      exactly K stream candidates (block-wide prefix sums keep index order);
-//   3. bitonic sort of the K candidates and of the K seeds in LDS, merge, write K ids/scores.
+//   1. two float4 sweeps of the row: a 2,048-bin histogram of the keys' top 11 bits locates the
+//      bin of the K-th largest stream key; the second sweep keeps the keys above that bin and
+//      lists the bin's own keys in LDS, whose sort by (key desc, index asc) completes exactly K
+//      stream candidates with the lowest-index ties (k_topk_rows). A row whose threshold bin
+//      holds more than 2,048 keys (heavy ties) takes the generic path instead: 4 radix passes
+//      of 8-bit digits and an ordered compaction (topk_generic);
+//   2. bitonic sort of the K candidates and of the K seeds in LDS, merge, write K ids/scores.
 // Masking is a separate scatter (hgd_mask_scores) that writes the reference's -10e8 in place.
 #include "hgd_internal.h"
 
@@ -63,7 +66,7 @@ __device__ __forceinline__ bool cand_before(const Cand& a, const Cand& b) {
 }
 
 // In-LDS bitonic sort of n (power of two, <= 2*kTopkBlock) candidates, best first.
-__device__ void bitonic_sort(Cand* c, int n) {
+__device__ __forceinline__ void bitonic_sort(Cand* c, int n) {
   for (int size = 2; size <= n; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
       for (int t = threadIdx.x; t < n / 2; t += kTopkBlock) {
@@ -82,17 +85,11 @@ __device__ void bitonic_sort(Cand* c, int n) {
   }
 }
 
-__global__ __launch_bounds__(kTopkBlock) void k_topk_rows(const float* __restrict__ S,
-                                                          int64_t n_cols, int64_t ld, int k,
-                                                          int32_t* __restrict__ out_ids,
-                                                          float* __restrict__ out_scores) {
-  __shared__ int s_hist[256];
-  __shared__ int s_warp[kTopkBlock / 64];
-  __shared__ Cand s_c[2 * kTopkMax];
-  __shared__ int s_sel[2];
-  const int64_t r = blockIdx.x;
-  const float* row = S + r * ld;
-
+// Generic path (any score distribution): 4 radix passes over the row for the k-th largest key,
+// then an ordered compaction pass. Used when the two-pass path's threshold bin is too full.
+__device__ __forceinline__ void topk_generic(const float* __restrict__ row, int64_t n_cols, int k, int* s_hist,
+                             int* s_warp, Cand* s_c, int* s_sel) {
+  __syncthreads();  // the caller's LDS (histogram) is reused
   // 1. radix select: the k-th largest key of the row
   uint32_t prefix = 0, pmask = 0;
   int need = k;  // rank (1-based) still to find inside the current prefix class
@@ -143,7 +140,12 @@ __global__ __launch_bounds__(kTopkBlock) void k_topk_rows(const float* __restric
     n_ties += tot_t;
     __syncthreads();
   }
-  // 3. seeds, sort both halves, merge (first k of the union)
+}
+
+// Seeds (the first k entries), sort of the k stream candidates in s_c[0, k) and of the seeds,
+// merge: the first k of the union in find_k_largest's order.
+__device__ __forceinline__ void topk_finish(const float* __restrict__ row, int k, Cand* s_c, int64_t r,
+                            int32_t* __restrict__ out_ids, float* __restrict__ out_scores) {
   int n2 = 1;
   while (n2 < k) n2 <<= 1;
   for (int t = threadIdx.x; t < n2; t += kTopkBlock) {
@@ -172,6 +174,164 @@ __global__ __launch_bounds__(kTopkBlock) void k_topk_rows(const float* __restric
         ++a;
     }
   }
+}
+
+// Two-pass top-k (the common case): pass 1 builds a 2,048-bin histogram of the keys' top 11 bits
+// and finds the bin holding the k-th largest; pass 2 appends every key of a higher bin to the
+// stream candidates (fewer than k of them, order irrelevant: they are sorted later) and every
+// key of the threshold bin (with its index) to an LDS list. Sorting that list by (key desc,
+// index asc) and taking its first `need` entries gives exactly the generic path's selection,
+// including the lowest-index ties at the k-th key. Two float4 sweeps of the row instead of five
+// scalar ones; rows whose threshold bin exceeds kBinCap entries fall back to topk_generic.
+constexpr int kHistBins = 2048;
+constexpr int kBinCap = 2048;
+
+struct KeyIdx {
+  uint32_t key;
+  int32_t i;
+};
+
+template <typename F>
+__device__ __forceinline__ void for_each_score(const float* __restrict__ row, int64_t n_cols,
+                                               F f) {
+  if ((reinterpret_cast<uintptr_t>(row) & 15) == 0) {
+    // kUnroll float4 loads per lane issued before any is consumed (64 B in flight per lane)
+    constexpr int kUnroll = 4;
+    const float4* r4 = reinterpret_cast<const float4*>(row);
+    const int64_t n4 = n_cols >> 2;
+    int64_t v0 = 0;
+    for (; v0 + kUnroll * kTopkBlock <= n4; v0 += kUnroll * kTopkBlock) {
+      float4 x[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) x[u] = r4[v0 + u * kTopkBlock + threadIdx.x];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const int64_t c = 4 * (v0 + u * kTopkBlock + threadIdx.x);
+        f(x[u].x, c);
+        f(x[u].y, c + 1);
+        f(x[u].z, c + 2);
+        f(x[u].w, c + 3);
+      }
+    }
+    for (int64_t v = v0 + threadIdx.x; v < n4; v += kTopkBlock) {
+      const float4 x = r4[v];
+      f(x.x, 4 * v);
+      f(x.y, 4 * v + 1);
+      f(x.z, 4 * v + 2);
+      f(x.w, 4 * v + 3);
+    }
+    for (int64_t c = 4 * n4 + threadIdx.x; c < n_cols; c += kTopkBlock) f(row[c], c);
+  } else {
+    for (int64_t c = threadIdx.x; c < n_cols; c += kTopkBlock) f(row[c], c);
+  }
+}
+
+__device__ __forceinline__ bool key_before(const KeyIdx& a, const KeyIdx& b) {
+  return a.key != b.key ? a.key > b.key : a.i < b.i;
+}
+
+__global__ __launch_bounds__(kTopkBlock) void k_topk_rows(const float* __restrict__ S,
+                                                          int64_t n_cols, int64_t ld, int k,
+                                                          int32_t* __restrict__ out_ids,
+                                                          float* __restrict__ out_scores) {
+  __shared__ int s_hist[kHistBins];
+  __shared__ int s_warp[kTopkBlock / 64];
+  __shared__ Cand s_c[2 * kTopkMax];
+  __shared__ KeyIdx s_bin[kBinCap];
+  __shared__ int s_sel[4];
+  const int64_t r = blockIdx.x;
+  const float* row = S + r * ld;
+
+  // pass 1: histogram of the top 11 key bits
+  for (int i = threadIdx.x; i < kHistBins; i += kTopkBlock) s_hist[i] = 0;
+  __syncthreads();
+  int* hist = s_hist;
+  for_each_score(row, n_cols, [hist](float s, int64_t) {
+    atomicAdd(&hist[float_key(s) >> 21], 1);
+  });
+  __syncthreads();
+  // threshold bin: thread t owns the 8 bins 2047-8t .. 2040-8t (highest first); a block scan
+  // of the per-thread counts (high bins first) finds the owner of the k-th largest key
+  constexpr int kPer = kHistBins / kTopkBlock;
+  const int top = kHistBins - 1 - kPer * threadIdx.x;
+  int mine = 0;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) mine += s_hist[top - j];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int incl = mine;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) s_warp[w] = incl;
+  __syncthreads();
+  for (int i = 0; i < w; ++i) incl += s_warp[i];
+  const int excl = incl - mine;
+  if (excl < k && incl >= k) {
+    int acc = excl, b = top;
+    for (;; --b) {
+      if (acc + s_hist[b] >= k) break;
+      acc += s_hist[b];
+    }
+    s_sel[0] = b;          // threshold bin
+    s_sel[1] = k - acc;    // entries still needed from it
+    s_sel[2] = s_hist[b];  // its population
+    s_sel[3] = 0;
+  }
+  __syncthreads();
+  const uint32_t sel = static_cast<uint32_t>(s_sel[0]);
+  const int need = s_sel[1];
+  const int in_bin = s_sel[2];
+  const int n_above = k - need;
+  if (in_bin > kBinCap) {  // a crowded threshold bin (heavy ties): the generic path
+    topk_generic(row, n_cols, k, s_hist, s_warp, s_c, s_sel);
+    topk_finish(row, k, s_c, r, out_ids, out_scores);
+    return;
+  }
+  // pass 2: keys of higher bins → stream candidates, threshold-bin keys → s_bin
+  if (threadIdx.x == 0) s_hist[0] = 0;  // reused as the two append counters
+  if (threadIdx.x == 1) s_hist[1] = 0;
+  __syncthreads();
+  Cand* cand = s_c;
+  KeyIdx* bin = s_bin;
+  for_each_score(row, n_cols, [hist, cand, bin, sel](float s, int64_t c) {
+    const uint32_t key = float_key(s);
+    const uint32_t b = key >> 21;
+    if (b > sel) {
+      cand[atomicAdd(&hist[0], 1)] = Cand{s, static_cast<int32_t>(c), 0};
+    } else if (b == sel) {
+      bin[atomicAdd(&hist[1], 1)] = KeyIdx{key, static_cast<int32_t>(c)};
+    }
+  });
+  __syncthreads();
+  // sort the threshold bin by (key desc, index asc); its first `need` entries complete the k
+  int n2 = 1;
+  while (n2 < in_bin) n2 <<= 1;
+  for (int t = in_bin + threadIdx.x; t < n2; t += kTopkBlock) s_bin[t] = KeyIdx{0u, 0x7fffffff};
+  __syncthreads();
+  for (int size = 2; size <= n2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = threadIdx.x; t < n2 / 2; t += kTopkBlock) {
+        const int lo = 2 * t - (t & (stride - 1));
+        const int hi = lo + stride;
+        const bool asc = (lo & size) == 0;
+        const bool swap = asc ? key_before(s_bin[hi], s_bin[lo]) : key_before(s_bin[lo], s_bin[hi]);
+        if (swap) {
+          const KeyIdx tmp = s_bin[lo];
+          s_bin[lo] = s_bin[hi];
+          s_bin[hi] = tmp;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int t = threadIdx.x; t < need; t += kTopkBlock) {
+    const int32_t c = s_bin[t].i;
+    s_c[n_above + t] = Cand{row[c], c, 0};  // the score itself (keeps the sign of a zero)
+  }
+  __syncthreads();
+  topk_finish(row, k, s_c, r, out_ids, out_scores);
 }
 
 // S[r, cols of mask row m(r)] = value, m(r) = row_map ? row_map[r] : r.

@@ -85,9 +85,23 @@ __global__ __launch_bounds__(256) void k_uq_minmax(Src src, int64_t n, State* st
   }
   lo = wave_min(lo);
   hi = wave_max(hi);
-  if ((threadIdx.x & 63) == 0 && lo <= hi) {
-    atomicMin(&st->lo, lo);
-    atomicMax(&st->hi, hi);
+  // one atomic pair per workgroup: every wave hitting the same two words serialised them
+  __shared__ long long s_lo[4], s_hi[4];
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    s_lo[w] = lo;
+    s_hi[w] = hi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < 4; ++i) {
+      lo = s_lo[i] < lo ? s_lo[i] : lo;
+      hi = s_hi[i] > hi ? s_hi[i] : hi;
+    }
+    if (lo <= hi) {
+      atomicMin(&st->lo, lo);
+      atomicMax(&st->hi, hi);
+    }
   }
 }
 
@@ -270,8 +284,8 @@ hgd_status unique_bitmap(Src src, int64_t n, int64_t* out, int64_t* n_out, void*
   int64_t* toff = reinterpret_cast<int64_t*>(w + kOffTileOff);
   uint32_t* bitmap = reinterpret_cast<uint32_t*>(w + kOffBitmap);
   hipLaunchKernelGGL(k_uq_init, dim3(1), dim3(1), 0, st, s);
-  if (n > 0) {
-    const unsigned g = static_cast<unsigned>(std::min<int64_t>(kGrid, (n + 255) / 256));
+  if (n > 0) {  // >= 16 keys per thread before the workgroup's atomic pair
+    const unsigned g = static_cast<unsigned>(std::min<int64_t>(kGrid, (n + 4095) / 4096));
     hipLaunchKernelGGL(k_uq_minmax<Src>, dim3(g), dim3(256), 0, st, src, n, s);
   }
   hipLaunchKernelGGL(k_uq_zero, dim3(kGrid), dim3(256), 0, st, bitmap, s);

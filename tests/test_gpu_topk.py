@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("k", [1, 2, 7, 20, 40, 256])
-@pytest.mark.parametrize("n_cols", [300, 5000])
+@pytest.mark.parametrize("n_cols", [300, 5000, 38048])
 def test_topk_rows_matches_find_k_largest(dev, k, n_cols):
     from hypergraph_diffusion_for_recommendation_amd.evaluation import topk_rows
     rng = np.random.default_rng(k * 31 + n_cols)
@@ -23,6 +23,8 @@ def test_topk_rows_matches_find_k_largest(dev, k, n_cols):
     S[1::4] = rng.standard_normal((len(S[1::4]), n_cols)).astype(np.float32)
     S[2, :] = 0.0                           # all equal
     S[5, 7] = -0.0                          # -0.0 ties +0.0
+    S[6] = np.round(rng.standard_normal(n_cols), 1).astype(np.float32)  # ~2,000-key tie bins
+    S[7, : n_cols // 2] = -10e8                                         # masked (rated) items
     ids, sc = topk_rows(torch.from_numpy(S).to(dev), k)
     ids, sc = ids.cpu().numpy(), sc.cpu().numpy()
     for r in range(rows):
