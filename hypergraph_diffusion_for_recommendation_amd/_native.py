@@ -174,7 +174,10 @@ _SIGNATURES = {
                                 c_void_p]),
     "hgd_topk_rows": (c_i32, [c_void_p, c_i64, c_i64, c_i64, c_i32, c_void_p, c_void_p,
                               c_void_p]),
-    "hgd_epilogue_apply": (c_i32, [c_void_p, c_i64, c_i32, c_f32, c_void_p, c_void_p]),
+    "hgd_rank_metrics": (c_i32, [c_void_p, c_i64, c_i64, c_i32, c_void_p, c_void_p,
+                                 ctypes.POINTER(c_i32), c_i32, c_void_p, c_void_p, c_void_p,
+                                 c_void_p]),
+    "hgd_epilogue_apply":(c_i32, [c_void_p, c_i64, c_i32, c_f32, c_void_p, c_void_p]),
     "hgd_epilogue_backward": (c_i32, [c_void_p, c_void_p, c_i64, c_i32, c_f32, c_void_p,
                                       c_void_p]),
     "hgd_unique_workspace_size": (c_size, [c_i64]),

@@ -10,6 +10,8 @@ first K candidates. Only the [n_users, K] result crosses to the host.
 """
 from __future__ import annotations
 
+import ctypes
+import math
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -83,6 +85,125 @@ def rank_users(user_emb: torch.Tensor, item_emb: torch.Tensor, users: torch.Tens
         out_ids[b0:b0 + batch] = ids
         out_sc[b0:b0 + batch] = sc
     return out_ids, out_sc
+
+
+def ndcg_discount(k: int) -> List[float]:
+    """1.0/math.log(n+2, 2) for n < k, as Metric.NDCG computes it (util/evaluation.py:92-95)."""
+    return [1.0 / math.log(n + 2, 2) for n in range(k)]
+
+
+class TestLists:
+    """The test set of ``ranking_evaluation`` (``origin`` = data.test_set, util/evaluation.py:169)
+    on the device: per test user (in the dict's order) the internal ids of its test items that
+    exist in the training maps (sorted; items never seen in training can never be recommended,
+    so they are never hits) and the full count ``len(origin[user])`` (the recall / hit-ratio /
+    IDCG denominators count them)."""
+
+    def __init__(self, origin: Dict, item_map: Dict, device):
+        self.users = list(origin)
+        counts = np.empty(len(self.users), dtype=np.int64)
+        rowptr = np.zeros(len(self.users) + 1, dtype=np.int64)
+        cols: List[np.ndarray] = []
+        for r, u in enumerate(self.users):
+            items = origin[u]
+            counts[r] = len(items)
+            ids = np.fromiter((item_map[i] for i in items if i in item_map), dtype=np.int64)
+            ids.sort()
+            cols.append(ids)
+            rowptr[r + 1] = rowptr[r] + ids.size
+        self.counts = counts
+        self.rowptr = torch.from_numpy(rowptr).to(device)
+        flat = np.concatenate(cols) if cols else np.zeros(0, dtype=np.int64)
+        self.cols = torch.from_numpy(flat.astype(np.int32)).to(device)
+
+
+@torch.no_grad()
+def rank_metrics(ids: torch.Tensor, tests: TestLists, cutoffs: Sequence[int],
+                 discount: Optional[torch.Tensor] = None) -> Tuple[np.ndarray, np.ndarray]:
+    """hgd_rank_metrics: per test user and cut-off N, the distinct hits among ids[:, :N] and the
+    DCG in position order (float64, bit-identical to Metric.NDCG's loop). ids: device int32
+    [n_users, k] of internal item ids, rows in ``tests.users`` order."""
+    if ids.dim() != 2 or ids.dtype != torch.int32 or ids.device.type != "cuda":
+        raise TypeError("rank_metrics: ids must be a 2-D int32 device tensor")
+    if ids.shape[0] != len(tests.users):
+        raise ValueError(f"rank_metrics: {ids.shape[0]} lists for {len(tests.users)} test users")
+    if ids.stride(1) != 1:
+        ids = ids.contiguous()
+    k = int(ids.shape[1])
+    cut = [int(c) for c in cutoffs]
+    if discount is None:
+        discount = torch.tensor(ndcg_discount(k), dtype=torch.float64, device=ids.device)
+    n = ids.shape[0]
+    hits = torch.empty((n, len(cut)), dtype=torch.int32, device=ids.device)
+    dcg = torch.empty((n, len(cut)), dtype=torch.float64, device=ids.device)
+    carr = (ctypes.c_int32 * len(cut))(*cut)
+    nat.check(nat.load().hgd_rank_metrics(
+        ids.data_ptr(), n, ids.stride(0), k, tests.rowptr.data_ptr(),
+        tests.cols.data_ptr() if tests.cols.numel() else None, carr, len(cut),
+        discount.data_ptr(), hits.data_ptr(), dcg.data_ptr(),
+        torch.cuda.current_stream(ids.device).cuda_stream), "hgd_rank_metrics")
+    return hits.cpu().numpy(), dcg.cpu().numpy()
+
+
+def _seq_sum(values) -> float:
+    """Left-to-right sum (the reference's ``sum(list)`` / ``+=`` loops; Python >= 3.12's
+    compensated float ``sum`` would round differently)."""
+    s = 0
+    for v in values:
+        s += v
+    return s
+
+
+def ranking_evaluation(tests: TestLists, ids: torch.Tensor, N: Sequence[int]) -> List[str]:
+    """Drop-in for ``ranking_evaluation(data.test_set, rec_list, N)`` (util/evaluation.py:169-196)
+    when rec_list came from ``rank_users`` for ``tests.users``: the same list of strings
+    ('Top N', 'Hit Ratio:…', 'Precision:…', 'Recall:…', 'NDCG:…' per N), the same float64
+    arithmetic in the same order, from the device per-user hits / DCG."""
+    N = [int(n) for n in N]
+    order = sorted(set(N))
+    hits, dcg = rank_metrics(ids, tests, order)
+    disc = ndcg_discount(max(order))
+    idcg_prefix = [0]  # IDCG of a c-item test list: the first min(N, c) discounts, in order
+    for v in disc:
+        idcg_prefix.append(idcg_prefix[-1] + v)
+    counts = tests.counts.tolist()
+    total_num = _seq_sum(counts)  # Metric.hit_ratio (:17-29)
+    n_users = len(counts)
+    measure: List[str] = []
+    for n in N:
+        c = order.index(n)
+        h = hits[:, c].tolist()
+        d = dcg[:, c].tolist()
+        hit_num = _seq_sum(h)
+        hr = round(hit_num / total_num, 5)
+        prec = round(hit_num / (n_users * n), 5)                                 # :49-52
+        recall = round(_seq_sum([hu / cu for hu, cu in zip(h, counts)]) / n_users, 5)  # :54-58
+        ndcg = round(_seq_sum([du / idcg_prefix[min(n, cu)] for du, cu in zip(d, counts)])
+                     / n_users, 5)                                              # :84-97
+        measure.append('Top ' + str(n) + '\n')
+        measure += ['Hit Ratio:' + str(hr) + '\n', 'Precision:' + str(prec) + '\n',
+                    'Recall:' + str(recall) + '\n', 'NDCG:' + str(ndcg) + '\n']
+    return measure
+
+
+def evaluate_test_users(data, user_emb: torch.Tensor, item_emb: torch.Tensor,
+                        topN: Sequence[int], tests: Optional[TestLists] = None,
+                        rated: Optional[CSR] = None,
+                        batch: Optional[int] = None) -> Tuple[List[str], torch.Tensor,
+                                                              torch.Tensor]:
+    """GraphRecommender.test() + ranking_evaluation (base/graph_recommender.py:61-92, 130-133)
+    on the device up to the per-user counts: scores, masking, find_k_largest lists and the
+    metric inputs. Returns (measure strings, ids, scores); ids / scores are the device
+    [n_test_users, max(topN)] lists in data.test_set order (internal item ids)."""
+    if tests is None:
+        tests = TestLists(data.test_set, data.item, user_emb.device)
+    if rated is None:
+        rated = rated_csr(data.interaction_mat, user_emb.device)
+    if not tests.users:
+        raise ValueError("evaluate_test_users: empty test set")
+    uid = torch.tensor([data.user[u] for u in tests.users], dtype=torch.int64)
+    ids, sc = rank_users(user_emb, item_emb, uid, rated, max(int(n) for n in topN), batch)
+    return ranking_evaluation(tests, ids, topN), ids, sc
 
 
 def test_rec_list(data, user_emb: torch.Tensor, item_emb: torch.Tensor, max_N: int,

@@ -358,6 +358,19 @@ hgd_status hgd_mask_scores(float* scores, int64_t n_rows, int64_t ld, const int6
 hgd_status hgd_topk_rows(const float* scores, int64_t n_rows, int64_t n_cols, int64_t ld,
                          int32_t k, int32_t* out_ids, float* out_scores, void* stream);
 
+/* Per-user inputs of ranking_evaluation (util/evaluation.py:169-196) for the lists above:
+ *   hits[r, c] = |set(test items of r) ∩ set(ids[r, :N_c])|        (Metric.hits, :8-15)
+ *   dcg[r, c]  = Σ_{n < N_c, ids[r, n] in test} discount[n], in n order (Metric.NDCG, :84-97)
+ * ids int32 [n_rows, ld] (device, k <= 256 used per row, negative = never a hit); the test items
+ * of row r are test_cols[test_rowptr[r] : test_rowptr[r+1]] (device, ascending, distinct
+ * internal item ids); discount float64 [k] (device) = 1.0/math.log(n+2, 2) computed by the host
+ * so DCG is bit-identical to the reference; cutoffs = the N values (HOST array, ascending, in
+ * [1, k], at most 16). Outputs hits int32 / dcg float64 [n_rows, n_cutoffs]. */
+hgd_status hgd_rank_metrics(const int32_t* ids, int64_t n_rows, int64_t ld, int32_t k,
+                            const int64_t* test_rowptr, const int32_t* test_cols,
+                            const int32_t* cutoffs, int32_t n_cutoffs, const double* discount,
+                            int32_t* hits, double* dcg, void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * Sorted unique of integer keys — torch.unique(t.long()) as HCCF's loss calls it every step on
  * [batch, d] embedding blocks: contrastLoss(..., torch.unique(ancs.long()), ...),

@@ -466,3 +466,57 @@ def masked_scores(user_emb, item_emb, users, rated, mask_value=-10e8):
     for r, u in enumerate(users):
         S[r, list(rated[u])] = mask_value
     return S
+
+
+# ---------------------------------------------------------------------------------------------
+# Ranking metrics — util/evaluation.py:8-97 (Metric) and :169-196 (ranking_evaluation)
+# ---------------------------------------------------------------------------------------------
+def ranking_evaluation(origin, res, N):
+    """Literal restatement of ranking_evaluation (util/evaluation.py:169-196) over
+    origin = {user: {item: rating}} and res = {user: [(item, score), ...]}: per N the
+    'Top N', 'Hit Ratio', 'Precision', 'Recall', 'NDCG' strings, with Metric.hits (:8-15),
+    hit_ratio (:17-29), precision (:49-52), recall (:54-58) and NDCG (:84-97) in their loop
+    order (plain ``+=`` sums, math.log(n+2, 2) discounts, round(·, 5))."""
+    import math
+
+    measure = []
+    for n in N:
+        predicted = {user: res[user][:n] for user in res}
+        if len(origin) != len(predicted):
+            raise ValueError("The Lengths of test set and predicted set do not match!")
+        hits = {}
+        for user in origin:                                   # Metric.hits
+            items = list(origin[user].keys())
+            pred = [item[0] for item in predicted[user]]
+            hits[user] = len(set(items).intersection(set(pred)))
+        total_num = 0                                         # Metric.hit_ratio
+        for user in origin:
+            total_num += len(list(origin[user].keys()))
+        hit_num = 0
+        for user in hits:
+            hit_num += hits[user]
+        hr = round(hit_num / total_num, 5)
+        prec = 0                                              # Metric.precision
+        for u in hits:
+            prec += hits[u]
+        prec = round(prec / (len(hits) * n), 5)
+        recall_list = [hits[u] / len(origin[u]) for u in hits]  # Metric.recall
+        s = 0
+        for v in recall_list:
+            s += v
+        recall = round(s / len(recall_list), 5)
+        sum_ndcg = 0                                          # Metric.NDCG
+        for user in predicted:
+            dcg = 0
+            idcg = 0
+            for k, item in enumerate(predicted[user]):
+                if item[0] in origin[user]:
+                    dcg += 1.0 / math.log(k + 2, 2)
+            for k, item in enumerate(list(origin[user].keys())[:n]):
+                idcg += 1.0 / math.log(k + 2, 2)
+            sum_ndcg += dcg / idcg
+        ndcg = round(sum_ndcg / len(predicted), 5)
+        measure.append('Top ' + str(n) + '\n')
+        measure += ['Hit Ratio:' + str(hr) + '\n', 'Precision:' + str(prec) + '\n',
+                    'Recall:' + str(recall) + '\n', 'NDCG:' + str(ndcg) + '\n']
+    return measure

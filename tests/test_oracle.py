@@ -205,3 +205,16 @@ def test_contrast_loss_restatements_agree():
     a = O.contrast_loss(E1, E2, nodes, 0.2)
     b = ref_cpu.contrast_loss(torch.tensor(E1), torch.tensor(E2), torch.tensor(nodes), 0.2)
     assert abs(a - b.item()) <= 1e-12 * max(1.0, abs(a))
+
+
+def test_ranking_evaluation_known_answer():
+    """ranking_evaluation (util/evaluation.py:169-196) on a hand-checked case: a duplicated
+    list entry counts once for hits and twice for DCG; unseen test items count in |test|."""
+    origin = {1: {10: 1, 11: 1}, 2: {12: 1, 99: 1, 13: 1}}
+    res = {1: [(10, .9), (10, .9), (5, .3)], 2: [(13, .5), (12, .4), (7, .1)]}
+    got = O.ranking_evaluation(origin, res, [1, 3])
+    # top 3: hits 1 + 2 of 5 test items; recall (1/2 + 2/3) / 2; NDCG: user 1 DCG = IDCG,
+    # user 2 (1 + 1/log2 3) / (1 + 1/log2 3 + 1/2)
+    assert got == ['Top 1\n', 'Hit Ratio:0.4\n', 'Precision:1.0\n', 'Recall:0.41667\n',
+                   'NDCG:1.0\n', 'Top 3\n', 'Hit Ratio:0.6\n', 'Precision:0.5\n',
+                   'Recall:0.58333\n', 'NDCG:0.88268\n']
