@@ -177,6 +177,10 @@ _SIGNATURES = {
     "hgd_rank_metrics": (c_i32, [c_void_p, c_i64, c_i64, c_i32, c_void_p, c_void_p,
                                  ctypes.POINTER(c_i32), c_i32, c_void_p, c_void_p, c_void_p,
                                  c_void_p]),
+    "hgd_py_shuffle": (c_i32, [c_void_p, c_void_p, c_i64]),
+    "hgd_sample_pairwise": (c_i32, [c_void_p, c_void_p, c_i64, c_i64, c_void_p, c_void_p,
+                                    c_void_p, c_void_p, c_i64, c_i64, c_i32, c_void_p, c_void_p,
+                                    c_void_p]),
     "hgd_epilogue_apply":(c_i32, [c_void_p, c_i64, c_i32, c_f32, c_void_p, c_void_p]),
     "hgd_epilogue_backward": (c_i32, [c_void_p, c_void_p, c_i64, c_i32, c_f32, c_void_p,
                                       c_void_p]),

@@ -372,6 +372,27 @@ hgd_status hgd_rank_metrics(const int32_t* ids, int64_t n_rows, int64_t ld, int3
                             int32_t* hits, double* dcg, void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * Pairwise training sampler (HOST functions, host pointers): next_batch_pairwise
+ * (util/sampler.py:237-264) with CPython's random module bit for bit. mt_state = the 625 words
+ * of random.getstate()[1] (624 MT19937 words + position), read and advanced in place — the
+ * caller hands it back with random.setstate, so the Python stream continues exactly as if the
+ * reference loop had run.
+ *   hgd_py_shuffle:      random.shuffle(x) applied to order[0..n) (x[k] = record order[k]).
+ *   hgd_sample_pairwise: records order[begin..end): out_u / out_i = rec_user / rec_item of the
+ *                        record, then n_negs draws choice(item_list) per record (dense id =
+ *                        _randbelow(n_items)), redrawn while in the user's training items
+ *                        user_items[user_rowptr[u] : user_rowptr[u+1]] (ascending);
+ *                        out_j [(end-begin) * n_negs]. Fails (instead of looping forever like the
+ *                        reference) for a user who has every item.
+ * ---------------------------------------------------------------------------------------- */
+hgd_status hgd_py_shuffle(uint32_t* mt_state, int64_t* order, int64_t n);
+hgd_status hgd_sample_pairwise(uint32_t* mt_state, const int64_t* order, int64_t begin,
+                               int64_t end, const int32_t* rec_user, const int32_t* rec_item,
+                               const int64_t* user_rowptr, const int32_t* user_items,
+                               int64_t n_users, int64_t n_items, int32_t n_negs, int32_t* out_u,
+                               int32_t* out_i, int32_t* out_j);
+
+/* ------------------------------------------------------------------------------------------
  * Sorted unique of integer keys — torch.unique(t.long()) as HCCF's loss calls it every step on
  * [batch, d] embedding blocks: contrastLoss(..., torch.unique(ancs.long()), ...),
  * model/graph/HCCF.py:65-66 (the truncated embedding values become the node list).

@@ -520,3 +520,34 @@ def ranking_evaluation(origin, res, N):
         measure += ['Hit Ratio:' + str(hr) + '\n', 'Precision:' + str(prec) + '\n',
                     'Recall:' + str(recall) + '\n', 'NDCG:' + str(ndcg) + '\n']
     return measure
+
+
+# ---------------------------------------------------------------------------------------------
+# Pairwise sampler — util/sampler.py:237-264
+# ---------------------------------------------------------------------------------------------
+def next_batch_pairwise(data, batch_size, n_negs=1):
+    """Restatement of next_batch_pairwise (util/sampler.py:237-264) on Python's ``random``:
+    in-place shuffle of data.training_data, then per record n_negs random.choice draws over
+    list(data.item.keys()), redrawn while in data.training_set_u[user]. Yields dense-id lists."""
+    from random import choice, shuffle
+
+    training_data = data.training_data
+    shuffle(training_data)
+    ptr = 0
+    data_size = len(training_data)
+    while ptr < data_size:
+        batch_end = ptr + batch_size if ptr + batch_size < data_size else data_size
+        users = [training_data[idx][0] for idx in range(ptr, batch_end)]
+        items = [training_data[idx][1] for idx in range(ptr, batch_end)]
+        ptr = batch_end
+        u_idx, i_idx, j_idx = [], [], []
+        item_list = list(data.item.keys())
+        for i, user in enumerate(users):
+            i_idx.append(data.item[items[i]])
+            u_idx.append(data.user[user])
+            for _ in range(n_negs):
+                neg_item = choice(item_list)
+                while neg_item in data.training_set_u[user]:
+                    neg_item = choice(item_list)
+                j_idx.append(data.item[neg_item])
+        yield u_idx, i_idx, j_idx
