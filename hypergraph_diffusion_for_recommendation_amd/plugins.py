@@ -1,0 +1,416 @@
+"""The hot-path carrier plugins on the SELFRec surface (``selfrec.py``), with the reference's
+training loops (paths relative to /root/reference/HD_SELFRec):
+
+* :class:`HCCF`     — model/graph/HCCF.py:26-133 (HCCFEncoder, BPR + per-layer InfoNCE);
+* :class:`HGNN_HD4` — model/graph/HGNN_HD4.py:32-251 with ``--mode=local_only`` (the ED-HNN
+  "hypergraph diffusion" LocalAwareEncoder; the reference's group / full modes are broken as
+  shipped, SURVEY.md §0.5, and are rejected here);
+* :class:`HGCN`     — model/graph/HGCN.py:15-164 (HGCNConv stack with per-layer
+  TransformerEncoder self-attention).
+
+Each keeps the reference's constructor, config keys, optimiser / scheduler settings, loss
+arithmetic and evaluation cadence — including its quirks (HCCF clips gradients before
+``backward`` and never resets its loss list; HGNN_HD4 steps its scheduler and switches to
+``eval()`` inside the batch loop; HGCN keeps its transformer layers in a plain list, so they
+are not trained) — so a run takes the same steps. What runs underneath is this build's: batches
+from ``sampler.next_batch_pairwise`` (bit-identical to util/sampler.py), the encoders of
+``encoders.py`` on libhgd, ``functional.contrast_loss`` for ``contrastLoss`` and the device
+evaluation of ``GraphRecommender``.
+"""
+from __future__ import annotations
+
+import os
+import random
+import time
+
+import numpy as np
+import torch
+import torch.nn as nn
+from torch.optim.lr_scheduler import ReduceLROnPlateau
+
+from .encoders import HCCFEncoder, LocalAwareEncoder, sparse_tensor_of
+from .functional import contrast_loss, unique_long
+from .layers import HGCNConv, SpAdjDropEdge
+from .sampler import next_batch_pairwise
+from .selfrec import GraphRecommender, early_stopping
+
+
+def bpr_loss(user_emb, pos_item_emb, neg_item_emb):
+    """util/loss_torch.py:5-9."""
+    pos_score = torch.mul(user_emb, pos_item_emb).sum(dim=1)
+    neg_score = torch.mul(user_emb, neg_item_emb).sum(dim=1)
+    return torch.mean(-torch.log(10e-6 + torch.sigmoid(pos_score - neg_score)))
+
+
+def l2_reg_loss(reg, *args):
+    """util/loss_torch.py:17-21."""
+    emb_loss = 0
+    for emb in args:
+        emb_loss += torch.norm(emb, p=2)
+    return emb_loss * reg
+
+
+class HCCF(GraphRecommender):
+    """model/graph/HCCF.py:26-133."""
+
+    def __init__(self, conf, training_set, test_set, knowledge_set, **kwargs):
+        GraphRecommender.__init__(self, conf, training_set, test_set, knowledge_set, **kwargs)
+        self.model = HCCFEncoder(kwargs, self.data, self.device)
+        self._parse_config(self.config, kwargs)
+        self.model.to(self.device)
+        self.optimizer = torch.optim.Adam(self.model.parameters(), lr=self.lRate)
+        self.scheduler = ReduceLROnPlateau(self.optimizer, 'min', factor=self.lr_decay,
+                                           patience=5)
+
+    def _parse_config(self, config, kwargs):  # HCCF.py:39-59
+        self.maxEpoch = int(kwargs['max_epoch'])
+        self.batchSize = int(kwargs['batch_size'])
+        self.lRate = float(kwargs['lrate'])
+        self.lr_decay = float(kwargs['lr_decay'])
+        self.reg = float(kwargs['reg'])
+        self.latent_size = int(kwargs['embedding_size'])
+        self.drop_rate = float(kwargs['drop_rate'])
+        self.leaky = float(kwargs['p'])
+        self.nLayers = int(kwargs['n_layers'])
+        self.ss_rate = float(kwargs['cl_rate'])
+        self.hyperDim = int(config['hyper.size'])
+        self.dropRate = float(config['dropout'])
+        self.negSlove = float(config['leaky'])
+        self.temp = float(config['temp'])
+        self.seed = int(kwargs['seed'])
+        self.early_stopping_steps = int(kwargs['early_stopping_steps'])
+
+    def calcLosses(self, ancs, poss, negs, gcnEmbedsLst, hyperEmbedsLst, reg):  # :61-70
+        bprLoss = bpr_loss(ancs, poss, negs)
+        nu = self.data.n_users
+        sslLoss = 0
+        for i in range(self.nLayers):
+            embeds1 = gcnEmbedsLst[i].detach()
+            embeds2 = hyperEmbedsLst[i]
+            sslLoss += contrast_loss(embeds1[:nu], embeds2[:nu], unique_long(ancs), self.temp) \
+                + contrast_loss(embeds1[nu:], embeds2[nu:], unique_long(poss), self.temp)
+        sslLoss *= self.ss_rate
+        return bprLoss, sslLoss
+
+    def train_step(self, user_idx, pos_idx, neg_idx) -> torch.Tensor:
+        """One batch of HCCF.py:79-97; returns the (device) batch loss."""
+        model = self.model
+        model.train()
+        user_emb, item_emb, gcnEmbedsLst, hyperEmbedsLst = model(keep_rate=1 - self.dropRate)
+        anchor_emb = user_emb[user_idx]
+        pos_emb = item_emb[pos_idx]
+        neg_emb = item_emb[neg_idx]
+        loss_rec, loss_ssl = self.calcLosses(anchor_emb, pos_emb, neg_emb, gcnEmbedsLst,
+                                             hyperEmbedsLst, self.reg)
+        batch_loss = loss_rec + loss_ssl
+        self.optimizer.zero_grad()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 4)  # before backward, as :95
+        batch_loss.backward()
+        self.optimizer.step()
+        return batch_loss
+
+    def train(self, load_pretrained=False):  # HCCF.py:72-118
+        model = self.model
+        recall_list = []
+        train_losses = []  # never reset: the scheduler sees the running mean, as the reference
+        lst_performances = []
+        for ep in range(self.maxEpoch):
+            s_train = time.time()
+            for n, batch in enumerate(next_batch_pairwise(self.data, self.batchSize,
+                                                          device=self.device)):
+                user_idx, pos_idx, neg_idx = batch
+                batch_loss = self.train_step(user_idx, pos_idx, neg_idx)
+                train_losses.append(batch_loss.item())
+            tr_time = time.time() - s_train
+            model.eval()
+            with torch.no_grad():
+                self.user_emb, self.item_emb, _, _ = model(keep_rate=1)
+                s_eval = time.time()
+                cur_data, data_ep = self.fast_evaluation(ep, train_time=tr_time)
+                lst_performances.append(data_ep)
+                print(data_ep)
+                recall_list.append(float(cur_data[2].split(':')[1]))
+                _, should_stop = early_stopping(recall_list, self.early_stopping_steps)
+                if should_stop:
+                    break
+            self.scheduler.step(np.mean(train_losses))
+            print("Eval time: %f s" % (time.time() - s_eval))
+        self.save_perfomance_training(lst_performances)
+        self.user_emb, self.item_emb = self.best_user_emb, self.best_item_emb
+
+    def save(self):
+        with torch.no_grad():
+            self.best_user_emb, self.best_item_emb, _, _ = self.model(keep_rate=1)
+            print("Saving")
+            self.save_model(self.model)
+
+    def predict(self, u):
+        user_id = self.data.get_user_id(u)
+        score = torch.matmul(self.user_emb[user_id], self.item_emb.transpose(0, 1))
+        return score.cpu().numpy()
+
+
+class HGNNModel(nn.Module):
+    """HGNN_HD4.HGNNModel (HGNN_HD4.py:253-335), local encoder only."""
+
+    def __init__(self, data, args, device):
+        super().__init__()
+        self.data = data
+        self.device = device
+        self.sparse_norm_adj = sparse_tensor_of(data.norm_adj, device)
+        self.p = args['p']
+        self.drop_rate = args['drop_rate']
+        self.layers = args['n_layers']
+        self.emb_size = int(args['input_dim'])
+        self.hyper_size = int(args['hyper_dim'])
+        self.hyper_dim = int(args['hyper_dim'])
+        self.batchSize = int(args['batch_size'])
+        init = nn.init.xavier_uniform_
+        self.embedding_dict = nn.ParameterDict({
+            'user_emb': nn.Parameter(init(torch.empty(data.n_users, self.hyper_dim)).to(device)),
+            'item_emb': nn.Parameter(init(torch.empty(data.n_items, self.hyper_dim)).to(device)),
+        })
+        self.hgnn_layer_local = LocalAwareEncoder(data, self.emb_size, self.hyper_size,
+                                                  self.layers, self.p, self.drop_rate, device)
+        self.act = nn.LeakyReLU(self.p)
+        self.dropout = nn.Dropout(self.drop_rate)
+        self.edgeDropper = SpAdjDropEdge()
+
+    def forward(self, mode='local', keep_rate=1):
+        if mode != 'local':
+            raise NotImplementedError("HGNN_HD4: only the local (ED-HNN) encoder is built; the "
+                                      "reference's group encoder is broken as shipped")
+        ego = torch.cat([self.embedding_dict['user_emb'], self.embedding_dict['item_emb']], 0)
+        adj = self.edgeDropper(self.sparse_norm_adj, keep_rate)
+        return self.hgnn_layer_local(ego, adj)
+
+    def calculate_cf_loss(self, anchor_emb, pos_emb, neg_emb, reg):  # :324-328
+        rec_loss = bpr_loss(anchor_emb, pos_emb, neg_emb)
+        reg_loss = l2_reg_loss(reg, anchor_emb, pos_emb, neg_emb) / self.batchSize
+        return rec_loss + reg_loss
+
+
+class HGNN_HD4(GraphRecommender):
+    """model/graph/HGNN_HD4.py:32-251, ``--mode=local_only``."""
+
+    def __init__(self, conf, training_set, test_set, knowledge_set, **kwargs):
+        GraphRecommender.__init__(self, conf, training_set, test_set, knowledge_set, **kwargs)
+        self._parse_config(kwargs)
+        if self.mode != 'local_only':
+            raise NotImplementedError(
+                f"HGNN_HD4 --mode={self.mode}: only local_only is supported (the reference's "
+                "group-aware encoder is broken as shipped, HGNN_HD4.py:320-322, :430)")
+        self.set_seed()
+        self.model = HGNNModel(self.data, kwargs, self.device).to(self.device)
+        self.optimizer = torch.optim.Adam(self.model.parameters(), lr=self.lRate,
+                                          weight_decay=self.weight_decay)
+        self.scheduler = ReduceLROnPlateau(self.optimizer, 'min', factor=self.lr_decay,
+                                           patience=10)
+
+    def _parse_config(self, kwargs):  # :44-79
+        self.dataset = kwargs['dataset']
+        self.lRate = float(kwargs['lrate'])
+        self.lr_decay = float(kwargs['lr_decay'])
+        self.maxEpoch = int(kwargs['max_epoch'])
+        self.batchSize = int(kwargs['batch_size'])
+        self.reg = float(kwargs['reg'])
+        self.hyper_dim = int(kwargs['hyper_dim'])
+        self.p = float(kwargs['p'])
+        self.drop_rate = float(kwargs['drop_rate'])
+        self.layers = int(kwargs['n_layers'])
+        self.cl_rate = float(kwargs['cl_rate'])
+        self.temp = kwargs['temp']
+        self.seed = kwargs['seed']
+        self.mode = kwargs['mode']
+        self.early_stopping_steps = kwargs['early_stopping_steps']
+        self.weight_decay = kwargs['weight_decay']
+
+    def set_seed(self):  # :81-92
+        seed = self.seed
+        np.random.seed(seed)
+        random.seed(seed)
+        torch.manual_seed(seed)
+        torch.cuda.manual_seed(seed)
+        torch.backends.cudnn.deterministic = True
+        torch.backends.cudnn.benchmark = False
+        os.environ["PYTHONHASHSEED"] = str(seed)
+        print(f"Random seed set as {seed}")
+
+    def train(self, load_pretrained=False):  # :94-225 (local_only branch)
+        train_model = self.model
+        lst_train_losses, lst_cf_losses, lst_cl_losses = [], [], []
+        lst_performances, recall_list = [], []
+        for ep in range(self.maxEpoch):
+            cf_losses = []
+            cf_total_loss = 0
+            n_cf_batch = int(self.data.n_cf_train // self.batchSize + 1)
+            train_model.train()
+            s_train = time.time()
+            for n, batch in enumerate(next_batch_pairwise(self.data, self.batch_size,
+                                                          device=self.device)):
+                user_idx, pos_idx, neg_idx = batch
+                user_emb_lc, item_emb_lc = train_model(mode='local', keep_rate=1 - self.drop_rate)
+                cf_batch_loss = train_model.calculate_cf_loss(
+                    user_emb_lc[user_idx], item_emb_lc[pos_idx], item_emb_lc[neg_idx], self.reg)
+                cf_total_loss += cf_batch_loss.item()
+                self.optimizer.zero_grad()
+                cf_batch_loss.backward()
+                self.optimizer.step()
+                cf_losses.append(cf_batch_loss.item())
+                if (n % 20) == 0:
+                    print('CF Training: Epoch {:04d} Iter {:04d} / {:04d} | Iter Loss {:.4f} | '
+                          'Iter Mean Loss {:.4f}'.format(ep, n, n_cf_batch, cf_batch_loss.item(),
+                                                         cf_total_loss / (n + 1)))
+                # the reference does the epoch bookkeeping inside the batch loop (:171-189):
+                # scheduler step on the running mean and eval() after every batch
+                cf_loss = np.mean(cf_losses)
+                train_time = time.time() - s_train
+                lst_cf_losses.append([ep, cf_loss])
+                lst_train_losses.append([ep, cf_loss])
+                lst_cl_losses.append([ep, 0])
+                self.scheduler.step(cf_loss)
+                train_model.eval()
+            with torch.no_grad():
+                self.user_emb, self.item_emb = train_model(mode='local')
+                cur_data, data_ep = self.fast_evaluation(ep, train_time=train_time)
+                lst_performances.append(data_ep)
+                recall_list.append(float(cur_data[2].split(':')[1]))
+                _, should_stop = early_stopping(recall_list, self.early_stopping_steps)
+                if should_stop:
+                    break
+        self.save_loss(lst_train_losses, lst_cf_losses, lst_cl_losses)
+        self.save_perfomance_training(lst_performances)
+        self.user_emb, self.item_emb = self.best_user_emb, self.best_item_emb
+
+    def predict(self, u):
+        user_id = self.data.get_user_id(u)
+        score = torch.matmul(self.user_emb[user_id], self.item_emb.transpose(0, 1))
+        return score.cpu().numpy()
+
+    def save(self):
+        with torch.no_grad():
+            self.best_user_emb, self.best_item_emb = self.model.forward(mode='local')
+            self.save_model(self.model)
+
+
+class HGCN_Encoder(nn.Module):
+    """HGCN.py:104-164: per layer a TransformerEncoder over all nodes (batch 1), then HGCNConv
+    on the edge-dropped norm_adj (LeakyReLU except the last layer), plus the input residual.
+    As in the reference the transformer / conv layers live in plain lists (not registered)."""
+
+    def __init__(self, data, emb_size, hyper_size, n_layers, leaky, drop_rate, device):
+        super().__init__()
+        self.data = data
+        self.latent_size = emb_size
+        self.hyper_size = hyper_size
+        self.layers = n_layers
+        self.norm_adj = data.norm_adj
+        init = nn.init.xavier_uniform_
+        self.embedding_dict = nn.ParameterDict({
+            'user_emb': nn.Parameter(init(torch.empty(data.n_users, hyper_size))),
+            'item_emb': nn.Parameter(init(torch.empty(data.n_items, hyper_size))),
+        })
+        self.sparse_norm_adj = sparse_tensor_of(self.norm_adj, device)
+        self.relu = nn.ReLU()
+        self.act = nn.LeakyReLU(leaky)
+        self.dropout = nn.Dropout(drop_rate)
+        self.edgeDropper = SpAdjDropEdge()
+        self.residuals = torch.nn.ModuleList()
+        self.hgnn_layers = []
+        self.ugformer_layers = []
+        for _ in range(self.layers):
+            enc = nn.TransformerEncoderLayer(d_model=hyper_size, nhead=2, dim_feedforward=32,
+                                             dropout=drop_rate)
+            self.ugformer_layers.append(
+                nn.TransformerEncoder(enc, 1, norm=nn.LayerNorm(hyper_size)).to(device))
+            self.hgnn_layers.append(HGCNConv(leaky=leaky))
+
+    def forward(self, keep_rate=1):
+        ego = torch.cat([self.embedding_dict['user_emb'], self.embedding_dict['item_emb']], 0)
+        adj = self.edgeDropper(self.sparse_norm_adj, keep_rate)
+        res = ego
+        all_embeddings = []
+        for k in range(self.layers):
+            ego = torch.squeeze(self.ugformer_layers[k](torch.unsqueeze(ego, 1)), 1)
+            if k != self.layers - 1:
+                ego = self.hgnn_layers[k](adj, ego)
+            else:
+                ego = self.hgnn_layers[k](adj, ego, act=False)
+            all_embeddings += [ego]
+        all_embeddings[-1] = all_embeddings[-1] + res
+        nu = self.data.n_users
+        return all_embeddings[-1][:nu], all_embeddings[-1][nu:]
+
+
+class HGCN(GraphRecommender):
+    """model/graph/HGCN.py:15-102."""
+
+    def __init__(self, conf, training_set, test_set, knowledge_set, **kwargs):
+        super().__init__(conf, training_set, test_set, knowledge_set, **kwargs)
+        self.n_layers = int(kwargs['n_layers'])
+        self.early_stopping_steps = int(kwargs['early_stopping_steps'])
+        self.weight_decay = float(kwargs['weight_decay'])
+        self.emb_size = int(kwargs['input_dim'])
+        self.hyper_size = int(kwargs['hyper_dim'])
+        self.leaky = float(kwargs['p'])
+        self.drop_rate = float(kwargs['drop_rate'])
+        self.reg = float(kwargs['reg'])
+        self.model = HGCN_Encoder(self.data, self.emb_size, self.hyper_size, self.n_layers,
+                                  self.leaky, self.drop_rate, self.device)
+
+    def train(self, load_pretrained=False):
+        model = self.model.to(self.device)
+        optimizer = torch.optim.Adam(model.parameters(), lr=self.lRate,
+                                     weight_decay=self.weight_decay)
+        scheduler = ReduceLROnPlateau(optimizer, 'min', factor=self.lr_decay, patience=10)
+        recall_list = []
+        lst_train_losses, lst_rec_losses, lst_reg_losses, lst_performances = [], [], [], []
+        for epoch in range(self.maxEpoch):
+            train_losses, rec_losses, reg_losses = [], [], []
+            for n, batch in enumerate(next_batch_pairwise(self.data, self.batch_size,
+                                                          device=self.device)):
+                user_idx, pos_idx, neg_idx = batch
+                rec_user_emb, rec_item_emb = model(keep_rate=1 - self.drop_rate)
+                user_emb = rec_user_emb[user_idx]
+                pos_item_emb, neg_item_emb = rec_item_emb[pos_idx], rec_item_emb[neg_idx]
+                rec_loss = bpr_loss(user_emb, pos_item_emb, neg_item_emb)
+                reg_loss = l2_reg_loss(self.reg, user_emb, pos_item_emb,
+                                       neg_item_emb) / self.batch_size
+                batch_loss = rec_loss + reg_loss
+                train_losses.append(batch_loss.item())
+                rec_losses.append(rec_loss.item())
+                reg_losses.append(reg_loss.item())
+                optimizer.zero_grad()
+                batch_loss.backward()
+                optimizer.step()
+                if n % 100 == 0 and n > 0:
+                    print('training:', epoch + 1, 'batch', n, 'batch_loss:', batch_loss.item())
+            train_loss = np.mean(train_losses)
+            scheduler.step(train_loss)
+            lst_train_losses.append([epoch, train_loss])
+            lst_rec_losses.append([epoch, np.mean(rec_losses)])
+            lst_reg_losses.append([epoch, np.mean(reg_losses)])
+            with torch.no_grad():
+                self.user_emb, self.item_emb = model()
+            measure, data_ep = self.fast_evaluation(epoch)
+            lst_performances.append(data_ep)
+            recall_list.append(float(measure[2].split(':')[1]))
+            _, should_stop = early_stopping(recall_list, self.early_stopping_steps)
+            if should_stop:
+                break
+        self.save_loss(lst_train_losses, lst_rec_losses, lst_reg_losses)
+        self.save_perfomance_training(lst_performances)
+        self.user_emb, self.item_emb = self.best_user_emb, self.best_item_emb
+
+    def save(self):
+        with torch.no_grad():
+            self.best_user_emb, self.best_item_emb = self.model.forward()
+            self.save_model(self.model)
+
+    def predict(self, u):
+        u = self.data.get_user_id(u)
+        score = torch.matmul(self.user_emb[u], self.item_emb.transpose(0, 1))
+        return score.cpu().numpy()
+
+
+PLUGINS = {"HCCF": HCCF, "HGNN_HD4": HGNN_HD4, "HGCN": HGCN}

@@ -106,3 +106,73 @@ def contrast_loss(embeds1: torch.Tensor, embeds2: torch.Tensor, nodes: torch.Ten
     nume = torch.exp(torch.sum(pck1 * pck2, dim=-1) / temp)
     deno = torch.exp(pck1 @ pck2.T / temp).sum(-1) + 1e-8
     return -torch.log(nume / deno).mean()
+
+
+# ---------------------------------------------------------------------------------------------
+# HCCF training step with the reference's own torch calls (device-agnostic; GPU tests run it on
+# the device as the plugin-level oracle) — model/graph/HCCF.py:61-97, 163-226, util/loss_torch.py
+# ---------------------------------------------------------------------------------------------
+def bpr_loss(user_emb, pos_item_emb, neg_item_emb):
+    """util/loss_torch.py:5-9."""
+    pos_score = torch.mul(user_emb, pos_item_emb).sum(dim=1)
+    neg_score = torch.mul(user_emb, neg_item_emb).sum(dim=1)
+    return torch.mean(-torch.log(10e-6 + torch.sigmoid(pos_score - neg_score)))
+
+
+def sp_adj_drop_edge(adj, keep_rate):
+    """SpAdjDropEdge.forward (HCCF.py:217-226): CPU torch.rand(nnz) mask, kept values / keep."""
+    if keep_rate == 1.0:
+        return adj
+    vals = adj._values()
+    idxs = adj._indices()
+    mask = ((torch.rand(vals.size()) + keep_rate).floor()).type(torch.bool)
+    return torch.sparse_coo_tensor(idxs[:, mask.to(idxs.device)],
+                                   vals[mask.to(vals.device)] / keep_rate, adj.shape)
+
+
+class HCCFEncoderRef(torch.nn.Module):
+    """HCCFEncoder.forward (HCCF.py:173-191) with torch.sparse.mm / torch.mm, parameter names
+    of the reference (and of encoders.HCCFEncoder, so a state_dict moves between them)."""
+
+    def __init__(self, n_users, n_items, latent, hyper_dim, n_layers, drop_rate, sparse_adj):
+        super().__init__()
+        self.n_users, self.n_layers = n_users, n_layers
+        self.adj = sparse_adj
+        dev = sparse_adj.device
+        self.embedding_dict = torch.nn.ParameterDict({
+            'user_emb': torch.nn.Parameter(torch.empty(n_users, latent, device=dev)),
+            'item_emb': torch.nn.Parameter(torch.empty(n_items, latent, device=dev)),
+            'user_w': torch.nn.Parameter(torch.empty(latent, hyper_dim, device=dev)),
+            'item_w': torch.nn.Parameter(torch.empty(latent, hyper_dim, device=dev)),
+        })
+        self.drop_out = torch.nn.Dropout(drop_rate)
+
+    def forward(self, keep_rate=0.5):
+        nu = self.n_users
+        e = self.embedding_dict
+        hidden = [torch.cat([e['user_emb'], e['item_emb']], 0)]
+        gcn_hidden, hgnn_hidden = [], []
+        hyper_uu = e['user_emb'] @ e['user_w']
+        hyper_ii = e['item_emb'] @ e['item_w']
+        for _ in range(self.n_layers):
+            gcn = torch.sparse.mm(sp_adj_drop_edge(self.adj, keep_rate), hidden[-1])
+            hu = self.drop_out(hyper_uu)
+            hi = self.drop_out(hyper_ii)
+            hyper_u = torch.mm(hu, torch.mm(hu.T, hidden[-1][:nu]))
+            hyper_i = torch.mm(hi, torch.mm(hi.T, hidden[-1][nu:]))
+            gcn_hidden.append(gcn)
+            hgnn_hidden.append(torch.cat([hyper_u, hyper_i], 0))
+            hidden.append(gcn + hgnn_hidden[-1])
+        emb = sum(hidden)
+        return emb[:nu], emb[nu:], gcn_hidden, hgnn_hidden
+
+
+def hccf_losses(n_users, n_layers, ancs, poss, negs, gcn, hyper, temp, ss_rate):
+    """HCCF.calcLosses (HCCF.py:61-70): BPR + ss_rate · Σ_layers InfoNCE(users) + InfoNCE(items)
+    over torch.unique(emb.long()) node lists."""
+    ssl = 0
+    for i in range(n_layers):
+        e1, e2 = gcn[i].detach(), hyper[i]
+        ssl += contrast_loss(e1[:n_users], e2[:n_users], torch.unique(ancs.long()), temp) \
+            + contrast_loss(e1[n_users:], e2[n_users:], torch.unique(poss.long()), temp)
+    return bpr_loss(ancs, poss, negs), ssl * ss_rate

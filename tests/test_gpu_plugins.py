@@ -1,0 +1,142 @@
+"""GPU: the SELFRec plugin surface (selfrec.py + plugins.py) end to end on a small dataset
+written in the reference's file formats, and HCCF's training steps against the reference's
+own torch calls (oracle/ref_cpu.py) with the same initial weights, batches and RNG draws."""
+import os
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import hgd_oracle as O
+from oracle import ref_cpu as RC
+
+pytestmark = pytest.mark.gpu
+
+HCCF_CONF = """training.set=train.txt
+test.set=test.txt
+dataset=toy
+model.name={model}
+model.type=graph
+item.ranking=-topN 10,20
+embedding.size=32
+num.max.epoch=2
+batch_size=256
+num_layers=2
+learnRate=0.001
+learnRateDecay=0.7
+reg.lambda=0.01
+use.knowledge=false
+hyper.size=32
+ss_rate=1
+dropout=0.3
+leaky=0.5
+temp=1
+"""
+
+
+def _write_dataset(root, n_users=300, n_items=500, n_train=6000, seed=0):
+    """train.txt / test.txt with a header line, comma separated (data/loader.py:24-38); raw ids
+    are not dense; the test file holds unseen users (dropped) and unseen items (kept)."""
+    rng = np.random.default_rng(seed)
+    d = os.path.join(root, "toy")
+    os.makedirs(d, exist_ok=True)
+    u = rng.integers(0, n_users, n_train) * 3 + 1
+    i = rng.zipf(1.3, n_train) % n_items * 7 + 2
+    with open(os.path.join(d, "train.txt"), "w") as f:
+        f.write("user,item,rating\n")
+        f.writelines(f"{a},{b},1\n" for a, b in zip(u, i))
+    tu = rng.integers(0, n_users + 20, 900) * 3 + 1
+    ti = rng.integers(0, n_items + 10, 900) * 7 + 2
+    with open(os.path.join(d, "test.txt"), "w") as f:
+        f.write("user\titem\trating\n")
+        f.writelines(f"{a}\t{b}\t1\n" for a, b in zip(tu, ti))
+    return d
+
+
+def _setup(tmp_path, monkeypatch, model="HCCF", **over):
+    from hypergraph_diffusion_for_recommendation_amd.selfrec import ModelConf, default_args
+    monkeypatch.chdir(tmp_path)
+    _write_dataset(str(tmp_path / "dataset"))
+    conf_path = tmp_path / f"{model}.conf"
+    conf_path.write_text(HCCF_CONF.format(model=model))
+    conf = ModelConf(str(conf_path))
+    conf.config['dataset'] = 'toy'
+    args = dict(dataset='toy', max_epoch=2, batch_size=256, embedding_size=32, hyper_dim=32,
+                input_dim=32, n_layers=2, item_ranking='10,20', drop_rate=0.3, p=0.5, temp=0.2,
+                cl_rate=1e-3, reg=0.01, early_stopping_steps=5, seed=7)
+    args.update(over)
+    kwargs = default_args(**args)
+    kwargs['dataset_root'] = str(tmp_path / "dataset")
+    return conf, kwargs
+
+
+@pytest.mark.parametrize("model,extra", [("HCCF", {}), ("HGNN_HD4", {"mode": "local_only"}),
+                                         ("HGCN", {})])
+def test_selfrec_execute_end_to_end(dev, tmp_path, monkeypatch, model, extra):
+    from hypergraph_diffusion_for_recommendation_amd.selfrec import SELFRec
+    conf, kwargs = _setup(tmp_path, monkeypatch, model, **extra)
+    random.seed(3)
+    torch.manual_seed(3)
+    rec = SELFRec(conf, kwargs).execute()
+    # the lifecycle's files (graph_recommender.py:94-119, 201-239)
+    out = rec.output + "/"
+    assert os.path.exists(out + f"{model}-top-20items.txt")
+    assert os.path.exists(out + f"{model}-performance.txt")
+    assert os.path.exists(rec.output + "/performance.csv")
+    # the device metrics are the reference's ranking_evaluation of the same lists
+    rec_list = rec.test()
+    assert list(rec_list) == list(rec.data.test_set)
+    assert rec.result == O.ranking_evaluation(rec.data.test_set, rec_list, rec.topN)
+    # users absent from training are dropped from the test set, unseen items are kept
+    assert all(u in rec.data.user for u in rec.data.test_set)
+    assert any(i not in rec.data.item for t in rec.data.test_set.values() for i in t)
+    assert len(rec.bestPerformance) == 2 and rec.bestPerformance[1]['Recall'] >= 0.0
+
+
+def test_hccf_steps_match_reference_ops(dev, tmp_path, monkeypatch):
+    """Six HCCF training steps (HCCF.py:79-97) through the plugin (libhgd hops, fused InfoNCE,
+    MFMA E·W) and through the reference's torch calls, from the same weights, on the same
+    batches, with the same CPU drop-edge masks and GPU dropout masks. Tolerance: batch losses
+    within 2e-4 relative, parameters within 1e-4 absolute (fp32 summation-order differences
+    through six Adam steps at lr 1e-3)."""
+    from hypergraph_diffusion_for_recommendation_amd.plugins import HCCF
+    from hypergraph_diffusion_for_recommendation_amd.sampler import next_batch_pairwise
+    from hypergraph_diffusion_for_recommendation_amd.selfrec import FileIO
+    conf, kwargs = _setup(tmp_path, monkeypatch, "HCCF")
+    kwargs.pop('dataset_root')
+    d = str(tmp_path / "dataset" / "toy") + "/"
+    torch.manual_seed(0)
+    rec = HCCF(conf, FileIO.load_data_set(d + "train.txt"), FileIO.load_data_set(d + "test.txt"),
+               None, **kwargs)
+    nu, ni = rec.data.n_users, rec.data.n_items
+    ref = RC.HCCFEncoderRef(nu, ni, 32, 32, rec.nLayers, rec.model.drop_rate,
+                            rec.model.sparse_norm_adj.detach())
+    ref.load_state_dict(rec.model.state_dict(), strict=False)
+    ref_opt = torch.optim.Adam(ref.parameters(), lr=rec.lRate)
+    random.seed(11)
+    batches = list(next_batch_pairwise(rec.data, 256, device=dev))[:6]
+    for k, (u, i, j) in enumerate(batches):
+        torch.manual_seed(100 + k)
+        got = float(rec.train_step(u, i, j).detach())
+        torch.manual_seed(100 + k)
+        ref.train()
+        ue, ie, gcn, hyp = ref(keep_rate=1 - rec.dropRate)
+        bpr, ssl = RC.hccf_losses(nu, rec.nLayers, ue[u], ie[i], ie[j], gcn, hyp, rec.temp,
+                                  rec.ss_rate)
+        loss = bpr + ssl
+        ref_opt.zero_grad()
+        torch.nn.utils.clip_grad_norm_(ref.parameters(), 4)
+        loss.backward()
+        ref_opt.step()
+        assert abs(got - float(loss)) <= 2e-4 * abs(float(loss)), (k, got, float(loss))
+    for name, p in rec.model.state_dict().items():
+        if name.startswith("embedding_dict"):
+            torch.testing.assert_close(p, ref.state_dict()[name], rtol=0, atol=1e-4)
+
+
+def test_hgnn_hd4_rejects_broken_modes(dev, tmp_path, monkeypatch):
+    from hypergraph_diffusion_for_recommendation_amd.selfrec import SELFRec
+    conf, kwargs = _setup(tmp_path, monkeypatch, "HGNN_HD4", mode="full")
+    with pytest.raises(NotImplementedError):
+        SELFRec(conf, kwargs).execute()
