@@ -1,0 +1,123 @@
+// SpAdjDropEdge's keep-mask from torch's CPU generator, bit for bit, without torch's four
+// tensor passes.
+//
+// Reference (paths relative to /root/reference/HD_SELFRec): SpAdjDropEdge.forward
+// (model/graph/HCCF.py:217-226 and its copies) draws
+//     mask = ((torch.rand(edgeNum) + keepRate).floor()).type(torch.bool)
+// on the default CPU generator every layer of every step — at Yelp2018 size 2.3 M draws per
+// layer, ≈ 10-30 ms per layer in torch (rand, add, floor, cast, then a count), which bounds the
+// whole training step. The same mask comes out of one pass here:
+//   * torch's CPU generator is at::mt19937 (MT19937, 32-bit outputs; ATen/core/MT19937RNGEngine.h)
+//     and torch.rand(float32) takes one output per element, serially, as
+//     ((y & 0xFFFFFF) · 2^-24) (uniform_real_distribution<float>, ATen/core/TransformationHelper.h);
+//   * `+ keepRate` adds the float32-rounded scalar in float32, floor(·) != 0  ⇔  sum >= 1.
+// The generator state is torch.get_rng_state()'s byte layout (CPUGeneratorImplState: the legacy
+// POD with the 624 MT words as uint64, then the float-normal cache), read and written in place
+// so the caller hands it back with torch.set_rng_state; the Python side checks the layout once
+// against torch.rand itself before using this path.
+#include <cstdint>
+#include <cstring>
+
+#include "../../include/hgd.h"
+#include "hgd_internal.h"
+
+namespace hgd {
+namespace {
+
+constexpr int kN = 624;
+constexpr int kM = 397;
+
+// torch/csrc (aten/src/ATen/CPUGeneratorImpl.cpp) CPUGeneratorImplStateLegacy + State
+struct TorchCpuStateLegacy {
+  uint64_t the_initial_seed;
+  int32_t left;
+  int32_t seeded;
+  uint64_t next;
+  uint64_t state[kN];
+  double normal_x;
+  double normal_y;
+  double normal_rho;
+  int32_t normal_is_valid;
+};
+struct TorchCpuState {
+  TorchCpuStateLegacy legacy_pod;
+  float next_float_normal_sample;
+  bool is_next_float_normal_sample_valid;
+};
+static_assert(sizeof(TorchCpuState) == 5056, "torch CPU generator state layout");
+
+inline uint32_t twist(uint32_t u, uint32_t v) {
+  return (((u & 0x80000000u) | (v & 0x7fffffffu)) >> 1) ^ ((v & 1u) ? 0x9908b0dfu : 0u);
+}
+
+// at::mt19937::next_state on a plain uint32 array
+void next_state(uint32_t* s) {
+  uint32_t* p = s;
+  for (int j = kN - kM + 1; --j; ++p) *p = p[kM] ^ twist(p[0], p[1]);
+  for (int j = kM; --j; ++p) *p = p[kM - kN] ^ twist(p[0], p[1]);
+  *p = p[kM - kN] ^ twist(p[0], s[0]);
+}
+
+inline uint32_t temper(uint32_t y) {
+  y ^= (y >> 11);
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= (y >> 18);
+  return y;
+}
+
+}  // namespace
+}  // namespace hgd
+
+extern "C" size_t hgd_torch_cpu_state_bytes(void) { return sizeof(hgd::TorchCpuState); }
+
+extern "C" hgd_status hgd_torch_cpu_keep_mask(uint8_t* torch_state, int64_t state_bytes,
+                                              int64_t n, float keep, uint8_t* mask,
+                                              int64_t* kept) {
+  using namespace hgd;
+  clear_error();
+  HGD_REQUIRE(torch_state && state_bytes == static_cast<int64_t>(sizeof(TorchCpuState)),
+              "hgd_torch_cpu_keep_mask: state must be the %zu bytes of torch.get_rng_state()",
+              sizeof(TorchCpuState));
+  HGD_REQUIRE(n >= 0 && (mask || n == 0), "hgd_torch_cpu_keep_mask: bad n / mask");
+  TorchCpuState st;
+  std::memcpy(&st, torch_state, sizeof(st));
+  TorchCpuStateLegacy& L = st.legacy_pod;
+  HGD_REQUIRE(L.left >= 1 && L.left <= kN && L.next <= static_cast<uint64_t>(kN),
+              "hgd_torch_cpu_keep_mask: generator state out of range (left=%d next=%llu)",
+              L.left, static_cast<unsigned long long>(L.next));
+  uint32_t s[kN];
+  for (int i = 0; i < kN; ++i) s[i] = static_cast<uint32_t>(L.state[i]);
+  int left = L.left;
+  uint32_t next = static_cast<uint32_t>(L.next);
+  int64_t cnt = 0;
+  int64_t k = 0;
+  while (k < n) {
+    // at::mt19937::operator(): if (--left == 0) next_state(); y = state[next++]
+    if (--left == 0) {
+      next_state(s);
+      left = kN;
+      next = 0;
+    }
+    // the run of outputs available before the next refill: `left` more calls succeed without
+    // one (this call included), each consuming s[next++]
+    const int64_t run = std::min<int64_t>(n - k, left);
+    for (int64_t t = 0; t < run; ++t) {
+      const uint32_t y = temper(s[next + t]);
+      const float r = static_cast<float>(y & 0xFFFFFFu) * (1.0f / 16777216.0f);
+      const float v = r + keep;            // float32 add, as the tensor op
+      const uint8_t m = v >= 1.0f ? 1 : 0;  // floor(v) != 0 for v in [keep, keep + 1)
+      mask[k + t] = m;
+      cnt += m;
+    }
+    next += static_cast<uint32_t>(run);
+    left -= static_cast<int>(run - 1);  // the first call of the run already decremented
+    k += run;
+  }
+  for (int i = 0; i < kN; ++i) L.state[i] = s[i];
+  L.left = left;
+  L.next = next;
+  std::memcpy(torch_state, &st, sizeof(st));
+  if (kept) *kept = cnt;
+  return HGD_OK;
+}

@@ -343,11 +343,12 @@ class Incidence:
         inc.perm_t = perm  # CSC position → CSR position (sort-free drop-edge rebuilds)
         return inc
 
-    def drop(self, mask: torch.Tensor, keep: float) -> "Incidence":
+    def drop(self, mask: torch.Tensor, keep: float, kept: Optional[int] = None) -> "Incidence":
         """The incidence of SpAdjDropEdge's output (HCCF.py:217-226) built from this one without
         any sort: ``mask`` (uint8/bool, CSR order) keeps nonzeros in order and values are divided
         by ``keep``; the CSC comes from compacting this CSC through ``perm_t``
-        (hgd_dropedge_structure). One device→host read (the kept count)."""
+        (hgd_dropedge_structure). One device→host read (the kept count) unless the caller passes
+        ``kept`` (e.g. counted with a host-drawn mask)."""
         lib = nat.load()
         dev = self.device
         st = _stream(dev)
@@ -371,7 +372,8 @@ class Incidence:
             col.data_ptr() if nnz else None, nat.ptr(val), colptr.data_ptr(),
             row_t.data_ptr() if nnz else None, nat.ptr(val_t), ws.data_ptr(), ws.numel(), st),
             "hgd_dropedge_structure")
-        kept = int(rowptr[R].item()) if R else 0
+        if kept is None:
+            kept = int(rowptr[R].item()) if R else 0
         col, row_t = col[:kept], row_t[:kept]
         if weighted:
             val, val_t = val[:kept], val_t[:kept]

@@ -75,6 +75,60 @@ class HGCNConv(nn.Module):
         return two_hop(inc, embs)
 
 
+_NATIVE_CPU_MASK: Optional[bool] = None
+
+
+def _native_cpu_mask_ok() -> bool:
+    """Once per process: hgd_torch_cpu_keep_mask must reproduce torch.rand's mask and leave the
+    generator where torch.rand leaves it (it restates torch's generator layout; if this torch
+    build differs, torch.rand itself draws the mask)."""
+    global _NATIVE_CPU_MASK
+    if _NATIVE_CPU_MASK is None:
+        from . import _native as nat
+        saved = torch.get_rng_state()
+        ok = saved.numel() == nat.load().hgd_torch_cpu_state_bytes()
+        try:
+            for n in (1, 623, 1250):
+                if not ok:
+                    break
+                torch.set_rng_state(saved)
+                ref = ((torch.rand(n) + 0.7).floor()).type(torch.bool)
+                ref_next = torch.rand(4)
+                torch.set_rng_state(saved)
+                got, cnt = _native_keep_mask(n, 0.7)
+                ok = bool((got.bool() == ref).all()) and cnt == int(ref.sum()) and bool(
+                    (torch.rand(4) == ref_next).all())
+        finally:
+            torch.set_rng_state(saved)
+        _NATIVE_CPU_MASK = ok
+    return _NATIVE_CPU_MASK
+
+
+def _native_keep_mask(n: int, keep: float):
+    import ctypes
+
+    from . import _native as nat
+    st = torch.get_rng_state()
+    mask = torch.empty(n, dtype=torch.uint8, pin_memory=torch.cuda.is_available())
+    kept = ctypes.c_int64(0)
+    nat.check(nat.load().hgd_torch_cpu_keep_mask(st.data_ptr(), st.numel(), n, float(keep),
+                                                 mask.data_ptr() if n else None,
+                                                 ctypes.byref(kept)), "hgd_torch_cpu_keep_mask")
+    torch.set_rng_state(st)
+    return mask, int(kept.value)
+
+
+def torch_cpu_keep_mask(n: int, keep: float):
+    """``((torch.rand(n) + keep).floor()).type(torch.bool)`` of HCCF.py:223 on the default CPU
+    generator — bit-identical mask and generator advance — as (uint8 host mask, kept count):
+    one native pass (hgd_torch_cpu_keep_mask, ≈5 ms at 2.3 M entries) instead of torch's rand +
+    add + floor + cast + count."""
+    if _native_cpu_mask_ok():
+        return _native_keep_mask(n, keep)
+    mask = ((torch.rand(n) + keep).floor()).type(torch.bool)
+    return mask, int(mask.sum())
+
+
 class SpAdjDropEdge(nn.Module):
     """Edge dropout on a sparse COO adjacency (HCCF.py:213-226).
 
@@ -109,14 +163,13 @@ class SpAdjDropEdge(nn.Module):
                     torch.cuda.current_stream(device).cuda_stream), "hgd_bernoulli_mask")
             count = None
         else:
-            mask = ((torch.rand(edgeNum) + keepRate).floor()).type(torch.bool)
-            count = int(mask.sum())
+            mask, count = torch_cpu_keep_mask(vals.numel(), keepRate)
             mask = mask.to(device, non_blocking=True)
         child = None
         if parent is not None and parent.coo_sorted and parent.perm_t is not None:
-            # COO order == CSR order: the structure first, its kept count (the one device→host
-            # read of the step) then sizes the COO compaction
-            child = parent.drop(mask, keepRate)
+            # COO order == CSR order: the structure first (sized by the host count when the mask
+            # was drawn on the host, else by its one device→host read), then the COO compaction
+            child = parent.drop(mask, keepRate, kept=count)
             count = child.nnz
         new_idx, new_vals = drop_edges(idxs.to(device), vals.to(device), mask, keepRate, count)
         out = torch.sparse_coo_tensor(new_idx, new_vals, adj.shape)

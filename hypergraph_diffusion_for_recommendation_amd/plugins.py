@@ -16,6 +16,11 @@ are not trained) — so a run takes the same steps. What runs underneath is this
 from ``sampler.next_batch_pairwise`` (bit-identical to util/sampler.py), the encoders of
 ``encoders.py`` on libhgd, ``functional.contrast_loss`` for ``contrastLoss`` and the device
 evaluation of ``GraphRecommender``.
+
+Drop-edge masks come from torch's default CPU generator exactly as the reference draws them
+(natively, ``layers.torch_cpu_keep_mask``), so runs are reproducible against the reference for a
+seed. ``kwargs['hgd_device_rng'] = True`` draws them on the device instead (same Bernoulli
+distribution, a different stream, no host work in the step).
 """
 from __future__ import annotations
 
@@ -56,6 +61,7 @@ class HCCF(GraphRecommender):
     def __init__(self, conf, training_set, test_set, knowledge_set, **kwargs):
         GraphRecommender.__init__(self, conf, training_set, test_set, knowledge_set, **kwargs)
         self.model = HCCFEncoder(kwargs, self.data, self.device)
+        self.model.edgeDropper.device_rng = bool(kwargs.get('hgd_device_rng', False))
         self._parse_config(self.config, kwargs)
         self.model.to(self.device)
         self.optimizer = torch.optim.Adam(self.model.parameters(), lr=self.lRate)
@@ -202,6 +208,7 @@ class HGNN_HD4(GraphRecommender):
                 "group-aware encoder is broken as shipped, HGNN_HD4.py:320-322, :430)")
         self.set_seed()
         self.model = HGNNModel(self.data, kwargs, self.device).to(self.device)
+        self.model.edgeDropper.device_rng = bool(kwargs.get('hgd_device_rng', False))
         self.optimizer = torch.optim.Adam(self.model.parameters(), lr=self.lRate,
                                           weight_decay=self.weight_decay)
         self.scheduler = ReduceLROnPlateau(self.optimizer, 'min', factor=self.lr_decay,
@@ -357,6 +364,7 @@ class HGCN(GraphRecommender):
         self.reg = float(kwargs['reg'])
         self.model = HGCN_Encoder(self.data, self.emb_size, self.hyper_size, self.n_layers,
                                   self.leaky, self.drop_rate, self.device)
+        self.model.edgeDropper.device_rng = bool(kwargs.get('hgd_device_rng', False))
 
     def train(self, load_pretrained=False):
         model = self.model.to(self.device)

@@ -392,6 +392,14 @@ hgd_status hgd_sample_pairwise(uint32_t* mt_state, const int64_t* order, int64_t
                                int64_t n_users, int64_t n_items, int32_t n_negs, int32_t* out_u,
                                int32_t* out_i, int32_t* out_j);
 
+/* SpAdjDropEdge's CPU keep-mask (HCCF.py:223: floor(torch.rand(nnz) + keepRate).bool()) from
+ * torch's default CPU generator, bit for bit, in one host pass (HOST function). torch_state =
+ * the bytes of torch.get_rng_state() (hgd_torch_cpu_state_bytes(), 5056 on x86-64), advanced in
+ * place by n draws for torch.set_rng_state; mask uint8 [n] (host); *kept = number of ones. */
+size_t hgd_torch_cpu_state_bytes(void);
+hgd_status hgd_torch_cpu_keep_mask(uint8_t* torch_state, int64_t state_bytes, int64_t n,
+                                   float keep, uint8_t* mask, int64_t* kept);
+
 /* ------------------------------------------------------------------------------------------
  * Sorted unique of integer keys — torch.unique(t.long()) as HCCF's loss calls it every step on
  * [batch, d] embedding blocks: contrastLoss(..., torch.unique(ancs.long()), ...),
