@@ -6,7 +6,11 @@ training loops (paths relative to /root/reference/HD_SELFRec):
   "hypergraph diffusion" LocalAwareEncoder; the reference's group / full modes are broken as
   shipped, SURVEY.md §0.5, and are rejected here);
 * :class:`HGCN`     — model/graph/HGCN.py:15-164 (HGCNConv stack with per-layer
-  TransformerEncoder self-attention).
+  TransformerEncoder self-attention);
+* :class:`HCCF_diffusion` — model/graph/HCCF_diffusion.py:22-129 (HCCF's loop with the ED-HNN
+  block on the learned hypergraph, ``encoders.HCCFDiffusionEncoder``);
+* :class:`DHCF`     — model/graph/DHCF.py:19-185 (HGCNConv on the interaction matrix, which
+  the reference densifies, for users and items).
 
 Each keeps the reference's constructor, config keys, optimiser / scheduler settings, loss
 arithmetic and evaluation cadence — including its quirks (HCCF clips gradients before
@@ -33,7 +37,7 @@ import torch
 import torch.nn as nn
 from torch.optim.lr_scheduler import ReduceLROnPlateau
 
-from .encoders import HCCFEncoder, LocalAwareEncoder, sparse_tensor_of
+from .encoders import HCCFDiffusionEncoder, HCCFEncoder, LocalAwareEncoder, sparse_tensor_of
 from .functional import contrast_loss, unique_long
 from .layers import HGCNConv, SpAdjDropEdge
 from .sampler import next_batch_pairwise
@@ -421,4 +425,134 @@ class HGCN(GraphRecommender):
         return score.cpu().numpy()
 
 
-PLUGINS = {"HCCF": HCCF, "HGNN_HD4": HGNN_HD4, "HGCN": HGCN}
+class HCCF_diffusion(HCCF):
+    """model/graph/HCCF_diffusion.py:22-129: HCCF's constructor, losses and loop verbatim, with
+    the encoder whose hypergraph hop is the ED-HNN block on the learned hypergraph."""
+
+    def __init__(self, conf, training_set, test_set, knowledge_set, **kwargs):
+        GraphRecommender.__init__(self, conf, training_set, test_set, knowledge_set, **kwargs)
+        self.model = HCCFDiffusionEncoder(kwargs, self.data, self.device)
+        self.model.edgeDropper.device_rng = bool(kwargs.get('hgd_device_rng', False))
+        self._parse_config(self.config, kwargs)
+        self.model.to(self.device)
+        self.optimizer = torch.optim.Adam(self.model.parameters(), lr=self.lRate)
+        self.scheduler = ReduceLROnPlateau(self.optimizer, 'min', factor=self.lr_decay,
+                                           patience=5)
+
+
+class DHCF_Encoder(nn.Module):
+    """DHCF.py:146-185. The reference densifies ``interaction_mat`` [U, I] and runs
+    HGCNConv (``leaky(A·(Aᵀ·E_u))`` for users, ``leaky(Aᵀ·(A·E_i))`` for items) on it with
+    torch.sparse.mm; here the same operator runs on the sparse matrix (values = interaction
+    counts, as the dense copy holds them). Every layer applies the conv to the layer-0
+    embeddings (the reference passes ``uEmbed`` / ``iEmbed`` each time), so all layers are the
+    same tensor: it is computed once and concatenated L times — identical values, and autograd
+    sums the L copies' gradients exactly as it sums the reference's L identical branches.
+    ``fc_u`` / ``fc_i`` exist (and are optimised) but are unused, as in the reference."""
+
+    def __init__(self, config, data, args, device):
+        super().__init__()
+        self.data = data
+        self.input_dim = args['input_dim']
+        self.hyper_dim = args['hyper_dim']
+        self.p = args['p']
+        self.drop_rate = args['drop_rate']
+        self.layers = args['n_layers']
+        self.adj = sparse_tensor_of(data.interaction_mat, device)        # [U, I]
+        self.adj_t = sparse_tensor_of(data.interaction_mat.T.tocsr(), device)  # [I, U]
+        init = nn.init.xavier_uniform_
+        self.embedding_dict = nn.ParameterDict({
+            'user_emb': nn.Parameter(init(torch.empty(data.n_users, self.hyper_dim)).to(device)),
+            'item_emb': nn.Parameter(init(torch.empty(data.n_items, self.hyper_dim)).to(device)),
+        })
+        self.fc_u = nn.Linear(self.hyper_dim, self.hyper_dim)
+        self.fc_i = nn.Linear(self.hyper_dim, self.hyper_dim)
+        self.hgnn_u = HGCNConv(leaky=self.p)
+        self.hgnn_i = HGCNConv(leaky=self.p)
+        self.non_linear = nn.ReLU()
+        self.dropout = nn.Dropout(self.drop_rate)
+
+    def forward(self):
+        uEmbed = self.embedding_dict['user_emb']
+        iEmbed = self.embedding_dict['item_emb']
+        hu = self.hgnn_u(self.adj, uEmbed)
+        hi = self.hgnn_i(self.adj_t, iEmbed)
+        return (torch.cat([uEmbed] + [hu] * self.layers, dim=1),
+                torch.cat([iEmbed] + [hi] * self.layers, dim=1))
+
+
+class DHCF(GraphRecommender):
+    """model/graph/DHCF.py:19-130."""
+
+    def __init__(self, conf, training_set, test_set, knowledge_set, **kwargs):
+        super().__init__(conf, training_set, test_set, knowledge_set, **kwargs)
+        self.kwargs = kwargs
+        self.model = DHCF_Encoder(self.config, self.data, kwargs, self.device)
+        self.lRate = float(kwargs['lrate'])
+        self.lr_decay = float(kwargs['lr_decay'])
+        self.maxEpoch = int(kwargs['max_epoch'])
+        self.batchSize = int(kwargs['batch_size'])
+        self.reg = float(kwargs['reg'])
+        self.weight_decay = float(kwargs['weight_decay'])
+        self.early_stopping_steps = int(kwargs['early_stopping_steps'])
+
+    def train(self, load_pretrained=False):
+        model = self.model.to(self.device)
+        optimizer = torch.optim.Adam(model.parameters(), lr=self.lRate,
+                                     weight_decay=self.weight_decay)
+        scheduler = ReduceLROnPlateau(optimizer, 'min', factor=self.lr_decay, patience=5)
+        lst_train_losses, lst_rec_losses, lst_reg_losses = [], [], []
+        lst_performances, recall_list = [], []
+        for epoch in range(self.maxEpoch):
+            train_losses, rec_losses, reg_losses = [], [], []
+            s_train = time.time()
+            for n, batch in enumerate(next_batch_pairwise(self.data, self.batch_size,
+                                                          device=self.device)):
+                user_idx, pos_idx, neg_idx = batch
+                rec_user_emb, rec_item_emb = model()
+                user_emb = rec_user_emb[user_idx]
+                pos_item_emb, neg_item_emb = rec_item_emb[pos_idx], rec_item_emb[neg_idx]
+                rec_loss = bpr_loss(user_emb, pos_item_emb, neg_item_emb)
+                reg_loss = l2_reg_loss(self.reg, user_emb, pos_item_emb,
+                                       neg_item_emb) / self.batch_size
+                batch_loss = rec_loss + reg_loss
+                train_losses.append(batch_loss.item())
+                rec_losses.append(rec_loss.item())
+                reg_losses.append(reg_loss.item())
+                optimizer.zero_grad()
+                torch.nn.utils.clip_grad_norm_(model.parameters(), 4)
+                batch_loss.backward()
+                optimizer.step()
+                if n % 100 == 0 and n > 0:
+                    print('training:', epoch + 1, 'batch', n, 'batch_loss:', batch_loss.item())
+            tr_time = time.time() - s_train
+            train_loss = np.mean(train_losses)
+            lst_train_losses.append([epoch, train_loss])
+            lst_rec_losses.append([epoch, np.mean(rec_losses)])
+            lst_reg_losses.append([epoch, np.mean(reg_losses)])
+            scheduler.step(train_loss)
+            with torch.no_grad():
+                self.user_emb, self.item_emb = model()
+                cur_data, data_ep = self.fast_evaluation(epoch, train_time=tr_time)
+                lst_performances.append(data_ep)
+                recall_list.append(float(cur_data[2].split(':')[1]))
+                _, should_stop = early_stopping(recall_list, self.early_stopping_steps)
+                if should_stop:
+                    break
+        self.save_loss(lst_train_losses, lst_rec_losses, lst_reg_losses)
+        self.save_perfomance_training(lst_performances)
+        self.user_emb, self.item_emb = self.best_user_emb, self.best_item_emb
+
+    def save(self):
+        with torch.no_grad():
+            self.best_user_emb, self.best_item_emb = self.model.forward()
+            self.save_model(self.model)
+
+    def predict(self, u):
+        u = self.data.get_user_id(u)
+        score = torch.matmul(self.user_emb[u], self.item_emb.transpose(0, 1))
+        return score.cpu().numpy()
+
+
+PLUGINS = {"HCCF": HCCF, "HGNN_HD4": HGNN_HD4, "HGCN": HGCN, "HCCF_diffusion": HCCF_diffusion,
+           "DHCF": DHCF}
