@@ -7,6 +7,8 @@ encoder (paths relative to /root/reference/HD_SELFRec):
 
 * :class:`HCCFEncoder`       model/graph/HCCF.py:136-191
 * :class:`LocalAwareEncoder` model/graph/HGNN_HD4.py:336-405 (``--mode=local_only``)
+* :class:`LocalAwareEncoderHD3` model/graph/HGNN_HD3.py:352-427 (the SpMM-form ED-HNN blocks)
+* :class:`HCCFDiffusionEncoder` model/graph/HCCF_diffusion.py:131-215
 
 Everything sparse runs on libhgd, with the LayerNorm / residual after a hop fused into its store;
 HCCF's dense ``E·W`` and learned-hypergraph products run on the skinny MFMA kernels; dropout
@@ -192,3 +194,48 @@ class HCCFDiffusionEncoder(HCCFEncoder):
             hidden += [gcn_emb + hgnn_hidden[-1]]
         emb = sum(hidden)
         return emb[:nu], emb[nu:], gcn_hidden, hgnn_hidden
+
+
+class LocalAwareEncoderHD3(nn.Module):
+    """HGNN_HD3's local encoder (HGNN_HD3.py:352-427): layers 0..L-2 are the SpMM form of the
+    ED-HNN block (``edhnn_spmm.EquivSetGNN``, both aggregations HGCNConv(0.5) two-hops over the
+    edge-dropped ``norm_adj``, HGNN_HD3.py:555-720) plus the layer-0 residual; the last layer is
+    ``lns[L-1](HGCNConv(Â, ·, act=False)) + res`` on the UN-dropped ``norm_adj`` (the reference
+    uses ``self.sparse_norm_adj`` there), fused into one hop store. The dense ``ui_adj`` copies
+    the reference builds for its group encoder (``hyper_uu`` / ``hyper_ii``, :386-387) are
+    unused by this encoder and not built."""
+
+    def __init__(self, data, emb_size, hyper_size, n_layers, leaky, drop_rate, device=None):
+        super().__init__()
+        from .edhnn_spmm import EquivSetGNN as EquivSetGNNSpMM
+        self.data = data
+        self.latent_size = emb_size
+        self.hyper_size = hyper_size
+        self.layers = n_layers
+        self.device = torch.device(device) if device is not None else torch.device("cuda")
+        self.relu = nn.ReLU()
+        self.act = nn.LeakyReLU(leaky)
+        self.dropout = nn.Dropout(drop_rate)
+        self.edgeDropper = SpAdjDropEdge()
+        self.sparse_norm_adj = sparse_tensor_of(data.norm_adj, self.device)
+        self.edhnn_args = edhnn_config(self.hyper_size)
+        self.hgcn_layer = HGCNConv(leaky=0.3)
+        self.hgnn_layers = nn.ModuleList([HGCNConv(leaky=0.3) for _ in range(self.layers)])
+        self.edhnn_layers = nn.ModuleList([
+            EquivSetGNNSpMM(hyper_size, self.edhnn_args, None, data, data.n_users, data.n_items,
+                            leaky=0.5) for _ in range(self.layers)])
+        self.lns = nn.ModuleList([LayerNorm(hyper_size) for _ in range(self.layers)])
+        self.edhnn_ui_n = data.n_users + data.n_items
+        self.to(self.device)
+
+    def forward(self, ego_embeddings, sparse_norm_adj):
+        res = ego_embeddings
+        for k in range(self.layers):
+            if k != self.layers - 1:
+                ego_embeddings = self.edhnn_layers[k](ego_embeddings, sparse_norm_adj,
+                                                      self.edhnn_ui_n) + res
+            else:
+                ego_embeddings = two_hop_fused(incidence_of(self.sparse_norm_adj), ego_embeddings,
+                                               norm=self.lns[k], res1=res, res1_scale=1.0)
+        nu = self.data.n_users
+        return ego_embeddings[:nu], ego_embeddings[nu:]

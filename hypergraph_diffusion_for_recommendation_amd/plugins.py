@@ -5,6 +5,8 @@ training loops (paths relative to /root/reference/HD_SELFRec):
 * :class:`HGNN_HD4` — model/graph/HGNN_HD4.py:32-251 with ``--mode=local_only`` (the ED-HNN
   "hypergraph diffusion" LocalAwareEncoder; the reference's group / full modes are broken as
   shipped, SURVEY.md §0.5, and are rejected here);
+* :class:`HGNN_HD3` — model/graph/HGNN_HD3.py:37-266, the same plugin around the SpMM-form
+  ED-HNN encoder (``encoders.LocalAwareEncoderHD3``);
 * :class:`HGCN`     — model/graph/HGCN.py:15-164 (HGCNConv stack with per-layer
   TransformerEncoder self-attention);
 * :class:`HCCF_diffusion` — model/graph/HCCF_diffusion.py:22-129 (HCCF's loop with the ED-HNN
@@ -37,7 +39,8 @@ import torch
 import torch.nn as nn
 from torch.optim.lr_scheduler import ReduceLROnPlateau
 
-from .encoders import HCCFDiffusionEncoder, HCCFEncoder, LocalAwareEncoder, sparse_tensor_of
+from .encoders import (HCCFDiffusionEncoder, HCCFEncoder, LocalAwareEncoder,
+                       LocalAwareEncoderHD3, sparse_tensor_of)
 from .functional import contrast_loss, unique_long
 from .layers import HGCNConv, SpAdjDropEdge
 from .sampler import next_batch_pairwise
@@ -161,9 +164,10 @@ class HCCF(GraphRecommender):
 
 
 class HGNNModel(nn.Module):
-    """HGNN_HD4.HGNNModel (HGNN_HD4.py:253-335), local encoder only."""
+    """HGNN_HD4.HGNNModel (HGNN_HD4.py:253-335; HGNN_HD3.py:268-350 is the same class around
+    its own LocalAwareEncoder), local encoder only."""
 
-    def __init__(self, data, args, device):
+    def __init__(self, data, args, device, local_encoder=LocalAwareEncoder):
         super().__init__()
         self.data = data
         self.device = device
@@ -180,8 +184,8 @@ class HGNNModel(nn.Module):
             'user_emb': nn.Parameter(init(torch.empty(data.n_users, self.hyper_dim)).to(device)),
             'item_emb': nn.Parameter(init(torch.empty(data.n_items, self.hyper_dim)).to(device)),
         })
-        self.hgnn_layer_local = LocalAwareEncoder(data, self.emb_size, self.hyper_size,
-                                                  self.layers, self.p, self.drop_rate, device)
+        self.hgnn_layer_local = local_encoder(data, self.emb_size, self.hyper_size,
+                                              self.layers, self.p, self.drop_rate, device)
         self.act = nn.LeakyReLU(self.p)
         self.dropout = nn.Dropout(self.drop_rate)
         self.edgeDropper = SpAdjDropEdge()
@@ -203,15 +207,19 @@ class HGNNModel(nn.Module):
 class HGNN_HD4(GraphRecommender):
     """model/graph/HGNN_HD4.py:32-251, ``--mode=local_only``."""
 
+    local_encoder = LocalAwareEncoder
+
     def __init__(self, conf, training_set, test_set, knowledge_set, **kwargs):
         GraphRecommender.__init__(self, conf, training_set, test_set, knowledge_set, **kwargs)
         self._parse_config(kwargs)
         if self.mode != 'local_only':
             raise NotImplementedError(
-                f"HGNN_HD4 --mode={self.mode}: only local_only is supported (the reference's "
+                f"{type(self).__name__} --mode={self.mode}: only local_only is supported (the "
+                "reference's "
                 "group-aware encoder is broken as shipped, HGNN_HD4.py:320-322, :430)")
         self.set_seed()
-        self.model = HGNNModel(self.data, kwargs, self.device).to(self.device)
+        self.model = HGNNModel(self.data, kwargs, self.device,
+                               self.local_encoder).to(self.device)
         self.model.edgeDropper.device_rng = bool(kwargs.get('hgd_device_rng', False))
         self.optimizer = torch.optim.Adam(self.model.parameters(), lr=self.lRate,
                                           weight_decay=self.weight_decay)
@@ -302,6 +310,17 @@ class HGNN_HD4(GraphRecommender):
         with torch.no_grad():
             self.best_user_emb, self.best_item_emb = self.model.forward(mode='local')
             self.save_model(self.model)
+
+
+class HGNN_HD3(HGNN_HD4):
+    """model/graph/HGNN_HD3.py:37-266: HGNN_HD4's plugin code line for line (plus
+    ``torch.cuda.manual_seed_all`` in set_seed) around the SpMM-form local encoder."""
+
+    local_encoder = LocalAwareEncoderHD3
+
+    def set_seed(self):  # HGNN_HD3.py:86-98
+        torch.cuda.manual_seed_all(self.seed)
+        super().set_seed()
 
 
 class HGCN_Encoder(nn.Module):
@@ -554,5 +573,5 @@ class DHCF(GraphRecommender):
         return score.cpu().numpy()
 
 
-PLUGINS = {"HCCF": HCCF, "HGNN_HD4": HGNN_HD4, "HGCN": HGCN, "HCCF_diffusion": HCCF_diffusion,
+PLUGINS = {"HCCF": HCCF, "HGNN_HD4": HGNN_HD4, "HGNN_HD3": HGNN_HD3, "HGCN": HGCN, "HCCF_diffusion": HCCF_diffusion,
            "DHCF": DHCF}
