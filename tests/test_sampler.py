@@ -118,3 +118,35 @@ def test_torch_cpu_keep_mask_matches_torch_rand(n, keep, skip):
     assert got.dtype == torch.uint8 and torch.equal(got.bool(), ref)
     assert kept == int(ref.sum())
     assert torch.equal(torch.rand(16), ref_next)
+
+
+def test_torch_cpu_keep_mask_prefetch_keeps_the_stream():
+    """The prefetched draw is used only when nothing else drew from the generator in between:
+    interleaved torch.rand calls, changed sizes / rates and reseeds all give torch's own masks."""
+    _lib_or_skip()
+    import torch
+    from hypergraph_diffusion_for_recommendation_amd.layers import torch_cpu_keep_mask
+
+    def ref_mask(n, keep):
+        return ((torch.rand(n) + keep).floor()).type(torch.bool)
+
+    plan = [(3000, 0.7, None), (3000, 0.7, None), (3000, 0.7, "rand"), (3000, 0.5, None),
+            (1000, 0.5, None), (1000, 0.5, "seed"), (1000, 0.5, None), (3000, 0.7, None)]
+    torch.manual_seed(123)
+    want = []
+    for n, keep, between in plan:
+        want.append(ref_mask(n, keep))
+        if between == "rand":
+            torch.rand(5)
+        elif between == "seed":
+            torch.manual_seed(7)
+    want_next = torch.rand(8)
+    torch.manual_seed(123)
+    for (n, keep, between), w in zip(plan, want):
+        got, kept = torch_cpu_keep_mask(n, keep)
+        assert torch.equal(got.bool(), w) and kept == int(w.sum())
+        if between == "rand":
+            torch.rand(5)
+        elif between == "seed":
+            torch.manual_seed(7)
+    assert torch.equal(torch.rand(8), want_next)
