@@ -87,13 +87,17 @@ class HCCFEncoder(nn.Module):
         hyper_ii = linear(self.embedding_dict['item_emb'], self.embedding_dict['item_w'].t())
         for _ in range(self.n_layers):
             gcn_emb = self.gcnlayer(self.edgeDropper(self.sparse_norm_adj, keep_rate), hidden[-1])
-            hyper_uemb = self.hgnnlayer(self.drop_out(hyper_uu), hidden[-1][:nu])
-            hyper_iemb = self.hgnnlayer(self.drop_out(hyper_ii), hidden[-1][nu:])
+            # torch.split views instead of [:nu] / [nu:] slices: same values, and autograd
+            # joins the two halves' gradients with one cat instead of zero-fill + copy per slice
+            h_u, h_i = torch.split(hidden[-1], [nu, hidden[-1].shape[0] - nu])
+            hyper_uemb = self.hgnnlayer(self.drop_out(hyper_uu), h_u)
+            hyper_iemb = self.hgnnlayer(self.drop_out(hyper_ii), h_i)
             gcn_hidden += [gcn_emb]
             hgnn_hidden += [torch.cat([hyper_uemb, hyper_iemb], 0)]
             hidden += [gcn_emb + hgnn_hidden[-1]]
         embeddings = sum(hidden)
-        return embeddings[:nu], embeddings[nu:], gcn_hidden, hgnn_hidden
+        user_emb, item_emb = torch.split(embeddings, [nu, embeddings.shape[0] - nu])
+        return user_emb, item_emb, gcn_hidden, hgnn_hidden
 
 
 def edhnn_config(hyper_size):

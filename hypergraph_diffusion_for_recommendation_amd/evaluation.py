@@ -145,13 +145,11 @@ def rank_metrics(ids: torch.Tensor, tests: TestLists, cutoffs: Sequence[int],
     return hits.cpu().numpy(), dcg.cpu().numpy()
 
 
-def _seq_sum(values) -> float:
-    """Left-to-right sum (the reference's ``sum(list)`` / ``+=`` loops; Python >= 3.12's
-    compensated float ``sum`` would round differently)."""
-    s = 0
-    for v in values:
-        s += v
-    return s
+def _seq_sum(values: np.ndarray) -> float:
+    """Left-to-right float64 sum, as the reference's ``sum(list)`` / ``+=`` loops round it:
+    ``np.cumsum`` accumulates sequentially (``np.sum`` is pairwise and Python >= 3.12's ``sum``
+    compensated — both would round differently)."""
+    return float(np.cumsum(np.asarray(values, dtype=np.float64))[-1]) if len(values) else 0.0
 
 
 def ranking_evaluation(tests: TestLists, ids: torch.Tensor, N: Sequence[int]) -> List[str]:
@@ -163,23 +161,23 @@ def ranking_evaluation(tests: TestLists, ids: torch.Tensor, N: Sequence[int]) ->
     order = sorted(set(N))
     hits, dcg = rank_metrics(ids, tests, order)
     disc = ndcg_discount(max(order))
-    idcg_prefix = [0]  # IDCG of a c-item test list: the first min(N, c) discounts, in order
+    idcg_prefix = [0.0]  # IDCG of a c-item test list: the first min(N, c) discounts, in order
     for v in disc:
         idcg_prefix.append(idcg_prefix[-1] + v)
-    counts = tests.counts.tolist()
-    total_num = _seq_sum(counts)  # Metric.hit_ratio (:17-29)
+    idcg_prefix = np.asarray(idcg_prefix, dtype=np.float64)
+    counts = tests.counts.astype(np.int64)
+    total_num = int(counts.sum())  # Metric.hit_ratio (:17-29), integer
     n_users = len(counts)
     measure: List[str] = []
     for n in N:
         c = order.index(n)
-        h = hits[:, c].tolist()
-        d = dcg[:, c].tolist()
-        hit_num = _seq_sum(h)
+        h = hits[:, c].astype(np.int64)
+        hit_num = int(h.sum())
         hr = round(hit_num / total_num, 5)
-        prec = round(hit_num / (n_users * n), 5)                                 # :49-52
-        recall = round(_seq_sum([hu / cu for hu, cu in zip(h, counts)]) / n_users, 5)  # :54-58
-        ndcg = round(_seq_sum([du / idcg_prefix[min(n, cu)] for du, cu in zip(d, counts)])
-                     / n_users, 5)                                              # :84-97
+        prec = round(hit_num / (n_users * n), 5)                                  # :49-52
+        recall = round(_seq_sum(h / counts) / n_users, 5)                         # :54-58
+        ndcg = round(_seq_sum(dcg[:, c] / idcg_prefix[np.minimum(counts, n)]) / n_users,
+                     5)                                                           # :84-97
         measure.append('Top ' + str(n) + '\n')
         measure += ['Hit Ratio:' + str(hr) + '\n', 'Precision:' + str(prec) + '\n',
                     'Recall:' + str(recall) + '\n', 'NDCG:' + str(ndcg) + '\n']

@@ -96,12 +96,15 @@ class HCCF(GraphRecommender):
     def calcLosses(self, ancs, poss, negs, gcnEmbedsLst, hyperEmbedsLst, reg):  # :61-70
         bprLoss = bpr_loss(ancs, poss, negs)
         nu = self.data.n_users
+        # torch.unique(ancs.long()) / torch.unique(poss.long()) are the same in every layer of the
+        # reference's loop: computed once here (each is a device→host read)
+        u_nodes, p_nodes = unique_long(ancs), unique_long(poss)
         sslLoss = 0
         for i in range(self.nLayers):
             embeds1 = gcnEmbedsLst[i].detach()
             embeds2 = hyperEmbedsLst[i]
-            sslLoss += contrast_loss(embeds1[:nu], embeds2[:nu], unique_long(ancs), self.temp) \
-                + contrast_loss(embeds1[nu:], embeds2[nu:], unique_long(poss), self.temp)
+            sslLoss += contrast_loss(embeds1[:nu], embeds2[:nu], u_nodes, self.temp) \
+                + contrast_loss(embeds1[nu:], embeds2[nu:], p_nodes, self.temp)
         sslLoss *= self.ss_rate
         return bprLoss, sslLoss
 
