@@ -77,9 +77,10 @@ class EquivSetConv(nn.Module):
         if fused and tuple(Xev.shape) == tuple(X0.shape):
             slope1 = self.hgcn_layers[1].act.negative_slope
             # (1-α)·(LN1(leaky(A·(Aᵀ·Xev))) + Xev) + α·X0 in one store
+            # (α = 0, the configs' restart_alpha: X0 drops out exactly, so it is not read)
             X = two_hop_fused(inc, Xev, epilogue="leaky_relu", slope=slope1, norm=self.lns[1],
                               out_scale=1 - self.alpha, res1=Xev, res1_scale=1 - self.alpha,
-                              res2=X0, res2_scale=self.alpha)
+                              res2=X0 if self.alpha != 0 else None, res2_scale=self.alpha)
         else:
             X_v = self.lns[1](self.hgcn_layers[1](sparse_norm_adj, Xev, act=True)) + Xev
             X = (1 - self.alpha) * X_v + self.alpha * X0

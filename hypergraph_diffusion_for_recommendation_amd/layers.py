@@ -361,6 +361,10 @@ class EquivSetConv(nn.Module):
         scale = "mean" if self.aggr == "mean" else None
         Xs = self.W1(X)
         if self.W2 is None:
+            if self.alpha == 0 and self.fused_epilogue:
+                # (1-0)·Xv + 0·X0 is Xv for finite X0 (HGNN_HD4's restart_alpha = 0): no blend,
+                # no X0 read, and the plain two-hop's backward
+                return self.W(two_hop(inc, Xs, P=scale, Q=scale, R=None))
             if self.fused_epilogue and torch.is_tensor(X0) and tuple(X0.shape) == (N, Xs.shape[1]):
                 # restart blend (1-α)·Xv + α·X0 fused into the second hop's store
                 return self.W(two_hop_fused(inc, Xs, P=scale, Q=scale, out_scale=1 - self.alpha,
