@@ -9,6 +9,8 @@ training loops (paths relative to /root/reference/HD_SELFRec):
   ED-HNN encoder (``encoders.LocalAwareEncoderHD3``);
 * :class:`HGCN`     — model/graph/HGCN.py:15-164 (HGCNConv stack with per-layer
   TransformerEncoder self-attention);
+* :class:`HCCF_sharded` — HCCF's loop on user-row shards under torch.distributed (no reference
+  counterpart: the north_star's multi-GPU partition carried up to the plugin);
 * :class:`HCCF_diffusion` — model/graph/HCCF_diffusion.py:22-129 (HCCF's loop with the ED-HNN
   block on the learned hypergraph, ``encoders.HCCFDiffusionEncoder``);
 * :class:`DHCF`     — model/graph/DHCF.py:19-185 (HGCNConv on the interaction matrix, which
@@ -447,6 +449,132 @@ class HGCN(GraphRecommender):
         return score.cpu().numpy()
 
 
+class HCCF_sharded(HCCF):
+    """HCCF's training loop (HCCF.py:72-118) on user-row shards, one process per GPU under
+    ``torch.distributed`` (backend "nccl" = RCCL over xGMI). Not a reference model
+    name: the reference has no distributed code; this is the north_star's user-row partition
+    carried up to the plugin.
+
+    Every rank builds the data, runs the same sampler (same Python random state, so the same
+    global batch) and holds ``sharded_encoders.ShardedHCCFEncoder`` (its users' rows; items and
+    W replicated, broadcast from rank 0 at start). A step computes the reference's loss exactly:
+    the batch's anchor rows and the user rows the InfoNCE node list picks are assembled on every
+    rank by a differentiable all-reduce of each owner's rows, so every rank evaluates the same
+    full loss; its backward is scaled by 1/world, which makes the per-rank gradients of the
+    replicated parameters the partials that ``allreduce_replicated_grads`` sums (and the
+    all-reduce's backward gives each owner its rows' full gradient). Evaluation all-reduces the
+    user table once per epoch and runs the single-GPU device evaluation; rank 0 writes the
+    result files. With ``drop_rate`` 0 and the reference's CPU drop-edge stream it takes the
+    same steps as :class:`HCCF` on one GPU (``tests/test_gpu_plugins.py``)."""
+
+    def __init__(self, conf, training_set, test_set, knowledge_set, **kwargs):
+        import torch.distributed as dist
+        from .sharded import all_reduce_sum
+        from .sharded_encoders import ShardedHCCFEncoder, shard_bounds
+        if not dist.is_initialized():
+            raise RuntimeError("HCCF_sharded: torch.distributed is not initialised")
+        GraphRecommender.__init__(self, conf, training_set, test_set, knowledge_set, **kwargs)
+        self._dist, self._all_reduce_sum = dist, all_reduce_sum
+        self.world, self.rank = dist.get_world_size(), dist.get_rank()
+        self.is_main = self.rank == 0
+        self.u0, self.u1 = shard_bounds(self.data.n_users, self.world, self.rank)
+        self._parse_config(self.config, kwargs)
+        self.model = ShardedHCCFEncoder(kwargs, self.data, self.u0, self.u1, device=self.device,
+                                        device_rng=bool(kwargs.get('hgd_device_rng', False)),
+                                        seed=self.seed)
+        with torch.no_grad():  # replicated parameters start equal on every rank
+            for p in self.model.replicated_parameters():
+                dist.broadcast(p.data, 0)
+        self.optimizer = torch.optim.Adam(self.model.parameters(), lr=self.lRate)
+        self.scheduler = ReduceLROnPlateau(self.optimizer, 'min', factor=self.lr_decay,
+                                           patience=5)
+
+    def _rows(self, table_local: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
+        """table[ids] for GLOBAL user ids (negative ids wrap, as torch indexing) of a user table
+        sharded by rows: each owner contributes its rows, the rest zeros, summed over ranks."""
+        n = self.data.n_users
+        if self.u1 == self.u0:  # a rank without users contributes nothing
+            return self._all_reduce_sum(torch.zeros(ids.numel(), table_local.shape[1],
+                                                    device=ids.device))
+        g = torch.where(ids < 0, ids + n, ids)
+        own = (g >= self.u0) & (g < self.u1)
+        loc = (g - self.u0).clamp(0, max(self.u1 - self.u0 - 1, 0))
+        part = torch.where(own[:, None], table_local[loc], torch.zeros((), device=ids.device))
+        return self._all_reduce_sum(part)
+
+    def train_step(self, user_idx, pos_idx, neg_idx) -> torch.Tensor:
+        from .sharded import allreduce_replicated_grads
+        model = self.model
+        model.train()
+        nl = self.u1 - self.u0
+        user_emb, item_emb, gcnEmbedsLst, hyperEmbedsLst = model(keep_rate=1 - self.dropRate)
+        anchor_emb = self._rows(user_emb, user_idx)
+        pos_emb = item_emb[pos_idx]
+        neg_emb = item_emb[neg_idx]
+        bprLoss = bpr_loss(anchor_emb, pos_emb, neg_emb)
+        u_nodes, p_nodes = unique_long(anchor_emb), unique_long(pos_emb)
+        k = torch.arange(u_nodes.numel(), device=u_nodes.device)
+        sslLoss = 0
+        for i in range(self.nLayers):
+            e1, e2 = gcnEmbedsLst[i].detach(), hyperEmbedsLst[i]
+            sslLoss += contrast_loss(self._rows(e1[:nl], u_nodes), self._rows(e2[:nl], u_nodes),
+                                     k, self.temp) \
+                + contrast_loss(e1[nl:], e2[nl:], p_nodes, self.temp)
+        batch_loss = bprLoss + sslLoss * self.ss_rate
+        self.optimizer.zero_grad()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 4)  # before backward, as HCCF.py:95
+        (batch_loss / self.world).backward()
+        allreduce_replicated_grads(model.replicated_parameters())
+        self.optimizer.step()
+        return batch_loss
+
+    def _full_user_table(self, user_local: torch.Tensor) -> torch.Tensor:
+        full = torch.zeros(self.data.n_users, user_local.shape[1], device=user_local.device)
+        full[self.u0:self.u1] = user_local
+        self._dist.all_reduce(full)
+        return full
+
+    def train(self, load_pretrained=False):
+        model = self.model
+        recall_list, train_losses, lst_performances = [], [], []
+        for ep in range(self.maxEpoch):
+            s_train = time.time()
+            for batch in next_batch_pairwise(self.data, self.batchSize, device=self.device):
+                train_losses.append(self.train_step(*batch).item())
+            tr_time = time.time() - s_train
+            model.eval()
+            with torch.no_grad():
+                ue, self.item_emb, _, _ = model(keep_rate=1)
+                self.user_emb = self._full_user_table(ue)
+                cur_data, data_ep = self.fast_evaluation(ep, train_time=tr_time)
+                lst_performances.append(data_ep)
+                recall_list.append(float(cur_data[2].split(':')[1]))
+                _, should_stop = early_stopping(recall_list, self.early_stopping_steps)
+                if should_stop:
+                    break
+            self.scheduler.step(np.mean(train_losses))
+        self.save_perfomance_training(lst_performances)
+        self.user_emb, self.item_emb = self.best_user_emb, self.best_item_emb
+
+    def save(self):
+        with torch.no_grad():
+            ue, self.best_item_emb, _, _ = self.model(keep_rate=1)
+            self.best_user_emb = self._full_user_table(ue)
+            self.save_model(self.model)
+
+    def save_model(self, model):
+        if self.is_main:  # every rank holds its own user rows: rank 0 saves its shard's state
+            super().save_model(model)
+
+    def save_perfomance_training(self, log_train):
+        if self.is_main:
+            super().save_perfomance_training(log_train)
+
+    def evaluate(self, rec_list):
+        if self.is_main:
+            super().evaluate(rec_list)
+
+
 class HCCF_diffusion(HCCF):
     """model/graph/HCCF_diffusion.py:22-129: HCCF's constructor, losses and loop verbatim, with
     the encoder whose hypergraph hop is the ED-HNN block on the learned hypergraph."""
@@ -576,5 +704,5 @@ class DHCF(GraphRecommender):
         return score.cpu().numpy()
 
 
-PLUGINS = {"HCCF": HCCF, "HGNN_HD4": HGNN_HD4, "HGNN_HD3": HGNN_HD3, "HGCN": HGCN, "HCCF_diffusion": HCCF_diffusion,
+PLUGINS = {"HCCF": HCCF, "HCCF_sharded": HCCF_sharded, "HGNN_HD4": HGNN_HD4, "HGNN_HD3": HGNN_HD3, "HGCN": HGCN, "HCCF_diffusion": HCCF_diffusion,
            "DHCF": DHCF}
