@@ -11,6 +11,8 @@ training loops (paths relative to /root/reference/HD_SELFRec):
   TransformerEncoder self-attention);
 * :class:`HCCF_sharded` — HCCF's loop on user-row shards under torch.distributed (no reference
   counterpart: the north_star's multi-GPU partition carried up to the plugin);
+* :class:`HGNN_HD4_sharded` — HGNN_HD4 local_only on user-row shards (configs[3]'s
+  "hypergraph diffusion, user-row sharded");
 * :class:`HCCF_diffusion` — model/graph/HCCF_diffusion.py:22-129 (HCCF's loop with the ED-HNN
   block on the learned hypergraph, ``encoders.HCCFDiffusionEncoder``);
 * :class:`DHCF`     — model/graph/DHCF.py:19-185 (HGCNConv on the interaction matrix, which
@@ -449,7 +451,71 @@ class HGCN(GraphRecommender):
         return score.cpu().numpy()
 
 
-class HCCF_sharded(HCCF):
+class _ShardedPlugin:
+    """What the sharded plugins share: the rank's user range, global-id row assembly by
+    differentiable all-reduce, the full user table for evaluation, rank-0 file output."""
+
+    def _init_dist(self):
+        import torch.distributed as dist
+        from .sharded import all_reduce_sum
+        from .sharded_encoders import shard_bounds
+        if not dist.is_initialized():
+            raise RuntimeError(f"{type(self).__name__}: torch.distributed is not initialised")
+        self._dist, self._all_reduce_sum = dist, all_reduce_sum
+        self.world, self.rank = dist.get_world_size(), dist.get_rank()
+        self.is_main = self.rank == 0
+        self.u0, self.u1 = shard_bounds(self.data.n_users, self.world, self.rank)
+
+    def _rows(self, table_local: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
+        """table[ids] for GLOBAL user ids (negative ids wrap, as torch indexing) of a user table
+        sharded by rows: each owner contributes its rows, the rest zeros, summed over ranks."""
+        n = self.data.n_users
+        if self.u1 == self.u0:  # a rank without users contributes nothing
+            return self._all_reduce_sum(torch.zeros(ids.numel(), table_local.shape[1],
+                                                    device=ids.device))
+        g = torch.where(ids < 0, ids + n, ids)
+        own = (g >= self.u0) & (g < self.u1)
+        loc = (g - self.u0).clamp(0, max(self.u1 - self.u0 - 1, 0))
+        part = torch.where(own[:, None], table_local[loc], torch.zeros((), device=ids.device))
+        return self._all_reduce_sum(part)
+
+    def _full_user_table(self, user_local: torch.Tensor) -> torch.Tensor:
+        full = torch.zeros(self.data.n_users, user_local.shape[1], device=user_local.device)
+        full[self.u0:self.u1] = user_local
+        self._dist.all_reduce(full)
+        return full
+
+
+    def _backward_step(self, loss: torch.Tensor, replicated) -> None:
+        """Every rank holds the same full loss: backward of loss/world, then the replicated
+        parameters' partial gradients summed over ranks, then the optimizer step."""
+        from .sharded import allreduce_replicated_grads
+        (loss / self.world).backward()
+        allreduce_replicated_grads(replicated)
+        self.optimizer.step()
+
+    def save_model(self, model):
+        if self.is_main:  # every rank holds its own user rows: rank 0 saves its shard's state
+            super().save_model(model)
+
+    def save_perfomance_training(self, log_train):
+        if self.is_main:
+            super().save_perfomance_training(log_train)
+
+    def save_loss(self, *a, **k):
+        if self.is_main:
+            super().save_loss(*a, **k)
+
+    def evaluate(self, rec_list):
+        if self.is_main:
+            return super().evaluate(rec_list)
+        # the other ranks hold the same measures, without writing the files
+        from .evaluation import ranking_evaluation
+        _, ids, _ = self._device_eval()
+        self.result = ranking_evaluation(self._tests, ids, self.topN)
+
+
+class HCCF_sharded(_ShardedPlugin, HCCF):
     """HCCF's training loop (HCCF.py:72-118) on user-row shards, one process per GPU under
     ``torch.distributed`` (backend "nccl" = RCCL over xGMI). Not a reference model
     name: the reference has no distributed code; this is the north_star's user-row partition
@@ -468,16 +534,10 @@ class HCCF_sharded(HCCF):
     same steps as :class:`HCCF` on one GPU (``tests/test_gpu_plugins.py``)."""
 
     def __init__(self, conf, training_set, test_set, knowledge_set, **kwargs):
-        import torch.distributed as dist
-        from .sharded import all_reduce_sum
-        from .sharded_encoders import ShardedHCCFEncoder, shard_bounds
-        if not dist.is_initialized():
-            raise RuntimeError("HCCF_sharded: torch.distributed is not initialised")
+        from .sharded_encoders import ShardedHCCFEncoder
         GraphRecommender.__init__(self, conf, training_set, test_set, knowledge_set, **kwargs)
-        self._dist, self._all_reduce_sum = dist, all_reduce_sum
-        self.world, self.rank = dist.get_world_size(), dist.get_rank()
-        self.is_main = self.rank == 0
-        self.u0, self.u1 = shard_bounds(self.data.n_users, self.world, self.rank)
+        self._init_dist()
+        dist = self._dist
         self._parse_config(self.config, kwargs)
         self.model = ShardedHCCFEncoder(kwargs, self.data, self.u0, self.u1, device=self.device,
                                         device_rng=bool(kwargs.get('hgd_device_rng', False)),
@@ -489,21 +549,7 @@ class HCCF_sharded(HCCF):
         self.scheduler = ReduceLROnPlateau(self.optimizer, 'min', factor=self.lr_decay,
                                            patience=5)
 
-    def _rows(self, table_local: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
-        """table[ids] for GLOBAL user ids (negative ids wrap, as torch indexing) of a user table
-        sharded by rows: each owner contributes its rows, the rest zeros, summed over ranks."""
-        n = self.data.n_users
-        if self.u1 == self.u0:  # a rank without users contributes nothing
-            return self._all_reduce_sum(torch.zeros(ids.numel(), table_local.shape[1],
-                                                    device=ids.device))
-        g = torch.where(ids < 0, ids + n, ids)
-        own = (g >= self.u0) & (g < self.u1)
-        loc = (g - self.u0).clamp(0, max(self.u1 - self.u0 - 1, 0))
-        part = torch.where(own[:, None], table_local[loc], torch.zeros((), device=ids.device))
-        return self._all_reduce_sum(part)
-
     def train_step(self, user_idx, pos_idx, neg_idx) -> torch.Tensor:
-        from .sharded import allreduce_replicated_grads
         model = self.model
         model.train()
         nl = self.u1 - self.u0
@@ -523,16 +569,8 @@ class HCCF_sharded(HCCF):
         batch_loss = bprLoss + sslLoss * self.ss_rate
         self.optimizer.zero_grad()
         torch.nn.utils.clip_grad_norm_(model.parameters(), 4)  # before backward, as HCCF.py:95
-        (batch_loss / self.world).backward()
-        allreduce_replicated_grads(model.replicated_parameters())
-        self.optimizer.step()
+        self._backward_step(batch_loss, model.replicated_parameters())
         return batch_loss
-
-    def _full_user_table(self, user_local: torch.Tensor) -> torch.Tensor:
-        full = torch.zeros(self.data.n_users, user_local.shape[1], device=user_local.device)
-        full[self.u0:self.u1] = user_local
-        self._dist.all_reduce(full)
-        return full
 
     def train(self, load_pretrained=False):
         model = self.model
@@ -562,17 +600,121 @@ class HCCF_sharded(HCCF):
             self.best_user_emb = self._full_user_table(ue)
             self.save_model(self.model)
 
-    def save_model(self, model):
-        if self.is_main:  # every rank holds its own user rows: rank 0 saves its shard's state
-            super().save_model(model)
 
-    def save_perfomance_training(self, log_train):
-        if self.is_main:
-            super().save_perfomance_training(log_train)
+class ShardedHGNNModel(nn.Module):
+    """HGNNModel (HGNN_HD4.py:253-335, local encoder) on user-row shards: ``user_emb`` holds this
+    rank's rows, ``item_emb`` and every encoder weight are replicated."""
 
-    def evaluate(self, rec_list):
-        if self.is_main:
-            super().evaluate(rec_list)
+    def __init__(self, data, args, device, u0, u1, device_rng=False):
+        super().__init__()
+        from .sharded_encoders import ShardedLocalAwareEncoder
+        self.data = data
+        self.p = args['p']
+        self.drop_rate = args['drop_rate']
+        self.layers = args['n_layers']
+        self.emb_size = int(args['input_dim'])
+        self.hyper_size = int(args['hyper_dim'])
+        self.hyper_dim = int(args['hyper_dim'])
+        self.batchSize = int(args['batch_size'])
+        self.device_rng = device_rng
+        U, d = data.n_users, self.hyper_dim
+        bu = (6.0 / (U + d)) ** 0.5  # xavier_uniform_ bound of the GLOBAL [U, d] table
+        self.embedding_dict = nn.ParameterDict({
+            'user_emb': nn.Parameter(torch.empty(u1 - u0, d, device=device).uniform_(-bu, bu)),
+            'item_emb': nn.Parameter(nn.init.xavier_uniform_(
+                torch.empty(data.n_items, d)).to(device)),
+        })
+        self.hgnn_layer_local = ShardedLocalAwareEncoder(
+            data, self.emb_size, self.hyper_size, self.layers, self.p, self.drop_rate, u0, u1,
+            device=device)
+
+    def replicated_parameters(self):
+        return [self.embedding_dict['item_emb']] + list(self.hgnn_layer_local.parameters())
+
+    def forward(self, mode='local', keep_rate=1):
+        if mode != 'local':
+            raise NotImplementedError("only the local (ED-HNN) encoder is built")
+        ego = torch.cat([self.embedding_dict['user_emb'], self.embedding_dict['item_emb']], 0)
+        enc = self.hgnn_layer_local
+        return enc(ego, enc.dropped(keep_rate, self.device_rng))
+
+
+class HGNN_HD4_sharded(_ShardedPlugin, HGNN_HD4):
+    """HGNN_HD4 ``local_only`` (the ED-HNN "hypergraph diffusion" model; BASELINE configs[3]:
+    Amazon-Book, user-row sharded on the GPUs of one node) on user-row shards under
+    torch.distributed, with :class:`HCCF_sharded`'s scheme: same global batch on every rank,
+    anchor rows assembled by a differentiable all-reduce, the full BPR + L2 loss on every rank,
+    backward scaled by 1/world, replicated gradients (item table and every encoder weight)
+    summed. The loop keeps HGNN_HD4's quirks (scheduler step and ``eval()`` inside the batch
+    loop)."""
+
+    def __init__(self, conf, training_set, test_set, knowledge_set, **kwargs):
+        GraphRecommender.__init__(self, conf, training_set, test_set, knowledge_set, **kwargs)
+        self._parse_config(kwargs)
+        if self.mode != 'local_only':
+            raise NotImplementedError(f"{type(self).__name__} --mode={self.mode}: only "
+                                      "local_only is supported")
+        self._init_dist()
+        self.set_seed()
+        self.model = ShardedHGNNModel(self.data, kwargs, self.device, self.u0, self.u1,
+                                      bool(kwargs.get('hgd_device_rng', False)))
+        with torch.no_grad():
+            for p in self.model.replicated_parameters():
+                self._dist.broadcast(p.data, 0)
+        self.optimizer = torch.optim.Adam(self.model.parameters(), lr=self.lRate,
+                                          weight_decay=self.weight_decay)
+        self.scheduler = ReduceLROnPlateau(self.optimizer, 'min', factor=self.lr_decay,
+                                           patience=10)
+
+    def cf_loss(self, anchor_emb, pos_emb, neg_emb):  # HGNNModel.calculate_cf_loss (:324-328)
+        rec_loss = bpr_loss(anchor_emb, pos_emb, neg_emb)
+        reg_loss = l2_reg_loss(self.reg, anchor_emb, pos_emb, neg_emb) / self.model.batchSize
+        return rec_loss + reg_loss
+
+    def train_step(self, user_idx, pos_idx, neg_idx) -> torch.Tensor:
+        """One batch of HGNN_HD4.py:118-160 (local_only): BPR + L2 over the global batch."""
+        user_emb_lc, item_emb_lc = self.model(mode='local', keep_rate=1 - self.drop_rate)
+        anchor = self._rows(user_emb_lc, user_idx)
+        loss = self.cf_loss(anchor, item_emb_lc[pos_idx], item_emb_lc[neg_idx])
+        self.optimizer.zero_grad()
+        self._backward_step(loss, self.model.replicated_parameters())
+        return loss
+
+    def train(self, load_pretrained=False):  # HGNN_HD4.py:94-225, local_only
+        train_model = self.model
+        lst_train_losses, lst_cf_losses, lst_cl_losses = [], [], []
+        lst_performances, recall_list = [], []
+        for ep in range(self.maxEpoch):
+            cf_losses = []
+            train_model.train()
+            s_train = time.time()
+            for batch in next_batch_pairwise(self.data, self.batch_size, device=self.device):
+                cf_losses.append(self.train_step(*batch).item())
+                cf_loss = np.mean(cf_losses)
+                train_time = time.time() - s_train
+                lst_cf_losses.append([ep, cf_loss])
+                lst_train_losses.append([ep, cf_loss])
+                lst_cl_losses.append([ep, 0])
+                self.scheduler.step(cf_loss)
+                train_model.eval()
+            with torch.no_grad():
+                ue, self.item_emb = train_model(mode='local')
+                self.user_emb = self._full_user_table(ue)
+                cur_data, data_ep = self.fast_evaluation(ep, train_time=train_time)
+                lst_performances.append(data_ep)
+                recall_list.append(float(cur_data[2].split(':')[1]))
+                _, should_stop = early_stopping(recall_list, self.early_stopping_steps)
+                if should_stop:
+                    break
+        self.save_loss(lst_train_losses, lst_cf_losses, lst_cl_losses)
+        self.save_perfomance_training(lst_performances)
+        self.user_emb, self.item_emb = self.best_user_emb, self.best_item_emb
+
+    def save(self):
+        with torch.no_grad():
+            ue, self.best_item_emb = self.model.forward(mode='local')
+            self.best_user_emb = self._full_user_table(ue)
+            self.save_model(self.model)
 
 
 class HCCF_diffusion(HCCF):
@@ -704,5 +846,5 @@ class DHCF(GraphRecommender):
         return score.cpu().numpy()
 
 
-PLUGINS = {"HCCF": HCCF, "HCCF_sharded": HCCF_sharded, "HGNN_HD4": HGNN_HD4, "HGNN_HD3": HGNN_HD3, "HGCN": HGCN, "HCCF_diffusion": HCCF_diffusion,
+PLUGINS = {"HCCF": HCCF, "HCCF_sharded": HCCF_sharded, "HGNN_HD4_sharded": HGNN_HD4_sharded, "HGNN_HD4": HGNN_HD4, "HGNN_HD3": HGNN_HD3, "HGCN": HGCN, "HCCF_diffusion": HCCF_diffusion,
            "DHCF": DHCF}

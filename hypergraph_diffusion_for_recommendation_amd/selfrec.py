@@ -149,8 +149,7 @@ class FileIO:
 
     @staticmethod
     def write_file(dir, file, content, op='w'):
-        if not os.path.exists(dir):
-            os.makedirs(dir)
+        os.makedirs(dir, exist_ok=True)
         with open(dir + file, op) as f:
             f.writelines(content)
 
@@ -174,8 +173,7 @@ class Log:
     def __init__(self, module, filename):
         self.logger = logging.getLogger(module)
         self.logger.setLevel(level=logging.INFO)
-        if not os.path.exists('./log/'):
-            os.makedirs('./log/')
+        os.makedirs('./log/', exist_ok=True)
         handler = logging.FileHandler('./log/' + filename + '.log')
         handler.setFormatter(logging.Formatter(
             '%(asctime)s - %(name)s - %(levelname)s - %(message)s'))
@@ -387,8 +385,7 @@ class GraphRecommender(Recommender):
                        f"-wdecay:{kwargs['weight_decay']}-reg:{kwargs['reg']}-leaky:{kwargs['p']}"
                        f"-dropout:{kwargs['drop_rate']}-n_layers:{kwargs['n_layers']}"
                        f"-temp:{kwargs['temp']}-cl_rate:{kwargs['cl_rate']}")
-        if not os.path.exists(self.output):
-            os.makedirs(self.output)
+        os.makedirs(self.output, exist_ok=True)  # (ranks of a sharded plugin race here)
         self._tests: Optional[ev.TestLists] = None
         self._rated = None
 

@@ -239,6 +239,20 @@ class ShardedBipartite:
         sh.sel_b, sh.sel_c = sel_b, sel_c
         return sh
 
+    def transpose(self) -> "ShardedBipartite":
+        """Aᵀ = [[0, Cᵀ], [Bᵀ, 0]] on the same partition (B' = C_gᵀ, C' = B_gᵀ, sharing their
+        arrays); a symmetric A is its own transpose. Needed once A is edge-dropped: HGCNConv is
+        A·(Aᵀ·X) (HGNN_HD4.py:459)."""
+        if self.symmetric:
+            return self
+        t = getattr(self, "_t", None)
+        if t is None:
+            t = ShardedBipartite(_transposed(self.C), _transposed(self.B), group=self.group,
+                                 n_chunks=self.n_chunks)
+            t._t = self
+            self._t = t
+        return t
+
     # -- scales ------------------------------------------------------------------------------
     def scale(self, side: str, kind: Optional[str]) -> Optional[torch.Tensor]:
         """Global-degree row scale of the user ('user') or item ('item') rows of A."""
@@ -380,10 +394,10 @@ def sharded_gcn_hop(sh: ShardedBipartite, X_local: torch.Tensor) -> torch.Tensor
 
 def sharded_hgcn_conv(sh: ShardedBipartite, X_local: torch.Tensor, act: bool = True,
                       slope: float = 0.5) -> torch.Tensor:
-    """HGCNConv (``leaky(A·(Aᵀ·X))``, HGNN_HD4.py:450-462) on user-row shards of a symmetric A
-    (norm_adj: Aᵀ = A as a matrix, whichever order its blocks are stored in): two hops, the
+    """HGCNConv (``leaky(A·(Aᵀ·X))``, HGNN_HD4.py:450-462) on user-row shards: the Aᵀ hop, then
+    the A hop (for the symmetric norm_adj both are A; an edge-dropped A is not symmetric), the
     LeakyReLU after the second exchange (it is not linear)."""
-    Z = bipartite_hop(sh, bipartite_hop(sh, X_local))
+    Z = bipartite_hop(sh, bipartite_hop(sh.transpose(), X_local))
     if not act:
         return Z
     return _Epilogue.apply(Z, nat.EPI_LEAKY_RELU, float(slope))

@@ -131,8 +131,9 @@ class ShardedHCCFEncoder(nn.Module):
             seed = int(torch.randint(0, 2 ** 40, (1,)).item())  # same draw on every rank
             rank = torch.distributed.get_rank(self.group) if self.adj.world > 1 else 0
             return self.adj.drop_device(keep_rate, seed * 4096 + rank)
-        mask = ((torch.rand(self.nnz_global) + keep_rate).floor()).type(torch.bool)
-        return self.adj.drop_global(keep_rate, mask)
+        from .layers import torch_cpu_keep_mask  # the reference's torch.rand stream, natively
+        mask, _ = torch_cpu_keep_mask(self.nnz_global, keep_rate)
+        return self.adj.drop_global(keep_rate, mask.bool())
 
     def forward(self, keep_rate=0.5):
         nl = self.n_local
@@ -210,13 +211,30 @@ class ShardedLocalAwareEncoder(nn.Module):
             x = blk.act(conv.W(xv))
         return self._drop(blk.dropout, x)
 
+    def dropped(self, keep_rate: float, device_rng: bool = False) -> ShardedBipartite:
+        """The edge-dropped ``norm_adj`` shard (HGNN_HD4.py:304, SpAdjDropEdge): the reference's
+        global CPU ``torch.rand(nnz)`` mask (same draw on every rank, same bits as one GPU) or,
+        with ``device_rng``, per-rank device masks."""
+        if keep_rate == 1.0:
+            return self.norm
+        if device_rng:
+            seed = int(torch.randint(0, 2 ** 40, (1,)).item())  # same draw on every rank
+            rank = torch.distributed.get_rank(self.group) if self.norm.world > 1 else 0
+            return self.norm.drop_device(keep_rate, seed * 4096 + rank)
+        from .layers import torch_cpu_keep_mask
+        mask, _ = torch_cpu_keep_mask(int(self.data.norm_adj.nnz), keep_rate)
+        return self.norm.drop_global(keep_rate, mask.bool())
+
     def forward(self, ego_embeddings, sparse_norm_adj=None):
+        """``sparse_norm_adj``: None (the full ``norm_adj``) or a :meth:`dropped` shard, which the
+        last layer's HGCNConv uses as the reference's does (HGNN_HD4.py:399)."""
+        norm = sparse_norm_adj if isinstance(sparse_norm_adj, ShardedBipartite) else self.norm
         res = ego_embeddings
         for k in range(self.layers):
             if k != self.layers - 1:
                 ego_embeddings = self._edhnn(self.edhnn_layers[k], ego_embeddings) + res
             else:
-                z = sharded_hgcn_conv(self.norm, ego_embeddings, act=False)
+                z = sharded_hgcn_conv(norm, ego_embeddings, act=False)
                 ego_embeddings = layer_norm(z, self.lns[0]) + res
         nl = self.n_local
         return ego_embeddings[:nl], ego_embeddings[nl:]

@@ -294,3 +294,136 @@ def test_hccf_sharded_steps_match_single_gpu(dev, tmp_path, world):
     for rank, worst, perr in res:
         assert worst <= 1e-5, (rank, worst)
         assert perr <= 1e-5, (rank, perr)
+
+
+def _sharded_hd4_worker(rank, world, port, root, out_q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from hypergraph_diffusion_for_recommendation_amd.plugins import (HGNN_HD4,
+                                                                         HGNN_HD4_sharded)
+        from hypergraph_diffusion_for_recommendation_amd.sampler import next_batch_pairwise
+        from hypergraph_diffusion_for_recommendation_amd.selfrec import (FileIO, ModelConf,
+                                                                         default_args)
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        os.chdir(root)
+        conf = ModelConf(os.path.join(root, "HGNN_HD4.conf"))
+        kw = default_args(dataset='toy', max_epoch=1, batch_size=256, embedding_size=32,
+                          hyper_dim=32, input_dim=32, n_layers=3, item_ranking='10,20',
+                          drop_rate=0.2, p=0.3, reg=0.1, seed=7, mode='local_only',
+                          lrate=0.001, weight_decay=5e-6)
+        d = os.path.join(root, "dataset", "toy") + "/"
+        train, test = FileIO.load_data_set(d + "train.txt"), FileIO.load_data_set(d + "test.txt")
+        single = HGNN_HD4(conf, [list(r) for r in train], test, None, **kw)
+        sh = HGNN_HD4_sharded(conf, train, test, None, **kw)
+        with torch.no_grad():
+            es, er = sh.model.embedding_dict, single.model.embedding_dict
+            es['user_emb'].copy_(er['user_emb'][sh.u0:sh.u1])
+            es['item_emb'].copy_(er['item_emb'])
+        missing, _ = sh.model.hgnn_layer_local.load_state_dict(
+            single.model.hgnn_layer_local.state_dict(), strict=False)
+        assert not missing, missing
+        single.model.eval()
+        sh.model.eval()
+        # SGD instead of the plugins' Adam for the comparison: Adam's normalised update turns
+        # ULP-level differences of near-zero gradients into parameter differences of up to ~lr,
+        # while SGD keeps parameter differences proportional to gradient differences (Adam is
+        # elementwise, so the shards change nothing about it)
+        single.optimizer = torch.optim.SGD(single.model.parameters(), lr=0.05)
+        sh.optimizer = torch.optim.SGD(sh.model.parameters(), lr=0.05)
+        random.seed(11)
+        batches = list(next_batch_pairwise(single.data, 256, device=dev))[:3]
+        worst = 0.0
+        for k, (u, i, j) in enumerate(batches):
+            torch.manual_seed(100 + k)
+            ue, ie = single.model(mode='local', keep_rate=1 - single.drop_rate)
+            loss = single.model.calculate_cf_loss(ue[u], ie[i], ie[j], single.reg)
+            single.optimizer.zero_grad()
+            loss.backward()
+            single.optimizer.step()
+            torch.manual_seed(100 + k)
+            got = float(sh.train_step(u, i, j).detach())
+            worst = max(worst, abs(got - float(loss)) / abs(float(loss)))
+        es, er = sh.model.embedding_dict, single.model.embedding_dict
+        perr = max((es['user_emb'] - er['user_emb'][sh.u0:sh.u1]).abs().max().item(),
+                   (es['item_emb'] - er['item_emb']).abs().max().item())
+        rp = dict(single.model.hgnn_layer_local.named_parameters())
+        for name, p in sh.model.hgnn_layer_local.named_parameters():
+            perr = max(perr, (p - rp[name]).abs().max().item())
+        torch.cuda.synchronize()
+        dist.barrier()
+        out_q.put((rank, worst, perr))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_hgnn_hd4_sharded_steps_match_single_gpu(dev, tmp_path, world):
+    """HGNN_HD4_sharded (the ED-HNN model on user-row shards; gloo between processes sharing
+    cuda:0) takes the same three steps as HGNN_HD4 on one GPU from the same weights and batches
+    with the same CPU drop-edge masks, eval mode (dropout off): batch losses within 1e-5
+    relative, embeddings and every encoder weight within 1e-5 after three SGD steps (see the
+    worker for why SGD)."""
+    import socket
+
+    import torch.multiprocessing as mp
+    _write_dataset(str(tmp_path / "dataset"))
+    (tmp_path / "HGNN_HD4.conf").write_text(HCCF_CONF.format(model="HGNN_HD4"))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    mp.start_processes(_sharded_hd4_worker, args=(world, port, str(tmp_path), q), nprocs=world,
+                       join=True, start_method="spawn")
+    for rank, worst, perr in sorted(q.get() for _ in range(world)):
+        assert worst <= 1e-5, (rank, worst)
+        assert perr <= 1e-5, (rank, perr)
+
+
+def _sharded_execute_worker(rank, world, port, root, model, out_q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from hypergraph_diffusion_for_recommendation_amd.selfrec import (ModelConf, SELFRec,
+                                                                         default_args)
+        torch.cuda.set_device(0)
+        os.chdir(root)
+        conf = ModelConf(os.path.join(root, f"{model}.conf"))
+        kw = default_args(dataset='toy', max_epoch=2, batch_size=512, embedding_size=32,
+                          hyper_dim=32, input_dim=32, n_layers=2, item_ranking='10,20',
+                          drop_rate=0.2, p=0.3, temp=0.2, cl_rate=1e-3, reg=0.01, seed=7,
+                          mode='local_only')
+        kw['dataset_root'] = os.path.join(root, "dataset")
+        random.seed(3)
+        torch.manual_seed(3)
+        rec = SELFRec(conf, kw).execute()
+        out_q.put((rank, rec.result, os.path.exists(rec.output + f"/{model}-performance.txt")))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("model", ["HCCF_sharded", "HGNN_HD4_sharded"])
+def test_sharded_plugins_execute(dev, tmp_path, model):
+    """SELFRec(conf, kwargs).execute() of a sharded plugin at 2 ranks: both ranks end with the
+    same measures (their evaluation all-reduces the user table), rank 0 writes the files."""
+    import socket
+
+    import torch.multiprocessing as mp
+    _write_dataset(str(tmp_path / "dataset"))
+    (tmp_path / f"{model}.conf").write_text(HCCF_CONF.format(model=model))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    q = mp.get_context("spawn").Queue()
+    mp.start_processes(_sharded_execute_worker, args=(2, port, str(tmp_path), model, q),
+                       nprocs=2, join=True, start_method="spawn")
+    res = sorted(q.get() for _ in range(2))
+    assert res[0][1] == res[1][1] and len(res[0][1]) == 10
+    assert res[0][2]
