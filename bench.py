@@ -250,9 +250,10 @@ def main():
     # one rank per GPU; the modulo only matters for rehearsing N ranks on fewer GPUs (gloo)
     dev_index = local_rank % max(1, torch.cuda.device_count())
     device = torch.device(f"cuda:{dev_index}")
+    dist_backend = None
     if world > 1:
         torch.cuda.set_device(device)
-        backend = os.environ.get("HGD_DIST_BACKEND", "nccl")  # nccl == RCCL on ROCm
+        backend = dist_backend = os.environ.get("HGD_DIST_BACKEND", "nccl")  # nccl == RCCL
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=device)
         else:
@@ -395,8 +396,10 @@ def main():
             "users_per_gpu": U, "items": I, "edges_per_gpu_requested": E,
             "edges_per_gpu": nnz, "emb_dim": d,
             "op": "hgconv2 fwd+bwd: D_v^-1/2 H D_e^-1 H^T D_v^-1/2 X, 4 hgd_spmm hops",
-            "parallelism": (f"user-row shards x{world}, RCCL all-reduce of item sums "
-                            f"({args.chunks} chunks)" if world > 1 else "single GPU"),
+            "parallelism": (f"user-row shards x{world}, "
+                            f"{'RCCL' if dist_backend == 'nccl' else dist_backend} all-reduce "
+                            f"of item sums ({args.chunks} chunks)" if world > 1
+                            else "single GPU"),
             "hip_graph": use_graph,
         },
         "roofline": roofline,
