@@ -1,0 +1,149 @@
+#!/usr/bin/env python3
+"""One HCCF_diffusion training step (model/graph/HCCF_diffusion.py: HCCF's loop with the ED-HNN
+block on the learned hypergraph dropout(E·W) [n, K]) at the Yelp2018 shape of BASELINE
+configs[2] (31,668 × 38,048, 1.24 M interactions, 3 layers, d = 64, K = 32, batch 4096):
+forward, BPR + per-layer InfoNCE, backward, Adam — the repo's "hypergraph diffusion" carrier.
+
+* hgd_device_mask — encoders.HCCFDiffusionEncoder: GCN hop and drop-edge on libhgd, the learned
+                    hypergraph's V/E by hgd_dense_threshold_* and both scatter-means as one fused
+                    two-hop, MFMA Linear / LayerNorm kernels, fused InfoNCE;
+* reference_ops   — the same step with the reference's torch calls on the same GPU and the same
+                    parameters: torch.sparse.mm, torch.nonzero(H > 0), the scatter-mean pair
+                    (torch_scatter's mean as index_reduce_, pytorch-scatter being absent),
+                    F.layer_norm / F.linear, torch.unique, contrastLoss.
+
+Prints one JSON line per variant (event-timed median of --reps steps)."""
+import argparse
+import json
+import os
+import statistics
+import sys
+import types
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--users", type=int, default=31_668)
+    ap.add_argument("--items", type=int, default=38_048)
+    ap.add_argument("--edges", type=int, default=1_237_259)
+    ap.add_argument("--dim", type=int, default=64)
+    ap.add_argument("--layers", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--variants", default="hgd_device_mask,reference_ops")
+    args = ap.parse_args()
+    import torch
+    import torch.nn.functional as F
+
+    import refops as R
+    from hypergraph_diffusion_for_recommendation_amd.encoders import HCCFDiffusionEncoder
+    from hypergraph_diffusion_for_recommendation_amd.functional import contrast_loss, unique_long
+
+    dev = torch.device("cuda")
+    nu, ni, d, L = args.users, args.items, args.dim, args.layers
+    u, i = R.synthetic_incidence(nu, ni, args.edges, seed=0)
+    A = R.normalize_graph_mat(R.bipartite_adjacency(u, i, nu, ni))
+    data = types.SimpleNamespace(n_users=nu, n_items=ni, norm_adj=A)
+    conf = dict(lrate=0.001, lr_decay=0.7, max_epoch=1, batch_size=args.batch, reg=0.1,
+                embedding_size=d, hyper_dim=32, drop_rate=0.5, p=0.1, n_layers=L)
+    temp, cl_rate, keep = 0.2, 1e-4, 0.5
+    g = torch.Generator(device=dev).manual_seed(0)
+    batches = [(torch.randint(0, nu, (args.batch,), device=dev, generator=g),
+                torch.randint(0, ni, (args.batch,), device=dev, generator=g),
+                torch.randint(0, ni, (args.batch,), device=dev, generator=g)) for _ in range(8)]
+    torch.manual_seed(0)
+    model = HCCFDiffusionEncoder(conf, data, dev)
+    model.edgeDropper.device_rng = True
+    adj = model.sparse_norm_adj.detach().clone().coalesce()
+    K = model.n_edges
+    blk = model.edhnnlayer
+
+    def ref_edhnn(x, H, n_nodes):
+        """EquivSetGNN + EquivSetConv (layers2, HCCF_diffusion.py:250-402) with torch ops."""
+        nz = torch.nonzero(H > 0)
+        V, E = nz[:, 0], nz[:, 1] + n_nodes
+        x = blk.dropout(x)
+        x = F.relu(F.linear(x, blk.lin_in.weight, blk.lin_in.bias))
+        x = blk.dropout(x)
+        xve = x[V]
+        xe = torch.zeros(int(E.max()) + 1, x.shape[1], device=x.device).index_reduce_(
+            0, E, xve, "mean", include_self=False)
+        xv = torch.zeros_like(x).index_reduce_(0, V, xe[E], "mean", include_self=False)
+        mlp = blk.conv.W
+        ln, lin = mlp.normalizations[0], mlp.lins[0]
+        h = F.layer_norm(xv, (xv.shape[1],), ln.weight, ln.bias, ln.eps)
+        x = F.relu(F.linear(h, lin.weight, lin.bias))
+        return blk.dropout(x)
+
+    def ref_forward(keep_rate):
+        e = model.embedding_dict
+        hidden = [torch.cat([e['user_emb'], e['item_emb']], 0)]
+        gcn_l, hyp_l = [], []
+        huu, hii = e['user_emb'] @ e['user_w'], e['item_emb'] @ e['item_w']
+        for _ in range(L):
+            gcn = torch.sparse.mm(R.sp_adj_drop_edge(adj, keep_rate), hidden[-1])
+            hu = ref_edhnn(hidden[-1][:nu], model.drop_out(huu), nu + K)
+            hi = ref_edhnn(hidden[-1][nu:], model.drop_out(hii), ni + K)
+            gcn_l.append(gcn)
+            hyp_l.append(torch.cat([hu, hi], 0))
+            hidden.append(gcn + hyp_l[-1])
+        emb = sum(hidden)
+        return emb[:nu], emb[nu:], gcn_l, hyp_l
+
+    def make_step(fwd, loss_fn, unique, hoist):
+        opt = torch.optim.Adam(model.parameters(), lr=conf["lrate"])
+        state = {"k": 0}
+
+        def step():
+            uid, pid, nid = batches[state["k"] % len(batches)]
+            state["k"] += 1
+            ue, ie, gcn, hyp = fwd(keep)
+            anc, pos, neg = ue[uid], ie[pid], ie[nid]
+            un = (unique(anc), unique(pos)) if hoist else None
+            ssl = 0
+            for layer in range(L):
+                e1, e2 = gcn[layer].detach(), hyp[layer]
+                a_n, p_n = un if hoist else (unique(anc), unique(pos))
+                ssl = ssl + loss_fn(e1[:nu], e2[:nu], a_n, temp) + loss_fn(e1[nu:], e2[nu:],
+                                                                           p_n, temp)
+            loss = R.bpr_loss(anc, pos, neg) + cl_rate * ssl
+            opt.zero_grad()
+            torch.nn.utils.clip_grad_norm_(model.parameters(), 4)  # before backward, as HCCF
+            loss.backward()
+            opt.step()
+        return step
+
+    def timed(step):
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(args.reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            step()
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        return statistics.median(ts)
+
+    model.train()
+    want = args.variants.split(",")
+    out = []
+    if "hgd_device_mask" in want:
+        out.append(("hgd_device_mask", timed(make_step(model, contrast_loss, unique_long,
+                                                       True))))
+    if "reference_ops" in want:
+        out.append(("reference_ops", timed(make_step(
+            ref_forward, R.contrast_loss, lambda t: torch.unique(t.long()), False))))
+    for name, ms in out:
+        print(json.dumps({"variant": name, "ms_per_step": round(ms, 3), "users": nu,
+                          "items": ni, "edges": len(u), "d": d, "layers": L,
+                          "batch": args.batch}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
