@@ -304,21 +304,28 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    # roofline: HIP events around every hop launch on its stream, recorded inside the timed
+    # region (two event records per hop, a few µs on a ~16 ms step); a captured graph cannot
+    # record them, so with --graph on the same steps are re-run eagerly afterwards for them
+    timer = profiling.HopTimer()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    if use_graph:
+        for _ in range(args.steps):
+            step()
+    else:
+        with timer:
+            for _ in range(args.steps):
+                step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    # roofline pass: the same steps again, eager, with HIP events around every hop launch on
-    # its stream (kept out of the timed loop above so the events cannot inflate ms_per_step)
-    timer = profiling.HopTimer()
-    with timer:
-        for _ in range(args.steps):
-            eager_step()
-    torch.cuda.synchronize()
+    if use_graph:
+        with timer:
+            for _ in range(args.steps):
+                eager_step()
+        torch.cuda.synchronize()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
