@@ -9,6 +9,10 @@ encoder (paths relative to /root/reference/HD_SELFRec):
 * :class:`LocalAwareEncoder` model/graph/HGNN_HD4.py:336-405 (``--mode=local_only``)
 * :class:`LocalAwareEncoderHD3` model/graph/HGNN_HD3.py:352-427 (the SpMM-form ED-HNN blocks)
 * :class:`HCCFDiffusionEncoder` model/graph/HCCF_diffusion.py:131-215
+* :class:`SelfAwareEncoder`  model/graph/HGNN_cp.py:368-411, KHGRec.py:374-417 (the KG
+  carriers' CF side)
+* :class:`RelationalAwareEncoder` model/graph/HGNN_cp.py:413-446 (their KG side)
+* :class:`SelfAwareEncoderHD` model/graph/HD.py:398-487 (ED-HNN blocks on the norm_adj pattern)
 
 Everything sparse runs on libhgd, with the LayerNorm / residual after a hop fused into its store;
 HCCF's dense ``E·W`` and learned-hypergraph products run on the skinny MFMA kernels; dropout
@@ -241,5 +245,148 @@ class LocalAwareEncoderHD3(nn.Module):
             else:
                 ego_embeddings = two_hop_fused(incidence_of(self.sparse_norm_adj), ego_embeddings,
                                                norm=self.lns[k], res1=res, res1_scale=1.0)
+        nu = self.data.n_users
+        return ego_embeddings[:nu], ego_embeddings[nu:]
+
+
+def ugformer_layers(hyper_size, n_layers, drop_rate, device=None) -> nn.ModuleList:
+    """The per-layer UGformer blocks of the KG carriers' SelfAwareEncoder (HGNN_cp.py:387-392,
+    HD.py:453-459): ``TransformerEncoder(TransformerEncoderLayer(d, nhead=1, ff=32), 1,
+    norm=LayerNorm(d))`` over all nodes as one sequence. Self-attention over n nodes is the
+    library's dense O(n²) attention, not a hop of the path; it runs only with ``use_self_att``."""
+    return nn.ModuleList([
+        nn.TransformerEncoder(nn.TransformerEncoderLayer(d_model=hyper_size, nhead=1,
+                                                         dim_feedforward=32, dropout=drop_rate),
+                              1, norm=nn.LayerNorm(hyper_size), enable_nested_tensor=False)
+        .to(device) for _ in range(n_layers)])
+
+
+def _self_attend(block, x):
+    # [seq = n nodes, batch = 1, d], the reference's unsqueeze / squeeze (HGNN_cp.py:400-402)
+    return block(x.unsqueeze(1)).squeeze(1)
+
+
+def _hgcn_ln_res_stack(inc, x, lns, slope, res, attend=None):
+    """``lns[k](HGCNConv(A, x)) + res`` per layer, no activation on the last (HGNN_cp.py:403-406,
+    :428-433): one fused two-hop per layer whose store applies the LeakyReLU, the LayerNorm
+    and the residual; ``attend[k]`` (the UGformer blocks) first when given."""
+    L = len(lns)
+    for k in range(L):
+        if attend is not None:
+            x = _self_attend(attend[k], x)
+        x = two_hop_fused(inc, x, epilogue=None if k == L - 1 else "leaky_relu", slope=slope,
+                          norm=lns[k], res1=res, res1_scale=1.0)
+    return x
+
+
+class SelfAwareEncoder(nn.Module):
+    """The CF encoder of the KG carriers HGNN_cp / KHGRec (HGNN_cp.py:368-411, KHGRec.py:374-
+    417): per layer ``lns[k](HGCNConv(Â, x)) + res`` with HGCNConv = LeakyReLU(Â·Âᵀ·x) (no
+    activation on the last layer) over the edge-dropped ``norm_adj`` the model passes in.
+    ``use_self_att`` (HGNN_cp's default True; KHGRec forces False) runs the UGformer block
+    before each layer's hop."""
+
+    def __init__(self, data, emb_size, hyper_size, n_layers, leaky, drop_rate, device=None,
+                 use_self_att=True):
+        super().__init__()
+        self.data = data
+        self.latent_size = emb_size
+        self.hyper_size = hyper_size
+        self.layers = n_layers
+        self.norm_adj = data.norm_adj
+        self.device = torch.device(device) if device is not None else torch.device("cuda")
+        self.relu = nn.ReLU()
+        self.leaky = float(leaky)
+        self.act = nn.LeakyReLU(leaky)
+        self.dropout = nn.Dropout(drop_rate)
+        self.edgeDropper = SpAdjDropEdge()
+        self.use_self_att = use_self_att
+        self.hgnn_layers = nn.ModuleList()
+        self.ugformer_layers = nn.ModuleList()
+        self.lns = nn.ModuleList()
+        for _ in range(n_layers):  # the reference's construction (and init) order
+            self.ugformer_layers.extend(ugformer_layers(hyper_size, 1, drop_rate))
+            self.hgnn_layers.append(HGCNConv(leaky=leaky))
+            self.lns.append(LayerNorm(hyper_size))
+        self.to(self.device)
+
+    def forward(self, ego_embeddings, sparse_norm_adj):
+        inc = incidence_of(sparse_norm_adj)
+        attend = self.ugformer_layers if self.use_self_att else None
+        ego_embeddings = _hgcn_ln_res_stack(inc, ego_embeddings, list(self.lns), self.leaky,
+                                            ego_embeddings, attend)
+        nu = self.data.n_users
+        return ego_embeddings[:nu], ego_embeddings[nu:]
+
+
+class RelationalAwareEncoder(nn.Module):
+    """HGNN_cp's KG encoder (HGNN_cp.py:413-446): the same ``lns[i](HGCNConv(A, x)) + res``
+    stack over the (edge-dropped) KG adjacency; its AttHGCNConv ignores ``att_adj`` (``adj =
+    inp_adj``, :440-446), as here. (KHGRec's variant multiplies ``att_adj·inp_adj`` first,
+    KHGRec.py:445-449 — a KG-attention SpGEMM outside the path.)"""
+
+    def __init__(self, leaky, dropout, n_layers, hyper_dim):
+        super().__init__()
+        self.leaky = leaky
+        self.dropout = dropout
+        self.n_layers = n_layers
+        self.act = nn.LeakyReLU(self.leaky)
+        self.convs = nn.ModuleList()
+        self.lns = nn.ModuleList()
+        for _ in range(n_layers):
+            self.convs.append(HGCNConv(leaky=leaky))
+            self.lns.append(LayerNorm(hyper_dim))
+
+    def forward(self, embs, sparse_adj, att_adj=None):
+        return _hgcn_ln_res_stack(incidence_of(sparse_adj), embs, list(self.lns),
+                                  float(self.leaky), embs)
+
+
+class SelfAwareEncoderHD(nn.Module):
+    """HD's CF encoder (HD.py:398-487): two ED-HNN blocks (layers2 EquivSetGNN, mean
+    aggregation, edhnn_config) on V/E = nonzero(norm_adj > 0) of the UN-dropped ``norm_adj`` —
+    ``edhnn_layers[0]`` for layers 0..L-2, ``edhnn_layers[1]`` for the last, each plus the layer-0
+    residual; the ``sparse_norm_adj`` argument of ``forward`` is ignored, as in the reference.
+    Each block's aggregation is one fused mean two-hop over the adjacency pattern.
+    ``use_self_att`` (default False) runs the UGformer block first. The dense ``ui_adj`` copies
+    the reference builds (``hyper_uu`` / ``hyper_ii`` / ``dense_hypergraph``, :447-450) are never
+    read by its forward and are not built."""
+
+    def __init__(self, data, emb_size, hyper_size, n_layers, leaky, drop_rate, device=None,
+                 use_self_att=False):
+        super().__init__()
+        self.data = data
+        self.latent_size = emb_size
+        self.hyper_size = hyper_size
+        self.layers = n_layers
+        self.norm_adj = data.norm_adj
+        self.device = torch.device(device) if device is not None else torch.device("cuda")
+        self.relu = nn.ReLU()
+        self.act = nn.LeakyReLU(leaky)
+        self.dropout = nn.Dropout(drop_rate)
+        self.edgeDropper = SpAdjDropEdge()
+        self.drop_out = nn.Dropout(drop_rate)
+        self.sparse_norm_adj = sparse_tensor_of(data.norm_adj, self.device)
+        self.use_self_att = use_self_att
+        self.edhnn_args = edhnn_config(hyper_size)
+        self.edhnn_layers = nn.ModuleList([
+            EquivSetGNN(hyper_size, self.edhnn_args, None, data) for _ in range(2)])
+        self.ugformer_layers = nn.ModuleList()
+        self.lns = nn.ModuleList()
+        for _ in range(n_layers):
+            self.ugformer_layers.extend(ugformer_layers(hyper_size, 1, drop_rate))
+            self.lns.append(nn.LayerNorm(hyper_size))
+        self.edhnn_user_n = data.n_users
+        self.edhnn_item_n = data.n_items
+        self.edhnn_ui_n = data.n_items + data.n_users
+        self.to(self.device)
+
+    def forward(self, ego_embeddings, sparse_norm_adj=None):
+        res = ego_embeddings
+        for k in range(self.layers):
+            if self.use_self_att:
+                ego_embeddings = _self_attend(self.ugformer_layers[k], ego_embeddings)
+            blk = self.edhnn_layers[0 if k != self.layers - 1 else 1]
+            ego_embeddings = blk(ego_embeddings, self.sparse_norm_adj, self.edhnn_ui_n) + res
         nu = self.data.n_users
         return ego_embeddings[:nu], ego_embeddings[nu:]
