@@ -605,9 +605,10 @@ class ShardedHGNNModel(nn.Module):
     """HGNNModel (HGNN_HD4.py:253-335, local encoder) on user-row shards: ``user_emb`` holds this
     rank's rows, ``item_emb`` and every encoder weight are replicated."""
 
-    def __init__(self, data, args, device, u0, u1, device_rng=False):
+    def __init__(self, data, args, device, u0, u1, device_rng=False, local_encoder=None):
         super().__init__()
         from .sharded_encoders import ShardedLocalAwareEncoder
+        local_encoder = local_encoder or ShardedLocalAwareEncoder
         self.data = data
         self.p = args['p']
         self.drop_rate = args['drop_rate']
@@ -624,7 +625,7 @@ class ShardedHGNNModel(nn.Module):
             'item_emb': nn.Parameter(nn.init.xavier_uniform_(
                 torch.empty(data.n_items, d)).to(device)),
         })
-        self.hgnn_layer_local = ShardedLocalAwareEncoder(
+        self.hgnn_layer_local = local_encoder(
             data, self.emb_size, self.hyper_size, self.layers, self.p, self.drop_rate, u0, u1,
             device=device)
 
@@ -657,7 +658,8 @@ class HGNN_HD4_sharded(_ShardedPlugin, HGNN_HD4):
         self._init_dist()
         self.set_seed()
         self.model = ShardedHGNNModel(self.data, kwargs, self.device, self.u0, self.u1,
-                                      bool(kwargs.get('hgd_device_rng', False)))
+                                      bool(kwargs.get('hgd_device_rng', False)),
+                                      self.sharded_encoder())
         with torch.no_grad():
             for p in self.model.replicated_parameters():
                 self._dist.broadcast(p.data, 0)
@@ -665,6 +667,11 @@ class HGNN_HD4_sharded(_ShardedPlugin, HGNN_HD4):
                                           weight_decay=self.weight_decay)
         self.scheduler = ReduceLROnPlateau(self.optimizer, 'min', factor=self.lr_decay,
                                            patience=10)
+
+    @staticmethod
+    def sharded_encoder():
+        from .sharded_encoders import ShardedLocalAwareEncoder
+        return ShardedLocalAwareEncoder
 
     def cf_loss(self, anchor_emb, pos_emb, neg_emb):  # HGNNModel.calculate_cf_loss (:324-328)
         rec_loss = bpr_loss(anchor_emb, pos_emb, neg_emb)
@@ -715,6 +722,22 @@ class HGNN_HD4_sharded(_ShardedPlugin, HGNN_HD4):
             ue, self.best_item_emb = self.model.forward(mode='local')
             self.best_user_emb = self._full_user_table(ue)
             self.save_model(self.model)
+
+
+class HGNN_HD3_sharded(HGNN_HD4_sharded):
+    """HGNN_HD3 ``local_only`` (HGNN_HD3.py:37-266: HGNN_HD4's loop around the SpMM-form ED-HNN
+    encoder) on user-row shards, with :class:`HGNN_HD4_sharded`'s scheme;
+    ``sharded_encoders.ShardedLocalAwareEncoderHD3`` runs its blocks' HGCNConv two-hops on the
+    edge-dropped ``norm_adj`` shard."""
+
+    @staticmethod
+    def sharded_encoder():
+        from .sharded_encoders import ShardedLocalAwareEncoderHD3
+        return ShardedLocalAwareEncoderHD3
+
+    def set_seed(self):  # HGNN_HD3.py:86-98
+        torch.cuda.manual_seed_all(self.seed)
+        super().set_seed()
 
 
 class HCCF_diffusion(HCCF):
@@ -846,5 +869,6 @@ class DHCF(GraphRecommender):
         return score.cpu().numpy()
 
 
-PLUGINS = {"HCCF": HCCF, "HCCF_sharded": HCCF_sharded, "HGNN_HD4_sharded": HGNN_HD4_sharded, "HGNN_HD4": HGNN_HD4, "HGNN_HD3": HGNN_HD3, "HGCN": HGCN, "HCCF_diffusion": HCCF_diffusion,
-           "DHCF": DHCF}
+PLUGINS = {"HCCF": HCCF, "HCCF_sharded": HCCF_sharded, "HGNN_HD4_sharded": HGNN_HD4_sharded,
+           "HGNN_HD3_sharded": HGNN_HD3_sharded, "HGNN_HD4": HGNN_HD4, "HGNN_HD3": HGNN_HD3,
+           "HGCN": HGCN, "HCCF_diffusion": HCCF_diffusion, "DHCF": DHCF}

@@ -27,7 +27,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .encoders import edhnn_config
-from .functional import dense_two_hop, layer_norm, linear
+from .functional import dense_two_hop, layer_norm, linear, row_epilogue
 from .layers import EquivSetGNN, LayerNorm
 from .sharded import (ShardedBipartite, bipartite_hop, sharded_dense_two_hop,
                       sharded_hgcn_conv, sharded_mean_two_hop)
@@ -236,5 +236,81 @@ class ShardedLocalAwareEncoder(nn.Module):
             else:
                 z = sharded_hgcn_conv(norm, ego_embeddings, act=False)
                 ego_embeddings = layer_norm(z, self.lns[0]) + res
+        nl = self.n_local
+        return ego_embeddings[:nl], ego_embeddings[nl:]
+
+
+class ShardedLocalAwareEncoderHD3(ShardedLocalAwareEncoder):
+    """LocalAwareEncoderHD3 (HGNN_HD3.py:352-427) on user-row shards, same submodules and
+    parameter names: layers 0..L-2 are the SpMM-form ED-HNN blocks (HGNN_HD3.py:555-720), whose
+    two aggregations are HGCNConv two-hops over the edge-dropped ``norm_adj`` shard
+    (:func:`sharded_hgcn_conv`, the LeakyReLU / LayerNorm / residual / restart blend in one
+    row-epilogue pass after the exchange); the last layer is ``lns[L-1](HGCNConv(Â, ·,
+    act=False)) + res`` on the un-dropped shard. Every layer adds the layer-0 residual."""
+
+    def __init__(self, data, emb_size, hyper_size, n_layers, leaky, drop_rate, u0: int, u1: int,
+                 group=None, device=None, n_chunks: int = 4, seed: int = 0):
+        nn.Module.__init__(self)
+        from .edhnn_spmm import EquivSetGNN as EquivSetGNNSpMM
+        from .layers import HGCNConv
+        self.data = data
+        self.latent_size = emb_size
+        self.hyper_size = hyper_size
+        self.layers = n_layers
+        self.u0, self.u1, self.n_local = int(u0), int(u1), int(u1) - int(u0)
+        self.device = torch.device(device) if device is not None else torch.device("cuda")
+        self.group = group
+        U, I = data.n_users, data.n_items
+        self.edhnn_args = edhnn_config(hyper_size)
+        self.hgcn_layer = HGCNConv(leaky=0.3)
+        self.hgnn_layers = nn.ModuleList([HGCNConv(leaky=0.3) for _ in range(n_layers)])
+        self.edhnn_layers = nn.ModuleList([
+            EquivSetGNNSpMM(hyper_size, self.edhnn_args, None, data, U, I, leaky=0.5)
+            for _ in range(n_layers)])
+        self.lns = nn.ModuleList([LayerNorm(hyper_size) for _ in range(n_layers)])
+        self.norm = ShardedBipartite.from_global(_coo_tensor(data.norm_adj), U, I, u0, u1,
+                                                 device=self.device, group=group,
+                                                 n_chunks=n_chunks)
+        self.rep_gen = torch.Generator(device=self.device).manual_seed(int(seed))
+        self._drops = {}
+        self.to(self.device)
+
+    def _edhnn_spmm(self, blk, x: torch.Tensor, sh: ShardedBipartite) -> torch.Tensor:
+        """edhnn_spmm.EquivSetGNN.forward (HGNN_HD3.py:680-720) with sharded hops."""
+        x = self._drop(blk.dropout, x)
+        x = blk.lin_in(x, relu=True)
+        x0 = x
+        conv = blk.conv
+        s0 = conv.hgcn_layers[0].act.negative_slope
+        s1 = conv.hgcn_layers[1].act.negative_slope
+        for _ in range(blk.nlayer):
+            x = self._drop(blk.dropout, x)
+            xve = conv.W1(x)
+            # Xe = LN0(leaky(A·(Aᵀ·Xve))) + Xve
+            xe = row_epilogue(sharded_hgcn_conv(sh, xve, act=False), epilogue="leaky_relu",
+                              slope=s0, norm=conv.lns[0], res1=xve)
+            xev = xe if conv.W2 is None else conv.W2(torch.cat([x, xe], -1))
+            if xev.shape[-1] != conv.out_features:
+                xev = conv.mean_pooling(xev)
+            # (1-α)·(LN1(leaky(A·(Aᵀ·Xev))) + Xev) + α·X0
+            a = conv.alpha
+            xv = row_epilogue(sharded_hgcn_conv(sh, xev, act=False), epilogue="leaky_relu",
+                              slope=s1, norm=conv.lns[1], out_scale=1 - a, res1=xev,
+                              res1_scale=1 - a, res2=x0 if a != 0 else None, res2_scale=a)
+            x = blk.act(conv.W(xv))
+        return self._drop(blk.dropout, x)
+
+    def forward(self, ego_embeddings, sparse_norm_adj=None):
+        """``sparse_norm_adj``: None (the full ``norm_adj``) or a :meth:`dropped` shard, which
+        the ED-HNN blocks use (HGNN_HD3.py:416-418); the last layer uses the full one (:420)."""
+        dropped = sparse_norm_adj if isinstance(sparse_norm_adj, ShardedBipartite) else self.norm
+        res = ego_embeddings
+        for k in range(self.layers):
+            if k != self.layers - 1:
+                ego_embeddings = self._edhnn_spmm(self.edhnn_layers[k], ego_embeddings,
+                                                  dropped) + res
+            else:
+                z = sharded_hgcn_conv(self.norm, ego_embeddings, act=False)
+                ego_embeddings = row_epilogue(z, norm=self.lns[k], res1=res)
         nl = self.n_local
         return ego_embeddings[:nl], ego_embeddings[nl:]

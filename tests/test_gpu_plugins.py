@@ -296,13 +296,12 @@ def test_hccf_sharded_steps_match_single_gpu(dev, tmp_path, world):
         assert perr <= 1e-5, (rank, perr)
 
 
-def _sharded_hd4_worker(rank, world, port, root, out_q):
+def _sharded_hd4_worker(rank, world, port, root, out_q, base="HGNN_HD4"):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from hypergraph_diffusion_for_recommendation_amd.plugins import (HGNN_HD4,
-                                                                         HGNN_HD4_sharded)
+        from hypergraph_diffusion_for_recommendation_amd.plugins import PLUGINS
         from hypergraph_diffusion_for_recommendation_amd.sampler import next_batch_pairwise
         from hypergraph_diffusion_for_recommendation_amd.selfrec import (FileIO, ModelConf,
                                                                          default_args)
@@ -316,8 +315,8 @@ def _sharded_hd4_worker(rank, world, port, root, out_q):
                           lrate=0.001, weight_decay=5e-6)
         d = os.path.join(root, "dataset", "toy") + "/"
         train, test = FileIO.load_data_set(d + "train.txt"), FileIO.load_data_set(d + "test.txt")
-        single = HGNN_HD4(conf, [list(r) for r in train], test, None, **kw)
-        sh = HGNN_HD4_sharded(conf, train, test, None, **kw)
+        single = PLUGINS[base](conf, [list(r) for r in train], test, None, **kw)
+        sh = PLUGINS[base + "_sharded"](conf, train, test, None, **kw)
         with torch.no_grad():
             es, er = sh.model.embedding_dict, single.model.embedding_dict
             es['user_emb'].copy_(er['user_emb'][sh.u0:sh.u1])
@@ -359,13 +358,13 @@ def _sharded_hd4_worker(rank, world, port, root, out_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_hgnn_hd4_sharded_steps_match_single_gpu(dev, tmp_path, world):
-    """HGNN_HD4_sharded (the ED-HNN model on user-row shards; gloo between processes sharing
-    cuda:0) takes the same three steps as HGNN_HD4 on one GPU from the same weights and batches
-    with the same CPU drop-edge masks, eval mode (dropout off): batch losses within 1e-5
-    relative, embeddings and every encoder weight within 1e-5 after three SGD steps (see the
-    worker for why SGD)."""
+@pytest.mark.parametrize("world,base", [(2, "HGNN_HD4"), (3, "HGNN_HD4"), (2, "HGNN_HD3")])
+def test_hgnn_hd4_sharded_steps_match_single_gpu(dev, tmp_path, world, base):
+    """HGNN_HD4_sharded / HGNN_HD3_sharded (the ED-HNN models on user-row shards; gloo between
+    processes sharing cuda:0) take the same three steps as HGNN_HD4 / HGNN_HD3 on one GPU from
+    the same weights and batches with the same CPU drop-edge masks, eval mode (dropout off):
+    batch losses within 1e-5 relative, embeddings and every encoder weight within 1e-5 after
+    three SGD steps (see the worker for why SGD)."""
     import socket
 
     import torch.multiprocessing as mp
@@ -377,7 +376,8 @@ def test_hgnn_hd4_sharded_steps_match_single_gpu(dev, tmp_path, world):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    mp.start_processes(_sharded_hd4_worker, args=(world, port, str(tmp_path), q), nprocs=world,
+    mp.start_processes(_sharded_hd4_worker, args=(world, port, str(tmp_path), q, base),
+                       nprocs=world,
                        join=True, start_method="spawn")
     for rank, worst, perr in sorted(q.get() for _ in range(world)):
         assert worst <= 1e-5, (rank, worst)
@@ -408,7 +408,8 @@ def _sharded_execute_worker(rank, world, port, root, model, out_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("model", ["HCCF_sharded", "HGNN_HD4_sharded"])
+@pytest.mark.parametrize("model", ["HCCF_sharded", "HGNN_HD4_sharded",
+                                   "HGNN_HD3_sharded"])
 def test_sharded_plugins_execute(dev, tmp_path, model):
     """SELFRec(conf, kwargs).execute() of a sharded plugin at 2 ranks: both ranks end with the
     same measures (their evaluation all-reduces the user table), rank 0 writes the files."""
