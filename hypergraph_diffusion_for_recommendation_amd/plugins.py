@@ -464,7 +464,9 @@ class _ShardedPlugin:
         self._dist, self._all_reduce_sum = dist, all_reduce_sum
         self.world, self.rank = dist.get_world_size(), dist.get_rank()
         self.is_main = self.rank == 0
-        self.u0, self.u1 = shard_bounds(self.data.n_users, self.world, self.rank)
+        # degree-balanced contiguous user ranges (every rank derives the same cuts from the data)
+        deg = np.diff(self.data.interaction_mat.tocsr().indptr)
+        self.u0, self.u1 = shard_bounds(self.data.n_users, self.world, self.rank, deg)
 
     def _rows(self, table_local: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
         """table[ids] for GLOBAL user ids (negative ids wrap, as torch indexing) of a user table

@@ -33,10 +33,31 @@ from .sharded import (ShardedBipartite, bipartite_hop, sharded_dense_two_hop,
                       sharded_hgcn_conv, sharded_mean_two_hop)
 
 
-def shard_bounds(n_users: int, world: int, rank: int):
-    """Contiguous user range of ``rank`` (sizes differ by at most one)."""
-    cuts = np.linspace(0, n_users, world + 1).astype(np.int64)
-    return int(cuts[rank]), int(cuts[rank + 1])
+def shard_bounds(n_users: int, world: int, rank: int, degrees=None):
+    """Contiguous user range of ``rank``. Without ``degrees``: sizes differ by at most one. With
+    the users' interaction counts: degree-balanced ranges — cut ``r`` is the first
+    user whose prefix count reaches r/world of the total (each hop's work and its
+    nonzero bytes on a rank are its users' nonzeros plus their rows), so every rank gets the same
+    share of nonzeros to within one user's degree. Cuts are non-decreasing; a rank may get no
+    users when a few users hold most interactions."""
+    if degrees is None:
+        cuts = np.linspace(0, n_users, world + 1).astype(np.int64)
+        return int(cuts[rank]), int(cuts[rank + 1])
+    deg = np.asarray(degrees, dtype=np.int64).reshape(-1)
+    if deg.shape[0] != n_users:
+        raise ValueError(f"shard_bounds: {deg.shape[0]} degrees for {n_users} users")
+    # weight = nonzeros + 1 (the row itself), so users without interactions still spread out
+    prefix = np.concatenate([[0], np.cumsum(deg + 1)])
+    total = int(prefix[-1])
+
+    def cut(r):
+        if r <= 0:
+            return 0
+        if r >= world:
+            return n_users
+        return int(np.searchsorted(prefix, (total * r + world - 1) // world, side="left"))
+
+    return cut(rank), cut(rank + 1)
 
 
 def _coo_tensor(mat, binary: bool = False):
