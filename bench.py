@@ -6,16 +6,24 @@ A step is one forward + backward of the HGNN-normalised 2-hop conv
 synthetic user×item incidence H, i.e. four hgd_spmm hops: CSC (into items) + CSR (into users)
 forward, the same pair backward. Unit of work = one nonzero of H.
 
-    python bench.py [--gpus N --steps K --warmup W --workload synthetic|ml1m|yelp|amazon|zipf]
+    python bench.py [--gpus N --steps K --warmup W --workload synthetic|zipf|ml1m|yelp|amazon
+                     --dim 64|256 --scaling strong|weak]
 
-N > 1 runs one process per GPU under torch.distributed.run (RCCL): every rank owns its own
-block of users (weak scaling: fixed users/edges per GPU, items shared) and the item sums are
-all-reduced over xGMI in each hop (hypergraph_diffusion_for_recommendation_amd/sharded.py).
+N > 1 runs one process per GPU (RCCL over xGMI). Launched without WORLD_SIZE in the environment,
+``--gpus N`` starts the N ranks itself (a child ``torch.distributed.run``, before this process
+touches the GPU) and exits with its status; under a launcher WORLD_SIZE must equal --gpus.
+
+* ``--scaling strong`` (default; BASELINE configs[4]): every rank builds the SAME global graph
+  (seed 0) and keeps its degree-balanced user range (sharded.shard_rows_of_sorted_coo); value =
+  global nonzeros × steps / max-over-ranks time. The item messages of every hop are all-reduced
+  over xGMI in column slices pipelined with the hops (sharded.py).
+* ``--scaling weak``: every rank owns its own full-size graph (seed = rank); value = Σ nonzeros.
 
 Rank 0 prints ONE JSON line. ``roofline`` prices the dominant kernel (hgd_spmm) from HIP events
-recorded around every hop launch on its stream during the timed steps; ``cpu_baseline`` times the
-reference's own library calls (torch.sparse.mm + autograd on CPU, oracle/ref_cpu.py) on a bounded
-sample of the same generator, on this box's host cores.
+recorded around every hop launch on its stream during the timed steps, with SURVEY.md §8d's
+algorithmic bytes; ``cpu_baseline`` times the reference's own library calls (torch.sparse.mm +
+autograd on CPU, oracle/ref_cpu.py) on a bounded sample of the same generator, on this box's
+host cores.
 """
 from __future__ import annotations
 
@@ -55,7 +63,17 @@ def parse():
     ap.add_argument("--users", type=int, default=None)
     ap.add_argument("--items", type=int, default=None)
     ap.add_argument("--edges", type=int, default=None)
-    ap.add_argument("--chunks", type=int, default=4, help="item chunks for the overlapped all-reduce")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="strong: one global graph sharded by user rows (default); weak: one "
+                         "full-size graph per rank")
+    ap.add_argument("--chunks", type=int, default=1,
+                    help="item-row chunks per exchanged column slice (N > 1)")
+    ap.add_argument("--slice-width", type=int, default=None,
+                    help="embedding columns per pipelined all-reduce block (N > 1; default 32 "
+                         "for d <= 128, else 64)")
+    ap.add_argument("--check", action="store_true",
+                    help="after timing, compare the sharded Y / dX with the single-GPU conv of "
+                         "the global graph (strong scaling) at the 1e-5 relative bound")
     ap.add_argument("--cpu-sample-edges", type=int, default=10_000_000)
     ap.add_argument("--cpu-budget-s", type=float, default=25.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -220,6 +238,42 @@ def copy_peak_gbps(device, n_bytes=1 << 30, reps=10):
     return max(rates.values()), rates
 
 
+def launch_ranks(args) -> int:
+    """Starts ``--gpus`` ranks of this script under torch.distributed.run as a CHILD process (no
+    exec: this process has not touched the GPU and never will) and returns its exit status."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def check_against_single_gpu(idx, U, I, X_global, dY_global, Y, dX, u0, u1):
+    """Strong scaling: this rank's sharded Y / dX rows against the single-GPU hgconv2 of the
+    global graph (functional.hgconv2, no exchange) at |err| <= 1e-5 · (the same conv of |X|)."""
+    import torch
+
+    from hypergraph_diffusion_for_recommendation_amd import Incidence, hgconv2
+    inc = Incidence.from_coo(idx, None, (U, I), validate=False, rows_sorted=True)
+    Xg = X_global.detach().clone().requires_grad_(True)
+    Yg = hgconv2(inc, Xg)
+    (dXg,) = torch.autograd.grad(Yg, Xg, dY_global)
+    with torch.no_grad():
+        mag = hgconv2(inc, X_global.abs())
+        dmag = hgconv2(inc, dY_global.abs())  # the conv is self-adjoint: dX = conv(dY)
+        out = {}
+        for name, got, ref, m in (("Y", Y, Yg[u0:u1], mag[u0:u1]),
+                                  ("dX", dX, dXg[u0:u1], dmag[u0:u1])):
+            err = (got - ref).abs()
+            out[name] = {"max_abs_err": float(err.max()) if err.numel() else 0.0,
+                         "max_rel_err": float((err / (m + 1e-30)).max()) if err.numel() else 0.0,
+                         "ok": bool((err <= 1e-5 * m + 1e-30).all())}
+    return out
+
+
 def main():
     args = parse()
     U0, I0, E0, zipf = WORKLOADS[args.workload]
@@ -228,13 +282,20 @@ def main():
     E = args.edges or E0
     d = args.dim
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; refusing to report a "
+              f"mislabelled run", file=sys.stderr)
+        sys.exit(2)
+    strong = args.scaling == "strong"
 
     pmc = None
     pmc_note = None
-    want_pmc = (args.pmc == "on" or (args.pmc == "auto" and world == 1 and args.gpus == 1
+    want_pmc = (args.pmc == "on" or (args.pmc == "auto" and world == 1
                                      and args.workload in ("synthetic", "zipf")))
     if want_pmc and not args.pmc_child:
         # child profiler processes run BEFORE this process touches the GPU
@@ -250,37 +311,56 @@ def main():
     # one rank per GPU; the modulo only matters for rehearsing N ranks on fewer GPUs (gloo)
     dev_index = local_rank % max(1, torch.cuda.device_count())
     device = torch.device(f"cuda:{dev_index}")
+    torch.cuda.set_device(device)
     dist_backend = None
     if world > 1:
-        torch.cuda.set_device(device)
         backend = dist_backend = os.environ.get("HGD_DIST_BACKEND", "nccl")  # nccl == RCCL
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=device)
         else:
             dist.init_process_group(backend)
 
-    idx = make_graph(U, I, E, seed=rank, zipf=zipf, device=device)
-    nnz = int(idx.shape[1])
-    inc = Incidence.from_coo(idx, None, (U, I), device=device, validate=False, rows_sorted=True)
-    del idx
-    sh = ShardedIncidence(inc, n_chunks=args.chunks, P="sym", Q="mean", R="sym")
-    g = torch.Generator(device=device).manual_seed(1000 + rank)
-    X = torch.empty(U, d, device=device)
-    bound = (6.0 / (U + d)) ** 0.5  # xavier_uniform_ on [U, d] (HCCF.py:164-169)
-    X.uniform_(-bound, bound, generator=g)
+    shard_kw = dict(n_chunks=args.chunks, P="sym", Q="mean", R="sym",
+                    slice_width=args.slice_width)
+    bound = (6.0 / (U + d)) ** 0.5  # xavier_uniform_ on the global [U, d] (HCCF.py:164-169)
+    keep_global = args.check and strong and world > 1
+    idx = make_graph(U, I, E, seed=0 if strong else rank, zipf=zipf, device=device)
+    nnz_graph = int(idx.shape[1])
+    u0, u1 = 0, U
+    if strong and world > 1:
+        sh, u0, u1 = ShardedIncidence.from_global(idx, U, I, device=device, **shard_kw)
+        inc = sh.inc
+    else:
+        inc = Incidence.from_coo(idx, None, (U, I), device=device, validate=False,
+                                 rows_sorted=True)
+        sh = ShardedIncidence(inc, **shard_kw)
+    if not keep_global:
+        del idx
+    nnz = inc.nnz
+    g = torch.Generator(device=device).manual_seed(1000 + (0 if strong else rank))
+    X_global = torch.empty(U, d, device=device).uniform_(-bound, bound, generator=g)
+    dY_global = torch.randn(U, d, device=device, generator=g)
+    if (u0, u1) == (0, U):
+        X, dY = X_global, dY_global
+    else:
+        X, dY = X_global[u0:u1].clone(), dY_global[u0:u1].clone()
+    if not keep_global:
+        del X_global, dY_global
     X.requires_grad_(True)
-    dY = torch.randn(U, d, device=device, generator=g)
     # warm the scale / edge-value caches outside the timed region
     inc.scale("row", "sym"), inc.edge_values("csc", "sym")
 
     def eager_step():
         Y = sharded_two_hop(sh, X)
         (dX,) = torch.autograd.grad(Y, X, dY)
-        return dX
+        return Y, dX
 
     step = eager_step
     use_graph = args.graph == "on"
     if use_graph:
+        if world > 1:
+            raise SystemExit("bench.py: --graph on is single-GPU only (RCCL calls are not "
+                             "captured here)")
         # whole-step capture: fwd + autograd bwd (4 hgd_spmm launches and their allocations) as
         # one hipGraph over the static X / dY — replay removes the host launch overhead that
         # dominates dataset-sized graphs, with no input copies (make_graphed_callables would
@@ -293,11 +373,11 @@ def main():
         torch.cuda.current_stream(device).wait_stream(side)
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
-            static_dX = eager_step()
+            static_out = eager_step()
 
         def step():
             graph.replay()
-            return static_dX
+            return static_out
 
     for _ in range(args.warmup):
         step()
@@ -309,6 +389,8 @@ def main():
     # record them, so with --graph on the same steps are re-run eagerly afterwards for them
     timer = profiling.HopTimer()
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     t0 = time.perf_counter()
     if use_graph:
         for _ in range(args.steps):
@@ -326,19 +408,37 @@ def main():
             for _ in range(args.steps):
                 eager_step()
         torch.cuda.synchronize()
+    hop = timer.summary()
+    hop_ms_step = hop["total_ms"] / args.steps
+    check = None
+    if args.check and not args.pmc_child:
+        Y, dX = eager_step()
+        if keep_global:
+            check = check_against_single_gpu(idx, U, I, X_global, dY_global, Y.detach(), dX,
+                                             u0, u1)
+            del idx, X_global, dY_global
+    per_rank = [{"rank": rank, "users": [u0, u1], "nnz": nnz, "hop_ms_per_step":
+                 round(hop_ms_step, 4)}]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        tot = torch.tensor([nnz], dtype=torch.float64, device=device)
-        dist.all_reduce(tot)
-        total_edges = float(tot.item())
-    else:
-        total_edges = float(nnz)
+        gathered = [None] * world
+        dist.all_gather_object(gathered, per_rank[0])
+        per_rank = gathered
+        if check is not None:
+            checks = [None] * world
+            dist.all_gather_object(checks, check)
+            check = {"ok": all(c["Y"]["ok"] and c["dX"]["ok"] for c in checks),
+                     "max_rel_err_Y": max(c["Y"]["max_rel_err"] for c in checks),
+                     "max_rel_err_dX": max(c["dX"]["max_rel_err"] for c in checks),
+                     "bound": "|err| <= 1e-5 * conv(|x|), per element"}
+    total_edges = float(nnz_graph if strong else sum(r["nnz"] for r in per_rank))
+    if strong and world > 1:
+        assert sum(r["nnz"] for r in per_rank) == nnz_graph, "shards do not tile the graph"
 
     if args.pmc_child:
         return
-    hop = timer.summary()
     if rank != 0:
         if world > 1:
             dist.barrier()
@@ -356,6 +456,8 @@ def main():
         "traffic": None if pmc is None else round(pmc / 1.0),
         "kernel": "hgd::spmm_kernel (hgd_spmm hop)",
         "algorithmic_bytes_per_launch": round(hop["avg_bytes"]),
+        "algorithmic_model": profiling.MODEL_NOTE,
+        "implementation_bytes_per_launch": round(hop["avg_impl_bytes"]),
         "avg_launch_ms": round(hop["avg_ms"], 4),
         "launches_timed": hop["launches"],
     }
@@ -379,11 +481,20 @@ def main():
         roofline["traffic_note"] = pmc_note
     if pmc is not None:
         roofline["traffic_over_algorithmic"] = round(pmc / hop["avg_bytes"], 3)
+        roofline["frac_by_traffic"] = round(pmc / (hop["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                                            4)
 
     cpu = None
     if not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(U, I, E, zipf, args.cpu_sample_edges, args.cpu_budget_s, d)
 
+    if world == 1:
+        parallelism = "single GPU"
+    else:
+        parallelism = (f"user-row shards x{world} ({'one global graph' if strong else 'a graph per rank'}), "
+                       f"{'RCCL' if dist_backend == 'nccl' else dist_backend} all-reduce of item "
+                       f"messages in {len(sh.slices(d))} column slices x {len(sh.bounds)} "
+                       f"item chunks, pipelined with the hops")
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -393,29 +504,34 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f32",
-        "data": ("synthetic: per-GPU uniform user x item incidence (torch generator seed=rank, "
-                 "dedup), xavier_uniform X, N(0,1) dY"),
+        "data": (f"synthetic: uniform{'' if zipf is None else '/Zipf items'} user x item "
+                 f"incidence (torch generator seed={'0, one global graph' if strong else 'rank'}"
+                 f", dedup), xavier_uniform X, N(0,1) dY"),
         "config": {
             "workload": f"{args.workload}-{U}x{I}x{E}-d{d}",
-            "users_per_gpu": U, "items": I, "edges_per_gpu_requested": E,
-            "edges_per_gpu": nnz, "emb_dim": d,
+            "users": U, "items": I, "edges_requested": E,
+            "edges": int(total_edges), "emb_dim": d,
             "op": "hgconv2 fwd+bwd: D_v^-1/2 H D_e^-1 H^T D_v^-1/2 X, 4 hgd_spmm hops",
-            "parallelism": (f"user-row shards x{world}, "
-                            f"{'RCCL' if dist_backend == 'nccl' else dist_backend} all-reduce "
-                            f"of item sums ({args.chunks} chunks)" if world > 1
-                            else "single GPU"),
+            "parallelism": parallelism,
             "hip_graph": use_graph,
         },
         "roofline": roofline,
         "cpu_baseline": cpu,
     }
+    if world > 1:
+        out["ranks"] = per_rank
+        out["exchange_bytes_per_step"] = 2 * sh.exchange_bytes(d)
+    if check is not None:
+        out["check"] = check
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if check is not None and not check["ok"]:
+        sys.exit(1)
 
 
 if __name__ == "__main__":

@@ -198,7 +198,8 @@ def spmm_csr(csr: CSR, X: torch.Tensor, val: Optional[torch.Tensor] = None,
         def nbytes(csr=csr, rb=rb, re_=re_, full=full, d=d, hv=val is not None,
                    hs=row_scale is not None):
             nnz = csr.nnz if full else int(csr.rowptr[re_].item() - csr.rowptr[rb].item())
-            return profiling.hop_bytes(nnz, re_ - rb, d, hv, hs)
+            return (profiling.hop_bytes(nnz, re_ - rb, d),
+                    profiling.impl_bytes(nnz, re_ - rb, d, hv, hs))
 
         timer.end(t0, nbytes)
     return out

@@ -467,6 +467,33 @@ class _ShardedPlugin:
         # degree-balanced contiguous user ranges (every rank derives the same cuts from the data)
         deg = np.diff(self.data.interaction_mat.tocsr().indptr)
         self.u0, self.u1 = shard_bounds(self.data.n_users, self.world, self.rank, deg)
+        self._sync_host_rng()
+
+    def _sync_host_rng(self):
+        """Every rank must draw the same global batch (the sampler shuffles and samples with
+        Python's ``random``) and the same CPU drop-edge mask (torch's CPU generator): rank 0's
+        Python, numpy and torch-CPU generator states are broadcast to all ranks. The per-rank
+        CUDA generators are left alone (per-rank dropout masks, sharded_encoders)."""
+        import random
+        dist = self._dist
+        box = [(random.getstate(), np.random.get_state(), torch.get_rng_state())]
+        dist.broadcast_object_list(box, src=0)
+        py, npy, th = box[0]
+        random.setstate(py)
+        np.random.set_state(npy)
+        torch.set_rng_state(th)
+
+    def _check_batch(self, *idx: torch.Tensor) -> None:
+        """Raises if the ranks do not hold the same global batch: one all-reduce of a position-
+        weighted checksum of the index tensors (MAX of (c, -c) equal to (c, -c) on every rank)."""
+        c = sum(int(k + 1) * (t.to(torch.int64) * torch.arange(
+            1, t.numel() + 1, device=t.device)).sum() for k, t in enumerate(idx))
+        v = torch.stack([c, -c]).to(torch.int64)
+        m = v.clone()
+        self._dist.all_reduce(m, op=self._dist.ReduceOp.MAX)
+        if not torch.equal(m, v):
+            raise RuntimeError(f"{type(self).__name__}: ranks drew different batches (the "
+                               "Python random state diverged); the sharded loss would be wrong")
 
     def _rows(self, table_local: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
         """table[ids] for GLOBAL user ids (negative ids wrap, as torch indexing) of a user table
@@ -554,6 +581,7 @@ class HCCF_sharded(_ShardedPlugin, HCCF):
     def train_step(self, user_idx, pos_idx, neg_idx) -> torch.Tensor:
         model = self.model
         model.train()
+        self._check_batch(user_idx, pos_idx, neg_idx)
         nl = self.u1 - self.u0
         user_emb, item_emb, gcnEmbedsLst, hyperEmbedsLst = model(keep_rate=1 - self.dropRate)
         anchor_emb = self._rows(user_emb, user_idx)
@@ -682,6 +710,7 @@ class HGNN_HD4_sharded(_ShardedPlugin, HGNN_HD4):
 
     def train_step(self, user_idx, pos_idx, neg_idx) -> torch.Tensor:
         """One batch of HGNN_HD4.py:118-160 (local_only): BPR + L2 over the global batch."""
+        self._check_batch(user_idx, pos_idx, neg_idx)
         user_emb_lc, item_emb_lc = self.model(mode='local', keep_rate=1 - self.drop_rate)
         anchor = self._rows(user_emb_lc, user_idx)
         loss = self.cf_loss(anchor, item_emb_lc[pos_idx], item_emb_lc[neg_idx])

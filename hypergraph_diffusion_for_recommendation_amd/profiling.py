@@ -2,13 +2,16 @@
 
 While a :class:`HopTimer` is active every :func:`incidence.spmm_csr` call records a start and
 an end event on the stream the hop is launched on (the current torch stream, which is the
-stream handed to ``hgd_spmm``) and remembers the hop's algorithmic bytes:
+stream handed to ``hgd_spmm``) and remembers two byte counts for the hop:
 
-    B_hop = nnz·(4 [col] + 4·[val] + 4d [gathered row]) + R·(4d [Y row] + 4·[row_scale])
-            + (R+1)·8 [int64 rowptr]
-
-i.e. what one launch must move at minimum: every index once, one d-wide fp32 row gathered per
-nonzero, every output row written once.
+* algorithmic (the figure ``roofline.achieved`` uses):
+      B_hop = nnz·(4 [int32 col] + 4d [gathered row]) + R·(4d [Y row] + 4 [row scale])
+              + (R+1)·4 [rowptr]
+  — every index once, one d-wide fp32 row gathered per nonzero, every output row written once;
+  the per-nonzero weights add 4·nnz only for an intrinsically weighted matrix (norm_adj);
+* implementation: what hgd_spmm actually streams besides — the rowptr is int64 (8 B per row)
+  and the source-side degree scale is folded into per-nonzero weights (4 B per nonzero), which
+  the algorithmic model does not count for the binary incidence of the benchmark.
 """
 from __future__ import annotations
 
@@ -18,8 +21,18 @@ import torch
 
 _ACTIVE: Optional["HopTimer"] = None
 
+MODEL_NOTE = ("SURVEY.md §8d B_hop = nnz*(4+4d) + R*(4d+4) + (R+1)*4 (binary H; the folded "
+              "per-nonzero source scale and the int64 rowptr are counted only in "
+              "implementation_bytes_per_launch)")
 
-def hop_bytes(nnz: int, rows: int, d: int, has_val: bool, has_scale: bool) -> int:
+
+def hop_bytes(nnz: int, rows: int, d: int, weighted: bool = False) -> int:
+    """SURVEY.md §8d algorithmic bytes of one hop (+4·nnz for an intrinsically weighted A)."""
+    return nnz * (4 + (4 if weighted else 0) + 4 * d) + rows * (4 * d + 4) + (rows + 1) * 4
+
+
+def impl_bytes(nnz: int, rows: int, d: int, has_val: bool, has_scale: bool) -> int:
+    """Bytes the hgd_spmm launch streams at minimum as implemented (int64 rowptr, weights)."""
     return (nnz * (4 + (4 if has_val else 0) + 4 * d)
             + rows * (4 * d + (4 if has_scale else 0)) + (rows + 1) * 8)
 
@@ -53,7 +66,9 @@ class HopTimer:
         """Synchronises, then returns launches, total ms, total algorithmic bytes, GB/s."""
         torch.cuda.synchronize()
         ms = [s.elapsed_time(e) for s, e, _ in self.records]
-        nbytes = [f() for _, _, f in self.records]
+        pairs = [f() for _, _, f in self.records]
+        nbytes = [p[0] for p in pairs]
+        impl = [p[1] for p in pairs]
         tot_ms = float(sum(ms))
         tot_b = int(sum(nbytes))
         n = len(ms)
@@ -63,6 +78,7 @@ class HopTimer:
             "avg_ms": tot_ms / n if n else 0.0,
             "bytes": tot_b,
             "avg_bytes": tot_b / n if n else 0.0,
+            "avg_impl_bytes": sum(impl) / n if n else 0.0,
             "gbps": (tot_b / (tot_ms * 1e-3) / 1e9) if tot_ms > 0 else 0.0,
             "per_launch_ms": ms,
             "per_launch_bytes": nbytes,

@@ -20,7 +20,9 @@ arguments, files and printed measures (paths relative to /root/reference/HD_SELF
   strings bit for bit;
 * :func:`early_stopping` — util/evaluation.py:195-202;
 * :class:`SELFRec` — SELFRec.py:4-42, resolving ``model.name`` in :data:`PLUGINS`
-  (``plugins.py``: HCCF, HGNN_HD4, HGCN) instead of ``exec`` on ``model.<type>.<name>``.
+  (``plugins.PLUGINS``: HCCF, HCCF_diffusion, HGNN_HD4, HGNN_HD3, HGCN, DHCF and the user-row
+  sharded HCCF_sharded, HGNN_HD4_sharded, HGNN_HD3_sharded) instead of ``exec`` on
+  ``model.<type>.<name>``.
 
 The training loops of the plugins use :func:`sampler.next_batch_pairwise` (bit-identical to
 util/sampler.py) and the drop-in encoders; nothing here falls back to the CPU for the path.
@@ -52,7 +54,11 @@ def namespace_to_dict(namespace) -> dict:
 
 class ModelConf:
     """``key=value`` lines (util/conf.py:11-35): blank lines skipped, a line with more or fewer
-    than one '=' reported and skipped, missing keys are fatal on lookup."""
+    than one '=' reported and skipped, missing keys are fatal on lookup.
+
+    A deliberate restatement of the reference's parser (util/conf.py:10-74, with
+    :class:`OptionConf`): ``conf/`` must stay untouched, so the ``.conf`` format has to parse
+    byte-identically, quirks included."""
 
     def __init__(self, file: str):
         self.config: Dict[str, str] = {}

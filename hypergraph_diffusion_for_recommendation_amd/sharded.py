@@ -1,40 +1,100 @@
 """User-row sharding of the 2-hop hypergraph conv across the GPUs of one node.
 
-Each rank owns a contiguous block of users (vertex rows of H), their embedding rows and the
-CSR/CSC of its slice of H; the item (hyperedge) dimension is replicated. The two hops are
+Each rank owns a contiguous, degree-balanced block of users (vertex rows of H), their embedding
+rows and the CSR/CSC of its slice of H; the item (hyperedge) dimension is replicated. The two
+hops are
 
     hop 1  M_g = Q·H_gᵀ·(R·X_g)         partial item sums on every rank      (CSC, hgd_spmm)
            M   = Σ_g M_g                RCCL all-reduce over xGMI             (torch.distributed)
     hop 2  Y_g = P·H_g·M                purely local                          (CSR, hgd_spmm)
 
 and the backward is the same pair with P and R swapped. Q = D_e^-1 must use the GLOBAL item
-degree, which is all-reduced once when the shard is built. To hide the exchange, hop 1 is
-issued in item chunks and each chunk's all-reduce is queued (async_op) right behind the kernel
-that produced it, so RCCL moves chunk k while the GPU computes chunk k+1; only the last chunk's
-exchange is exposed before hop 2.
+degree, which is all-reduced once when the shard is built.
+
+The exchange is pipelined over COLUMN SLICES of the embedding (``slice_width`` columns, 32 at
+d = 64): hop 1 of slice s writes its own contiguous [I, w] message block, whose all-reduce is
+queued (async_op) right behind the kernel that produced it, and hop 2 of slice s only waits for
+that block. So RCCL moves slice 0 while hop 1 computes slice 1, and hop 2 of slice 0 computes
+while slice 1 is in flight: only the first slice's hop 1 and the last slice's hop 2 are exposed
+around the exchange. Each slice is a full hop over a narrower row (w·4 bytes per gathered row,
+128 B = one L2 line at w = 32), so it adds no accumulation traffic; the cost is re-reading the
+index stream once per slice (4 B per nonzero). Item-row chunks (``n_chunks``) split each slice's
+exchange further (hop 2 of a slice then waits for all of its chunks).
 
 The reference has no distributed code at all; this is new design.
 """
 from __future__ import annotations
 
-from typing import List, Optional
+from typing import List, Optional, Tuple
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
 from .incidence import Incidence, spmm_csr
 
 
-class ShardedIncidence:
-    """One rank's slice of H (users [u0,u1) × all items) plus global item scales."""
+def shard_bounds(n_users: int, world: int, rank: int, degrees=None):
+    """Contiguous user range of ``rank``. Without ``degrees``: sizes differ by at most one. With
+    the users' interaction counts: degree-balanced ranges — cut ``r`` is the first
+    user whose prefix count reaches r/world of the total (each hop's work and its
+    nonzero bytes on a rank are its users' nonzeros plus their rows), so every rank gets the same
+    share of nonzeros to within one user's degree. Cuts are non-decreasing; a rank may get no
+    users when a few users hold most interactions."""
+    if degrees is None:
+        cuts = np.linspace(0, n_users, world + 1).astype(np.int64)
+        return int(cuts[rank]), int(cuts[rank + 1])
+    deg = np.asarray(degrees, dtype=np.int64).reshape(-1)
+    if deg.shape[0] != n_users:
+        raise ValueError(f"shard_bounds: {deg.shape[0]} degrees for {n_users} users")
+    # weight = nonzeros + 1 (the row itself), so users without interactions still spread out
+    prefix = np.concatenate([[0], np.cumsum(deg + 1)])
+    total = int(prefix[-1])
 
-    def __init__(self, inc: Incidence, group=None, n_chunks: int = 4,
-                 P: Optional[str] = "sym", Q: Optional[str] = "mean", R: Optional[str] = "sym"):
+    def cut(r):
+        if r <= 0:
+            return 0
+        if r >= world:
+            return n_users
+        return int(np.searchsorted(prefix, (total * r + world - 1) // world, side="left"))
+
+    return cut(rank), cut(rank + 1)
+
+
+def shard_rows_of_sorted_coo(indices: torch.Tensor, n_users: int, world: int, rank: int,
+                             degrees: Optional[torch.Tensor] = None):
+    """This rank's share of a GLOBAL user×item COO whose rows are sorted (the row-major order of
+    ``convert_sparse_mat_to_tensor``, base/torch_interface.py:8-12): the degree-balanced user
+    range (:func:`shard_bounds`) and its entries re-indexed to local rows, in the input's order.
+    Returns ``(u0, u1, local_indices)``; every global entry lies in exactly one rank's share."""
+    rows = indices[0]
+    if degrees is None:
+        degrees = torch.bincount(rows, minlength=n_users)
+    if rows.numel() > 1 and bool((rows[1:] < rows[:-1]).any()):
+        raise ValueError("shard_rows_of_sorted_coo: rows must be sorted")
+    u0, u1 = shard_bounds(n_users, world, rank, degrees.cpu().numpy())
+    bounds = torch.tensor([u0, u1], dtype=rows.dtype, device=rows.device)
+    lo, hi = torch.searchsorted(rows, bounds).tolist()
+    loc = indices[:, lo:hi].clone()
+    loc[0] -= u0
+    return u0, u1, loc
+
+
+class ShardedIncidence:
+    """One rank's slice of H (users [u0,u1) × all items) plus global item scales.
+
+    ``slice_width``: embedding columns per pipelined exchange block (None: 32 for d ≤ 128, else
+    64; a multiple of 4 keeps the float4 gathers). ``n_chunks``: item-row chunks per slice."""
+
+    def __init__(self, inc: Incidence, group=None, n_chunks: int = 1,
+                 P: Optional[str] = "sym", Q: Optional[str] = "mean", R: Optional[str] = "sym",
+                 slice_width: Optional[int] = None):
         self.inc = inc
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.P, self.R = P, R
         self.n_chunks = max(1, int(n_chunks)) if self.world > 1 else 1
+        self.slice_width = slice_width
         self.q = self._global_col_scale(Q)
         # item-row chunk boundaries for the overlapped exchange
         n_items = inc.n_cols
@@ -42,6 +102,32 @@ class ShardedIncidence:
         self.bounds = [(min(k * step, n_items), min((k + 1) * step, n_items))
                        for k in range(self.n_chunks)]
         self.bounds = [(a, b) for a, b in self.bounds if b > a] or [(0, n_items)]
+
+    @classmethod
+    def from_global(cls, indices: torch.Tensor, n_users: int, n_items: int, group=None,
+                    device=None, **kw) -> Tuple["ShardedIncidence", int, int]:
+        """Shards a global row-sorted user×item COO (int64 [2, nnz]) over the ranks of ``group``
+        by degree-balanced user ranges; returns ``(shard, u0, u1)``."""
+        world = dist.get_world_size(group) if dist.is_initialized() else 1
+        rank = dist.get_rank(group) if dist.is_initialized() else 0
+        u0, u1, loc = shard_rows_of_sorted_coo(indices, n_users, world, rank)
+        inc = Incidence.from_coo(loc, None, (u1 - u0, n_items),
+                                 device=device if device is not None else indices.device,
+                                 validate=False, rows_sorted=True)
+        return cls(inc, group=group, **kw), u0, u1
+
+    def slices(self, d: int) -> List[Tuple[int, int]]:
+        """Column ranges of the pipelined exchange (one range on a single rank unless
+        ``slice_width`` is given explicitly, which measures the sliced hops alone)."""
+        if self.world == 1 and self.slice_width is None:
+            return [(0, d)]
+        w = self.slice_width or (32 if d <= 128 else 64)
+        w = max(4, (int(w) // 4) * 4)
+        return [(c, min(c + w, d)) for c in range(0, d, w)]
+
+    def exchange_bytes(self, d: int) -> int:
+        """fp32 bytes all-reduced per hop pair (the [I, d] item messages)."""
+        return 0 if self.world == 1 else 4 * self.inc.n_cols * d
 
     def _global_col_scale(self, kind: Optional[str]) -> Optional[torch.Tensor]:
         if kind is None:
@@ -56,34 +142,44 @@ class ShardedIncidence:
         s = torch.where(deg > 0, deg.pow(p), torch.zeros_like(deg))
         return s.to(torch.float32)
 
-    def _hop1_exchange(self, X: torch.Tensor, src_kind: Optional[str]) -> torch.Tensor:
+    def two_hop(self, X: torch.Tensor, src_kind: Optional[str],
+                dst_kind: Optional[str]) -> torch.Tensor:
+        """``S_dst·H_g·Σ_ranks(Q·H_gᵀ·S_src·X_g)`` with the slice pipeline described above."""
         inc = self.inc
-        M = torch.empty((inc.n_cols, X.shape[1]), dtype=torch.float32, device=X.device)
-        val = inc.edge_values("csc", src_kind)
-        works: List = []
-        for a, b in self.bounds:
-            spmm_csr(inc.csc, X, val=val, row_scale=self.q, out=M, row_begin=a, row_end=b)
-            if self.world > 1:
-                works.append(dist.all_reduce(M[a:b], group=self.group, async_op=True))
-        for w in works:
-            w.wait()
-        return M
+        d = X.shape[1]
+        Y = torch.empty((inc.n_rows, d), dtype=torch.float32, device=X.device)
+        val_t = inc.edge_values("csc", src_kind)
+        row_scale = inc.scale("row", dst_kind)
+        pieces = []
+        for c0, c1 in self.slices(d):
+            w = c1 - c0
+            Xs = X if w == d else X[:, c0:c1]
+            Ms = torch.empty((inc.n_cols, w), dtype=torch.float32, device=X.device)
+            works: List = []
+            for a, b in self.bounds:
+                spmm_csr(inc.csc, Xs, val=val_t, row_scale=self.q, out=Ms, row_begin=a,
+                         row_end=b)
+                if self.world > 1:
+                    works.append(dist.all_reduce(Ms[a:b], group=self.group, async_op=True))
+            pieces.append((c0, c1, Ms, works))
+        for c0, c1, Ms, works in pieces:
+            for wk in works:
+                wk.wait()
+            out = Y if c1 - c0 == d else Y[:, c0:c1]
+            spmm_csr(inc.csr, Ms, val=inc.val, row_scale=row_scale, out=out)
+        return Y
 
 
 class _ShardedHGConv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, X, sh: ShardedIncidence):
         ctx.sh = sh
-        X = X.contiguous()
-        M = sh._hop1_exchange(X, sh.R)
-        return spmm_csr(sh.inc.csr, M, val=sh.inc.val, row_scale=sh.inc.scale("row", sh.P))
+        return sh.two_hop(X.contiguous(), sh.R, sh.P)
 
     @staticmethod
     def backward(ctx, dY):
         sh = ctx.sh
-        dM = sh._hop1_exchange(dY.contiguous(), sh.P)
-        dX = spmm_csr(sh.inc.csr, dM, val=sh.inc.val, row_scale=sh.inc.scale("row", sh.R))
-        return dX, None
+        return sh.two_hop(dY.contiguous(), sh.P, sh.R), None
 
 
 def sharded_two_hop(sh: ShardedIncidence, X_local: torch.Tensor) -> torch.Tensor:
@@ -142,11 +238,21 @@ def block_coo(indices: torch.Tensor, values: Optional[torch.Tensor], n_users: in
               u1: int):
     """The two blocks of a bipartite [N, N] COO (users first) that user rows [u0, u1) own:
     ``B = A[u0:u1, U:]`` (local users → items) and ``C = A[U:, u0:u1]`` (items → local users),
-    re-indexed locally, in the input's order (row-major stays row-major), with the positions of
-    their entries in the input (to slice a global drop-edge mask the same way)."""
+    re-indexed locally in CSR order (the input's order when it is row-sorted, else a stable row
+    sort of it), with the positions of their entries in the input (to slice a global drop-edge
+    mask the same way)."""
     r, c = indices[0], indices[1]
     sel_b = ((r >= u0) & (r < u1) & (c >= n_users)).nonzero().flatten()
     sel_c = ((r >= n_users) & (c >= u0) & (c < u1)).nonzero().flatten()
+    # a row-unsorted (or uncoalesced) input: order each block by row, stably, so the block COO is
+    # in CSR order and a global mask sliced by sel_b / sel_c lines up with Incidence.drop's
+    for_sort = []
+    for sel in (sel_b, sel_c):
+        rs = r[sel]
+        if rs.numel() > 1 and bool((rs[1:] < rs[:-1]).any()):
+            sel = sel[torch.sort(rs, stable=True).indices]
+        for_sort.append(sel)
+    sel_b, sel_c = for_sort
     b_idx = torch.stack([r[sel_b] - u0, c[sel_b] - n_users])
     c_idx = torch.stack([r[sel_c] - n_users, c[sel_c] - u0])
     b_val = None if values is None else values[sel_b]

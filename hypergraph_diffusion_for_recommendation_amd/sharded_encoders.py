@@ -15,7 +15,9 @@ restricted to this rank's users. Exchanges (RCCL over xGMI with backend "nccl"):
 Replicated tensors follow :mod:`.sharded`'s convention (same value on every rank, per-rank
 partial gradients): call :func:`~.sharded.allreduce_replicated_grads` on the replicated
 parameters (:meth:`replicated_parameters`) before the optimizer step. Dropout on replicated rows
-draws from a generator seeded identically on every rank (``seed``), so the replicas stay equal.
+draws from a generator seeded identically on every rank (``seed``), so the replicas stay equal;
+dropout on a rank's own user rows draws from a per-rank generator, so the users of different ranks
+get independent masks (:class:`_SplitDropout`).
 """
 from __future__ import annotations
 
@@ -29,35 +31,8 @@ import torch.nn.functional as F
 from .encoders import edhnn_config
 from .functional import dense_two_hop, layer_norm, linear, row_epilogue
 from .layers import EquivSetGNN, LayerNorm
-from .sharded import (ShardedBipartite, bipartite_hop, sharded_dense_two_hop,
-                      sharded_hgcn_conv, sharded_mean_two_hop)
-
-
-def shard_bounds(n_users: int, world: int, rank: int, degrees=None):
-    """Contiguous user range of ``rank``. Without ``degrees``: sizes differ by at most one. With
-    the users' interaction counts: degree-balanced ranges — cut ``r`` is the first
-    user whose prefix count reaches r/world of the total (each hop's work and its
-    nonzero bytes on a rank are its users' nonzeros plus their rows), so every rank gets the same
-    share of nonzeros to within one user's degree. Cuts are non-decreasing; a rank may get no
-    users when a few users hold most interactions."""
-    if degrees is None:
-        cuts = np.linspace(0, n_users, world + 1).astype(np.int64)
-        return int(cuts[rank]), int(cuts[rank + 1])
-    deg = np.asarray(degrees, dtype=np.int64).reshape(-1)
-    if deg.shape[0] != n_users:
-        raise ValueError(f"shard_bounds: {deg.shape[0]} degrees for {n_users} users")
-    # weight = nonzeros + 1 (the row itself), so users without interactions still spread out
-    prefix = np.concatenate([[0], np.cumsum(deg + 1)])
-    total = int(prefix[-1])
-
-    def cut(r):
-        if r <= 0:
-            return 0
-        if r >= world:
-            return n_users
-        return int(np.searchsorted(prefix, (total * r + world - 1) // world, side="left"))
-
-    return cut(rank), cut(rank + 1)
+from .sharded import (ShardedBipartite, bipartite_hop, shard_bounds,  # noqa: F401
+                      sharded_dense_two_hop, sharded_hgcn_conv, sharded_mean_two_hop)
 
 
 def _coo_tensor(mat, binary: bool = False):
@@ -78,21 +53,34 @@ def _coo_tensor(mat, binary: bool = False):
 
 
 class _SplitDropout(nn.Module):
-    """nn.Dropout over the local layout: local rows draw from the default generator, replicated
-    rows (``start`` onward) from ``gen`` (identical on every rank)."""
+    """nn.Dropout over the local layout: rows before ``start`` are this rank's own (local users),
+    rows from ``start`` on are replicated (items). Local rows draw from ``local_gen``, seeded per
+    rank, so users on different ranks get independent masks (one i.i.d. mask over all users, as
+    the reference's single nn.Dropout); replicated rows draw from ``gen``, identical on every rank,
+    so the replicas stay equal. ``start`` = rows.shape[0] drops every row as local."""
 
-    def __init__(self, p: float, gen: torch.Generator):
+    def __init__(self, p: float, gen: torch.Generator, local_gen: torch.Generator):
         super().__init__()
-        self.p, self.gen = float(p), gen
+        self.p, self.gen, self.local_gen = float(p), gen, local_gen
 
     def forward(self, x: torch.Tensor, start: int) -> torch.Tensor:
         if not self.training or self.p == 0.0:
             return x
         if self.p == 1.0:
             return torch.zeros_like(x)
-        loc = F.dropout(x[:start], self.p, True)
-        keep = torch.empty_like(x[start:]).bernoulli_(1.0 - self.p, generator=self.gen)
-        return torch.cat([loc, x[start:] * keep / (1.0 - self.p)])
+        q = 1.0 - self.p
+        keep_loc = torch.empty_like(x[:start]).bernoulli_(q, generator=self.local_gen)
+        keep_rep = torch.empty_like(x[start:]).bernoulli_(q, generator=self.gen)
+        return torch.cat([x[:start] * keep_loc / q, x[start:] * keep_rep / q])
+
+
+def _rank_generators(device, seed: int, group):
+    """(replicated, local) dropout generators: the first seeded identically on every rank, the
+    second per rank."""
+    rank = torch.distributed.get_rank(group) if torch.distributed.is_initialized() else 0
+    rep = torch.Generator(device=device).manual_seed(int(seed))
+    loc = torch.Generator(device=device).manual_seed(int(seed) * 65537 + 1 + rank)
+    return rep, loc
 
 
 class ShardedHCCFEncoder(nn.Module):
@@ -129,9 +117,8 @@ class ShardedHCCFEncoder(nn.Module):
             'user_w': nn.Parameter(nn.init.xavier_uniform_(torch.empty(d, K)).to(self.device)),
             'item_w': nn.Parameter(nn.init.xavier_uniform_(torch.empty(d, K)).to(self.device)),
         })
-        self.rep_gen = torch.Generator(device=self.device).manual_seed(int(seed))
-        self.drop_out = nn.Dropout(self.drop_rate)
-        self.rep_drop = _SplitDropout(self.drop_rate, self.rep_gen)
+        self.rep_gen, self.loc_gen = _rank_generators(self.device, seed, group)
+        self.rep_drop = _SplitDropout(self.drop_rate, self.rep_gen, self.loc_gen)
 
     @torch.no_grad()
     def load_global(self, embedding_dict) -> None:
@@ -166,7 +153,8 @@ class ShardedHCCFEncoder(nn.Module):
         hyper_ii = linear(e['item_emb'], e['item_w'].t())
         for _ in range(self.n_layers):
             gcn_emb = bipartite_hop(self._dropped(keep_rate), hidden[-1])
-            hyper_u = sharded_dense_two_hop(self.drop_out(hyper_uu), hidden[-1][:nl], self.group)
+            hyper_u = sharded_dense_two_hop(self.rep_drop(hyper_uu, nl), hidden[-1][:nl],
+                                            self.group)
             hyper_i = dense_two_hop(self.rep_drop(hyper_ii, 0), hidden[-1][nl:])
             gcn_hidden += [gcn_emb]
             hgnn_hidden += [torch.cat([hyper_u, hyper_i], 0)]
@@ -204,7 +192,7 @@ class ShardedLocalAwareEncoder(nn.Module):
         self.norm = ShardedBipartite.from_global(_coo_tensor(data.norm_adj), U, I, u0, u1,
                                                  device=self.device, group=group,
                                                  n_chunks=n_chunks)
-        self.rep_gen = torch.Generator(device=self.device).manual_seed(int(seed))
+        self.rep_gen, self.loc_gen = _rank_generators(self.device, seed, group)
         self._drops = {}
         self.to(self.device)
 
@@ -214,7 +202,7 @@ class ShardedLocalAwareEncoder(nn.Module):
     def _drop(self, module: nn.Dropout, x: torch.Tensor) -> torch.Tensor:
         d = self._drops.get(id(module))
         if d is None:
-            d = self._drops[id(module)] = _SplitDropout(module.p, self.rep_gen)
+            d = self._drops[id(module)] = _SplitDropout(module.p, self.rep_gen, self.loc_gen)
         d.training = self.training
         return d(x, self.n_local)
 
@@ -292,7 +280,7 @@ class ShardedLocalAwareEncoderHD3(ShardedLocalAwareEncoder):
         self.norm = ShardedBipartite.from_global(_coo_tensor(data.norm_adj), U, I, u0, u1,
                                                  device=self.device, group=group,
                                                  n_chunks=n_chunks)
-        self.rep_gen = torch.Generator(device=self.device).manual_seed(int(seed))
+        self.rep_gen, self.loc_gen = _rank_generators(self.device, seed, group)
         self._drops = {}
         self.to(self.device)
 

@@ -43,7 +43,7 @@ def load_data_set(path):
 
 
 def remap_ids(pairs):
-    """Id maps in first-appearance order of the training file (data/ui_graph.py:107-125)."""
+    """Id maps in first-appearance order of the training file (data/ui_graph.py:43-68)."""
     user, item = {}, {}
     for u, i in pairs:
         if u not in user:
@@ -55,7 +55,7 @@ def remap_ids(pairs):
 
 def bipartite_adjacency(user_idx, item_idx, n_users, n_items):
     """ui_adj = [[0, R], [Rᵀ, 0]] as float32 CSR, duplicates summed
-    (Interaction.__create_sparse_bipartite_adjacency, data/ui_graph.py:134-148)."""
+    (Interaction.__create_sparse_bipartite_adjacency, data/ui_graph.py:70-84)."""
     n = n_users + n_items
     user_idx = np.asarray(user_idx)
     item_idx = np.asarray(item_idx)

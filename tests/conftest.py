@@ -1,4 +1,6 @@
+import hashlib
 import os
+import subprocess
 import sys
 
 import pytest
@@ -6,10 +8,35 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
+CSRC = os.path.join(ROOT, "hypergraph_diffusion_for_recommendation_amd", "csrc")
+LIB = os.path.join(ROOT, "hypergraph_diffusion_for_recommendation_amd", "_lib", "libhgd.so")
+
+
+def _ensure_built():
+    """The library under test is the one HEAD's sources compile to: ``make -q`` (a no-op check
+    when the shipped objects and .so are newer than every source) and, if anything is stale or
+    missing, the same ``make`` __graft_entry__.build() runs. HGD_SKIP_BUILD=1 skips it."""
+    if os.environ.get("HGD_SKIP_BUILD") == "1":
+        return "skipped (HGD_SKIP_BUILD=1)"
+    if subprocess.run(["make", "-q", "-C", CSRC], stdout=subprocess.DEVNULL,
+                      stderr=subprocess.DEVNULL).returncode == 0:
+        return "up to date"
+    jobs = str(min(16, os.cpu_count() or 1))
+    subprocess.run(["make", "-C", CSRC, "-j", jobs], check=True, stdout=subprocess.DEVNULL)
+    return "rebuilt from sources"
 
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device) and libhgd.so")
+    config._hgd_build = _ensure_built()
+
+
+def pytest_report_header(config):
+    sha = "missing"
+    if os.path.exists(LIB):
+        with open(LIB, "rb") as fh:
+            sha = hashlib.sha256(fh.read()).hexdigest()[:16]
+    return f"libhgd.so: {getattr(config, '_hgd_build', '?')}, sha256 {sha}"
 
 
 def gpu_available():

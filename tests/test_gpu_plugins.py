@@ -399,8 +399,10 @@ def _sharded_execute_worker(rank, world, port, root, model, out_q):
                           drop_rate=0.2, p=0.3, temp=0.2, cl_rate=1e-3, reg=0.01, seed=7,
                           mode='local_only')
         kw['dataset_root'] = os.path.join(root, "dataset")
-        random.seed(3)
-        torch.manual_seed(3)
+        # different host seeds per rank: the plugin itself must give every rank the same
+        # batches (rank 0's random state is broadcast; _check_batch raises otherwise)
+        random.seed(3 + rank)
+        torch.manual_seed(3 + rank)
         rec = SELFRec(conf, kw).execute()
         out_q.put((rank, rec.result, os.path.exists(rec.output + f"/{model}-performance.txt")))
         dist.barrier()
