@@ -387,6 +387,7 @@ namespace {
 constexpr int kDefaultPolicy = kPolPrefetch;
 int g_unroll = 8;
 int g_policy = kDefaultPolicy;
+int g_pass_cols = 256;  // widest column pass of the float4 path without a fused epilogue
 
 template <int G, int VEC, int U, int POL, bool EX = false>
 void launch_kernel(const SpmmArgs& a, bool has_val, bool seg, int64_t blocks, hipStream_t st) {
@@ -561,9 +562,11 @@ hgd_status spmm_impl(const int64_t* rowptr, const int32_t* col, const float* val
                 "%s: layer_norm needs d <= 256 (16-byte aligned rows) or d <= 64 (got d=%d%s)",
                 fn, d, aligned ? "" : ", unaligned");
   if (aligned) {
-    // float4 path: one pass when d/4 <= 64 lanes, else 256-column passes.
+    // float4 path: one pass when d/4 <= 64 lanes, else 256-column passes; without a fused
+    // epilogue (which needs the whole row in one group) passes are at most g_pass_cols wide.
     const int lanes = d / 4;
-    const int G = lanes >= 64 ? 64 : next_pow2(lanes);
+    int G = lanes >= 64 ? 64 : next_pow2(lanes);
+    if (!ex && 4 * G > g_pass_cols) G = g_pass_cols / 4;
     for (int c0 = 0; c0 < d; c0 += 4 * G) {
       a.col0 = c0;
       hgd_status s = ex ? launch_vec<4, true>(G, a, has_val, st)
@@ -622,6 +625,11 @@ extern "C" hgd_status hgd_set_tuning(int32_t key, int32_t value) {
       HGD_REQUIRE(value == 0 || value == 1 || value == 8 || value == 9,
                   "hgd_set_tuning: policy must be 0, 1 (nt stores), 8 (index prefetch) or 9");
       g_policy = value;
+      return HGD_OK;
+    case HGD_TUNE_SPMM_PASS_COLS:
+      HGD_REQUIRE(value == 64 || value == 128 || value == 256,
+                  "hgd_set_tuning: pass columns must be 64, 128 or 256");
+      g_pass_cols = value;
       return HGD_OK;
     default:
       return fail(HGD_ERR_INVALID_ARG, "hgd_set_tuning: unknown key %d", key);

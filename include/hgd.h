@@ -59,8 +59,14 @@ typedef enum hgd_epilogue {
 /* Tuning knobs of the SpMM hop (process-wide; defaults are the measured best on MI355X).
  *   HGD_TUNE_SPMM_UNROLL: independent row gathers in flight per lane (8 or 16)
  *   HGD_TUNE_SPMM_POLICY: 0 plain, 1 non-temporal Y stores, 8 software-pipelined index
- *                         batches (default), 9 both */
-typedef enum hgd_tune_key { HGD_TUNE_SPMM_UNROLL = 1, HGD_TUNE_SPMM_POLICY = 2 } hgd_tune_key;
+ *                         batches (default), 9 both
+ *   HGD_TUNE_SPMM_PASS_COLS: widest column pass of a hop without a fused row epilogue
+ *                         (64, 128 or 256 fp32 columns; wider rows run as several passes) */
+typedef enum hgd_tune_key {
+  HGD_TUNE_SPMM_UNROLL = 1,
+  HGD_TUNE_SPMM_POLICY = 2,
+  HGD_TUNE_SPMM_PASS_COLS = 3
+} hgd_tune_key;
 hgd_status hgd_set_tuning(int32_t key, int32_t value);
 
 /* Library ABI version (major*10000 + minor*100 + patch). */

@@ -1,0 +1,382 @@
+"""GPU: the encoders of BASELINE.json's configs at the configs' own shapes, in TRAIN mode, forward
+and backward, against the reference restated in float64 with its own torch calls
+(tests/_ref64.py; paths relative to /root/reference/HD_SELFRec):
+
+* configs[0] LastFM HCCF, 1 layer, d = 32: 1,891 users × 14,777 items (HCCF_diffusion.py:140-141
+  sizes), BPR + per-layer InfoNCE (HCCF.py:61-97, 173-191);
+* configs[2] Yelp2018 HCCF, 3 layers, d = 64, with drop-edge and InfoNCE: 31,668 × 38,048;
+* configs[3] Amazon-Book "hypergraph diffusion" (HGNN_HD4 local encoder, HGNN_HD4.py:390-405),
+  3 layers, d = 128: 52,643 × 91,599, single GPU and user-row sharded over 2 ranks;
+* HCCF_diffusion's encoder (HCCF_diffusion.py:131-215), train mode.
+
+Interaction counts follow the public statistics with the reference's 75 % train split
+(SURVEY.md §8); the graphs are synthetic (no datasets ship). Every dropout mask and drop-edge
+draw is taken once and fed to both sides (tests/_ref64.py FixedDropout / DropRecorder; the
+drop-edge structure itself must equal the reference's CPU draw bit for bit).
+
+Bounds (tests/_ref64.py, calibrated in tests/test_ref64.py): every row of every output and
+gradient within 1e-5 of that row's largest |value| (north_star's "fp32 within 1e-5 relative",
+no absolute floor); scalar losses — means of positive terms (−log σ, −log softmax) — within
+1e-5 relative.
+"""
+import os
+import socket
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import hgd_oracle as O
+from tests import _ref64 as R
+
+pytestmark = pytest.mark.gpu
+
+LASTFM = (1_891, 14_777, 70_000)
+YELP = (31_668, 38_048, 1_170_000)
+AMAZON = (52_643, 91_599, 2_240_000)
+
+
+def _graph(U, I, R_, seed):
+    rows, cols = O.synthetic_incidence(U, I, R_, seed=seed)
+    ui = O.bipartite_adjacency(rows, cols, U, I)
+    return ui, O.normalize_graph_mat(ui)
+
+
+def _coo_host(adj):
+    return adj._indices().cpu(), adj._values().cpu()
+
+
+# ---------------------------------------------------------------------------------------------
+# HCCF (configs[0], configs[2])
+# ---------------------------------------------------------------------------------------------
+def _hccf_case(dev, shape, d, n_layers, seed, batch=4096, temp=1.0, cl_rate=0.01):
+    """One HCCF training step's forward and backward (HCCF.py:79-97): encoder with drop-edge
+    (keep 1 - conf dropout 0.3) and learned-hypergraph dropout (--drop_rate 0.2), then
+    HCCF.calcLosses (BPR + cl_rate · Σ_layers InfoNCE at conf temp), as the plugin computes it
+    (plugins.HCCF.calcLosses: fused InfoNCE kernel, MFMA E·W and HGNN products)."""
+    from hypergraph_diffusion_for_recommendation_amd.encoders import HCCFEncoder
+    from hypergraph_diffusion_for_recommendation_amd.plugins import HCCF
+    U, I, nnz = shape
+    N = U + I
+    _, A = _graph(U, I, nnz, seed)
+    data = SimpleNamespace(n_users=U, n_items=I, norm_adj=A)
+    kw = dict(lrate=1e-3, lr_decay=0.9, max_epoch=1, batch_size=batch, reg=0.01,
+              embedding_size=d, hyper_dim=32, drop_rate=0.2, p=0.3, n_layers=n_layers)
+    torch.manual_seed(seed)
+    enc = HCCFEncoder(kw, data, device=dev).train()
+    enc.drop_out = R.FixedDropout(0.2, seed + 1)
+    enc.edgeDropper = R.DropRecorder(enc.edgeDropper)
+    rng = np.random.default_rng(seed + 2)
+    u, i, j = (torch.from_numpy(rng.integers(0, n, batch)) for n in (U, I, I))
+    host = SimpleNamespace(data=data, nLayers=n_layers, temp=temp, ss_rate=cl_rate)
+
+    torch.manual_seed(seed + 3)
+    ue, ie, gcns, hyps = enc(keep_rate=0.7)
+    bpr, ssl = HCCF.calcLosses(host, ue[u.to(dev)], ie[i.to(dev)], ie[j.to(dev)], gcns, hyps,
+                               0.01)
+    loss = bpr + ssl
+    loss.backward()
+
+    P = R.leaves(enc)
+    idx, vals = _coo_host(enc.sparse_norm_adj)
+    torch.manual_seed(seed + 3)
+    adjs = []
+    for layer in range(n_layers):
+        di, dv = R.drop_edge_reference(idx, vals, 0.7)
+        gi, gv = enc.edgeDropper.outputs[layer]
+        assert torch.equal(di, gi) and torch.equal(dv, gv), f"drop-edge layer {layer}"
+        adjs.append(R.sparse(di, dv, (N, N)))
+    assert len(enc.drop_out.masks) == 2 * n_layers
+    ueR, ieR, gR, hR = R.hccf_encoder(P, adjs, enc.drop_out.masks, 0.8, U, n_layers)
+    anc, pos, neg = ueR[u], ieR[i], ieR[j]
+    u_nodes, p_nodes = torch.unique(anc.long()), torch.unique(pos.long())
+    sslR = 0
+    for layer in range(n_layers):
+        e1, e2 = gR[layer].detach(), hR[layer]
+        sslR = sslR + R.contrast_loss(e1[:U], e2[:U], u_nodes, temp) \
+            + R.contrast_loss(e1[U:], e2[U:], p_nodes, temp)
+    lossR = R.bpr_loss(anc, pos, neg) + sslR * cl_rate
+
+    worst = R.check_rows(ue, ueR, "user_emb")
+    worst = max(worst, R.check_rows(ie, ieR, "item_emb"))
+    for layer in range(n_layers):
+        worst = max(worst, R.check_rows(gcns[layer], gR[layer], f"gcn[{layer}]"),
+                    R.check_rows(hyps[layer], hR[layer], f"hyper[{layer}]"))
+    assert abs(float(loss) - float(lossR)) <= R.TOL * abs(float(lossR)), (float(loss),
+                                                                         float(lossR))
+    names = list(P)
+    gref = torch.autograd.grad(lossR, [P[k] for k in names])
+    got = dict(enc.named_parameters())
+    for k, g in zip(names, gref):
+        worst = max(worst, R.check_rows(got[k].grad, g, f"d {k}"))
+    print(f"HCCF {shape} d={d} L={n_layers}: worst row ratio {worst:.2e}")
+
+
+def test_hccf_lastfm_1layer_d32_train_step(dev):
+    """configs[0]: LastFM HCCF, n_layers = 1, d = 32."""
+    _hccf_case(dev, LASTFM, 32, 1, seed=10)
+
+
+def test_hccf_yelp_3layer_d64_infonce_train_step(dev):
+    """configs[2]: Yelp2018 HCCF, 3 layers, d = 64, drop-edge + InfoNCE."""
+    _hccf_case(dev, YELP, 64, 3, seed=20)
+
+
+# ---------------------------------------------------------------------------------------------
+# HGNN_HD4's local (ED-HNN) encoder (configs[3])
+# ---------------------------------------------------------------------------------------------
+def _local_aware_reference(enc_state, ui, A_idx, A_val, U, I, d, n_layers, ego, G, masks,
+                           keep_b, drop_keep, seed_drop, prefix=""):
+    """float64 LocalAwareEncoder forward + backward; returns (out, grads by name incl. 'ego')."""
+    N = U + I
+    P = {k: v.detach().cpu().double().requires_grad_(True) for k, v in enc_state.items()}
+    mean_e, mean_v = R.ui_mean_operators(ui, N)
+    if drop_keep < 1.0:
+        torch.manual_seed(seed_drop)
+        di, dv = R.drop_edge_reference(A_idx, A_val, drop_keep)
+    else:
+        di, dv = A_idx, A_val
+    adj = R.sparse(di, dv, (N, N))
+    x = ego.detach().cpu().double().requires_grad_(True)
+    out = R.local_aware(x, P, n_layers, mean_e, mean_v, adj, masks, keep_b, 1e-5, prefix)
+    names = list(P)
+    grads = torch.autograd.grad(out, [x] + [P[k] for k in names], G.double(),
+                                allow_unused=True)
+    return out, dict(zip(["ego"] + names, grads)), (di, dv)
+
+
+def test_local_aware_amazon_d128_train(dev):
+    """configs[3] on one GPU: LocalAwareEncoder (HGNN_HD4 --mode=local_only, --n_layers=3,
+    --drop_rate=0.2, --p=0.3) at d = 128, train mode: ED-HNN block dropout 0.5 (edhnn_config),
+    the last layer's HGCNConv on the edge-dropped norm_adj (keep 0.8). Output rows, the ego
+    gradient and every weight gradient (lin_in, the MLP's LayerNorm and Linear, lns[0])."""
+    from hypergraph_diffusion_for_recommendation_amd.encoders import LocalAwareEncoder
+    from hypergraph_diffusion_for_recommendation_amd.layers import SpAdjDropEdge
+    U, I, nnz = AMAZON
+    N, d, L = U + I, 128, 3
+    ui, A = _graph(U, I, nnz, seed=30)
+    data = SimpleNamespace(n_users=U, n_items=I, norm_adj=A, ui_adj=ui)
+    torch.manual_seed(31)
+    enc = LocalAwareEncoder(data, d, d, L, 0.3, 0.2, device=dev).train()
+    fd = R.FixedDropout(0.5, 32)
+    for blk in enc.edhnn_layers:
+        blk.dropout = fd
+    g = torch.Generator().manual_seed(33)
+    bound = (6.0 / (N + d)) ** 0.5
+    ego = (torch.rand(N, d, generator=g) * 2 - 1) * bound
+    G = torch.randn(N, d, generator=g)
+    torch.manual_seed(34)
+    dropped = SpAdjDropEdge()(enc.sparse_norm_adj, 0.8)
+    x = ego.to(dev).requires_grad_(True)
+    ue, ie = enc(x, dropped)
+    out = torch.cat([ue, ie])
+    out.backward(G.to(dev))
+    assert len(fd.masks) == 3 * (L - 1)
+
+    idx, vals = _coo_host(enc.sparse_norm_adj)
+    state = dict(enc.named_parameters())
+    outR, gradsR, (di, dv) = _local_aware_reference(state, ui, idx, vals, U, I, d, L, ego, G,
+                                                    fd.masks, 0.5, 0.8, 34)
+    gi, gv = _coo_host(dropped)
+    assert torch.equal(di, gi) and torch.equal(dv, gv), "drop-edge structure"
+    worst = R.check_rows(out, outR, "output")
+    worst = max(worst, R.check_rows(x.grad, gradsR["ego"], "d ego"))
+    for k, p in state.items():
+        if gradsR[k] is None:  # lns[1:] are unused by the reference too
+            assert p.grad is None, k
+            continue
+        worst = max(worst, R.check_rows(p.grad, gradsR[k], f"d {k}"))
+    print(f"LocalAware Amazon d=128: worst row ratio {worst:.2e}")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _sharded_worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        from hypergraph_diffusion_for_recommendation_amd import sharded_encoders as SE
+        U, I, nnz = AMAZON
+        N, d, L = U + I, 128, 3
+        ui, A = _graph(U, I, nnz, seed=30)
+        data = SimpleNamespace(n_users=U, n_items=I, norm_adj=A, ui_adj=ui)
+        deg = np.diff(ui.tocsr().indptr)[:U]
+        u0, u1 = SE.shard_bounds(U, world, rank, deg)
+        torch.manual_seed(31)
+        enc = SE.ShardedLocalAwareEncoder(data, d, d, L, 0.3, 0.2, u0, u1, device=dev,
+                                          n_chunks=3).eval()
+        g = torch.Generator().manual_seed(33)
+        bound = (6.0 / (N + d)) ** 0.5
+        ego = (torch.rand(N, d, generator=g) * 2 - 1) * bound
+        G = torch.randn(N, d, generator=g)
+        torch.manual_seed(34)
+        dropped = enc.dropped(0.8, device_rng=False)  # the reference's global CPU mask
+        xl = torch.cat([ego[u0:u1], ego[U:]]).to(dev).requires_grad_(True)
+        su, si = enc(xl, dropped)
+        (torch.cat([su, si]) * torch.cat([G[u0:u1], G[U:]]).to(dev)).sum().backward()
+        n = u1 - u0
+        out = {"u0": u0, "u1": u1, "users": su.detach().cpu(), "items": si.detach().cpu(),
+               "d_ego_users": xl.grad[:n].cpu(), "d_ego_items": xl.grad[n:].cpu()}
+        for k, p in enc.named_parameters():
+            out["param." + k] = p.detach().cpu()
+            out["grad." + k] = None if p.grad is None else p.grad.cpu()
+        torch.save(out, os.path.join(outdir, f"r{rank}.pt"))
+        torch.cuda.synchronize()
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_local_aware_amazon_d128_user_row_sharded(dev, tmp_path):
+    """configs[3] user-row sharded: ShardedLocalAwareEncoder over 2 ranks (gloo between
+    processes sharing cuda:0; RCCL cannot put two ranks on one device), degree-balanced user
+    ranges, the reference's global drop-edge mask, eval mode. Users' rows from their owner, item
+    rows from every rank, the ego and weight gradients as the sum of the ranks' partials —
+    against the float64 reference at the same row bound."""
+    world = 2
+    mp.start_processes(_sharded_worker, args=(world, _free_port(), str(tmp_path)),
+                       nprocs=world, join=True, start_method="spawn")
+    parts = [torch.load(str(tmp_path / f"r{r}.pt"), weights_only=True) for r in range(world)]
+    U, I, nnz = AMAZON
+    N, d, L = U + I, 128, 3
+    ui, A = _graph(U, I, nnz, seed=30)
+    assert parts[0]["u0"] == 0 and parts[-1]["u1"] == U
+    state = {k[len("param."):]: v for k, v in parts[0].items() if k.startswith("param.")}
+    for p in parts[1:]:  # replicated weights are equal on every rank
+        for k, v in state.items():
+            assert torch.equal(p["param." + k], v), k
+    g = torch.Generator().manual_seed(33)
+    bound = (6.0 / (N + d)) ** 0.5
+    ego = (torch.rand(N, d, generator=g) * 2 - 1) * bound
+    G = torch.randn(N, d, generator=g)
+    Au = A.tocoo()
+    idx = torch.from_numpy(np.stack([Au.row, Au.col]).astype(np.int64))
+    val = torch.from_numpy(Au.data.astype(np.float32))
+    outR, gradsR, _ = _local_aware_reference(state, ui, idx, val, U, I, d, L, ego, G, [], 1.0,
+                                             0.8, 34)
+    users = torch.cat([p["users"] for p in parts])
+    worst = R.check_rows(users, outR[:U], "user rows")
+    for r, p in enumerate(parts):
+        worst = max(worst, R.check_rows(p["items"], outR[U:], f"item rows (rank {r})"))
+    worst = max(worst, R.check_rows(torch.cat([p["d_ego_users"] for p in parts]),
+                                    gradsR["ego"][:U], "d ego users"))
+    worst = max(worst, R.check_rows(sum(p["d_ego_items"] for p in parts), gradsR["ego"][U:],
+                                    "d ego items"))
+    for k in state:
+        gs = [p["grad." + k] for p in parts]
+        if gradsR[k] is None:
+            assert all(x is None for x in gs), k
+            continue
+        worst = max(worst, R.check_rows(sum(gs), gradsR[k], f"d {k}"))
+    print(f"sharded LocalAware Amazon d=128 x{world}: worst row ratio {worst:.2e}")
+
+
+# ---------------------------------------------------------------------------------------------
+# HCCF_diffusion's encoder, train mode
+# ---------------------------------------------------------------------------------------------
+def test_hccf_diffusion_encoder_train(dev):
+    """HCCFDiffusionEncoder (HCCF_diffusion.py:131-215), 2 layers, d = 32, K = 32, train mode:
+    drop-edge (keep 0.7), learned-hypergraph dropout (0.2) and the ED-HNN block's dropout (0.5)
+    drawn once for both sides; the output rows, per-layer GCN / hypergraph embeddings and the
+    gradients of every parameter for a fixed upstream gradient."""
+    from hypergraph_diffusion_for_recommendation_amd.encoders import HCCFDiffusionEncoder
+    U, I, nnz, d, L = 3_000, 4_000, 60_000, 32, 2
+    N = U + I
+    _, A = _graph(U, I, nnz, seed=40)
+    data = SimpleNamespace(n_users=U, n_items=I, norm_adj=A)
+    kw = dict(lrate=1e-3, lr_decay=0.9, max_epoch=1, batch_size=64, reg=0.01,
+              embedding_size=d, hyper_dim=32, drop_rate=0.2, p=0.3, n_layers=L)
+    torch.manual_seed(41)
+    enc = HCCFDiffusionEncoder(kw, data, device=dev).train()
+    enc.drop_out = R.FixedDropout(0.2, 42)
+    enc.edhnnlayer.dropout = R.FixedDropout(0.5, 43)
+    enc.edgeDropper = R.DropRecorder(enc.edgeDropper)
+    torch.manual_seed(44)
+    ue, ie, gcns, hyps = enc(keep_rate=0.7)
+    g = torch.Generator().manual_seed(45)
+    Gu, Gi = torch.randn(U, d, generator=g), torch.randn(I, d, generator=g)
+    Gh = [torch.randn(N, d, generator=g) for _ in range(L)]
+    tot = (ue * Gu.to(dev)).sum() + (ie * Gi.to(dev)).sum()
+    for layer in range(L):
+        tot = tot + (hyps[layer] * Gh[layer].to(dev)).sum()
+    tot.backward()
+
+    P = R.leaves(enc)
+    idx, vals = _coo_host(enc.sparse_norm_adj)
+    torch.manual_seed(44)
+    adjs = []
+    for layer in range(L):
+        di, dv = R.drop_edge_reference(idx, vals, 0.7)
+        gi, gv = enc.edgeDropper.outputs[layer]
+        assert torch.equal(di, gi) and torch.equal(dv, gv), f"drop-edge layer {layer}"
+        adjs.append(R.sparse(di, dv, (N, N)))
+    ueR, ieR, gR, hR = R.hccf_diffusion(P, adjs, enc.drop_out.masks, 0.8,
+                                        enc.edhnnlayer.dropout.masks, 0.5, U, L, 1e-5)
+    worst = max(R.check_rows(ue, ueR, "user_emb"), R.check_rows(ie, ieR, "item_emb"))
+    for layer in range(L):
+        worst = max(worst, R.check_rows(gcns[layer], gR[layer], f"gcn[{layer}]"),
+                    R.check_rows(hyps[layer], hR[layer], f"hyper[{layer}]"))
+    totR = (ueR * Gu.double()).sum() + (ieR * Gi.double()).sum()
+    for layer in range(L):
+        totR = totR + (hR[layer] * Gh[layer].double()).sum()
+    names = list(P)
+    gref = torch.autograd.grad(totR, [P[k] for k in names], allow_unused=True)
+    got = dict(enc.named_parameters())
+    for k, gr in zip(names, gref):
+        if gr is None:
+            assert got[k].grad is None or not got[k].grad.any(), k
+            continue
+        worst = max(worst, R.check_rows(got[k].grad, gr, f"d {k}"))
+    print(f"HCCF_diffusion train: worst row ratio {worst:.2e}")
+
+
+# ---------------------------------------------------------------------------------------------
+# configs[0] end to end: the HCCF plugin at n_layers = 1, d = 32 on a LastFM-shaped data file
+# ---------------------------------------------------------------------------------------------
+def test_hccf_plugin_lastfm_shape_executes(dev, tmp_path, monkeypatch):
+    """SELFRec(conf, kwargs).execute() of HCCF with conf/HCCF.conf's keys and --n_layers 1
+    --embedding_size 32 on a 1,891-user × 14,777-item train file (data/loader.py format): one
+    epoch trains and evaluates; the device ranking metrics equal the reference's
+    ranking_evaluation of the same top-K lists (oracle)."""
+    from hypergraph_diffusion_for_recommendation_amd.selfrec import (ModelConf, SELFRec,
+                                                                     default_args)
+    U, I, nnz = LASTFM
+    rng = np.random.default_rng(50)
+    root = tmp_path / "dataset" / "lastfm"
+    root.mkdir(parents=True)
+    users = rng.integers(0, U, nnz) * 5 + 3
+    items = rng.integers(0, I, nnz) * 11 + 7
+    with open(root / "train.txt", "w") as f:
+        f.write("user,item,rating\n")
+        f.writelines(f"{a},{b},1\n" for a, b in zip(users, items))
+    tu, ti = rng.integers(0, U, 20_000) * 5 + 3, rng.integers(0, I, 20_000) * 11 + 7
+    with open(root / "test.txt", "w") as f:
+        f.write("user\titem\trating\n")
+        f.writelines(f"{a}\t{b}\t1\n" for a, b in zip(tu, ti))
+    conf_text = ("training.set=train.txt\ntest.set=test.txt\ndataset=lastfm\nmodel.name=HCCF\n"
+                 "model.type=graph\nitem.ranking=-topN 10,20\nembedding.size=32\n"
+                 "num.max.epoch=500\nbatch_size=2048\nnum_layers=2\nlearnRate=0.001\n"
+                 "learnRateDecay=0.7\nreg.lambda=0.01\nuse.knowledge=false\nhyper.size=128\n"
+                 "ss_rate=1\ndropout=0.3\nleaky=0.5\ntemp=1\n")
+    (tmp_path / "HCCF.conf").write_text(conf_text)
+    monkeypatch.chdir(tmp_path)
+    conf = ModelConf(str(tmp_path / "HCCF.conf"))
+    kw = default_args(dataset='lastfm', max_epoch=1, n_layers=1, embedding_size=32,
+                      item_ranking='10,20', seed=7)
+    kw['dataset_root'] = str(tmp_path / "dataset")
+    rec = SELFRec(conf, kw).execute()
+    assert rec.data.n_users == len(set(users.tolist()))
+    assert rec.model.n_layers == 1 and rec.model.latent_size == 32
+    rec_list = rec.test()
+    assert rec.result == O.ranking_evaluation(rec.data.test_set, rec_list, rec.topN)
