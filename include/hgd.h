@@ -61,7 +61,8 @@ typedef enum hgd_epilogue {
  *   HGD_TUNE_SPMM_POLICY: 0 plain, 1 non-temporal Y stores, 8 software-pipelined index
  *                         batches (default), 9 both
  *   HGD_TUNE_SPMM_PASS_COLS: widest column pass of a hop without a fused row epilogue
- *                         (64, 128 or 256 fp32 columns; wider rows run as several passes) */
+ *                         (64, 128 or 256 fp32 columns; wider rows run as several passes;
+ *                         0 = auto, the default: one pass up to 128 columns, else 64) */
 typedef enum hgd_tune_key {
   HGD_TUNE_SPMM_UNROLL = 1,
   HGD_TUNE_SPMM_POLICY = 2,

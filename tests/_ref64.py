@@ -78,6 +78,60 @@ def drop_edge_reference(indices: torch.Tensor, values: torch.Tensor, keep: float
     return indices[:, mask], values[mask] / keep
 
 
+class ReluMasks:
+    """The device's ReLU decisions, recorded in call order (:meth:`wrap_linear` for the fused
+    ``Linear(..., relu=True)``, :meth:`module` for an ``nn.ReLU``), replayed by the reference's
+    :func:`relu`. A ReLU's derivative at a pre-activation within fp32 rounding of zero is
+    decided by that rounding (the reference's own fp32 run could go either way), so the
+    reference takes the device's mask — after checking that every element where it disagrees
+    with the float64 sign lies within TOL of zero relative to its row (``flips`` counts them)."""
+
+    def __init__(self):
+        self.masks: List[torch.Tensor] = []
+        self.pos = 0
+        self.flips = 0
+
+    def wrap_linear(self, lin):
+        orig = lin.forward
+
+        def forward(x, relu=False):
+            y = orig(x, relu)
+            if relu:
+                self.masks.append((y > 0).detach().cpu())
+            return y
+
+        lin.forward = forward
+
+    def module(self) -> nn.Module:
+        rec = self
+
+        class _Relu(nn.Module):
+            def forward(self, x):
+                y = torch.relu(x)
+                rec.masks.append((y > 0).detach().cpu())
+                return y
+
+        return _Relu()
+
+    def take(self, x: torch.Tensor) -> torch.Tensor:
+        m = self.masks[self.pos]
+        self.pos += 1
+        v = x.detach()
+        flipped = (v > 0) != m
+        if bool(flipped.any()):
+            scale = v.abs().amax(-1, keepdim=True).expand_as(v)
+            assert bool((v[flipped].abs() <= TOL * scale[flipped]).all()), \
+                "device ReLU mask differs from the reference at a clearly signed element"
+            self.flips += int(flipped.sum())
+        return m
+
+
+def relu(x: torch.Tensor, masks: "ReluMasks" = None) -> torch.Tensor:
+    if masks is None:
+        return F.relu(x)
+    return x * masks.take(x).to(x.dtype)
+
+
 def sparse(indices, values, shape, dtype=torch.float64) -> torch.Tensor:
     i = torch.as_tensor(np.asarray(indices), dtype=torch.int64)
     v = torch.as_tensor(np.asarray(values)).to(dtype)
@@ -137,8 +191,48 @@ def hccf_encoder(P: Dict[str, torch.Tensor], adjs: List[torch.Tensor],
     return emb[:n_users], emb[n_users:], gcn_l, hyp_l
 
 
+class Probe:
+    """Records, per weight of the reference forward, every use's input and (grad-retaining)
+    output, so that after ``backward`` (not ``autograd.grad``: the outputs' ``.grad`` must be
+    populated) the weight gradient's bound can be formed from the reduction it is
+    (:func:`check_weight_grad`). A weight shared between calls (HCCF_diffusion's one ED-HNN
+    block, called for users and items in every layer) keeps every use."""
+
+    def __init__(self):
+        self.uses: Dict[str, list] = {}
+
+    def _add(self, name, entry_w, entry_b):
+        self.uses.setdefault(name + ".weight", []).append(entry_w)
+        self.uses.setdefault(name + ".bias", []).append(entry_b)
+
+    def linear(self, name: str, x, y):
+        y.retain_grad()
+        self._add(name, ("linear_w", x, y), ("bias", x, y))
+
+    def layer_norm(self, name: str, x, y, eps: float):
+        y.retain_grad()
+        xd = x.detach()
+        mu = xd.mean(-1, keepdim=True)
+        xh = (xd - mu) * torch.rsqrt(xd.var(-1, unbiased=False, keepdim=True) + eps)
+        self._add(name, ("ln_w", xh, y), ("bias", xh, y))
+
+
+def _lin(x, P, name, probe):
+    y = F.linear(x, P[name + ".weight"], P[name + ".bias"])
+    if probe is not None:
+        probe.linear(name, x, y)
+    return y
+
+
+def _ln(x, P, name, eps, probe):
+    y = F.layer_norm(x, (x.shape[-1],), P[name + ".weight"], P[name + ".bias"], eps)
+    if probe is not None:
+        probe.layer_norm(name, x, y, eps)
+    return y
+
+
 def edhnn_block(x, P, prefix: str, mean_e, mean_v, masks: List[torch.Tensor], keep: float,
-                ln_eps: float):
+                ln_eps: float, relu_masks: ReluMasks = None, probe: Probe = None):
     """EquivSetGNN2.forward (:83-103) for HGNN_HD4's edhnn_config: dropout → ReLU(lin_in) →
     dropout → EquivSetConv (Xe = mean over each hyperedge's vertices, Xv = mean over each
     vertex's hyperedges, α = 0, W = Linear(LayerNorm(·))) → ReLU → dropout. ``masks``: the
@@ -147,18 +241,18 @@ def edhnn_block(x, P, prefix: str, mean_e, mean_v, masks: List[torch.Tensor], ke
         return t * masks[k].to(t.dtype) / keep if masks else t
 
     x = drop(x, 0)
-    x = F.relu(F.linear(x, P[prefix + "lin_in.weight"], P[prefix + "lin_in.bias"]))
+    x = relu(_lin(x, P, prefix + "lin_in", probe), relu_masks)
     x = drop(x, 1)
     xv = torch.sparse.mm(mean_v, torch.sparse.mm(mean_e, x))
     W = prefix + "conv.W."
-    xn = F.layer_norm(xv, (xv.shape[-1],), P[W + "normalizations.0.weight"],
-                      P[W + "normalizations.0.bias"], ln_eps)
-    x = F.relu(F.linear(xn, P[W + "lins.0.weight"], P[W + "lins.0.bias"]))
+    xn = _ln(xv, P, W + "normalizations.0", ln_eps, probe)
+    x = relu(_lin(xn, P, W + "lins.0", probe), relu_masks)
     return drop(x, 2)
 
 
 def local_aware(ego, P, n_layers: int, mean_e, mean_v, adj, masks: List[torch.Tensor],
-                keep: float, ln_eps: float, prefix: str = ""):
+                keep: float, ln_eps: float, prefix: str = "", relu_masks: ReluMasks = None,
+                probe: Probe = None):
     """LocalAwareEncoder.forward (HGNN_HD4.py:390-405): layers 0..L-2 ED-HNN blocks on V/E =
     nonzero(ui_adj) plus the layer-0 residual; the last LN0(A·(Aᵀ·x)) + residual (HGCNConv
     act=False, :450-462)."""
@@ -167,11 +261,10 @@ def local_aware(ego, P, n_layers: int, mean_e, mean_v, adj, masks: List[torch.Te
     for k in range(n_layers):
         if k != n_layers - 1:
             ego = edhnn_block(ego, P, f"{prefix}edhnn_layers.{k}.", mean_e, mean_v,
-                              masks[3 * k:3 * k + 3], keep, ln_eps) + res
+                              masks[3 * k:3 * k + 3], keep, ln_eps, relu_masks, probe) + res
         else:
             z = torch.sparse.mm(adj, torch.sparse.mm(adj_t, ego))
-            ego = F.layer_norm(z, (z.shape[-1],), P[prefix + "lns.0.weight"],
-                               P[prefix + "lns.0.bias"], ln_eps) + res
+            ego = _ln(z, P, prefix + "lns.0", ln_eps, probe) + res
     return ego
 
 
@@ -186,7 +279,8 @@ def nonzero_mean_operators(H: torch.Tensor, n_nodes: int):
 
 
 def hccf_diffusion(P, adjs, hyper_masks, keep_h: float, blk_masks, keep_b: float, n_users: int,
-                   n_layers: int, ln_eps: float):
+                   n_layers: int, ln_eps: float, relu_masks: ReluMasks = None,
+                   probe: Probe = None):
     """HCCF_diffusion.py:173-215: per layer the GCN hop plus one shared ED-HNN block on the
     learned hypergraphs dropout(E·W) of users and of items (V/E = nonzero(H > 0); the block
     sees only their structure). ``blk_masks``: 3 per block call, users then items."""
@@ -205,8 +299,10 @@ def hccf_diffusion(P, adjs, hyper_masks, keep_h: float, blk_masks, keep_b: float
         ei, vi = nonzero_mean_operators(Hi, n_i)
         bu = blk_masks[6 * layer:6 * layer + 3]
         bi = blk_masks[6 * layer + 3:6 * layer + 6]
-        hyp_u = edhnn_block(h[:n_users], P, "edhnnlayer.", eu, vu, bu, keep_b, ln_eps)
-        hyp_i = edhnn_block(h[n_users:], P, "edhnnlayer.", ei, vi, bi, keep_b, ln_eps)
+        hyp_u = edhnn_block(h[:n_users], P, "edhnnlayer.", eu, vu, bu, keep_b, ln_eps,
+                            relu_masks, probe)
+        hyp_i = edhnn_block(h[n_users:], P, "edhnnlayer.", ei, vi, bi, keep_b, ln_eps,
+                            relu_masks, probe)
         gcn_l.append(gcn)
         hyp_l.append(torch.cat([hyp_u, hyp_i], 0))
         hidden.append(gcn + hyp_l[-1])
@@ -261,3 +357,37 @@ def check_rows(got, ref, what: str, tol: float = TOL) -> float:
                              f"{float(scale[k]):.3e} (ratio {worst:.3e} > {tol:g}); "
                              f"{int((ratio > tol).sum())} / {ratio.numel()} rows out")
     return worst
+
+
+def check_weight_grad(got, ref, entries, what: str, tol: float = TOL) -> float:
+    """A weight gradient is a reduction over the N rows of (upstream gradient, op input) pairs:
+    dW = Σ_n dY_nᵀ·X_n (Linear), dγ = Σ_n dY_n ⊙ x̂_n (LayerNorm), db = dβ = Σ_n dY_n. Its
+    operands are row-bounded (every row within TOL of its scale, :func:`check_rows`), and the
+    reduction's own fp32 rounding is at most a few ulp of Σ|terms| (blocked / split-K sums).
+    So the element-wise bound is TOL times the first-order propagation of the operands' row
+    errors through the sum — Σ_n (‖dY_n‖∞·|X_n| + |dY_n|·‖X_n‖∞) — which is ≥ Σ|terms| of the
+    reduction. ``entries``: the (kind, input, output) records of every use of the weight (a
+    block shared between calls contributes each call's terms)."""
+    bound = None
+    for kind, x, y in entries:
+        dy = y.grad.detach()
+        ax = x.detach().abs()
+        sdy = dy.abs().amax(-1, keepdim=True)
+        sx = ax.amax(-1, keepdim=True)
+        if kind == "linear_w":
+            b = sdy.expand_as(dy).T @ ax + dy.abs().T @ sx.expand_as(ax)
+        elif kind == "ln_w":
+            b = (sdy * ax + dy.abs() * sx).sum(0)
+        else:  # bias / β
+            b = sdy.expand_as(dy).sum(0)
+        bound = b if bound is None else bound + b
+    g = got.detach().to(device="cpu", dtype=torch.float64)
+    r = ref.detach().to(torch.float64)
+    assert g.shape == r.shape == bound.shape, (what, g.shape, r.shape, bound.shape)
+    err = (g - r).abs()
+    ratio = float((err / bound).max())
+    if ratio > tol:
+        i = tuple(int(k) for k in (err > tol * bound).nonzero()[0])
+        raise AssertionError(f"{what}: element {i} off by {float(err[i]):.3e}, reduction bound "
+                             f"{float(tol * bound[i]):.3e} (ratio {ratio:.3e} > {tol:g})")
+    return ratio

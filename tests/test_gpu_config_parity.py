@@ -17,7 +17,10 @@ drop-edge structure itself must equal the reference's CPU draw bit for bit).
 Bounds (tests/_ref64.py, calibrated in tests/test_ref64.py): every row of every output and
 gradient within 1e-5 of that row's largest |value| (north_star's "fp32 within 1e-5 relative",
 no absolute floor); scalar losses — means of positive terms (−log σ, −log softmax) — within
-1e-5 relative.
+1e-5 relative. A ReLU whose pre-activation lies within fp32 rounding of zero has no defined
+fp32 derivative (the reference's own fp32 run could take either branch; at 10^7 elements a
+few such elements occur): there the reference replays the device's decision, after checking
+that every disagreement is such an element (tests/_ref64.py ReluMasks).
 """
 import os
 import socket
@@ -129,7 +132,7 @@ def test_hccf_yelp_3layer_d64_infonce_train_step(dev):
 # HGNN_HD4's local (ED-HNN) encoder (configs[3])
 # ---------------------------------------------------------------------------------------------
 def _local_aware_reference(enc_state, ui, A_idx, A_val, U, I, d, n_layers, ego, G, masks,
-                           keep_b, drop_keep, seed_drop, prefix=""):
+                           keep_b, drop_keep, seed_drop, relu_masks, prefix=""):
     """float64 LocalAwareEncoder forward + backward; returns (out, grads by name incl. 'ego')."""
     N = U + I
     P = {k: v.detach().cpu().double().requires_grad_(True) for k, v in enc_state.items()}
@@ -141,11 +144,27 @@ def _local_aware_reference(enc_state, ui, A_idx, A_val, U, I, d, n_layers, ego, 
         di, dv = A_idx, A_val
     adj = R.sparse(di, dv, (N, N))
     x = ego.detach().cpu().double().requires_grad_(True)
-    out = R.local_aware(x, P, n_layers, mean_e, mean_v, adj, masks, keep_b, 1e-5, prefix)
-    names = list(P)
-    grads = torch.autograd.grad(out, [x] + [P[k] for k in names], G.double(),
-                                allow_unused=True)
-    return out, dict(zip(["ego"] + names, grads)), (di, dv)
+    probe = R.Probe()
+    out = R.local_aware(x, P, n_layers, mean_e, mean_v, adj, masks, keep_b, 1e-5, prefix,
+                        relu_masks, probe)
+    out.backward(G.double())
+    grads = {"ego": x.grad, **{k: v.grad for k, v in P.items()}}
+    return out.detach(), grads, (di, dv), probe
+
+
+def _check_params(named_grads, gradsR, probe):
+    """Weights used in a reduction over the node rows (Linear, LayerNorm): the reduction bound
+    (tests/_ref64.py check_weight_grad); anything else row-bound."""
+    worst = 0.0
+    for k, g in named_grads.items():
+        if gradsR[k] is None:  # lns[1:] are unused by the reference too
+            assert g is None, k
+            continue
+        if k in probe.uses:
+            worst = max(worst, R.check_weight_grad(g, gradsR[k], probe.uses[k], f"d {k}"))
+        else:
+            worst = max(worst, R.check_rows(g, gradsR[k], f"d {k}"))
+    return worst
 
 
 def test_local_aware_amazon_d128_train(dev):
@@ -162,8 +181,11 @@ def test_local_aware_amazon_d128_train(dev):
     torch.manual_seed(31)
     enc = LocalAwareEncoder(data, d, d, L, 0.3, 0.2, device=dev).train()
     fd = R.FixedDropout(0.5, 32)
+    rm = R.ReluMasks()
     for blk in enc.edhnn_layers:
         blk.dropout = fd
+        rm.wrap_linear(blk.lin_in)
+        blk.act = rm.module()
     g = torch.Generator().manual_seed(33)
     bound = (6.0 / (N + d)) ** 0.5
     ego = (torch.rand(N, d, generator=g) * 2 - 1) * bound
@@ -178,18 +200,16 @@ def test_local_aware_amazon_d128_train(dev):
 
     idx, vals = _coo_host(enc.sparse_norm_adj)
     state = dict(enc.named_parameters())
-    outR, gradsR, (di, dv) = _local_aware_reference(state, ui, idx, vals, U, I, d, L, ego, G,
-                                                    fd.masks, 0.5, 0.8, 34)
+    outR, gradsR, (di, dv), probe = _local_aware_reference(state, ui, idx, vals, U, I, d, L,
+                                                           ego, G, fd.masks, 0.5, 0.8, 34, rm)
+    assert rm.pos == len(rm.masks) == 2 * (L - 1)
     gi, gv = _coo_host(dropped)
     assert torch.equal(di, gi) and torch.equal(dv, gv), "drop-edge structure"
     worst = R.check_rows(out, outR, "output")
     worst = max(worst, R.check_rows(x.grad, gradsR["ego"], "d ego"))
-    for k, p in state.items():
-        if gradsR[k] is None:  # lns[1:] are unused by the reference too
-            assert p.grad is None, k
-            continue
-        worst = max(worst, R.check_rows(p.grad, gradsR[k], f"d {k}"))
-    print(f"LocalAware Amazon d=128: worst row ratio {worst:.2e}")
+    worst = max(worst, _check_params({k: p.grad for k, p in state.items()}, gradsR, probe))
+    print(f"LocalAware Amazon d=128: worst row ratio {worst:.2e}; {rm.flips} ReLU decisions "
+          f"within fp32 rounding of zero taken from the device")
 
 
 def _free_port():
@@ -216,6 +236,10 @@ def _sharded_worker(rank, world, port, outdir):
         torch.manual_seed(31)
         enc = SE.ShardedLocalAwareEncoder(data, d, d, L, 0.3, 0.2, u0, u1, device=dev,
                                           n_chunks=3).eval()
+        rm = R.ReluMasks()
+        for blk in enc.edhnn_layers:
+            rm.wrap_linear(blk.lin_in)
+            blk.act = rm.module()
         g = torch.Generator().manual_seed(33)
         bound = (6.0 / (N + d)) ** 0.5
         ego = (torch.rand(N, d, generator=g) * 2 - 1) * bound
@@ -224,10 +248,14 @@ def _sharded_worker(rank, world, port, outdir):
         dropped = enc.dropped(0.8, device_rng=False)  # the reference's global CPU mask
         xl = torch.cat([ego[u0:u1], ego[U:]]).to(dev).requires_grad_(True)
         su, si = enc(xl, dropped)
-        (torch.cat([su, si]) * torch.cat([G[u0:u1], G[U:]]).to(dev)).sum().backward()
+        # item outputs are replicated: their upstream gradient enters on one rank only (the
+        # loss counts every item once), each rank's item gradients are partials
+        Gi = G[U:] if rank == 0 else torch.zeros_like(G[U:])
+        (torch.cat([su, si]) * torch.cat([G[u0:u1], Gi]).to(dev)).sum().backward()
         n = u1 - u0
         out = {"u0": u0, "u1": u1, "users": su.detach().cpu(), "items": si.detach().cpu(),
-               "d_ego_users": xl.grad[:n].cpu(), "d_ego_items": xl.grad[n:].cpu()}
+               "d_ego_users": xl.grad[:n].cpu(), "d_ego_items": xl.grad[n:].cpu(),
+               "relu_users": [m[:n] for m in rm.masks], "relu_items": [m[n:] for m in rm.masks]}
         for k, p in enc.named_parameters():
             out["param." + k] = p.detach().cpu()
             out["grad." + k] = None if p.grad is None else p.grad.cpu()
@@ -263,8 +291,14 @@ def test_local_aware_amazon_d128_user_row_sharded(dev, tmp_path):
     Au = A.tocoo()
     idx = torch.from_numpy(np.stack([Au.row, Au.col]).astype(np.int64))
     val = torch.from_numpy(Au.data.astype(np.float32))
-    outR, gradsR, _ = _local_aware_reference(state, ui, idx, val, U, I, d, L, ego, G, [], 1.0,
-                                             0.8, 34)
+    rm = R.ReluMasks()  # the global masks: users from their owners, items (replicated) rank 0's
+    for k in range(len(parts[0]["relu_users"])):
+        for p in parts[1:]:
+            assert torch.equal(p["relu_items"][k], parts[0]["relu_items"][k])
+        rm.masks.append(torch.cat([p["relu_users"][k] for p in parts]
+                                  + [parts[0]["relu_items"][k]]))
+    outR, gradsR, _, probe = _local_aware_reference(state, ui, idx, val, U, I, d, L, ego, G,
+                                                    [], 1.0, 0.8, 34, rm)
     users = torch.cat([p["users"] for p in parts])
     worst = R.check_rows(users, outR[:U], "user rows")
     for r, p in enumerate(parts):
@@ -273,13 +307,13 @@ def test_local_aware_amazon_d128_user_row_sharded(dev, tmp_path):
                                     gradsR["ego"][:U], "d ego users"))
     worst = max(worst, R.check_rows(sum(p["d_ego_items"] for p in parts), gradsR["ego"][U:],
                                     "d ego items"))
+    summed = {}
     for k in state:
         gs = [p["grad." + k] for p in parts]
-        if gradsR[k] is None:
-            assert all(x is None for x in gs), k
-            continue
-        worst = max(worst, R.check_rows(sum(gs), gradsR[k], f"d {k}"))
-    print(f"sharded LocalAware Amazon d=128 x{world}: worst row ratio {worst:.2e}")
+        summed[k] = None if all(x is None for x in gs) else sum(gs)
+    worst = max(worst, _check_params(summed, gradsR, probe))
+    print(f"sharded LocalAware Amazon d=128 x{world}: worst row ratio {worst:.2e}; "
+          f"{rm.flips} ReLU decisions within fp32 rounding of zero taken from the device")
 
 
 # ---------------------------------------------------------------------------------------------
@@ -301,6 +335,9 @@ def test_hccf_diffusion_encoder_train(dev):
     enc = HCCFDiffusionEncoder(kw, data, device=dev).train()
     enc.drop_out = R.FixedDropout(0.2, 42)
     enc.edhnnlayer.dropout = R.FixedDropout(0.5, 43)
+    rm = R.ReluMasks()
+    rm.wrap_linear(enc.edhnnlayer.lin_in)
+    enc.edhnnlayer.act = rm.module()
     enc.edgeDropper = R.DropRecorder(enc.edgeDropper)
     torch.manual_seed(44)
     ue, ie, gcns, hyps = enc(keep_rate=0.7)
@@ -321,8 +358,9 @@ def test_hccf_diffusion_encoder_train(dev):
         gi, gv = enc.edgeDropper.outputs[layer]
         assert torch.equal(di, gi) and torch.equal(dv, gv), f"drop-edge layer {layer}"
         adjs.append(R.sparse(di, dv, (N, N)))
+    probe = R.Probe()
     ueR, ieR, gR, hR = R.hccf_diffusion(P, adjs, enc.drop_out.masks, 0.8,
-                                        enc.edhnnlayer.dropout.masks, 0.5, U, L, 1e-5)
+                                        enc.edhnnlayer.dropout.masks, 0.5, U, L, 1e-5, rm, probe)
     worst = max(R.check_rows(ue, ueR, "user_emb"), R.check_rows(ie, ieR, "item_emb"))
     for layer in range(L):
         worst = max(worst, R.check_rows(gcns[layer], gR[layer], f"gcn[{layer}]"),
@@ -330,15 +368,15 @@ def test_hccf_diffusion_encoder_train(dev):
     totR = (ueR * Gu.double()).sum() + (ieR * Gi.double()).sum()
     for layer in range(L):
         totR = totR + (hR[layer] * Gh[layer].double()).sum()
-    names = list(P)
-    gref = torch.autograd.grad(totR, [P[k] for k in names], allow_unused=True)
-    got = dict(enc.named_parameters())
-    for k, gr in zip(names, gref):
-        if gr is None:
-            assert got[k].grad is None or not got[k].grad.any(), k
-            continue
-        worst = max(worst, R.check_rows(got[k].grad, gr, f"d {k}"))
-    print(f"HCCF_diffusion train: worst row ratio {worst:.2e}")
+    totR.backward()
+    got = {k: p.grad for k, p in enc.named_parameters()}
+    gradsR = {k: v.grad for k, v in P.items()}
+    for k in ("embedding_dict.user_w", "embedding_dict.item_w"):  # structure only: no gradient
+        assert gradsR[k] is None and (got[k] is None or not got[k].any()), k
+        got[k] = gradsR[k] = None
+    worst = max(worst, _check_params(got, gradsR, probe))
+    print(f"HCCF_diffusion train: worst row ratio {worst:.2e}; {rm.flips} ReLU decisions "
+          f"within fp32 rounding of zero taken from the device")
 
 
 # ---------------------------------------------------------------------------------------------

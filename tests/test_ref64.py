@@ -8,7 +8,8 @@ precision the reference itself runs in — and in float64:
   rows ~1e-6 through the ED-HNN stack, but up to ~6.5e-6 through HCCF's BPR + InfoNCE losses
   and the learned-hypergraph products — fp32 gradient rows that sum many signed terms come
   within 1.5x of the bound, so 1e-5 is the tightest row bound fp32 arithmetic itself meets;
-* an error of 2e-5 of one row's scale is rejected, so the bound is not vacuous.
+* an error of 2e-5 of one row's scale is rejected, so the bound is not vacuous;
+* the weight gradients (reductions over all node rows) also meet ``check_weight_grad``.
 """
 import numpy as np
 import pytest
@@ -53,11 +54,12 @@ def _local_aware(dtype, n_layers=3):
     adj = R.sparse(idx, vals, (N, N), dtype)
     g = torch.Generator().manual_seed(3)
     masks = [torch.empty(N, D).bernoulli_(0.5, generator=g) for _ in range(3 * (n_layers - 1))]
-    out = R.local_aware(ego, P, n_layers, mean_e, mean_v, adj, masks, 0.5, 1e-5)
+    probe = R.Probe()
+    out = R.local_aware(ego, P, n_layers, mean_e, mean_v, adj, masks, 0.5, 1e-5, probe=probe)
     G = torch.randn(N, D, generator=g, dtype=torch.float64).to(dtype)
-    names = list(P)
-    grads = torch.autograd.grad(out, [ego] + [P[k] for k in names], G)
-    return out, dict(zip(["ego"] + names, grads))
+    out.backward(G)
+    grads = {"ego": ego.grad, **{k: v.grad for k, v in P.items()}}
+    return out.detach(), grads, probe
 
 
 def _hccf(dtype, n_layers=2, K=8):
@@ -92,13 +94,17 @@ def _hccf(dtype, n_layers=2, K=8):
 
 
 def test_fp32_local_aware_meets_the_row_bound():
-    o64, g64 = _local_aware(torch.float64)
-    o32, g32 = _local_aware(torch.float32)
+    o64, g64, probe = _local_aware(torch.float64)
+    o32, g32, _ = _local_aware(torch.float32)
     worst = R.check_rows(o32, o64, "forward")
     for k in g64:
         worst = max(worst, R.check_rows(g32[k], g64[k], f"d {k}"))
     print(f"fp32 LocalAware worst row ratio {worst:.2e}")
     assert worst < 5e-6
+    # the weight gradients' reduction bound (check_weight_grad) holds too, with a wide margin
+    wr = max(R.check_weight_grad(g32[k], g64[k], probe.uses[k], f"d {k}") for k in probe.uses)
+    print(f"fp32 LocalAware worst weight-gradient reduction ratio {wr:.2e}")
+    assert wr < 1e-6
 
 
 def test_fp32_hccf_with_losses_meets_the_row_bound():
@@ -111,7 +117,7 @@ def test_fp32_hccf_with_losses_meets_the_row_bound():
 
 
 def test_row_bound_rejects_an_error_above_it():
-    o64, _ = _local_aware(torch.float64)
+    o64, _, _ = _local_aware(torch.float64)
     bad = o64.detach().clone()
     bad[7, 3] += 2e-5 * bad[7].abs().max()
     with pytest.raises(AssertionError):
