@@ -1,5 +1,7 @@
-"""GPU: the encoder callers against the golden HCCF vectors and a CPU restatement of
-LocalAwareEncoder (eval mode: dropout off, keep_rate = 1)."""
+"""GPU: the encoder callers against the golden HCCF vectors and float64 CPU restatements of
+LocalAwareEncoder and HCCF_diffusion's encoder (eval mode: dropout off, keep_rate = 1). Bound:
+every row within 1e-5 of its scale (tests/_ref64.py check_rows; the train-mode forward and
+backward at the configs' shapes are in test_gpu_config_parity.py)."""
 import copy
 import os
 from types import SimpleNamespace
@@ -11,6 +13,7 @@ import torch
 
 from oracle import hgd_oracle as O
 from oracle import ref_cpu
+from tests import _ref64 as R
 from tests._util import random_coo
 
 pytestmark = pytest.mark.gpu
@@ -32,10 +35,10 @@ def test_hccf_encoder_golden(dev):
             name = {"E_u": "user_emb", "E_i": "item_emb", "W_u": "user_w", "W_i": "item_w"}[k]
             enc.embedding_dict[name].copy_(torch.from_numpy(g[k]))
         ue, ie, gcns, hyps = enc(keep_rate=1)
-    for got, ref in ((ue, g["user_emb"]), (ie, g["item_emb"]), (gcns[0], g["gcn0"]),
-                     (gcns[1], g["gcn1"]), (hyps[0], g["hyp0"]), (hyps[1], g["hyp1"])):
-        err = np.abs(got.cpu().numpy() - ref).max()
-        assert err <= 1e-5 * max(1.0, np.abs(ref).max()), err
+    for name, got, ref in (("user_emb", ue, g["user_emb"]), ("item_emb", ie, g["item_emb"]),
+                           ("gcn0", gcns[0], g["gcn0"]), ("gcn1", gcns[1], g["gcn1"]),
+                           ("hyp0", hyps[0], g["hyp0"]), ("hyp1", hyps[1], g["hyp1"])):
+        R.check_rows(got, torch.from_numpy(ref), name)
 
 
 def test_hccf_encoder_trains(dev):
@@ -70,26 +73,24 @@ def test_local_aware_encoder_eval(dev):
     adj = enc.sparse_norm_adj
     with torch.no_grad():
         ue, ie = enc(ego.to(dev), adj)
-    # CPU restatement of HGNN_HD4.py:390-405 with the same parameters
-    ec = copy.deepcopy(enc).cpu().eval()
+    # float64 CPU restatement of HGNN_HD4.py:390-405 with the same parameters
+    ec = copy.deepcopy(enc).cpu().double().eval()
     dense = torch.tensor(ui.todense(), dtype=torch.float32)
     nz = torch.nonzero(dense > 0)
     V, E = nz[:, 0], nz[:, 1]
     idx, vals = O.coo_of(A)
-    adj_c = ref_cpu.coo_tensor(idx[0], idx[1], vals, A.shape)
-    x = ego
+    adj_c = ref_cpu.coo_tensor(idx[0], idx[1], vals, A.shape).double()
+    x = ego.double()
     with torch.no_grad():
         for k in range(3):
             if k != 2:
                 blk = ec.edhnn_layers[k]
                 h = torch.relu(blk.lin_in(x))
                 h = ref_cpu.equivset_conv(h, V, E, h, blk.conv.W1, None, blk.conv.W, 0.0, "mean")
-                x = torch.relu(h) + ego
+                x = torch.relu(h) + ego.double()
             else:
-                x = ec.lns[0](ref_cpu.hgcn_conv(adj_c, x, act=False)) + ego
-    ref = x.numpy()
-    got = torch.cat([ue, ie]).cpu().numpy()
-    assert np.abs(got - ref).max() <= 2e-5 * max(1.0, np.abs(ref).max())
+                x = ec.lns[0](ref_cpu.hgcn_conv(adj_c, x, act=False)) + ego.double()
+    R.check_rows(torch.cat([ue, ie]), x, "LocalAwareEncoder")
 
 
 def test_hccf_diffusion_encoder_eval(dev):
@@ -106,10 +107,10 @@ def test_hccf_diffusion_encoder_eval(dev):
     enc = HCCFDiffusionEncoder(HCCF_KW, data, device=dev).eval()
     with torch.no_grad():
         ue, ie, gcns, hyps = enc(keep_rate=1)
-    ec = copy.deepcopy(enc).cpu().eval()
+    ec = copy.deepcopy(enc).cpu().double().eval()
     e = {k: v.detach().cpu() for k, v in ec.embedding_dict.items()}
     idx, vals = O.coo_of(A)
-    adj_c = ref_cpu.coo_tensor(idx[0], idx[1], vals, A.shape)
+    adj_c = ref_cpu.coo_tensor(idx[0], idx[1], vals, A.shape).double()
     K = e["user_w"].shape[1]
     blk = ec.edhnnlayer
 
@@ -126,10 +127,8 @@ def test_hccf_diffusion_encoder_eval(dev):
         for layer in range(HCCF_KW["n_layers"]):
             gcn = torch.sparse.mm(adj_c, hidden[-1])
             hyp = torch.cat([edhnn(hidden[-1][:U], huu, U + K), edhnn(hidden[-1][U:], hii, I + K)])
-            for got, ref in ((gcns[layer], gcn), (hyps[layer], hyp)):
-                assert np.abs(got.cpu().numpy() - ref.numpy()).max() <= 2e-5 * max(
-                    1.0, ref.abs().max().item()), layer
+            R.check_rows(gcns[layer], gcn, f"gcn[{layer}]")
+            R.check_rows(hyps[layer], hyp, f"hyper[{layer}]")
             hidden.append(gcn + hyp)
         emb = sum(hidden)
-    assert np.abs(torch.cat([ue, ie]).cpu().numpy() - emb.numpy()).max() <= 2e-5 * max(
-        1.0, emb.abs().max().item())
+    R.check_rows(torch.cat([ue, ie]), emb, "HCCFDiffusionEncoder")

@@ -7,6 +7,7 @@ import torch
 
 from oracle import hgd_oracle as O
 from oracle import ref_cpu
+from tests import _ref64 as R
 from tests._util import random_coo
 
 pytestmark = pytest.mark.gpu
@@ -33,15 +34,14 @@ def test_equivset_gnn_eval_matches_reference(dev):
     m = EquivSetGNN(32, EDHNN_ARGS, dense).to(dev).eval()
     x = torch.randn(N, 32)
     y = m(x.to(dev), dense, N)
-    # CPU restatement with the same parameters
-    mc = copy.deepcopy(m).cpu().eval()
+    # float64 CPU restatement with the same parameters; every row within 1e-5 (tests/_ref64.py)
+    mc = copy.deepcopy(m).cpu().double().eval()
     nz = torch.nonzero(dense > 0)
     V, E = nz[:, 0], nz[:, 1]
-    h = torch.relu(mc.lin_in(x))
+    h = torch.relu(mc.lin_in(x.double()))
     h = ref_cpu.equivset_conv(h, V, E, h, mc.conv.W1, None, mc.conv.W, 0.0, "mean")
     ref = torch.relu(h)
-    err = (y.detach().cpu() - ref).abs().max().item()
-    assert err <= 1e-5 * max(1.0, ref.abs().max().item()), err
+    R.check_rows(y, ref, "EquivSetGNN")
     Vg, Eg = m.generate_V_E(N, dense)
     assert torch.equal(Vg.cpu(), V) and torch.equal(Eg.cpu(), E)
 
@@ -63,14 +63,12 @@ def test_equivset_conv_paths(dev, aggr, mlp2):
     Xg = X.to(dev).requires_grad_(True)
     y = conv(Xg, V.to(dev), E.to(dev), X0.to(dev))
     y.sum().backward()
-    cc = copy.deepcopy(conv).cpu().eval()
-    Xc = X.clone().requires_grad_(True)
-    ref = ref_cpu.equivset_conv(Xc, V, E, X0, cc.W1, cc.W2, cc.W, 0.3, aggr)
+    cc = copy.deepcopy(conv).cpu().double().eval()
+    Xc = X.double().requires_grad_(True)
+    ref = ref_cpu.equivset_conv(Xc, V, E, X0.double(), cc.W1, cc.W2, cc.W, 0.3, aggr)
     ref.sum().backward()
-    scale = max(1.0, ref.abs().max().item())
-    assert (y.detach().cpu() - ref).abs().max().item() <= 2e-5 * scale
-    gs = max(1.0, Xc.grad.abs().max().item())
-    assert (Xg.grad.cpu() - Xc.grad).abs().max().item() <= 2e-5 * gs
+    R.check_rows(y, ref, "EquivSetConv")
+    R.check_rows(Xg.grad, Xc.grad, "d X")
 
 
 def test_spadj_dropedge_layer_bit_exact(dev):
@@ -119,20 +117,19 @@ def test_spmm_form_equivset_gnn(dev, mlp2):
     xg = x.to(dev).requires_grad_(True)
     y = m(xg, adj.to(dev), N)
     y.square().sum().backward()
-    mc = copy.deepcopy(m).cpu().eval()
-    xc = x.clone().requires_grad_(True)
+    mc = copy.deepcopy(m).cpu().double().eval()
+    adj64 = adj.double()
+    xc = x.double().requires_grad_(True)
     h = torch.relu(mc.lin_in(xc))
     c = mc.conv
     Xve = c.W1(h)
-    Xe = c.lns[0](ref_cpu.hgcn_conv(adj, Xve, act=True, slope=0.2)) + Xve
+    Xe = c.lns[0](ref_cpu.hgcn_conv(adj64, Xve, act=True, slope=0.2)) + Xve
     Xev = Xe if c.W2 is None else c.W2(torch.cat([h, Xe], -1))
-    Xv = c.lns[1](ref_cpu.hgcn_conv(adj, Xev, act=True, slope=0.2)) + Xev
+    Xv = c.lns[1](ref_cpu.hgcn_conv(adj64, Xev, act=True, slope=0.2)) + Xev
     ref = torch.relu(c.W((1 - c.alpha) * Xv + c.alpha * h))
     ref.square().sum().backward()
-    s = max(1.0, ref.abs().max().item())
-    assert (y.detach().cpu() - ref.detach()).abs().max().item() <= 2e-5 * s
-    gs = max(1.0, xc.grad.abs().max().item())
-    assert (xg.grad.cpu() - xc.grad).abs().max().item() <= 2e-5 * gs
+    R.check_rows(y, ref, "SpMM-form EquivSetGNN")
+    R.check_rows(xg.grad, xc.grad, "d x")
 
 
 def test_hgcnconv_dense_adjacency_dhcf(dev):
@@ -146,12 +143,12 @@ def test_hgcnconv_dense_adjacency_dhcf(dev):
     Xg = torch.from_numpy(X).to(dev).requires_grad_(True)
     y = HGCNConv(0.3)(A, Xg, act=True)
     y.sum().backward()
-    At = torch.from_numpy(Ad)
-    Xc = torch.from_numpy(X).requires_grad_(True)
+    At = torch.from_numpy(Ad).double()
+    Xc = torch.from_numpy(X).double().requires_grad_(True)
     ref = torch.nn.functional.leaky_relu(At @ (At.T @ Xc), 0.3)
     ref.sum().backward()
-    torch.testing.assert_close(y.detach().cpu(), ref.detach(), rtol=1e-5, atol=1e-5)
-    torch.testing.assert_close(Xg.grad.cpu(), Xc.grad, rtol=1e-5, atol=1e-5)
+    R.check_rows(y, ref, "HGCNConv(dense A)")
+    R.check_rows(Xg.grad, Xc.grad, "d X")
     r, c = np.nonzero(Ad)
     inc = A._hgd_incidence
     np.testing.assert_array_equal(inc.csr.col.cpu().numpy(), c)
@@ -204,11 +201,19 @@ def test_hgnn_layer_dense_two_hop(dev, n, K, d):
     Xd = X.detach().double().cpu().requires_grad_(True)
     Yd = Hd @ (Hd.T @ Xd)
     rH, rX = torch.autograd.grad(Yd, (Hd, Xd), dY.double().cpu())
-    # |err| <= 1e-5 · Σ|terms| (magnitude from the same products on |·|)
-    mag = Hd.abs() @ (Hd.abs().T @ Xd.abs())
-    assert ((Y.detach().double().cpu() - Yd.detach()).abs() <= 1e-5 * mag + 1e-12).all()
-    for g, r in ((gH, rH), (gX, rX)):
-        assert (g.double().cpu() - r).abs().max().item() <= 1e-5 * r.abs().max().item() * 50
+    # |err| <= 1e-5 · Σ|terms| element-wise, Σ|terms| from the same products on |·|:
+    #   Y = H·(Hᵀ·X)                  -> |H|·(|H|ᵀ·|X|)
+    #   dX = H·(Hᵀ·dY)                -> |H|·(|H|ᵀ·|dY|)
+    #   dH = dY·Mᵀ + X·dMᵀ, M = HᵀX,  -> |dY|·(|H|ᵀ|X|)ᵀ + |X|·(|H|ᵀ|dY|)ᵀ
+    #        dM = HᵀdY                   (the inner reductions' own terms expanded)
+    aH, aX, adY = Hd.abs().detach(), Xd.abs().detach(), dY.double().cpu().abs()
+    mag = aH @ (aH.T @ aX)
+    assert ((Y.detach().double().cpu() - Yd.detach()).abs() <= 1e-5 * mag + 1e-300).all()
+    mag_dX = aH @ (aH.T @ adY)
+    mag_dH = adY @ (aH.T @ aX).T + aX @ (aH.T @ adY).T
+    for g, r, m, what in ((gH, rH, mag_dH, "dH"), (gX, rX, mag_dX, "dX")):
+        err = (g.double().cpu() - r).abs()
+        assert (err <= 1e-5 * m + 1e-300).all(), (what, float((err / m).max()))
 
 
 def test_equivset_gnn_fresh_learned_hypergraph_each_call(dev):
@@ -226,13 +231,11 @@ def test_equivset_gnn_fresh_learned_hypergraph_each_call(dev):
         H = torch.randn(n, K, device=dev, generator=g)  # new tensor, likely the same address
         y = m(x, H, n)
         r, c = torch.nonzero(H > 0, as_tuple=True)
-        # reference math for this call's pattern: mean over edges, then over vertices
-        h = torch.relu(m.lin_in(x))
-        Xs = m.conv.W1(h)
-        cnt_e = torch.zeros(K, device=dev).index_add_(0, c, torch.ones_like(c, dtype=torch.float))
-        Xe = torch.zeros(K, 16, device=dev).index_add_(0, c, Xs[r]) / cnt_e.clamp(min=1)[:, None]
-        cnt_v = torch.zeros(n, device=dev).index_add_(0, r, torch.ones_like(r, dtype=torch.float))
-        Xv = torch.zeros(n, 16, device=dev).index_add_(0, r, Xe[c]) / cnt_v.clamp(min=1)[:, None]
-        ref = m.act(m.conv.W((1 - m.conv.alpha) * Xv + m.conv.alpha * h))
-        torch.testing.assert_close(y, ref, rtol=1e-4, atol=1e-5)
+        # this call's pattern, float64 (α = 0): mean over each hyperedge, then over each vertex
+        md = copy.deepcopy(m).cpu().double()
+        hd = torch.relu(md.lin_in(x.cpu().double()))
+        me = R.mean_operator(c.cpu().numpy(), r.cpu().numpy(), K, n)
+        mv = R.mean_operator(r.cpu().numpy(), c.cpu().numpy(), n, K)
+        ref64 = md.act(md.conv.W(torch.sparse.mm(mv, torch.sparse.mm(me, md.conv.W1(hd)))))
+        R.check_rows(y, ref64, f"call {step}")
         del H
