@@ -12,9 +12,9 @@ produces the hot path's input matrices (paths relative to /root/reference/HD_SEL
   :class:`~.incidence.Incidence` objects ready for the hops, or torch sparse tensors / scipy
   matrices for the reference harness.
 
-Parity: ids, structure and counts are bit-exact with the reference's dict loop and scipy;
-normalised values are within 1 ulp of ``np.power(rowsum, -0.5)`` (numpy's float32 power is not
-correctly rounded; ``hgd_degree_scale`` is), i.e. inside the path's 1e-5 relative tolerance.
+Parity: ids, structure, counts and the normalised values are bit-exact with the reference's
+dict loop and scipy (the per-row scale is numpy's own float32 ``np.power``, see
+:func:`normalize_graph_mat`).
 """
 from __future__ import annotations
 
@@ -92,16 +92,28 @@ def coalesce(rows: torch.Tensor, cols: torch.Tensor, n_rows: int,
 def normalize_graph_mat(rowptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor,
                         shape) -> torch.Tensor:
     """Values of Graph.normalize_graph_mat (data/graph.py:11-25) for a CSR with float32 values:
-    D^-1/2·A·D^-1/2 when square, D^-1·A otherwise (rowsum 0 → scale 0)."""
+    D^-1/2·A·D^-1/2 when square, D^-1·A otherwise (rowsum 0 → scale 0), bit-identical to the
+    reference's scipy path.
+
+    The float32 row sums (scipy sums the float32 matrix in float32) come from the device
+    (hgd_degree_scale with power 1); the N-element scale ``np.power(rowsum, -0.5)`` (or ``-1``)
+    is then taken with numpy itself, exactly the reference's call: numpy's float32 power is not
+    correctly rounded and its rounding depends on the host's SIMD dispatch, so only numpy on this
+    host reproduces it (N floats through PCIe, once per graph). The per-nonzero products
+    ``(a·d_r)·d_c`` run on the device in the reference's float32 order (hgd_normalize_values)."""
     lib = nat.load()
     dev = val.device
     n_rows, n_cols = shape
     square = n_rows == n_cols
-    d = torch.empty(n_rows, dtype=torch.float32, device=dev)
+    rowsum = torch.empty(n_rows, dtype=torch.float32, device=dev)
     st = _stream(dev)
     nat.check(lib.hgd_degree_scale(rowptr.data_ptr(), val.data_ptr() if val.numel() else None,
-                                   n_rows, -0.5 if square else -1.0, d.data_ptr(), st),
-              "hgd_degree_scale")
+                                   n_rows, 1.0, rowsum.data_ptr(), st), "hgd_degree_scale")
+    rs = rowsum.cpu().numpy().reshape(-1, 1)  # np.array(adj_mat.sum(1)): [n, 1] float32
+    with np.errstate(divide="ignore"):
+        d_inv = np.power(rs, -0.5 if square else -1).flatten()
+    d_inv[np.isinf(d_inv)] = 0.
+    d = torch.from_numpy(np.ascontiguousarray(d_inv, dtype=np.float32)).to(dev)
     out = torch.empty_like(val)
     if val.numel():
         nat.check(lib.hgd_normalize_values(rowptr.data_ptr(), col.data_ptr(), val.data_ptr(),

@@ -60,14 +60,12 @@ def test_interaction_graph_matches_reference(dev, n, nu, ni):
     assert np.array_equal(g.ui_adj.val.cpu().numpy(), counts)
     vals = _same_structure(g.norm_adj, norm)
     got = g.norm_adj.val.cpu().numpy()
-    # d_r·a·d_c with d = rowsum^-1/2 correctly rounded here, numpy's float32 power is not
-    # (≤ 1 ulp each): ≤ 4 ulp apart, far inside the path's 1e-5 relative tolerance
-    ulp = np.spacing(np.abs(vals).astype(np.float32))
-    assert (np.abs(got - vals) <= 4 * ulp).all()
+    # bit-identical to scipy's normalize_graph_mat (data/graph.py:11-25)
+    assert np.array_equal(got.view(np.uint32), np.asarray(vals, np.float32).view(np.uint32))
     assert np.array_equal(g.interaction_mat.val.cpu().numpy(), _same_structure(g.interaction_mat, R))
     v = _same_structure(g.norm_interaction_mat, normR)
-    assert (np.abs(g.norm_interaction_mat.val.cpu().numpy() - v)
-            <= 4 * np.spacing(np.abs(v).astype(np.float32))).all()
+    assert np.array_equal(g.norm_interaction_mat.val.cpu().numpy().view(np.uint32),
+                          np.asarray(v, np.float32).view(np.uint32))
     # the CSC side is the transpose
     t = _canon(adj.T.tocsr())
     assert np.array_equal(g.ui_adj.csc.rowptr.cpu().numpy(), t.indptr)
