@@ -25,6 +25,7 @@ The reference has no distributed code at all; this is new desi
 """
 from __future__ import annotations
 
+import ctypes
 from typing import List, Optional, Tuple
 
 import numpy as np
@@ -455,19 +456,147 @@ class _BipartiteHop(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dY):
-        sh, kind = ctx.sh, ctx.kind
+        return _bipartite_backward(ctx.sh, ctx.kind, dY.contiguous()), None, None
+
+
+def _bipartite_backward(sh: "ShardedBipartite", kind, dY: torch.Tensor) -> torch.Tensor:
+    """dX of ``S·A·X`` on the local layout: the item rows' partial gradients are summed over
+    the ranks (all-reduce, overlapped with dX_i = B_gᵀ·S_u·dY_u, a partial), then
+    dX_u = C_gᵀ·S_i·dY_i."""
+    n = sh.n_local
+    w_b, w_c = sh._src_folded("b_t", kind), sh._src_folded("c_t", kind)  # before the async
+    dYi = dY[n:]
+    work = None
+    if sh.world > 1:
+        dYi = dYi.clone()
+        work = dist.all_reduce(dYi, group=sh.group, async_op=True)
+    dX = torch.empty_like(dY)
+    # partial dX_i = B_gᵀ·S_u·dY_u while the item gradient is summed
+    spmm_csr(sh.B.csc, dY[:n], val=w_b, out=dX[n:])
+    if work is not None:
+        work.wait()
+    spmm_csr(sh.C.csc, dYi, val=w_c, out=dX[:n])
+    return dX
+
+
+class _BipartiteHopFused(torch.autograd.Function):
+    """``out_scale·LN(act(S·A·X)) + s1·res1 + s2·res2`` on the local layout: the user rows'
+    epilogue runs in the store of their (local, complete) hop (hgd_spmm_fused); the item rows are
+    complete only after their exchange, so on N > 1 ranks their epilogue is one row pass after it
+    (hgd_row_epilogue_forward) — on one rank it is fused too. The backward is one
+    hgd_row_epilogue_backward over all local rows, then the hop's backward."""
+
+    @staticmethod
+    def forward(ctx, X, gamma, beta, res1, res2, sh: "ShardedBipartite", kind, cfg):
+        epi, slope, ln, eps, out_scale, s1, s2 = cfg
+        X = X.contiguous()
         n = sh.n_local
+        N, d = X.shape
+        dev = X.device
+        Y = torch.empty_like(X)
+        A = torch.empty_like(X) if (ln or epi != nat.EPI_NONE) else None
+        stats = torch.empty((N, 2), dtype=torch.float32, device=dev) if ln else None
+        res1 = None if res1 is None else res1.contiguous()
+        res2 = None if res2 is None else res2.contiguous()
+
+        def ex_rows(r0):  # the epilogue descriptor for local rows r0, r0+1, ...
+            return nat.RowEpilogue(
+                act=epi, slope=slope, layer_norm=int(ln), ln_eps=eps,
+                ln_gamma=nat.ptr(gamma) if ln else None, ln_beta=nat.ptr(beta) if ln else None,
+                out_scale=out_scale,
+                res1=None if res1 is None else res1[r0:].data_ptr(),
+                ld_res1=0 if res1 is None else res1.stride(0), res1_scale=s1,
+                res2=None if res2 is None else res2[r0:].data_ptr(),
+                ld_res2=0 if res2 is None else res2.stride(0), res2_scale=s2,
+                act_out=None if A is None else A[r0:].data_ptr(),
+                ld_act=0 if A is None else A.stride(0),
+                stats=None if stats is None else stats[r0:].data_ptr())
+
+        si, su = sh.scale("item", kind), sh.scale("user", kind)
+        works: List = []
+        Zi = None
+        if sh.world > 1:
+            Zi = torch.empty((sh.n_items, d), dtype=torch.float32, device=dev)
+            for a, b in sh.bounds:
+                if b > a:
+                    spmm_csr(sh.C.csr, X[:n], val=sh.C.val, row_scale=si, out=Zi, row_begin=a,
+                             row_end=b)
+                works.append(dist.all_reduce(Zi[a:b], group=sh.group, async_op=True))
+        else:
+            spmm_csr(sh.C.csr, X[:n], val=sh.C.val, row_scale=si, out=Y[n:], ex=ex_rows(n))
+        spmm_csr(sh.B.csr, X[n:], val=sh.B.val, row_scale=su, out=Y[:n], ex=ex_rows(0))
+        for w in works:
+            w.wait()
+        if Zi is not None and sh.n_items:
+            ex = ex_rows(n)
+            nat.check(nat.load().hgd_row_epilogue_forward(
+                Zi.data_ptr(), Zi.stride(0), sh.n_items, d, ctypes.byref(ex), Y[n:].data_ptr(),
+                Y.stride(0), torch.cuda.current_stream(dev).cuda_stream),
+                "hgd_row_epilogue_forward")
+        ctx.sh, ctx.kind, ctx.cfg = sh, kind, cfg
+        ctx.has_res = (res1 is not None, res2 is not None)
+        ctx.save_for_backward(A, stats, gamma if ln else None)
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        epi, slope, ln, eps, out_scale, s1, s2 = ctx.cfg
+        A, stats, gamma = ctx.saved_tensors
         dY = dY.contiguous()
-        w_b, w_c = sh._src_folded("b_t", kind), sh._src_folded("c_t", kind)  # before the async
-        dYi = dY[n:].clone()
-        work = dist.all_reduce(dYi, group=sh.group, async_op=True) if sh.world > 1 else None
-        dX = torch.empty_like(dY)
-        # partial dX_i = B_gᵀ·S_u·dY_u while the item gradient is summed
-        spmm_csr(sh.B.csc, dY[:n], val=w_b, out=dX[n:])
-        if work is not None:
-            work.wait()
-        spmm_csr(sh.C.csc, dYi, val=w_c, out=dX[:n])
-        return dX, None, None
+        N, d = dY.shape
+        dev = dY.device
+        want_g = ln and ctx.needs_input_grad[1]
+        want_b = ln and ctx.needs_input_grad[2]
+        dgamma = torch.empty(d, dtype=torch.float32, device=dev) if want_g else None
+        dbeta = torch.empty(d, dtype=torch.float32, device=dev) if want_b else None
+        if not ln and epi == nat.EPI_NONE:
+            dZ = dY if out_scale == 1.0 else dY * out_scale
+        else:
+            lib = nat.load()
+            wsb = lib.hgd_row_epilogue_backward_workspace_size(N, d) if (want_g or want_b) else 0
+            ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev) if wsb else None
+            dZ = torch.empty_like(dY)
+            nat.check(lib.hgd_row_epilogue_backward(
+                dY.data_ptr(), dY.stride(0), nat.ptr(A), 0 if A is None else A.stride(0),
+                nat.ptr(stats), nat.ptr(gamma), N, d, epi, float(slope), int(ln),
+                float(out_scale), dZ.data_ptr(), dZ.stride(0), nat.ptr(dgamma), nat.ptr(dbeta),
+                nat.ptr(ws), wsb, torch.cuda.current_stream(dev).cuda_stream),
+                "hgd_row_epilogue_backward")
+        dX = _bipartite_backward(ctx.sh, ctx.kind, dZ) if ctx.needs_input_grad[0] else None
+
+        def res_grad(k, s):
+            if not ctx.has_res[k] or not ctx.needs_input_grad[3 + k]:
+                return None
+            return dY if s == 1.0 else dY * s
+
+        return dX, dgamma, dbeta, res_grad(0, s1), res_grad(1, s2), None, None, None
+
+
+def bipartite_hop_fused(sh: "ShardedBipartite", X_local: torch.Tensor,
+                        scale: Optional[str] = None, epilogue: Optional[str] = None,
+                        slope: float = 0.0, norm: Optional[torch.nn.LayerNorm] = None,
+                        out_scale: float = 1.0, res1: Optional[torch.Tensor] = None,
+                        res1_scale: float = 1.0, res2: Optional[torch.Tensor] = None,
+                        res2_scale: float = 1.0) -> torch.Tensor:
+    """``out_scale·norm(epi(S·A·X)) + res1_scale·res1 + res2_scale·res2`` on this rank's
+    layout (functional.two_hop_fused's store for the sharded hop); falls back to the separate
+    row pass where the fused store cannot hold a row (LayerNorm with d > 256)."""
+    from .functional import _EPI, _ln_supported, row_epilogue
+    if X_local.shape[0] != sh.n_local + sh.n_items:
+        raise ValueError(f"bipartite_hop_fused: X has {X_local.shape[0]} rows, shard expects "
+                         f"{sh.n_local} users + {sh.n_items} items")
+    d = X_local.shape[1]
+    ln = norm is not None
+    epi = _EPI[epilogue]
+    if (ln and not _ln_supported(d)) or (epi != nat.EPI_NONE and slope < 0):
+        return row_epilogue(bipartite_hop(sh, X_local, scale), epilogue=epilogue, slope=slope,
+                            norm=norm, out_scale=out_scale, res1=res1, res1_scale=res1_scale,
+                            res2=res2, res2_scale=res2_scale)
+    gamma = norm.weight if ln and norm.weight is not None else None
+    beta = norm.bias if ln and norm.bias is not None else None
+    cfg = (epi, float(slope), ln, float(norm.eps) if ln else 0.0, float(out_scale),
+           float(res1_scale), float(res2_scale))
+    return _BipartiteHopFused.apply(X_local, gamma, beta, res1, res2, sh, scale, cfg)
 
 
 def bipartite_hop(sh: ShardedBipartite, X_local: torch.Tensor,

@@ -29,10 +29,10 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .encoders import edhnn_config
-from .functional import dense_two_hop, layer_norm, linear, row_epilogue
+from .functional import dense_two_hop, linear
 from .layers import EquivSetGNN, LayerNorm
-from .sharded import (ShardedBipartite, bipartite_hop, shard_bounds,  # noqa: F401
-                      sharded_dense_two_hop, sharded_hgcn_conv, sharded_mean_two_hop)
+from .sharded import (ShardedBipartite, bipartite_hop, bipartite_hop_fused,  # noqa: F401
+                      shard_bounds, sharded_dense_two_hop, sharded_mean_two_hop)
 
 
 def _coo_tensor(mat, binary: bool = False):
@@ -68,10 +68,15 @@ class _SplitDropout(nn.Module):
             return x
         if self.p == 1.0:
             return torch.zeros_like(x)
+        if not torch.distributed.is_initialized() or torch.distributed.get_world_size() == 1:
+            return F.dropout(x, self.p, True)  # one rank: no replicas to keep equal
         q = 1.0 - self.p
-        keep_loc = torch.empty_like(x[:start]).bernoulli_(q, generator=self.local_gen)
-        keep_rep = torch.empty_like(x[start:]).bernoulli_(q, generator=self.gen)
-        return torch.cat([x[:start] * keep_loc / q, x[start:] * keep_rep / q])
+        # one mask tensor drawn in two parts, pre-scaled by 1/q: a single product with x (and
+        # one in the backward), no per-part products and concatenation
+        mask = torch.empty_like(x)
+        mask[:start].bernoulli_(q, generator=self.local_gen)
+        mask[start:].bernoulli_(q, generator=self.gen)
+        return x * mask.mul_(1.0 / q)
 
 
 def _rank_generators(device, seed: int, group):
@@ -167,9 +172,10 @@ class ShardedLocalAwareEncoder(nn.Module):
     """LocalAwareEncoder (HGNN_HD4.py:336-405, ``--mode=local_only``) on user-row shards, same
     submodules and parameter names (``state_dict``s load either way): layers 0..L-2 are ED-HNN
     blocks whose vertex/edge mean pair over V/E = nonzero(ui_adj) runs as
-    :func:`sharded_mean_two_hop`; the last layer is LN0(HGCNConv(Â, ·, act=False)) with the
-    two hops as :func:`sharded_hgcn_conv`; every layer adds the layer-0 residual. All other
-    ops are row-wise, so they run on the local layout unchanged."""
+    :func:`sharded_mean_two_hop`; the last layer is LN0(HGCNConv(Â, ·, act=False)) + res with
+    the two hops as :func:`~.sharded.bipartite_hop` and :func:`~.sharded.bipartite_hop_fused`
+    (LayerNorm and residual in the second hop's store); every layer adds the layer-0 residual.
+    All other ops are row-wise, so they run on the local layout unchanged."""
 
     def __init__(self, data, emb_size, hyper_size, n_layers, leaky, drop_rate, u0: int, u1: int,
                  group=None, device=None, n_chunks: int = 4, seed: int = 0):
@@ -243,8 +249,10 @@ class ShardedLocalAwareEncoder(nn.Module):
             if k != self.layers - 1:
                 ego_embeddings = self._edhnn(self.edhnn_layers[k], ego_embeddings) + res
             else:
-                z = sharded_hgcn_conv(norm, ego_embeddings, act=False)
-                ego_embeddings = layer_norm(z, self.lns[0]) + res
+                # LN0(A·(Aᵀ·x)) + res, the LayerNorm and residual in the second hop's store
+                ego_embeddings = bipartite_hop_fused(
+                    norm, bipartite_hop(norm.transpose(), ego_embeddings), norm=self.lns[0],
+                    res1=res)
         nl = self.n_local
         return ego_embeddings[:nl], ego_embeddings[nl:]
 
@@ -253,8 +261,9 @@ class ShardedLocalAwareEncoderHD3(ShardedLocalAwareEncoder):
     """LocalAwareEncoderHD3 (HGNN_HD3.py:352-427) on user-row shards, same submodules and
     parameter names: layers 0..L-2 are the SpMM-form ED-HNN blocks (HGNN_HD3.py:555-720), whose
     two aggregations are HGCNConv two-hops over the edge-dropped ``norm_adj`` shard
-    (:func:`sharded_hgcn_conv`, the LeakyReLU / LayerNorm / residual / restart blend in one
-    row-epilogue pass after the exchange); the last layer is ``lns[L-1](HGCNConv(Â, ·,
+    (:func:`~.sharded.bipartite_hop_fused`: the LeakyReLU / LayerNorm / residual / restart
+    blend in the second hop's store for user rows, one row pass after the exchange for item
+    rows); the last layer is ``lns[L-1](HGCNConv(Â, ·,
     act=False)) + res`` on the un-dropped shard. Every layer adds the layer-0 residual."""
 
     def __init__(self, data, emb_size, hyper_size, n_layers, leaky, drop_rate, u0: int, u1: int,
@@ -295,17 +304,18 @@ class ShardedLocalAwareEncoderHD3(ShardedLocalAwareEncoder):
         for _ in range(blk.nlayer):
             x = self._drop(blk.dropout, x)
             xve = conv.W1(x)
-            # Xe = LN0(leaky(A·(Aᵀ·Xve))) + Xve
-            xe = row_epilogue(sharded_hgcn_conv(sh, xve, act=False), epilogue="leaky_relu",
-                              slope=s0, norm=conv.lns[0], res1=xve)
+            # Xe = LN0(leaky(A·(Aᵀ·Xve))) + Xve, the epilogue in the second hop's store
+            xe = bipartite_hop_fused(sh, bipartite_hop(sh.transpose(), xve),
+                                     epilogue="leaky_relu", slope=s0, norm=conv.lns[0], res1=xve)
             xev = xe if conv.W2 is None else conv.W2(torch.cat([x, xe], -1))
             if xev.shape[-1] != conv.out_features:
                 xev = conv.mean_pooling(xev)
             # (1-α)·(LN1(leaky(A·(Aᵀ·Xev))) + Xev) + α·X0
             a = conv.alpha
-            xv = row_epilogue(sharded_hgcn_conv(sh, xev, act=False), epilogue="leaky_relu",
-                              slope=s1, norm=conv.lns[1], out_scale=1 - a, res1=xev,
-                              res1_scale=1 - a, res2=x0 if a != 0 else None, res2_scale=a)
+            xv = bipartite_hop_fused(sh, bipartite_hop(sh.transpose(), xev),
+                                     epilogue="leaky_relu", slope=s1, norm=conv.lns[1],
+                                     out_scale=1 - a, res1=xev, res1_scale=1 - a,
+                                     res2=x0 if a != 0 else None, res2_scale=a)
             x = blk.act(conv.W(xv))
         return self._drop(blk.dropout, x)
 
@@ -319,7 +329,8 @@ class ShardedLocalAwareEncoderHD3(ShardedLocalAwareEncoder):
                 ego_embeddings = self._edhnn_spmm(self.edhnn_layers[k], ego_embeddings,
                                                   dropped) + res
             else:
-                z = sharded_hgcn_conv(self.norm, ego_embeddings, act=False)
-                ego_embeddings = row_epilogue(z, norm=self.lns[k], res1=res)
+                ego_embeddings = bipartite_hop_fused(
+                    self.norm, bipartite_hop(self.norm.transpose(), ego_embeddings),
+                    norm=self.lns[k], res1=res)
         nl = self.n_local
         return ego_embeddings[:nl], ego_embeddings[nl:]
