@@ -132,6 +132,17 @@ _SIGNATURES = {
     "hgd_infonce_backward": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_i64,
                                      c_i32, c_f32, c_void_p, c_void_p, c_void_p, c_void_p,
                                      c_size, c_void_p]),
+    "hgd_infonce_forward_n": (c_i32, [c_void_p, c_i64, c_void_p, c_i64, c_i64, c_void_p, c_i64,
+                                      c_void_p, c_i32, c_f32, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size,
+                                      c_void_p]),
+    "hgd_infonce_backward_n": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_i64,
+                                       c_void_p, c_i32, c_f32, c_void_p, c_void_p, c_i64,
+                                       c_void_p, c_i64, c_void_p, c_i64, c_void_p, c_size,
+                                       c_void_p]),
+    "hgd_bernoulli_mask_dev": (c_i32, [c_void_p, c_i64, c_f32, c_void_p, c_void_p]),
+    "hgd_dropedge_fill_tail": (c_i32, [c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_void_p]),
     "hgd_ingest_read": (c_i32, [ctypes.c_char_p, c_i32, c_i32, ctypes.POINTER(c_void_p)]),
     "hgd_ingest_count": (c_i64, [c_void_p]),
     "hgd_ingest_copy": (c_i32, [c_void_p, c_void_p, c_void_p]),

@@ -35,12 +35,13 @@ __global__ __launch_bounds__(256) void k_nce_gather(const float* __restrict__ E1
                                                     int64_t n_rows, int32_t d, float inv_temp,
                                                     float* P1,
                                                     float* P2, float* inv1, float* inv2,
-                                                    float* pos_logit) {
+                                                    float* pos_logit, const int64_t* Bp) {
   constexpr int GPB = 256 / G;
   const int g = threadIdx.x / G;
   const int l = threadIdx.x % G;
   const int64_t b = static_cast<int64_t>(blockIdx.x) * GPB + g;
   if (b >= B) return;
+  if (Bp && b >= *Bp) return;  // a capacity row past the device-side count: never read
   // torch indexing semantics: negative ids count from the end (the reference passes
   // torch.unique(emb.long()), HCCF.py:65-66, which yields -1 / 0 / 1); out-of-range ids are
   // rejected by the caller — clamped here only so that no load leaves the table
@@ -93,22 +94,23 @@ template <int DQ>  // d = 4·DQ
 __global__ __launch_bounds__(256) void k_nce_rowsum(const float* __restrict__ P1,
                                                     const float* __restrict__ P2, int64_t B,
                                                     float inv_temp, int64_t j_per_slice,
-                                                    float* partial) {
+                                                    float* partial, const int64_t* Bp) {
   constexpr int Q4 = DQ / 4;
   constexpr int SUB = 4;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int64_t b0 = static_cast<int64_t>(blockIdx.x) * 64 + 16 * wave;
-  if (b0 >= B) return;
+  const int64_t Be = Bp ? *Bp : B;  // live rows (B is the capacity: strides, clamps)
+  if (b0 >= Be) return;
   const int d = 4 * DQ;
   f32x4 a[Q4];
-  load_frag4<DQ>(P1, B, d, b0, lane, a);
+  load_frag4<DQ>(P1, Be, d, b0, lane, a);  // rows clamped to the live ones (the rest unwritten)
   const int64_t j_begin = static_cast<int64_t>(blockIdx.y) * j_per_slice;
-  const int64_t j_end = min(B, j_begin + j_per_slice);
+  const int64_t j_end = min(Be, j_begin + j_per_slice);
   float psum[4] = {0.f, 0.f, 0.f, 0.f};
   auto load = [&](int64_t j0, f32x4 (&f)[SUB][Q4]) {
 #pragma unroll
-    for (int t = 0; t < SUB; ++t) load_frag4<DQ>(P2, B, d, j0 + 16 * t, lane, f[t]);
+    for (int t = 0; t < SUB; ++t) load_frag4<DQ>(P2, Be, d, j0 + 16 * t, lane, f[t]);
   };
   auto compute = [&](int64_t j0, const f32x4 (&f)[SUB][Q4]) {
 #pragma unroll
@@ -146,7 +148,7 @@ __global__ __launch_bounds__(256) void k_nce_rowsum(const float* __restrict__ P1
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t b = b0 + 4 * (lane >> 4) + r;
-      if (b < B) partial[static_cast<int64_t>(blockIdx.y) * B + b] = psum[r];
+      if (b < Be) partial[static_cast<int64_t>(blockIdx.y) * B + b] = psum[r];
     }
   }
 }
@@ -155,10 +157,12 @@ __global__ __launch_bounds__(256) void k_nce_rowsum(const float* __restrict__ P1
 __global__ __launch_bounds__(1024) void k_nce_finish(const float* __restrict__ partial,
                                                      int64_t S, int64_t B,
                                                      const float* __restrict__ pos_logit,
-                                                     float* deno, float* loss) {
+                                                     float* deno, float* loss,
+                                                     const int64_t* Bp) {
   __shared__ float red[1024];
+  const int64_t Be = Bp ? *Bp : B;
   float acc = 0.f;
-  for (int64_t b = threadIdx.x; b < B; b += 1024) {
+  for (int64_t b = threadIdx.x; b < Be; b += 1024) {
     float den = 0.f;
     for (int64_t s = 0; s < S; ++s) den += partial[s * B + b];
     den += kDenoEps;
@@ -171,7 +175,7 @@ __global__ __launch_bounds__(1024) void k_nce_finish(const float* __restrict__ p
     if (static_cast<int>(threadIdx.x) < w) red[threadIdx.x] += red[threadIdx.x + w];
     __syncthreads();
   }
-  if (threadIdx.x == 0) *loss = -red[0] / static_cast<float>(B);
+  if (threadIdx.x == 0) *loss = -red[0] / static_cast<float>(Be);
 }
 
 // ---- backward partials ----
@@ -182,26 +186,29 @@ template <int DQ, bool ROWS>
 __global__ __launch_bounds__(256) void k_nce_bwd(const float* __restrict__ P1,
                                                  const float* __restrict__ P2, int64_t B,
                                                  float inv_temp, const float* __restrict__ deno,
-                                                 const float* __restrict__ grad, float coef_base,
-                                                 int64_t k_per_slice, float* part) {
+                                                 const float* __restrict__ grad, float temp,
+                                                 int64_t k_per_slice, float* part,
+                                                 const int64_t* Bp) {
   constexpr int Q4 = DQ / 4;
   constexpr int SUB = 2;  // 16-row tiles of the streamed matrix per ping-pong stage
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int d = 4 * DQ;
-  const float coef = grad[0] * coef_base;  // upstream dL/dloss (device scalar: no host sync)
+  const int64_t Be = Bp ? *Bp : B;  // live rows (B is the capacity: strides, clamps)
+  // upstream dL/dloss and the 1/(B·τ) of the mean: device values, no host sync
+  const float coef = grad[0] / (static_cast<float>(Be) * temp);
   // "own" rows: b (ROWS) or j (!ROWS); "other" rows are streamed in 16-row tiles
   const float* own_m = ROWS ? P1 : P2;
   const float* oth_m = ROWS ? P2 : P1;
   const int64_t o0 = static_cast<int64_t>(blockIdx.x) * 64 + 16 * wave;
-  if (o0 >= B) return;
+  if (o0 >= Be) return;
   f32x4 own[Q4];
-  load_frag4<DQ>(own_m, B, d, o0, lane, own);
+  load_frag4<DQ>(own_m, Be, d, o0, lane, own);  // rows clamped to the live ones
   const int64_t o_lane = o0 + (lane & 15);  // own row of this lane in the logit tile below
   float deno_own = 1.f;
-  if (ROWS) deno_own = deno[o_lane < B ? o_lane : B - 1];
+  if (ROWS) deno_own = deno[o_lane < Be ? o_lane : Be - 1];
   const int64_t k_begin = static_cast<int64_t>(blockIdx.y) * k_per_slice;
-  const int64_t k_end = min(B, k_begin + k_per_slice);
+  const int64_t k_end = min(Be, k_begin + k_per_slice);
   f32x4 acc[DQ / 4];
 #pragma unroll
   for (int t = 0; t < DQ / 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -215,11 +222,11 @@ __global__ __launch_bounds__(256) void k_nce_bwd(const float* __restrict__ P1,
 #pragma unroll
     for (int u = 0; u < SUB; ++u) {
       const int64_t kt = k0 + 16 * u;
-      load_frag4<DQ>(oth_m, B, d, kt, lane, T[u].of);
+      load_frag4<DQ>(oth_m, Be, d, kt, lane, T[u].of);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         int64_t k = kt + 4 * (lane >> 4) + r;
-        k = k < B ? k : B - 1;
+        k = k < Be ? k : Be - 1;
 #pragma unroll
         for (int t = 0; t < DQ / 4; ++t) T[u].bv[r][t] = oth_m[k * d + 16 * t + (lane & 15)];
       }
@@ -241,11 +248,11 @@ __global__ __launch_bounds__(256) void k_nce_bwd(const float* __restrict__ P1,
       for (int r = 0; r < 4; ++r) {
         const int64_t k = kt + 4 * (lane >> 4) + r;  // other index of register r
         const bool kok = k < k_end;
-        const int64_t kc = k < B ? k : B - 1;
+        const int64_t kc = k < Be ? k : Be - 1;
         const float e = expf(s[r] * inv_temp);
         const float den = ROWS ? deno_own : deno[kc];
         const float delta = (k == o_lane) ? 1.f : 0.f;
-        gk[r] = (kok && o_lane < B) ? coef * (e / den - delta) : 0.f;
+        gk[r] = (kok && o_lane < Be) ? coef * (e / den - delta) : 0.f;
       }
       // acc[own row][n] += Σ_k G[own][k]·oth_k[n]: A operand = gk (own row on the lane, k-step
       // r covers other rows {4(l>>4) + r}), B operand = those rows' features (bv).
@@ -277,7 +284,7 @@ __global__ __launch_bounds__(256) void k_nce_bwd(const float* __restrict__ P1,
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t o = o0 + 4 * (lane >> 4) + r;
-      if (o < B) part[(static_cast<int64_t>(blockIdx.y) * B + o) * d + 16 * t + (lane & 15)] =
+      if (o < Be) part[(static_cast<int64_t>(blockIdx.y) * B + o) * d + 16 * t + (lane & 15)] =
           acc[t][r];
     }
 }
@@ -287,7 +294,10 @@ template <int G>
 __global__ __launch_bounds__(256) void k_nce_norm_bwd(const float* __restrict__ part, int64_t S,
                                                       int64_t B, int32_t d,
                                                       const float* __restrict__ P,
-                                                      const float* __restrict__ inv, float* dX) {
+                                                      const float* __restrict__ inv, float* dX,
+                                                      const int64_t* Bp,
+                                                      const int64_t* __restrict__ nodes,
+                                                      int64_t n_rows, float* dE, int64_t ldE) {
   constexpr int GPB = 256 / G;
   const int g = threadIdx.x / G;
   const int l = threadIdx.x % G;
@@ -295,6 +305,10 @@ __global__ __launch_bounds__(256) void k_nce_norm_bwd(const float* __restrict__ 
   if (b >= B) return;
   const int c0 = 4 * l;
   const bool ok = c0 < d;
+  if (Bp && b >= *Bp) {  // capacity row: a zero gradient row, or nothing to scatter
+    if (ok && dX) *reinterpret_cast<f32x4*>(dX + b * d + c0) = f32x4{0.f, 0.f, 0.f, 0.f};
+    return;
+  }
   f32x4 dp = {0.f, 0.f, 0.f, 0.f}, p = {0.f, 0.f, 0.f, 0.f};
   if (ok) {
     for (int64_t s = 0; s < S; ++s) dp += *reinterpret_cast<const f32x4*>(part + (s * B + b) * d + c0);
@@ -305,7 +319,22 @@ __global__ __launch_bounds__(256) void k_nce_norm_bwd(const float* __restrict__ 
   // F.normalize backward: x / max(‖x‖, eps); when ‖x‖ <= eps the op is x·(1/eps), linear
   const bool clamped = r >= 1.f / kNormEps;
   const f32x4 dx = clamped ? dp * r : (dp - p * dot) * r;
-  if (ok) *reinterpret_cast<f32x4*>(dX + b * d + c0) = dx;
+  if (!ok) return;
+  if (dE) {
+    // scatter-add into the [n_rows, d] table gradient at this batch row's node (torch indexing:
+    // negative ids wrap). At most two batch rows meet on one table row (x and x − n), and a sum
+    // of two terms onto 0 is order-independent, so the atomics stay deterministic.
+    int64_t node = nodes[b];
+    if (node < 0) node += n_rows;
+    node = node < 0 ? 0 : (node >= n_rows ? n_rows - 1 : node);
+    float* row = dE + node * ldE + c0;
+    atomicAdd(row + 0, dx.x);
+    atomicAdd(row + 1, dx.y);
+    atomicAdd(row + 2, dx.z);
+    atomicAdd(row + 3, dx.w);
+  } else {
+    *reinterpret_cast<f32x4*>(dX + b * d + c0) = dx;
+  }
 }
 
 // lanes per row for the row kernels: the next power of two ≥ d/4 (each lane holds 4 columns)
@@ -340,15 +369,15 @@ extern "C" size_t hgd_infonce_workspace_size(int64_t batch, int32_t d) {
   return hgd::align_up(S * B * 4) + 2 * hgd::align_up(S * B * static_cast<size_t>(d) * 4);
 }
 
-extern "C" hgd_status hgd_infonce_forward(const float* E1, int64_t ld1, const float* E2,
-                                          int64_t ld2, int64_t n_rows, const int64_t* nodes,
-                                          int64_t batch, int32_t d, float temp, float* P1,
-                                          float* P2, float* inv_norm1, float* inv_norm2,
-                                          float* pos_logit, float* deno, float* loss,
-                                          void* workspace, size_t workspace_bytes,
-                                          void* stream) {
-  using namespace hgd;
-  clear_error();
+namespace hgd {
+namespace {
+
+hgd_status infonce_forward(const float* E1, int64_t ld1, const float* E2, int64_t ld2,
+                           int64_t n_rows, const int64_t* nodes, int64_t batch,
+                           const int64_t* batch_count, int32_t d, float temp, float* P1,
+                           float* P2, float* inv_norm1, float* inv_norm2, float* pos_logit,
+                           float* deno, float* loss, void* workspace, size_t workspace_bytes,
+                           void* stream) {
   HGD_REQUIRE(batch > 0 && n_rows > 0, "hgd_infonce_forward: empty batch or table");
   HGD_REQUIRE(d % 16 == 0 && d >= 16 && d <= 256,
               "hgd_infonce_forward: d = %d must be a multiple of 16 in [16, 256]", d);
@@ -369,11 +398,11 @@ extern "C" hgd_status hgd_infonce_forward(const float* E1, int64_t ld1, const fl
   const int64_t gpb = 256 / G;
   const dim3 gg(static_cast<unsigned>((batch + gpb - 1) / gpb));
   switch (G) {
-    case 4: hipLaunchKernelGGL((k_nce_gather<4>), gg, dim3(256), 0, st, E1, ld1, E2, ld2, nodes, batch, n_rows, d, inv_temp, P1, P2, inv_norm1, inv_norm2, pos_logit); break;
-    case 8: hipLaunchKernelGGL((k_nce_gather<8>), gg, dim3(256), 0, st, E1, ld1, E2, ld2, nodes, batch, n_rows, d, inv_temp, P1, P2, inv_norm1, inv_norm2, pos_logit); break;
-    case 16: hipLaunchKernelGGL((k_nce_gather<16>), gg, dim3(256), 0, st, E1, ld1, E2, ld2, nodes, batch, n_rows, d, inv_temp, P1, P2, inv_norm1, inv_norm2, pos_logit); break;
-    case 32: hipLaunchKernelGGL((k_nce_gather<32>), gg, dim3(256), 0, st, E1, ld1, E2, ld2, nodes, batch, n_rows, d, inv_temp, P1, P2, inv_norm1, inv_norm2, pos_logit); break;
-    default: hipLaunchKernelGGL((k_nce_gather<64>), gg, dim3(256), 0, st, E1, ld1, E2, ld2, nodes, batch, n_rows, d, inv_temp, P1, P2, inv_norm1, inv_norm2, pos_logit); break;
+    case 4: hipLaunchKernelGGL((k_nce_gather<4>), gg, dim3(256), 0, st, E1, ld1, E2, ld2, nodes, batch, n_rows, d, inv_temp, P1, P2, inv_norm1, inv_norm2, pos_logit, batch_count); break;
+    case 8: hipLaunchKernelGGL((k_nce_gather<8>), gg, dim3(256), 0, st, E1, ld1, E2, ld2, nodes, batch, n_rows, d, inv_temp, P1, P2, inv_norm1, inv_norm2, pos_logit, batch_count); break;
+    case 16: hipLaunchKernelGGL((k_nce_gather<16>), gg, dim3(256), 0, st, E1, ld1, E2, ld2, nodes, batch, n_rows, d, inv_temp, P1, P2, inv_norm1, inv_norm2, pos_logit, batch_count); break;
+    case 32: hipLaunchKernelGGL((k_nce_gather<32>), gg, dim3(256), 0, st, E1, ld1, E2, ld2, nodes, batch, n_rows, d, inv_temp, P1, P2, inv_norm1, inv_norm2, pos_logit, batch_count); break;
+    default: hipLaunchKernelGGL((k_nce_gather<64>), gg, dim3(256), 0, st, E1, ld1, E2, ld2, nodes, batch, n_rows, d, inv_temp, P1, P2, inv_norm1, inv_norm2, pos_logit, batch_count); break;
   }
   hgd_status s = check_launch("hgd_infonce_forward gather");
   if (s != HGD_OK) return s;
@@ -386,7 +415,7 @@ extern "C" hgd_status hgd_infonce_forward(const float* E1, int64_t ld1, const fl
 #define HGD_CASE(DQ)                                                                              \
     case DQ:                                                                                      \
       hipLaunchKernelGGL((k_nce_rowsum<DQ>), gr, dim3(256), 0, st, P1, P2, batch, inv_temp, jps, \
-                         partial);                                                                \
+                         partial, batch_count);                                                   \
       break;
     HGD_CASE(4) HGD_CASE(8) HGD_CASE(12) HGD_CASE(16) HGD_CASE(20) HGD_CASE(24) HGD_CASE(28)
     HGD_CASE(32) HGD_CASE(36) HGD_CASE(40) HGD_CASE(44) HGD_CASE(48) HGD_CASE(52) HGD_CASE(56)
@@ -397,32 +426,35 @@ extern "C" hgd_status hgd_infonce_forward(const float* E1, int64_t ld1, const fl
   s = check_launch("hgd_infonce_forward rowsum");
   if (s != HGD_OK) return s;
   hipLaunchKernelGGL(k_nce_finish, dim3(1), dim3(1024), 0, st, partial, S_used, batch, pos_logit,
-                     deno, loss);
+                     deno, loss, batch_count);
   return check_launch("hgd_infonce_forward finish");
 }
 
-extern "C" hgd_status hgd_infonce_backward(const float* P1, const float* P2,
-                                           const float* inv_norm1, const float* inv_norm2,
-                                           const float* deno, int64_t batch, int32_t d,
-                                           float temp, const float* grad_loss, float* dX1,
-                                           float* dX2,
-                                           void* workspace, size_t workspace_bytes,
-                                           void* stream) {
-  using namespace hgd;
-  clear_error();
+
+hgd_status infonce_backward(const float* P1, const float* P2, const float* inv_norm1,
+                            const float* inv_norm2, const float* deno, int64_t batch,
+                            const int64_t* batch_count, int32_t d, float temp,
+                            const float* grad_loss, float* dX1, float* dX2,
+                            const int64_t* nodes, int64_t n_rows, float* dE1, int64_t ldE1,
+                            float* dE2, int64_t ldE2, void* workspace,
+                            size_t workspace_bytes, void* stream) {
   HGD_REQUIRE(batch > 0, "hgd_infonce_backward: empty batch");
   HGD_REQUIRE(d % 16 == 0 && d >= 16 && d <= 256,
               "hgd_infonce_backward: d = %d must be a multiple of 16 in [16, 256]", d);
   HGD_REQUIRE(temp > 0.f, "hgd_infonce_backward: temperature must be > 0");
-  HGD_REQUIRE(P1 && P2 && inv_norm1 && inv_norm2 && deno && grad_loss && dX1 && dX2,
+  HGD_REQUIRE(P1 && P2 && inv_norm1 && inv_norm2 && deno && grad_loss,
               "hgd_infonce_backward: null pointer");
+  const bool side1 = dX1 || dE1, side2 = dX2 || dE2;  // a side without an output is skipped
+  HGD_REQUIRE(side1 || side2, "hgd_infonce_backward: no output");
+  HGD_REQUIRE(!(dE1 || dE2) || (nodes && n_rows > 0 && (!dE1 || ldE1 >= d) &&
+                                (!dE2 || ldE2 >= d)),
+              "hgd_infonce_backward: a table scatter needs nodes, n_rows and ld >= d");
   const size_t need = hgd_infonce_workspace_size(batch, d);
   if (workspace_bytes < need || !workspace)
     return fail(HGD_ERR_WORKSPACE, "hgd_infonce_backward: workspace %zu < required %zu",
                 workspace_bytes, need);
   hipStream_t st = as_stream(stream);
   const float inv_temp = 1.f / temp;
-  const float coef_base = 1.f / (static_cast<float>(batch) * temp);
   const int64_t S = slices_for(batch);
   const int64_t kps = per_slice(batch, S);
   const int64_t S_used = (batch + kps - 1) / kps;
@@ -434,10 +466,12 @@ extern "C" hgd_status hgd_infonce_backward(const float* P1, const float* P2,
   switch (d / 4) {
 #define HGD_CASE(DQ)                                                                              \
     case DQ:                                                                                      \
-      hipLaunchKernelGGL((k_nce_bwd<DQ, true>), gr, dim3(256), 0, st, P1, P2, batch, inv_temp,   \
-                         deno, grad_loss, coef_base, kps, part1);                                                 \
-      hipLaunchKernelGGL((k_nce_bwd<DQ, false>), gr, dim3(256), 0, st, P1, P2, batch, inv_temp,  \
-                         deno, grad_loss, coef_base, kps, part2);                                                 \
+      if (side1)                                                                                  \
+        hipLaunchKernelGGL((k_nce_bwd<DQ, true>), gr, dim3(256), 0, st, P1, P2, batch, inv_temp, \
+                           deno, grad_loss, temp, kps, part1, batch_count);                        \
+      if (side2)                                                                                  \
+        hipLaunchKernelGGL((k_nce_bwd<DQ, false>), gr, dim3(256), 0, st, P1, P2, batch,          \
+                           inv_temp, deno, grad_loss, temp, kps, part2, batch_count);              \
       break;
     HGD_CASE(4) HGD_CASE(8) HGD_CASE(12) HGD_CASE(16) HGD_CASE(20) HGD_CASE(24) HGD_CASE(28)
     HGD_CASE(32) HGD_CASE(36) HGD_CASE(40) HGD_CASE(44) HGD_CASE(48) HGD_CASE(52) HGD_CASE(56)
@@ -453,14 +487,74 @@ extern "C" hgd_status hgd_infonce_backward(const float* P1, const float* P2,
   switch (G) {
 #define HGD_CASE(GG)                                                                         \
     case GG:                                                                                 \
-      hipLaunchKernelGGL((k_nce_norm_bwd<GG>), gn, dim3(256), 0, st, part1, S_used, batch, d, \
-                         P1, inv_norm1, dX1);                                                \
-      hipLaunchKernelGGL((k_nce_norm_bwd<GG>), gn, dim3(256), 0, st, part2, S_used, batch, d, \
-                         P2, inv_norm2, dX2);                                                \
+      if (side1)                                                                             \
+        hipLaunchKernelGGL((k_nce_norm_bwd<GG>), gn, dim3(256), 0, st, part1, S_used, batch, \
+                           d, P1, inv_norm1, dX1, batch_count, nodes, n_rows, dE1, ldE1);    \
+      if (side2)                                                                             \
+        hipLaunchKernelGGL((k_nce_norm_bwd<GG>), gn, dim3(256), 0, st, part2, S_used, batch, \
+                           d, P2, inv_norm2, dX2, batch_count, nodes, n_rows, dE2, ldE2);    \
       break;
     HGD_CASE(4) HGD_CASE(8) HGD_CASE(16) HGD_CASE(32) HGD_CASE(64)
 #undef HGD_CASE
     default: return fail(HGD_ERR_UNSUPPORTED, "hgd_infonce_backward: group %d", G);
   }
   return check_launch("hgd_infonce_backward norm");
+}
+
+}  // namespace
+}  // namespace hgd
+
+extern "C" hgd_status hgd_infonce_forward(const float* E1, int64_t ld1, const float* E2,
+                                          int64_t ld2, int64_t n_rows, const int64_t* nodes,
+                                          int64_t batch, int32_t d, float temp, float* P1,
+                                          float* P2, float* inv_norm1, float* inv_norm2,
+                                          float* pos_logit, float* deno, float* loss,
+                                          void* workspace, size_t workspace_bytes,
+                                          void* stream) {
+  hgd::clear_error();
+  return hgd::infonce_forward(E1, ld1, E2, ld2, n_rows, nodes, batch, nullptr, d, temp, P1, P2,
+                              inv_norm1, inv_norm2, pos_logit, deno, loss, workspace,
+                              workspace_bytes, stream);
+}
+
+extern "C" hgd_status hgd_infonce_forward_n(const float* E1, int64_t ld1, const float* E2,
+                                            int64_t ld2, int64_t n_rows, const int64_t* nodes,
+                                            int64_t capacity, const int64_t* batch_count,
+                                            int32_t d, float temp, float* P1, float* P2,
+                                            float* inv_norm1, float* inv_norm2, float* pos_logit,
+                                            float* deno, float* loss, void* workspace,
+                                            size_t workspace_bytes, void* stream) {
+  hgd::clear_error();
+  HGD_REQUIRE(batch_count, "hgd_infonce_forward_n: null batch_count");
+  return hgd::infonce_forward(E1, ld1, E2, ld2, n_rows, nodes, capacity, batch_count, d, temp,
+                              P1, P2, inv_norm1, inv_norm2, pos_logit, deno, loss, workspace,
+                              workspace_bytes, stream);
+}
+
+extern "C" hgd_status hgd_infonce_backward(const float* P1, const float* P2,
+                                           const float* inv_norm1, const float* inv_norm2,
+                                           const float* deno, int64_t batch, int32_t d,
+                                           float temp, const float* grad_loss, float* dX1,
+                                           float* dX2, void* workspace, size_t workspace_bytes,
+                                           void* stream) {
+  hgd::clear_error();
+  HGD_REQUIRE(dX1 && dX2, "hgd_infonce_backward: null dX1/dX2");
+  return hgd::infonce_backward(P1, P2, inv_norm1, inv_norm2, deno, batch, nullptr, d, temp,
+                               grad_loss, dX1, dX2, nullptr, 0, nullptr, 0, nullptr, 0,
+                               workspace, workspace_bytes, stream);
+}
+
+extern "C" hgd_status hgd_infonce_backward_n(const float* P1, const float* P2,
+                                             const float* inv_norm1, const float* inv_norm2,
+                                             const float* deno, int64_t capacity,
+                                             const int64_t* batch_count, int32_t d, float temp,
+                                             const float* grad_loss, const int64_t* nodes,
+                                             int64_t n_rows, float* dE1, int64_t ldE1,
+                                             float* dE2, int64_t ldE2, void* workspace,
+                                             size_t workspace_bytes, void* stream) {
+  hgd::clear_error();
+  HGD_REQUIRE(batch_count, "hgd_infonce_backward_n: null batch_count");
+  return hgd::infonce_backward(P1, P2, inv_norm1, inv_norm2, deno, capacity, batch_count, d,
+                               temp, grad_loss, nullptr, nullptr, nodes, n_rows, dE1, ldE1, dE2,
+                               ldE2, workspace, workspace_bytes, stream);
 }

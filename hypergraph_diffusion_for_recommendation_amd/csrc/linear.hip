@@ -62,6 +62,30 @@ __global__ __launch_bounds__(256) void k_row_gemm(RowGemm p) {
   const int h = lane >> 4;
   const int n0 = blockIdx.y * 64;
   const int nt = min(4, (p.N - n0) / 16);  // live 16-column tiles of this slice (uniform)
+  const int64_t tiles = (p.rows + 16 * SUB - 1) / (16 * SUB);  // 32-row super-tiles
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * 4;
+  int64_t tile = static_cast<int64_t>(blockIdx.x) * 4 + wave;
+  // Unconditional raw loads (the compiler then counts them exactly in its vmcnt waits): rows
+  // past the end are clamped to the last row and their results never stored; the ReLU mask is
+  // applied when the tile is consumed.
+  auto load = [&](int64_t tl, f32x4 (&a)[SUB][KQ], f32x4 (&m)[SUB][KQ]) {
+    tl = tl < tiles ? tl : tiles - 1;
+#pragma unroll
+    for (int s = 0; s < SUB; ++s) {
+      int64_t ra = tl * 16 * SUB + 16 * s + i16;
+      ra = ra < p.rows ? ra : p.rows - 1;
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) a[s][q] = ld4(p.A + ra * p.lda + 4 * h + 16 * q);
+      if constexpr (MASK) {
+#pragma unroll
+        for (int q = 0; q < KQ; ++q) m[s][q] = ld4(p.mask + ra * p.ldm + 4 * h + 16 * q);
+      }
+    }
+  };
+  // the first tile's row loads go out before the W staging below: on small problems (one or
+  // two tiles per wave) the two HBM round trips then overlap instead of adding up
+  f32x4 a0[SUB][KQ], a1[SUB][KQ], m0v[SUB][KQ], m1v[SUB][KQ];
+  if (tile < tiles) load(tile, a0, m0v);
   {
     // all loads first (independent, in flight together), then the LDS writes
     float tmp[PER];
@@ -94,25 +118,6 @@ __global__ __launch_bounds__(256) void k_row_gemm(RowGemm p) {
 #pragma unroll
   for (int t = 0; t < 4; ++t) bias_v[t] = (p.bias && t < nt) ? p.bias[n0 + 16 * t + i16] : 0.f;
 
-  const int64_t tiles = (p.rows + 16 * SUB - 1) / (16 * SUB);  // 32-row super-tiles
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * 4;
-  // Unconditional raw loads (the compiler then counts them exactly in its vmcnt waits): rows
-  // past the end are clamped to the last row and their results never stored; the ReLU mask is
-  // applied when the tile is consumed.
-  auto load = [&](int64_t tile, f32x4 (&a)[SUB][KQ], f32x4 (&m)[SUB][KQ]) {
-    tile = tile < tiles ? tile : tiles - 1;
-#pragma unroll
-    for (int s = 0; s < SUB; ++s) {
-      int64_t ra = tile * 16 * SUB + 16 * s + i16;
-      ra = ra < p.rows ? ra : p.rows - 1;
-#pragma unroll
-      for (int q = 0; q < KQ; ++q) a[s][q] = ld4(p.A + ra * p.lda + 4 * h + 16 * q);
-      if constexpr (MASK) {
-#pragma unroll
-        for (int q = 0; q < KQ; ++q) m[s][q] = ld4(p.mask + ra * p.ldm + 4 * h + 16 * q);
-      }
-    }
-  };
   auto compute = [&](int64_t tile, f32x4 (&a)[SUB][KQ], const f32x4 (&m)[SUB][KQ]) {
 #pragma unroll
     for (int s = 0; s < SUB; ++s) {
@@ -153,11 +158,8 @@ __global__ __launch_bounds__(256) void k_row_gemm(RowGemm p) {
       }
     }
   };
-  int64_t tile = static_cast<int64_t>(blockIdx.x) * 4 + wave;
-  if (tile >= tiles) return;
+  if (tile >= tiles) return;  // after the block's barrier: every wave took part in it
   // ping-pong buffers: the next super-tile's loads are in flight during this one's MFMAs
-  f32x4 a0[SUB][KQ], a1[SUB][KQ], m0v[SUB][KQ], m1v[SUB][KQ];
-  load(tile, a0, m0v);
   while (tile < tiles) {
     load(tile + stride, a1, m1v);
     __builtin_amdgcn_sched_barrier(0);
@@ -322,7 +324,9 @@ hgd_status row_gemm(const RowGemm& p, hipStream_t st, const char* fn) {
 }
 
 int64_t splits_for(int64_t rows) {
-  int64_t s = (rows + 511) / 512;
+  // one 128-row batch per workgroup (4 waves × 32 rows): ≈ 250 workgroups already at 32 K rows
+  // (the Yelp-shaped learned-hypergraph products), where 512-row splits left 3/4 of the CUs idle
+  int64_t s = (rows + 127) / 128;
   if (s > kMaxSplits) s = kMaxSplits;
   return s < 1 ? 1 : s;
 }

@@ -390,6 +390,29 @@ __global__ void k_bernoulli_mask(uint64_t seed, int64_t n, float keep,
   mask[i] = floorf(u + keep) != 0.f ? 1 : 0;
 }
 
+// The same draw with the seed read from device memory (a counter a captured step advances).
+__global__ void k_bernoulli_mask_dev(const uint64_t* __restrict__ seed_ptr, int64_t n, float keep,
+                                     uint8_t* __restrict__ mask) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t h = splitmix64(seed_ptr[0] ^ splitmix64(static_cast<uint64_t>(i)));
+  const float u = static_cast<float>(h >> 40) * (1.0f / 16777216.0f);
+  mask[i] = floorf(u + keep) != 0.f ? 1 : 0;
+}
+
+// Zeroes entries [*count, capacity) of a capacity-sized dropped structure (valid index 0,
+// weight 0), so that nothing reading the arrays linearly meets uninitialised indices.
+__global__ void k_fill_tail(const int64_t* __restrict__ count, int64_t capacity,
+                            int32_t* __restrict__ col, float* __restrict__ val,
+                            int32_t* __restrict__ row_t, float* __restrict__ val_t) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= capacity || i < count[0]) return;
+  if (col) col[i] = 0;
+  if (row_t) row_t[i] = 0;
+  if (val) val[i] = 0.f;
+  if (val_t) val_t[i] = 0.f;
+}
+
 // HGD_DENSE_GREATER: v > thresh (torch.nonzero(H > thresh)); HGD_DENSE_NONZERO: v != 0
 // (torch.nonzero(H), the pattern of a dense adjacency such as DHCF's, DHCF.py:140).
 __device__ __forceinline__ bool dense_keep(float v, float thresh, int mode) {
@@ -681,6 +704,27 @@ extern "C" hgd_status hgd_bernoulli_mask(uint64_t seed, int64_t n, float keep, u
   hipLaunchKernelGGL(k_bernoulli_mask, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream),
                      seed, n, keep, mask);
   return check_launch("hgd_bernoulli_mask");
+}
+
+extern "C" hgd_status hgd_bernoulli_mask_dev(const uint64_t* seed, int64_t n, float keep,
+                                             uint8_t* mask, void* stream) {
+  clear_error();
+  HGD_REQUIRE(n >= 0 && seed && (mask || n == 0), "hgd_bernoulli_mask_dev: bad arguments");
+  if (n == 0) return HGD_OK;
+  hipLaunchKernelGGL(k_bernoulli_mask_dev, dim3(grid_for(n)), dim3(kBlock), 0,
+                     as_stream(stream), seed, n, keep, mask);
+  return check_launch("hgd_bernoulli_mask_dev");
+}
+
+extern "C" hgd_status hgd_dropedge_fill_tail(const int64_t* count, int64_t capacity,
+                                             int32_t* col, float* val, int32_t* row_t,
+                                             float* val_t, void* stream) {
+  clear_error();
+  HGD_REQUIRE(capacity >= 0 && count, "hgd_dropedge_fill_tail: bad arguments");
+  if (capacity == 0) return HGD_OK;
+  hipLaunchKernelGGL(k_fill_tail, dim3(grid_for(capacity)), dim3(kBlock), 0, as_stream(stream),
+                     count, capacity, col, val, row_t, val_t);
+  return check_launch("hgd_dropedge_fill_tail");
 }
 
 extern "C" size_t hgd_dropedge_structure_workspace_size(int64_t nnz) {

@@ -24,7 +24,7 @@ diagonals swapped.
 from __future__ import annotations
 
 import ctypes
-from typing import Optional
+from typing import Optional, Tuple
 
 import torch
 
@@ -431,7 +431,7 @@ class _ContrastLoss(torch.autograd.Function):
     """hgd_infonce_forward / hgd_infonce_backward (see contrast_loss)."""
 
     @staticmethod
-    def forward(ctx, E1, E2, nodes, temp: float):
+    def forward(ctx, E1, E2, nodes, temp: float, count=None):
         lib = nat.load()
         dev = E1.device
         E1c = E1 if E1.stride(1) == 1 else E1.contiguous()
@@ -445,42 +445,65 @@ class _ContrastLoss(torch.autograd.Function):
         wsb = lib.hgd_infonce_workspace_size(B, d)
         ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
         st = torch.cuda.current_stream(dev).cuda_stream
-        nat.check(lib.hgd_infonce_forward(
-            E1c.data_ptr(), E1c.stride(0), E2c.data_ptr(), E2c.stride(0), E1.shape[0],
-            nodes.data_ptr(), B, d, float(temp), P1.data_ptr(), P2.data_ptr(), inv1.data_ptr(),
-            inv2.data_ptr(), pos.data_ptr(), deno.data_ptr(), loss.data_ptr(), ws.data_ptr(), wsb,
-            st), "hgd_infonce_forward")
+        if count is None:
+            nat.check(lib.hgd_infonce_forward(
+                E1c.data_ptr(), E1c.stride(0), E2c.data_ptr(), E2c.stride(0), E1.shape[0],
+                nodes.data_ptr(), B, d, float(temp), P1.data_ptr(), P2.data_ptr(),
+                inv1.data_ptr(), inv2.data_ptr(), pos.data_ptr(), deno.data_ptr(),
+                loss.data_ptr(), ws.data_ptr(), wsb, st), "hgd_infonce_forward")
+        else:  # B is the capacity, the live count stays on the device
+            nat.check(lib.hgd_infonce_forward_n(
+                E1c.data_ptr(), E1c.stride(0), E2c.data_ptr(), E2c.stride(0), E1.shape[0],
+                nodes.data_ptr(), B, count.data_ptr(), d, float(temp), P1.data_ptr(),
+                P2.data_ptr(), inv1.data_ptr(), inv2.data_ptr(), pos.data_ptr(), deno.data_ptr(),
+                loss.data_ptr(), ws.data_ptr(), wsb, st), "hgd_infonce_forward_n")
         ctx.temp = float(temp)
         ctx.shapes = (E1.shape, E2.shape)
-        ctx.save_for_backward(P1, P2, inv1, inv2, deno, nodes)
+        ctx.has_count = count is not None
+        ctx.save_for_backward(P1, P2, inv1, inv2, deno, nodes, count)
         return loss
 
     @staticmethod
     def backward(ctx, g):
         lib = nat.load()
-        P1, P2, inv1, inv2, deno, nodes = ctx.saved_tensors
+        P1, P2, inv1, inv2, deno, nodes, count = ctx.saved_tensors
         B, d = P1.shape
         dev = P1.device
         g = g.to(dtype=torch.float32).reshape(1).contiguous()
-        dX1, dX2 = torch.empty_like(P1), torch.empty_like(P2)
         wsb = lib.hgd_infonce_workspace_size(B, d)
         ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
-        nat.check(lib.hgd_infonce_backward(
-            P1.data_ptr(), P2.data_ptr(), inv1.data_ptr(), inv2.data_ptr(), deno.data_ptr(), B, d,
-            ctx.temp, g.data_ptr(), dX1.data_ptr(), dX2.data_ptr(), ws.data_ptr(), wsb,
-            torch.cuda.current_stream(dev).cuda_stream), "hgd_infonce_backward")
+        st = torch.cuda.current_stream(dev).cuda_stream
         dE1 = dE2 = None
+        if ctx.has_count:
+            # the scatter into the table gradients runs inside the backward kernel (live rows
+            # only); the capacity rows past the count add nothing
+            f = dict(dtype=torch.float32, device=dev)
+            dE1 = torch.zeros(ctx.shapes[0], **f) if ctx.needs_input_grad[0] else None
+            dE2 = torch.zeros(ctx.shapes[1], **f) if ctx.needs_input_grad[1] else None
+            if dE1 is None and dE2 is None:
+                return None, None, None, None, None
+            nat.check(lib.hgd_infonce_backward_n(
+                P1.data_ptr(), P2.data_ptr(), inv1.data_ptr(), inv2.data_ptr(), deno.data_ptr(),
+                B, count.data_ptr(), d, ctx.temp, g.data_ptr(), nodes.data_ptr(),
+                ctx.shapes[0][0], nat.ptr(dE1), d, nat.ptr(dE2), d, ws.data_ptr(), wsb, st),
+                "hgd_infonce_backward_n")
+            return dE1, dE2, None, None, None
+        dX1, dX2 = torch.empty_like(P1), torch.empty_like(P2)
+        nat.check(lib.hgd_infonce_backward(
+            P1.data_ptr(), P2.data_ptr(), inv1.data_ptr(), inv2.data_ptr(), deno.data_ptr(),
+            B, d, ctx.temp, g.data_ptr(), dX1.data_ptr(), dX2.data_ptr(), ws.data_ptr(), wsb,
+            st), "hgd_infonce_backward")
         if ctx.needs_input_grad[0]:
             dE1 = torch.zeros(ctx.shapes[0], dtype=torch.float32, device=dev)
             dE1.index_add_(0, nodes, dX1)
         if ctx.needs_input_grad[1]:
             dE2 = torch.zeros(ctx.shapes[1], dtype=torch.float32, device=dev)
             dE2.index_add_(0, nodes, dX2)
-        return dE1, dE2, None, None
+        return dE1, dE2, None, None, None
 
 
 def contrast_loss(embeds1: torch.Tensor, embeds2: torch.Tensor, nodes: torch.Tensor,
-                  temp: float) -> torch.Tensor:
+                  temp: float, count: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``contrastLoss(embeds1, embeds2, nodes, temp)`` of util/loss_torch.py:103-110 (InfoNCE over
     the batch rows ``nodes``), fused: only the B batch rows are normalised and the [B, B]
     logits are never materialised. Device float32 tables with d a multiple of 16 up to 256;
@@ -494,6 +517,11 @@ def contrast_loss(embeds1: torch.Tensor, embeds2: torch.Tensor, nodes: torch.Ten
     if nodes.numel() == 0:
         raise ValueError("contrast_loss: empty batch")
     n = embeds1.shape[0]
+    if count is not None:
+        # capacity-sized node list with its live count on the device (unique_long_n): no bounds
+        # read to the host — the kernels wrap live ids like torch indexing (and clamp them),
+        # skip the rows past the count and scatter the gradient rows themselves
+        return _ContrastLoss.apply(embeds1, embeds2, nodes, float(temp), count)
     # torch indexing semantics (negative ids wrap; HCCF passes torch.unique(emb.long()), which
     # holds -1 / 0 / 1); out of range raises like embeds[nodes] would
     rng = getattr(nodes, "_hgd_range", None)  # set by unique_long: no device read needed
@@ -546,6 +574,32 @@ def unique_long(x: torch.Tensor) -> torch.Tensor:
 
 
 _UQ_HEAD = 256  # bytes before the unique workspace (count at 0; 256-byte aligned workspace)
+
+
+def unique_long_n(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """:func:`unique_long` without the device→host read, for a captured training step:
+    ``(nodes, count)`` with ``nodes`` int64 capacity-sized (x.numel()), its first ``count[0]``
+    entries the sorted unique values of ``x.long()`` and the rest 0, ``count`` an int64 [1]
+    device tensor (hgd_unique_sort_*: the range-independent path). Feed both to
+    :func:`contrast_loss`."""
+    if not x.is_cuda or x.dtype not in (torch.float32, torch.int64):
+        raise ValueError("unique_long_n: needs a float32 or int64 device tensor")
+    x = x.detach().contiguous().view(-1)
+    n = x.numel()
+    if n == 0:
+        raise ValueError("unique_long_n: empty input")
+    lib = nat.load()
+    dev = x.device
+    out = torch.empty(n, dtype=torch.int64, device=dev)
+    wsb = lib.hgd_unique_workspace_size(n)
+    buf = torch.empty(_UQ_HEAD + max(wsb, 1), dtype=torch.uint8, device=dev)
+    base = buf.data_ptr()
+    slow = lib.hgd_unique_sort_trunc_f32 if x.dtype == torch.float32 else lib.hgd_unique_sort_i64
+    nat.check(slow(x.data_ptr(), n, out.data_ptr(), base, base + _UQ_HEAD, wsb,
+                   torch.cuda.current_stream(dev).cuda_stream), "hgd_unique_sort")
+    count = buf[:8].view(torch.int64)
+    live = torch.arange(n, device=dev) < count
+    return torch.where(live, out, torch.zeros((), dtype=torch.int64, device=dev)), count
 
 
 def _mm_ok(H: torch.Tensor, X: torch.Tensor) -> bool:

@@ -344,12 +344,17 @@ class Incidence:
         inc.perm_t = perm  # CSC position → CSR position (sort-free drop-edge rebuilds)
         return inc
 
-    def drop(self, mask: torch.Tensor, keep: float, kept: Optional[int] = None) -> "Incidence":
+    def drop(self, mask: torch.Tensor, keep: float, kept: Optional[int] = None,
+             capacity: bool = False) -> "Incidence":
         """The incidence of SpAdjDropEdge's output (HCCF.py:217-226) built from this one without
         any sort: ``mask`` (uint8/bool, CSR order) keeps nonzeros in order and values are divided
         by ``keep``; the CSC comes from compacting this CSC through ``perm_t``
         (hgd_dropedge_structure). One device→host read (the kept count) unless the caller passes
-        ``kept`` (e.g. counted with a host-drawn mask)."""
+        ``kept`` (e.g. counted with a host-drawn mask) or asks for ``capacity``: then the kept
+        count stays on the device (the row pointers end at it), the arrays keep the parent's
+        length with a zeroed tail (hgd_dropedge_fill_tail), and rows longer than the split
+        threshold are walked by one lane group (no split plan: it would need the count) — no
+        host read, so a training step can be captured in a HIP graph."""
         lib = nat.load()
         dev = self.device
         st = _stream(dev)
@@ -373,6 +378,18 @@ class Incidence:
             col.data_ptr() if nnz else None, nat.ptr(val), colptr.data_ptr(),
             row_t.data_ptr() if nnz else None, nat.ptr(val_t), ws.data_ptr(), ws.numel(), st),
             "hgd_dropedge_structure")
+        if capacity:
+            if nnz:
+                nat.check(lib.hgd_dropedge_fill_tail(
+                    rowptr.data_ptr() + 8 * R, nnz, col.data_ptr(), nat.ptr(val),
+                    row_t.data_ptr(), nat.ptr(val_t), st), "hgd_dropedge_fill_tail")
+            csr = CSR(rowptr, col, R, C, 0, self.csr.split_chunk)
+            csc = CSR(colptr, row_t, C, R, 0, self.csc.split_chunk)
+            for child, parent in ((csr, self.csr), (csc, self.csc)):
+                child.plan.flags = parent.plan.flags if parent.n_heavy == 0 else 0
+            out = Incidence(csr, csc, val, val_t)
+            out.perm_t = None
+            return out
         if kept is None:
             kept = int(rowptr[R].item()) if R else 0
         col, row_t = col[:kept], row_t[:kept]

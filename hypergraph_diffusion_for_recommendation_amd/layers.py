@@ -183,13 +183,21 @@ class SpAdjDropEdge(nn.Module):
     structure is derived from the parent's without sorting (Incidence.drop).
     """
 
-    def __init__(self, device_rng: bool = False):
+    def __init__(self, device_rng: bool = False, capture_safe: bool = False):
         super().__init__()
         self.device_rng = device_rng
+        # capture_safe: device mask from a device-side seed counter and a capacity-sized child
+        # structure returned as the Incidence itself — no host read, no host RNG, so the step
+        # can be replayed from a HIP graph (fresh masks every replay). The return value is then
+        # an Incidence (what GCNLayer / HGCNConv consume), not a torch sparse COO.
+        self.capture_safe = capture_safe
+        self._seed = None
 
     def forward(self, adj, keepRate):
         if keepRate == 1.0:
             return adj
+        if self.capture_safe:
+            return self._capture_safe_drop(adj, float(keepRate))
         vals = adj._values()
         idxs = adj._indices()
         edgeNum = vals.size()
@@ -218,6 +226,24 @@ class SpAdjDropEdge(nn.Module):
         out._hgd_incidence = child if child is not None else Incidence.from_coo(
             new_idx, new_vals, adj.shape, device=device, validate=False)
         return out
+
+    def _capture_safe_drop(self, adj, keep: float) -> Incidence:
+        from . import _native as nat
+        parent = incidence_of(adj)
+        if not (parent.coo_sorted and parent.perm_t is not None):
+            raise RuntimeError("SpAdjDropEdge(capture_safe): needs a row-sorted base adjacency")
+        dev = parent.device
+        if self._seed is None or self._seed.device != dev:
+            # drawn once from the CPU generator (torch.manual_seed fixes the stream); advanced
+            # on the device afterwards
+            self._seed = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).to(dev)
+        mask = torch.empty(parent.nnz, dtype=torch.uint8, device=dev)
+        if parent.nnz:
+            nat.check(nat.load().hgd_bernoulli_mask_dev(
+                self._seed.data_ptr(), parent.nnz, keep, mask.data_ptr(),
+                torch.cuda.current_stream(dev).cuda_stream), "hgd_bernoulli_mask_dev")
+        self._seed.add_(1)
+        return parent.drop(mask, keep, capacity=True)
 
 
 class Linear(nn.Linear):

@@ -45,7 +45,7 @@ from torch.optim.lr_scheduler import ReduceLROnPlateau
 
 from .encoders import (HCCFDiffusionEncoder, HCCFEncoder, LocalAwareEncoder,
                        LocalAwareEncoderHD3, sparse_tensor_of)
-from .functional import contrast_loss, unique_long
+from .functional import contrast_loss, unique_long, unique_long_n
 from .layers import HGCNConv, SpAdjDropEdge
 from .sampler import next_batch_pairwise
 from .selfrec import GraphRecommender, early_stopping
@@ -75,7 +75,18 @@ class HCCF(GraphRecommender):
         self.model.edgeDropper.device_rng = bool(kwargs.get('hgd_device_rng', False))
         self._parse_config(self.config, kwargs)
         self.model.to(self.device)
-        self.optimizer = torch.optim.Adam(self.model.parameters(), lr=self.lRate)
+        # hgd_graph: the training step replayed from one HIP graph (graphs.CapturedStep) — the
+        # device drop-edge mask from a device seed counter, device-side InfoNCE node counts and a
+        # capturable Adam (its lr a device tensor the scheduler updates in place); the same math
+        self.graph_mode = bool(kwargs.get('hgd_graph', False))
+        self._captured = None
+        if self.graph_mode:
+            self.model.edgeDropper.device_rng = True
+            self.model.edgeDropper.capture_safe = True
+            lr = torch.tensor(self.lRate, dtype=torch.float32, device=self.device)
+            self.optimizer = torch.optim.Adam(self.model.parameters(), lr=lr, capturable=True)
+        else:
+            self.optimizer = torch.optim.Adam(self.model.parameters(), lr=self.lRate)
         self.scheduler = ReduceLROnPlateau(self.optimizer, 'min', factor=self.lr_decay,
                                            patience=5)
 
@@ -101,14 +112,19 @@ class HCCF(GraphRecommender):
         bprLoss = bpr_loss(ancs, poss, negs)
         nu = self.data.n_users
         # torch.unique(ancs.long()) / torch.unique(poss.long()) are the same in every layer of the
-        # reference's loop: computed once here (each is a device→host read)
-        u_nodes, p_nodes = unique_long(ancs), unique_long(poss)
+        # reference's loop: computed once here (each is a device→host read — or, in graph mode,
+        # capacity-sized with the count kept on the device)
+        if getattr(self, "graph_mode", False):
+            (u_nodes, u_cnt), (p_nodes, p_cnt) = unique_long_n(ancs), unique_long_n(poss)
+        else:
+            u_nodes, p_nodes = unique_long(ancs), unique_long(poss)
+            u_cnt = p_cnt = None
         sslLoss = 0
         for i in range(self.nLayers):
             embeds1 = gcnEmbedsLst[i].detach()
             embeds2 = hyperEmbedsLst[i]
-            sslLoss += contrast_loss(embeds1[:nu], embeds2[:nu], u_nodes, self.temp) \
-                + contrast_loss(embeds1[nu:], embeds2[nu:], p_nodes, self.temp)
+            sslLoss += contrast_loss(embeds1[:nu], embeds2[:nu], u_nodes, self.temp, u_cnt) \
+                + contrast_loss(embeds1[nu:], embeds2[nu:], p_nodes, self.temp, p_cnt)
         sslLoss *= self.ss_rate
         return bprLoss, sslLoss
 
@@ -129,6 +145,26 @@ class HCCF(GraphRecommender):
         self.optimizer.step()
         return batch_loss
 
+    def graph_step(self, user_idx, pos_idx, neg_idx) -> torch.Tensor:
+        """:meth:`train_step`, replayed from a HIP graph in graph mode: the first full-size batch
+        runs eagerly (a real step that also allocates the optimizer state), the second is
+        recorded (recording runs nothing) and replayed, every later full-size batch replays;
+        a short last batch runs eagerly (its shapes differ)."""
+        if not getattr(self, "graph_mode", False):  # (subclasses with their own __init__)
+            return self.train_step(user_idx, pos_idx, neg_idx)
+        full = user_idx.numel() == self.batchSize
+        cap = self._captured
+        if cap is not None and full:
+            return cap(user_idx, pos_idx, neg_idx).detach().clone()
+        if cap is None and full and getattr(self, "_eager_steps", 0) >= 1:
+            from .graphs import CapturedStep
+            self._captured = CapturedStep(self.train_step, (user_idx, pos_idx, neg_idx))
+            return self._captured(user_idx, pos_idx, neg_idx).detach().clone()
+        self._eager_steps = getattr(self, "_eager_steps", 0) + 1
+        # detached: a caller holding the loss would keep the eager autograd graph — and with it
+        # the parameters' AccumulateGrad nodes, bound to the eager stream — alive into the capture
+        return self.train_step(user_idx, pos_idx, neg_idx).detach()
+
     def train(self, load_pretrained=False):  # HCCF.py:72-118
         model = self.model
         recall_list = []
@@ -139,7 +175,7 @@ class HCCF(GraphRecommender):
             for n, batch in enumerate(next_batch_pairwise(self.data, self.batchSize,
                                                           device=self.device)):
                 user_idx, pos_idx, neg_idx = batch
-                batch_loss = self.train_step(user_idx, pos_idx, neg_idx)
+                batch_loss = self.graph_step(user_idx, pos_idx, neg_idx)
                 train_losses.append(batch_loss.item())
             tr_time = time.time() - s_train
             model.eval()

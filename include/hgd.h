@@ -235,6 +235,30 @@ hgd_status hgd_infonce_backward(const float* P1, const float* P2, const float* i
                                 int32_t d, float temp, const float* grad_loss, float* dX1,
                                 float* dX2, void* workspace, size_t workspace_bytes,
                                 void* stream);
+/* The same with the batch size held on the device (*batch_count <= capacity; the node list
+ * is capacity-sized, e.g. a device-side unique whose count is never read back): grids and
+ * strides use `capacity`, the kernels read the live count, rows past it come out as zeros
+ * (P1/P2/dX1/dX2) and the mean divides by the live count. Nothing is read to the host, so a
+ * training step using them can be captured in a HIP graph. Workspace:
+ * hgd_infonce_workspace_size(capacity, d). */
+hgd_status hgd_infonce_forward_n(const float* E1, int64_t ld1, const float* E2, int64_t ld2,
+                                 int64_t n_rows, const int64_t* nodes, int64_t capacity,
+                                 const int64_t* batch_count, int32_t d, float temp, float* P1,
+                                 float* P2, float* inv_norm1, float* inv_norm2, float* pos_logit,
+                                 float* deno, float* loss, void* workspace,
+                                 size_t workspace_bytes, void* stream);
+/* Backward with the scatter fused: the gradient rows are added straight into the [n_rows, d]
+ * table gradients dE1 / dE2 (zero-filled by the caller; either may be NULL: that side is not
+ * computed) at
+ * the batch rows' nodes (torch indexing, negative ids wrap), rows past *batch_count add nothing.
+ * Atomic adds, but at most two batch rows meet on one table row, so the result is
+ * deterministic. */
+hgd_status hgd_infonce_backward_n(const float* P1, const float* P2, const float* inv_norm1,
+                                  const float* inv_norm2, const float* deno, int64_t capacity,
+                                  const int64_t* batch_count, int32_t d, float temp,
+                                  const float* grad_loss, const int64_t* nodes, int64_t n_rows,
+                                  float* dE1, int64_t ldE1, float* dE2, int64_t ldE2,
+                                  void* workspace, size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Ingest and graph build — the data path producing the hot path's
@@ -322,6 +346,15 @@ hgd_status hgd_dropedge_compact(const int64_t* rows, const int64_t* cols, const 
  * from a counter-based hash of (seed, i) — the SpAdjDropEdge expression (HCCF.py:223) without
  * the host RNG round trip (statistically, not bitwise, equal to torch's CPU stream). */
 hgd_status hgd_bernoulli_mask(uint64_t seed, int64_t n, float keep, uint8_t* mask, void* stream);
+/* The same draw with the 64-bit seed read from device memory (seed[0]): a captured training step
+ * advances the counter on the device, so every graph replay draws a fresh mask. */
+hgd_status hgd_bernoulli_mask_dev(const uint64_t* seed, int64_t n, float keep, uint8_t* mask,
+                                  void* stream);
+/* Zeroes entries [*count, capacity) of the capacity-sized outputs of hgd_dropedge_structure
+ * (count = rowptr_out + n_rows, on the device): a dropped structure whose kept count is never read
+ * back keeps full-size arrays with a defined tail (index 0, weight 0). Null arrays are skipped. */
+hgd_status hgd_dropedge_fill_tail(const int64_t* count, int64_t capacity, int32_t* col,
+                                  float* val, int32_t* row_t, float* val_t, void* stream);
 
 /* Sort-free rebuild of a drop-edge'd structure from its parent: compacts the parent CSR with the
  * mask (CSR order) and the parent CSC with mask[perm_t[e']] (perm_t: CSC position → CSR

@@ -551,3 +551,25 @@ def next_batch_pairwise(data, batch_size, n_negs=1):
                     neg_item = choice(item_list)
                 j_idx.append(data.item[neg_item])
         yield u_idx, i_idx, j_idx
+
+
+def device_keep_mask(seed, n, keep):
+    """The keep-mask of the library's device drop-edge draw (hgd_bernoulli_mask /
+    hgd_bernoulli_mask_dev: the build's own counter-based RNG for ``SpAdjDropEdge(device_rng=
+    True)``; the reference draws ``torch.rand`` on the CPU, HCCF.py:223, which the default path
+    reproduces bit for bit instead). u = top 24 bits of splitmix64(seed ^ splitmix64(i)) / 2^24,
+    kept iff floor(u + keep) != 0 in float32 — the same Bernoulli(keep) decision rule as
+    HCCF.py:223 on a different uniform stream. Bit-exact restatement for testing."""
+    m64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+    def splitmix64(x):
+        with np.errstate(over="ignore"):
+            x = (x + np.uint64(0x9E3779B97F4A7C15)) & m64
+            x = ((x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)) & m64
+            x = ((x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)) & m64
+            return x ^ (x >> np.uint64(31))
+
+    i = np.arange(n, dtype=np.uint64)
+    h = splitmix64(np.uint64(seed) ^ splitmix64(i))
+    u = (h >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+    return np.floor(u + np.float32(keep)) != 0

@@ -8,6 +8,8 @@ reference calls it) and Adam. Variants:
                      HGNNLayer and InfoNCE on this library; the drop-edge mask drawn by the
                      reference's CPU torch.rand (bit-identical masks for a seed);
 * hgd_device_mask  — the same with SpAdjDropEdge(device_rng=True);
+* hgd_graph        — the device-mask step replayed from one HIP graph (graphs.CapturedStep:
+                     capture-safe drop-edge, device-side InfoNCE node counts, capturable Adam);
 * reference_ops    — scripts/refops.HCCFEncoderRef + the reference's losses (torch.sparse.mm,
                      torch.mm, F.normalize …) on the same GPU, same parameters.
 
@@ -33,13 +35,16 @@ def main():
     ap.add_argument("--layers", type=int, default=3)
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--variants", default="hgd_cpu_mask,hgd_device_mask,reference_ops")
+    ap.add_argument("--variants", default="hgd_cpu_mask,hgd_device_mask,hgd_graph,reference_ops")
     args = ap.parse_args()
     import torch
 
     import refops as R
     from hypergraph_diffusion_for_recommendation_amd.encoders import HCCFEncoder
-    from hypergraph_diffusion_for_recommendation_amd.functional import contrast_loss, unique_long
+    from hypergraph_diffusion_for_recommendation_amd.functional import (contrast_loss,
+                                                                         unique_long,
+                                                                         unique_long_n)
+    from hypergraph_diffusion_for_recommendation_amd.graphs import CapturedStep
 
     dev = torch.device("cuda")
     u, i = R.synthetic_incidence(args.users, args.items, args.edges, seed=0)
@@ -55,13 +60,16 @@ def main():
                 torch.randint(0, ni, (args.batch,), device=dev, generator=g),
                 torch.randint(0, ni, (args.batch,), device=dev, generator=g)) for _ in range(8)]
 
-    def make_step(model, loss_fn, unique, hoist=True):
-        opt = torch.optim.Adam(model.parameters(), lr=conf["lrate"])
-        state = {"k": 0}
+    def make_step(model, loss_fn, unique, hoist=True, graph=False, counted=None):
+        counted = graph if counted is None else counted
+        if counted:
+            lr = torch.tensor(conf["lrate"], dtype=torch.float32, device=dev)
+            opt = torch.optim.Adam(model.parameters(), lr=lr, capturable=True)
+        else:
+            opt = torch.optim.Adam(model.parameters(), lr=conf["lrate"])
+        state = {"k": 0, "cap": None}
 
-        def step():
-            uid, pid, nid = batches[state["k"] % len(batches)]
-            state["k"] += 1
+        def body(uid, pid, nid):
             ue, ie, gcn, hyp = model(keep_rate=keep)
             anc, pos, neg = ue[uid], ie[pid], ie[nid]
             ssl = 0
@@ -70,13 +78,29 @@ def main():
             for layer in range(args.layers):
                 e1, e2 = gcn[layer].detach(), hyp[layer]
                 nu_nodes, np_nodes = un if hoist else (unique(anc), unique(pos))
-                ssl = ssl + loss_fn(e1[:nu], e2[:nu], nu_nodes, temp) \
-                    + loss_fn(e1[nu:], e2[nu:], np_nodes, temp)
+                if counted:  # (nodes, device count) pairs
+                    ssl = ssl + loss_fn(e1[:nu], e2[:nu], nu_nodes[0], temp, nu_nodes[1]) \
+                        + loss_fn(e1[nu:], e2[nu:], np_nodes[0], temp, np_nodes[1])
+                else:
+                    ssl = ssl + loss_fn(e1[:nu], e2[:nu], nu_nodes, temp) \
+                        + loss_fn(e1[nu:], e2[nu:], np_nodes, temp)
             loss = R.bpr_loss(anc, pos, neg) + cl_rate * ssl
             opt.zero_grad()
             torch.nn.utils.clip_grad_norm_(model.parameters(), 4)  # before backward, as HCCF.py:95
             loss.backward()
             opt.step()
+            return loss
+
+        def step():
+            uid, pid, nid = batches[state["k"] % len(batches)]
+            state["k"] += 1
+            if not graph:
+                return body(uid, pid, nid)
+            if state["cap"] is None:
+                if state["k"] == 1:
+                    return body(uid, pid, nid)  # one eager step: optimizer state, handles
+                state["cap"] = CapturedStep(body, (uid, pid, nid))
+            return state["cap"](uid, pid, nid)
         return step
 
     def timed(step):
@@ -105,6 +129,22 @@ def main():
     if "hgd_device_mask" in want:
         ours.edgeDropper.device_rng = True
         out.append(("hgd_device_mask", timed(make_step(ours, contrast_loss, unique_long))))
+    if "hgd_graph" in want:
+        torch.manual_seed(0)
+        g_model = HCCFEncoder(conf, data, dev)
+        g_model.load_state_dict(ours.state_dict())
+        g_model.edgeDropper.device_rng = True
+        g_model.edgeDropper.capture_safe = True
+        out.append(("hgd_graph", timed(make_step(g_model, contrast_loss, unique_long_n,
+                                                 graph=True))))
+    if "hgd_capture_safe_eager" in want:  # the graph variant's ops, launched eagerly
+        torch.manual_seed(0)
+        e_model = HCCFEncoder(conf, data, dev)
+        e_model.load_state_dict(ours.state_dict())
+        e_model.edgeDropper.device_rng = True
+        e_model.edgeDropper.capture_safe = True
+        out.append(("hgd_capture_safe_eager", timed(make_step(e_model, contrast_loss,
+                                                              unique_long_n, counted=True))))
     if "reference_ops" in want:
         out.append(("reference_ops", timed(make_step(ref, R.contrast_loss, lambda t: torch.unique(t.long()), hoist=False))))
     for name, ms in out:
