@@ -16,6 +16,7 @@ executes nothing) and every later batch is copied into its static inputs and rep
 """
 from __future__ import annotations
 
+import gc
 from typing import Callable, Sequence
 
 import torch
@@ -31,6 +32,9 @@ class CapturedStep:
 
     def __init__(self, step: Callable, example_inputs: Sequence[torch.Tensor]):
         self.static = [t.detach().clone() for t in example_inputs]
+        # free eager autograd graphs still held by reference cycles: their AccumulateGrad nodes
+        # would otherwise carry the eager stream into the capture
+        gc.collect()
         torch.cuda.synchronize(self.static[0].device)
         self.graph = torch.cuda.CUDAGraph()
         # thread-local capture: a host thread of the harness (e.g. a keep-mask prefetch worker
