@@ -66,8 +66,9 @@ def parse():
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                     help="strong: one global graph sharded by user rows (default); weak: one "
                          "full-size graph per rank")
-    ap.add_argument("--chunks", type=int, default=1,
-                    help="item-row chunks per exchanged column slice (N > 1)")
+    ap.add_argument("--chunks", type=int, default=4,
+                    help="item-row chunks per exchanged column slice (N > 1): each chunk's "
+                         "all-reduce is queued behind the hop-1 kernel that produced it")
     ap.add_argument("--slice-width", type=int, default=None,
                     help="embedding columns per pipelined all-reduce block (N > 1; default 32 "
                          "for d <= 128, else 64)")
@@ -309,6 +310,7 @@ def main():
 
     from hypergraph_diffusion_for_recommendation_amd import Incidence, profiling
     from hypergraph_diffusion_for_recommendation_amd.sharded import (ShardedIncidence,
+                                                                       init_process_group,
                                                                        sharded_two_hop)
 
     # one rank per GPU; the modulo only matters for rehearsing N ranks on fewer GPUs (gloo)
@@ -317,11 +319,8 @@ def main():
     torch.cuda.set_device(device)
     dist_backend = None
     if world > 1:
-        backend = dist_backend = os.environ.get("HGD_DIST_BACKEND", "nccl")  # nccl == RCCL
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=device)
-        else:
-            dist.init_process_group(backend)
+        dist_backend = os.environ.get("HGD_DIST_BACKEND", "nccl")  # nccl == RCCL
+        init_process_group(device, dist_backend)
 
     shard_kw = dict(n_chunks=args.chunks, P="sym", Q="mean", R="sym",
                     slice_width=args.slice_width)

@@ -27,6 +27,17 @@ constexpr float kShift = 1e-8f;   // embeds + 1e-8 (loss_torch.py:104-105)
 constexpr float kNormEps = 1e-12f;  // F.normalize eps
 constexpr float kDenoEps = 1e-8f;   // ... .sum(-1) + 1e-8 (loss_torch.py:109)
 
+// exp(s/τ) as 2^(s·k2) with k2 = log2(e)/τ rounded once on the host: the bare v_exp_f32 (about
+// 1 ulp) instead of expf's 12-instruction range reduction. The extra error is the rounding of
+// s·k2, |s·k2|·2^-24 relative (3e-7 at τ = 0.05, |s| ≤ 1): far inside the 1e-5 bound, and the
+// forward sums and the backward's recomputed weights use the same formula. Results below 2^-126
+// flush to 0 (a logit 87·τ below the row's: no weight at fp32 resolution of the sum anyway).
+__device__ __forceinline__ float exp2_raw(float x) { return __builtin_amdgcn_exp2f(x); }
+
+inline float exp2_scale(float temp) {
+  return static_cast<float>(1.4426950408889634 / static_cast<double>(temp));
+}
+
 // ---- gather + normalise: one group of G = d/4 lanes per batch row ----
 template <int G>
 __global__ __launch_bounds__(256) void k_nce_gather(const float* __restrict__ E1, int64_t ld1,
@@ -86,61 +97,100 @@ __device__ __forceinline__ void load_frag4(const float* M, int64_t B, int d, int
   for (int q = 0; q < DQ / 4; ++q) f[q] = *reinterpret_cast<const f32x4*>(row + 16 * q);
 }
 
+// ---- shared staging of the streamed rows ----
+// The four waves of a workgroup own different 16-row blocks but stream the SAME rows of the other
+// matrix, so those rows go through LDS once per workgroup (a quarter of the L2 traffic of per-wave
+// loads, and no register ping-pong: the double buffer is in LDS). A stage is KT rows, loaded
+// cooperatively as float4s into registers while the previous stage is consumed, then written to
+// the other LDS buffer behind one barrier. Rows are padded by 4 floats, so the 16 lanes that read
+// 16 different rows at one column (a fragment load) hit 16 different bank quads.
+constexpr int kStageRows = 32;
+
+template <int DQ>
+struct Stage {
+  static constexpr int D = 4 * DQ;
+  static constexpr int LDR = D + 4;                       // padded row (floats)
+  static constexpr int PER = (kStageRows * DQ + 255) / 256;  // float4s per thread per stage
+};
+
+template <int DQ>
+__device__ __forceinline__ void stage_load(const float* M, int64_t Be, int64_t k0,
+                                           f32x4 (&v)[Stage<DQ>::PER]) {
+#pragma unroll
+  for (int i = 0; i < Stage<DQ>::PER; ++i) {
+    const int e = threadIdx.x + 256 * i;
+    int64_t row = k0 + e / DQ;
+    row = row < Be ? row : Be - 1;  // rows past the live count: clamped, masked when consumed
+    if (e < kStageRows * DQ) v[i] = ld4(M + row * (4 * DQ) + 4 * (e % DQ));
+  }
+}
+
+template <int DQ>
+__device__ __forceinline__ void stage_store(float* s, const f32x4 (&v)[Stage<DQ>::PER]) {
+#pragma unroll
+  for (int i = 0; i < Stage<DQ>::PER; ++i) {
+    const int e = threadIdx.x + 256 * i;
+    if (e < kStageRows * DQ)
+      *reinterpret_cast<f32x4*>(s + (e / DQ) * Stage<DQ>::LDR + 4 * (e % DQ)) = v[i];
+  }
+}
+
+// Fragment of rows [r0, r0+16) of a staged tile, in load_frag4's k order.
+template <int DQ>
+__device__ __forceinline__ void lds_frag4(const float* s, int r0, int lane, f32x4 (&f)[DQ / 4]) {
+  const float* row = s + (r0 + (lane & 15)) * Stage<DQ>::LDR + 4 * (lane >> 4);
+#pragma unroll
+  for (int q = 0; q < DQ / 4; ++q) f[q] = *reinterpret_cast<const f32x4*>(row + 16 * q);
+}
+
 // ---- forward exp-sums: partial[s][b] = Σ_{j in slice s} exp(<p1_b, p2_j>/τ) ----
-// A wave owns 16 rows of p1; the slice's p2 rows stream in 64-row super-tiles (4 MFMA tiles)
-// through a copy-free ping-pong, so a super-tile's loads are in flight behind the previous
-// one's MFMAs and exps.
+// A wave owns 16 rows of p1 (fragments in registers); the slice's p2 rows stream through LDS in
+// 32-row stages shared by the workgroup's four waves.
 template <int DQ>  // d = 4·DQ
 __global__ __launch_bounds__(256) void k_nce_rowsum(const float* __restrict__ P1,
                                                     const float* __restrict__ P2, int64_t B,
-                                                    float inv_temp, int64_t j_per_slice,
+                                                    float k2, int64_t j_per_slice,
                                                     float* partial, const int64_t* Bp) {
+  using St = Stage<DQ>;
   constexpr int Q4 = DQ / 4;
-  constexpr int SUB = 4;
+  __shared__ float sm[2][kStageRows * St::LDR];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int64_t b0 = static_cast<int64_t>(blockIdx.x) * 64 + 16 * wave;
   const int64_t Be = Bp ? *Bp : B;  // live rows (B is the capacity: strides, clamps)
-  if (b0 >= Be) return;
+  const int64_t blk0 = static_cast<int64_t>(blockIdx.x) * 64;
+  if (blk0 >= Be) return;  // uniform over the workgroup
+  const int64_t b0 = blk0 + 16 * wave;
   const int d = 4 * DQ;
   f32x4 a[Q4];
-  load_frag4<DQ>(P1, Be, d, b0, lane, a);  // rows clamped to the live ones (the rest unwritten)
+  load_frag4<DQ>(P1, Be, d, b0 < Be ? b0 : blk0, lane, a);  // a wave past the end: dummy rows
   const int64_t j_begin = static_cast<int64_t>(blockIdx.y) * j_per_slice;
   const int64_t j_end = min(Be, j_begin + j_per_slice);
   float psum[4] = {0.f, 0.f, 0.f, 0.f};
-  auto load = [&](int64_t j0, f32x4 (&f)[SUB][Q4]) {
+  f32x4 v[St::PER];
+  stage_load<DQ>(P2, Be, j_begin, v);
+  stage_store<DQ>(sm[0], v);
+  __syncthreads();
+  int buf = 0;
+  for (int64_t j0 = j_begin; j0 < j_end; j0 += kStageRows) {
+    const bool more = j0 + kStageRows < j_end;
+    if (more) stage_load<DQ>(P2, Be, j0 + kStageRows, v);
 #pragma unroll
-    for (int t = 0; t < SUB; ++t) load_frag4<DQ>(P2, Be, d, j0 + 16 * t, lane, f[t]);
-  };
-  auto compute = [&](int64_t j0, const f32x4 (&f)[SUB][Q4]) {
-#pragma unroll
-    for (int t = 0; t < SUB; ++t) {
+    for (int t = 0; t < kStageRows / 16; ++t) {
+      f32x4 f[Q4];
+      lds_frag4<DQ>(sm[buf], 16 * t, lane, f);
       f32x4 s = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int q = 0; q < Q4; ++q)
 #pragma unroll
-        for (int c = 0; c < 4; ++c) s = mfma4(a[q][c], f[t][q][c], s);
+        for (int c = 0; c < 4; ++c) s = mfma4(a[q][c], f[q][c], s);
       // s[r] = <p1_{b0 + 4(l>>4) + r}, p2_{j0 + 16t + (l&15)}>
       const bool jok = j0 + 16 * t + (lane & 15) < j_end;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) psum[r] += jok ? expf(s[r] * inv_temp) : 0.f;
+      for (int r = 0; r < 4; ++r) psum[r] += jok ? exp2_raw(s[r] * k2) : 0.f;
     }
-  };
-  f32x4 f0[SUB][Q4], f1[SUB][Q4];
-  int64_t j0 = j_begin;
-  load(j0, f0);
-  while (j0 < j_end) {
-    load(j0 + 16 * SUB, f1);
-    __builtin_amdgcn_sched_barrier(0);
-    compute(j0, f0);
-    __builtin_amdgcn_sched_barrier(0);
-    j0 += 16 * SUB;
-    if (j0 >= j_end) break;
-    load(j0 + 16 * SUB, f0);
-    __builtin_amdgcn_sched_barrier(0);
-    compute(j0, f1);
-    __builtin_amdgcn_sched_barrier(0);
-    j0 += 16 * SUB;
+    if (more) stage_store<DQ>(sm[buf ^ 1], v);
+    __syncthreads();
+    buf ^= 1;
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) psum[r] = group_sum<16>(psum[r]);
@@ -154,6 +204,8 @@ __global__ __launch_bounds__(256) void k_nce_rowsum(const float* __restrict__ P1
 }
 
 // ---- finish: deno_b, loss = -(1/B) Σ_b log(exp(pos_b) / deno_b), fixed-order reductions ----
+// One workgroup; each thread's rows are summed over the S slice partials in slice order, eight
+// independent loads at a time (a serial chain of S dependent loads per row was 19 µs at B = 4096).
 __global__ __launch_bounds__(1024) void k_nce_finish(const float* __restrict__ partial,
                                                      int64_t S, int64_t B,
                                                      const float* __restrict__ pos_logit,
@@ -164,7 +216,15 @@ __global__ __launch_bounds__(1024) void k_nce_finish(const float* __restrict__ p
   float acc = 0.f;
   for (int64_t b = threadIdx.x; b < Be; b += 1024) {
     float den = 0.f;
-    for (int64_t s = 0; s < S; ++s) den += partial[s * B + b];
+    int64_t s = 0;
+    for (; s + 8 <= S; s += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = partial[(s + u) * B + b];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) den += v[u];
+    }
+    for (; s < S; ++s) den += partial[s * B + b];
     den += kDenoEps;
     deno[b] = den;
     acc += logf(expf(pos_logit[b]) / den);
@@ -182,109 +242,112 @@ __global__ __launch_bounds__(1024) void k_nce_finish(const float* __restrict__ p
 // ROWS = true : part[s][b][:] = Σ_{j in slice s} G_bj p2_j       (dP1)
 // ROWS = false: part[s][j][:] = Σ_{b in slice s} G_bj p1_b       (dP2)
 // with G_bj = coef·(exp(s_bj/τ)/deno_b − δ_bj), coef = g/(B·τ).
+// The "other" rows of the slice stream through LDS in 32-row stages shared by the workgroup's
+// four waves (with their denominators when those index the other rows); each 16-row tile is read
+// twice from the stage: as logit fragments (row on the lane) and, transposed, as the B operand of
+// the accumulation (feature on the lane) — the LDS read replaces the per-lane strided scalar
+// loads of that operand.
 template <int DQ, bool ROWS>
 __global__ __launch_bounds__(256) void k_nce_bwd(const float* __restrict__ P1,
                                                  const float* __restrict__ P2, int64_t B,
-                                                 float inv_temp, const float* __restrict__ deno,
+                                                 float k2, const float* __restrict__ deno,
                                                  const float* __restrict__ grad, float temp,
                                                  int64_t k_per_slice, float* part,
                                                  const int64_t* Bp) {
+  using St = Stage<DQ>;
   constexpr int Q4 = DQ / 4;
-  constexpr int SUB = 2;  // 16-row tiles of the streamed matrix per ping-pong stage
+  __shared__ float sm[2][kStageRows * St::LDR];
+  __shared__ float sinv[2][kStageRows];  // 1/deno of the staged other rows (ROWS = false)
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
+  const int i16 = lane & 15;
+  const int h = lane >> 4;
   const int d = 4 * DQ;
   const int64_t Be = Bp ? *Bp : B;  // live rows (B is the capacity: strides, clamps)
+  const int64_t blk0 = static_cast<int64_t>(blockIdx.x) * 64;
+  if (blk0 >= Be) return;  // uniform over the workgroup
   // upstream dL/dloss and the 1/(B·τ) of the mean: device values, no host sync
   const float coef = grad[0] / (static_cast<float>(Be) * temp);
-  // "own" rows: b (ROWS) or j (!ROWS); "other" rows are streamed in 16-row tiles
+  // "own" rows: b (ROWS) or j (!ROWS); "other" rows are streamed
   const float* own_m = ROWS ? P1 : P2;
   const float* oth_m = ROWS ? P2 : P1;
-  const int64_t o0 = static_cast<int64_t>(blockIdx.x) * 64 + 16 * wave;
-  if (o0 >= Be) return;
+  const int64_t o0 = blk0 + 16 * wave;
   f32x4 own[Q4];
-  load_frag4<DQ>(own_m, Be, d, o0, lane, own);  // rows clamped to the live ones
-  const int64_t o_lane = o0 + (lane & 15);  // own row of this lane in the logit tile below
-  float deno_own = 1.f;
-  if (ROWS) deno_own = deno[o_lane < Be ? o_lane : Be - 1];
+  load_frag4<DQ>(own_m, Be, d, o0 < Be ? o0 : blk0, lane, own);  // rows clamped to live ones
+  const int64_t o_lane = o0 + i16;  // own row of this lane in the logit tile below
+  float inv_own = 1.f;
+  if (ROWS) inv_own = 1.f / deno[o_lane < Be ? o_lane : Be - 1];
   const int64_t k_begin = static_cast<int64_t>(blockIdx.y) * k_per_slice;
   const int64_t k_end = min(Be, k_begin + k_per_slice);
   f32x4 acc[DQ / 4];
 #pragma unroll
   for (int t = 0; t < DQ / 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // per 16-row tile: the other rows as logit fragments (row on the lane) and as the B operand of
-  // the accumulation (feature on the lane): bv[r][t] = oth[k0 + 4(l>>4) + r][16t + (l&15)]
-  struct Tile {
-    f32x4 of[Q4];
-    float bv[4][DQ / 4];
+  auto load_inv = [&](int64_t k0) -> float {
+    if (ROWS || threadIdx.x >= kStageRows) return 0.f;
+    int64_t k = k0 + threadIdx.x;
+    k = k < Be ? k : Be - 1;
+    return 1.f / deno[k];
   };
-  auto load = [&](int64_t k0, Tile (&T)[SUB]) {
-#pragma unroll
-    for (int u = 0; u < SUB; ++u) {
-      const int64_t kt = k0 + 16 * u;
-      load_frag4<DQ>(oth_m, Be, d, kt, lane, T[u].of);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        int64_t k = kt + 4 * (lane >> 4) + r;
-        k = k < Be ? k : Be - 1;
-#pragma unroll
-        for (int t = 0; t < DQ / 4; ++t) T[u].bv[r][t] = oth_m[k * d + 16 * t + (lane & 15)];
-      }
+  f32x4 v[St::PER];
+  stage_load<DQ>(oth_m, Be, k_begin, v);
+  float vinv = load_inv(k_begin);
+  stage_store<DQ>(sm[0], v);
+  if (!ROWS && threadIdx.x < kStageRows) sinv[0][threadIdx.x] = vinv;
+  __syncthreads();
+  int buf = 0;
+  for (int64_t k0 = k_begin; k0 < k_end; k0 += kStageRows) {
+    const bool more = k0 + kStageRows < k_end;
+    if (more) {
+      stage_load<DQ>(oth_m, Be, k0 + kStageRows, v);
+      vinv = load_inv(k0 + kStageRows);
     }
-  };
-  auto compute = [&](int64_t k0, const Tile (&T)[SUB]) {
+    const float* s_tile = sm[buf];
 #pragma unroll
-    for (int u = 0; u < SUB; ++u) {
+    for (int u = 0; u < kStageRows / 16; ++u) {
       const int64_t kt = k0 + 16 * u;
       // logit tile with the OTHER index on the output rows:
       // s[r] = <oth_{kt + 4(l>>4) + r}, own_{o0 + (l&15)}>
+      f32x4 of[Q4];
+      lds_frag4<DQ>(s_tile, 16 * u, lane, of);
       f32x4 s = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int q = 0; q < Q4; ++q)
 #pragma unroll
-        for (int c = 0; c < 4; ++c) s = mfma4(T[u].of[q][c], own[q][c], s);
+        for (int c = 0; c < 4; ++c) s = mfma4(of[q][c], own[q][c], s);
       float gk[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int64_t k = kt + 4 * (lane >> 4) + r;  // other index of register r
-        const bool kok = k < k_end;
-        const int64_t kc = k < Be ? k : Be - 1;
-        const float e = expf(s[r] * inv_temp);
-        const float den = ROWS ? deno_own : deno[kc];
+        const int64_t k = kt + 4 * h + r;  // other index of register r
+        const float e = exp2_raw(s[r] * k2);
+        const float inv = ROWS ? inv_own : sinv[buf][16 * u + 4 * h + r];
         const float delta = (k == o_lane) ? 1.f : 0.f;
-        gk[r] = (kok && o_lane < Be) ? coef * (e / den - delta) : 0.f;
+        gk[r] = (k < k_end && o_lane < Be) ? coef * (e * inv - delta) : 0.f;
       }
       // acc[own row][n] += Σ_k G[own][k]·oth_k[n]: A operand = gk (own row on the lane, k-step
-      // r covers other rows {4(l>>4) + r}), B operand = those rows' features (bv).
+      // r covers other rows {4(l>>4) + r}), B operand = those rows' features, read transposed
+      // from the stage: bv = oth[kt + 4(l>>4) + r][16t + (l&15)]
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
+      for (int r = 0; r < 4; ++r) {
+        const float* brow = s_tile + (16 * u + 4 * h + r) * St::LDR + i16;
 #pragma unroll
-        for (int t = 0; t < DQ / 4; ++t) acc[t] = mfma4(gk[r], T[u].bv[r][t], acc[t]);
+        for (int t = 0; t < DQ / 4; ++t) acc[t] = mfma4(gk[r], brow[16 * t], acc[t]);
+      }
     }
-  };
-  Tile t0[SUB], t1[SUB];
-  int64_t k0 = k_begin;
-  load(k0, t0);
-  while (k0 < k_end) {
-    load(k0 + 16 * SUB, t1);
-    __builtin_amdgcn_sched_barrier(0);
-    compute(k0, t0);
-    __builtin_amdgcn_sched_barrier(0);
-    k0 += 16 * SUB;
-    if (k0 >= k_end) break;
-    load(k0 + 16 * SUB, t0);
-    __builtin_amdgcn_sched_barrier(0);
-    compute(k0, t1);
-    __builtin_amdgcn_sched_barrier(0);
-    k0 += 16 * SUB;
+    if (more) {
+      stage_store<DQ>(sm[buf ^ 1], v);
+      if (!ROWS && threadIdx.x < kStageRows) sinv[buf ^ 1][threadIdx.x] = vinv;
+    }
+    __syncthreads();
+    buf ^= 1;
   }
+  if (o0 >= Be) return;
   // acc[t] reg r: own row o0 + 4(l>>4) + r, feature 16t + (l&15)
 #pragma unroll
   for (int t = 0; t < DQ / 4; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int64_t o = o0 + 4 * (lane >> 4) + r;
-      if (o < Be) part[(static_cast<int64_t>(blockIdx.y) * B + o) * d + 16 * t + (lane & 15)] =
+      const int64_t o = o0 + 4 * h + r;
+      if (o < Be) part[(static_cast<int64_t>(blockIdx.y) * B + o) * d + 16 * t + i16] =
           acc[t][r];
     }
 }
@@ -394,6 +457,7 @@ hgd_status infonce_forward(const float* E1, int64_t ld1, const float* E2, int64_
                 workspace_bytes, need);
   hipStream_t st = as_stream(stream);
   const float inv_temp = 1.f / temp;
+  const float k2 = exp2_scale(temp);
   const int G = group_for(d);
   const int64_t gpb = 256 / G;
   const dim3 gg(static_cast<unsigned>((batch + gpb - 1) / gpb));
@@ -414,7 +478,7 @@ hgd_status infonce_forward(const float* E1, int64_t ld1, const float* E2, int64_
   switch (d / 4) {
 #define HGD_CASE(DQ)                                                                              \
     case DQ:                                                                                      \
-      hipLaunchKernelGGL((k_nce_rowsum<DQ>), gr, dim3(256), 0, st, P1, P2, batch, inv_temp, jps, \
+      hipLaunchKernelGGL((k_nce_rowsum<DQ>), gr, dim3(256), 0, st, P1, P2, batch, k2, jps,       \
                          partial, batch_count);                                                   \
       break;
     HGD_CASE(4) HGD_CASE(8) HGD_CASE(12) HGD_CASE(16) HGD_CASE(20) HGD_CASE(24) HGD_CASE(28)
@@ -454,7 +518,7 @@ hgd_status infonce_backward(const float* P1, const float* P2, const float* inv_n
     return fail(HGD_ERR_WORKSPACE, "hgd_infonce_backward: workspace %zu < required %zu",
                 workspace_bytes, need);
   hipStream_t st = as_stream(stream);
-  const float inv_temp = 1.f / temp;
+  const float k2 = exp2_scale(temp);
   const int64_t S = slices_for(batch);
   const int64_t kps = per_slice(batch, S);
   const int64_t S_used = (batch + kps - 1) / kps;
@@ -467,11 +531,11 @@ hgd_status infonce_backward(const float* P1, const float* P2, const float* inv_n
 #define HGD_CASE(DQ)                                                                              \
     case DQ:                                                                                      \
       if (side1)                                                                                  \
-        hipLaunchKernelGGL((k_nce_bwd<DQ, true>), gr, dim3(256), 0, st, P1, P2, batch, inv_temp, \
+        hipLaunchKernelGGL((k_nce_bwd<DQ, true>), gr, dim3(256), 0, st, P1, P2, batch, k2,       \
                            deno, grad_loss, temp, kps, part1, batch_count);                        \
       if (side2)                                                                                  \
         hipLaunchKernelGGL((k_nce_bwd<DQ, false>), gr, dim3(256), 0, st, P1, P2, batch,          \
-                           inv_temp, deno, grad_loss, temp, kps, part2, batch_count);              \
+                           k2, deno, grad_loss, temp, kps, part2, batch_count);                    \
       break;
     HGD_CASE(4) HGD_CASE(8) HGD_CASE(12) HGD_CASE(16) HGD_CASE(20) HGD_CASE(24) HGD_CASE(28)
     HGD_CASE(32) HGD_CASE(36) HGD_CASE(40) HGD_CASE(44) HGD_CASE(48) HGD_CASE(52) HGD_CASE(56)

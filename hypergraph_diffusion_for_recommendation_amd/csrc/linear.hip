@@ -32,7 +32,7 @@ __device__ __forceinline__ f32x4 relu_mask(f32x4 v, f32x4 m) {
 }
 
 constexpr int kRowGemmMaxBlocks = 512;
-constexpr int kMaxSplits = 1024;
+constexpr int kSplitKResident = 512;
 
 struct RowGemm {
   const float* A;     // [rows, K]
@@ -54,7 +54,10 @@ __global__ __launch_bounds__(256) void k_row_gemm(RowGemm p) {
   constexpr int K = 16 * KQ;
   constexpr int LDB = 65;           // padded row: the k-contiguous staging writes spread banks
   constexpr int PER = K * 64 / 256;  // staged floats per thread
-  constexpr int SUB = 2;             // 16-row sub-tiles per wave iteration
+  // 16-row sub-tiles per wave iteration. One: at two (32-row super-tiles) the operand ping-pong
+  // held 64-128 VGPRs and the 69,716 × 64 forward ran 18.4 µs against 16.8 µs for the masked
+  // backward-data form with one, which moves 1.5× the bytes (profiles/r02_small_kernels)
+  constexpr int SUB = 1;
   __shared__ float sB[K * LDB];      // Bm[k][n0 + nl], zero past N
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -62,7 +65,7 @@ __global__ __launch_bounds__(256) void k_row_gemm(RowGemm p) {
   const int h = lane >> 4;
   const int n0 = blockIdx.y * 64;
   const int nt = min(4, (p.N - n0) / 16);  // live 16-column tiles of this slice (uniform)
-  const int64_t tiles = (p.rows + 16 * SUB - 1) / (16 * SUB);  // 32-row super-tiles
+  const int64_t tiles = (p.rows + 16 * SUB - 1) / (16 * SUB);  // super-tiles
   const int64_t stride = static_cast<int64_t>(gridDim.x) * 4;
   int64_t tile = static_cast<int64_t>(blockIdx.x) * 4 + wave;
   // Unconditional raw loads (the compiler then counts them exactly in its vmcnt waits): rows
@@ -213,7 +216,9 @@ __global__ __launch_bounds__(256) void k_splitk_tn(SplitK p) {
     for (int u = 0; u < 4; ++u) acc[t][u] = f32x4{0.f, 0.f, 0.f, 0.f};
   float bsum[4] = {0.f, 0.f, 0.f, 0.f};
 
-  constexpr int U = 8;  // 4-row steps per wave per batch (loads of batch b+1 overlap b's MFMAs)
+  // 4-row steps per wave per batch (loads of batch b+1 overlap b's MFMAs); 8 steps held 212-256
+  // VGPRs (one wave per SIMD), 4 steps allow two
+  constexpr int U = 4;
   // Unconditional loads from clamped rows (exact vmcnt accounting by the compiler); rows past
   // k_end and columns past M / N are zeroed when consumed.
   auto load = [&](int64_t kb, f32x4 (&a)[U], f32x4 (&b)[U], f32x4 (&m)[U]) {
@@ -302,7 +307,7 @@ bool al16(const void* p, int64_t ld) {
 
 hgd_status row_gemm(const RowGemm& p, hipStream_t st, const char* fn) {
   if (p.rows == 0) return HGD_OK;
-  const int64_t tiles = (p.rows + 31) / 32;
+  const int64_t tiles = (p.rows + 15) / 16;  // the kernel's 16-row tiles
   int64_t bx = (tiles + 3) / 4;
   if (bx > kRowGemmMaxBlocks) bx = kRowGemmMaxBlocks;
   const dim3 grid(static_cast<unsigned>(bx), static_cast<unsigned>((p.N + 63) / 64));
@@ -324,10 +329,12 @@ hgd_status row_gemm(const RowGemm& p, hipStream_t st, const char* fn) {
 }
 
 int64_t splits_for(int64_t rows) {
-  // one 128-row batch per workgroup (4 waves × 32 rows): ≈ 250 workgroups already at 32 K rows
-  // (the Yelp-shaped learned-hypergraph products), where 512-row splits left 3/4 of the CUs idle
+  // ≥ 128 rows per workgroup (two 64-row batches of 4 waves × 16 rows): ≈ 250 workgroups at 32 K
+  // rows (the Yelp-shaped learned-hypergraph products), where 512-row splits left 3/4 of the CUs
+  // idle; at most 512 workgroups (two per CU at the kernel's two waves per SIMD), so a mid-sized
+  // problem runs in one round instead of a full second round for a few leftover workgroups
   int64_t s = (rows + 127) / 128;
-  if (s > kMaxSplits) s = kMaxSplits;
+  if (s > kSplitKResident) s = kSplitKResident;
   return s < 1 ? 1 : s;
 }
 
@@ -442,7 +449,7 @@ extern "C" hgd_status hgd_linear_backward_weight(const float* dY, int64_t ldy,
                 workspace_bytes, need);
   const int64_t S = splits_for(n_rows);
   int64_t per = (n_rows + S - 1) / S;
-  per = (per + 15) / 16 * 16;
+  per = (per + 63) / 64 * 64;  // whole 64-row batches
   SplitK p{};
   p.A = dY;
   p.lda = ldy;

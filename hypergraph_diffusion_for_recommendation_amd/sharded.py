@@ -35,6 +35,21 @@ import torch.distributed as dist
 from .incidence import Incidence, spmm_csr
 
 
+def init_process_group(device: torch.device, backend: str = "nccl", **kw) -> None:
+    """One rank per GPU: ``torch.distributed`` over RCCL ("nccl" on ROCm) bound to ``device``,
+    with the communicator's kernels on a HIGH-PRIORITY stream. The exchanges run beside hop
+    kernels whose grids fill every CU; at high priority the dispatcher places RCCL's few
+    workgroups as soon as a CU slot frees instead of behind the queued hop workgroups, so the
+    all-reduce of slice s starts when its producer finishes, not when the next hop drains.
+    Other backends (gloo, for CPU / one-device rehearsals) are initialised plainly."""
+    if backend == "nccl":
+        opts = dist.ProcessGroupNCCL.Options()
+        opts.is_high_priority_stream = True
+        dist.init_process_group("nccl", device_id=device, pg_options=opts, **kw)
+    else:
+        dist.init_process_group(backend, **kw)
+
+
 def shard_bounds(n_users: int, world: int, rank: int, degrees=None):
     """Contiguous user range of ``rank``. Without ``degrees``: sizes differ by at most one. With
     the users' interaction counts: degree-balanced ranges — cut ``r`` is the first

@@ -43,7 +43,8 @@ def main():
     from hypergraph_diffusion_for_recommendation_amd import sharded_encoders as SE
     from hypergraph_diffusion_for_recommendation_amd.encoders import (HCCFEncoder,
                                                                       LocalAwareEncoder)
-    from hypergraph_diffusion_for_recommendation_amd.sharded import allreduce_replicated_grads
+    from hypergraph_diffusion_for_recommendation_amd.sharded import (allreduce_replicated_grads,
+                                                                       init_process_group)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -52,10 +53,7 @@ def main():
     torch.cuda.set_device(dev)
     backend = os.environ.get("HGD_DIST_BACKEND", "nccl")
     if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
+        init_process_group(dev, backend)
 
     U, I, d = args.users, args.items, args.dim
     u, i = R.synthetic_incidence(U, I, args.edges, seed=0)  # same graph on every rank
