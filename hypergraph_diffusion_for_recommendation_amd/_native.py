@@ -105,6 +105,10 @@ _SIGNATURES = {
     "hgd_spmm": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_i64, c_i64, c_i64,
                          c_void_p, c_i64, c_void_p, c_i64, c_i32, c_i32, c_f32,
                          ctypes.POINTER(SplitPlan), c_void_p, c_size, c_void_p]),
+    "hgd_spmm_masked": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p, c_f32, c_void_p, c_i64,
+                                c_i64, c_i64, c_i64, c_void_p, c_i64, c_void_p, c_i64, c_i32,
+                                c_i32, c_f32, ctypes.POINTER(SplitPlan), c_void_p, c_size,
+                                c_void_p]),
     "hgd_spmm_fused": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_i64, c_i64,
                                c_i64, c_void_p, c_i64, c_void_p, c_i64, c_i32,
                                ctypes.POINTER(RowEpilogue), ctypes.POINTER(SplitPlan), c_void_p,
@@ -162,6 +166,7 @@ _SIGNATURES = {
     "hgd_rowptr_from_sorted": (c_i32, [c_void_p, c_i64, c_i64, c_void_p, c_void_p]),
     "hgd_check_sorted": (c_i32, [c_void_p, c_i64, c_i64, c_void_p, c_void_p]),
     "hgd_expand_rows": (c_i32, [c_void_p, c_i64, c_i64, c_void_p, c_void_p]),
+    "hgd_gather_u8": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p, c_void_p]),
     "hgd_gather32": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p, c_void_p]),
     "hgd_degree_scale": (c_i32, [c_void_p, c_void_p, c_i64, c_f64, c_void_p, c_void_p]),
     "hgd_edge_values": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_void_p,
@@ -202,6 +207,10 @@ _SIGNATURES = {
     "hgd_unique_i64": (c_i32, [c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_size, c_void_p]),
     "hgd_unique_trunc_f32": (c_i32, [c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_size,
                                      c_void_p]),
+    "hgd_unique_dev_i64": (c_i32, [c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_size,
+                                   c_void_p]),
+    "hgd_unique_dev_trunc_f32": (c_i32, [c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_size,
+                                         c_void_p]),
     "hgd_unique_sort_i64": (c_i32, [c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_size,
                                     c_void_p]),
     "hgd_unique_sort_trunc_f32": (c_i32, [c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_size,

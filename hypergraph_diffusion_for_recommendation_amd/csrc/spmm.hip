@@ -45,6 +45,11 @@ struct SpmmArgs {
   float* partial;  // [n_chunks, d]
   int64_t heavy_blocks;
   hgd_row_epilogue ex;  // used by the EX (hgd_spmm_fused) instantiations only
+  // masked hop (hgd_spmm_masked, the MASK instantiations): the edge-dropped matrix of
+  // SpAdjDropEdge as a view of its parent — edge e counts iff mask[e] != 0, with weight
+  // val[e] / keep (IEEE, as the dropped COO's values)
+  const uint8_t* mask;
+  float keep;
 };
 
 __device__ __forceinline__ float epilogue(float y, int epi, float slope) {
@@ -114,13 +119,16 @@ __device__ __forceinline__ void finish_row(const SpmmArgs& a, int64_t r, float s
   if (col_ok) store_vec<VEC, NT_STORE>(a.Y + r * a.ldy + coff, acc);
 }
 
-// Lane l's share of a batch of G column indices (and weights) starting at nonzero eb.
-template <bool HAS_VAL, int POL>
+// Lane l's share of a batch of G column indices (and weights) starting at nonzero eb; with MASK
+// also its keep flag (0 past the batch).
+template <bool HAS_VAL, int POL, bool MASK = false>
 __device__ __forceinline__ void load_index(const SpmmArgs& a, int64_t eb, int n, int l, int& c,
-                                           float& w) {
+                                           float& w, int& keep) {
   c = 0;
   w = 1.f;
+  keep = 0;
   if (l < n) {
+    if constexpr (MASK) keep = a.mask[eb + l];
     if constexpr (POL & kPolNtIndex) {
       c = __builtin_nontemporal_load(a.col + eb + l);
       if constexpr (HAS_VAL) w = __builtin_nontemporal_load(a.val + eb + l);
@@ -131,37 +139,71 @@ __device__ __forceinline__ void load_index(const SpmmArgs& a, int64_t eb, int n,
   }
 }
 
+// Position of the j-th set bit (0-based) of a G-bit group mask: a popcount binary search.
+template <int G>
+__device__ __forceinline__ int nth_set_bit(unsigned long long m, int j) {
+  int pos = 0;
+#pragma unroll
+  for (int w = G / 2; w >= 1; w >>= 1) {
+    const int c = __popcll(m & ((1ull << w) - 1ull));
+    if (j >= c) {
+      j -= c;
+      m >>= w;
+      pos += w;
+    }
+  }
+  return pos;
+}
+
+// MASK: packs the kept entries of a fetched batch to the front of the group (in edge order) with
+// their weights val/keep; returns how many there are. Every lane of the group calls it.
+template <int G, bool HAS_VAL>
+__device__ __forceinline__ int compact_kept(const SpmmArgs& a, int l, int keep, int& c, float& w) {
+  const unsigned long long bal = __ballot(keep != 0);
+  const int base = (static_cast<int>(threadIdx.x) & 63) & ~(G - 1);
+  const unsigned long long gm =
+      G == 64 ? bal : (bal >> base) & ((1ull << (G == 64 ? 0 : G)) - 1ull);
+  const int src = nth_set_bit<G>(gm, l);
+  if constexpr (HAS_VAL) w = __fdiv_rn(w, a.keep);  // vals[mask] / keepRate (HCCF.py:224)
+  c = __shfl(c, src, G);
+  if constexpr (HAS_VAL) w = __shfl(w, src, G);
+  return __popcll(gm);
+}
+
 // Σ_{e in [e0,e1)} val[e] * X[col[e], cols of this lane], in edge order. With kPolPrefetch the
 // index batch b+1 is loaded before the gathers of batch b are issued, so the dependent
 // index → gather round trip is paid once per row instead of once per batch of G nonzeros.
-template <int G, int VEC, int U, bool HAS_VAL, int POL>
+// With MASK only the kept edges are summed (same order as over the compacted matrix).
+template <int G, int VEC, int U, bool HAS_VAL, int POL, bool MASK = false>
 __device__ __forceinline__ void gather_sum(const SpmmArgs& a, int64_t e0, int64_t e1, int l,
                                            bool col_ok, float (&acc)[VEC]) {
 #pragma unroll
   for (int i = 0; i < VEC; ++i) acc[i] = 0.f;
   const int64_t coff = static_cast<int64_t>(a.col0) + static_cast<int64_t>(l) * VEC;
   constexpr bool PF = (POL & kPolPrefetch) != 0;
-  int nxc = 0;
+  int nxc = 0, nxk = 0;
   float nxw = 1.f;
   if constexpr (PF) {
     if (e0 < e1)
-      load_index<HAS_VAL, POL>(a, e0, static_cast<int>(min(static_cast<int64_t>(G), e1 - e0)), l,
-                               nxc, nxw);
+      load_index<HAS_VAL, POL, MASK>(
+          a, e0, static_cast<int>(min(static_cast<int64_t>(G), e1 - e0)), l, nxc, nxw, nxk);
   }
   for (int64_t eb = e0; eb < e1; eb += G) {
-    const int n = static_cast<int>(min(static_cast<int64_t>(G), e1 - eb));
-    int myc;
+    int n = static_cast<int>(min(static_cast<int64_t>(G), e1 - eb));
+    int myc, myk;
     float myw;
     if constexpr (PF) {
       myc = nxc;
       myw = nxw;
+      myk = nxk;
       const int64_t en = eb + G;
       if (en < e1)
-        load_index<HAS_VAL, POL>(a, en, static_cast<int>(min(static_cast<int64_t>(G), e1 - en)),
-                                 l, nxc, nxw);
+        load_index<HAS_VAL, POL, MASK>(
+            a, en, static_cast<int>(min(static_cast<int64_t>(G), e1 - en)), l, nxc, nxw, nxk);
     } else {
-      load_index<HAS_VAL, POL>(a, eb, n, l, myc, myw);
+      load_index<HAS_VAL, POL, MASK>(a, eb, n, l, myc, myw, myk);
     }
+    if constexpr (MASK) n = compact_kept<G, HAS_VAL>(a, l, myk, myc, myw);
     for (int k = 0; k < n; k += U) {
       float xv[U][VEC];
       float w[U];
@@ -194,7 +236,7 @@ __device__ __forceinline__ void gather_sum(const SpmmArgs& a, int64_t e0, int64_
   }
 }
 
-template <int G, int VEC, int U, bool HAS_VAL, int POL, bool EX>
+template <int G, int VEC, int U, bool HAS_VAL, int POL, bool EX, bool MASK = false>
 __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
   constexpr int GPB = kBlock / G;
   const int g = threadIdx.x / G;
@@ -213,7 +255,7 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
     const int64_t re = a.rowptr[r + 1];
     const int64_t e0 = a.rowptr[r] + k * a.chunk;
     const int64_t e1 = min(e0 + static_cast<int64_t>(a.chunk), re);
-    gather_sum<G, VEC, U, HAS_VAL, POL>(a, e0, e1, l, col_ok, acc);
+    gather_sum<G, VEC, U, HAS_VAL, POL, MASK>(a, e0, e1, l, col_ok, acc);
     if (col_ok) store_vec<VEC>(a.partial + t * a.d + coff, acc);
     return;
   }
@@ -224,7 +266,7 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
   const int64_t e0 = a.rowptr[r];
   const int64_t e1 = a.rowptr[r + 1];
   if (a.heavy_threshold > 0 && e1 - e0 > a.heavy_threshold) return;  // split-plan row
-  gather_sum<G, VEC, U, HAS_VAL, POL>(a, e0, e1, l, col_ok, acc);
+  gather_sum<G, VEC, U, HAS_VAL, POL, MASK>(a, e0, e1, l, col_ok, acc);
   const float s = a.row_scale ? a.row_scale[r] : 1.f;
   finish_row<G, VEC, EX, (POL & kPolNtStore) != 0>(a, r, s, l, coff, col_ok, acc);
 }
@@ -273,13 +315,13 @@ __global__ __launch_bounds__(kBlock) void spmm_seg_kernel(SpmmArgs a) {
   };
 
   constexpr bool PF = (POL & kPolPrefetch) != 0;
-  int nxc = 0;
+  int nxc = 0, unused_keep = 0;
   float nxw = 1.f;
   if constexpr (PF) {
     if (e_begin < e_end)
       load_index<HAS_VAL, POL>(
           a, e_begin, static_cast<int>(min(static_cast<int64_t>(G), e_end - e_begin)), l, nxc,
-          nxw);
+          nxw, unused_keep);
   }
   for (int64_t eb = e_begin; eb < e_end; eb += G) {
     const int n = static_cast<int>(min(static_cast<int64_t>(G), e_end - eb));
@@ -291,9 +333,10 @@ __global__ __launch_bounds__(kBlock) void spmm_seg_kernel(SpmmArgs a) {
       const int64_t en = eb + G;
       if (en < e_end)
         load_index<HAS_VAL, POL>(
-            a, en, static_cast<int>(min(static_cast<int64_t>(G), e_end - en)), l, nxc, nxw);
+            a, en, static_cast<int>(min(static_cast<int64_t>(G), e_end - en)), l, nxc, nxw,
+            unused_keep);
     } else {
-      load_index<HAS_VAL, POL>(a, eb, n, l, myc, myw);
+      load_index<HAS_VAL, POL>(a, eb, n, l, myc, myw, unused_keep);
     }
     for (int k = 0; k < n; k += U) {
       float xv[U][VEC];
@@ -394,6 +437,17 @@ int g_pass_cols = 0;
 
 template <int G, int VEC, int U, int POL, bool EX = false>
 void launch_kernel(const SpmmArgs& a, bool has_val, bool seg, int64_t blocks, hipStream_t st) {
+  if constexpr (!EX && POL == kDefaultPolicy && U == 8) {
+    if (a.mask) {  // masked (edge-dropped view) hop: the row kernel only
+      if (has_val)
+        hipLaunchKernelGGL((spmm_kernel<G, VEC, U, true, POL, false, true>), dim3(blocks),
+                           dim3(kBlock), 0, st, a);
+      else
+        hipLaunchKernelGGL((spmm_kernel<G, VEC, U, false, POL, false, true>), dim3(blocks),
+                           dim3(kBlock), 0, st, a);
+      return;
+    }
+  }
   if constexpr (G >= 8) {
     if (seg) {
       if (has_val)
@@ -415,7 +469,9 @@ void launch_kernel(const SpmmArgs& a, bool has_val, bool seg, int64_t blocks, hi
 
 template <int G, int VEC, bool EX>
 void launch_tuned(const SpmmArgs& a, bool has_val, bool seg, int64_t blocks, hipStream_t st) {
-  if constexpr (EX) {
+  if (!EX && a.mask) {
+    launch_kernel<G, VEC, 8, kDefaultPolicy>(a, has_val, false, blocks, st);
+  } else if constexpr (EX) {
     launch_kernel<G, VEC, 8, kDefaultPolicy, true>(a, has_val, seg, blocks, st);
   } else if constexpr (G == 16 && VEC == 4) {
     // the d = 64 path carries the tuning matrix (unroll × {plain, nt-store, prefetch, both})
@@ -494,8 +550,8 @@ hgd_status spmm_impl(const int64_t* rowptr, const int32_t* col, const float* val
                      const float* row_scale, int64_t n_rows, int64_t n_src_rows, int64_t row_begin,
                      int64_t row_end, const float* X, int64_t ldx, float* Y, int64_t ldy,
                      int32_t d, int32_t epilogue, float slope, const hgd_row_epilogue* ex,
-                     const hgd_split_plan* plan, void* workspace, size_t workspace_bytes,
-                     void* stream, const char* fn) {
+                     const uint8_t* mask, float keep, const hgd_split_plan* plan,
+                     void* workspace, size_t workspace_bytes, void* stream, const char* fn) {
   HGD_REQUIRE(d > 0, "%s: d must be > 0 (got %d)", fn, d);
   HGD_REQUIRE(n_rows >= 0 && n_src_rows >= 0, "%s: negative sizes", fn);
   HGD_REQUIRE(row_begin >= 0 && row_begin <= row_end && row_end <= n_rows,
@@ -532,6 +588,8 @@ hgd_status spmm_impl(const int64_t* rowptr, const int32_t* col, const float* val
   a.epi = epilogue;
   a.slope = slope;
   if (ex) a.ex = *ex;
+  a.mask = mask;
+  a.keep = keep;
   if (plan && plan->threshold > 0 && plan->n_heavy > 0) {
     HGD_REQUIRE(plan->chunk > 0 && plan->heavy_rows && plan->heavy_cptr && plan->chunk_heavy,
                 "%s: incomplete split plan", fn);
@@ -547,7 +605,7 @@ hgd_status spmm_impl(const int64_t* rowptr, const int32_t* col, const float* val
     a.heavy_rows = plan->heavy_rows;
     a.heavy_cptr = plan->heavy_cptr;
     a.partial = static_cast<float*>(workspace);
-  } else if (plan && (plan->flags & HGD_PLAN_SEGMENTED)) {
+  } else if (plan && (plan->flags & HGD_PLAN_SEGMENTED) && !mask) {
     a.seg = 1;  // only without split rows: the segmented walk covers every nonzero of its rows
   }
 
@@ -600,7 +658,7 @@ extern "C" hgd_status hgd_spmm(const int64_t* rowptr, const int32_t* col, const 
                                size_t workspace_bytes, void* stream) {
   hgd::clear_error();
   return hgd::spmm_impl(rowptr, col, val, row_scale, n_rows, n_src_rows, row_begin, row_end, X,
-                        ldx, Y, ldy, d, epilogue, slope, nullptr, plan, workspace,
+                        ldx, Y, ldy, d, epilogue, slope, nullptr, nullptr, 1.f, plan, workspace,
                         workspace_bytes, stream, "hgd_spmm");
 }
 
@@ -613,8 +671,23 @@ extern "C" hgd_status hgd_spmm_fused(const int64_t* rowptr, const int32_t* col, 
   hgd::clear_error();
   HGD_REQUIRE(epi != nullptr, "hgd_spmm_fused: null epilogue descriptor");
   return hgd::spmm_impl(rowptr, col, val, row_scale, n_rows, n_src_rows, row_begin, row_end, X,
-                        ldx, Y, ldy, d, epi->act, epi->slope, epi, plan, workspace,
+                        ldx, Y, ldy, d, epi->act, epi->slope, epi, nullptr, 1.f, plan, workspace,
                         workspace_bytes, stream, "hgd_spmm_fused");
+}
+
+extern "C" hgd_status hgd_spmm_masked(const int64_t* rowptr, const int32_t* col, const float* val,
+                                      const uint8_t* mask, float keep, const float* row_scale,
+                                      int64_t n_rows, int64_t n_src_rows, int64_t row_begin,
+                                      int64_t row_end, const float* X, int64_t ldx, float* Y,
+                                      int64_t ldy, int32_t d, int32_t epilogue, float slope,
+                                      const hgd_split_plan* plan, void* workspace,
+                                      size_t workspace_bytes, void* stream) {
+  hgd::clear_error();
+  HGD_REQUIRE(keep > 0.f, "hgd_spmm_masked: keep must be > 0 (got %g)", (double)keep);
+  HGD_REQUIRE(mask || row_end == row_begin, "hgd_spmm_masked: null mask");
+  return hgd::spmm_impl(rowptr, col, val, row_scale, n_rows, n_src_rows, row_begin, row_end, X,
+                        ldx, Y, ldy, d, epilogue, slope, nullptr, mask, keep, plan, workspace,
+                        workspace_bytes, stream, "hgd_spmm_masked");
 }
 
 extern "C" hgd_status hgd_set_tuning(int32_t key, int32_t value) {

@@ -163,6 +163,23 @@ __global__ void k_gather32(const uint32_t* __restrict__ src, const int32_t* __re
   if (i < n) out[i] = src[perm[i]];
 }
 
+// out[i] = src[perm[i]] for bytes (a keep-mask into the other orientation's edge order): four
+// outputs per thread, so the permutation is read as one 16-byte load and the output written as
+// one 4-byte store.
+__global__ void k_gather_u8(const uint8_t* __restrict__ src, const int32_t* __restrict__ perm,
+                            int64_t n, uint8_t* __restrict__ out) {
+  const int64_t i = 4 * (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x);
+  if (i + 4 <= n) {
+    const int4 p = *reinterpret_cast<const int4*>(perm + i);
+    const uint32_t v = static_cast<uint32_t>(src[p.x]) | (static_cast<uint32_t>(src[p.y]) << 8) |
+                       (static_cast<uint32_t>(src[p.z]) << 16) |
+                       (static_cast<uint32_t>(src[p.w]) << 24);
+    *reinterpret_cast<uint32_t*>(out + i) = v;
+  } else {
+    for (int64_t j = i; j < n; ++j) out[j] = src[perm[j]];
+  }
+}
+
 __global__ void k_degree_scale(const int64_t* __restrict__ rowptr, const float* __restrict__ val,
                                int64_t n_rows, double power, float* __restrict__ out) {
   const int64_t r = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
@@ -636,6 +653,20 @@ extern "C" hgd_status hgd_gather32(const void* src, const int32_t* perm, int64_t
   hipLaunchKernelGGL(k_gather32, dim3(grid_for(n)), dim3(kBlock), 0, as_stream(stream),
                      static_cast<const uint32_t*>(src), perm, n, static_cast<uint32_t*>(out));
   return check_launch("hgd_gather32");
+}
+
+extern "C" hgd_status hgd_gather_u8(const uint8_t* src, const int32_t* perm, int64_t n,
+                                    uint8_t* out, void* stream) {
+  clear_error();
+  HGD_REQUIRE(n >= 0, "hgd_gather_u8: n < 0");
+  if (n == 0) return HGD_OK;
+  HGD_REQUIRE(src && perm && out, "hgd_gather_u8: null pointer");
+  HGD_REQUIRE(reinterpret_cast<uintptr_t>(perm) % 16 == 0 && reinterpret_cast<uintptr_t>(out) % 4 == 0,
+              "hgd_gather_u8: perm must be 16-byte and out 4-byte aligned");
+  const int64_t threads = (n + 3) / 4;
+  hipLaunchKernelGGL(k_gather_u8, dim3(grid_for(threads)), dim3(kBlock), 0, as_stream(stream),
+                     src, perm, n, out);
+  return check_launch("hgd_gather_u8");
 }
 
 extern "C" hgd_status hgd_degree_scale(const int64_t* rowptr, const float* val, int64_t n_rows,

@@ -34,6 +34,7 @@ struct State {
   long long lo, hi;  // min / max key
   int overflow;
   int pad;
+  unsigned long long far_n;  // device-complete path: keys beyond the bitmap window
 };
 
 struct I64Src {
@@ -71,6 +72,7 @@ __global__ void k_uq_init(State* st) {
   st->lo = LLONG_MAX;
   st->hi = LLONG_MIN;
   st->overflow = 0;
+  st->far_n = 0;
 }
 
 template <class Src>
@@ -105,6 +107,9 @@ __global__ __launch_bounds__(256) void k_uq_minmax(Src src, int64_t n, State* st
   }
 }
 
+// Bitmap words of the key range. CLAMP (the device-complete path): a range beyond the bitmap
+// keeps the window [lo, lo + kCapBits) and the keys past it go to the far-key list instead.
+template <bool CLAMP = false>
 __device__ __forceinline__ bool range_words(const State* st, int64_t* words) {
   const long long lo = st->lo, hi = st->hi;
   if (lo > hi) {  // no keys
@@ -112,16 +117,20 @@ __device__ __forceinline__ bool range_words(const State* st, int64_t* words) {
     return true;
   }
   // hi - lo may overflow int64: compare in unsigned
-  const unsigned long long span = static_cast<unsigned long long>(hi) -
-                                  static_cast<unsigned long long>(lo);
-  if (span >= static_cast<unsigned long long>(kCapBits)) return false;
+  unsigned long long span = static_cast<unsigned long long>(hi) -
+                            static_cast<unsigned long long>(lo);
+  if (span >= static_cast<unsigned long long>(kCapBits)) {
+    if (!CLAMP) return false;
+    span = static_cast<unsigned long long>(kCapBits) - 1;
+  }
   *words = static_cast<int64_t>((span + 1 + 31) / 32);
   return true;
 }
 
+template <bool CLAMP>
 __global__ __launch_bounds__(256) void k_uq_zero(uint32_t* bitmap, State* st) {
   int64_t words;
-  if (!range_words(st, &words)) {
+  if (!range_words<CLAMP>(st, &words)) {
     if (blockIdx.x == 0 && threadIdx.x == 0) st->overflow = 1;
     return;
   }
@@ -131,29 +140,43 @@ __global__ __launch_bounds__(256) void k_uq_zero(uint32_t* bitmap, State* st) {
     bitmap[w] = 0u;
 }
 
-template <class Src>
+// Sets every key's bit. FAR (device-complete path): keys past the kCapBits window are appended
+// to `far` (State::far_n counts them) instead.
+template <class Src, bool FAR = false>
 __global__ __launch_bounds__(256) void k_uq_mark(Src src, int64_t n, uint32_t* bitmap,
-                                                 const State* st) {
+                                                 State* st, int64_t* far = nullptr) {
   __shared__ uint32_t s_bits[kLdsWords];
   int64_t words;
-  if (!range_words(st, &words) || words == 0) return;  // uniform over the grid
+  if (!range_words<FAR>(st, &words) || words == 0) return;  // uniform over the grid
   const long long lo = st->lo;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   const int64_t i0 = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  auto far_key = [&](uint64_t b, int64_t key) {
+    if constexpr (FAR) {
+      if (b >= static_cast<uint64_t>(kCapBits)) {
+        const unsigned long long p = atomicAdd(&st->far_n, 1ull);
+        far[p] = key;
+        return true;
+      }
+    }
+    return false;
+  };
   if (words <= kLdsWords) {
     for (int w = threadIdx.x; w < words; w += blockDim.x) s_bits[w] = 0u;
     __syncthreads();
     for (int64_t i = i0; i < n; i += stride) {
-      const uint64_t b = static_cast<uint64_t>(src(i)) - static_cast<uint64_t>(lo);
-      atomicOr(&s_bits[b >> 5], 1u << (b & 31));
+      const int64_t key = src(i);
+      const uint64_t b = static_cast<uint64_t>(key) - static_cast<uint64_t>(lo);
+      if (!far_key(b, key)) atomicOr(&s_bits[b >> 5], 1u << (b & 31));
     }
     __syncthreads();
     for (int w = threadIdx.x; w < words; w += blockDim.x)
       if (s_bits[w]) atomicOr(&bitmap[w], s_bits[w]);
   } else {
     for (int64_t i = i0; i < n; i += stride) {
-      const uint64_t b = static_cast<uint64_t>(src(i)) - static_cast<uint64_t>(lo);
-      atomicOr(&bitmap[b >> 5], 1u << (b & 31));
+      const int64_t key = src(i);
+      const uint64_t b = static_cast<uint64_t>(key) - static_cast<uint64_t>(lo);
+      if (!far_key(b, key)) atomicOr(&bitmap[b >> 5], 1u << (b & 31));
     }
   }
 }
@@ -178,10 +201,11 @@ __device__ __forceinline__ int block_exclusive_scan(int v, int* total) {
   return base + incl - v;
 }
 
+template <bool CLAMP>
 __global__ __launch_bounds__(kEmitThreads) void k_uq_count(const uint32_t* bitmap,
                                                            const State* st, int* tile_cnt) {
   int64_t words;
-  if (!range_words(st, &words)) return;
+  if (!range_words<CLAMP>(st, &words)) return;
   const int64_t tiles = (words + kTileWords - 1) / kTileWords;
   if (blockIdx.x >= tiles) return;
   const int64_t w0 = blockIdx.x * kTileWords + threadIdx.x * kWordsPerThread;
@@ -194,11 +218,12 @@ __global__ __launch_bounds__(kEmitThreads) void k_uq_count(const uint32_t* bitma
   if (threadIdx.x == 0) tile_cnt[blockIdx.x] = total;
 }
 
+template <bool CLAMP>
 __global__ __launch_bounds__(kMaxTiles) void k_uq_scan(const int* tile_cnt, const State* st,
                                                        int64_t* tile_off, int64_t* n_out) {
   __shared__ int64_t s[kMaxTiles];
   int64_t words;
-  if (!range_words(st, &words)) {
+  if (!range_words<CLAMP>(st, &words)) {
     if (threadIdx.x == 0) *n_out = -1;  // the caller runs hgd_unique_sort
     return;
   }
@@ -216,10 +241,11 @@ __global__ __launch_bounds__(kMaxTiles) void k_uq_scan(const int* tile_cnt, cons
   if (threadIdx.x == kMaxTiles - 1) *n_out = s[threadIdx.x];
 }
 
+template <bool CLAMP>
 __global__ __launch_bounds__(kEmitThreads) void k_uq_emit(const uint32_t* bitmap, const State* st,
                                                           const int64_t* tile_off, int64_t* out) {
   int64_t words;
-  if (!range_words(st, &words)) return;
+  if (!range_words<CLAMP>(st, &words)) return;
   const int64_t tiles = (words + kTileWords - 1) / kTileWords;
   if (blockIdx.x >= tiles) return;
   const long long lo = st->lo;
@@ -243,6 +269,97 @@ __global__ __launch_bounds__(kEmitThreads) void k_uq_emit(const uint32_t* bitmap
                                         static_cast<unsigned long long>((w0 + j) * 32 + k));
     }
   }
+}
+
+// The far keys (device-complete path), one workgroup: nothing to do in the common case (every
+// key inside the bitmap window: one load and exit). Otherwise they are sorted — in LDS when they
+// fit kFarLds, else by an in-place bitonic network over the workspace (P = next power of two;
+// slow but bounded: a degenerate input such as a NaN embedding, whose INT64_MIN key drags the
+// window away from the others) — and their distinct values appended after the bitmap's, which
+// are all smaller: the output stays torch.unique's sorted order.
+constexpr int kFarThreads = 1024;
+constexpr int kFarLds = 4096;
+
+__device__ __forceinline__ void cas(int64_t& a, int64_t& b, bool up) {
+  if ((a > b) == up) {
+    const int64_t t = a;
+    a = b;
+    b = t;
+  }
+}
+
+// Bitonic sort of keys[0, P) (P a power of two) by one workgroup; KEYS is the LDS array or the
+// workspace buffer, indexed directly (no pointer that may be either).
+template <class Keys>
+__device__ __forceinline__ void block_bitonic(Keys& keys, int P) {
+  const int t = threadIdx.x;
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = t; i < P / 2; i += kFarThreads) {
+        const int lo_i = 2 * i - (i & (stride - 1));
+        const bool up = (lo_i & size) == 0;
+        int64_t x = keys[lo_i], y = keys[lo_i + stride];
+        cas(x, y, up);
+        keys[lo_i] = x;
+        keys[lo_i + stride] = y;
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__global__ __launch_bounds__(kFarThreads) void k_uq_far(State* st, int64_t* far, int64_t cap,
+                                                        int64_t* out, int64_t* n_out,
+                                                        int64_t n) {
+  __shared__ int64_t s_keys[kFarLds];
+  __shared__ int s_wave[kFarThreads / 64];
+  int64_t kk = static_cast<int64_t>(st->far_n);
+  if (kk == 0) return;  // uniform
+  kk = kk < cap ? kk : cap;  // defensive: never past the far buffer
+  const int k = static_cast<int>(kk);
+  const int t = threadIdx.x;
+  int P = 1;
+  while (P < k) P <<= 1;
+  const bool lds = P <= kFarLds;
+  if (lds) {
+    for (int i = t; i < P; i += kFarThreads) s_keys[i] = i < k ? far[i] : LLONG_MAX;
+    __syncthreads();
+    block_bitonic(s_keys, P);
+  } else {
+    for (int i = k + t; i < P; i += kFarThreads) far[i] = LLONG_MAX;
+    __syncthreads();
+    block_bitonic(far, P);
+  }
+  // distinct values of the sorted first k, in chunks of kFarThreads with a running offset
+  int64_t base = *n_out;
+  for (int c0 = 0; c0 < k; c0 += kFarThreads) {
+    const int i = c0 + t;
+    int f = 0;
+    int64_t v = 0;
+    if (i < k) {
+      v = lds ? s_keys[i] : far[i];
+      const int64_t prev = i == 0 ? 0 : (lds ? s_keys[i - 1] : far[i - 1]);
+      f = (i == 0 || v != prev) ? 1 : 0;
+    }
+    const int lane = t & 63, wave = t >> 6;
+    int incl = f;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(incl, o);
+      if (lane >= o) incl += u;
+    }
+    if (lane == 63) s_wave[wave] = incl;
+    __syncthreads();
+    int pre = 0, tot = 0;
+    for (int w = 0; w < kFarThreads / 64; ++w) {
+      pre += w < wave ? s_wave[w] : 0;
+      tot += s_wave[w];
+    }
+    const int64_t pos = base + pre + incl - f;
+    if (f && pos >= 0 && pos < n) out[pos] = v;  // bounds: defensive, never false for valid state
+    base += tot;
+    __syncthreads();
+  }
+  if (t == 0) *n_out = base;
 }
 
 template <class Src>
@@ -271,14 +388,29 @@ size_t sort_path_bytes(int64_t n) {
   return 2 * align_up(static_cast<size_t>(n) * 8) + align_up(a > b ? a : b);
 }
 
-template <class Src>
+int64_t far_capacity(int64_t n) {
+  int64_t p = 1;
+  while (p < n) p <<= 1;
+  return p;
+}
+
+size_t dev_path_bytes(int64_t n) {
+  return kBitmapPathBytes + align_up(static_cast<size_t>(far_capacity(n)) * 8);
+}
+
+// DEV (device-complete): the window clamps instead of failing and the far keys are merged by
+// k_uq_far, so *n_out is always the unique count — no host decision, capturable in a graph.
+template <class Src, bool DEV = false>
 hgd_status unique_bitmap(Src src, int64_t n, int64_t* out, int64_t* n_out, void* ws, size_t wsb,
                          hipStream_t st, const char* fn) {
   HGD_REQUIRE(n >= 0 && n < (int64_t(1) << 31), "%s: n must be in [0, 2^31)", fn);
   HGD_REQUIRE(n_out && (n == 0 || out), "%s: null output", fn);
-  if (wsb < kBitmapPathBytes || !ws)
-    return fail(HGD_ERR_WORKSPACE, "%s: workspace %zu < required %zu", fn, wsb, kBitmapPathBytes);
+  const size_t need = DEV ? dev_path_bytes(n) : kBitmapPathBytes;
+  if (wsb < need || !ws)
+    return fail(HGD_ERR_WORKSPACE, "%s: workspace %zu < required %zu", fn, wsb, need);
   char* w = static_cast<char*>(ws);
+  int64_t* far = DEV ? reinterpret_cast<int64_t*>(w + kBitmapPathBytes) : nullptr;
+  const int64_t far_cap = DEV ? far_capacity(n) : 0;
   State* s = reinterpret_cast<State*>(w + kOffState);
   int* cnt = reinterpret_cast<int*>(w + kOffCnt);
   int64_t* toff = reinterpret_cast<int64_t*>(w + kOffTileOff);
@@ -288,14 +420,17 @@ hgd_status unique_bitmap(Src src, int64_t n, int64_t* out, int64_t* n_out, void*
     const unsigned g = static_cast<unsigned>(std::min<int64_t>(kGrid, (n + 4095) / 4096));
     hipLaunchKernelGGL(k_uq_minmax<Src>, dim3(g), dim3(256), 0, st, src, n, s);
   }
-  hipLaunchKernelGGL(k_uq_zero, dim3(kGrid), dim3(256), 0, st, bitmap, s);
+  hipLaunchKernelGGL(k_uq_zero<DEV>, dim3(kGrid), dim3(256), 0, st, bitmap, s);
   if (n > 0) {
     const unsigned g = static_cast<unsigned>(std::min<int64_t>(kGrid, (n + 255) / 256));
-    hipLaunchKernelGGL(k_uq_mark<Src>, dim3(g), dim3(256), 0, st, src, n, bitmap, s);
+    hipLaunchKernelGGL((k_uq_mark<Src, DEV>), dim3(g), dim3(256), 0, st, src, n, bitmap, s, far);
   }
-  hipLaunchKernelGGL(k_uq_count, dim3(kMaxTiles), dim3(kEmitThreads), 0, st, bitmap, s, cnt);
-  hipLaunchKernelGGL(k_uq_scan, dim3(1), dim3(kMaxTiles), 0, st, cnt, s, toff, n_out);
-  hipLaunchKernelGGL(k_uq_emit, dim3(kMaxTiles), dim3(kEmitThreads), 0, st, bitmap, s, toff, out);
+  hipLaunchKernelGGL(k_uq_count<DEV>, dim3(kMaxTiles), dim3(kEmitThreads), 0, st, bitmap, s, cnt);
+  hipLaunchKernelGGL(k_uq_scan<DEV>, dim3(1), dim3(kMaxTiles), 0, st, cnt, s, toff, n_out);
+  hipLaunchKernelGGL(k_uq_emit<DEV>, dim3(kMaxTiles), dim3(kEmitThreads), 0, st, bitmap, s, toff,
+                     out);
+  if (DEV) hipLaunchKernelGGL(k_uq_far, dim3(1), dim3(kFarThreads), 0, st, s, far, far_cap, out,
+                              n_out, n);
   return check_launch(fn);
 }
 
@@ -337,7 +472,8 @@ using namespace hgd;
 
 extern "C" size_t hgd_unique_workspace_size(int64_t n) {
   const size_t s = n > 0 ? sort_path_bytes(n) : 0;
-  return s > kBitmapPathBytes ? s : kBitmapPathBytes;
+  const size_t d = dev_path_bytes(n > 0 ? n : 1);
+  return std::max(s, d);
 }
 
 extern "C" hgd_status hgd_unique_i64(const int64_t* keys, int64_t n, int64_t* out,
@@ -370,4 +506,21 @@ extern "C" hgd_status hgd_unique_sort_trunc_f32(const float* x, int64_t n, int64
   HGD_REQUIRE(n == 0 || x, "hgd_unique_sort_trunc_f32: null x");
   return unique_sort(TruncSrc{x}, nullptr, n, out, n_out, ws, wsb, as_stream(stream),
                      "hgd_unique_sort_trunc_f32");
+}
+
+extern "C" hgd_status hgd_unique_dev_i64(const int64_t* keys, int64_t n, int64_t* out,
+                                         int64_t* n_out, void* ws, size_t wsb, void* stream) {
+  clear_error();
+  HGD_REQUIRE(n == 0 || keys, "hgd_unique_dev_i64: null keys");
+  return unique_bitmap<I64Src, true>(I64Src{keys}, n, out, n_out, ws, wsb, as_stream(stream),
+                                     "hgd_unique_dev_i64");
+}
+
+extern "C" hgd_status hgd_unique_dev_trunc_f32(const float* x, int64_t n, int64_t* out,
+                                               int64_t* n_out, void* ws, size_t wsb,
+                                               void* stream) {
+  clear_error();
+  HGD_REQUIRE(n == 0 || x, "hgd_unique_dev_trunc_f32: null x");
+  return unique_bitmap<TruncSrc, true>(TruncSrc{x}, n, out, n_out, ws, wsb, as_stream(stream),
+                                       "hgd_unique_dev_trunc_f32");
 }

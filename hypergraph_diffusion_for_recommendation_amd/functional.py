@@ -580,8 +580,8 @@ def unique_long_n(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     """:func:`unique_long` without the device→host read, for a captured training step:
     ``(nodes, count)`` with ``nodes`` int64 capacity-sized (x.numel()), its first ``count[0]``
     entries the sorted unique values of ``x.long()`` and the rest 0, ``count`` an int64 [1]
-    device tensor (hgd_unique_sort_*: the range-independent path). Feed both to
-    :func:`contrast_loss`."""
+    device tensor (hgd_unique_dev_*: the range bitmap with the far keys merged on the device, so
+    no host decision). Feed both to :func:`contrast_loss`."""
     if not x.is_cuda or x.dtype not in (torch.float32, torch.int64):
         raise ValueError("unique_long_n: needs a float32 or int64 device tensor")
     x = x.detach().contiguous().view(-1)
@@ -594,9 +594,9 @@ def unique_long_n(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     wsb = lib.hgd_unique_workspace_size(n)
     buf = torch.empty(_UQ_HEAD + max(wsb, 1), dtype=torch.uint8, device=dev)
     base = buf.data_ptr()
-    slow = lib.hgd_unique_sort_trunc_f32 if x.dtype == torch.float32 else lib.hgd_unique_sort_i64
-    nat.check(slow(x.data_ptr(), n, out.data_ptr(), base, base + _UQ_HEAD, wsb,
-                   torch.cuda.current_stream(dev).cuda_stream), "hgd_unique_sort")
+    fn = lib.hgd_unique_dev_trunc_f32 if x.dtype == torch.float32 else lib.hgd_unique_dev_i64
+    nat.check(fn(x.data_ptr(), n, out.data_ptr(), base, base + _UQ_HEAD, wsb,
+                 torch.cuda.current_stream(dev).cuda_stream), "hgd_unique_dev")
     count = buf[:8].view(torch.int64)
     live = torch.arange(n, device=dev) < count
     return torch.where(live, out, torch.zeros((), dtype=torch.int64, device=dev)), count

@@ -16,6 +16,7 @@ for each orientation; split plans for rows longer than ``split_threshold`` nonze
 """
 from __future__ import annotations
 
+import copy
 import ctypes
 import os
 from typing import Dict, Optional, Tuple
@@ -179,7 +180,18 @@ def spmm_csr(csr: CSR, X: torch.Tensor, val: Optional[torch.Tensor] = None,
     timer = profiling.active()
     if timer is not None:
         t0 = timer.begin()
-    if ex is None:
+    mask = getattr(csr, "mask", None)
+    if mask is not None:
+        if ex is not None:
+            raise NotImplementedError("spmm: no fused row epilogue over a masked (edge-dropped) "
+                                      "view")
+        nat.check(lib.hgd_spmm_masked(
+            csr.rowptr.data_ptr(), csr.col.data_ptr() if csr.nnz else None, nat.ptr(val),
+            mask.data_ptr() if csr.nnz else None, float(csr.keep), nat.ptr(row_scale),
+            csr.n_rows, csr.n_cols, int(row_begin), int(row_end), X.data_ptr(), X.stride(0),
+            out.data_ptr(), out.stride(0), d, int(epilogue), float(slope), plan_ptr, nat.ptr(ws),
+            wsb, _stream(X.device)), "hgd_spmm_masked")
+    elif ex is None:
         nat.check(lib.hgd_spmm(
             csr.rowptr.data_ptr(), csr.col.data_ptr() if csr.nnz else None, nat.ptr(val),
             nat.ptr(row_scale), csr.n_rows, csr.n_cols, int(row_begin), int(row_end),
@@ -408,6 +420,35 @@ class Incidence:
         out.perm_t = None  # a dropped structure is not dropped again (the reference drops the base)
         return out
 
+    def masked(self, mask: torch.Tensor, keep: float) -> "MaskedIncidence":
+        """SpAdjDropEdge's output (HCCF.py:217-226) as a VIEW of this incidence: no compaction
+        at all. The hops run over this structure and skip the dropped edges
+        (hgd_spmm_masked: weight val[e] / keep, kept edges in edge order — the sums of the
+        compacted matrix of :meth:`drop`, bitwise when no row is split). The CSC-order mask is
+        one byte gather through ``perm_t``; nothing is read back to the host, so a step using
+        it can be captured in a HIP graph. For the plain hops (GCNLayer, HGCNConv without
+        degree scales); degree scales of the dropped matrix need :meth:`drop`."""
+        if self.perm_t is None:
+            raise RuntimeError("Incidence.masked: needs the CSC→CSR permutation (a structure "
+                               "built from a COO)")
+        dev = self.device
+        m = mask.to(device=dev, dtype=torch.uint8).contiguous()
+        if m.numel() != self.nnz:
+            raise ValueError("Incidence.masked: mask size mismatch")
+        if not keep > 0.0:
+            raise ValueError("Incidence.masked: keep must be > 0")
+        m_t = torch.empty_like(m)
+        if self.nnz:
+            nat.check(nat.load().hgd_gather_u8(m.data_ptr(), self.perm_t.data_ptr(), self.nnz,
+                                               m_t.data_ptr(), _stream(dev)), "hgd_gather_u8")
+        csr = copy.copy(self.csr)
+        csc = copy.copy(self.csc)
+        csr.mask, csr.keep = m, float(keep)
+        csc.mask, csc.keep = m_t, float(keep)
+        out = MaskedIncidence(csr, csc, self.val, self.val_t)
+        out.parent = self
+        return out
+
     @classmethod
     def from_dense(cls, A: torch.Tensor, device=None, **kw) -> "Incidence":
         """The nonzero pattern and values of a dense matrix (``torch.nonzero(A)`` order), e.g.
@@ -510,6 +551,23 @@ class Incidence:
         v = self.val.cpu() if self.val is not None else torch.ones(self.nnz)
         out.index_put_((rows, self.csr.col.cpu().long()), v, accumulate=True)
         return out
+
+
+class MaskedIncidence(Incidence):
+    """An edge-dropped view of a parent incidence (:meth:`Incidence.masked`): both orientations
+    share the parent's arrays and carry a keep-mask; hops skip the dropped edges. ``nnz`` is
+    the parent's (the kept count stays on the device). Degree scales of the dropped matrix are
+    not available on a view."""
+
+    def scale(self, side: str, kind: Optional[str]) -> Optional[torch.Tensor]:
+        if kind is None:
+            return None
+        raise NotImplementedError("MaskedIncidence: degree scales of an edge-dropped view; "
+                                  "build the dropped structure with Incidence.drop")
+
+    def materialize(self, capacity: bool = True) -> Incidence:
+        """The compacted structure of the same drop (Incidence.drop)."""
+        return self.parent.drop(self.csr.mask, self.csr.keep, capacity=capacity)
 
 
 def drop_edges(indices: torch.Tensor, values: torch.Tensor, mask: torch.Tensor,

@@ -31,8 +31,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .functional import dense_two_hop, layer_norm, linear, spmm, two_hop, two_hop_fused
-from .incidence import (CSR, Incidence, dense_threshold, drop_edges, expand_rows,
-                        incidence_of)
+from .incidence import (CSR, Incidence, MaskedIncidence, dense_threshold, drop_edges,
+                        expand_rows, incidence_of)
 
 
 class GCNLayer(nn.Module):
@@ -186,10 +186,11 @@ class SpAdjDropEdge(nn.Module):
     def __init__(self, device_rng: bool = False, capture_safe: bool = False):
         super().__init__()
         self.device_rng = device_rng
-        # capture_safe: device mask from a device-side seed counter and a capacity-sized child
-        # structure returned as the Incidence itself — no host read, no host RNG, so the step
-        # can be replayed from a HIP graph (fresh masks every replay). The return value is then
-        # an Incidence (what GCNLayer / HGCNConv consume), not a torch sparse COO.
+        # capture_safe: device mask from a device-side seed counter, returned as a masked VIEW of
+        # the parent (Incidence.masked: the hops skip the dropped edges, no compaction) — no
+        # host read, no host RNG, so the step can be replayed from a HIP graph (fresh masks
+        # every replay). The return value is then an Incidence (what GCNLayer / HGCNConv
+        # consume), not a torch sparse COO.
         self.capture_safe = capture_safe
         self._seed = None
 
@@ -227,7 +228,7 @@ class SpAdjDropEdge(nn.Module):
             new_idx, new_vals, adj.shape, device=device, validate=False)
         return out
 
-    def _capture_safe_drop(self, adj, keep: float) -> Incidence:
+    def _capture_safe_drop(self, adj, keep: float) -> "MaskedIncidence":
         from . import _native as nat
         parent = incidence_of(adj)
         if not (parent.coo_sorted and parent.perm_t is not None):
@@ -243,7 +244,7 @@ class SpAdjDropEdge(nn.Module):
                 self._seed.data_ptr(), parent.nnz, keep, mask.data_ptr(),
                 torch.cuda.current_stream(dev).cuda_stream), "hgd_bernoulli_mask_dev")
         self._seed.add_(1)
-        return parent.drop(mask, keep, capacity=True)
+        return parent.masked(mask, keep)
 
 
 class Linear(nn.Linear):

@@ -121,6 +121,22 @@ hgd_status hgd_spmm(const int64_t* rowptr, const int32_t* col, const float* val,
                     const hgd_split_plan* plan, void* workspace, size_t workspace_bytes,
                     void* stream);
 
+/* The same hop over the EDGE-DROPPED matrix of SpAdjDropEdge (model/graph/HCCF.py:213-226:
+ * mask = floor(rand + keepRate), idxs[:, mask], vals[mask] / keepRate) without building it: the
+ * structure is the parent's, `mask` (uint8, this orientation's edge order; for the CSC of the
+ * parent that is mask_csr[perm_t]) selects the kept edges, each weighted by val[e] / keep (IEEE
+ * fp32 division, as the dropped COO's values; val == NULL keeps all-ones weights, like
+ * hgd_dropedge_structure). Kept edges are summed in edge order, so a row's sum equals the hop
+ * over the compacted matrix of hgd_dropedge_structure whenever the split plan covers the same
+ * rows (no split rows: bit-identical). Replaces the per-step compaction (count, scan, compact,
+ * row pointers for the CSR and the CSC) of a training step's drop-edge. */
+hgd_status hgd_spmm_masked(const int64_t* rowptr, const int32_t* col, const float* val,
+                           const uint8_t* mask, float keep, const float* row_scale,
+                           int64_t n_rows, int64_t n_src_rows, int64_t row_begin,
+                           int64_t row_end, const float* X, int64_t ldx, float* Y, int64_t ldy,
+                           int32_t d, int32_t epilogue, float slope, const hgd_split_plan* plan,
+                           void* workspace, size_t workspace_bytes, void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * Fused row epilogue of an ED-HNN / HGCN layer. Replaces the torch ops
  * the reference runs on the hop output, each an extra [N,d] HBM round trip and launch:
@@ -325,6 +341,10 @@ hgd_status hgd_expand_rows(const int64_t* rowptr, int64_t n_rows, int64_t nnz, i
 /* out[i] = src[perm[i]] (4-byte elements: int32 or fp32 bit patterns). */
 hgd_status hgd_gather32(const void* src, const int32_t* perm, int64_t n, void* out,
                         void* stream);
+/* out[i] = src[perm[i]] for bytes: a CSR-order keep-mask into CSC order through perm_t
+ * (hgd_spmm_masked's backward hop). perm 16-byte aligned, out 4-byte aligned. */
+hgd_status hgd_gather_u8(const uint8_t* src, const int32_t* perm, int64_t n, uint8_t* out,
+                         void* stream);
 /* s[r] = deg(r)^power with deg = rowptr diff (val == NULL) or Σ val over the row; deg == 0 → 0.
  * power is -1.0 (D^-1) or -0.5 (D^-1/2) or any other exponent. */
 hgd_status hgd_degree_scale(const int64_t* rowptr, const float* val, int64_t n_rows,
@@ -459,6 +479,14 @@ hgd_status hgd_unique_sort_i64(const int64_t* keys, int64_t n, int64_t* out, int
                                void* workspace, size_t workspace_bytes, void* stream);
 hgd_status hgd_unique_sort_trunc_f32(const float* x, int64_t n, int64_t* out, int64_t* n_out,
                                      void* workspace, size_t workspace_bytes, void* stream);
+/* Device-complete form (a captured training step cannot take the host-side fallback): the
+ * bitmap window is [min, min + 2^24); keys beyond it are collected and sorted by one workgroup
+ * (in LDS up to 4,096 of them, else a bitonic network over the workspace) and appended — they
+ * are all larger. *n_out is always the unique count. Same output as the forms above. */
+hgd_status hgd_unique_dev_i64(const int64_t* keys, int64_t n, int64_t* out, int64_t* n_out,
+                              void* workspace, size_t workspace_bytes, void* stream);
+hgd_status hgd_unique_dev_trunc_f32(const float* x, int64_t n, int64_t* out, int64_t* n_out,
+                                    void* workspace, size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Elementwise epilogues around the hops (contiguous fp32, 16-byte aligned).

@@ -65,6 +65,63 @@ def test_device_seed_mask_and_capacity_drop(dev):
     assert torch.equal(torch.autograd.grad(y1, X, g)[0], torch.autograd.grad(y2, X, g)[0])
 
 
+@pytest.mark.parametrize("d", [64, 32, 7, 256])
+def test_masked_view_hops_equal_compacted(dev, d):
+    """Incidence.masked (hgd_spmm_masked: the dropped matrix as a view of its parent) against
+    the compacted structure of the same mask (Incidence.drop): without split rows every hop is
+    bit-identical (kept edges summed in edge order), forward (CSR) and backward (CSC, the mask
+    gathered through perm_t), for the float4 widths, a scalar width (d = 7) and a multi-pass one
+    (d = 256); the two-hop A·(Aᵀ·X) of HGCNConv too."""
+    from hypergraph_diffusion_for_recommendation_amd.encoders import sparse_tensor_of
+    from hypergraph_diffusion_for_recommendation_amd.functional import spmm, two_hop
+    A = _graph(900, 1300, 20_000, seed=5)
+    parent = sparse_tensor_of(A, dev)._hgd_incidence
+    assert parent.csr.n_heavy == 0 and parent.csc.n_heavy == 0
+    mask = torch.from_numpy(O.device_keep_mask(99, parent.nnz, 0.6).astype(np.uint8)).to(dev)
+    view = parent.masked(mask, 0.6)
+    exact = parent.drop(mask, 0.6)
+    X = torch.randn(A.shape[0], d, device=dev, requires_grad=True)
+    g = torch.randn(A.shape[0], d, device=dev)
+    for tr in (False, True):
+        yv, ye = spmm(view, X, transpose=tr), spmm(exact, X, transpose=tr)
+        assert torch.equal(yv, ye)
+        assert torch.equal(torch.autograd.grad(yv, X, g)[0], torch.autograd.grad(ye, X, g)[0])
+    zv, ze = two_hop(view, X, None, None, None), two_hop(exact, X, None, None, None)
+    assert torch.equal(zv, ze)
+    assert torch.equal(torch.autograd.grad(zv, X, g)[0], torch.autograd.grad(ze, X, g)[0])
+    with pytest.raises(NotImplementedError):
+        view.scale("row", "sym")
+
+
+def test_masked_view_with_split_rows(dev):
+    """Rows longer than the split threshold keep the parent's split plan under a mask: chunk
+    partials of the parent's 512-edge chunks (kept edges only), so sums agree with the compacted
+    structure's to fp32 rounding of a different association (1e-5 of Σ|terms|), and with the
+    float64 restatement of the dropped matrix."""
+    from hypergraph_diffusion_for_recommendation_amd import Incidence
+    from hypergraph_diffusion_for_recommendation_amd.functional import spmm
+    rng = np.random.default_rng(3)
+    rows = np.concatenate([np.zeros(6000, np.int64), rng.integers(1, 400, 8000)])
+    cols = np.concatenate([np.arange(6000), rng.integers(0, 6000, 8000)])
+    vals = rng.random(rows.size).astype(np.float32) + 0.5
+    key = np.unique(rows * 6000 + cols, return_index=True)[1]
+    rows, cols, vals = rows[key], cols[key], vals[key]
+    inc = Incidence.from_coo(torch.from_numpy(np.stack([rows, cols])), torch.from_numpy(vals),
+                             (400, 6000), device=dev)
+    assert inc.csr.n_heavy >= 1
+    m = (rng.random(rows.size) < 0.5).astype(np.uint8)
+    view = inc.masked(torch.from_numpy(m), 0.5)
+    X = torch.randn(6000, 64, device=dev)
+    got = spmm(view, X).double().cpu().numpy()
+    kv = (vals[m == 1] / np.float32(0.5)).astype(np.float64)
+    Xd = X.double().cpu().numpy()
+    ref = np.zeros((400, 64))
+    mag = np.zeros((400, 64))
+    np.add.at(ref, rows[m == 1], kv[:, None] * Xd[cols[m == 1]])
+    np.add.at(mag, rows[m == 1], np.abs(kv[:, None] * Xd[cols[m == 1]]))
+    assert np.all(np.abs(got - ref) <= 1e-5 * mag + 1e-30)
+
+
 def test_unique_long_n_and_counted_contrast_loss(dev):
     from hypergraph_diffusion_for_recommendation_amd.functional import (contrast_loss,
                                                                          unique_long_n)
@@ -155,23 +212,24 @@ def test_captured_hccf_steps_equal_eager_steps(dev):
 
 
 def test_capture_safe_step_matches_reference(dev):
-    """One eager capture-safe HCCF step (device mask, capacity structures, counted InfoNCE)
-    against the float64 reference with the same drop-edge structures."""
+    """One eager capture-safe HCCF step (device mask, masked drop-edge views, counted InfoNCE)
+    against the float64 reference with the same drop-edge matrices."""
     enc, U, I = _hccf(dev, drop_rate=0.0)
     N = U + I
     drops = []
 
-    class Recording(torch.nn.Module):  # keeps each capacity child's live COO (eager test only)
+    class Recording(torch.nn.Module):  # keeps each dropped matrix's live COO (eager test only)
         def __init__(self, inner):
             super().__init__()
             self.inner = inner
 
         def forward(self, adj, keep):
-            child = self.inner(adj, keep)
-            k = int(child.csr.rowptr[-1])
+            child = self.inner(adj, keep)  # a masked view of the parent (Incidence.masked)
+            m = child.csr.mask.bool().cpu()
             rows = torch.repeat_interleave(torch.arange(N), child.csr.rowptr.diff().cpu())
-            drops.append((torch.stack([rows, child.csr.col[:k].cpu().long()]),
-                          child.val[:k].cpu()))
+            # vals[mask] / keepRate in float32, as the reference's SpAdjDropEdge (HCCF.py:224)
+            drops.append((torch.stack([rows[m], child.csr.col.cpu().long()[m]]),
+                          child.val.cpu()[m] / keep))
             return child
 
     enc.edgeDropper = Recording(enc.edgeDropper)

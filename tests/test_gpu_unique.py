@@ -79,3 +79,47 @@ def test_unique_range_feeds_contrast_loss_bounds(dev):
     ok[1] = 12  # in-place change: the cached range is ignored, the check reads the values
     with pytest.raises(IndexError):
         contrast_loss(E, E.clone(), ok, 0.2)
+
+
+def _dev_unique(t):
+    from hypergraph_diffusion_for_recommendation_amd.functional import unique_long_n
+    vals, count = unique_long_n(t)
+    k = int(count.item())
+    assert vals.numel() == t.numel() and not vals[k:].any()
+    return vals[:k]
+
+
+def test_device_complete_unique_paths(dev):
+    """hgd_unique_dev_* (functional.unique_long_n, the captured step's unique): the bitmap window
+    [min, min + 2^24) plus the far keys merged on the device — the LDS sort of up to 4,096 far
+    keys and the in-workspace bitonic network beyond — against torch.unique, bit-exact."""
+    rng = np.random.default_rng(1)
+    cases = {
+        "small_range": rng.integers(-5, 6, size=100_000),
+        "global_bitmap": rng.integers(-10**6, 10**6, size=300_000),
+        "cap_minus_one": np.array([7, 7 + (1 << 24) - 1, 100, 7]),
+        "one_far_key": np.array([7, 7 + (1 << 24), 100, 7 + (1 << 24)]),
+        "far_lds": np.concatenate([rng.integers(0, 50, 10_000),
+                                   rng.integers(1 << 40, (1 << 40) + 3000, 3000)]),
+        "far_global": rng.integers(-2**62, 2**62, size=200_000),   # ~all keys far: bitonic path
+        "extremes": np.array([-2**63, 2**63 - 1, 0, -2**63, 5]),
+        "single": np.array([42]),
+        "dups": np.full(1000, -3),
+    }
+    for name, a in cases.items():
+        print("device-complete unique case:", name, flush=True)
+        t = torch.from_numpy(a.astype(np.int64)).to(dev)
+        assert torch.equal(_dev_unique(t).cpu(), torch.unique(t.cpu())), name
+
+
+def test_device_complete_unique_of_floats(dev):
+    """Truncated embeddings (HCCF.py:65-66), including a NaN that drags the window to INT64_MIN
+    (every other key becomes a far key)."""
+    g = torch.Generator(device=dev).manual_seed(3)
+    x = torch.randn(4096, 64, device=dev, generator=g) * 3.0
+    assert torch.equal(_dev_unique(x).cpu(), _ref(x))
+    y = x.clone()
+    y[5, 7] = float("nan")
+    want = _ref(y)  # the host cast maps NaN to INT64_MIN too
+    assert want[0] == -2**63
+    assert torch.equal(_dev_unique(y).cpu(), want)
