@@ -68,6 +68,46 @@ class RowEpilogue(ctypes.Structure):
     ]
 
 
+class GemmRowsDesc(ctypes.Structure):
+    """Mirror of ``hgd_gemm_rows_desc`` (include/hgd.h)."""
+
+    _fields_ = [
+        ("A", c_void_p),
+        ("lda", c_i64),
+        ("relu_mask", c_void_p),
+        ("ldm", c_i64),
+        ("B", c_void_p),
+        ("bsk", c_i64),
+        ("bsn", c_i64),
+        ("bias", c_void_p),
+        ("relu", c_i32),
+        ("accumulate", c_i32),
+        ("Y", c_void_p),
+        ("ldy", c_i64),
+        ("rows", c_i64),
+        ("K", c_i32),
+        ("N", c_i32),
+    ]
+
+
+class GemmTnDesc(ctypes.Structure):
+    """Mirror of ``hgd_gemm_tn_desc`` (include/hgd.h)."""
+
+    _fields_ = [
+        ("A", c_void_p),
+        ("lda", c_i64),
+        ("relu_mask", c_void_p),
+        ("ldm", c_i64),
+        ("B", c_void_p),
+        ("ldb", c_i64),
+        ("rows", c_i64),
+        ("M", c_i32),
+        ("N", c_i32),
+        ("C", c_void_p),
+        ("colsum_A", c_void_p),
+    ]
+
+
 class IncidenceView(ctypes.Structure):
     """Mirror of ``hgd_incidence_view`` (include/hgd.h)."""
 
@@ -129,6 +169,9 @@ _SIGNATURES = {
     "hgd_linear_backward_weight": (c_i32, [c_void_p, c_i64, c_void_p, c_i64, c_void_p, c_i64,
                                            c_i64, c_i32, c_i32, c_void_p, c_void_p, c_void_p,
                                            c_size, c_void_p]),
+    "hgd_gemm_rows": (c_i32, [ctypes.POINTER(GemmRowsDesc), c_i32, c_void_p]),
+    "hgd_gemm_tn_workspace_size": (c_size, [ctypes.POINTER(GemmTnDesc), c_i32]),
+    "hgd_gemm_tn": (c_i32, [ctypes.POINTER(GemmTnDesc), c_i32, c_void_p, c_size, c_void_p]),
     "hgd_infonce_workspace_size": (c_size, [c_i64, c_i32]),
     "hgd_infonce_forward": (c_i32, [c_void_p, c_i64, c_void_p, c_i64, c_i64, c_void_p, c_i64,
                                     c_i32, c_f32, c_void_p, c_void_p, c_void_p, c_void_p,

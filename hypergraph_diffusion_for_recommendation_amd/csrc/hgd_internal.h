@@ -60,4 +60,12 @@ inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 // (reduce.hip). Used for split-K and per-block partials.
 hgd_status sum_rows(const float* P, int64_t S, int64_t W, float* out, hipStream_t st);
 
+// Several independent column sums (up to 4) in one launch, each exactly as sum_rows.
+struct SumRowsJob {
+  const float* P;
+  int64_t S, W;
+  float* out;
+};
+hgd_status sum_rows_jobs(const SumRowsJob* jobs, int n, hipStream_t st);
+
 }  // namespace hgd

@@ -20,6 +20,8 @@
 //    MFMAs of a 4-row step produce the whole 64 × 64 tile with (m, n) = (4i + t, 4j + u)
 //    permuted; the 4 waves are combined in LDS in wave order, the S slice partials by sum_rows in
 //    slice order. No atomics: results are bitwise reproducible.
+#include <algorithm>
+
 #include "device_util.h"
 #include "hgd_internal.h"
 
@@ -47,10 +49,26 @@ struct RowGemm {
   int64_t ldy;
   int64_t rows;
   int32_t K, N;
+  int32_t accumulate;  // Y += product (the bias / ReLU apply to the product alone)
+};
+
+// Up to two independent products of the same K, N and mask mode in ONE launch (HCCF's user and
+// item halves of the learned-hypergraph products): blocks [0, nb0) take p[0], the rest p[1],
+// each with its own grid-stride loop. The launch count, not the bytes, bounds these 10 MB
+// products (profiles/r02_small_kernels).
+struct RowGemmGroup {
+  RowGemm p[2];
+  int32_t count;
+  int32_t nb0;
 };
 
 template <int KQ, bool MASK>  // K = 16·KQ; MASK: A ⊙ (mask > 0)
-__global__ __launch_bounds__(256) void k_row_gemm(RowGemm p) {
+__global__ __launch_bounds__(256) void k_row_gemm(RowGemmGroup grp) {
+  const bool second = grp.count > 1 && static_cast<int>(blockIdx.x) >= grp.nb0;
+  const RowGemm p = second ? grp.p[1] : grp.p[0];
+  const int bx = static_cast<int>(blockIdx.x) - (second ? grp.nb0 : 0);
+  const int nbx = grp.count > 1 ? (second ? static_cast<int>(gridDim.x) - grp.nb0 : grp.nb0)
+                                : static_cast<int>(gridDim.x);
   constexpr int K = 16 * KQ;
   constexpr int LDB = 65;           // padded row: the k-contiguous staging writes spread banks
   constexpr int PER = K * 64 / 256;  // staged floats per thread
@@ -66,8 +84,8 @@ __global__ __launch_bounds__(256) void k_row_gemm(RowGemm p) {
   const int n0 = blockIdx.y * 64;
   const int nt = min(4, (p.N - n0) / 16);  // live 16-column tiles of this slice (uniform)
   const int64_t tiles = (p.rows + 16 * SUB - 1) / (16 * SUB);  // super-tiles
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * 4;
-  int64_t tile = static_cast<int64_t>(blockIdx.x) * 4 + wave;
+  const int64_t stride = static_cast<int64_t>(nbx) * 4;
+  int64_t tile = static_cast<int64_t>(bx) * 4 + wave;
   // Unconditional raw loads (the compiler then counts them exactly in its vmcnt waits): rows
   // past the end are clamped to the last row and their results never stored; the ReLU mask is
   // applied when the tile is consumed.
@@ -146,6 +164,14 @@ __global__ __launch_bounds__(256) void k_row_gemm(RowGemm p) {
         }
       const int64_t r0 = tile * 16 * SUB + 16 * s;
       float* yb = p.Y + n0 + i16;
+      if (p.accumulate) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (t < nt && r0 + 4 * h + r < p.rows)
+              acc[t][r] += yb[(r0 + 4 * h + r) * p.ldy + 16 * t];
+      }
       if (nt == 4 && r0 + 16 <= p.rows) {
 #pragma unroll
         for (int t = 0; t < 4; ++t)
@@ -192,8 +218,17 @@ struct SplitK {
   float* part_bias;  // [S, M] or NULL
 };
 
+struct SplitKGroup {  // as RowGemmGroup: blocks [0, nb0) along x are p[0]'s row slices
+  SplitK p[2];
+  int32_t count;
+  int32_t nb0;
+};
+
 template <bool MASK>
-__global__ __launch_bounds__(256) void k_splitk_tn(SplitK p) {
+__global__ __launch_bounds__(256) void k_splitk_tn(SplitKGroup grp) {
+  const bool second = grp.count > 1 && static_cast<int>(blockIdx.x) >= grp.nb0;
+  const SplitK p = second ? grp.p[1] : grp.p[0];
+  const int64_t bx = static_cast<int64_t>(blockIdx.x) - (second ? grp.nb0 : 0);
   __shared__ float s_acc[4][64 * 64];
   __shared__ float s_bias[4][64];
   const int lane = threadIdx.x & 63;
@@ -202,7 +237,7 @@ __global__ __launch_bounds__(256) void k_splitk_tn(SplitK p) {
   const int h = lane >> 4;
   const int m0 = blockIdx.y * 64;
   const int n0 = blockIdx.z * 64;
-  const int64_t k_begin = static_cast<int64_t>(blockIdx.x) * p.rows_per_split;
+  const int64_t k_begin = bx * p.rows_per_split;
   const int64_t k_end = min(p.rows, k_begin + p.rows_per_split);
   const bool mcol = m0 + 4 * i16 < p.M;
   const bool ncol = n0 + 4 * i16 < p.N;
@@ -290,13 +325,12 @@ __global__ __launch_bounds__(256) void k_splitk_tn(SplitK p) {
     const int ml = e >> 6, nl = e & 63;
     if (m0 + ml < p.M && n0 + nl < p.N) {
       const float v = ((s_acc[0][e] + s_acc[1][e]) + s_acc[2][e]) + s_acc[3][e];
-      p.part[static_cast<int64_t>(blockIdx.x) * MN + static_cast<int64_t>(m0 + ml) * p.N + n0 +
-             nl] = v;
+      p.part[bx * MN + static_cast<int64_t>(m0 + ml) * p.N + n0 + nl] = v;
     }
   }
   if (want_bias && threadIdx.x < 64 && m0 + static_cast<int>(threadIdx.x) < p.M) {
     const int ml = threadIdx.x;
-    p.part_bias[static_cast<int64_t>(blockIdx.x) * p.M + m0 + ml] =
+    p.part_bias[bx * p.M + m0 + ml] =
         ((s_bias[0][ml] + s_bias[1][ml]) + s_bias[2][ml]) + s_bias[3][ml];
   }
 }
@@ -305,27 +339,62 @@ bool al16(const void* p, int64_t ld) {
   return p == nullptr || (reinterpret_cast<uintptr_t>(p) % 16 == 0 && ld % 4 == 0);
 }
 
-hgd_status row_gemm(const RowGemm& p, hipStream_t st, const char* fn) {
-  if (p.rows == 0) return HGD_OK;
-  const int64_t tiles = (p.rows + 15) / 16;  // the kernel's 16-row tiles
-  int64_t bx = (tiles + 3) / 4;
-  if (bx > kRowGemmMaxBlocks) bx = kRowGemmMaxBlocks;
-  const dim3 grid(static_cast<unsigned>(bx), static_cast<unsigned>((p.N + 63) / 64));
-  switch (p.K / 16) {
+// Blocks per product: one per 4 16-row tiles up to the 512 workgroups resident at once; a group
+// of two shares that budget in proportion to the rows.
+void blocks_for(const int64_t* rows, int count, int64_t* bx) {
+  int64_t tiles[2] = {0, 0}, want[2] = {0, 0}, total = 0;
+  for (int i = 0; i < count; ++i) {
+    tiles[i] = (rows[i] + 15) / 16;
+    want[i] = (tiles[i] + 3) / 4;
+    total += want[i];
+  }
+  for (int i = 0; i < count; ++i) {
+    bx[i] = want[i];
+    if (total > kRowGemmMaxBlocks) bx[i] = std::max<int64_t>(1, want[i] * kRowGemmMaxBlocks / total);
+  }
+}
+
+hgd_status row_gemm_group(RowGemmGroup g, hipStream_t st, const char* fn) {
+  const RowGemm& p = g.p[0];
+  if (g.count == 2) {
+    const RowGemm& q = g.p[1];
+    HGD_REQUIRE(q.K == p.K && q.N == p.N && (q.mask != nullptr) == (p.mask != nullptr),
+                "%s: grouped products need equal K, N and mask mode", fn);
+    if (q.rows == 0) g.count = 1;
+    if (p.rows == 0) {
+      g.p[0] = g.p[1];
+      g.count = g.p[0].rows > 0 ? 1 : 0;
+    }
+  }
+  if (g.count == 0 || g.p[0].rows == 0) return HGD_OK;
+  const int64_t rows[2] = {g.p[0].rows, g.count > 1 ? g.p[1].rows : 0};
+  int64_t bx[2] = {0, 0};
+  blocks_for(rows, g.count, bx);
+  g.nb0 = static_cast<int32_t>(bx[0]);
+  const dim3 grid(static_cast<unsigned>(bx[0] + bx[1]), static_cast<unsigned>((p.N + 63) / 64));
+  switch (g.p[0].K / 16) {
 #define HGD_CASE(Q)                                                                \
     case Q:                                                                        \
-      if (p.mask)                                                                  \
-        hipLaunchKernelGGL((k_row_gemm<Q, true>), grid, dim3(256), 0, st, p);      \
+      if (g.p[0].mask)                                                             \
+        hipLaunchKernelGGL((k_row_gemm<Q, true>), grid, dim3(256), 0, st, g);      \
       else                                                                         \
-        hipLaunchKernelGGL((k_row_gemm<Q, false>), grid, dim3(256), 0, st, p);     \
+        hipLaunchKernelGGL((k_row_gemm<Q, false>), grid, dim3(256), 0, st, g);     \
       break;
     HGD_CASE(1) HGD_CASE(2) HGD_CASE(3) HGD_CASE(4) HGD_CASE(5) HGD_CASE(6) HGD_CASE(7)
     HGD_CASE(8)
 #undef HGD_CASE
     default:
-      return fail(HGD_ERR_UNSUPPORTED, "%s: K = %d (needs 16..128, multiple of 16)", fn, p.K);
+      return fail(HGD_ERR_UNSUPPORTED, "%s: K = %d (needs 16..128, multiple of 16)", fn,
+                  g.p[0].K);
   }
   return check_launch(fn);
+}
+
+hgd_status row_gemm(const RowGemm& p, hipStream_t st, const char* fn) {
+  RowGemmGroup g{};
+  g.p[0] = p;
+  g.count = 1;
+  return row_gemm_group(g, st, fn);
 }
 
 int64_t splits_for(int64_t rows) {
@@ -336,6 +405,59 @@ int64_t splits_for(int64_t rows) {
   int64_t s = (rows + 127) / 128;
   if (s > kSplitKResident) s = kSplitKResident;
   return s < 1 ? 1 : s;
+}
+
+// Row slices of each product of a split-K group (the pair shares the resident budget).
+void tn_splits(const hgd_gemm_tn_desc* d, int count, int64_t* S, int64_t* per) {
+  int64_t total = 0;
+  for (int i = 0; i < count; ++i) {
+    S[i] = splits_for(d[i].rows);
+    total += S[i];
+  }
+  for (int i = 0; i < count; ++i) {
+    if (count > 1 && total > kSplitKResident)
+      S[i] = std::max<int64_t>(1, S[i] * kSplitKResident / total);
+    const int64_t rows = d[i].rows > 0 ? d[i].rows : 1;
+    int64_t pr = (rows + S[i] - 1) / S[i];
+    per[i] = (pr + 63) / 64 * 64;  // whole 64-row batches
+    S[i] = (rows + per[i] - 1) / per[i];
+  }
+}
+
+size_t tn_part_bytes(const hgd_gemm_tn_desc& d, int64_t S) {
+  return align_up(static_cast<size_t>(S) * d.M * d.N * 4);
+}
+size_t tn_bias_bytes(const hgd_gemm_tn_desc& d, int64_t S) {
+  return d.colsum_A ? align_up(static_cast<size_t>(S) * d.M * 4) : 0;
+}
+
+hgd_status check_tn(const hgd_gemm_tn_desc& d, const char* fn) {
+  HGD_REQUIRE(d.rows >= 0, "%s: negative rows", fn);
+  HGD_REQUIRE(d.M % 16 == 0 && d.M >= 16 && d.N % 16 == 0 && d.N >= 16,
+              "%s: M, N (%d, %d) must be positive multiples of 16", fn, d.M, d.N);
+  HGD_REQUIRE(d.lda >= d.M && d.ldb >= d.N && (!d.relu_mask || d.ldm >= d.M),
+              "%s: leading dimension too small", fn);
+  HGD_REQUIRE(d.C, "%s: null C", fn);
+  if (d.rows == 0) return HGD_OK;
+  HGD_REQUIRE(d.A && d.B, "%s: null A / B", fn);
+  HGD_REQUIRE(al16(d.A, d.lda) && al16(d.B, d.ldb) && al16(d.relu_mask, d.ldm),
+              "%s: rows must be 16-byte aligned", fn);
+  return HGD_OK;
+}
+
+hgd_status check_rows(const hgd_gemm_rows_desc& d, const char* fn) {
+  HGD_REQUIRE(d.rows >= 0, "%s: negative rows", fn);
+  HGD_REQUIRE(d.K % 16 == 0 && d.K >= 16 && d.K <= 128,
+              "%s: K = %d must be a multiple of 16 in [16, 128]", fn, d.K);
+  HGD_REQUIRE(d.N % 16 == 0 && d.N >= 16, "%s: N = %d must be a positive multiple of 16", fn,
+              d.N);
+  HGD_REQUIRE(d.lda >= d.K && d.ldy >= d.N && (!d.relu_mask || d.ldm >= d.K),
+              "%s: leading dimension too small", fn);
+  if (d.rows == 0) return HGD_OK;
+  HGD_REQUIRE(d.A && d.B && d.Y, "%s: null pointer", fn);
+  HGD_REQUIRE(al16(d.A, d.lda) && al16(d.relu_mask, d.ldm), "%s: A / mask rows must be 16-byte "
+              "aligned", fn);
+  return HGD_OK;
 }
 
 }  // namespace
@@ -411,11 +533,136 @@ extern "C" hgd_status hgd_linear_backward_data(const float* dY, int64_t ldy, con
   return row_gemm(p, as_stream(stream), "hgd_linear_backward_data");
 }
 
+extern "C" size_t hgd_gemm_tn_workspace_size(const hgd_gemm_tn_desc* descs, int32_t count) {
+  if (!descs || count < 1 || count > 2) return 0;
+  int64_t S[2] = {0, 0}, per[2] = {0, 0};
+  hgd::tn_splits(descs, count, S, per);
+  size_t b = 0;
+  for (int i = 0; i < count; ++i) {
+    if (descs[i].rows <= 0 || descs[i].M <= 0 || descs[i].N <= 0) continue;
+    b += hgd::tn_part_bytes(descs[i], S[i]) + hgd::tn_bias_bytes(descs[i], S[i]);
+  }
+  return b;
+}
+
+extern "C" hgd_status hgd_gemm_tn(const hgd_gemm_tn_desc* descs, int32_t count, void* workspace,
+                                  size_t workspace_bytes, void* stream) {
+  using namespace hgd;
+  clear_error();
+  HGD_REQUIRE(descs && count >= 1 && count <= 2, "hgd_gemm_tn: 1 or 2 descriptors");
+  for (int i = 0; i < count; ++i) {
+    const hgd_status c = check_tn(descs[i], "hgd_gemm_tn");
+    if (c != HGD_OK) return c;
+  }
+  if (count == 2)
+    HGD_REQUIRE(descs[0].M == descs[1].M && descs[0].N == descs[1].N &&
+                    (descs[0].relu_mask != nullptr) == (descs[1].relu_mask != nullptr),
+                "hgd_gemm_tn: grouped products need equal M, N and mask mode");
+  hipStream_t st = as_stream(stream);
+  const size_t need = hgd_gemm_tn_workspace_size(descs, count);
+  if (workspace_bytes < need || (need && !workspace))
+    return fail(HGD_ERR_WORKSPACE, "hgd_gemm_tn: workspace %zu < required %zu", workspace_bytes,
+                need);
+  int64_t S[2] = {0, 0}, per[2] = {0, 0};
+  tn_splits(descs, count, S, per);
+  SplitKGroup g{};
+  char* w = static_cast<char*>(workspace);
+  int live = 0;
+  for (int i = 0; i < count; ++i) {
+    const hgd_gemm_tn_desc& d = descs[i];
+    if (d.rows == 0) {  // an empty product: zeros
+      HGD_HIP(hipMemsetAsync(d.C, 0, static_cast<size_t>(d.M) * d.N * 4, st));
+      if (d.colsum_A) HGD_HIP(hipMemsetAsync(d.colsum_A, 0, static_cast<size_t>(d.M) * 4, st));
+      continue;
+    }
+    SplitK& p = g.p[live];
+    p.A = d.A;
+    p.lda = d.lda;
+    p.mask = d.relu_mask;
+    p.ldm = d.ldm;
+    p.B = d.B;
+    p.ldb = d.ldb;
+    p.rows = d.rows;
+    p.M = d.M;
+    p.N = d.N;
+    p.rows_per_split = per[i];
+    p.part = reinterpret_cast<float*>(w);
+    w += tn_part_bytes(d, S[i]);
+    p.part_bias = d.colsum_A ? reinterpret_cast<float*>(w) : nullptr;
+    w += tn_bias_bytes(d, S[i]);
+    if (live == 0) g.nb0 = static_cast<int32_t>(S[i]);
+    ++live;
+  }
+  if (live == 0) return HGD_OK;
+  g.count = live;
+  int64_t Stot = 0;
+  int li = 0;
+  const hgd_gemm_tn_desc* ld[2] = {nullptr, nullptr};
+  int64_t Sl[2] = {0, 0};
+  for (int i = 0; i < count; ++i)
+    if (descs[i].rows > 0) {
+      ld[li] = &descs[i];
+      Sl[li++] = S[i];
+      Stot += S[i];
+    }
+  const dim3 grid(static_cast<unsigned>(Stot), static_cast<unsigned>((g.p[0].M + 63) / 64),
+                  static_cast<unsigned>((g.p[0].N + 63) / 64));
+  if (g.p[0].mask)
+    hipLaunchKernelGGL((k_splitk_tn<true>), grid, dim3(256), 0, st, g);
+  else
+    hipLaunchKernelGGL((k_splitk_tn<false>), grid, dim3(256), 0, st, g);
+  hgd_status s = check_launch("hgd_gemm_tn");
+  if (s != HGD_OK) return s;
+  // the slice partials in slice order: all sums of the group in one launch
+  SumRowsJob jobs[4];
+  int nj = 0;
+  for (int i = 0; i < live; ++i) {
+    jobs[nj++] = SumRowsJob{g.p[i].part, Sl[i], static_cast<int64_t>(g.p[i].M) * g.p[i].N,
+                            ld[i]->C};
+    if (ld[i]->colsum_A) jobs[nj++] = SumRowsJob{g.p[i].part_bias, Sl[i], g.p[i].M, ld[i]->colsum_A};
+  }
+  return sum_rows_jobs(jobs, nj, st);
+}
+
+extern "C" hgd_status hgd_gemm_rows(const hgd_gemm_rows_desc* descs, int32_t count, void* stream) {
+  using namespace hgd;
+  clear_error();
+  HGD_REQUIRE(descs && count >= 1 && count <= 2, "hgd_gemm_rows: 1 or 2 descriptors");
+  RowGemmGroup g{};
+  for (int i = 0; i < count; ++i) {
+    const hgd_gemm_rows_desc& d = descs[i];
+    const hgd_status c = check_rows(d, "hgd_gemm_rows");
+    if (c != HGD_OK) return c;
+    RowGemm& p = g.p[i];
+    p.A = d.A;
+    p.lda = d.lda;
+    p.mask = d.relu_mask;
+    p.ldm = d.ldm;
+    p.B = d.B;
+    p.bsk = d.bsk;
+    p.bsn = d.bsn;
+    p.bias = d.bias;
+    p.relu = d.relu != 0;
+    p.Y = d.Y;
+    p.ldy = d.ldy;
+    p.rows = d.rows;
+    p.K = d.K;
+    p.N = d.N;
+    p.accumulate = d.accumulate != 0;
+  }
+  g.count = count;
+  return row_gemm_group(g, as_stream(stream), "hgd_gemm_rows");
+}
+
 extern "C" size_t hgd_linear_backward_weight_workspace_size(int64_t n_rows, int32_t out_features,
                                                            int32_t in_features) {
   if (n_rows <= 0 || out_features <= 0 || in_features <= 0) return 0;
-  const size_t S = static_cast<size_t>(hgd::splits_for(n_rows));
-  return hgd::align_up(S * out_features * in_features * 4) + hgd::align_up(S * out_features * 4);
+  hgd_gemm_tn_desc d{};
+  d.rows = n_rows;
+  d.M = out_features;
+  d.N = in_features;
+  d.colsum_A = reinterpret_cast<float*>(16);  // sized with the bias partials
+  return hgd_gemm_tn_workspace_size(&d, 1);
 }
 
 extern "C" hgd_status hgd_linear_backward_weight(const float* dY, int64_t ldy,
@@ -424,56 +671,17 @@ extern "C" hgd_status hgd_linear_backward_weight(const float* dY, int64_t ldy,
                                                  int32_t out_features, int32_t in_features,
                                                  float* dW, float* db, void* workspace,
                                                  size_t workspace_bytes, void* stream) {
-  using namespace hgd;
-  clear_error();
-  HGD_REQUIRE(n_rows >= 0, "hgd_linear_backward_weight: negative rows");
-  HGD_REQUIRE(out_features % 16 == 0 && out_features >= 16 && in_features % 16 == 0 &&
-                  in_features >= 16,
-              "hgd_linear_backward_weight: features (%d, %d) must be positive multiples of 16",
-              out_features, in_features);
-  HGD_REQUIRE(ldy >= out_features && ldx >= in_features && (!relu_out || ldr >= out_features),
-              "hgd_linear_backward_weight: leading dimension too small");
-  HGD_REQUIRE(dW, "hgd_linear_backward_weight: null dW");
-  hipStream_t st = as_stream(stream);
-  if (n_rows == 0) {
-    HGD_HIP(hipMemsetAsync(dW, 0, static_cast<size_t>(out_features) * in_features * 4, st));
-    if (db) HGD_HIP(hipMemsetAsync(db, 0, static_cast<size_t>(out_features) * 4, st));
-    return HGD_OK;
-  }
-  HGD_REQUIRE(dY && X, "hgd_linear_backward_weight: null dY / X");
-  HGD_REQUIRE(al16(dY, ldy) && al16(X, ldx) && al16(relu_out, ldr),
-              "hgd_linear_backward_weight: rows must be 16-byte aligned");
-  const size_t need = hgd_linear_backward_weight_workspace_size(n_rows, out_features, in_features);
-  if (workspace_bytes < need || !workspace)
-    return fail(HGD_ERR_WORKSPACE, "hgd_linear_backward_weight: workspace %zu < required %zu",
-                workspace_bytes, need);
-  const int64_t S = splits_for(n_rows);
-  int64_t per = (n_rows + S - 1) / S;
-  per = (per + 63) / 64 * 64;  // whole 64-row batches
-  SplitK p{};
-  p.A = dY;
-  p.lda = ldy;
-  p.mask = relu_out;
-  p.ldm = ldr;
-  p.B = X;
-  p.ldb = ldx;
-  p.rows = n_rows;
-  p.M = out_features;
-  p.N = in_features;
-  p.rows_per_split = per;
-  p.part = static_cast<float*>(workspace);
-  const size_t part_bytes = align_up(static_cast<size_t>(S) * out_features * in_features * 4);
-  p.part_bias = db ? reinterpret_cast<float*>(static_cast<char*>(workspace) + part_bytes) : nullptr;
-  const int64_t S_used = (n_rows + per - 1) / per;
-  const dim3 grid(static_cast<unsigned>(S_used), static_cast<unsigned>((out_features + 63) / 64),
-                  static_cast<unsigned>((in_features + 63) / 64));
-  if (relu_out)
-    hipLaunchKernelGGL((k_splitk_tn<true>), grid, dim3(256), 0, st, p);
-  else
-    hipLaunchKernelGGL((k_splitk_tn<false>), grid, dim3(256), 0, st, p);
-  hgd_status s = check_launch("hgd_linear_backward_weight");
-  if (s != HGD_OK) return s;
-  s = sum_rows(p.part, S_used, static_cast<int64_t>(out_features) * in_features, dW, st);
-  if (s != HGD_OK || !db) return s;
-  return sum_rows(p.part_bias, S_used, out_features, db, st);
+  hgd_gemm_tn_desc d{};
+  d.A = dY;
+  d.lda = ldy;
+  d.relu_mask = relu_out;
+  d.ldm = ldr;
+  d.B = X;
+  d.ldb = ldx;
+  d.rows = n_rows;
+  d.M = out_features;
+  d.N = in_features;
+  d.C = dW;
+  d.colsum_A = db;
+  return hgd_gemm_tn(&d, 1, workspace, workspace_bytes, stream);
 }

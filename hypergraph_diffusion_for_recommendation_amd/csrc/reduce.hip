@@ -11,12 +11,23 @@ namespace {
 
 constexpr int kWaves = 16;
 
-__global__ __launch_bounds__(kWaves * 64) void k_sum_rows(const float* __restrict__ P, int64_t S,
-                                                          int64_t W, float* __restrict__ out) {
+struct Jobs {
+  SumRowsJob j[4];
+  int64_t first[5];  // first block of each job
+  int n;
+};
+
+__global__ __launch_bounds__(kWaves * 64) void k_sum_rows(Jobs jobs) {
   __shared__ float s_part[kWaves][64];
+  int ji = 0;
+  for (int k = 1; k < jobs.n; ++k) ji += static_cast<int64_t>(blockIdx.x) >= jobs.first[k];
+  const SumRowsJob J = jobs.j[ji];
+  const float* __restrict__ P = J.P;
+  const int64_t S = J.S, W = J.W;
+  float* __restrict__ out = J.out;
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
-  const int64_t c = static_cast<int64_t>(blockIdx.x) * 64 + lane;
+  const int64_t c = (static_cast<int64_t>(blockIdx.x) - jobs.first[ji]) * 64 + lane;
   const int64_t per = (S + kWaves - 1) / kWaves;
   const int64_t s0 = w * per;
   const int64_t s1 = s0 + per < S ? s0 + per : S;
@@ -43,12 +54,25 @@ __global__ __launch_bounds__(kWaves * 64) void k_sum_rows(const float* __restric
 
 }  // namespace
 
-hgd_status sum_rows(const float* P, int64_t S, int64_t W, float* out, hipStream_t st) {
-  if (W <= 0) return HGD_OK;
-  const int64_t blocks = (W + 63) / 64;
+hgd_status sum_rows_jobs(const SumRowsJob* js, int n, hipStream_t st) {
+  Jobs jobs{};
+  int64_t blocks = 0;
+  for (int i = 0; i < n; ++i) {
+    if (js[i].W <= 0) continue;
+    jobs.first[jobs.n] = blocks;
+    jobs.j[jobs.n++] = js[i];
+    blocks += (js[i].W + 63) / 64;
+  }
+  if (jobs.n == 0) return HGD_OK;
+  jobs.first[jobs.n] = blocks;
   if (blocks > 0x7fffffffLL) return fail(HGD_ERR_UNSUPPORTED, "sum_rows: too many columns");
-  hipLaunchKernelGGL(k_sum_rows, dim3(blocks), dim3(kWaves * 64), 0, st, P, S, W, out);
+  hipLaunchKernelGGL(k_sum_rows, dim3(blocks), dim3(kWaves * 64), 0, st, jobs);
   return check_launch("sum_rows");
+}
+
+hgd_status sum_rows(const float* P, int64_t S, int64_t W, float* out, hipStream_t st) {
+  const SumRowsJob j{P, S, W, out};
+  return sum_rows_jobs(&j, 1, st);
 }
 
 }  // namespace hgd

@@ -24,7 +24,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from .functional import linear, two_hop_fused
+from .functional import dense_two_hop_pair, linear, two_hop_fused
 from .incidence import Incidence, incidence_of
 from .layers import EquivSetGNN, GCNLayer, HGCNConv, HGNNLayer, LayerNorm, SpAdjDropEdge
 
@@ -91,13 +91,12 @@ class HCCFEncoder(nn.Module):
         hyper_ii = linear(self.embedding_dict['item_emb'], self.embedding_dict['item_w'].t())
         for _ in range(self.n_layers):
             gcn_emb = self.gcnlayer(self.edgeDropper(self.sparse_norm_adj, keep_rate), hidden[-1])
-            # torch.split views instead of [:nu] / [nu:] slices: same values, and autograd
-            # joins the two halves' gradients with one cat instead of zero-fill + copy per slice
-            h_u, h_i = torch.split(hidden[-1], [nu, hidden[-1].shape[0] - nu])
-            hyper_uemb = self.hgnnlayer(self.drop_out(hyper_uu), h_u)
-            hyper_iemb = self.hgnnlayer(self.drop_out(hyper_ii), h_i)
+            # the user and item HGNNLayer calls (hgnnlayer(·, hidden[-1][:nu]) and [nu:]) and
+            # their cat as one pair op: grouped launches over both halves, the output and the
+            # table gradient written in place (no split / cat forward or backward)
             gcn_hidden += [gcn_emb]
-            hgnn_hidden += [torch.cat([hyper_uemb, hyper_iemb], 0)]
+            hgnn_hidden += [dense_two_hop_pair(self.drop_out(hyper_uu), self.drop_out(hyper_ii),
+                                               hidden[-1], nu)]
             hidden += [gcn_emb + hgnn_hidden[-1]]
         embeddings = sum(hidden)
         user_emb, item_emb = torch.split(embeddings, [nu, embeddings.shape[0] - nu])

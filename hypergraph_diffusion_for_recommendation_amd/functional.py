@@ -683,3 +683,96 @@ def dense_two_hop(H: torch.Tensor, X: torch.Tensor) -> torch.Tensor:
     if not _mm_ok(H, X):
         return torch.mm(H, torch.mm(H.T, X))
     return _DenseTwoHop.apply(H, X)
+
+
+def _rows_desc(A, B, bsk, bsn, K, N, Y, accumulate=False):
+    d = nat.GemmRowsDesc()
+    d.A, d.lda = A.data_ptr(), A.stride(0)
+    d.B, d.bsk, d.bsn = B.data_ptr(), bsk, bsn
+    d.accumulate = 1 if accumulate else 0
+    d.Y, d.ldy = Y.data_ptr(), Y.stride(0)
+    d.rows, d.K, d.N = A.shape[0], K, N
+    return d
+
+
+def _gemm_rows(descs, device):
+    arr = (nat.GemmRowsDesc * len(descs))(*descs)
+    nat.check(nat.load().hgd_gemm_rows(arr, len(descs),
+                                       torch.cuda.current_stream(device).cuda_stream),
+              "hgd_gemm_rows")
+
+
+def _gemm_tn_pair(pairs, device):
+    """[Aᵢᵀ·Bᵢ] for (A [n_i, m], B [n_i, k]) pairs in one grouped split-K launch."""
+    lib = nat.load()
+    descs, outs = [], []
+    for A, B in pairs:
+        C = torch.empty((A.shape[1], B.shape[1]), dtype=torch.float32, device=device)
+        d = nat.GemmTnDesc()
+        d.A, d.lda = A.data_ptr(), A.stride(0)
+        d.B, d.ldb = B.data_ptr(), B.stride(0)
+        d.rows, d.M, d.N = A.shape[0], A.shape[1], B.shape[1]
+        d.C = C.data_ptr()
+        descs.append(d)
+        outs.append(C)
+    arr = (nat.GemmTnDesc * len(descs))(*descs)
+    wsb = lib.hgd_gemm_tn_workspace_size(arr, len(descs))
+    ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=device)
+    nat.check(lib.hgd_gemm_tn(arr, len(descs), ws.data_ptr(), wsb,
+                              torch.cuda.current_stream(device).cuda_stream), "hgd_gemm_tn")
+    return outs
+
+
+class _DenseTwoHopPair(torch.autograd.Function):
+    """HCCF's two HGNNLayer calls of a layer (HCCF.py:184-186, 201-211) on the halves of one
+    [U + I, d] table: ``cat([H_u·(H_uᵀ·X_u), H_i·(H_iᵀ·X_i)])`` with every product a grouped
+    launch over both halves (hgd_gemm_tn / hgd_gemm_rows) and the output written in place — no
+    split / cat of the table forward or backward."""
+
+    @staticmethod
+    def forward(ctx, H_u, H_i, X, nu):
+        H_u, H_i, X = H_u.contiguous(), H_i.contiguous(), X.contiguous()
+        dev = X.device
+        K, d = H_u.shape[1], X.shape[1]
+        X_u, X_i = X[:nu], X[nu:]
+        M_u, M_i = _gemm_tn_pair([(H_u, X_u), (H_i, X_i)], dev)
+        Y = torch.empty_like(X)
+        _gemm_rows([_rows_desc(H_u, M_u, d, 1, K, d, Y[:nu]),
+                    _rows_desc(H_i, M_i, d, 1, K, d, Y[nu:])], dev)
+        ctx.save_for_backward(H_u, H_i, X, M_u, M_i)
+        ctx.nu = nu
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        H_u, H_i, X, M_u, M_i = ctx.saved_tensors
+        nu = ctx.nu
+        dev = X.device
+        K, d = H_u.shape[1], X.shape[1]
+        dY = dY.contiguous()
+        dY_u, dY_i = dY[:nu], dY[nu:]
+        dM_u, dM_i = _gemm_tn_pair([(H_u, dY_u), (H_i, dY_i)], dev)
+        dX = None
+        if ctx.needs_input_grad[2]:
+            dX = torch.empty_like(X)
+            _gemm_rows([_rows_desc(H_u, dM_u, d, 1, K, d, dX[:nu]),
+                        _rows_desc(H_i, dM_i, d, 1, K, d, dX[nu:])], dev)
+        dH_u = dH_i = None
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+            # dH = dY·Mᵀ + X·dMᵀ: Bm[k][n] = M[n][k] (bsk 1, bsn d), the second accumulated
+            dH_u = torch.empty_like(H_u)
+            dH_i = torch.empty_like(H_i)
+            _gemm_rows([_rows_desc(dY_u, M_u, 1, d, d, K, dH_u),
+                        _rows_desc(dY_i, M_i, 1, d, d, K, dH_i)], dev)
+            _gemm_rows([_rows_desc(X[:nu], dM_u, 1, d, d, K, dH_u, accumulate=True),
+                        _rows_desc(X[nu:], dM_i, 1, d, d, K, dH_i, accumulate=True)], dev)
+        return dH_u, dH_i, dX, None
+
+
+def dense_two_hop_pair(H_u: torch.Tensor, H_i: torch.Tensor, X: torch.Tensor,
+                       nu: int) -> torch.Tensor:
+    """``torch.cat([H_u·(H_uᵀ·X[:nu]), H_i·(H_iᵀ·X[nu:])])`` (HCCF's user and item HGNNLayer of
+    one layer); falls back to two :func:`dense_two_hop` calls outside the kernels' shapes."""
+    if not (_mm_ok(H_u, X[:nu]) and _mm_ok(H_i, X[nu:]) and H_u.shape[1] == H_i.shape[1]):
+        return torch.cat([dense_two_hop(H_u, X[:nu]), dense_two_hop(H_i, X[nu:])], 0)
+    return _DenseTwoHopPair.apply(H_u, H_i, X, int(nu))

@@ -227,6 +227,51 @@ hgd_status hgd_linear_backward_weight(const float* dY, int64_t ldy, const float*
                                       float* db, void* workspace, size_t workspace_bytes,
                                       void* stream);
 
+/* Grouped forms of the skinny products above (HCCF's learned hypergraph HCCF.py:201-211 runs
+ * every product once for the users and once for the items): one launch for one or two
+ * independent products of equal shape class, which is what bounds these ~10 MB products.
+ *   hgd_gemm_rows: Y = relu?((A ⊙ [relu_mask > 0])·B + bias) (+ Y when accumulate), A [rows, K]
+ *     (16-byte aligned rows), B[k][n] = B[k·bsk + n·bsn]; K a multiple of 16 in [16, 128], N a
+ *     multiple of 16; the two products must share K, N and mask presence.
+ *   hgd_gemm_tn: C [M, N] = (A ⊙ [relu_mask > 0])ᵀ·B over `rows` rows (split-K, partials summed
+ *     in slice order: deterministic), colsum_A [M] = Σ_rows A ⊙ mask when non-NULL; the two
+ *     products must share M, N and mask presence. Workspace: hgd_gemm_tn_workspace_size. */
+typedef struct hgd_gemm_rows_desc {
+  const float* A;
+  int64_t lda;
+  const float* relu_mask; /* [rows, K] or NULL */
+  int64_t ldm;
+  const float* B;
+  int64_t bsk;
+  int64_t bsn;
+  const float* bias;      /* [N] or NULL */
+  int32_t relu;
+  int32_t accumulate;
+  float* Y;
+  int64_t ldy;
+  int64_t rows;
+  int32_t K;
+  int32_t N;
+} hgd_gemm_rows_desc;
+hgd_status hgd_gemm_rows(const hgd_gemm_rows_desc* descs, int32_t count, void* stream);
+
+typedef struct hgd_gemm_tn_desc {
+  const float* A;
+  int64_t lda;
+  const float* relu_mask; /* [rows, M] or NULL */
+  int64_t ldm;
+  const float* B;
+  int64_t ldb;
+  int64_t rows;
+  int32_t M;
+  int32_t N;
+  float* C;               /* [M, N] */
+  float* colsum_A;        /* [M] or NULL */
+} hgd_gemm_tn_desc;
+size_t hgd_gemm_tn_workspace_size(const hgd_gemm_tn_desc* descs, int32_t count);
+hgd_status hgd_gemm_tn(const hgd_gemm_tn_desc* descs, int32_t count, void* workspace,
+                       size_t workspace_bytes, void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * Fused InfoNCE, contrastLoss of util/loss_torch.py:103-110:
  *   p1 = normalize(E1[nodes] + 1e-8), p2 = normalize(E2[nodes] + 1e-8)   (eps 1e-12)

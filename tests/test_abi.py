@@ -62,14 +62,16 @@ def test_package_never_imports_oracle():
 
 
 def test_struct_layouts_match_header(tmp_path):
-    """The ctypes mirrors (SplitPlan, RowEpilogue) have the header's size and field offsets."""
+    """The ctypes mirrors (SplitPlan, RowEpilogue, IncidenceView, the grouped GEMM descriptors)
+    have the header's size and field offsets."""
     import shutil
     import subprocess
     from hypergraph_diffusion_for_recommendation_amd import _native
     if shutil.which("gcc") is None:
         pytest.skip("gcc not available")
     structs = {"hgd_split_plan": _native.SplitPlan, "hgd_row_epilogue": _native.RowEpilogue,
-               "hgd_incidence_view": _native.IncidenceView}
+               "hgd_incidence_view": _native.IncidenceView,
+               "hgd_gemm_rows_desc": _native.GemmRowsDesc, "hgd_gemm_tn_desc": _native.GemmTnDesc}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "hgd.h"', 'int main(void) {']
     for cname, py in structs.items():
         lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')

@@ -216,6 +216,37 @@ def test_hgnn_layer_dense_two_hop(dev, n, K, d):
         assert (err <= 1e-5 * m + 1e-300).all(), (what, float((err / m).max()))
 
 
+@pytest.mark.parametrize("nu,ni,K,d", [(31_668, 38_048, 32, 64), (300, 1000, 16, 32),
+                                        (5, 77, 48, 128)])
+def test_dense_two_hop_pair(dev, nu, ni, K, d):
+    """HCCF's user + item HGNNLayer pair of a layer as one grouped op
+    (functional.dense_two_hop_pair: hgd_gemm_tn / hgd_gemm_rows over both halves, output and
+    table gradient in place) vs float64: output, dX and both dH at the 1e-5·Σ|terms| bound."""
+    from hypergraph_diffusion_for_recommendation_amd.functional import dense_two_hop_pair
+    torch.manual_seed(nu + ni)
+    Hu = (torch.randn(nu, K) * 0.2).to(dev).requires_grad_(True)
+    Hi = (torch.randn(ni, K) * 0.2).to(dev).requires_grad_(True)
+    X = torch.randn(nu + ni, d).to(dev).requires_grad_(True)
+    dY = torch.randn(nu + ni, d).to(dev)
+    Y = dense_two_hop_pair(Hu, Hi, X, nu)
+    gHu, gHi, gX = torch.autograd.grad(Y, (Hu, Hi, X), dY)
+    adY = dY.double().cpu().abs()
+    for H, gH, sl in ((Hu, gHu, slice(0, nu)), (Hi, gHi, slice(nu, nu + ni))):
+        Hd = H.detach().double().cpu()
+        Xd = X.detach().double().cpu()[sl]
+        dYd = dY.double().cpu()[sl]
+        Yd = Hd @ (Hd.T @ Xd)
+        rX = Hd @ (Hd.T @ dYd)
+        rH = dYd @ (Hd.T @ Xd).T + Xd @ (Hd.T @ dYd).T
+        aH, aX, ad = Hd.abs(), Xd.abs(), adY[sl]
+        checks = ((Y.detach().double().cpu()[sl], Yd, aH @ (aH.T @ aX), "Y"),
+                  (gX.double().cpu()[sl], rX, aH @ (aH.T @ ad), "dX"),
+                  (gH.double().cpu(), rH, ad @ (aH.T @ aX).T + aX @ (aH.T @ ad).T, "dH"))
+        for got, ref, mag, what in checks:
+            err = (got - ref).abs()
+            assert (err <= 1e-5 * mag + 1e-300).all(), (what, float((err / mag).max()))
+
+
 def test_equivset_gnn_fresh_learned_hypergraph_each_call(dev):
     """HCCF_diffusion.py:205-206 feeds EquivSetGNN a NEW dense learned hypergraph
     (dropout(E·W) [n, K]) every call: each call must use that call's nonzero pattern, even when the
