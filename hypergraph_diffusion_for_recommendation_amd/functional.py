@@ -502,6 +502,92 @@ class _ContrastLoss(torch.autograd.Function):
         return dE1, dE2, None, None, None
 
 
+class _ContrastLossPair(torch.autograd.Function):
+    """The user and item contrastLoss terms of one HCCF layer on the halves of the [U + I, d]
+    tables (HCCF.py:65-66), with device counts: both InfoNCE forwards on row offsets of the
+    full tables, and in the backward ONE zeroed [U + I, d] gradient per table that both
+    scatters write into — instead of, per half, a zeroed half gradient, the slice backward's
+    zeroed full table plus copy, and the add joining the halves."""
+
+    @staticmethod
+    def forward(ctx, E1, E2, nu, nodes_u, count_u, nodes_i, count_i, temp: float):
+        lib = nat.load()
+        dev = E1.device
+        E1c, E2c = E1.contiguous(), E2.contiguous()
+        d = E1.shape[1]
+        N = E1.shape[0]
+        f = dict(dtype=torch.float32, device=dev)
+        loss2 = torch.empty(2, **f)
+        st = torch.cuda.current_stream(dev).cuda_stream
+        saved = []
+        for k, (r0, rows, nodes, count) in enumerate(((0, nu, nodes_u, count_u),
+                                                      (nu, N - nu, nodes_i, count_i))):
+            nodes = nodes.to(device=dev, dtype=torch.int64).contiguous()
+            B = nodes.numel()
+            P1, P2 = torch.empty((B, d), **f), torch.empty((B, d), **f)
+            inv1, inv2, pos, deno = (torch.empty(B, **f) for _ in range(4))
+            wsb = lib.hgd_infonce_workspace_size(B, d)
+            ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+            off = r0 * d * 4
+            nat.check(lib.hgd_infonce_forward_n(
+                E1c.data_ptr() + off, d, E2c.data_ptr() + off, d, rows, nodes.data_ptr(), B,
+                count.data_ptr(), d, float(temp), P1.data_ptr(), P2.data_ptr(), inv1.data_ptr(),
+                inv2.data_ptr(), pos.data_ptr(), deno.data_ptr(), loss2.data_ptr() + 4 * k,
+                ws.data_ptr(), wsb, st), "hgd_infonce_forward_n")
+            saved += [P1, P2, inv1, inv2, deno, nodes, count]
+        ctx.temp = float(temp)
+        ctx.nu, ctx.N, ctx.d = nu, N, d
+        ctx.save_for_backward(*saved)
+        return loss2[0] + loss2[1]
+
+    @staticmethod
+    def backward(ctx, g):
+        lib = nat.load()
+        saved = ctx.saved_tensors
+        dev = saved[0].device
+        nu, N, d = ctx.nu, ctx.N, ctx.d
+        g = g.to(dtype=torch.float32).reshape(1).contiguous()
+        f = dict(dtype=torch.float32, device=dev)
+        dE1 = torch.zeros((N, d), **f) if ctx.needs_input_grad[0] else None
+        dE2 = torch.zeros((N, d), **f) if ctx.needs_input_grad[1] else None
+        if dE1 is None and dE2 is None:
+            return (None,) * 8
+        st = torch.cuda.current_stream(dev).cuda_stream
+        for k, (r0, rows) in enumerate(((0, nu), (nu, N - nu))):
+            P1, P2, inv1, inv2, deno, nodes, count = saved[7 * k: 7 * k + 7]
+            B = P1.shape[0]
+            wsb = lib.hgd_infonce_workspace_size(B, d)
+            ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+            off = r0 * d * 4
+            nat.check(lib.hgd_infonce_backward_n(
+                P1.data_ptr(), P2.data_ptr(), inv1.data_ptr(), inv2.data_ptr(), deno.data_ptr(),
+                B, count.data_ptr(), d, ctx.temp, g.data_ptr(), nodes.data_ptr(), rows,
+                dE1.data_ptr() + off if dE1 is not None else None, d,
+                dE2.data_ptr() + off if dE2 is not None else None, d, ws.data_ptr(), wsb, st),
+                "hgd_infonce_backward_n")
+        return dE1, dE2, None, None, None, None, None, None
+
+
+def contrast_loss_pair(embeds1: torch.Tensor, embeds2: torch.Tensor, nu: int,
+                       nodes_u: torch.Tensor, nodes_i: torch.Tensor, temp: float,
+                       count_u: Optional[torch.Tensor] = None,
+                       count_i: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``contrastLoss(e1[:nu], e2[:nu], nodes_u, temp) + contrastLoss(e1[nu:], e2[nu:], nodes_i,
+    temp)`` (HCCF.py:65-66, util/loss_torch.py:103-110) as one op when both node lists carry
+    device counts (:func:`unique_long_n`); otherwise the two :func:`contrast_loss` calls."""
+    d = embeds1.shape[-1]
+    ok = (count_u is not None and count_i is not None and embeds1.dim() == 2
+          and embeds2.shape == embeds1.shape and embeds1.is_cuda
+          and embeds1.dtype == torch.float32 and embeds2.dtype == torch.float32
+          and d % 16 == 0 and 16 <= d <= 256 and 0 < nu < embeds1.shape[0]
+          and nodes_u.numel() > 0 and nodes_i.numel() > 0)
+    if not ok:
+        return (contrast_loss(embeds1[:nu], embeds2[:nu], nodes_u, temp, count_u)
+                + contrast_loss(embeds1[nu:], embeds2[nu:], nodes_i, temp, count_i))
+    return _ContrastLossPair.apply(embeds1, embeds2, int(nu), nodes_u, count_u, nodes_i,
+                                   count_i, float(temp))
+
+
 def contrast_loss(embeds1: torch.Tensor, embeds2: torch.Tensor, nodes: torch.Tensor,
                   temp: float, count: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``contrastLoss(embeds1, embeds2, nodes, temp)`` of util/loss_torch.py:103-110 (InfoNCE over

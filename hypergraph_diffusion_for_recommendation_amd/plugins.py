@@ -45,7 +45,7 @@ from torch.optim.lr_scheduler import ReduceLROnPlateau
 
 from .encoders import (HCCFDiffusionEncoder, HCCFEncoder, LocalAwareEncoder,
                        LocalAwareEncoderHD3, sparse_tensor_of)
-from .functional import contrast_loss, unique_long, unique_long_n
+from .functional import contrast_loss, contrast_loss_pair, unique_long, unique_long_n
 from .layers import HGCNConv, SpAdjDropEdge
 from .sampler import next_batch_pairwise
 from .selfrec import GraphRecommender, early_stopping
@@ -123,8 +123,8 @@ class HCCF(GraphRecommender):
         for i in range(self.nLayers):
             embeds1 = gcnEmbedsLst[i].detach()
             embeds2 = hyperEmbedsLst[i]
-            sslLoss += contrast_loss(embeds1[:nu], embeds2[:nu], u_nodes, self.temp, u_cnt) \
-                + contrast_loss(embeds1[nu:], embeds2[nu:], p_nodes, self.temp, p_cnt)
+            sslLoss += contrast_loss_pair(embeds1, embeds2, nu, u_nodes, p_nodes, self.temp,
+                                          u_cnt, p_cnt)
         sslLoss *= self.ss_rate
         return bprLoss, sslLoss
 

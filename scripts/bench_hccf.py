@@ -42,6 +42,7 @@ def main():
     import refops as R
     from hypergraph_diffusion_for_recommendation_amd.encoders import HCCFEncoder
     from hypergraph_diffusion_for_recommendation_amd.functional import (contrast_loss,
+                                                                         contrast_loss_pair,
                                                                          unique_long,
                                                                          unique_long_n)
     from hypergraph_diffusion_for_recommendation_amd.graphs import CapturedStep
@@ -78,9 +79,9 @@ def main():
             for layer in range(args.layers):
                 e1, e2 = gcn[layer].detach(), hyp[layer]
                 nu_nodes, np_nodes = un if hoist else (unique(anc), unique(pos))
-                if counted:  # (nodes, device count) pairs
-                    ssl = ssl + loss_fn(e1[:nu], e2[:nu], nu_nodes[0], temp, nu_nodes[1]) \
-                        + loss_fn(e1[nu:], e2[nu:], np_nodes[0], temp, np_nodes[1])
+                if counted:  # (nodes, device count) pairs: both halves in one op
+                    ssl = ssl + contrast_loss_pair(e1, e2, nu, nu_nodes[0], np_nodes[0], temp,
+                                                   nu_nodes[1], np_nodes[1])
                 else:
                     ssl = ssl + loss_fn(e1[:nu], e2[:nu], nu_nodes, temp) \
                         + loss_fn(e1[nu:], e2[nu:], np_nodes, temp)

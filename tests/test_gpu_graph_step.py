@@ -162,8 +162,31 @@ def _hccf(dev, drop_rate, seed=3):
     return enc, U, I
 
 
-def _step_fn(enc, opt, U, temp=1.0, cl=0.01):
+def test_contrast_loss_pair_equals_two_calls(dev):
+    """contrast_loss_pair (one op over both halves of the tables, one zeroed gradient table)
+    against the two contrast_loss calls of HCCF.py:65-66 it replaces: the same loss bitwise and
+    the same table gradients (each row is written by one half's scatter only)."""
     from hypergraph_diffusion_for_recommendation_amd.functional import (contrast_loss,
+                                                                         contrast_loss_pair,
+                                                                         unique_long_n)
+    g = torch.Generator(device=dev).manual_seed(11)
+    U, N, d = 700, 1900, 64
+    E1 = torch.randn(N, d, device=dev, generator=g)
+    E2 = torch.randn(N, d, device=dev, generator=g)
+    un, uc = unique_long_n(torch.randint(-40, 400, (300,), device=dev, generator=g))
+    pn, pc = unique_long_n(torch.randint(0, 1200, (500,), device=dev, generator=g))
+    a = E2.clone().requires_grad_(True)
+    la = contrast_loss_pair(E1, a, U, un, pn, 0.3, uc, pc)
+    la.backward()
+    b = E2.clone().requires_grad_(True)
+    lb = contrast_loss(E1[:U], b[:U], un, 0.3, uc) + contrast_loss(E1[U:], b[U:], pn, 0.3, pc)
+    lb.backward()
+    assert torch.equal(la, lb)
+    assert torch.equal(a.grad, b.grad)
+
+
+def _step_fn(enc, opt, U, temp=1.0, cl=0.01):
+    from hypergraph_diffusion_for_recommendation_amd.functional import (contrast_loss_pair,
                                                                          unique_long_n)
     from hypergraph_diffusion_for_recommendation_amd.plugins import bpr_loss
 
@@ -174,8 +197,7 @@ def _step_fn(enc, opt, U, temp=1.0, cl=0.01):
         ssl = 0
         for layer in range(enc.n_layers):
             e1, e2 = gcn[layer].detach(), hyp[layer]
-            ssl = ssl + contrast_loss(e1[:U], e2[:U], un, temp, uc) + \
-                contrast_loss(e1[U:], e2[U:], pn, temp, pc)
+            ssl = ssl + contrast_loss_pair(e1, e2, U, un, pn, temp, uc, pc)
         loss = bpr_loss(anc, pos, neg) + ssl * cl
         opt.zero_grad()
         loss.backward()
