@@ -187,6 +187,8 @@ _SIGNATURES = {
                                        c_void_p, c_i32, c_f32, c_void_p, c_void_p, c_i64,
                                        c_void_p, c_i64, c_void_p, c_i64, c_void_p, c_size,
                                        c_void_p]),
+    "hgd_bernoulli_mask_dev_pair": (c_i32, [c_void_p, c_void_p, c_i64, c_f32, c_void_p, c_void_p,
+                                            c_void_p]),
     "hgd_bernoulli_mask_dev": (c_i32, [c_void_p, c_i64, c_f32, c_void_p, c_void_p]),
     "hgd_dropedge_fill_tail": (c_i32, [c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_void_p,
                                        c_void_p]),

@@ -417,6 +417,25 @@ __global__ void k_bernoulli_mask_dev(const uint64_t* __restrict__ seed_ptr, int6
   mask[i] = floorf(u + keep) != 0.f ? 1 : 0;
 }
 
+// Both orientations' masks of one device draw: mask[j] = bern(j) in CSR order and
+// mask_t[j] = bern(perm_t[j]) in CSC order — the CSC mask without a random byte gather.
+__device__ __forceinline__ uint8_t bern_bit(uint64_t seed, uint64_t i, float keep) {
+  const uint64_t h = splitmix64(seed ^ splitmix64(i));
+  const float u = static_cast<float>(h >> 40) * (1.0f / 16777216.0f);
+  return floorf(u + keep) != 0.f ? 1 : 0;
+}
+
+__global__ void k_bernoulli_mask_dev_pair(const uint64_t* __restrict__ seed_ptr,
+                                          const int32_t* __restrict__ perm_t, int64_t n,
+                                          float keep, uint8_t* __restrict__ mask,
+                                          uint8_t* __restrict__ mask_t) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t seed = seed_ptr[0];
+  mask[i] = bern_bit(seed, static_cast<uint64_t>(i), keep);
+  mask_t[i] = bern_bit(seed, static_cast<uint64_t>(perm_t[i]), keep);
+}
+
 // Zeroes entries [*count, capacity) of a capacity-sized dropped structure (valid index 0,
 // weight 0), so that nothing reading the arrays linearly meets uninitialised indices.
 __global__ void k_fill_tail(const int64_t* __restrict__ count, int64_t capacity,
@@ -745,6 +764,18 @@ extern "C" hgd_status hgd_bernoulli_mask_dev(const uint64_t* seed, int64_t n, fl
   hipLaunchKernelGGL(k_bernoulli_mask_dev, dim3(grid_for(n)), dim3(kBlock), 0,
                      as_stream(stream), seed, n, keep, mask);
   return check_launch("hgd_bernoulli_mask_dev");
+}
+
+extern "C" hgd_status hgd_bernoulli_mask_dev_pair(const uint64_t* seed, const int32_t* perm_t,
+                                                  int64_t n, float keep, uint8_t* mask,
+                                                  uint8_t* mask_t, void* stream) {
+  clear_error();
+  HGD_REQUIRE(n >= 0 && seed && ((mask && mask_t && perm_t) || n == 0),
+              "hgd_bernoulli_mask_dev_pair: bad arguments");
+  if (n == 0) return HGD_OK;
+  hipLaunchKernelGGL(k_bernoulli_mask_dev_pair, dim3(grid_for(n)), dim3(kBlock), 0,
+                     as_stream(stream), seed, perm_t, n, keep, mask, mask_t);
+  return check_launch("hgd_bernoulli_mask_dev_pair");
 }
 
 extern "C" hgd_status hgd_dropedge_fill_tail(const int64_t* count, int64_t capacity,

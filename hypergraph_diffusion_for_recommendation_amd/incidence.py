@@ -420,14 +420,16 @@ class Incidence:
         out.perm_t = None  # a dropped structure is not dropped again (the reference drops the base)
         return out
 
-    def masked(self, mask: torch.Tensor, keep: float) -> "MaskedIncidence":
+    def masked(self, mask: torch.Tensor, keep: float,
+               mask_t: Optional[torch.Tensor] = None) -> "MaskedIncidence":
         """SpAdjDropEdge's output (HCCF.py:217-226) as a VIEW of this incidence: no compaction
         at all. The hops run over this structure and skip the dropped edges
         (hgd_spmm_masked: weight val[e] / keep, kept edges in edge order — the sums of the
         compacted matrix of :meth:`drop`, bitwise when no row is split). The CSC-order mask is
         one byte gather through ``perm_t``; nothing is read back to the host, so a step using
         it can be captured in a HIP graph. For the plain hops (GCNLayer, HGCNConv without
-        degree scales); degree scales of the dropped matrix need :meth:`drop`."""
+        degree scales); degree scales of the dropped matrix need :meth:`drop`. ``mask_t``: the
+        same mask already in CSC order (hgd_bernoulli_mask_dev_pair draws both)."""
         if self.perm_t is None:
             raise RuntimeError("Incidence.masked: needs the CSC→CSR permutation (a structure "
                                "built from a COO)")
@@ -437,10 +439,16 @@ class Incidence:
             raise ValueError("Incidence.masked: mask size mismatch")
         if not keep > 0.0:
             raise ValueError("Incidence.masked: keep must be > 0")
-        m_t = torch.empty_like(m)
-        if self.nnz:
-            nat.check(nat.load().hgd_gather_u8(m.data_ptr(), self.perm_t.data_ptr(), self.nnz,
-                                               m_t.data_ptr(), _stream(dev)), "hgd_gather_u8")
+        if mask_t is not None:
+            m_t = mask_t.to(device=dev, dtype=torch.uint8).contiguous()
+            if m_t.numel() != self.nnz:
+                raise ValueError("Incidence.masked: mask_t size mismatch")
+        else:
+            m_t = torch.empty_like(m)
+            if self.nnz:
+                nat.check(nat.load().hgd_gather_u8(m.data_ptr(), self.perm_t.data_ptr(),
+                                                   self.nnz, m_t.data_ptr(), _stream(dev)),
+                          "hgd_gather_u8")
         csr = copy.copy(self.csr)
         csc = copy.copy(self.csc)
         csr.mask, csr.keep = m, float(keep)

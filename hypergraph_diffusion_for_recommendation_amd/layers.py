@@ -239,12 +239,14 @@ class SpAdjDropEdge(nn.Module):
             # on the device afterwards
             self._seed = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).to(dev)
         mask = torch.empty(parent.nnz, dtype=torch.uint8, device=dev)
+        mask_t = torch.empty_like(mask)
         if parent.nnz:
-            nat.check(nat.load().hgd_bernoulli_mask_dev(
-                self._seed.data_ptr(), parent.nnz, keep, mask.data_ptr(),
-                torch.cuda.current_stream(dev).cuda_stream), "hgd_bernoulli_mask_dev")
+            nat.check(nat.load().hgd_bernoulli_mask_dev_pair(
+                self._seed.data_ptr(), parent.perm_t.data_ptr(), parent.nnz, keep,
+                mask.data_ptr(), mask_t.data_ptr(), torch.cuda.current_stream(dev).cuda_stream),
+                "hgd_bernoulli_mask_dev_pair")
         self._seed.add_(1)
-        return parent.masked(mask, keep)
+        return parent.masked(mask, keep, mask_t)
 
 
 class Linear(nn.Linear):

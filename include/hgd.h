@@ -415,6 +415,11 @@ hgd_status hgd_bernoulli_mask(uint64_t seed, int64_t n, float keep, uint8_t* mas
  * advances the counter on the device, so every graph replay draws a fresh mask. */
 hgd_status hgd_bernoulli_mask_dev(const uint64_t* seed, int64_t n, float keep, uint8_t* mask,
                                   void* stream);
+/* The same draw for both orientations of a structure (hgd_spmm_masked's forward and backward
+ * hops): mask[i] as hgd_bernoulli_mask_dev, mask_t[j] = mask[perm_t[j]] computed from the hash
+ * of perm_t[j] (perm_t: CSC position → CSR position) instead of a byte gather. */
+hgd_status hgd_bernoulli_mask_dev_pair(const uint64_t* seed, const int32_t* perm_t, int64_t n,
+                                       float keep, uint8_t* mask, uint8_t* mask_t, void* stream);
 /* Zeroes entries [*count, capacity) of the capacity-sized outputs of hgd_dropedge_structure
  * (count = rowptr_out + n_rows, on the device): a dropped structure whose kept count is never read
  * back keeps full-size arrays with a defined tail (index 0, weight 0). Null arrays are skipped. */

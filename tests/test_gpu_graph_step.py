@@ -65,6 +65,29 @@ def test_device_seed_mask_and_capacity_drop(dev):
     assert torch.equal(torch.autograd.grad(y1, X, g)[0], torch.autograd.grad(y2, X, g)[0])
 
 
+def test_paired_device_mask_is_the_csc_permutation(dev):
+    """hgd_bernoulli_mask_dev_pair: the CSR-order mask equals hgd_bernoulli_mask_dev's and the
+    CSC-order one equals it gathered through perm_t, bit for bit (the capture-safe drop's two
+    masks from one draw)."""
+    from hypergraph_diffusion_for_recommendation_amd import _native as nat
+    from hypergraph_diffusion_for_recommendation_amd.encoders import sparse_tensor_of
+    A = _graph(800, 1100, 15_000, seed=9)
+    parent = sparse_tensor_of(A, dev)._hgd_incidence
+    seed = torch.tensor([987654321], dtype=torch.int64, device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+    m = torch.empty(parent.nnz, dtype=torch.uint8, device=dev)
+    mt = torch.empty_like(m)
+    ref = torch.empty_like(m)
+    lib = nat.load()
+    nat.check(lib.hgd_bernoulli_mask_dev_pair(seed.data_ptr(), parent.perm_t.data_ptr(),
+                                              parent.nnz, 0.6, m.data_ptr(), mt.data_ptr(), st),
+              "pair")
+    nat.check(lib.hgd_bernoulli_mask_dev(seed.data_ptr(), parent.nnz, 0.6, ref.data_ptr(), st),
+              "single")
+    assert torch.equal(m, ref)
+    assert torch.equal(mt, ref[parent.perm_t.long()])
+
+
 @pytest.mark.parametrize("d", [64, 32, 7, 256])
 def test_masked_view_hops_equal_compacted(dev, d):
     """Incidence.masked (hgd_spmm_masked: the dropped matrix as a view of its parent) against
