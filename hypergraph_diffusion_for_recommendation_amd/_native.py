@@ -65,6 +65,10 @@ class RowEpilogue(ctypes.Structure):
         ("act_out", c_void_p),
         ("ld_act", c_i64),
         ("stats", c_void_p),
+        ("sum_res", c_void_p),
+        ("ld_sum_res", c_i64),
+        ("sum_out", c_void_p),
+        ("ld_sum_out", c_i64),
     ]
 
 
@@ -149,6 +153,10 @@ _SIGNATURES = {
                                 c_i64, c_i64, c_i64, c_void_p, c_i64, c_void_p, c_i64, c_i32,
                                 c_i32, c_f32, ctypes.POINTER(SplitPlan), c_void_p, c_size,
                                 c_void_p]),
+    "hgd_spmm_masked_fused": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p, c_f32, c_void_p,
+                                      c_i64, c_i64, c_i64, c_i64, c_void_p, c_i64, c_void_p,
+                                      c_i64, c_i32, ctypes.POINTER(RowEpilogue),
+                                      ctypes.POINTER(SplitPlan), c_void_p, c_size, c_void_p]),
     "hgd_spmm_fused": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_i64, c_i64,
                                c_i64, c_void_p, c_i64, c_void_p, c_i64, c_i32,
                                ctypes.POINTER(RowEpilogue), ctypes.POINTER(SplitPlan), c_void_p,
@@ -248,6 +256,7 @@ _SIGNATURES = {
     "hgd_epilogue_apply":(c_i32, [c_void_p, c_i64, c_i32, c_f32, c_void_p, c_void_p]),
     "hgd_epilogue_backward": (c_i32, [c_void_p, c_void_p, c_i64, c_i32, c_f32, c_void_p,
                                       c_void_p]),
+    "hgd_sum_slices": (c_i32, [c_void_p, c_i64, c_i64, c_i64, c_void_p, c_void_p]),
     "hgd_unique_workspace_size": (c_size, [c_i64]),
     "hgd_unique_i64": (c_i32, [c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_size, c_void_p]),
     "hgd_unique_trunc_f32": (c_i32, [c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_size,

@@ -4,6 +4,8 @@
 //             fused into hgd_spmm's store (negative slope).
 //   backward: dZ = dY * (ref > 0 ? 1 : slope) — torch's leaky_relu_backward on the saved
 //             pre-activation, or on the output when slope >= 0 (same sign).
+//   sum_slices: the layer sum of HCCF's encoder, sum(hidden) (model/graph/HCCF.py:188), over
+//             the hidden tables stored as slices of one buffer — one pass instead of L adds.
 #include "hgd_internal.h"
 
 namespace hgd {
@@ -51,6 +53,30 @@ __global__ void k_epi_backward(const float* __restrict__ ref, const float* __res
   }
 }
 
+// out[i] = ((P_0[i] + P_1[i]) + P_2[i]) + … — Python's sum() order over the slices (its
+// leading 0 + P_0 is P_0 exactly), so the result is bit-identical to the chain of adds.
+__global__ void k_sum_slices(const float* __restrict__ P, int64_t S, int64_t stride, int64_t n,
+                             float* __restrict__ out) {
+  const int64_t i4 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) * 4;
+  if (i4 + 3 < n) {
+    float4 acc = *reinterpret_cast<const float4*>(P + i4);
+    for (int64_t s = 1; s < S; ++s) {
+      const float4 v = *reinterpret_cast<const float4*>(P + s * stride + i4);
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
+    }
+    *reinterpret_cast<float4*>(out + i4) = acc;
+  } else {
+    for (int64_t i = i4; i < n; ++i) {
+      float acc = P[i];
+      for (int64_t s = 1; s < S; ++s) acc += P[s * stride + i];
+      out[i] = acc;
+    }
+  }
+}
+
 inline bool aligned16(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
 
 }  // namespace hgd
@@ -79,4 +105,16 @@ extern "C" hgd_status hgd_epilogue_backward(const float* ref, const float* dy, i
   hipLaunchKernelGGL(k_epi_backward, dim3(grid_for((n + 3) / 4)), dim3(kBlock), 0,
                      as_stream(stream), ref, dy, n, epilogue, slope, dz);
   return check_launch("hgd_epilogue_backward");
+}
+
+extern "C" hgd_status hgd_sum_slices(const float* P, int64_t n_slices, int64_t slice_stride,
+                                     int64_t n, float* out, void* stream) {
+  clear_error();
+  HGD_REQUIRE(n >= 0 && n_slices >= 1 && slice_stride >= n, "hgd_sum_slices: bad sizes");
+  if (n == 0) return HGD_OK;
+  HGD_REQUIRE(P && out && aligned16(P) && aligned16(out) && slice_stride % 4 == 0,
+              "hgd_sum_slices: null/unaligned (16-byte slices needed)");
+  hipLaunchKernelGGL(k_sum_slices, dim3(grid_for((n + 3) / 4)), dim3(kBlock), 0,
+                     as_stream(stream), P, n_slices, slice_stride, n, out);
+  return check_launch("hgd_sum_slices");
 }

@@ -194,6 +194,13 @@ __global__ __launch_bounds__(kBlock) void k_rowepi_fwd(RowEpiFwd p) {
       for (int i = 0; i < VEC; ++i) v[i] = fmaf(e.res2_scale, rv[i], v[i]);
     }
     store_vec<VEC>(p.Y + r * p.ldy + coff, v);
+    if (e.sum_out) {
+      float rv[VEC];
+      load_vec<VEC>(e.sum_res + r * e.ld_sum_res + coff, rv);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) rv[i] += v[i];
+      store_vec<VEC>(e.sum_out + r * e.ld_sum_out + coff, rv);
+    }
   }
 }
 
@@ -336,8 +343,11 @@ extern "C" hgd_status hgd_row_epilogue_forward(const float* Z, int64_t ldz, int6
               "hgd_row_epilogue_forward: layer_norm 0/1");
   HGD_REQUIRE(ldz >= d && ldy >= d, "hgd_row_epilogue_forward: ldz/ldy < d");
   HGD_REQUIRE((!epi->res1 || epi->ld_res1 >= d) && (!epi->res2 || epi->ld_res2 >= d) &&
-                  (!epi->act_out || epi->ld_act >= d),
+                  (!epi->act_out || epi->ld_act >= d) &&
+                  (!epi->sum_out || (epi->ld_sum_out >= d && epi->ld_sum_res >= d)),
               "hgd_row_epilogue_forward: leading dimension < d");
+  HGD_REQUIRE((epi->sum_out == nullptr) == (epi->sum_res == nullptr),
+              "hgd_row_epilogue_forward: sum_out and sum_res go together");
   if (n_rows == 0) return HGD_OK;
   HGD_REQUIRE(Z && Y, "hgd_row_epilogue_forward: null Z/Y");
   auto al16 = [](const void* p, int64_t ld) {
@@ -345,7 +355,8 @@ extern "C" hgd_status hgd_row_epilogue_forward(const float* Z, int64_t ldz, int6
   };
   const bool aligned = d % 4 == 0 && al16(Z, ldz) && al16(Y, ldy) &&
                        al16(epi->res1, epi->ld_res1) && al16(epi->res2, epi->ld_res2) &&
-                       al16(epi->act_out, epi->ld_act);
+                       al16(epi->act_out, epi->ld_act) && al16(epi->sum_out, epi->ld_sum_out) &&
+                       al16(epi->sum_res, epi->ld_sum_res);
   const int G = aligned ? (d / 4 >= 64 ? 64 : next_pow2(d / 4)) : (d >= 64 ? 64 : next_pow2(d));
   const int span = aligned ? 4 * G : G;
   if (span < d)

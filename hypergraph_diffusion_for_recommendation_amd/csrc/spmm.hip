@@ -117,6 +117,16 @@ __device__ __forceinline__ void finish_row(const SpmmArgs& a, int64_t r, float s
     }
   }
   if (col_ok) store_vec<VEC, NT_STORE>(a.Y + r * a.ldy + coff, acc);
+  if constexpr (EX) {
+    const hgd_row_epilogue& e = a.ex;
+    if (e.sum_out && col_ok) {
+      float rv[VEC];
+      load_vec<VEC>(e.sum_res + r * e.ld_sum_res + coff, rv);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) rv[i] = acc[i] + rv[i];
+      store_vec<VEC>(e.sum_out + r * e.ld_sum_out + coff, rv);
+    }
+  }
 }
 
 // Lane l's share of a batch of G column indices (and weights) starting at nonzero eb; with MASK
@@ -437,13 +447,13 @@ int g_pass_cols = 0;
 
 template <int G, int VEC, int U, int POL, bool EX = false>
 void launch_kernel(const SpmmArgs& a, bool has_val, bool seg, int64_t blocks, hipStream_t st) {
-  if constexpr (!EX && POL == kDefaultPolicy && U == 8) {
+  if constexpr (POL == kDefaultPolicy && U == 8) {
     if (a.mask) {  // masked (edge-dropped view) hop: the row kernel only
       if (has_val)
-        hipLaunchKernelGGL((spmm_kernel<G, VEC, U, true, POL, false, true>), dim3(blocks),
+        hipLaunchKernelGGL((spmm_kernel<G, VEC, U, true, POL, EX, true>), dim3(blocks),
                            dim3(kBlock), 0, st, a);
       else
-        hipLaunchKernelGGL((spmm_kernel<G, VEC, U, false, POL, false, true>), dim3(blocks),
+        hipLaunchKernelGGL((spmm_kernel<G, VEC, U, false, POL, EX, true>), dim3(blocks),
                            dim3(kBlock), 0, st, a);
       return;
     }
@@ -469,8 +479,8 @@ void launch_kernel(const SpmmArgs& a, bool has_val, bool seg, int64_t blocks, hi
 
 template <int G, int VEC, bool EX>
 void launch_tuned(const SpmmArgs& a, bool has_val, bool seg, int64_t blocks, hipStream_t st) {
-  if (!EX && a.mask) {
-    launch_kernel<G, VEC, 8, kDefaultPolicy>(a, has_val, false, blocks, st);
+  if (a.mask) {
+    launch_kernel<G, VEC, 8, kDefaultPolicy, EX>(a, has_val, false, blocks, st);
   } else if constexpr (EX) {
     launch_kernel<G, VEC, 8, kDefaultPolicy, true>(a, has_val, seg, blocks, st);
   } else if constexpr (G == 16 && VEC == 4) {
@@ -567,6 +577,10 @@ hgd_status spmm_impl(const int64_t* rowptr, const int32_t* col, const float* val
     HGD_REQUIRE(!ex->res1 || ex->ld_res1 >= d, "%s: ld_res1 < d", fn);
     HGD_REQUIRE(!ex->res2 || ex->ld_res2 >= d, "%s: ld_res2 < d", fn);
     HGD_REQUIRE(!ex->act_out || ex->ld_act >= d, "%s: ld_act < d", fn);
+    HGD_REQUIRE((ex->sum_out == nullptr) == (ex->sum_res == nullptr),
+                "%s: sum_out and sum_res go together", fn);
+    HGD_REQUIRE(!ex->sum_out || (ex->ld_sum_out >= d && ex->ld_sum_res >= d),
+                "%s: ld_sum_out / ld_sum_res < d", fn);
   }
   if (row_end == row_begin) return HGD_OK;
   // col / X may be NULL for a structure without nonzeros (never dereferenced then).
@@ -617,7 +631,8 @@ hgd_status spmm_impl(const int64_t* rowptr, const int32_t* col, const float* val
   bool aligned = al16(X, ldx) && al16(Y, ldy) && (d % 4 == 0);
   if (ex)
     aligned = aligned && al16(ex->res1, ex->ld_res1) && al16(ex->res2, ex->ld_res2) &&
-              al16(ex->act_out, ex->ld_act);
+              al16(ex->act_out, ex->ld_act) && al16(ex->sum_out, ex->ld_sum_out) &&
+              al16(ex->sum_res, ex->ld_sum_res);
   if (ex && ex->layer_norm && (aligned ? d > 256 : d > 64))
     return fail(HGD_ERR_UNSUPPORTED,
                 "%s: layer_norm needs d <= 256 (16-byte aligned rows) or d <= 64 (got d=%d%s)",
@@ -688,6 +703,24 @@ extern "C" hgd_status hgd_spmm_masked(const int64_t* rowptr, const int32_t* col,
   return hgd::spmm_impl(rowptr, col, val, row_scale, n_rows, n_src_rows, row_begin, row_end, X,
                         ldx, Y, ldy, d, epilogue, slope, nullptr, mask, keep, plan, workspace,
                         workspace_bytes, stream, "hgd_spmm_masked");
+}
+
+extern "C" hgd_status hgd_spmm_masked_fused(const int64_t* rowptr, const int32_t* col,
+                                            const float* val, const uint8_t* mask, float keep,
+                                            const float* row_scale, int64_t n_rows,
+                                            int64_t n_src_rows, int64_t row_begin,
+                                            int64_t row_end, const float* X, int64_t ldx,
+                                            float* Y, int64_t ldy, int32_t d,
+                                            const hgd_row_epilogue* epi,
+                                            const hgd_split_plan* plan, void* workspace,
+                                            size_t workspace_bytes, void* stream) {
+  hgd::clear_error();
+  HGD_REQUIRE(epi != nullptr, "hgd_spmm_masked_fused: null epilogue descriptor");
+  HGD_REQUIRE(keep > 0.f, "hgd_spmm_masked_fused: keep must be > 0 (got %g)", (double)keep);
+  HGD_REQUIRE(mask || row_end == row_begin, "hgd_spmm_masked_fused: null mask");
+  return hgd::spmm_impl(rowptr, col, val, row_scale, n_rows, n_src_rows, row_begin, row_end, X,
+                        ldx, Y, ldy, d, epi->act, epi->slope, epi, mask, keep, plan, workspace,
+                        workspace_bytes, stream, "hgd_spmm_masked_fused");
 }
 
 extern "C" hgd_status hgd_set_tuning(int32_t key, int32_t value) {

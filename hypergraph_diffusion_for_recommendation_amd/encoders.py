@@ -24,7 +24,8 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from .functional import dense_two_hop_pair, linear, two_hop_fused
+from .functional import (dense_two_hop_pair, hccf_layers, hccf_layers_supported, linear,
+                         two_hop_fused)
 from .incidence import Incidence, incidence_of
 from .layers import EquivSetGNN, GCNLayer, HGCNConv, HGNNLayer, LayerNorm, SpAdjDropEdge
 
@@ -57,6 +58,8 @@ class HCCFEncoder(nn.Module):
         self.embedding_dict = self._init_model()
         self.drop_out = nn.Dropout(self.drop_rate)
         self.edgeDropper = SpAdjDropEdge()
+        # False: the per-layer module graph below (GCNLayer / dense_two_hop_pair and torch adds)
+        self.fused_layers = True
 
     def _parse_config(self, config):
         self.lRate = float(config['lrate'])
@@ -83,12 +86,26 @@ class HCCFEncoder(nn.Module):
 
     def forward(self, keep_rate=0.5):
         nu = self.data.n_users
-        embeddings = torch.cat([self.embedding_dict['user_emb'], self.embedding_dict['item_emb']], 0)
-        hidden = [embeddings]
-        gcn_hidden, hgnn_hidden = [], []
         # E·W [n, d]·[d, K] on the skinny MFMA Linear (functional.linear takes W as [out, in])
         hyper_uu = linear(self.embedding_dict['user_emb'], self.embedding_dict['user_w'].t())
         hyper_ii = linear(self.embedding_dict['item_emb'], self.embedding_dict['item_w'].t())
+        if self.fused_layers and hccf_layers_supported(self.embedding_dict['user_emb'],
+                                                       self.embedding_dict['item_emb'], hyper_uu):
+            # the whole loop as one op (functional.hccf_layers): the layer sum, the layer adds
+            # and autograd's accumulations ride in the hop / product stores. Same draws in the
+            # same order as the loop below (drop-edge, then the two dropouts, per layer).
+            adjs, hus, his = [], [], []
+            for _ in range(self.n_layers):
+                adjs.append(incidence_of(self.edgeDropper(self.sparse_norm_adj, keep_rate)))
+                hus.append(self.drop_out(hyper_uu))
+                his.append(self.drop_out(hyper_ii))
+            embeddings, gcn_hidden, hgnn_hidden = hccf_layers(
+                adjs, self.embedding_dict['user_emb'], self.embedding_dict['item_emb'], hus, his)
+            user_emb, item_emb = torch.split(embeddings, [nu, embeddings.shape[0] - nu])
+            return user_emb, item_emb, gcn_hidden, hgnn_hidden
+        embeddings = torch.cat([self.embedding_dict['user_emb'], self.embedding_dict['item_emb']], 0)
+        hidden = [embeddings]
+        gcn_hidden, hgnn_hidden = [], []
         for _ in range(self.n_layers):
             gcn_emb = self.gcnlayer(self.edgeDropper(self.sparse_norm_adj, keep_rate), hidden[-1])
             # the user and item HGNNLayer calls (hgnnlayer(·, hidden[-1][:nu]) and [nu:]) and

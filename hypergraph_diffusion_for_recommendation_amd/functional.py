@@ -862,3 +862,150 @@ def dense_two_hop_pair(H_u: torch.Tensor, H_i: torch.Tensor, X: torch.Tensor,
     if not (_mm_ok(H_u, X[:nu]) and _mm_ok(H_i, X[nu:]) and H_u.shape[1] == H_i.shape[1]):
         return torch.cat([dense_two_hop(H_u, X[:nu]), dense_two_hop(H_i, X[nu:])], 0)
     return _DenseTwoHopPair.apply(H_u, H_i, X, int(nu))
+
+
+def _res_epilogue(res: Optional[torch.Tensor], act_out: Optional[torch.Tensor] = None,
+                  res2: Optional[torch.Tensor] = None, sum_res: Optional[torch.Tensor] = None,
+                  sum_out: Optional[torch.Tensor] = None):
+    """hgd_row_epilogue of a plain hop whose store adds ``res`` and ``res2`` (either may be the
+    output itself), keeps the bare hop in ``act_out`` and writes ``sum_out = Y + sum_res``."""
+    def ld(t):
+        return 0 if t is None else t.stride(0)
+    return nat.RowEpilogue(
+        act=nat.EPI_NONE, slope=0.0, layer_norm=0, ln_eps=0.0, ln_gamma=None, ln_beta=None,
+        out_scale=1.0, res1=nat.ptr(res), ld_res1=ld(res), res1_scale=1.0,
+        res2=nat.ptr(res2), ld_res2=ld(res2), res2_scale=1.0, act_out=nat.ptr(act_out),
+        ld_act=ld(act_out), stats=None, sum_res=nat.ptr(sum_res), ld_sum_res=ld(sum_res),
+        sum_out=nat.ptr(sum_out), ld_sum_out=ld(sum_out))
+
+
+class _HCCFLayers(torch.autograd.Function):
+    """HCCF's layer loop (model/graph/HCCF.py:173-191) as one op, so that none of its sums is a
+    separate kernel:
+
+    * forward, layer k: the learned-hypergraph pair ``hgnn_k = [H_u·(H_uᵀ·h_u); H_i·(H_iᵀ·h_i)]``
+      (grouped skinny MFMA products), then ONE GCN hop over the (edge-dropped) adjacency whose
+      store writes ``gcn_k = A·h_k`` (act_out) and ``h_{k+1} = gcn_k + hgnn_k`` (res1) — the
+      reference's ``hidden += [gcn_emb + hgnn_hidden[-1]]``; the hidden tables are slices of one
+      [L+1, N, d] buffer and ``sum(hidden)`` is one slice-sum pass (hgd_sum_slices, same order);
+    * backward, layer k: the grouped row product H·dM, then ``dh_k = dE + Aᵀ·dgcn_k + H·dM``
+      as one backward hop whose store adds both, and writes, in the same pass, the next layer's
+      ``dhgnn_{k-1} = dh_k + dInfoNCE_{k-1}`` (the row epilogue's sum_out). Autograd's
+      accumulation adds (≈ 2 per layer), the layer adds and the L sum adds of the per-layer
+      graph disappear.
+
+    Inputs: the per-layer adjacency incidences (plain, compacted-dropped or masked views),
+    user / item embedding tables, and the per-layer dropped hypergraphs H_u [nu, K], H_i
+    [ni, K]. Outputs: E = sum(hidden) [N, d], gcn_0..gcn_{L-1}, hgnn_0..hgnn_{L-1}."""
+
+    @staticmethod
+    def forward(ctx, adjs, nu, user_emb, item_emb, *Hs):
+        L = len(adjs)
+        dev = user_emb.device
+        N = user_emb.shape[0] + item_emb.shape[0]
+        d = user_emb.shape[1]
+        K = Hs[0].shape[1]
+        f = dict(dtype=torch.float32, device=dev)
+        hid = torch.empty((L + 1, N, d), **f)
+        torch.cat([user_emb, item_emb], 0, out=hid[0])
+        Hs = [H.contiguous() for H in Hs]
+        gcn, hgnn, Ms = [], [], []
+        for k in range(L):
+            H_u, H_i = Hs[2 * k], Hs[2 * k + 1]
+            h = hid[k]
+            M_u, M_i = _gemm_tn_pair([(H_u, h[:nu]), (H_i, h[nu:])], dev)
+            Hh = torch.empty((N, d), **f)
+            _gemm_rows([_rows_desc(H_u, M_u, d, 1, K, d, Hh[:nu]),
+                        _rows_desc(H_i, M_i, d, 1, K, d, Hh[nu:])], dev)
+            G = torch.empty((N, d), **f)
+            inc = adjs[k]
+            spmm_csr(inc.csr, h, val=inc.val, ex=_res_epilogue(Hh, act_out=G), out=hid[k + 1])
+            gcn.append(G)
+            hgnn.append(Hh)
+            Ms += [M_u, M_i]
+        E = torch.empty((N, d), **f)
+        nat.check(nat.load().hgd_sum_slices(hid.data_ptr(), L + 1, N * d, N * d, E.data_ptr(),
+                                            torch.cuda.current_stream(dev).cuda_stream),
+                  "hgd_sum_slices")
+        ctx.adjs, ctx.nu, ctx.L, ctx.K = adjs, nu, L, K
+        ctx.save_for_backward(hid, *Hs, *Ms)
+        ctx.set_materialize_grads(False)
+        return (E, *gcn, *hgnn)
+
+    @staticmethod
+    def backward(ctx, dE, *grads):
+        L, nu, K = ctx.L, ctx.nu, ctx.K
+        saved = ctx.saved_tensors
+        hid = saved[0]
+        Hs = saved[1:1 + 2 * L]
+        Ms = saved[1 + 2 * L:]
+        dgcn, dhgnn = grads[:L], grads[L:]
+        _, N, d = hid.shape
+        dev = hid.device
+        f = dict(dtype=torch.float32, device=dev)
+        if dE is not None:
+            dE = dE.contiguous()
+        dh = dE if dE is not None else torch.zeros((N, d), **f)
+        dHh = dh if dhgnn[L - 1] is None else dh + dhgnn[L - 1].contiguous()
+        want_emb = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
+        dHs = [None] * (2 * L)
+        for k in reversed(range(L)):
+            H_u, H_i = Hs[2 * k], Hs[2 * k + 1]
+            M_u, M_i = Ms[2 * k], Ms[2 * k + 1]
+            h = hid[k]
+            dG = dh if dgcn[k] is None else dh + dgcn[k]
+            dM_u, dM_i = _gemm_tn_pair([(H_u, dHh[:nu]), (H_i, dHh[nu:])], dev)
+            if ctx.needs_input_grad[4 + 2 * k] or ctx.needs_input_grad[5 + 2 * k]:
+                # dH = dhgnn·Mᵀ + h·dMᵀ (Bm[k][n] = M[n][k]: bsk 1, bsn d), the second accumulated
+                dH_u, dH_i = torch.empty_like(H_u), torch.empty_like(H_i)
+                _gemm_rows([_rows_desc(dHh[:nu], M_u, 1, d, d, K, dH_u),
+                            _rows_desc(dHh[nu:], M_i, 1, d, d, K, dH_i)], dev)
+                _gemm_rows([_rows_desc(h[:nu], dM_u, 1, d, d, K, dH_u, accumulate=True),
+                            _rows_desc(h[nu:], dM_i, 1, d, d, K, dH_i, accumulate=True)], dev)
+                dHs[2 * k], dHs[2 * k + 1] = dH_u, dH_i
+            if k == 0 and not want_emb:
+                break
+            inc = ctx.adjs[k]
+            # H·dM first (plain grouped store), then the backward hop adds it and dE in its
+            # store (res2 = its own output row, read before written) and writes the next
+            # layer's dhgnn = dh + dInfoNCE as a second output
+            dh_new = torch.empty((N, d), **f)
+            _gemm_rows([_rows_desc(H_u, dM_u, d, 1, K, d, dh_new[:nu]),
+                        _rows_desc(H_i, dM_i, d, 1, K, d, dh_new[nu:])], dev)
+            nxt = dhgnn[k - 1].contiguous() if k > 0 and dhgnn[k - 1] is not None else None
+            dHh_new = torch.empty((N, d), **f) if nxt is not None else None
+            spmm_csr(inc.csc, dG.contiguous(), val=inc.val_t,
+                     ex=_res_epilogue(dE, res2=dh_new, sum_res=nxt, sum_out=dHh_new),
+                     out=dh_new)
+            dh = dh_new
+            dHh = dHh_new if nxt is not None else dh_new
+        d_u = dh[:nu] if ctx.needs_input_grad[2] else None
+        d_i = dh[nu:] if ctx.needs_input_grad[3] else None
+        return (None, None, d_u, d_i, *dHs)
+
+
+def hccf_layers_supported(user_emb: torch.Tensor, item_emb: torch.Tensor,
+                          H: torch.Tensor) -> bool:
+    """Shapes :func:`hccf_layers` runs (the skinny MFMA products and float4 slice sums)."""
+    d = user_emb.shape[1]
+    return (user_emb.is_cuda and item_emb.is_cuda and H.is_cuda
+            and user_emb.dtype == item_emb.dtype == H.dtype == torch.float32
+            and item_emb.shape[1] == d and d % 16 == 0 and 16 <= d <= 128
+            and H.shape[1] % 16 == 0 and 16 <= H.shape[1] <= 128
+            and user_emb.shape[0] > 0 and item_emb.shape[0] > 0)
+
+
+def hccf_layers(adjs, user_emb: torch.Tensor, item_emb: torch.Tensor, hypers_u, hypers_i):
+    """HCCF's propagation (model/graph/HCCF.py:173-191) over per-layer adjacencies ``adjs``
+    (Incidences of ``edgeDropper(sparse_norm_adj)``) and per-layer dropped hypergraphs:
+    returns ``(sum(hidden), gcn_hidden, hgnn_hidden)`` (see :class:`_HCCFLayers`)."""
+    L = len(adjs)
+    nu, N = user_emb.shape[0], user_emb.shape[0] + item_emb.shape[0]
+    for inc in adjs:
+        if inc.n_rows != N or inc.n_cols != N:
+            raise ValueError(f"hccf_layers: adjacency {inc.n_rows}x{inc.n_cols}, tables have {N} rows")
+    Hs = []
+    for Hu, Hi in zip(hypers_u, hypers_i):
+        Hs += [Hu, Hi]
+    out = _HCCFLayers.apply(list(adjs), int(nu), user_emb, item_emb, *Hs)
+    return out[0], list(out[1:1 + L]), list(out[1 + L:])

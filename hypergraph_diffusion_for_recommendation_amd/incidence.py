@@ -181,10 +181,14 @@ def spmm_csr(csr: CSR, X: torch.Tensor, val: Optional[torch.Tensor] = None,
     if timer is not None:
         t0 = timer.begin()
     mask = getattr(csr, "mask", None)
-    if mask is not None:
-        if ex is not None:
-            raise NotImplementedError("spmm: no fused row epilogue over a masked (edge-dropped) "
-                                      "view")
+    if mask is not None and ex is not None:
+        nat.check(lib.hgd_spmm_masked_fused(
+            csr.rowptr.data_ptr(), csr.col.data_ptr() if csr.nnz else None, nat.ptr(val),
+            mask.data_ptr() if csr.nnz else None, float(csr.keep), nat.ptr(row_scale),
+            csr.n_rows, csr.n_cols, int(row_begin), int(row_end), X.data_ptr(), X.stride(0),
+            out.data_ptr(), out.stride(0), d, ctypes.byref(ex), plan_ptr, nat.ptr(ws), wsb,
+            _stream(X.device)), "hgd_spmm_masked_fused")
+    elif mask is not None:
         nat.check(lib.hgd_spmm_masked(
             csr.rowptr.data_ptr(), csr.col.data_ptr() if csr.nnz else None, nat.ptr(val),
             mask.data_ptr() if csr.nnz else None, float(csr.keep), nat.ptr(row_scale),

@@ -84,7 +84,9 @@ class HCCF(GraphRecommender):
             self.model.edgeDropper.device_rng = True
             self.model.edgeDropper.capture_safe = True
             lr = torch.tensor(self.lRate, dtype=torch.float32, device=self.device)
-            self.optimizer = torch.optim.Adam(self.model.parameters(), lr=lr, capturable=True)
+            # fused: one multi-tensor kernel per step instead of the ~15 foreach passes
+            self.optimizer = torch.optim.Adam(self.model.parameters(), lr=lr, capturable=True,
+                                              fused=True)
         else:
             self.optimizer = torch.optim.Adam(self.model.parameters(), lr=self.lRate)
         self.scheduler = ReduceLROnPlateau(self.optimizer, 'min', factor=self.lr_decay,

@@ -148,6 +148,7 @@ hgd_status hgd_spmm_masked(const int64_t* rowptr, const int32_t* col, const floa
  *   b = layer_norm ? (a - μ_r)·rstd_r·γ + β : a      (biased variance, rstd = 1/sqrt(var+eps);
  *                                                      stats[2r] = μ_r, stats[2r+1] = rstd_r)
  *   Y[r] = out_scale·b + res1_scale·res1[r] + res2_scale·res2[r]    (NULL residuals skipped)
+ *   sum_out[r] = Y[r] + sum_res[r]                                    (when sum_out != NULL)
  * layer_norm needs the whole row in one lane group: d <= 256 with 16-byte aligned rows (X, Y,
  * residuals, act_out, leading dims % 4 == 0), or d <= 64 otherwise (HGD_ERR_UNSUPPORTED beyond).
  * act must be NONE or have slope >= 0, so that act'(z) can be read from the sign of a.
@@ -169,6 +170,14 @@ typedef struct hgd_row_epilogue {
   float* act_out;         /* [n_rows, ld_act] or NULL */
   int64_t ld_act;
   float* stats;           /* [n_rows, 2] or NULL */
+  /* optional second output after the residuals: sum_out[r] = Y[r] + sum_res[r] (HCCF's
+   * backward: the layer gradient dh and dh + the InfoNCE gradient of the layer below in one
+   * store); both NULL or both set. res1 / res2 may alias Y (each row is read before it is
+   * written, by the same lanes). */
+  const float* sum_res;
+  int64_t ld_sum_res;
+  float* sum_out;
+  int64_t ld_sum_out;
 } hgd_row_epilogue;
 
 /* hgd_spmm with the fused row epilogue `epi` (which replaces hgd_spmm's epilogue/slope). */
@@ -178,6 +187,18 @@ hgd_status hgd_spmm_fused(const int64_t* rowptr, const int32_t* col, const float
                           float* Y, int64_t ldy, int32_t d, const hgd_row_epilogue* epi,
                           const hgd_split_plan* plan, void* workspace, size_t workspace_bytes,
                           void* stream);
+
+/* hgd_spmm_masked (the edge-dropped view) with the fused row epilogue `epi`. HCCF's layer
+ * (model/graph/HCCF.py:182-187): gcn = A_drop·h stored through act_out while the row store adds
+ * the layer's hypergraph term as res1, so hidden[k+1] = gcn + hgnn needs no separate add; the
+ * backward hop adds the layer-sum gradient the same way. */
+hgd_status hgd_spmm_masked_fused(const int64_t* rowptr, const int32_t* col, const float* val,
+                                 const uint8_t* mask, float keep, const float* row_scale,
+                                 int64_t n_rows, int64_t n_src_rows, int64_t row_begin,
+                                 int64_t row_end, const float* X, int64_t ldx, float* Y,
+                                 int64_t ldy, int32_t d, const hgd_row_epilogue* epi,
+                                 const hgd_split_plan* plan, void* workspace,
+                                 size_t workspace_bytes, void* stream);
 
 /* The same row epilogue applied to an existing matrix Z [n_rows, ldz] (z = Z[r], no hop): the
  * LayerNorms that do not follow a hop, e.g. the MLP InputNorm of model/layers/MLP.py:65-71,109-110.
@@ -548,6 +569,11 @@ hgd_status hgd_epilogue_apply(const float* z, int64_t n, int32_t epilogue, float
                               void* stream);
 hgd_status hgd_epilogue_backward(const float* ref, const float* dy, int64_t n, int32_t epilogue,
                                  float slope, float* dz, void* stream);
+/* out[i] = Σ_s P[s·slice_stride + i] over s = 0..n_slices-1, summed in slice order (bitwise the
+ * chain ((P_0 + P_1) + P_2) + …): HCCF's `sum(hidden)` (model/graph/HCCF.py:188) over the layer
+ * tables kept as slices of one buffer. P, out 16-byte aligned, slice_stride % 4 == 0. */
+hgd_status hgd_sum_slices(const float* P, int64_t n_slices, int64_t slice_stride, int64_t n,
+                          float* out, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Incidence objects (SURVEY.md §8b "C ABI libhgd"): the library-owned form of the structure the

@@ -65,7 +65,7 @@ def main():
         counted = graph if counted is None else counted
         if counted:
             lr = torch.tensor(conf["lrate"], dtype=torch.float32, device=dev)
-            opt = torch.optim.Adam(model.parameters(), lr=lr, capturable=True)
+            opt = torch.optim.Adam(model.parameters(), lr=lr, capturable=True, fused=True)
         else:
             opt = torch.optim.Adam(model.parameters(), lr=conf["lrate"])
         state = {"k": 0, "cap": None}

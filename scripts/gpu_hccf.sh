@@ -1,0 +1,23 @@
+#!/bin/bash
+# HCCF iteration on one MI355X: the HCCF-path GPU tests, then scripts/bench_hccf.py (graph and
+# eager variants) and a rocprof kernel-stats pass over the graph-replayed step.
+# usage: gpu_hccf.sh <tag> [pytest args...]
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+tag=$1; shift
+O=gpurun_out/$tag
+mkdir -p $O
+export TMPDIR=/tmp
+if [ $# -gt 0 ]; then
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider "$@" \
+  > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+fi
+timeout -k 10 300 python scripts/bench_hccf.py --variants hgd_graph,hgd_device_mask > $O/bench_hccf.jsonl 2>&1 \
+  || { tail -20 $O/bench_hccf.jsonl; exit 1; }
+grep variant $O/bench_hccf.jsonl
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
+  python scripts/bench_hccf.py --variants hgd_graph --reps 20 > $O/prof.log 2>&1 || { tail -20 $O/prof.log; exit 1; }
+find $O/prof -name '*kernel_stats.csv' -exec cp {} $O/kernel_stats.csv \;
+find $O/prof -name '*kernel_trace.csv' -exec cp {} $O/kernel_trace.csv \;
+rm -rf $O/prof

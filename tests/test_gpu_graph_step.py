@@ -239,7 +239,7 @@ def test_captured_hccf_steps_equal_eager_steps(dev):
     for captured in (False, True):
         enc, U, I = _hccf(dev, drop_rate=0.0)
         lr = torch.tensor(1e-3, device=dev)
-        opt = torch.optim.Adam(enc.parameters(), lr=lr, capturable=True)
+        opt = torch.optim.Adam(enc.parameters(), lr=lr, capturable=True, fused=True)
         step = _step_fn(enc, opt, U)
         torch.manual_seed(11)  # the drop-edge seed counter's start
         losses = [float(step(*batches[0]))]

@@ -1,0 +1,144 @@
+"""GPU: HCCF's layer loop as one op (functional.hccf_layers, model/graph/HCCF.py:173-191) and the
+three store extensions it rides on.
+
+* hgd_sum_slices is bitwise the chain of adds ``sum(hidden)`` makes;
+* hgd_spmm_masked_fused over an edge-dropped view stores the bare hop through act_out bitwise
+  equal to hgd_spmm_masked, hop + res1 + res2 (res2 aliasing the output) bitwise equal to the
+  adds, and the second output sum_out = Y + sum_res;
+* HCCFEncoder with the fused loop gives bitwise the forward of the per-layer module graph
+  (same hops, same products, same add and sum orders) and the same gradients up to the order
+  of autograd's accumulations, for the capture-safe masked drop-edge and the reference's CPU
+  drop-edge stream, with nn dropout on. Parity against the float64 reference at the configs'
+  shapes is tests/test_gpu_config_parity.py (which runs this fused path).
+"""
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import hgd_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _norm_adj(U, I, nnz, seed):
+    rows, cols = O.synthetic_incidence(U, I, nnz, seed=seed)
+    return O.normalize_graph_mat(O.bipartite_adjacency(rows, cols, U, I))
+
+
+def test_sum_slices_is_the_chain_of_adds(dev):
+    from hypergraph_diffusion_for_recommendation_amd import _native as nat
+    g = torch.Generator(device=dev).manual_seed(0)
+    for S, n in ((1, 64), (4, 1000 * 64), (4, 4099), (3, 5)):
+        stride = (n + 3) // 4 * 4
+        P = torch.randn(S, stride, device=dev, generator=g)
+        out = torch.empty(n, device=dev)
+        nat.check(nat.load().hgd_sum_slices(P.data_ptr(), S, stride, n, out.data_ptr(),
+                                            torch.cuda.current_stream().cuda_stream), "sum")
+        ref = P[0, :n].clone()
+        for s in range(1, S):
+            ref = ref + P[s, :n]
+        assert torch.equal(out, ref), (S, n)
+
+
+def test_masked_fused_hop_stores(dev):
+    from hypergraph_diffusion_for_recommendation_amd.encoders import sparse_tensor_of
+    from hypergraph_diffusion_for_recommendation_amd.functional import _res_epilogue
+    from hypergraph_diffusion_for_recommendation_amd.incidence import spmm_csr
+    from hypergraph_diffusion_for_recommendation_amd.layers import SpAdjDropEdge
+    A = _norm_adj(900, 1300, 20_000, seed=3)
+    adj = sparse_tensor_of(A, dev)
+    torch.manual_seed(5)
+    view = SpAdjDropEdge(device_rng=True, capture_safe=True)(adj, 0.6)
+    N = A.shape[0]
+    for d in (32, 64, 128):
+        X = torch.randn(N, d, device=dev)
+        res = torch.randn(N, d, device=dev)
+        for csr, val in ((view.csr, view.val), (view.csc, view.val_t)):
+            plain = spmm_csr(csr, X, val=val)
+            act = torch.empty_like(plain)
+            y = spmm_csr(csr, X, val=val, ex=_res_epilogue(res, act_out=act))
+            assert torch.equal(act, plain), d
+            assert torch.equal(y, plain + res), d
+            # in place: res2 is the output buffer itself; second output y + sres
+            r2 = torch.randn(N, d, device=dev)
+            buf = r2.clone()
+            sres = torch.randn(N, d, device=dev)
+            sout = torch.empty_like(buf)
+            spmm_csr(csr, X, val=val, ex=_res_epilogue(res, res2=buf, sum_res=sres,
+                                                       sum_out=sout), out=buf)
+            assert torch.equal(buf, (plain + res) + r2), d
+            assert torch.equal(sout, buf + sres), d
+
+
+def _encoder(dev, A, U, I, d, L, capture_safe, fused):
+    from hypergraph_diffusion_for_recommendation_amd.encoders import HCCFEncoder
+    data = SimpleNamespace(n_users=U, n_items=I, norm_adj=A)
+    kw = dict(lrate=1e-3, lr_decay=0.9, max_epoch=1, batch_size=256, reg=0.01,
+              embedding_size=d, hyper_dim=32, drop_rate=0.25, p=0.3, n_layers=L)
+    torch.manual_seed(0)
+    enc = HCCFEncoder(kw, data, device=dev).train()
+    enc.fused_layers = fused
+    if capture_safe:
+        enc.edgeDropper.device_rng = True
+        enc.edgeDropper.capture_safe = True
+    return enc
+
+
+def _run(enc, dev, U, I, seed):
+    """Forward + a loss touching every output (the sum, every gcn_k — not detached here, so its
+    gradient path is exercised too — and every hgnn_k through the paired InfoNCE), backward."""
+    from hypergraph_diffusion_for_recommendation_amd.functional import (contrast_loss_pair,
+                                                                         unique_long_n)
+    torch.manual_seed(seed)
+    torch.cuda.manual_seed(seed)
+    ue, ie, gcn, hyp = enc(keep_rate=0.7)
+    g = torch.Generator(device=dev).manual_seed(seed)
+    N = U + I
+    W = torch.randn(N, ue.shape[1], device=dev, generator=g)
+    loss = (torch.cat([ue, ie]) * W).sum()
+    uid = torch.randint(0, U, (300,), device=dev, generator=g)
+    pid = torch.randint(0, I, (300,), device=dev, generator=g)
+    (un, uc), (pn, pc) = unique_long_n(uid), unique_long_n(pid)
+    for k, (e1, e2) in enumerate(zip(gcn, hyp)):
+        loss = loss + 0.3 * contrast_loss_pair(e1.detach(), e2, U, un, pn, 0.5, uc, pc)
+        loss = loss + 1e-3 * (e1 * W).sum() * (k + 1)
+    loss.backward()
+    grads = {k: p.grad.clone() for k, p in enc.named_parameters()}
+    return [ue.detach(), ie.detach()] + [t.detach() for t in gcn + hyp], float(loss), grads
+
+
+@pytest.mark.parametrize("capture_safe", [True, False])
+@pytest.mark.parametrize("L", [1, 3])
+def test_fused_layers_match_module_graph(dev, capture_safe, L):
+    U, I, d = 1500, 2200, 64
+    A = _norm_adj(U, I, 40_000, seed=11)
+    outs = {}
+    for fused in (False, True):
+        enc = _encoder(dev, A, U, I, d, L, capture_safe, fused)
+        outs[fused] = _run(enc, dev, U, I, seed=7)
+    (o0, l0, g0), (o1, l1, g1) = outs[False], outs[True]
+    for a, b in zip(o0, o1):
+        assert torch.equal(a, b)  # same kernels, same sums in the same order
+    assert abs(l0 - l1) <= 1e-6 * abs(l0)
+    for k in g0:
+        a, b = g0[k], g1[k]
+        scale = float(a.abs().max())
+        err = float((a - b).abs().max())
+        assert err <= 1e-5 * scale, (k, err, scale)
+
+
+def test_fused_layers_eval_and_no_grad(dev):
+    """keep_rate 1 (the eval forward, HCCF.py:103) under no_grad: same tables as the loop."""
+    U, I, d = 700, 900, 32
+    A = _norm_adj(U, I, 10_000, seed=2)
+    res = []
+    for fused in (False, True):
+        enc = _encoder(dev, A, U, I, d, 2, True, fused).eval()
+        with torch.no_grad():
+            ue, ie, gcn, hyp = enc(keep_rate=1)
+        res.append([ue, ie] + gcn + hyp)
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+    assert np.isfinite(res[1][0].cpu().numpy()).all()
