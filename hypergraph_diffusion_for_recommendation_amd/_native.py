@@ -257,6 +257,13 @@ _SIGNATURES = {
     "hgd_epilogue_backward": (c_i32, [c_void_p, c_void_p, c_i64, c_i32, c_f32, c_void_p,
                                       c_void_p]),
     "hgd_sum_slices": (c_i32, [c_void_p, c_i64, c_i64, c_i64, c_void_p, c_void_p]),
+    "hgd_bpr_workspace_size": (c_size, [c_i64, c_i64]),
+    "hgd_bpr_forward": (c_i32, [c_void_p, c_i64, c_i64, c_i64, c_i32, c_void_p, c_void_p,
+                                c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_void_p,
+                                c_void_p, c_size, c_void_p]),
+    "hgd_bpr_backward": (c_i32, [c_void_p, c_i64, c_i64, c_i64, c_i32, c_void_p, c_void_p,
+                                 c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_i64, c_void_p,
+                                 c_size, c_void_p]),
     "hgd_unique_workspace_size": (c_size, [c_i64]),
     "hgd_unique_i64": (c_i32, [c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_size, c_void_p]),
     "hgd_unique_trunc_f32": (c_i32, [c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_size,

@@ -1009,3 +1009,81 @@ def hccf_layers(adjs, user_emb: torch.Tensor, item_emb: torch.Tensor, hypers_u, 
         Hs += [Hu, Hi]
     out = _HCCFLayers.apply(list(adjs), int(nu), user_emb, item_emb, *Hs)
     return out[0], list(out[1:1 + L]), list(out[1 + L:])
+
+
+class _BPRTable(torch.autograd.Function):
+    """bpr_loss(E[uid], E[nu + pid], E[nu + nid]) (util/loss_torch.py:5-9) on one [N, d] table
+    (hgd_bpr_forward / hgd_bpr_backward); also returns the gathered anchor and positive rows
+    (non-differentiable: HCCF takes its InfoNCE node lists from them, HCCF.py:65-66)."""
+
+    @staticmethod
+    def forward(ctx, E, nu, uid, pid, nid):
+        lib = nat.load()
+        dev = E.device
+        N, d = E.shape
+        B = uid.numel()
+        f = dict(dtype=torch.float32, device=dev)
+        anc, pos = torch.empty((B, d), **f), torch.empty((B, d), **f)
+        coef, loss = torch.empty(B, **f), torch.empty((), **f)
+        wsb = lib.hgd_bpr_workspace_size(B, N)
+        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        nat.check(lib.hgd_bpr_forward(
+            E.data_ptr(), E.stride(0), nu, N - nu, d, uid.data_ptr(), pid.data_ptr(),
+            nid.data_ptr(), B, anc.data_ptr(), pos.data_ptr(), coef.data_ptr(), loss.data_ptr(),
+            ws.data_ptr(), wsb, torch.cuda.current_stream(dev).cuda_stream), "hgd_bpr_forward")
+        ctx.nu = nu
+        ctx.save_for_backward(E, uid, pid, nid, coef)
+        ctx.mark_non_differentiable(anc, pos)
+        return loss, anc, pos
+
+    @staticmethod
+    def backward(ctx, g, _g_anc, _g_pos):
+        E, uid, pid, nid, coef = ctx.saved_tensors
+        lib = nat.load()
+        dev = E.device
+        N, d = E.shape
+        B = uid.numel()
+        g = g.to(dtype=torch.float32).reshape(1).contiguous()
+        dE = torch.empty_like(E)
+        wsb = lib.hgd_bpr_workspace_size(B, N)
+        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        nat.check(lib.hgd_bpr_backward(
+            E.data_ptr(), E.stride(0), ctx.nu, N - ctx.nu, d, uid.data_ptr(), pid.data_ptr(),
+            nid.data_ptr(), B, coef.data_ptr(), g.data_ptr(), dE.data_ptr(), dE.stride(0),
+            ws.data_ptr(), wsb, torch.cuda.current_stream(dev).cuda_stream), "hgd_bpr_backward")
+        return dE, None, None, None, None
+
+
+def _table_of(user_emb: torch.Tensor, item_emb: torch.Tensor) -> Optional[torch.Tensor]:
+    """The [nu + ni, d] table whose row blocks ``user_emb`` / ``item_emb`` are (the split of an
+    encoder's layer sum, HCCF.py:189-190), or None."""
+    base = user_emb._base
+    if base is None or item_emb._base is not base or base.dim() != 2 or not base.is_contiguous():
+        return None
+    nu, d = user_emb.shape
+    if (base.shape != (nu + item_emb.shape[0], d) or user_emb.data_ptr() != base.data_ptr()
+            or item_emb.data_ptr() != base.data_ptr() + nu * d * base.element_size()
+            or user_emb.stride() != base.stride() or item_emb.stride() != base.stride()):
+        return None
+    return base
+
+
+def bpr_loss_rows(user_emb: torch.Tensor, item_emb: torch.Tensor, uid: torch.Tensor,
+                  pid: torch.Tensor, nid: torch.Tensor):
+    """``bpr_loss(user_emb[uid], item_emb[pid], item_emb[nid])`` (util/loss_torch.py:5-9 on the
+    gathers of HCCF.py:84-86) → ``(loss, anchor_rows, positive_rows)``. When both tables are the
+    row blocks of one device table (an encoder's split layer sum) it is one fused op
+    (:class:`_BPRTable`: two kernels forward, three backward, deterministic, the table gradient
+    written whole — no index_put sorts, no split/cat); otherwise the reference's torch ops."""
+    E = _table_of(user_emb, item_emb)
+    d = user_emb.shape[1]
+    if (E is not None and E.is_cuda and E.dtype == torch.float32 and d % 4 == 0 and d <= 256
+            and uid.numel() > 0 and uid.numel() == pid.numel() == nid.numel()
+            and E.data_ptr() % 16 == 0):
+        idx = [t.to(device=E.device, dtype=torch.int64).contiguous() for t in (uid, pid, nid)]
+        return _BPRTable.apply(E, int(user_emb.shape[0]), *idx)
+    anc, pos, neg = user_emb[uid], item_emb[pid], item_emb[nid]
+    pos_score = torch.mul(anc, pos).sum(dim=1)
+    neg_score = torch.mul(anc, neg).sum(dim=1)
+    loss = torch.mean(-torch.log(10e-6 + torch.sigmoid(pos_score - neg_score)))
+    return loss, anc, pos

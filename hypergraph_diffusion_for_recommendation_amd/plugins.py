@@ -45,7 +45,8 @@ from torch.optim.lr_scheduler import ReduceLROnPlateau
 
 from .encoders import (HCCFDiffusionEncoder, HCCFEncoder, LocalAwareEncoder,
                        LocalAwareEncoderHD3, sparse_tensor_of)
-from .functional import contrast_loss, contrast_loss_pair, unique_long, unique_long_n
+from .functional import (bpr_loss_rows, contrast_loss, contrast_loss_pair, unique_long,
+                         unique_long_n)
 from .layers import HGCNConv, SpAdjDropEdge
 from .sampler import next_batch_pairwise
 from .selfrec import GraphRecommender, early_stopping
@@ -111,7 +112,10 @@ class HCCF(GraphRecommender):
         self.early_stopping_steps = int(kwargs['early_stopping_steps'])
 
     def calcLosses(self, ancs, poss, negs, gcnEmbedsLst, hyperEmbedsLst, reg):  # :61-70
-        bprLoss = bpr_loss(ancs, poss, negs)
+        return bpr_loss(ancs, poss, negs), HCCF.ssl_loss(self, ancs, poss, gcnEmbedsLst,
+                                                          hyperEmbedsLst)
+
+    def ssl_loss(self, ancs, poss, gcnEmbedsLst, hyperEmbedsLst):  # :62-67
         nu = self.data.n_users
         # torch.unique(ancs.long()) / torch.unique(poss.long()) are the same in every layer of the
         # reference's loop: computed once here (each is a device→host read — or, in graph mode,
@@ -128,18 +132,18 @@ class HCCF(GraphRecommender):
             sslLoss += contrast_loss_pair(embeds1, embeds2, nu, u_nodes, p_nodes, self.temp,
                                           u_cnt, p_cnt)
         sslLoss *= self.ss_rate
-        return bprLoss, sslLoss
+        return sslLoss
 
     def train_step(self, user_idx, pos_idx, neg_idx) -> torch.Tensor:
         """One batch of HCCF.py:79-97; returns the (device) batch loss."""
         model = self.model
         model.train()
         user_emb, item_emb, gcnEmbedsLst, hyperEmbedsLst = model(keep_rate=1 - self.dropRate)
-        anchor_emb = user_emb[user_idx]
-        pos_emb = item_emb[pos_idx]
-        neg_emb = item_emb[neg_idx]
-        loss_rec, loss_ssl = self.calcLosses(anchor_emb, pos_emb, neg_emb, gcnEmbedsLst,
-                                             hyperEmbedsLst, self.reg)
+        # the gathers + bpr_loss of :84-88 as one op on the encoder's table (functional.
+        # bpr_loss_rows; the reference's torch ops when the tables are not one device block)
+        loss_rec, anchor_emb, pos_emb = bpr_loss_rows(user_emb, item_emb, user_idx, pos_idx,
+                                                      neg_idx)
+        loss_ssl = self.ssl_loss(anchor_emb, pos_emb, gcnEmbedsLst, hyperEmbedsLst)
         batch_loss = loss_rec + loss_ssl
         self.optimizer.zero_grad()
         torch.nn.utils.clip_grad_norm_(model.parameters(), 4)  # before backward, as :95

@@ -560,6 +560,27 @@ hgd_status hgd_unique_dev_trunc_f32(const float* x, int64_t n, int64_t* out, int
                                     void* workspace, size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * BPR loss from the embedding table (util/loss_torch.py:5-9 over the rows HCCF.py:84-86
+ * gathers): E [n_users + n_items, lde] (users first, 16-byte aligned rows, d % 4 == 0,
+ * d <= 256); anc = E[uid], pos = E[n_users + pid], neg = E[n_users + nid] (int64 ids, torch
+ * indexing semantics; out-of-range ids are clamped, never dereferenced);
+ *   loss = mean_k −log(1e-5 + σ(⟨anc_k,pos_k⟩ − ⟨anc_k,neg_k⟩)), coef_k = σ(1−σ)/(1e-5+σ).
+ * anc_out / pos_out ([batch, d], optional) receive the gathered rows (HCCF's InfoNCE node lists
+ * are taken from them). Backward: dE = ∂(grad·loss)/∂E written in full (zero rows included;
+ * `grad` a device scalar), every touched row summed over its positions in position order
+ * (deterministic; integer atomics only). Workspace: hgd_bpr_workspace_size(batch, n_rows). */
+size_t hgd_bpr_workspace_size(int64_t batch, int64_t n_rows);
+hgd_status hgd_bpr_forward(const float* E, int64_t lde, int64_t n_users, int64_t n_items,
+                           int32_t d, const int64_t* uid, const int64_t* pid, const int64_t* nid,
+                           int64_t batch, float* anc_out, float* pos_out, float* coef,
+                           float* loss, void* workspace, size_t workspace_bytes, void* stream);
+hgd_status hgd_bpr_backward(const float* E, int64_t lde, int64_t n_users, int64_t n_items,
+                            int32_t d, const int64_t* uid, const int64_t* pid,
+                            const int64_t* nid, int64_t batch, const float* coef,
+                            const float* grad, float* dE, int64_t ldd, void* workspace,
+                            size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Elementwise epilogues around the hops (contiguous fp32, 16-byte aligned).
  *   apply:    y = epi(z)                                   (nn.LeakyReLU / nn.ReLU forward)
  *   backward: dz = dy * (ref > 0 ? 1 : slope) for LEAKY, dy * (ref > 0) for RELU, where ref is

@@ -41,7 +41,8 @@ def main():
 
     import refops as R
     from hypergraph_diffusion_for_recommendation_amd.encoders import HCCFEncoder
-    from hypergraph_diffusion_for_recommendation_amd.functional import (contrast_loss,
+    from hypergraph_diffusion_for_recommendation_amd.functional import (bpr_loss_rows,
+                                                                         contrast_loss,
                                                                          contrast_loss_pair,
                                                                          unique_long,
                                                                          unique_long_n)
@@ -72,7 +73,11 @@ def main():
 
         def body(uid, pid, nid):
             ue, ie, gcn, hyp = model(keep_rate=keep)
-            anc, pos, neg = ue[uid], ie[pid], ie[nid]
+            if counted:  # the plugin's fused BPR on the encoder table (functional.bpr_loss_rows)
+                bpr, anc, pos = bpr_loss_rows(ue, ie, uid, pid, nid)
+            else:
+                anc, pos, neg = ue[uid], ie[pid], ie[nid]
+                bpr = R.bpr_loss(anc, pos, neg)
             ssl = 0
             # the reference recomputes torch.unique(·.long()) per layer; ours hoists it (same value)
             un = (unique(anc), unique(pos)) if hoist else None
@@ -85,7 +90,7 @@ def main():
                 else:
                     ssl = ssl + loss_fn(e1[:nu], e2[:nu], nu_nodes, temp) \
                         + loss_fn(e1[nu:], e2[nu:], np_nodes, temp)
-            loss = R.bpr_loss(anc, pos, neg) + cl_rate * ssl
+            loss = bpr + cl_rate * ssl
             opt.zero_grad()
             torch.nn.utils.clip_grad_norm_(model.parameters(), 4)  # before backward, as HCCF.py:95
             loss.backward()

@@ -142,3 +142,43 @@ def test_fused_layers_eval_and_no_grad(dev):
     for a, b in zip(*res):
         assert torch.equal(a, b)
     assert np.isfinite(res[1][0].cpu().numpy()).all()
+
+
+@pytest.mark.parametrize("d", [12, 16, 32, 64, 128, 256])
+def test_bpr_loss_rows_matches_torch(dev, d):
+    """functional.bpr_loss_rows (hgd_bpr_*) against util/loss_torch.py:5-9 on the gathers of
+    HCCF.py:84-86 in float64: loss within 1e-6 relative, the table gradient row-bound
+    (1e-5 · Σ|terms| of each row), the gathered rows bitwise; a small table makes most rows
+    repeat within the batch (the summed-duplicates path); two runs are bitwise equal."""
+    from hypergraph_diffusion_for_recommendation_amd.functional import bpr_loss_rows
+    g = torch.Generator(device=dev).manual_seed(d)
+    for U, I, B in ((300, 500, 4096), (31_668, 38_048, 4096), (5, 3, 64)):
+        E = (0.3 * torch.randn(U + I, d, device=dev, generator=g)).requires_grad_(True)
+        uid = torch.randint(0, U, (B,), device=dev, generator=g)
+        pid = torch.randint(0, I, (B,), device=dev, generator=g)
+        nid = torch.randint(0, I, (B,), device=dev, generator=g)
+        ue, ie = torch.split(E, [U, I])
+        outs = []
+        for _ in range(2):
+            loss, anc, pos = bpr_loss_rows(ue, ie, uid, pid, nid)
+            (gE,) = torch.autograd.grad(2.5 * loss, E)
+            outs.append((loss.detach(), anc, pos, gE))
+        assert all(torch.equal(a, b) for a, b in zip(outs[0], outs[1]))
+        loss, anc, pos, gE = outs[0]
+        assert torch.equal(anc, E.detach()[uid]) and torch.equal(pos, E.detach()[U + pid])
+        E64 = E.detach().double().cpu().requires_grad_(True)
+        u64, i64 = torch.split(E64, [U, I])
+        a, p, n = u64[uid.cpu()], i64[pid.cpu()], i64[nid.cpu()]
+        ps, ns = (a * p).sum(1), (a * n).sum(1)
+        ref = torch.mean(-torch.log(1e-5 + torch.sigmoid(ps - ns)))
+        (gR,) = torch.autograd.grad(2.5 * ref, E64)
+        assert abs(float(loss) - float(ref)) <= 1e-6 * abs(float(ref)), (float(loss), float(ref))
+        # Σ|terms| of each gradient row: the same chain on |·| (|coef| ≤ 1/B · 2.5)
+        a_, p_, n_ = a.detach().abs(), p.detach().abs(), n.detach().abs()
+        mag = torch.zeros_like(E64)
+        w = 2.5 / B
+        mag.index_add_(0, uid.cpu(), w * (p_ + n_))
+        mag.index_add_(0, U + pid.cpu(), w * a_)
+        mag.index_add_(0, U + nid.cpu(), w * a_)
+        err = (gE.double().cpu() - gR).abs()
+        assert bool((err <= 1e-5 * mag + 1e-30).all()), float((err / (mag + 1e-30)).max())
