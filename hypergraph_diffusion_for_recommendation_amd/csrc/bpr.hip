@@ -6,10 +6,9 @@
 // neg and mean forward, and the same chain backward ending in three sort-based index_put
 // scatters (~40 small launches per step). Here: forward = one row kernel (gather, both dots,
 // per-row term and backward coefficient) + one fixed-order reduction; backward = zero/init,
-// one atomic pass that finds each destination row's first position and count (integer
-// atomics: order-independent results), and one row kernel in which the FIRST position of every
-// destination sums the contributions of all its positions in position order — deterministic,
-// no float atomics, no sort.
+// one pass linking every position into its destination row's list (integer atomics), and one
+// row kernel in which one position per destination sums the contributions of all the row's
+// positions in ascending position order — deterministic, no float atomics, no sort.
 #include <algorithm>
 
 #include "device_util.h"
@@ -90,8 +89,7 @@ __global__ __launch_bounds__(1024) void k_bpr_mean(const float* term, int64_t B,
   if (threadIdx.x == 0) *loss = s[0] / static_cast<float>(B);
 }
 
-__global__ void k_bpr_bwd_init(float* dE, int64_t lde, int64_t n_rows, int32_t d, int* first,
-                               int* cnt) {
+__global__ void k_bpr_bwd_init(float* dE, int64_t lde, int64_t n_rows, int32_t d, int* head) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   const int64_t per = d / 4;
   if (i < n_rows * per) {
@@ -99,36 +97,35 @@ __global__ void k_bpr_bwd_init(float* dE, int64_t lde, int64_t n_rows, int32_t d
     const float z[4] = {0.f, 0.f, 0.f, 0.f};
     store_vec<4>(dE + r * lde + c, z);
   }
-  if (i < n_rows) {
-    first[i] = 0x7fffffff;
-    cnt[i] = 0;
-  }
+  if (i < n_rows) head[i] = -1;
 }
 
-__global__ void k_bpr_bwd_mark(BprArgs a, int* first, int* cnt) {
+// Every position pushes itself onto its destination row's list (integer atomics; the list
+// ORDER depends on timing, the set does not — the row kernel sorts it).
+__global__ void k_bpr_bwd_link(BprArgs a, int* head, int* next, int* dst) {
   const int64_t q = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (q >= 3 * a.B) return;
-  const int64_t r = dest_row(a, q);
-  atomicMin(first + r, static_cast<int>(q));
-  atomicAdd(cnt + r, 1);
+  const int r = static_cast<int>(dest_row(a, q));
+  dst[q] = r;
+  next[q] = atomicExch(head + r, static_cast<int>(q));
 }
 
-// One lane group per position; the first position of each destination row writes that row:
-// the contributions of all its positions, summed in position order.
+// One lane group per position; the position left at the head of each destination row's list
+// writes that row: the contributions of all its positions, summed in ascending position order
+// (the list is walked once into the group's lanes and ranked there; a list longer than the
+// group — only with tables much smaller than the batch — is summed by repeated minimum walks).
 template <int G>
 __global__ __launch_bounds__(kBlock) void k_bpr_bwd_rows(BprArgs a, const float* coef,
-                                                        const float* grad, const int* first,
-                                                        const int* cnt, float* dE, int64_t ldd) {
+                                                        const float* grad, const int* head,
+                                                        const int* next, const int* dst,
+                                                        float* dE, int64_t ldd) {
   constexpr int GPB = kBlock / G;
   const int l = threadIdx.x % G;
   const int64_t q = static_cast<int64_t>(blockIdx.x) * GPB + threadIdx.x / G;
   if (q >= 3 * a.B) return;
-  const int64_t r = dest_row(a, q);
-  if (first[r] != static_cast<int>(q)) return;  // group-uniform
+  const int r = dst[q];
+  if (head[r] != static_cast<int>(q)) return;  // group-uniform
   const float gB = -(*grad) / static_cast<float>(a.B);
-  const int n_pos = cnt[r];
-  // positions of an anchor row are anchors; of an item row, positives or negatives
-  const int64_t seg_end = q < a.B ? a.B : 3 * a.B;
   constexpr int NV = 4;  // float4 column blocks per lane: d / 4 <= NV·G for every group_for(d)
   float acc[NV][4];
 #pragma unroll
@@ -144,39 +141,50 @@ __global__ __launch_bounds__(kBlock) void k_bpr_bwd_rows(BprArgs a, const float*
       if (c >= a.d) break;
       if (j < a.B) {  // anchor: t·(pos − neg)
         float p[4], n[4];
-        load_vec<4>(a.E + dest_row(a, a.B + k) * a.lde + c, p);
-        load_vec<4>(a.E + dest_row(a, 2 * a.B + k) * a.lde + c, n);
+        load_vec<4>(a.E + static_cast<int64_t>(dst[a.B + k]) * a.lde + c, p);
+        load_vec<4>(a.E + static_cast<int64_t>(dst[2 * a.B + k]) * a.lde + c, n);
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[v][i] += t * (p[i] - n[i]);
       } else {  // positive: t·anc, negative: −t·anc
         float u[4];
-        load_vec<4>(a.E + dest_row(a, k) * a.lde + c, u);
+        load_vec<4>(a.E + static_cast<int64_t>(dst[k]) * a.lde + c, u);
         const float s = j < 2 * a.B ? t : -t;
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[v][i] += s * u[i];
       }
     }
   };
-  add(q);
-  int left = n_pos - 1;
-  for (int64_t base = q + 1; left > 0 && base < seg_end; base += G) {
-    const int64_t j = base + l;
-    const bool hit = j < seg_end && dest_row(a, j) == r;
-    unsigned long long m = __ballot(hit);
-    const int sh = (static_cast<int>(threadIdx.x) & 63) & ~(G - 1);
-    m = G == 64 ? m : (m >> sh) & ((1ull << G) - 1ull);
-    while (m) {  // ascending positions: group-uniform
-      const int b = __ffsll(static_cast<long long>(m)) - 1;
-      m &= m - 1;
-      add(base + b);
-      --left;
+  // walk the list: its length, and element t held by lane t (t < G)
+  int n_pos = 0, mine = 0x7fffffff;
+  for (int e = static_cast<int>(q); e >= 0; e = next[e]) {
+    if (n_pos == l) mine = e;
+    ++n_pos;
+  }
+  if (n_pos <= G) {
+    int rank = 0;  // elements smaller than this lane's
+    for (int t = 0; t < n_pos; ++t) rank += __shfl(mine, t, G) < mine ? 1 : 0;
+    for (int t = 0; t < n_pos; ++t) {
+      int pos = 0;
+      for (int s = 0; s < n_pos; ++s) {
+        const int rs = __shfl(rank, s, G), ms = __shfl(mine, s, G);
+        pos = rs == t ? ms : pos;
+      }
+      add(pos);
+    }
+  } else {
+    int last = -1;
+    for (int t = 0; t < n_pos; ++t) {
+      int best = 0x7fffffff;
+      for (int e = static_cast<int>(q); e >= 0; e = next[e]) best = (e > last && e < best) ? e : best;
+      add(best);
+      last = best;
     }
   }
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const int c = 4 * (l + v * G);
     if (c >= a.d) break;
-    store_vec<4>(dE + r * ldd + c, acc[v]);
+    store_vec<4>(dE + static_cast<int64_t>(r) * ldd + c, acc[v]);
   }
 }
 
@@ -205,8 +213,9 @@ hgd_status check(const BprArgs& a, const char* fn) {
 using namespace hgd;
 
 extern "C" size_t hgd_bpr_workspace_size(int64_t batch, int64_t n_rows) {
-  return align_up(static_cast<size_t>(batch > 0 ? batch : 0) * 4) * 2 +
-         align_up(static_cast<size_t>(n_rows > 0 ? n_rows : 0) * 4) * 2;
+  const size_t b = static_cast<size_t>(batch > 0 ? batch : 0);
+  return align_up(b * 4) + align_up(static_cast<size_t>(n_rows > 0 ? n_rows : 0) * 4) +
+         2 * align_up(3 * b * 4);
 }
 
 extern "C" hgd_status hgd_bpr_forward(const float* E, int64_t lde, int64_t n_users,
@@ -259,22 +268,24 @@ extern "C" hgd_status hgd_bpr_backward(const float* E, int64_t lde, int64_t n_us
     return fail(HGD_ERR_WORKSPACE, "hgd_bpr_backward: workspace %zu < required %zu",
                 workspace_bytes, need);
   const int64_t N = n_users + n_items;
-  char* w = static_cast<char*>(workspace) + 2 * align_up(static_cast<size_t>(batch) * 4);
-  int* first = reinterpret_cast<int*>(w);
-  int* cnt = reinterpret_cast<int*>(w + align_up(static_cast<size_t>(N) * 4));
+  char* w = static_cast<char*>(workspace) + align_up(static_cast<size_t>(batch) * 4);
+  int* head = reinterpret_cast<int*>(w);
+  w += align_up(static_cast<size_t>(N) * 4);
+  int* next = reinterpret_cast<int*>(w);
+  int* dst = reinterpret_cast<int*>(w + align_up(static_cast<size_t>(3 * batch) * 4));
   hipStream_t st = as_stream(stream);
   const int64_t init_n = std::max<int64_t>(N * (d / 4), N);
   hipLaunchKernelGGL(k_bpr_bwd_init, dim3(grid_for(init_n)), dim3(kBlock), 0, st, dE, ldd, N, d,
-                     first, cnt);
-  hipLaunchKernelGGL(k_bpr_bwd_mark, dim3(grid_for(3 * batch)), dim3(kBlock), 0, st, a, first,
-                     cnt);
+                     head);
+  hipLaunchKernelGGL(k_bpr_bwd_link, dim3(grid_for(3 * batch)), dim3(kBlock), 0, st, a, head,
+                     next, dst);
   const int G = group_for(d);
   const unsigned blocks = static_cast<unsigned>((3 * batch + kBlock / G - 1) / (kBlock / G));
   switch (G) {
-    case 64: hipLaunchKernelGGL(k_bpr_bwd_rows<64>, dim3(blocks), dim3(kBlock), 0, st, a, coef, grad, first, cnt, dE, ldd); break;
-    case 16: hipLaunchKernelGGL(k_bpr_bwd_rows<16>, dim3(blocks), dim3(kBlock), 0, st, a, coef, grad, first, cnt, dE, ldd); break;
-    case 4: hipLaunchKernelGGL(k_bpr_bwd_rows<4>, dim3(blocks), dim3(kBlock), 0, st, a, coef, grad, first, cnt, dE, ldd); break;
-    default: hipLaunchKernelGGL(k_bpr_bwd_rows<1>, dim3(blocks), dim3(kBlock), 0, st, a, coef, grad, first, cnt, dE, ldd); break;
+    case 64: hipLaunchKernelGGL(k_bpr_bwd_rows<64>, dim3(blocks), dim3(kBlock), 0, st, a, coef, grad, head, next, dst, dE, ldd); break;
+    case 16: hipLaunchKernelGGL(k_bpr_bwd_rows<16>, dim3(blocks), dim3(kBlock), 0, st, a, coef, grad, head, next, dst, dE, ldd); break;
+    case 4: hipLaunchKernelGGL(k_bpr_bwd_rows<4>, dim3(blocks), dim3(kBlock), 0, st, a, coef, grad, head, next, dst, dE, ldd); break;
+    default: hipLaunchKernelGGL(k_bpr_bwd_rows<1>, dim3(blocks), dim3(kBlock), 0, st, a, coef, grad, head, next, dst, dE, ldd); break;
   }
   return check_launch("hgd_bpr_backward");
 }
