@@ -315,6 +315,20 @@ class MLP(nn.Module):
         return self.lins[-1](x)
 
 
+def _relu_if(x: torch.Tensor, relu: bool) -> torch.Tensor:
+    return F.relu(x) if relu else x
+
+
+def input_norm_linear(W) -> Optional[tuple]:
+    """(LayerNorm, Linear) when ``W`` is an :class:`MLP` of one Linear behind its InputNorm
+    LayerNorm (HGNN_HD4's EquivSetConv.W: MLP3_num_layers 1, normalization 'ln', input_norm,
+    HGNN_HD4.py:371-388) — the LayerNorm can then run in the store of the hop that feeds it."""
+    if (isinstance(W, MLP) and len(W.lins) == 1 and W.InputNorm
+            and isinstance(W.normalizations[0], LayerNorm)):
+        return W.normalizations[0], W.lins[0]
+    return None
+
+
 def _position_incidence(index: torch.Tensor, n_out: int) -> Incidence:
     """P[index[k], k] = 1: scatter over nonzero positions (P·src) and, transposed, the gather
     src[index] (Pᵀ·X) — both as hgd_spmm hops."""
@@ -384,7 +398,9 @@ class EquivSetConv(nn.Module):
                        (int(N), vertex._version, edges._version), inc)
         return inc
 
-    def forward(self, X, vertex, edges, X0):
+    def forward(self, X, vertex, edges, X0, relu: bool = False):
+        """``relu``: apply the ReLU that follows the conv in EquivSetGNN (its ``act``), fused
+        into W's Linear where the fused path runs."""
         N = X.shape[-2]
         inc = self._incidence(vertex, edges, N)
         scale = "mean" if self.aggr == "mean" else None
@@ -392,12 +408,18 @@ class EquivSetConv(nn.Module):
         if self.W2 is None:
             if self.alpha == 0 and self.fused_epilogue:
                 # (1-0)·Xv + 0·X0 is Xv for finite X0 (HGNN_HD4's restart_alpha = 0): no blend,
-                # no X0 read, and the plain two-hop's backward
-                return self.W(two_hop(inc, Xs, P=scale, Q=scale, R=None))
+                # no X0 read, and the plain two-hop's backward; W's InputNorm LayerNorm (MLP.py:
+                # 109-110) runs in the second hop's store instead of its own [N, d] pass
+                ln_lin = input_norm_linear(self.W)
+                if ln_lin is not None:
+                    return ln_lin[1](two_hop_fused(inc, Xs, P=scale, Q=scale, norm=ln_lin[0]),
+                                     relu=relu)
+                return _relu_if(self.W(two_hop(inc, Xs, P=scale, Q=scale, R=None)), relu)
             if self.fused_epilogue and torch.is_tensor(X0) and tuple(X0.shape) == (N, Xs.shape[1]):
                 # restart blend (1-α)·Xv + α·X0 fused into the second hop's store
-                return self.W(two_hop_fused(inc, Xs, P=scale, Q=scale, out_scale=1 - self.alpha,
-                                            res1=X0, res1_scale=self.alpha))
+                return _relu_if(self.W(two_hop_fused(inc, Xs, P=scale, Q=scale,
+                                                     out_scale=1 - self.alpha, res1=X0,
+                                                     res1_scale=self.alpha)), relu)
             Xv = two_hop(inc, Xs, P=scale, Q=scale, R=None)
         else:
             # general path: Xe = aggr(W1(X)[V], E); Xv = aggr(W2([X[V], Xe[E]]), V)
@@ -413,7 +435,7 @@ class EquivSetConv(nn.Module):
             if scale:
                 Xv = Xv * inc.scale("row", "mean")[:, None]
         X = (1 - self.alpha) * Xv + self.alpha * X0
-        return self.W(X)
+        return _relu_if(self.W(X), relu)
 
     def _pos(self, index, n_out, tag):
         attr = f"_pos_{tag}"
@@ -470,10 +492,12 @@ class EquivSetGNN(nn.Module):
         x = self.dropout(x)
         x = self.lin_in(x, relu=True)  # F.relu(lin_in(x)) fused
         x0 = x
+        relu = isinstance(self.act, nn.ReLU)  # fused into the conv's last Linear when it can
         for _ in range(self.nlayer):
             x = self.dropout(x)
-            x = self.conv(x, V, E, x0)
-            x = self.act(x)
+            x = self.conv(x, V, E, x0, relu=relu)
+            if not relu:
+                x = self.act(x)
         return self.dropout(x)
 
     def generate_V_E(self, n_nodes, hypergraph):

@@ -30,7 +30,7 @@ import torch.nn.functional as F
 
 from .encoders import edhnn_config
 from .functional import dense_two_hop, linear
-from .layers import EquivSetGNN, LayerNorm
+from .layers import EquivSetGNN, LayerNorm, input_norm_linear
 from .sharded import (ShardedBipartite, bipartite_hop, bipartite_hop_fused,  # noqa: F401
                       shard_bounds, sharded_dense_two_hop, sharded_mean_two_hop)
 
@@ -218,8 +218,17 @@ class ShardedLocalAwareEncoder(nn.Module):
         x = blk.lin_in(x, relu=True)
         x0 = x
         conv = blk.conv
+        ln_lin = input_norm_linear(conv.W) if not conv.alpha else None
         for _ in range(blk.nlayer):
             x = self._drop(blk.dropout, x)
+            if ln_lin is not None:  # W's InputNorm LayerNorm in the second hop's store
+                xv = bipartite_hop_fused(self.ui, bipartite_hop(self.ui, conv.W1(x), "mean"),
+                                         "mean", norm=ln_lin[0])
+                if isinstance(blk.act, nn.ReLU):
+                    x = ln_lin[1](xv, relu=True)  # the block's ReLU fused into the Linear
+                else:
+                    x = blk.act(ln_lin[1](xv))
+                continue
             xv = sharded_mean_two_hop(self.ui, conv.W1(x))
             if conv.alpha:
                 xv = (1 - conv.alpha) * xv + conv.alpha * x0
