@@ -112,6 +112,36 @@ class GemmTnDesc(ctypes.Structure):
     ]
 
 
+class InfonceTerm(ctypes.Structure):
+    """Mirror of ``hgd_infonce_term`` (include/hgd.h)."""
+
+    _fields_ = [
+        ("E1", c_void_p),
+        ("ld1", c_i64),
+        ("E2", c_void_p),
+        ("ld2", c_i64),
+        ("n_rows", c_i64),
+        ("nodes", c_void_p),
+        ("capacity", c_i64),
+        ("batch_count", c_void_p),
+        ("P1", c_void_p),
+        ("P2", c_void_p),
+        ("inv_norm1", c_void_p),
+        ("inv_norm2", c_void_p),
+        ("pos_logit", c_void_p),
+        ("deno", c_void_p),
+        ("loss", c_void_p),
+        ("dX1", c_void_p),
+        ("dX2", c_void_p),
+        ("dE1", c_void_p),
+        ("ldE1", c_i64),
+        ("dE2", c_void_p),
+        ("ldE2", c_i64),
+        ("workspace", c_void_p),
+        ("workspace_bytes", c_size),
+    ]
+
+
 class IncidenceView(ctypes.Structure):
     """Mirror of ``hgd_incidence_view`` (include/hgd.h)."""
 
@@ -195,6 +225,10 @@ _SIGNATURES = {
                                        c_void_p, c_i32, c_f32, c_void_p, c_void_p, c_i64,
                                        c_void_p, c_i64, c_void_p, c_i64, c_void_p, c_size,
                                        c_void_p]),
+    "hgd_infonce_forward_group": (c_i32, [ctypes.POINTER(InfonceTerm), c_i32, c_i32, c_f32,
+                                          c_void_p]),
+    "hgd_infonce_backward_group": (c_i32, [ctypes.POINTER(InfonceTerm), c_i32, c_i32, c_f32,
+                                           c_void_p, c_void_p]),
     "hgd_bernoulli_mask_dev_pair": (c_i32, [c_void_p, c_void_p, c_i64, c_f32, c_void_p, c_void_p,
                                             c_void_p]),
     "hgd_bernoulli_mask_dev": (c_i32, [c_void_p, c_i64, c_f32, c_void_p, c_void_p]),

@@ -17,6 +17,8 @@
 //     4 registers = the k index, in a permuted order the B operand follows); the split-j partials
 //     are summed in order and the F.normalize backward (dx = (dp − p<p,dp>)/‖x‖) is fused into
 //     that final pass. The scatter into the [N, d] table gradients is left to the caller.
+#include <algorithm>
+
 #include "device_util.h"
 #include "hgd_internal.h"
 
@@ -38,33 +40,74 @@ inline float exp2_scale(float temp) {
   return static_cast<float>(1.4426950408889634 / static_cast<double>(temp));
 }
 
+// One InfoNCE term's operands (both halves of HCCF's paired terms, HCCF.py:65-66, run as ONE
+// launch per kernel: blocks [0, nb0) along x take p[0], the rest p[1]).
+struct NceProb {
+  const float* E1;
+  int64_t ld1;
+  const float* E2;
+  int64_t ld2;
+  int64_t n_rows;
+  const int64_t* nodes;
+  int64_t B;          // capacity (strides, grid)
+  const int64_t* Bp;  // live count on the device, or NULL (= B)
+  float* P1;
+  float* P2;
+  float* inv1;
+  float* inv2;
+  float* pos_logit;
+  float* deno;
+  float* loss;
+  float* partial;  // forward [S, B]
+  float* part1;    // backward [S, B, d] (dP1 side)
+  float* part2;    // backward [S, B, d] (dP2 side)
+  int64_t per_slice;
+  int64_t S_used;
+  float* dX1;  // backward outputs: compact [B, d] rows, or scatter into dE
+  float* dX2;
+  float* dE1;
+  int64_t ldE1;
+  float* dE2;
+  int64_t ldE2;
+};
+
+struct NceGroup {
+  NceProb p[2];
+  int32_t count;
+  int32_t nb0;  // x-blocks of p[0]
+};
+
+__device__ __forceinline__ NceProb pick(const NceGroup& g, int64_t& bx) {
+  if (g.count > 1 && bx >= g.nb0) {
+    bx -= g.nb0;
+    return g.p[1];
+  }
+  return g.p[0];
+}
+
 // ---- gather + normalise: one group of G = d/4 lanes per batch row ----
 template <int G>
-__global__ __launch_bounds__(256) void k_nce_gather(const float* __restrict__ E1, int64_t ld1,
-                                                    const float* __restrict__ E2, int64_t ld2,
-                                                    const int64_t* __restrict__ nodes, int64_t B,
-                                                    int64_t n_rows, int32_t d, float inv_temp,
-                                                    float* P1,
-                                                    float* P2, float* inv1, float* inv2,
-                                                    float* pos_logit, const int64_t* Bp) {
+__global__ __launch_bounds__(256) void k_nce_gather(NceGroup grp, int32_t d, float inv_temp) {
   constexpr int GPB = 256 / G;
   const int g = threadIdx.x / G;
   const int l = threadIdx.x % G;
-  const int64_t b = static_cast<int64_t>(blockIdx.x) * GPB + g;
-  if (b >= B) return;
-  if (Bp && b >= *Bp) return;  // a capacity row past the device-side count: never read
+  int64_t bx = blockIdx.x;
+  const NceProb p = pick(grp, bx);
+  const int64_t b = bx * GPB + g;
+  if (b >= p.B) return;
+  if (p.Bp && b >= *p.Bp) return;  // a capacity row past the device-side count: never read
   // torch indexing semantics: negative ids count from the end (the reference passes
   // torch.unique(emb.long()), HCCF.py:65-66, which yields -1 / 0 / 1); out-of-range ids are
   // rejected by the caller — clamped here only so that no load leaves the table
-  int64_t node = nodes[b];
-  if (node < 0) node += n_rows;
-  node = node < 0 ? 0 : (node >= n_rows ? n_rows - 1 : node);
+  int64_t node = p.nodes[b];
+  if (node < 0) node += p.n_rows;
+  node = node < 0 ? 0 : (node >= p.n_rows ? p.n_rows - 1 : node);
   const int c0 = 4 * l;
   const bool ok = c0 < d;
   f32x4 x1 = {0.f, 0.f, 0.f, 0.f}, x2 = {0.f, 0.f, 0.f, 0.f};
   if (ok) {
-    x1 = *reinterpret_cast<const f32x4*>(E1 + node * ld1 + c0) + kShift;
-    x2 = *reinterpret_cast<const f32x4*>(E2 + node * ld2 + c0) + kShift;
+    x1 = *reinterpret_cast<const f32x4*>(p.E1 + node * p.ld1 + c0) + kShift;
+    x2 = *reinterpret_cast<const f32x4*>(p.E2 + node * p.ld2 + c0) + kShift;
   }
   const float n1 = sqrtf(group_sum<G>(x1.x * x1.x + x1.y * x1.y + x1.z * x1.z + x1.w * x1.w));
   const float n2 = sqrtf(group_sum<G>(x2.x * x2.x + x2.y * x2.y + x2.z * x2.z + x2.w * x2.w));
@@ -73,13 +116,13 @@ __global__ __launch_bounds__(256) void k_nce_gather(const float* __restrict__ E1
   const f32x4 p1 = x1 * r1, p2 = x2 * r2;
   const float dot = group_sum<G>(p1.x * p2.x + p1.y * p2.y + p1.z * p2.z + p1.w * p2.w);
   if (ok) {
-    *reinterpret_cast<f32x4*>(P1 + b * d + c0) = p1;
-    *reinterpret_cast<f32x4*>(P2 + b * d + c0) = p2;
+    *reinterpret_cast<f32x4*>(p.P1 + b * d + c0) = p1;
+    *reinterpret_cast<f32x4*>(p.P2 + b * d + c0) = p2;
   }
   if (l == 0) {
-    inv1[b] = r1;
-    inv2[b] = r2;
-    pos_logit[b] = dot * inv_temp;
+    p.inv1[b] = r1;
+    p.inv2[b] = r2;
+    p.pos_logit[b] = dot * inv_temp;
   }
 }
 
@@ -147,24 +190,27 @@ __device__ __forceinline__ void lds_frag4(const float* s, int r0, int lane, f32x
 // A wave owns 16 rows of p1 (fragments in registers); the slice's p2 rows stream through LDS in
 // 32-row stages shared by the workgroup's four waves.
 template <int DQ>  // d = 4·DQ
-__global__ __launch_bounds__(256) void k_nce_rowsum(const float* __restrict__ P1,
-                                                    const float* __restrict__ P2, int64_t B,
-                                                    float k2, int64_t j_per_slice,
-                                                    float* partial, const int64_t* Bp) {
+__global__ __launch_bounds__(256) void k_nce_rowsum(NceGroup grp, float k2) {
   using St = Stage<DQ>;
   constexpr int Q4 = DQ / 4;
   __shared__ float sm[2][kStageRows * St::LDR];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int64_t Be = Bp ? *Bp : B;  // live rows (B is the capacity: strides, clamps)
-  const int64_t blk0 = static_cast<int64_t>(blockIdx.x) * 64;
+  int64_t bx = blockIdx.x;
+  const NceProb p = pick(grp, bx);
+  if (static_cast<int64_t>(blockIdx.y) >= p.S_used) return;  // uniform over the workgroup
+  const float* __restrict__ P1 = p.P1;
+  const float* __restrict__ P2 = p.P2;
+  const int64_t B = p.B;
+  const int64_t Be = p.Bp ? *p.Bp : B;  // live rows (B is the capacity: strides, clamps)
+  const int64_t blk0 = bx * 64;
   if (blk0 >= Be) return;  // uniform over the workgroup
   const int64_t b0 = blk0 + 16 * wave;
   const int d = 4 * DQ;
   f32x4 a[Q4];
   load_frag4<DQ>(P1, Be, d, b0 < Be ? b0 : blk0, lane, a);  // a wave past the end: dummy rows
-  const int64_t j_begin = static_cast<int64_t>(blockIdx.y) * j_per_slice;
-  const int64_t j_end = min(Be, j_begin + j_per_slice);
+  const int64_t j_begin = static_cast<int64_t>(blockIdx.y) * p.per_slice;
+  const int64_t j_end = min(Be, j_begin + p.per_slice);
   float psum[4] = {0.f, 0.f, 0.f, 0.f};
   f32x4 v[St::PER];
   stage_load<DQ>(P2, Be, j_begin, v);
@@ -198,7 +244,7 @@ __global__ __launch_bounds__(256) void k_nce_rowsum(const float* __restrict__ P1
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t b = b0 + 4 * (lane >> 4) + r;
-      if (b < Be) partial[static_cast<int64_t>(blockIdx.y) * B + b] = psum[r];
+      if (b < Be) p.partial[static_cast<int64_t>(blockIdx.y) * B + b] = psum[r];
     }
   }
 }
@@ -206,13 +252,14 @@ __global__ __launch_bounds__(256) void k_nce_rowsum(const float* __restrict__ P1
 // ---- finish: deno_b, loss = -(1/B) Σ_b log(exp(pos_b) / deno_b), fixed-order reductions ----
 // One workgroup; each thread's rows are summed over the S slice partials in slice order, eight
 // independent loads at a time (a serial chain of S dependent loads per row was 19 µs at B = 4096).
-__global__ __launch_bounds__(1024) void k_nce_finish(const float* __restrict__ partial,
-                                                     int64_t S, int64_t B,
-                                                     const float* __restrict__ pos_logit,
-                                                     float* deno, float* loss,
-                                                     const int64_t* Bp) {
+__global__ __launch_bounds__(1024) void k_nce_finish(NceGroup grp) {
+  const NceProb& p = grp.p[blockIdx.x];  // one workgroup per term
+  const float* __restrict__ partial = p.partial;
+  const float* __restrict__ pos_logit = p.pos_logit;
+  const int64_t S = p.S_used, B = p.B;
+  float* deno = p.deno;
   __shared__ float red[1024];
-  const int64_t Be = Bp ? *Bp : B;
+  const int64_t Be = p.Bp ? *p.Bp : B;
   float acc = 0.f;
   for (int64_t b = threadIdx.x; b < Be; b += 1024) {
     float den = 0.f;
@@ -235,7 +282,7 @@ __global__ __launch_bounds__(1024) void k_nce_finish(const float* __restrict__ p
     if (static_cast<int>(threadIdx.x) < w) red[threadIdx.x] += red[threadIdx.x + w];
     __syncthreads();
   }
-  if (threadIdx.x == 0) *loss = -red[0] / static_cast<float>(Be);
+  if (threadIdx.x == 0) *p.loss = -red[0] / static_cast<float>(Be);
 }
 
 // ---- backward partials ----
@@ -248,12 +295,8 @@ __global__ __launch_bounds__(1024) void k_nce_finish(const float* __restrict__ p
 // the accumulation (feature on the lane) — the LDS read replaces the per-lane strided scalar
 // loads of that operand.
 template <int DQ, bool ROWS>
-__global__ __launch_bounds__(256) void k_nce_bwd(const float* __restrict__ P1,
-                                                 const float* __restrict__ P2, int64_t B,
-                                                 float k2, const float* __restrict__ deno,
-                                                 const float* __restrict__ grad, float temp,
-                                                 int64_t k_per_slice, float* part,
-                                                 const int64_t* Bp) {
+__global__ __launch_bounds__(256) void k_nce_bwd(NceGroup grp, float k2,
+                                                 const float* __restrict__ grad, float temp) {
   using St = Stage<DQ>;
   constexpr int Q4 = DQ / 4;
   __shared__ float sm[2][kStageRows * St::LDR];
@@ -263,8 +306,16 @@ __global__ __launch_bounds__(256) void k_nce_bwd(const float* __restrict__ P1,
   const int i16 = lane & 15;
   const int h = lane >> 4;
   const int d = 4 * DQ;
-  const int64_t Be = Bp ? *Bp : B;  // live rows (B is the capacity: strides, clamps)
-  const int64_t blk0 = static_cast<int64_t>(blockIdx.x) * 64;
+  int64_t bx = blockIdx.x;
+  const NceProb p = pick(grp, bx);
+  if (static_cast<int64_t>(blockIdx.y) >= p.S_used) return;  // uniform over the workgroup
+  const float* __restrict__ P1 = p.P1;
+  const float* __restrict__ P2 = p.P2;
+  const float* __restrict__ deno = p.deno;
+  const int64_t B = p.B;
+  float* part = ROWS ? p.part1 : p.part2;
+  const int64_t Be = p.Bp ? *p.Bp : B;  // live rows (B is the capacity: strides, clamps)
+  const int64_t blk0 = bx * 64;
   if (blk0 >= Be) return;  // uniform over the workgroup
   // upstream dL/dloss and the 1/(B·τ) of the mean: device values, no host sync
   const float coef = grad[0] / (static_cast<float>(Be) * temp);
@@ -277,8 +328,8 @@ __global__ __launch_bounds__(256) void k_nce_bwd(const float* __restrict__ P1,
   const int64_t o_lane = o0 + i16;  // own row of this lane in the logit tile below
   float inv_own = 1.f;
   if (ROWS) inv_own = 1.f / deno[o_lane < Be ? o_lane : Be - 1];
-  const int64_t k_begin = static_cast<int64_t>(blockIdx.y) * k_per_slice;
-  const int64_t k_end = min(Be, k_begin + k_per_slice);
+  const int64_t k_begin = static_cast<int64_t>(blockIdx.y) * p.per_slice;
+  const int64_t k_end = min(Be, k_begin + p.per_slice);
   f32x4 acc[DQ / 4];
 #pragma unroll
   for (int t = 0; t < DQ / 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -353,22 +404,26 @@ __global__ __launch_bounds__(256) void k_nce_bwd(const float* __restrict__ P1,
 }
 
 // ---- sum the split partials in order and apply the F.normalize backward per row ----
-template <int G>
-__global__ __launch_bounds__(256) void k_nce_norm_bwd(const float* __restrict__ part, int64_t S,
-                                                      int64_t B, int32_t d,
-                                                      const float* __restrict__ P,
-                                                      const float* __restrict__ inv, float* dX,
-                                                      const int64_t* Bp,
-                                                      const int64_t* __restrict__ nodes,
-                                                      int64_t n_rows, float* dE, int64_t ldE) {
+template <int G, bool SIDE1>
+__global__ __launch_bounds__(256) void k_nce_norm_bwd(NceGroup grp, int32_t d) {
   constexpr int GPB = 256 / G;
   const int g = threadIdx.x / G;
   const int l = threadIdx.x % G;
-  const int64_t b = static_cast<int64_t>(blockIdx.x) * GPB + g;
+  int64_t bx = blockIdx.x;
+  const NceProb q = pick(grp, bx);
+  const float* __restrict__ part = SIDE1 ? q.part1 : q.part2;
+  const float* __restrict__ P = SIDE1 ? q.P1 : q.P2;
+  const float* __restrict__ inv = SIDE1 ? q.inv1 : q.inv2;
+  float* dX = SIDE1 ? q.dX1 : q.dX2;
+  float* dE = SIDE1 ? q.dE1 : q.dE2;
+  const int64_t ldE = SIDE1 ? q.ldE1 : q.ldE2;
+  if (!dX && !dE) return;  // this term does not want this side (uniform)
+  const int64_t S = q.S_used, B = q.B, n_rows = q.n_rows;
+  const int64_t b = bx * GPB + g;
   if (b >= B) return;
   const int c0 = 4 * l;
   const bool ok = c0 < d;
-  if (Bp && b >= *Bp) {  // capacity row: a zero gradient row, or nothing to scatter
+  if (q.Bp && b >= *q.Bp) {  // capacity row: a zero gradient row, or nothing to scatter
     if (ok && dX) *reinterpret_cast<f32x4*>(dX + b * d + c0) = f32x4{0.f, 0.f, 0.f, 0.f};
     return;
   }
@@ -387,7 +442,7 @@ __global__ __launch_bounds__(256) void k_nce_norm_bwd(const float* __restrict__ 
     // scatter-add into the [n_rows, d] table gradient at this batch row's node (torch indexing:
     // negative ids wrap). At most two batch rows meet on one table row (x and x − n), and a sum
     // of two terms onto 0 is order-independent, so the atomics stay deterministic.
-    int64_t node = nodes[b];
+    int64_t node = q.nodes[b];
     if (node < 0) node += n_rows;
     node = node < 0 ? 0 : (node >= n_rows ? n_rows - 1 : node);
     float* row = dE + node * ldE + c0;
@@ -435,134 +490,178 @@ extern "C" size_t hgd_infonce_workspace_size(int64_t batch, int32_t d) {
 namespace hgd {
 namespace {
 
-hgd_status infonce_forward(const float* E1, int64_t ld1, const float* E2, int64_t ld2,
-                           int64_t n_rows, const int64_t* nodes, int64_t batch,
-                           const int64_t* batch_count, int32_t d, float temp, float* P1,
-                           float* P2, float* inv_norm1, float* inv_norm2, float* pos_logit,
-                           float* deno, float* loss, void* workspace, size_t workspace_bytes,
-                           void* stream) {
-  HGD_REQUIRE(batch > 0 && n_rows > 0, "hgd_infonce_forward: empty batch or table");
-  HGD_REQUIRE(d % 16 == 0 && d >= 16 && d <= 256,
-              "hgd_infonce_forward: d = %d must be a multiple of 16 in [16, 256]", d);
-  HGD_REQUIRE(temp > 0.f, "hgd_infonce_forward: temperature must be > 0");
-  HGD_REQUIRE(ld1 >= d && ld2 >= d && ld1 % 4 == 0 && ld2 % 4 == 0,
-              "hgd_infonce_forward: leading dimensions must be >= d and multiples of 4");
-  HGD_REQUIRE(E1 && E2 && nodes && P1 && P2 && inv_norm1 && inv_norm2 && pos_logit && deno && loss,
-              "hgd_infonce_forward: null pointer");
-  HGD_REQUIRE(reinterpret_cast<uintptr_t>(E1) % 16 == 0 && reinterpret_cast<uintptr_t>(E2) % 16 == 0,
-              "hgd_infonce_forward: tables must be 16-byte aligned");
-  const size_t need = hgd_infonce_workspace_size(batch, d);
-  if (workspace_bytes < need || !workspace)
-    return fail(HGD_ERR_WORKSPACE, "hgd_infonce_forward: workspace %zu < required %zu",
-                workspace_bytes, need);
-  hipStream_t st = as_stream(stream);
+// Checks one term and fills its problem descriptor (workspace partition, slice plan).
+hgd_status prepare(const hgd_infonce_term& t, int32_t d, bool backward, NceProb* p,
+                   const char* fn) {
+  HGD_REQUIRE(t.capacity > 0, "%s: empty batch", fn);
+  HGD_REQUIRE(d % 16 == 0 && d >= 16 && d <= 256, "%s: d = %d must be a multiple of 16 in [16, 256]",
+              fn, d);
+  const size_t need = hgd_infonce_workspace_size(t.capacity, d);
+  if (t.workspace_bytes < need || !t.workspace)
+    return fail(HGD_ERR_WORKSPACE, "%s: workspace %zu < required %zu", fn, t.workspace_bytes,
+                need);
+  HGD_REQUIRE(t.P1 && t.P2 && t.inv_norm1 && t.inv_norm2 && t.deno, "%s: null pointer", fn);
+  if (!backward) {
+    HGD_REQUIRE(t.n_rows > 0, "%s: empty table", fn);
+    HGD_REQUIRE(t.ld1 >= d && t.ld2 >= d && t.ld1 % 4 == 0 && t.ld2 % 4 == 0,
+                "%s: leading dimensions must be >= d and multiples of 4", fn);
+    HGD_REQUIRE(t.E1 && t.E2 && t.nodes && t.pos_logit && t.loss, "%s: null pointer", fn);
+    HGD_REQUIRE(reinterpret_cast<uintptr_t>(t.E1) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(t.E2) % 16 == 0,
+                "%s: tables must be 16-byte aligned", fn);
+  } else {
+    const bool side1 = t.dX1 || t.dE1, side2 = t.dX2 || t.dE2;
+    HGD_REQUIRE(side1 || side2, "%s: no output", fn);
+    HGD_REQUIRE(!(t.dE1 || t.dE2) || (t.nodes && t.n_rows > 0 && (!t.dE1 || t.ldE1 >= d) &&
+                                      (!t.dE2 || t.ldE2 >= d)),
+                "%s: a table scatter needs nodes, n_rows and ld >= d", fn);
+  }
+  const int64_t B = t.capacity;
+  const int64_t S = slices_for(B);
+  const int64_t ps = per_slice(B, S);
+  NceProb& q = *p;
+  q = NceProb{};
+  q.E1 = t.E1; q.ld1 = t.ld1; q.E2 = t.E2; q.ld2 = t.ld2; q.n_rows = t.n_rows;
+  q.nodes = t.nodes; q.B = B; q.Bp = t.batch_count;
+  q.P1 = t.P1; q.P2 = t.P2; q.inv1 = t.inv_norm1; q.inv2 = t.inv_norm2;
+  q.pos_logit = t.pos_logit; q.deno = t.deno; q.loss = t.loss;
+  char* ws = static_cast<char*>(t.workspace);
+  const size_t off = align_up(static_cast<size_t>(S) * B * 4);
+  q.partial = reinterpret_cast<float*>(ws);
+  q.part1 = reinterpret_cast<float*>(ws + off);
+  q.part2 = reinterpret_cast<float*>(ws + off + align_up(static_cast<size_t>(S) * B * d * 4));
+  q.per_slice = ps;
+  q.S_used = (B + ps - 1) / ps;
+  q.dX1 = t.dX1; q.dX2 = t.dX2; q.dE1 = t.dE1; q.ldE1 = t.ldE1; q.dE2 = t.dE2; q.ldE2 = t.ldE2;
+  return HGD_OK;
+}
+
+// x-blocks of each term for a kernel with `rows_per_block` batch rows per workgroup
+NceGroup group_of(const NceProb* p, int count, int64_t rows_per_block, unsigned* grid_x) {
+  NceGroup g{};
+  g.count = count;
+  int64_t total = 0;
+  for (int i = 0; i < count; ++i) {
+    g.p[i] = p[i];
+    const int64_t nb = (p[i].B + rows_per_block - 1) / rows_per_block;
+    if (i == 0) g.nb0 = static_cast<int32_t>(nb);
+    total += nb;
+  }
+  *grid_x = static_cast<unsigned>(total);
+  return g;
+}
+
+hgd_status infonce_forward(const hgd_infonce_term* terms, int count, int32_t d, float temp,
+                           hipStream_t st, const char* fn) {
+  HGD_REQUIRE(terms && count >= 1 && count <= 2, "%s: 1 or 2 terms", fn);
+  HGD_REQUIRE(temp > 0.f, "%s: temperature must be > 0", fn);
+  NceProb p[2];
+  int64_t s_max = 1;
+  for (int i = 0; i < count; ++i) {
+    const hgd_status c = prepare(terms[i], d, false, &p[i], fn);
+    if (c != HGD_OK) return c;
+    s_max = std::max<int64_t>(s_max, p[i].S_used);
+  }
   const float inv_temp = 1.f / temp;
   const float k2 = exp2_scale(temp);
   const int G = group_for(d);
-  const int64_t gpb = 256 / G;
-  const dim3 gg(static_cast<unsigned>((batch + gpb - 1) / gpb));
+  unsigned gx = 0;
+  NceGroup gg = group_of(p, count, 256 / G, &gx);
   switch (G) {
-    case 4: hipLaunchKernelGGL((k_nce_gather<4>), gg, dim3(256), 0, st, E1, ld1, E2, ld2, nodes, batch, n_rows, d, inv_temp, P1, P2, inv_norm1, inv_norm2, pos_logit, batch_count); break;
-    case 8: hipLaunchKernelGGL((k_nce_gather<8>), gg, dim3(256), 0, st, E1, ld1, E2, ld2, nodes, batch, n_rows, d, inv_temp, P1, P2, inv_norm1, inv_norm2, pos_logit, batch_count); break;
-    case 16: hipLaunchKernelGGL((k_nce_gather<16>), gg, dim3(256), 0, st, E1, ld1, E2, ld2, nodes, batch, n_rows, d, inv_temp, P1, P2, inv_norm1, inv_norm2, pos_logit, batch_count); break;
-    case 32: hipLaunchKernelGGL((k_nce_gather<32>), gg, dim3(256), 0, st, E1, ld1, E2, ld2, nodes, batch, n_rows, d, inv_temp, P1, P2, inv_norm1, inv_norm2, pos_logit, batch_count); break;
-    default: hipLaunchKernelGGL((k_nce_gather<64>), gg, dim3(256), 0, st, E1, ld1, E2, ld2, nodes, batch, n_rows, d, inv_temp, P1, P2, inv_norm1, inv_norm2, pos_logit, batch_count); break;
+    case 4: hipLaunchKernelGGL((k_nce_gather<4>), dim3(gx), dim3(256), 0, st, gg, d, inv_temp); break;
+    case 8: hipLaunchKernelGGL((k_nce_gather<8>), dim3(gx), dim3(256), 0, st, gg, d, inv_temp); break;
+    case 16: hipLaunchKernelGGL((k_nce_gather<16>), dim3(gx), dim3(256), 0, st, gg, d, inv_temp); break;
+    case 32: hipLaunchKernelGGL((k_nce_gather<32>), dim3(gx), dim3(256), 0, st, gg, d, inv_temp); break;
+    default: hipLaunchKernelGGL((k_nce_gather<64>), dim3(gx), dim3(256), 0, st, gg, d, inv_temp); break;
   }
-  hgd_status s = check_launch("hgd_infonce_forward gather");
+  hgd_status s = check_launch("hgd_infonce forward gather");
   if (s != HGD_OK) return s;
-  const int64_t S = slices_for(batch);
-  const int64_t jps = per_slice(batch, S);
-  const int64_t S_used = (batch + jps - 1) / jps;
-  float* partial = static_cast<float*>(workspace);
-  const dim3 gr(static_cast<unsigned>((batch + 63) / 64), static_cast<unsigned>(S_used));
+  NceGroup gr = group_of(p, count, 64, &gx);
+  const dim3 grid(gx, static_cast<unsigned>(s_max));
   switch (d / 4) {
-#define HGD_CASE(DQ)                                                                              \
-    case DQ:                                                                                      \
-      hipLaunchKernelGGL((k_nce_rowsum<DQ>), gr, dim3(256), 0, st, P1, P2, batch, k2, jps,       \
-                         partial, batch_count);                                                   \
+#define HGD_CASE(DQ)                                                                       \
+    case DQ:                                                                               \
+      hipLaunchKernelGGL((k_nce_rowsum<DQ>), grid, dim3(256), 0, st, gr, k2);              \
       break;
     HGD_CASE(4) HGD_CASE(8) HGD_CASE(12) HGD_CASE(16) HGD_CASE(20) HGD_CASE(24) HGD_CASE(28)
     HGD_CASE(32) HGD_CASE(36) HGD_CASE(40) HGD_CASE(44) HGD_CASE(48) HGD_CASE(52) HGD_CASE(56)
     HGD_CASE(60) HGD_CASE(64)
 #undef HGD_CASE
-    default: return fail(HGD_ERR_UNSUPPORTED, "hgd_infonce_forward: d = %d", d);
+    default: return fail(HGD_ERR_UNSUPPORTED, "%s: d = %d", fn, d);
   }
-  s = check_launch("hgd_infonce_forward rowsum");
+  s = check_launch("hgd_infonce forward rowsum");
   if (s != HGD_OK) return s;
-  hipLaunchKernelGGL(k_nce_finish, dim3(1), dim3(1024), 0, st, partial, S_used, batch, pos_logit,
-                     deno, loss, batch_count);
-  return check_launch("hgd_infonce_forward finish");
+  hipLaunchKernelGGL(k_nce_finish, dim3(count), dim3(1024), 0, st, gr);
+  return check_launch("hgd_infonce forward finish");
 }
 
-
-hgd_status infonce_backward(const float* P1, const float* P2, const float* inv_norm1,
-                            const float* inv_norm2, const float* deno, int64_t batch,
-                            const int64_t* batch_count, int32_t d, float temp,
-                            const float* grad_loss, float* dX1, float* dX2,
-                            const int64_t* nodes, int64_t n_rows, float* dE1, int64_t ldE1,
-                            float* dE2, int64_t ldE2, void* workspace,
-                            size_t workspace_bytes, void* stream) {
-  HGD_REQUIRE(batch > 0, "hgd_infonce_backward: empty batch");
-  HGD_REQUIRE(d % 16 == 0 && d >= 16 && d <= 256,
-              "hgd_infonce_backward: d = %d must be a multiple of 16 in [16, 256]", d);
-  HGD_REQUIRE(temp > 0.f, "hgd_infonce_backward: temperature must be > 0");
-  HGD_REQUIRE(P1 && P2 && inv_norm1 && inv_norm2 && deno && grad_loss,
-              "hgd_infonce_backward: null pointer");
-  const bool side1 = dX1 || dE1, side2 = dX2 || dE2;  // a side without an output is skipped
-  HGD_REQUIRE(side1 || side2, "hgd_infonce_backward: no output");
-  HGD_REQUIRE(!(dE1 || dE2) || (nodes && n_rows > 0 && (!dE1 || ldE1 >= d) &&
-                                (!dE2 || ldE2 >= d)),
-              "hgd_infonce_backward: a table scatter needs nodes, n_rows and ld >= d");
-  const size_t need = hgd_infonce_workspace_size(batch, d);
-  if (workspace_bytes < need || !workspace)
-    return fail(HGD_ERR_WORKSPACE, "hgd_infonce_backward: workspace %zu < required %zu",
-                workspace_bytes, need);
-  hipStream_t st = as_stream(stream);
+hgd_status infonce_backward(const hgd_infonce_term* terms, int count, int32_t d, float temp,
+                            const float* grad_loss, hipStream_t st, const char* fn) {
+  HGD_REQUIRE(terms && count >= 1 && count <= 2, "%s: 1 or 2 terms", fn);
+  HGD_REQUIRE(temp > 0.f, "%s: temperature must be > 0", fn);
+  HGD_REQUIRE(grad_loss, "%s: null grad_loss", fn);
+  NceProb p[2];
+  int64_t s_max = 1;
+  bool side1 = false, side2 = false;
+  for (int i = 0; i < count; ++i) {
+    const hgd_status c = prepare(terms[i], d, true, &p[i], fn);
+    if (c != HGD_OK) return c;
+    s_max = std::max<int64_t>(s_max, p[i].S_used);
+    side1 = side1 || p[i].dX1 || p[i].dE1;
+    side2 = side2 || p[i].dX2 || p[i].dE2;
+  }
+  // a side is computed for every term of the launch when any term wants it (its partials go
+  // to that term's workspace; the norm pass skips a term without that side's output)
   const float k2 = exp2_scale(temp);
-  const int64_t S = slices_for(batch);
-  const int64_t kps = per_slice(batch, S);
-  const int64_t S_used = (batch + kps - 1) / kps;
-  char* ws = static_cast<char*>(workspace);
-  const size_t off = align_up(static_cast<size_t>(S) * batch * 4);
-  float* part1 = reinterpret_cast<float*>(ws + off);
-  float* part2 = reinterpret_cast<float*>(ws + off + align_up(static_cast<size_t>(S) * batch * d * 4));
-  const dim3 gr(static_cast<unsigned>((batch + 63) / 64), static_cast<unsigned>(S_used));
+  unsigned gx = 0;
+  NceGroup gr = group_of(p, count, 64, &gx);
+  const dim3 grid(gx, static_cast<unsigned>(s_max));
   switch (d / 4) {
-#define HGD_CASE(DQ)                                                                              \
-    case DQ:                                                                                      \
-      if (side1)                                                                                  \
-        hipLaunchKernelGGL((k_nce_bwd<DQ, true>), gr, dim3(256), 0, st, P1, P2, batch, k2,       \
-                           deno, grad_loss, temp, kps, part1, batch_count);                        \
-      if (side2)                                                                                  \
-        hipLaunchKernelGGL((k_nce_bwd<DQ, false>), gr, dim3(256), 0, st, P1, P2, batch,          \
-                           k2, deno, grad_loss, temp, kps, part2, batch_count);                    \
+#define HGD_CASE(DQ)                                                                           \
+    case DQ:                                                                                   \
+      if (side1)                                                                               \
+        hipLaunchKernelGGL((k_nce_bwd<DQ, true>), grid, dim3(256), 0, st, gr, k2, grad_loss,   \
+                           temp);                                                              \
+      if (side2)                                                                               \
+        hipLaunchKernelGGL((k_nce_bwd<DQ, false>), grid, dim3(256), 0, st, gr, k2, grad_loss,  \
+                           temp);                                                              \
       break;
     HGD_CASE(4) HGD_CASE(8) HGD_CASE(12) HGD_CASE(16) HGD_CASE(20) HGD_CASE(24) HGD_CASE(28)
     HGD_CASE(32) HGD_CASE(36) HGD_CASE(40) HGD_CASE(44) HGD_CASE(48) HGD_CASE(52) HGD_CASE(56)
     HGD_CASE(60) HGD_CASE(64)
 #undef HGD_CASE
-    default: return fail(HGD_ERR_UNSUPPORTED, "hgd_infonce_backward: d = %d", d);
+    default: return fail(HGD_ERR_UNSUPPORTED, "%s: d = %d", fn, d);
   }
-  hgd_status s = check_launch("hgd_infonce_backward partials");
+  hgd_status s = check_launch("hgd_infonce backward partials");
   if (s != HGD_OK) return s;
   const int G = group_for(d);
-  const int64_t gpb = 256 / G;
-  const dim3 gn(static_cast<unsigned>((batch + gpb - 1) / gpb));
+  NceGroup gn = group_of(p, count, 256 / G, &gx);
   switch (G) {
 #define HGD_CASE(GG)                                                                         \
     case GG:                                                                                 \
       if (side1)                                                                             \
-        hipLaunchKernelGGL((k_nce_norm_bwd<GG>), gn, dim3(256), 0, st, part1, S_used, batch, \
-                           d, P1, inv_norm1, dX1, batch_count, nodes, n_rows, dE1, ldE1);    \
+        hipLaunchKernelGGL((k_nce_norm_bwd<GG, true>), dim3(gx), dim3(256), 0, st, gn, d);  \
       if (side2)                                                                             \
-        hipLaunchKernelGGL((k_nce_norm_bwd<GG>), gn, dim3(256), 0, st, part2, S_used, batch, \
-                           d, P2, inv_norm2, dX2, batch_count, nodes, n_rows, dE2, ldE2);    \
+        hipLaunchKernelGGL((k_nce_norm_bwd<GG, false>), dim3(gx), dim3(256), 0, st, gn, d); \
       break;
     HGD_CASE(4) HGD_CASE(8) HGD_CASE(16) HGD_CASE(32) HGD_CASE(64)
 #undef HGD_CASE
-    default: return fail(HGD_ERR_UNSUPPORTED, "hgd_infonce_backward: group %d", G);
+    default: return fail(HGD_ERR_UNSUPPORTED, "%s: group %d", fn, G);
   }
-  return check_launch("hgd_infonce_backward norm");
+  return check_launch("hgd_infonce backward norm");
+}
+
+hgd_infonce_term term_of(const float* E1, int64_t ld1, const float* E2, int64_t ld2,
+                         int64_t n_rows, const int64_t* nodes, int64_t capacity,
+                         const int64_t* batch_count, float* P1, float* P2, float* inv1,
+                         float* inv2, float* pos_logit, float* deno, float* loss, void* ws,
+                         size_t wsb) {
+  hgd_infonce_term t{};
+  t.E1 = E1; t.ld1 = ld1; t.E2 = E2; t.ld2 = ld2; t.n_rows = n_rows; t.nodes = nodes;
+  t.capacity = capacity; t.batch_count = batch_count; t.P1 = P1; t.P2 = P2;
+  t.inv_norm1 = inv1; t.inv_norm2 = inv2; t.pos_logit = pos_logit; t.deno = deno; t.loss = loss;
+  t.workspace = ws; t.workspace_bytes = wsb;
+  return t;
 }
 
 }  // namespace
@@ -576,9 +675,10 @@ extern "C" hgd_status hgd_infonce_forward(const float* E1, int64_t ld1, const fl
                                           void* workspace, size_t workspace_bytes,
                                           void* stream) {
   hgd::clear_error();
-  return hgd::infonce_forward(E1, ld1, E2, ld2, n_rows, nodes, batch, nullptr, d, temp, P1, P2,
-                              inv_norm1, inv_norm2, pos_logit, deno, loss, workspace,
-                              workspace_bytes, stream);
+  const hgd_infonce_term t = hgd::term_of(E1, ld1, E2, ld2, n_rows, nodes, batch, nullptr, P1,
+                                          P2, inv_norm1, inv_norm2, pos_logit, deno, loss,
+                                          workspace, workspace_bytes);
+  return hgd::infonce_forward(&t, 1, d, temp, hgd::as_stream(stream), "hgd_infonce_forward");
 }
 
 extern "C" hgd_status hgd_infonce_forward_n(const float* E1, int64_t ld1, const float* E2,
@@ -590,9 +690,10 @@ extern "C" hgd_status hgd_infonce_forward_n(const float* E1, int64_t ld1, const 
                                             size_t workspace_bytes, void* stream) {
   hgd::clear_error();
   HGD_REQUIRE(batch_count, "hgd_infonce_forward_n: null batch_count");
-  return hgd::infonce_forward(E1, ld1, E2, ld2, n_rows, nodes, capacity, batch_count, d, temp,
-                              P1, P2, inv_norm1, inv_norm2, pos_logit, deno, loss, workspace,
-                              workspace_bytes, stream);
+  const hgd_infonce_term t = hgd::term_of(E1, ld1, E2, ld2, n_rows, nodes, capacity, batch_count,
+                                          P1, P2, inv_norm1, inv_norm2, pos_logit, deno, loss,
+                                          workspace, workspace_bytes);
+  return hgd::infonce_forward(&t, 1, d, temp, hgd::as_stream(stream), "hgd_infonce_forward_n");
 }
 
 extern "C" hgd_status hgd_infonce_backward(const float* P1, const float* P2,
@@ -603,9 +704,15 @@ extern "C" hgd_status hgd_infonce_backward(const float* P1, const float* P2,
                                            void* stream) {
   hgd::clear_error();
   HGD_REQUIRE(dX1 && dX2, "hgd_infonce_backward: null dX1/dX2");
-  return hgd::infonce_backward(P1, P2, inv_norm1, inv_norm2, deno, batch, nullptr, d, temp,
-                               grad_loss, dX1, dX2, nullptr, 0, nullptr, 0, nullptr, 0,
-                               workspace, workspace_bytes, stream);
+  hgd_infonce_term t = hgd::term_of(nullptr, 0, nullptr, 0, 0, nullptr, batch, nullptr,
+                                    const_cast<float*>(P1), const_cast<float*>(P2),
+                                    const_cast<float*>(inv_norm1), const_cast<float*>(inv_norm2),
+                                    nullptr, const_cast<float*>(deno), nullptr, workspace,
+                                    workspace_bytes);
+  t.dX1 = dX1;
+  t.dX2 = dX2;
+  return hgd::infonce_backward(&t, 1, d, temp, grad_loss, hgd::as_stream(stream),
+                               "hgd_infonce_backward");
 }
 
 extern "C" hgd_status hgd_infonce_backward_n(const float* P1, const float* P2,
@@ -618,7 +725,30 @@ extern "C" hgd_status hgd_infonce_backward_n(const float* P1, const float* P2,
                                              size_t workspace_bytes, void* stream) {
   hgd::clear_error();
   HGD_REQUIRE(batch_count, "hgd_infonce_backward_n: null batch_count");
-  return hgd::infonce_backward(P1, P2, inv_norm1, inv_norm2, deno, capacity, batch_count, d,
-                               temp, grad_loss, nullptr, nullptr, nodes, n_rows, dE1, ldE1, dE2,
-                               ldE2, workspace, workspace_bytes, stream);
+  hgd_infonce_term t = hgd::term_of(nullptr, 0, nullptr, 0, n_rows, nodes, capacity,
+                                    batch_count, const_cast<float*>(P1), const_cast<float*>(P2),
+                                    const_cast<float*>(inv_norm1), const_cast<float*>(inv_norm2),
+                                    nullptr, const_cast<float*>(deno), nullptr, workspace,
+                                    workspace_bytes);
+  t.dE1 = dE1;
+  t.ldE1 = ldE1;
+  t.dE2 = dE2;
+  t.ldE2 = ldE2;
+  return hgd::infonce_backward(&t, 1, d, temp, grad_loss, hgd::as_stream(stream),
+                               "hgd_infonce_backward_n");
+}
+
+extern "C" hgd_status hgd_infonce_forward_group(const hgd_infonce_term* terms, int32_t count,
+                                                int32_t d, float temp, void* stream) {
+  hgd::clear_error();
+  return hgd::infonce_forward(terms, count, d, temp, hgd::as_stream(stream),
+                              "hgd_infonce_forward_group");
+}
+
+extern "C" hgd_status hgd_infonce_backward_group(const hgd_infonce_term* terms, int32_t count,
+                                                 int32_t d, float temp, const float* grad_loss,
+                                                 void* stream) {
+  hgd::clear_error();
+  return hgd::infonce_backward(terms, count, d, temp, grad_loss, hgd::as_stream(stream),
+                               "hgd_infonce_backward_group");
 }

@@ -504,10 +504,11 @@ class _ContrastLoss(torch.autograd.Function):
 
 class _ContrastLossPair(torch.autograd.Function):
     """The user and item contrastLoss terms of one HCCF layer on the halves of the [U + I, d]
-    tables (HCCF.py:65-66), with device counts: both InfoNCE forwards on row offsets of the
-    full tables, and in the backward ONE zeroed [U + I, d] gradient per table that both
-    scatters write into — instead of, per half, a zeroed half gradient, the slice backward's
-    zeroed full table plus copy, and the add joining the halves."""
+    tables (HCCF.py:65-66), with device counts: both InfoNCE terms as ONE launch per kernel
+    (hgd_infonce_forward_group / _backward_group, each term on its row offset of the full
+    tables), and in the backward ONE zeroed [U + I, d] gradient per table that both terms'
+    scatters write into — instead of per-term launches, per-half zeroed gradients, the slice
+    backward's zeroed full table plus copy, and the add joining the halves."""
 
     @staticmethod
     def forward(ctx, E1, E2, nu, nodes_u, count_u, nodes_i, count_i, temp: float):
@@ -518,8 +519,8 @@ class _ContrastLossPair(torch.autograd.Function):
         N = E1.shape[0]
         f = dict(dtype=torch.float32, device=dev)
         loss2 = torch.empty(2, **f)
-        st = torch.cuda.current_stream(dev).cuda_stream
-        saved = []
+        terms = (nat.InfonceTerm * 2)()
+        saved, keep = [], []
         for k, (r0, rows, nodes, count) in enumerate(((0, nu, nodes_u, count_u),
                                                       (nu, N - nu, nodes_i, count_i))):
             nodes = nodes.to(device=dev, dtype=torch.int64).contiguous()
@@ -528,13 +529,21 @@ class _ContrastLossPair(torch.autograd.Function):
             inv1, inv2, pos, deno = (torch.empty(B, **f) for _ in range(4))
             wsb = lib.hgd_infonce_workspace_size(B, d)
             ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+            t = terms[k]
             off = r0 * d * 4
-            nat.check(lib.hgd_infonce_forward_n(
-                E1c.data_ptr() + off, d, E2c.data_ptr() + off, d, rows, nodes.data_ptr(), B,
-                count.data_ptr(), d, float(temp), P1.data_ptr(), P2.data_ptr(), inv1.data_ptr(),
-                inv2.data_ptr(), pos.data_ptr(), deno.data_ptr(), loss2.data_ptr() + 4 * k,
-                ws.data_ptr(), wsb, st), "hgd_infonce_forward_n")
+            t.E1, t.ld1, t.E2, t.ld2 = E1c.data_ptr() + off, d, E2c.data_ptr() + off, d
+            t.n_rows, t.nodes, t.capacity, t.batch_count = rows, nodes.data_ptr(), B, \
+                count.data_ptr()
+            t.P1, t.P2, t.inv_norm1, t.inv_norm2 = (P1.data_ptr(), P2.data_ptr(),
+                                                    inv1.data_ptr(), inv2.data_ptr())
+            t.pos_logit, t.deno, t.loss = pos.data_ptr(), deno.data_ptr(), \
+                loss2.data_ptr() + 4 * k
+            t.workspace, t.workspace_bytes = ws.data_ptr(), wsb
             saved += [P1, P2, inv1, inv2, deno, nodes, count]
+            keep.append(ws)
+        nat.check(lib.hgd_infonce_forward_group(terms, 2, d, float(temp),
+                                                torch.cuda.current_stream(dev).cuda_stream),
+                  "hgd_infonce_forward_group")
         ctx.temp = float(temp)
         ctx.nu, ctx.N, ctx.d = nu, N, d
         ctx.save_for_backward(*saved)
@@ -552,19 +561,29 @@ class _ContrastLossPair(torch.autograd.Function):
         dE2 = torch.zeros((N, d), **f) if ctx.needs_input_grad[1] else None
         if dE1 is None and dE2 is None:
             return (None,) * 8
-        st = torch.cuda.current_stream(dev).cuda_stream
+        terms = (nat.InfonceTerm * 2)()
+        keep = []
         for k, (r0, rows) in enumerate(((0, nu), (nu, N - nu))):
             P1, P2, inv1, inv2, deno, nodes, count = saved[7 * k: 7 * k + 7]
             B = P1.shape[0]
             wsb = lib.hgd_infonce_workspace_size(B, d)
             ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+            keep.append(ws)
+            t = terms[k]
             off = r0 * d * 4
-            nat.check(lib.hgd_infonce_backward_n(
-                P1.data_ptr(), P2.data_ptr(), inv1.data_ptr(), inv2.data_ptr(), deno.data_ptr(),
-                B, count.data_ptr(), d, ctx.temp, g.data_ptr(), nodes.data_ptr(), rows,
-                dE1.data_ptr() + off if dE1 is not None else None, d,
-                dE2.data_ptr() + off if dE2 is not None else None, d, ws.data_ptr(), wsb, st),
-                "hgd_infonce_backward_n")
+            t.n_rows, t.nodes, t.capacity, t.batch_count = rows, nodes.data_ptr(), B, \
+                count.data_ptr()
+            t.P1, t.P2, t.inv_norm1, t.inv_norm2 = (P1.data_ptr(), P2.data_ptr(),
+                                                    inv1.data_ptr(), inv2.data_ptr())
+            t.deno = deno.data_ptr()
+            if dE1 is not None:
+                t.dE1, t.ldE1 = dE1.data_ptr() + off, d
+            if dE2 is not None:
+                t.dE2, t.ldE2 = dE2.data_ptr() + off, d
+            t.workspace, t.workspace_bytes = ws.data_ptr(), wsb
+        nat.check(lib.hgd_infonce_backward_group(terms, 2, d, ctx.temp, g.data_ptr(),
+                                                 torch.cuda.current_stream(dev).cuda_stream),
+                  "hgd_infonce_backward_group")
         return dE1, dE2, None, None, None, None, None, None
 
 

@@ -342,6 +342,42 @@ hgd_status hgd_infonce_backward_n(const float* P1, const float* P2, const float*
                                   float* dE1, int64_t ldE1, float* dE2, int64_t ldE2,
                                   void* workspace, size_t workspace_bytes, void* stream);
 
+/* Several InfoNCE terms in ONE launch per kernel (HCCF's user and item terms of a layer,
+ * HCCF.py:65-66): each term as hgd_infonce_forward_n / hgd_infonce_backward_n would take it
+ * (batch_count NULL = all `capacity` rows live), with its own workspace
+ * (hgd_infonce_workspace_size(capacity, d)). Backward outputs: dX1 / dX2 compact [capacity, d]
+ * rows, or dE1 / dE2 scatter-adds into [n_rows, ld] tables (nodes required); a side without an
+ * output is skipped. count is 1 or 2; all terms share d and temp. */
+typedef struct hgd_infonce_term {
+  const float* E1;
+  int64_t ld1;
+  const float* E2;
+  int64_t ld2;
+  int64_t n_rows;
+  const int64_t* nodes;
+  int64_t capacity;
+  const int64_t* batch_count;
+  float* P1;
+  float* P2;
+  float* inv_norm1;
+  float* inv_norm2;
+  float* pos_logit;
+  float* deno;
+  float* loss;
+  float* dX1;
+  float* dX2;
+  float* dE1;
+  int64_t ldE1;
+  float* dE2;
+  int64_t ldE2;
+  void* workspace;
+  size_t workspace_bytes;
+} hgd_infonce_term;
+hgd_status hgd_infonce_forward_group(const hgd_infonce_term* terms, int32_t count, int32_t d,
+                                     float temp, void* stream);
+hgd_status hgd_infonce_backward_group(const hgd_infonce_term* terms, int32_t count, int32_t d,
+                                      float temp, const float* grad_loss, void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * Ingest and graph build — the data path producing the hot path's
  * input matrices (data/loader.py:24-38, data/ui_graph.py:43-112, data/graph.py:11-25).
