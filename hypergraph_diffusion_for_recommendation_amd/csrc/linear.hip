@@ -62,7 +62,9 @@ struct RowGemmGroup {
   int32_t nb0;
 };
 
-template <int KQ, bool MASK>  // K = 16·KQ; MASK: A ⊙ (mask > 0)
+// K = 16·KQ; NT = live 16-column tiles of a 64-column slice (N < 64: no MFMAs on zero columns);
+// MASK: A ⊙ (mask > 0)
+template <int KQ, int NT, bool MASK>
 __global__ __launch_bounds__(256) void k_row_gemm(RowGemmGroup grp) {
   const bool second = grp.count > 1 && static_cast<int>(blockIdx.x) >= grp.nb0;
   const RowGemm p = second ? grp.p[1] : grp.p[0];
@@ -82,7 +84,7 @@ __global__ __launch_bounds__(256) void k_row_gemm(RowGemmGroup grp) {
   const int i16 = lane & 15;
   const int h = lane >> 4;
   const int n0 = blockIdx.y * 64;
-  const int nt = min(4, (p.N - n0) / 16);  // live 16-column tiles of this slice (uniform)
+  const int nt = min(NT, (p.N - n0) / 16);  // live 16-column tiles of this slice (uniform)
   const int64_t tiles = (p.rows + 16 * SUB - 1) / (16 * SUB);  // super-tiles
   const int64_t stride = static_cast<int64_t>(nbx) * 4;
   int64_t tile = static_cast<int64_t>(bx) * 4 + wave;
@@ -128,16 +130,16 @@ __global__ __launch_bounds__(256) void k_row_gemm(RowGemmGroup grp) {
     }
   }
   __syncthreads();
-  float bf[KQ][4][4];
+  float bf[KQ][4][NT];
 #pragma unroll
   for (int q = 0; q < KQ; ++q)
 #pragma unroll
     for (int c = 0; c < 4; ++c)
 #pragma unroll
-      for (int t = 0; t < 4; ++t) bf[q][c][t] = sB[(4 * h + 16 * q + c) * LDB + 16 * t + i16];
-  float bias_v[4];
+      for (int t = 0; t < NT; ++t) bf[q][c][t] = sB[(4 * h + 16 * q + c) * LDB + 16 * t + i16];
+  float bias_v[NT];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) bias_v[t] = (p.bias && t < nt) ? p.bias[n0 + 16 * t + i16] : 0.f;
+  for (int t = 0; t < NT; ++t) bias_v[t] = (p.bias && t < nt) ? p.bias[n0 + 16 * t + i16] : 0.f;
 
   auto compute = [&](int64_t tile, f32x4 (&a)[SUB][KQ], const f32x4 (&m)[SUB][KQ]) {
 #pragma unroll
@@ -146,17 +148,17 @@ __global__ __launch_bounds__(256) void k_row_gemm(RowGemmGroup grp) {
 #pragma unroll
         for (int q = 0; q < KQ; ++q) a[s][q] = relu_mask(a[s][q], m[s][q]);
       }
-      f32x4 acc[4];
+      f32x4 acc[NT];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int q = 0; q < KQ; ++q)
 #pragma unroll
         for (int c = 0; c < 4; ++c)
 #pragma unroll
-          for (int t = 0; t < 4; ++t) acc[t] = mfma4(a[s][q][c], bf[q][c][t], acc[t]);
+          for (int t = 0; t < NT; ++t) acc[t] = mfma4(a[s][q][c], bf[q][c][t], acc[t]);
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
+      for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float v = acc[t][r] + bias_v[t];
@@ -166,20 +168,20 @@ __global__ __launch_bounds__(256) void k_row_gemm(RowGemmGroup grp) {
       float* yb = p.Y + n0 + i16;
       if (p.accumulate) {
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
+        for (int t = 0; t < NT; ++t)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
             if (t < nt && r0 + 4 * h + r < p.rows)
               acc[t][r] += yb[(r0 + 4 * h + r) * p.ldy + 16 * t];
       }
-      if (nt == 4 && r0 + 16 <= p.rows) {
+      if (nt == NT && r0 + 16 <= p.rows) {
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
+        for (int t = 0; t < NT; ++t)
 #pragma unroll
           for (int r = 0; r < 4; ++r) yb[(r0 + 4 * h + r) * p.ldy + 16 * t] = acc[t][r];
       } else {
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
+        for (int t = 0; t < NT; ++t)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
             if (t < nt && r0 + 4 * h + r < p.rows)
@@ -372,17 +374,21 @@ hgd_status row_gemm_group(RowGemmGroup g, hipStream_t st, const char* fn) {
   blocks_for(rows, g.count, bx);
   g.nb0 = static_cast<int32_t>(bx[0]);
   const dim3 grid(static_cast<unsigned>(bx[0] + bx[1]), static_cast<unsigned>((p.N + 63) / 64));
-  switch (g.p[0].K / 16) {
-#define HGD_CASE(Q)                                                                \
-    case Q:                                                                        \
-      if (g.p[0].mask)                                                             \
-        hipLaunchKernelGGL((k_row_gemm<Q, true>), grid, dim3(256), 0, st, g);      \
-      else                                                                         \
-        hipLaunchKernelGGL((k_row_gemm<Q, false>), grid, dim3(256), 0, st, g);     \
+  // 16-column tiles per slice: 4 for N >= 64, else N / 16 (the slice is the whole N)
+  const int ntiles = g.p[0].N >= 64 ? 4 : g.p[0].N / 16;
+  switch ((g.p[0].K / 16) * 8 + ntiles) {
+#define HGD_CASE_NT(Q, T)                                                              \
+    case Q * 8 + T:                                                                    \
+      if (g.p[0].mask)                                                                 \
+        hipLaunchKernelGGL((k_row_gemm<Q, T, true>), grid, dim3(256), 0, st, g);       \
+      else                                                                             \
+        hipLaunchKernelGGL((k_row_gemm<Q, T, false>), grid, dim3(256), 0, st, g);      \
       break;
+#define HGD_CASE(Q) HGD_CASE_NT(Q, 1) HGD_CASE_NT(Q, 2) HGD_CASE_NT(Q, 3) HGD_CASE_NT(Q, 4)
     HGD_CASE(1) HGD_CASE(2) HGD_CASE(3) HGD_CASE(4) HGD_CASE(5) HGD_CASE(6) HGD_CASE(7)
     HGD_CASE(8)
 #undef HGD_CASE
+#undef HGD_CASE_NT
     default:
       return fail(HGD_ERR_UNSUPPORTED, "%s: K = %d (needs 16..128, multiple of 16)", fn,
                   g.p[0].K);
