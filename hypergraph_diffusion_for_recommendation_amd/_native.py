@@ -91,6 +91,13 @@ class GemmRowsDesc(ctypes.Structure):
         ("rows", c_i64),
         ("K", c_i32),
         ("N", c_i32),
+        ("drop_seed", c_void_p),
+        ("drop_keep", c_f32),
+        ("drop_scale", c_f32),
+        ("res", c_void_p),
+        ("ldres", c_i64),
+        ("Y2", c_void_p),
+        ("ldy2", c_i64),
     ]
 
 
@@ -291,6 +298,7 @@ _SIGNATURES = {
     "hgd_epilogue_backward": (c_i32, [c_void_p, c_void_p, c_i64, c_i32, c_f32, c_void_p,
                                       c_void_p]),
     "hgd_sum_slices": (c_i32, [c_void_p, c_i64, c_i64, c_i64, c_void_p, c_void_p]),
+    "hgd_dropout_apply": (c_i32, [c_void_p, c_i64, c_void_p, c_f32, c_f32, c_void_p, c_void_p]),
     "hgd_bpr_workspace_size": (c_size, [c_i64, c_i64]),
     "hgd_bpr_forward": (c_i32, [c_void_p, c_i64, c_i64, c_i64, c_i32, c_void_p, c_void_p,
                                 c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_void_p,

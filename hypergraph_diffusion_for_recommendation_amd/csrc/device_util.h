@@ -54,6 +54,35 @@ __device__ __forceinline__ void store_vec(float* p, const float (&v)[VEC]) {
   }
 }
 
+// SplitMix64 finaliser (the counter-based RNGs of the device drop-edge and dropout draws).
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+// 32-bit integer finaliser ("lowbias32": two multiplies, three xor-shifts).
+__device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+// Dropout keep-bit of element i (< 2^32) of a draw (nn.Dropout(p): keep with probability
+// keep = 1 - p): h = lowbias32(lowbias32(i + lo32(seed)) ^ hi32(seed)), u = (h >> 8)·2^-24,
+// kept iff floor(u + keep) != 0 — 32-bit arithmetic only, so it costs a few VALU slots beside
+// the MFMAs of the Linear it rides in (oracle: hgd_oracle.dropout_keep_mask).
+__device__ __forceinline__ bool dropout_keep(uint64_t seed, uint32_t i, float keep) {
+  const uint32_t h = lowbias32(lowbias32(i + static_cast<uint32_t>(seed)) ^
+                               static_cast<uint32_t>(seed >> 32));
+  const float u = static_cast<float>(h >> 8) * (1.0f / 16777216.0f);
+  return floorf(u + keep) != 0.f;
+}
+
 inline int next_pow2(int x) {
   int p = 1;
   while (p < x) p <<= 1;

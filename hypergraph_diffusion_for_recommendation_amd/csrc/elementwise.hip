@@ -6,6 +6,7 @@
 //             pre-activation, or on the output when slope >= 0 (same sign).
 //   sum_slices: the layer sum of HCCF's encoder, sum(hidden) (model/graph/HCCF.py:188), over
 //             the hidden tables stored as slices of one buffer — one pass instead of L adds.
+#include "device_util.h"
 #include "hgd_internal.h"
 
 namespace hgd {
@@ -77,6 +78,26 @@ __global__ void k_sum_slices(const float* __restrict__ P, int64_t S, int64_t str
   }
 }
 
+// nn.Dropout on the device RNG of dropout_keep (device_util.h): y[i] = keep(i) ? x[i]·scale : 0.
+// The same call on the upstream gradient with the same seed is the backward (no stored mask).
+__global__ void k_dropout(const float* __restrict__ x, int64_t n, const uint64_t* __restrict__ seed_p,
+                          float keep, float scale, float* __restrict__ y) {
+  const uint64_t seed = *seed_p;
+  const int64_t i4 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) * 4;
+  if (i4 + 3 < n) {
+    float4 v = *reinterpret_cast<const float4*>(x + i4);
+    const uint32_t j = static_cast<uint32_t>(i4);
+    v.x = dropout_keep(seed, j, keep) ? v.x * scale : 0.f;
+    v.y = dropout_keep(seed, j + 1, keep) ? v.y * scale : 0.f;
+    v.z = dropout_keep(seed, j + 2, keep) ? v.z * scale : 0.f;
+    v.w = dropout_keep(seed, j + 3, keep) ? v.w * scale : 0.f;
+    *reinterpret_cast<float4*>(y + i4) = v;
+  } else {
+    for (int64_t i = i4; i < n; ++i)
+      y[i] = dropout_keep(seed, static_cast<uint32_t>(i), keep) ? x[i] * scale : 0.f;
+  }
+}
+
 inline bool aligned16(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
 
 }  // namespace hgd
@@ -117,4 +138,17 @@ extern "C" hgd_status hgd_sum_slices(const float* P, int64_t n_slices, int64_t s
   hipLaunchKernelGGL(k_sum_slices, dim3(grid_for((n + 3) / 4)), dim3(kBlock), 0,
                      as_stream(stream), P, n_slices, slice_stride, n, out);
   return check_launch("hgd_sum_slices");
+}
+
+extern "C" hgd_status hgd_dropout_apply(const float* x, int64_t n, const uint64_t* seed,
+                                        float keep, float scale, float* y, void* stream) {
+  clear_error();
+  HGD_REQUIRE(n >= 0, "hgd_dropout_apply: n < 0");
+  HGD_REQUIRE(keep > 0.f && keep <= 1.f, "hgd_dropout_apply: keep must be in (0, 1]");
+  HGD_REQUIRE(n <= 0xffffffffLL, "hgd_dropout_apply: n must be < 2^32 (32-bit element counter)");
+  if (n == 0) return HGD_OK;
+  HGD_REQUIRE(x && y && seed && aligned16(x) && aligned16(y), "hgd_dropout_apply: null/unaligned");
+  hipLaunchKernelGGL(k_dropout, dim3(grid_for((n + 3) / 4)), dim3(kBlock), 0, as_stream(stream),
+                     x, n, seed, keep, scale, y);
+  return check_launch("hgd_dropout_apply");
 }

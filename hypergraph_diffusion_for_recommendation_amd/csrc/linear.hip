@@ -50,6 +50,16 @@ struct RowGemm {
   int64_t rows;
   int32_t K, N;
   int32_t accumulate;  // Y += product (the bias / ReLU apply to the product alone)
+  // forward epilogue after the bias / ReLU: nn.Dropout on the product (keep-bit of element
+  // row·N + col from dropout_keep(*drop_seed, ·, drop_keep), kept values × drop_scale), and a
+  // second store Y2 = Y + res (the residual add after an ED-HNN block)
+  const uint64_t* drop_seed;
+  float drop_keep;
+  float drop_scale;
+  const float* res;
+  int64_t ldres;
+  float* Y2;
+  int64_t ldy2;
 };
 
 // Up to two independent products of the same K, N and mask mode in ONE launch (HCCF's user and
@@ -141,6 +151,7 @@ __global__ __launch_bounds__(256) void k_row_gemm(RowGemmGroup grp) {
 #pragma unroll
   for (int t = 0; t < NT; ++t) bias_v[t] = (p.bias && t < nt) ? p.bias[n0 + 16 * t + i16] : 0.f;
 
+  const uint64_t drop_seed = p.drop_seed ? *p.drop_seed : 0ull;
   auto compute = [&](int64_t tile, f32x4 (&a)[SUB][KQ], const f32x4 (&m)[SUB][KQ]) {
 #pragma unroll
     for (int s = 0; s < SUB; ++s) {
@@ -165,6 +176,16 @@ __global__ __launch_bounds__(256) void k_row_gemm(RowGemmGroup grp) {
           acc[t][r] = (p.relu && v < 0.f) ? 0.f : v;
         }
       const int64_t r0 = tile * 16 * SUB + 16 * s;
+      if (p.drop_seed) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const uint32_t e = static_cast<uint32_t>(r0 + 4 * h + r) * static_cast<uint32_t>(p.N) +
+                               static_cast<uint32_t>(n0 + 16 * t + i16);
+            acc[t][r] = dropout_keep(drop_seed, e, p.drop_keep) ? acc[t][r] * p.drop_scale : 0.f;
+          }
+      }
       float* yb = p.Y + n0 + i16;
       if (p.accumulate) {
 #pragma unroll
@@ -186,6 +207,17 @@ __global__ __launch_bounds__(256) void k_row_gemm(RowGemmGroup grp) {
           for (int r = 0; r < 4; ++r)
             if (t < nt && r0 + 4 * h + r < p.rows)
               yb[(r0 + 4 * h + r) * p.ldy + 16 * t] = acc[t][r];
+      }
+      if (p.Y2) {
+        const float* rb = p.res + n0 + i16;
+        float* y2 = p.Y2 + n0 + i16;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (t < nt && r0 + 4 * h + r < p.rows)
+              y2[(r0 + 4 * h + r) * p.ldy2 + 16 * t] =
+                  acc[t][r] + rb[(r0 + 4 * h + r) * p.ldres + 16 * t];
       }
     }
   };
@@ -459,6 +491,12 @@ hgd_status check_rows(const hgd_gemm_rows_desc& d, const char* fn) {
               d.N);
   HGD_REQUIRE(d.lda >= d.K && d.ldy >= d.N && (!d.relu_mask || d.ldm >= d.K),
               "%s: leading dimension too small", fn);
+  HGD_REQUIRE(!d.drop_seed || (d.drop_keep > 0.f && d.drop_keep <= 1.f),
+              "%s: dropout keep must be in (0, 1]", fn);
+  HGD_REQUIRE(!d.drop_seed || d.rows * static_cast<int64_t>(d.N) <= 0xffffffffLL,
+              "%s: dropout needs rows·N < 2^32 (32-bit element counter)", fn);
+  HGD_REQUIRE((d.res == nullptr) == (d.Y2 == nullptr), "%s: res and Y2 go together", fn);
+  HGD_REQUIRE(!d.Y2 || (d.ldres >= d.N && d.ldy2 >= d.N), "%s: ldres / ldy2 too small", fn);
   if (d.rows == 0) return HGD_OK;
   HGD_REQUIRE(d.A && d.B && d.Y, "%s: null pointer", fn);
   HGD_REQUIRE(al16(d.A, d.lda) && al16(d.relu_mask, d.ldm), "%s: A / mask rows must be 16-byte "
@@ -655,6 +693,13 @@ extern "C" hgd_status hgd_gemm_rows(const hgd_gemm_rows_desc* descs, int32_t cou
     p.K = d.K;
     p.N = d.N;
     p.accumulate = d.accumulate != 0;
+    p.drop_seed = d.drop_seed;
+    p.drop_keep = d.drop_keep;
+    p.drop_scale = d.drop_scale;
+    p.res = d.res;
+    p.ldres = d.ldres;
+    p.Y2 = d.Y2;
+    p.ldy2 = d.ldy2;
   }
   g.count = count;
   return row_gemm_group(g, as_stream(stream), "hgd_gemm_rows");

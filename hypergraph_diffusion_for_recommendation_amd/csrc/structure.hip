@@ -10,6 +10,7 @@
 //   dense threshold    model/layers/layers2/EquivSetGNN2.py:105-133 (torch.nonzero(H > 0))
 #include <hipcub/hipcub.hpp>
 
+#include "device_util.h"
 #include "hgd_internal.h"
 
 namespace hgd {
@@ -389,14 +390,9 @@ hgd_status tile_compact(F flag, W write, int64_t n, char* ws, bool with_pos, hip
   return check_launch(what);
 }
 
-// Counter-based keep-mask: u = 24-bit uniform in [0,1) from a splitmix64 hash of (seed, i);
-// keep iff floor(u + keep) != 0, the expression of SpAdjDropEdge (HCCF.py:223) on a device RNG.
-__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
-  x += 0x9E3779B97F4A7C15ull;
-  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-  return x ^ (x >> 31);
-}
+// Counter-based keep-mask: u = 24-bit uniform in [0,1) from a splitmix64 hash of (seed, i)
+// (device_util.h); keep iff floor(u + keep) != 0, the expression of SpAdjDropEdge (HCCF.py:223)
+// on a device RNG.
 
 __global__ void k_bernoulli_mask(uint64_t seed, int64_t n, float keep,
                                  uint8_t* __restrict__ mask) {

@@ -172,8 +172,9 @@ class LocalAwareEncoder(nn.Module):
         all_embeddings = []
         for k in range(self.layers):
             if k != self.layers - 1:
+                # the "+ res" rides in the block's last Linear store when its fused path runs
                 ego_embeddings = self.edhnn_layers[k](ego_embeddings, self.hypergraph,
-                                                      self.edhnn_ui_n) + res
+                                                      self.edhnn_ui_n, residual=res)
             else:
                 # LN0(HGCNConv(Â, x, act=False)) + res in one fused hop store
                 ego_embeddings = two_hop_fused(incidence_of(sparse_norm_adj), ego_embeddings,

@@ -331,6 +331,145 @@ def linear(X: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] =
     return Y.reshape(*lead, weight.shape[0])
 
 
+def dropout_seed(device) -> torch.Tensor:
+    """A fresh seed for the library's device dropout, drawn from torch's generator of ``device``
+    (so ``torch.manual_seed`` fixes the stream, and a captured step draws it inside the graph)."""
+    return torch.randint(0, 2 ** 62, (1,), device=device, dtype=torch.int64)
+
+
+def _drop_consts(p: float):
+    keep = 1.0 - float(p)
+    return keep, float(torch.tensor(1.0 / keep, dtype=torch.float32))  # nn.Dropout's 1/(1-p)
+
+
+def _dropout_call(x: torch.Tensor, p: float, seed: torch.Tensor) -> torch.Tensor:
+    keep, scale = _drop_consts(p)
+    y = torch.empty_like(x)
+    nat.check(nat.load().hgd_dropout_apply(x.data_ptr(), x.numel(), seed.data_ptr(), keep, scale,
+                                           y.data_ptr(),
+                                           torch.cuda.current_stream(x.device).cuda_stream),
+              "hgd_dropout_apply")
+    return y
+
+
+class _Dropout(torch.autograd.Function):
+    """nn.Dropout(p) on the library's counter-based RNG (hgd_dropout_apply): the backward
+    regenerates the mask from the seed instead of storing it."""
+
+    @staticmethod
+    def forward(ctx, x, p: float, seed):
+        ctx.p = p
+        ctx.save_for_backward(seed)
+        return _dropout_call(x.contiguous(), p, seed)
+
+    @staticmethod
+    def backward(ctx, g):
+        (seed,) = ctx.saved_tensors
+        return _dropout_call(g.contiguous(), ctx.p, seed), None, None
+
+
+def dropout(x: torch.Tensor, p: float, seed: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``F.dropout(x, p, training=True)`` for device fp32 tensors on the library RNG (same
+    distribution, its own stream: oracle.hgd_oracle.dropout_keep_mask restates the mask)."""
+    if p == 0.0:
+        return x
+    if not (0.0 < p < 1.0):
+        raise ValueError(f"dropout: p = {p} outside (0, 1)")
+    if x.numel() > 0xFFFFFFFF or not x.is_cuda or x.dtype != torch.float32:
+        return torch.nn.functional.dropout(x, p, training=True)  # beyond the 32-bit counter
+    if seed is None:
+        seed = dropout_seed(x.device)
+    return _Dropout.apply(x, float(p), seed)
+
+
+class _LinearReluDrop(torch.autograd.Function):
+    """``dropout(relu(X·Wᵀ + b), p) (+ res)`` in the row GEMM's store (hgd_gemm_rows: the
+    ReLU, the dropout mask of the library RNG and its 1/(1-p), the residual as a second
+    output). Backward on the two hgd_linear_backward kernels with the stored dropped activation
+    as the mask (it is > 0 exactly where the ReLU passed and the element was kept) and 1/(1-p)
+    folded into W for dX and into dW / db."""
+
+    @staticmethod
+    def forward(ctx, X, weight, bias, res, p: float, seed):
+        X = X.contiguous()
+        W = weight.contiguous()
+        n, in_f = X.shape
+        out_f = W.shape[0]
+        dev = X.device
+        Y = torch.empty((n, out_f), dtype=torch.float32, device=dev)
+        d = _rows_desc(X, W, 1, W.stride(0), in_f, out_f, Y)
+        d.bias, d.relu = nat.ptr(bias), 1
+        scale = 1.0
+        if p > 0.0:
+            keep, scale = _drop_consts(p)
+            d.drop_seed, d.drop_keep, d.drop_scale = seed.data_ptr(), keep, scale
+        out = Y
+        if res is not None:
+            res = res.contiguous()
+            out = torch.empty_like(Y)
+            d.res, d.ldres, d.Y2, d.ldy2 = res.data_ptr(), res.stride(0), out.data_ptr(), \
+                out.stride(0)
+        _gemm_rows([d], dev)
+        ctx.scale = scale
+        ctx.has_bias, ctx.has_res = bias is not None, res is not None
+        ctx.save_for_backward(X, W, Y)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        lib = nat.load()
+        X, W, Y = ctx.saved_tensors
+        dY = dout.contiguous()
+        n, in_f = X.shape
+        out_f = W.shape[0]
+        st = torch.cuda.current_stream(dY.device).cuda_stream
+        s = ctx.scale
+        dX = dW = db = None
+        if ctx.needs_input_grad[0]:
+            Ws = W * s if s != 1.0 else W
+            dX = torch.empty_like(X)
+            nat.check(lib.hgd_linear_backward_data(
+                dY.data_ptr(), dY.stride(0), Y.data_ptr(), Y.stride(0), n, out_f, Ws.data_ptr(),
+                Ws.stride(0), in_f, dX.data_ptr(), dX.stride(0), st), "hgd_linear_backward_data")
+        want_b = ctx.has_bias and ctx.needs_input_grad[2]
+        if ctx.needs_input_grad[1] or want_b:
+            dW = torch.empty((out_f, in_f), dtype=torch.float32, device=dY.device)
+            db = torch.empty(out_f, dtype=torch.float32, device=dY.device) if want_b else None
+            wsb = lib.hgd_linear_backward_weight_workspace_size(n, out_f, in_f)
+            ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dY.device)
+            nat.check(lib.hgd_linear_backward_weight(
+                dY.data_ptr(), dY.stride(0), Y.data_ptr(), Y.stride(0), X.data_ptr(),
+                X.stride(0), n, out_f, in_f, dW.data_ptr(), nat.ptr(db), ws.data_ptr(), wsb, st),
+                "hgd_linear_backward_weight")
+            if s != 1.0:
+                dW.mul_(s)
+                if db is not None:
+                    db.mul_(s)
+            if not ctx.needs_input_grad[1]:
+                dW = None
+        dres = dY if ctx.has_res and ctx.needs_input_grad[3] else None
+        return dX, dW, db, dres, None, None
+
+
+def linear_relu_dropout(X: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
+                        p: float, res: Optional[torch.Tensor] = None,
+                        seed: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``F.dropout(F.relu(F.linear(X, weight, bias)), p) + res`` (the ED-HNN block's lin_in →
+    dropout and W → ReLU → dropout → + residual, layers2/EquivSetGNN2.py:91-101 and
+    HGNN_HD4.py:399) with everything after the product in the row GEMM's store. ``p = 0``:
+    no dropout; ``res`` None: no residual. Shapes outside the kernels run the torch ops (with
+    the library dropout)."""
+    if res is not None and tuple(res.shape) != (X.shape[0], weight.shape[0]):
+        raise ValueError("linear_relu_dropout: residual shape mismatch")
+    if not (_linear_native_ok(X, weight) and X.dim() == 2
+            and X.shape[0] * weight.shape[0] <= 0xFFFFFFFF):
+        y = dropout(linear(X, weight, bias, relu=True), p, seed)
+        return y if res is None else y + res
+    if p > 0.0 and seed is None:
+        seed = dropout_seed(X.device)
+    return _LinearReluDrop.apply(X, weight, bias, res, float(p), seed)
+
+
 class _RowEpilogue(torch.autograd.Function):
     """``out_scale·LN(act(Z)) + s1·res1 + s2·res2`` on an existing matrix
     (hgd_row_epilogue_forward / hgd_row_epilogue_backward)."""

@@ -273,6 +273,18 @@ typedef struct hgd_gemm_rows_desc {
   int64_t rows;
   int32_t K;
   int32_t N;
+  /* forward epilogue after bias / ReLU (NULL / 0 = off): nn.Dropout — element (row, col) kept as
+   * hgd_dropout_apply keeps element row·N + col (rows·N < 2^32) for seed *drop_seed (a device
+   * value: a captured step draws it inside the graph), kept values × drop_scale (1 / (1 - p));
+   * then the second store Y2 = Y + res (res and Y2 both NULL or both set) — the "+ res" after
+   * an ED-HNN block (HGNN_HD4.py:399) */
+  const uint64_t* drop_seed;
+  float drop_keep;
+  float drop_scale;
+  const float* res;
+  int64_t ldres;
+  float* Y2;
+  int64_t ldy2;
 } hgd_gemm_rows_desc;
 hgd_status hgd_gemm_rows(const hgd_gemm_rows_desc* descs, int32_t count, void* stream);
 
@@ -626,6 +638,14 @@ hgd_status hgd_epilogue_apply(const float* z, int64_t n, int32_t epilogue, float
                               void* stream);
 hgd_status hgd_epilogue_backward(const float* ref, const float* dy, int64_t n, int32_t epilogue,
                                  float slope, float* dz, void* stream);
+/* nn.Dropout(p) on the library's counter-based RNG (the ED-HNN block's dropouts,
+ * layers2/EquivSetGNN2.py:91-101, when they run in its Linear stores or alone): y[i] = x[i]·scale
+ * if element i (< 2^32) is kept, else 0 — kept iff floor(u + keep) != 0 with
+ * u = (h >> 8)·2^-24, h = lowbias32(lowbias32(i + lo32(s)) ^ hi32(s)), s = *seed (a device
+ * value). keep = 1 - p, scale = 1 / (1 - p). The backward is the same call on the gradient with
+ * the same seed (no mask is stored). x, y 16-byte aligned; y may alias x. */
+hgd_status hgd_dropout_apply(const float* x, int64_t n, const uint64_t* seed, float keep,
+                             float scale, float* y, void* stream);
 /* out[i] = Σ_s P[s·slice_stride + i] over s = 0..n_slices-1, summed in slice order (bitwise the
  * chain ((P_0 + P_1) + P_2) + …): HCCF's `sum(hidden)` (model/graph/HCCF.py:188) over the layer
  * tables kept as slices of one buffer. P, out 16-byte aligned, slice_stride % 4 == 0. */

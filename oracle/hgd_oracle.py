@@ -553,6 +553,32 @@ def next_batch_pairwise(data, batch_size, n_negs=1):
         yield u_idx, i_idx, j_idx
 
 
+def dropout_keep_mask(seed, n, keep):
+    """The keep-mask of the library's device dropout (hgd_dropout_apply and the row GEMM's
+    dropout epilogue, hgd_gemm_rows_desc.drop_*: the build's own counter-based RNG for the
+    ED-HNN block's nn.Dropout, layers2/EquivSetGNN2.py:91-101; the reference draws torch's
+    CUDA philox stream, which no test can share, so the parity tests rebuild these masks here
+    and feed them to the float64 reference). For element i < 2^32:
+    h = lowbias32(lowbias32(i + lo32(seed)) ^ hi32(seed)), u = (h >> 8) / 2^24, kept iff
+    floor(u + keep) != 0 in float32. Bit-exact restatement for testing."""
+    m32 = np.uint32(0xFFFFFFFF)
+
+    def lowbias32(x):
+        x = x ^ (x >> np.uint32(16))
+        x = (x * np.uint32(0x7FEB352D)) & m32
+        x = x ^ (x >> np.uint32(15))
+        x = (x * np.uint32(0x846CA68B)) & m32
+        return x ^ (x >> np.uint32(16))
+
+    seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    lo, hi = np.uint32(seed & 0xFFFFFFFF), np.uint32(seed >> 32)
+    with np.errstate(over="ignore"):
+        i = np.arange(n, dtype=np.uint32)
+        h = lowbias32(lowbias32((i + lo) & m32) ^ hi)
+    u = (h >> np.uint32(8)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+    return np.floor(u + np.float32(keep)) != 0
+
+
 def device_keep_mask(seed, n, keep):
     """The keep-mask of the library's device drop-edge draw (hgd_bernoulli_mask /
     hgd_bernoulli_mask_dev: the build's own counter-based RNG for ``SpAdjDropEdge(device_rng=

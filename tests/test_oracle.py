@@ -218,3 +218,30 @@ def test_ranking_evaluation_known_answer():
     assert got == ['Top 1\n', 'Hit Ratio:0.4\n', 'Precision:1.0\n', 'Recall:0.41667\n',
                    'NDCG:1.0\n', 'Top 3\n', 'Hit Ratio:0.6\n', 'Precision:0.5\n',
                    'Recall:0.58333\n', 'NDCG:0.88268\n']
+
+
+def test_dropout_keep_mask_restatement():
+    """oracle.dropout_keep_mask (the library dropout's RNG, hgd_dropout_apply): the numpy form
+    equals a scalar Python restatement of the two lowbias32 rounds, and keeps about keep·n
+    elements; successive seeds give uncorrelated masks."""
+    import numpy as np
+    from oracle import hgd_oracle as O
+    M = 0xFFFFFFFF
+
+    def lb(x):
+        x ^= x >> 16
+        x = (x * 0x7FEB352D) & M
+        x ^= x >> 15
+        x = (x * 0x846CA68B) & M
+        return x ^ (x >> 16)
+
+    seed, keep = 0x123456789ABCDEF, 0.7
+    got = O.dropout_keep_mask(seed, 300, keep)
+    for i in range(300):
+        h = lb(lb((i + (seed & M)) & M) ^ (seed >> 32))
+        u = np.float32(h >> 8) * np.float32(1 / 16777216)
+        assert got[i] == (np.floor(u + np.float32(keep)) != 0)
+    a = O.dropout_keep_mask(7, 1_000_000, 0.5)
+    b = O.dropout_keep_mask(8, 1_000_000, 0.5)
+    assert abs(a.mean() - 0.5) < 0.003
+    assert abs((a == b).mean() - 0.5) < 0.003
