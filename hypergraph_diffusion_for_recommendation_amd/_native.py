@@ -98,6 +98,8 @@ class GemmRowsDesc(ctypes.Structure):
         ("ldres", c_i64),
         ("Y2", c_void_p),
         ("ldy2", c_i64),
+        ("row_inv", c_void_p),
+        ("binarize_a", c_i32),
     ]
 
 
@@ -116,6 +118,7 @@ class GemmTnDesc(ctypes.Structure):
         ("N", c_i32),
         ("C", c_void_p),
         ("colsum_A", c_void_p),
+        ("binarize_a", c_i32),
     ]
 
 

@@ -60,6 +60,11 @@ struct RowGemm {
   int64_t ldres;
   float* Y2;
   int64_t ldy2;
+  // A as its nonzero pattern (a > 0 ? 1 : 0: the binary incidence of a dense learned hypergraph,
+  // nonzero(H > 0) of EquivSetGNN2.py:105-133); row_inv: the product's rows scaled by
+  // 1 / max(Σ_k A[r, k], 1) (the scatter mean over a vertex's hyperedges) and that factor stored
+  int32_t binarize_a;
+  float* row_inv;
 };
 
 // Up to two independent products of the same K, N and mask mode in ONE launch (HCCF's user and
@@ -159,6 +164,12 @@ __global__ __launch_bounds__(256) void k_row_gemm(RowGemmGroup grp) {
 #pragma unroll
         for (int q = 0; q < KQ; ++q) a[s][q] = relu_mask(a[s][q], m[s][q]);
       }
+      if (p.binarize_a) {
+#pragma unroll
+        for (int q = 0; q < KQ; ++q)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) a[s][q][c] = a[s][q][c] > 0.f ? 1.f : 0.f;
+      }
       f32x4 acc[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -168,6 +179,23 @@ __global__ __launch_bounds__(256) void k_row_gemm(RowGemmGroup grp) {
         for (int c = 0; c < 4; ++c)
 #pragma unroll
           for (int t = 0; t < NT; ++t) acc[t] = mfma4(a[s][q][c], bf[q][c][t], acc[t]);
+      const int64_t r0 = tile * 16 * SUB + 16 * s;
+      if (p.row_inv) {
+        // Σ_k A[row i16][k]: this lane's 4·KQ columns, then the four lanes h of the row
+        float rs = 0.f;
+#pragma unroll
+        for (int q = 0; q < KQ; ++q) rs += (a[s][q][0] + a[s][q][1]) + (a[s][q][2] + a[s][q][3]);
+        rs += __shfl_xor(rs, 16);
+        rs += __shfl_xor(rs, 32);
+        const float inv = 1.f / fmaxf(rs, 1.f);
+        if (h == 0 && n0 == 0 && r0 + i16 < p.rows) p.row_inv[r0 + i16] = inv;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float sc = __shfl(inv, 4 * h + r);  // lane 4h + r holds output row 4h + r's
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[t][r] *= sc;
+        }
+      }
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -175,7 +203,6 @@ __global__ __launch_bounds__(256) void k_row_gemm(RowGemmGroup grp) {
           const float v = acc[t][r] + bias_v[t];
           acc[t][r] = (p.relu && v < 0.f) ? 0.f : v;
         }
-      const int64_t r0 = tile * 16 * SUB + 16 * s;
       if (p.drop_seed) {
 #pragma unroll
         for (int t = 0; t < NT; ++t)
@@ -250,6 +277,7 @@ struct SplitK {
   int64_t rows_per_split;
   float* part;       // [S, M·N]
   float* part_bias;  // [S, M] or NULL
+  int32_t binarize_a;  // A as its nonzero pattern (a > 0 ? 1 : 0)
 };
 
 struct SplitKGroup {  // as RowGemmGroup: blocks [0, nb0) along x are p[0]'s row slices
@@ -307,6 +335,9 @@ __global__ __launch_bounds__(256) void k_splitk_tn(SplitKGroup grp) {
       const bool ok = kb + 16 * s + h < k_end;
       f32x4 av = ca[s], bv = cb[s];
       if constexpr (MASK) av = relu_mask(av, cm[s]);
+      if (p.binarize_a)
+        av = f32x4{av.x > 0.f ? 1.f : 0.f, av.y > 0.f ? 1.f : 0.f, av.z > 0.f ? 1.f : 0.f,
+                   av.w > 0.f ? 1.f : 0.f};
       if (!(ok && mcol)) av = f32x4{0.f, 0.f, 0.f, 0.f};
       if (!(ok && ncol)) bv = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -630,6 +661,7 @@ extern "C" hgd_status hgd_gemm_tn(const hgd_gemm_tn_desc* descs, int32_t count, 
     p.M = d.M;
     p.N = d.N;
     p.rows_per_split = per[i];
+    p.binarize_a = d.binarize_a;
     p.part = reinterpret_cast<float*>(w);
     w += tn_part_bytes(d, S[i]);
     p.part_bias = d.colsum_A ? reinterpret_cast<float*>(w) : nullptr;
@@ -700,6 +732,8 @@ extern "C" hgd_status hgd_gemm_rows(const hgd_gemm_rows_desc* descs, int32_t cou
     p.ldres = d.ldres;
     p.Y2 = d.Y2;
     p.ldy2 = d.ldy2;
+    p.binarize_a = d.binarize_a;
+    p.row_inv = d.row_inv;
   }
   g.count = count;
   return row_gemm_group(g, as_stream(stream), "hgd_gemm_rows");

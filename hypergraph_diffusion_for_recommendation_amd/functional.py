@@ -1245,3 +1245,82 @@ def bpr_loss_rows(user_emb: torch.Tensor, item_emb: torch.Tensor, uid: torch.Ten
     neg_score = torch.mul(anc, neg).sum(dim=1)
     loss = torch.mean(-torch.log(10e-6 + torch.sigmoid(pos_score - neg_score)))
     return loss, anc, pos
+
+
+def _bin_tn(H: torch.Tensor, B: torch.Tensor, colsum: Optional[torch.Tensor]):
+    """(H > 0)ᵀ·B [K, d] (split-K over the n rows, binarized A) and, optionally, the column
+    counts of (H > 0)."""
+    lib = nat.load()
+    dev = H.device
+    n, K = H.shape
+    d = B.shape[1]
+    C = torch.empty((K, d), dtype=torch.float32, device=dev)
+    t = nat.GemmTnDesc()
+    t.A, t.lda, t.B, t.ldb = H.data_ptr(), H.stride(0), B.data_ptr(), B.stride(0)
+    t.rows, t.M, t.N, t.C = n, K, d, C.data_ptr()
+    t.colsum_A = nat.ptr(colsum)
+    t.binarize_a = 1
+    arr = (nat.GemmTnDesc * 1)(t)
+    wsb = lib.hgd_gemm_tn_workspace_size(arr, 1)
+    ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+    nat.check(lib.hgd_gemm_tn(arr, 1, ws.data_ptr(), wsb,
+                              torch.cuda.current_stream(dev).cuda_stream), "hgd_gemm_tn")
+    return C
+
+
+def _bin_rows(H: torch.Tensor, M: torch.Tensor, row_inv: Optional[torch.Tensor]):
+    """(H > 0)·M [n, d] (row GEMM, binarized A); with ``row_inv`` the rows are divided by
+    max(their nonzero count, 1), which is stored there."""
+    n, K = H.shape
+    d = M.shape[1]
+    Y = torch.empty((n, d), dtype=torch.float32, device=H.device)
+    desc = _rows_desc(H, M, M.stride(0), 1, K, d, Y)
+    desc.binarize_a = 1
+    desc.row_inv = nat.ptr(row_inv)
+    _gemm_rows([desc], H.device)
+    return Y
+
+
+class _DenseMeanTwoHop(torch.autograd.Function):
+    """The ED-HNN scatter-mean pair over V/E = nonzero(H > 0) of a DENSE learned hypergraph
+    H [n, K] (HCCF_diffusion.py:205-206 → EquivSetGNN.generate_V_E :382-402, EquivSetConv
+    :291-308, torch_scatter means): Xv = D_v^-1·B·D_e^-1·Bᵀ·X with B = (H > 0), empty means 0.
+    Bᵀ·X is a split-K product that counts B's columns as it goes, B·Xe a row GEMM that divides
+    each row by its own count (both read H and binarize it on load): no nonzero list, no
+    structure build, no host read — the same means as the sparse V/E path."""
+
+    @staticmethod
+    def forward(ctx, H, X):
+        H, X = H.contiguous(), X.contiguous()
+        n, K = H.shape
+        f = dict(dtype=torch.float32, device=X.device)
+        cnt = torch.empty(K, **f)
+        Xe = _bin_tn(H, X, cnt)
+        inv_e = 1.0 / cnt.clamp_min(1.0)
+        row_inv = torch.empty(n, **f)
+        Y = _bin_rows(H, Xe * inv_e[:, None], row_inv)
+        ctx.save_for_backward(H, inv_e, row_inv)
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        H, inv_e, row_inv = ctx.saved_tensors
+        dM = _bin_tn(H, dY.contiguous() * row_inv[:, None], None)
+        dX = _bin_rows(H, dM * inv_e[:, None], None)
+        return None, dX  # the structure carries no gradient (nonzero(H > 0) is integer)
+
+
+def dense_mean_two_hop_ok(H, X) -> bool:
+    return (H.is_cuda and X.is_cuda and H.dim() == 2 and X.dim() == 2
+            and H.dtype == X.dtype == torch.float32 and H.shape[0] == X.shape[0]
+            and H.shape[1] % 16 == 0 and 16 <= H.shape[1] <= 128
+            and X.shape[1] % 16 == 0 and X.shape[1] >= 16 and H.shape[0] > 0)
+
+
+def dense_mean_two_hop(H: torch.Tensor, X: torch.Tensor) -> torch.Tensor:
+    """``scatter_mean(scatter_mean(X[V], E)[E], V, dim_size=n)`` for V/E = nonzero(H > 0) of a
+    dense [n, K] hypergraph (see :class:`_DenseMeanTwoHop`); K a multiple of 16 up to 128."""
+    if not dense_mean_two_hop_ok(H, X):
+        raise ValueError("dense_mean_two_hop: needs device fp32 H [n, K] (K % 16 == 0, <= 128) "
+                         "and X [n, d] (d % 16 == 0)")
+    return _DenseMeanTwoHop.apply(H.detach(), X)

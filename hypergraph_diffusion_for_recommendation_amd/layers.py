@@ -30,8 +30,9 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .functional import (dense_two_hop, dropout, dropout_seed, layer_norm, linear,
-                         linear_relu_dropout, spmm, two_hop, two_hop_fused)
+from .functional import (dense_mean_two_hop, dense_mean_two_hop_ok, dense_two_hop, dropout,
+                         dropout_seed, layer_norm, linear, linear_relu_dropout, spmm, two_hop,
+                         two_hop_fused)
 from .incidence import (CSR, Incidence, MaskedIncidence, dense_threshold, drop_edges,
                         expand_rows, incidence_of)
 
@@ -512,6 +513,18 @@ class EquivSetGNN(nn.Module):
     def forward(self, x, hypergraph, n_nodes, residual=None):
         """``residual``: added to the block's output (LocalAwareEncoder's ``+ res``,
         HGNN_HD4.py:399) — in the last Linear's store when the fused path runs."""
+        if (self._fused_dropout_ok() and torch.is_tensor(hypergraph)
+                and hypergraph.layout == torch.strided and dense_mean_two_hop_ok(hypergraph, x)
+                and hypergraph.shape[0] == x.shape[0]):
+            # a dense learned hypergraph (HCCF_diffusion.py:205-206): the mean pair straight
+            # from H (functional.dense_mean_two_hop), no V/E lists and no host read
+            p = self.dropout.p if self.training else 0.0
+            seeds = [dropout_seed(x.device) for _ in range(3)] if p > 0.0 else [None] * 3
+            x = dropout(x, p, seeds[0])
+            x = linear_relu_dropout(x, self.lin_in.weight, self.lin_in.bias, p, seed=seeds[1])
+            ln, lin = input_norm_linear(self.conv.W)
+            y = layer_norm(dense_mean_two_hop(hypergraph, self.conv.W1(x)), ln)
+            return linear_relu_dropout(y, lin.weight, lin.bias, p, res=residual, seed=seeds[2])
         V, E = self.generate_V_E(n_nodes, hypergraph)
         if self._fused_dropout_ok():
             # HGNN_HD4's block: every dropout on the library RNG (functional.dropout), the

@@ -285,6 +285,12 @@ typedef struct hgd_gemm_rows_desc {
   int64_t ldres;
   float* Y2;
   int64_t ldy2;
+  /* row_inv (NULL = off): the product's rows scaled by 1 / max(Σ_k A'[r, k], 1) before bias /
+   * ReLU and that factor stored to row_inv[r] — with binarize_a, the scatter mean over a vertex's
+   * hyperedges of a dense learned hypergraph (EquivSetConv2.py:93 on nonzero(H > 0),
+   * EquivSetGNN2.py:105-133); binarize_a: A' = (A > 0 ? 1 : 0) instead of A */
+  float* row_inv;
+  int32_t binarize_a;
 } hgd_gemm_rows_desc;
 hgd_status hgd_gemm_rows(const hgd_gemm_rows_desc* descs, int32_t count, void* stream);
 
@@ -300,6 +306,7 @@ typedef struct hgd_gemm_tn_desc {
   int32_t N;
   float* C;               /* [M, N] */
   float* colsum_A;        /* [M] or NULL */
+  int32_t binarize_a;     /* A' = (A > 0 ? 1 : 0) instead of A (colsum_A then counts nonzeros) */
 } hgd_gemm_tn_desc;
 size_t hgd_gemm_tn_workspace_size(const hgd_gemm_tn_desc* descs, int32_t count);
 hgd_status hgd_gemm_tn(const hgd_gemm_tn_desc* descs, int32_t count, void* workspace,

@@ -138,3 +138,100 @@ def test_module_path_unchanged_under_recorded_dropout(dev):
         b = torch.cat(enc(x, enc.sparse_norm_adj))
     err = float((a - b).abs().max())
     assert err <= 1e-6 * float(b.abs().max()), err
+
+
+@pytest.mark.parametrize("n,K,d", [(3000, 32, 64), (517, 16, 32), (2048, 128, 128)])
+def test_dense_mean_two_hop_matches_the_vertex_edge_means(dev, n, K, d):
+    """functional.dense_mean_two_hop (V/E = nonzero(H > 0) of a dense learned hypergraph,
+    HCCF_diffusion.py:382-402 + the torch_scatter mean pair) against the float64 restatement of
+    the two scatter means, forward and backward; rows and columns without a positive entry
+    included (their means are 0)."""
+    from hypergraph_diffusion_for_recommendation_amd.functional import dense_mean_two_hop
+    g = torch.Generator(device=dev).manual_seed(n + K)
+    H = torch.randn(n, K, device=dev, generator=g)
+    H[:7] = -1.0          # vertices without hyperedges
+    H[:, 3] = -1.0        # a hyperedge without vertices
+    X = torch.randn(n, d, device=dev, generator=g).requires_grad_(True)
+    Y = dense_mean_two_hop(H, X)
+    G = torch.randn(n, d, device=dev, generator=g)
+    (dX,) = torch.autograd.grad(Y, X, G)
+    B = (H > 0).double().cpu()
+    ce = B.sum(0).clamp_min(1.0)
+    cv = B.sum(1).clamp_min(1.0)
+    Xd = X.detach().double().cpu()
+    Xe = (B.t() @ Xd) / ce[:, None]
+    Yr = (B @ Xe) / cv[:, None]
+    dXr = B @ ((B.t() @ (G.double().cpu() / cv[:, None])) / ce[:, None])
+    R.check_rows(Y, Yr, "Y")
+    R.check_rows(dX, dXr, "dX")
+    assert not Y[:7].any()
+
+
+def test_hccf_diffusion_dense_fused_train_matches_reference(dev, monkeypatch):
+    """HCCFDiffusionEncoder (HCCF_diffusion.py:131-215), train mode, on the fused path: the ED-HNN
+    block on the dense learned hypergraph through dense_mean_two_hop, its dropouts on the
+    library RNG (masks rebuilt from the recorded seeds), against the float64 reference."""
+    from hypergraph_diffusion_for_recommendation_amd import layers
+    from hypergraph_diffusion_for_recommendation_amd.encoders import HCCFDiffusionEncoder
+    from tests.test_gpu_config_parity import _check_params, _coo_host, _graph
+    seeds = []
+
+    def recorded_seed(device):
+        s = 7919 * (len(seeds) + 3) + (len(seeds) << 33)
+        seeds.append(s)
+        return torch.tensor([s], dtype=torch.int64, device=device)
+
+    monkeypatch.setattr(layers, "dropout_seed", recorded_seed)
+    U, I, nnz, d, L = 1_200, 1_500, 20_000, 32, 2
+    N = U + I
+    _, A = _graph(U, I, nnz, seed=60)
+    data = SimpleNamespace(n_users=U, n_items=I, norm_adj=A)
+    kw = dict(lrate=1e-3, lr_decay=0.9, max_epoch=1, batch_size=64, reg=0.01,
+              embedding_size=d, hyper_dim=32, drop_rate=0.2, p=0.3, n_layers=L)
+    torch.manual_seed(61)
+    enc = HCCFDiffusionEncoder(kw, data, device=dev).train()
+    assert enc.edhnnlayer._fused_dropout_ok()
+    enc.drop_out = R.FixedDropout(0.2, 62)
+    enc.edgeDropper = R.DropRecorder(enc.edgeDropper)
+    torch.manual_seed(64)
+    ue, ie, gcns, hyps = enc(keep_rate=0.7)
+    g = torch.Generator().manual_seed(65)
+    Gu, Gi = torch.randn(U, d, generator=g), torch.randn(I, d, generator=g)
+    Gh = [torch.randn(N, d, generator=g) for _ in range(L)]
+    tot = (ue * Gu.to(dev)).sum() + (ie * Gi.to(dev)).sum()
+    for layer in range(L):
+        tot = tot + (hyps[layer] * Gh[layer].to(dev)).sum()
+    tot.backward()
+    assert len(seeds) == 3 * 2 * L
+    blk_masks = []
+    for k, s in enumerate(seeds):
+        rows = U if (k // 3) % 2 == 0 else I
+        blk_masks.append(_mask(s, (rows, d), 0.5))
+
+    P = R.leaves(enc)
+    idx, vals = _coo_host(enc.sparse_norm_adj)
+    torch.manual_seed(64)
+    adjs = []
+    for layer in range(L):
+        di, dv = R.drop_edge_reference(idx, vals, 0.7)
+        gi, gv = enc.edgeDropper.outputs[layer]
+        assert torch.equal(di, gi) and torch.equal(dv, gv), f"drop-edge layer {layer}"
+        adjs.append(R.sparse(di, dv, (N, N)))
+    probe = R.Probe()
+    ueR, ieR, gR, hR = R.hccf_diffusion(P, adjs, enc.drop_out.masks, 0.8, blk_masks, 0.5, U, L,
+                                        1e-5, None, probe)
+    worst = max(R.check_rows(ue, ueR, "user_emb"), R.check_rows(ie, ieR, "item_emb"))
+    for layer in range(L):
+        worst = max(worst, R.check_rows(gcns[layer], gR[layer], f"gcn[{layer}]"),
+                    R.check_rows(hyps[layer], hR[layer], f"hyper[{layer}]"))
+    totR = (ueR * Gu.double()).sum() + (ieR * Gi.double()).sum()
+    for layer in range(L):
+        totR = totR + (hR[layer] * Gh[layer].double()).sum()
+    totR.backward()
+    got = {k: p.grad for k, p in enc.named_parameters()}
+    gradsR = {k: v.grad for k, v in P.items()}
+    for k in ("embedding_dict.user_w", "embedding_dict.item_w"):  # structure only: no gradient
+        assert gradsR[k] is None and (got[k] is None or not got[k].any()), k
+        got[k] = gradsR[k] = None
+    worst = max(worst, _check_params(got, gradsR, probe))
+    print(f"HCCF_diffusion dense fused: worst row ratio {worst:.2e}")
