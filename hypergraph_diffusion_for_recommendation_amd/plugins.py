@@ -76,6 +76,9 @@ class HCCF(GraphRecommender):
         self.model.edgeDropper.device_rng = bool(kwargs.get('hgd_device_rng', False))
         self._parse_config(self.config, kwargs)
         self.model.to(self.device)
+        self._init_optimizer(kwargs)
+
+    def _init_optimizer(self, kwargs):
         # hgd_graph: the training step replayed from one HIP graph (graphs.CapturedStep) — the
         # device drop-edge mask from a device seed counter, device-side InfoNCE node counts and a
         # capturable Adam (its lr a device tensor the scheduler updates in place); the same math
@@ -823,9 +826,7 @@ class HCCF_diffusion(HCCF):
         self.model.edgeDropper.device_rng = bool(kwargs.get('hgd_device_rng', False))
         self._parse_config(self.config, kwargs)
         self.model.to(self.device)
-        self.optimizer = torch.optim.Adam(self.model.parameters(), lr=self.lRate)
-        self.scheduler = ReduceLROnPlateau(self.optimizer, 'min', factor=self.lr_decay,
-                                           patience=5)
+        self._init_optimizer(kwargs)  # hgd_graph as HCCF's (the ED-HNN block is capture-safe)
 
 
 class DHCF_Encoder(nn.Module):

@@ -7,6 +7,10 @@ forward, BPR + per-layer InfoNCE, backward, Adam — the repo's "hypergraph diff
 * hgd_device_mask — encoders.HCCFDiffusionEncoder: GCN hop and drop-edge on libhgd, the learned
                     hypergraph's V/E by hgd_dense_threshold_* and both scatter-means as one fused
                     two-hop, MFMA Linear / LayerNorm kernels, fused InfoNCE;
+* hgd_graph       — the same step replayed from one HIP graph (graphs.CapturedStep: capture-safe
+                    drop-edge as masked views, the ED-HNN block's dropouts on the library RNG,
+                    fused BPR on the encoder table, device-side InfoNCE node counts, capturable
+                    fused Adam) — HCCF_diffusion(hgd_graph=True);
 * reference_ops   — the same step with the reference's torch calls on the same GPU and the same
                     parameters: torch.sparse.mm, torch.nonzero(H > 0), the scatter-mean pair
                     (torch_scatter's mean as index_reduce_, pytorch-scatter being absent),
@@ -33,14 +37,19 @@ def main():
     ap.add_argument("--layers", type=int, default=3)
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--variants", default="hgd_device_mask,reference_ops")
+    ap.add_argument("--variants", default="hgd_device_mask,hgd_graph,reference_ops")
     args = ap.parse_args()
     import torch
     import torch.nn.functional as F
 
     import refops as R
     from hypergraph_diffusion_for_recommendation_amd.encoders import HCCFDiffusionEncoder
-    from hypergraph_diffusion_for_recommendation_amd.functional import contrast_loss, unique_long
+    from hypergraph_diffusion_for_recommendation_amd.functional import (bpr_loss_rows,
+                                                                         contrast_loss,
+                                                                         contrast_loss_pair,
+                                                                         unique_long,
+                                                                         unique_long_n)
+    from hypergraph_diffusion_for_recommendation_amd.graphs import CapturedStep
 
     dev = torch.device("cuda")
     nu, ni, d, L = args.users, args.items, args.dim, args.layers
@@ -93,27 +102,51 @@ def main():
         emb = sum(hidden)
         return emb[:nu], emb[nu:], gcn_l, hyp_l
 
-    def make_step(fwd, loss_fn, unique, hoist):
-        opt = torch.optim.Adam(model.parameters(), lr=conf["lrate"])
-        state = {"k": 0}
+    def make_step(fwd, loss_fn, unique, hoist, graph=False, params=None):
+        params = list(model.parameters() if params is None else params)
+        if graph:
+            lr = torch.tensor(conf["lrate"], dtype=torch.float32, device=dev)
+            opt = torch.optim.Adam(params, lr=lr, capturable=True, fused=True)
+        else:
+            opt = torch.optim.Adam(params, lr=conf["lrate"])
+        state = {"k": 0, "cap": None}
+
+        def body(uid, pid, nid):
+            ue, ie, gcn, hyp = fwd(keep)
+            if graph:  # HCCF_diffusion(hgd_graph=True)'s train_step
+                bpr, anc, pos = bpr_loss_rows(ue, ie, uid, pid, nid)
+                (un, uc), (pn, pc) = unique_long_n(anc), unique_long_n(pos)
+                ssl = 0
+                for layer in range(L):
+                    ssl = ssl + contrast_loss_pair(gcn[layer].detach(), hyp[layer], nu, un, pn,
+                                                   temp, uc, pc)
+            else:
+                anc, pos, neg = ue[uid], ie[pid], ie[nid]
+                bpr = R.bpr_loss(anc, pos, neg)
+                un = (unique(anc), unique(pos)) if hoist else None
+                ssl = 0
+                for layer in range(L):
+                    e1, e2 = gcn[layer].detach(), hyp[layer]
+                    a_n, p_n = un if hoist else (unique(anc), unique(pos))
+                    ssl = ssl + loss_fn(e1[:nu], e2[:nu], a_n, temp) + loss_fn(e1[nu:], e2[nu:],
+                                                                               p_n, temp)
+            loss = bpr + cl_rate * ssl
+            opt.zero_grad()
+            torch.nn.utils.clip_grad_norm_(params, 4)  # before backward, as HCCF
+            loss.backward()
+            opt.step()
+            return loss
 
         def step():
             uid, pid, nid = batches[state["k"] % len(batches)]
             state["k"] += 1
-            ue, ie, gcn, hyp = fwd(keep)
-            anc, pos, neg = ue[uid], ie[pid], ie[nid]
-            un = (unique(anc), unique(pos)) if hoist else None
-            ssl = 0
-            for layer in range(L):
-                e1, e2 = gcn[layer].detach(), hyp[layer]
-                a_n, p_n = un if hoist else (unique(anc), unique(pos))
-                ssl = ssl + loss_fn(e1[:nu], e2[:nu], a_n, temp) + loss_fn(e1[nu:], e2[nu:],
-                                                                           p_n, temp)
-            loss = R.bpr_loss(anc, pos, neg) + cl_rate * ssl
-            opt.zero_grad()
-            torch.nn.utils.clip_grad_norm_(model.parameters(), 4)  # before backward, as HCCF
-            loss.backward()
-            opt.step()
+            if not graph:
+                return body(uid, pid, nid)
+            if state["cap"] is None:
+                if state["k"] == 1:
+                    return body(uid, pid, nid)  # one eager step: optimizer state, handles
+                state["cap"] = CapturedStep(body, (uid, pid, nid))
+            return state["cap"](uid, pid, nid)
         return step
 
     def timed(step):
@@ -136,6 +169,15 @@ def main():
     if "hgd_device_mask" in want:
         out.append(("hgd_device_mask", timed(make_step(model, contrast_loss, unique_long,
                                                        True))))
+    if "hgd_graph" in want:
+        torch.manual_seed(0)
+        g_model = HCCFDiffusionEncoder(conf, data, dev)
+        g_model.load_state_dict(model.state_dict())
+        g_model.edgeDropper.device_rng = True
+        g_model.edgeDropper.capture_safe = True
+        g_model.train()
+        out.append(("hgd_graph", timed(make_step(g_model, None, None, True, graph=True,
+                                                 params=g_model.parameters()))))
     if "reference_ops" in want:
         out.append(("reference_ops", timed(make_step(
             ref_forward, R.contrast_loss, lambda t: torch.unique(t.long()), False))))

@@ -10,6 +10,9 @@ step itself.
 * HCCF steps replayed from a captured graph take bitwise the same steps as the same capture-safe
   step run eagerly (same seeds, nn dropout off), and the eager capture-safe step matches the
   float64 reference (loss 1e-5 relative, gradient rows 1e-5);
+* the HCCF_diffusion step (ED-HNN block on the dense learned hypergraph, its dropouts on the
+  library RNG seeded from torch's device generator) replayed from a graph equals the same steps
+  run eagerly — dropouts on;
 * the HCCF plugin trains end to end in graph mode (hgd_graph).
 """
 import numpy as np
@@ -301,3 +304,45 @@ def test_capture_safe_step_matches_reference(dev):
     params = dict(enc.named_parameters())
     for k, gr in zip(names, grads):
         R.check_rows(params[k].grad, gr, f"d {k}")
+
+
+def test_captured_hccf_diffusion_steps_equal_eager_steps(dev):
+    """HCCF_diffusion(hgd_graph=True)'s step: replays draw the ED-HNN dropout seeds from torch's
+    device generator inside the graph (the same philox offsets eager launches consume) and the
+    drop-edge masks from the device seed counter, so replayed and eager steps agree bitwise."""
+    from types import SimpleNamespace
+
+    from hypergraph_diffusion_for_recommendation_amd.encoders import HCCFDiffusionEncoder
+    from hypergraph_diffusion_for_recommendation_amd.graphs import CapturedStep
+    g = torch.Generator(device=dev).manual_seed(8)
+    U, I = 1500, 1200
+    batches = [tuple(torch.randint(0, n, (256,), device=dev, generator=g) for n in (U, I, I))
+               for _ in range(5)]
+    A = _graph(U, I, 30_000, seed=2)
+    data = SimpleNamespace(n_users=U, n_items=I, norm_adj=A)
+    kw = dict(lrate=1e-3, lr_decay=0.9, max_epoch=1, batch_size=256, reg=0.01,
+              embedding_size=32, hyper_dim=32, drop_rate=0.0, p=0.3, n_layers=2)
+    runs = []
+    for captured in (False, True):
+        torch.manual_seed(3)
+        enc = HCCFDiffusionEncoder(kw, data, device=dev).train()
+        enc.edgeDropper.device_rng = True
+        enc.edgeDropper.capture_safe = True
+        assert enc.edhnnlayer._fused_dropout_ok()
+        lr = torch.tensor(1e-3, device=dev)
+        opt = torch.optim.Adam(enc.parameters(), lr=lr, capturable=True, fused=True)
+        step = _step_fn(enc, opt, U)
+        torch.manual_seed(11)
+        torch.cuda.manual_seed(12)
+        losses = [float(step(*batches[0]))]
+        if captured:
+            cap = CapturedStep(step, batches[1])
+            losses += [float(cap(*b)) for b in batches[1:]]
+        else:
+            losses += [float(step(*b)) for b in batches[1:]]
+        torch.cuda.synchronize()
+        runs.append((losses, {k: v.detach().clone() for k, v in enc.state_dict().items()}))
+    (l0, s0), (l1, s1) = runs
+    assert l0 == l1, (l0, l1)
+    for k in s0:
+        assert torch.equal(s0[k], s1[k]), k
