@@ -100,6 +100,7 @@ class GemmRowsDesc(ctypes.Structure):
         ("ldy2", c_i64),
         ("row_inv", c_void_p),
         ("binarize_a", c_i32),
+        ("b_row_count", c_void_p),
     ]
 
 
@@ -119,6 +120,7 @@ class GemmTnDesc(ctypes.Structure):
         ("C", c_void_p),
         ("colsum_A", c_void_p),
         ("binarize_a", c_i32),
+        ("b_row_scale", c_void_p),
     ]
 
 

@@ -65,6 +65,7 @@ struct RowGemm {
   // 1 / max(Σ_k A[r, k], 1) (the scatter mean over a vertex's hyperedges) and that factor stored
   int32_t binarize_a;
   float* row_inv;
+  const float* b_row_count;  // Bm row k × 1 / max(b_row_count[k], 1) (hyperedge means)
 };
 
 // Up to two independent products of the same K, N and mask mode in ONE launch (HCCF's user and
@@ -152,6 +153,16 @@ __global__ __launch_bounds__(256) void k_row_gemm(RowGemmGroup grp) {
     for (int c = 0; c < 4; ++c)
 #pragma unroll
       for (int t = 0; t < NT; ++t) bf[q][c][t] = sB[(4 * h + 16 * q + c) * LDB + 16 * t + i16];
+  if (p.b_row_count) {  // fl(Bm[k][n] · fl(1 / max(count, 1))): the scaled-B product, bitwise
+#pragma unroll
+    for (int q = 0; q < KQ; ++q)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float inv = 1.f / fmaxf(p.b_row_count[4 * h + 16 * q + c], 1.f);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) bf[q][c][t] *= inv;
+      }
+  }
   float bias_v[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) bias_v[t] = (p.bias && t < nt) ? p.bias[n0 + 16 * t + i16] : 0.f;
@@ -278,6 +289,7 @@ struct SplitK {
   float* part;       // [S, M·N]
   float* part_bias;  // [S, M] or NULL
   int32_t binarize_a;  // A as its nonzero pattern (a > 0 ? 1 : 0)
+  const float* b_row_scale;  // [rows] or NULL: B row × scale on load
 };
 
 struct SplitKGroup {  // as RowGemmGroup: blocks [0, nb0) along x are p[0]'s row slices
@@ -326,6 +338,10 @@ __global__ __launch_bounds__(256) void k_splitk_tn(SplitKGroup grp) {
       a[s] = ld4(p.A + kr * p.lda + mc);
       if constexpr (MASK) m[s] = ld4(p.mask + kr * p.ldm + mc);
       b[s] = ld4(p.B + kr * p.ldb + nc);
+      if (p.b_row_scale) {  // fl(B · scale), as a pre-scaled B would hold it
+        const float sc = p.b_row_scale[kr];
+        b[s] = f32x4{b[s].x * sc, b[s].y * sc, b[s].z * sc, b[s].w * sc};
+      }
     }
   };
   auto compute = [&](int64_t kb, const f32x4 (&ca)[U], const f32x4 (&cb)[U],
@@ -662,6 +678,7 @@ extern "C" hgd_status hgd_gemm_tn(const hgd_gemm_tn_desc* descs, int32_t count, 
     p.N = d.N;
     p.rows_per_split = per[i];
     p.binarize_a = d.binarize_a;
+    p.b_row_scale = d.b_row_scale;
     p.part = reinterpret_cast<float*>(w);
     w += tn_part_bytes(d, S[i]);
     p.part_bias = d.colsum_A ? reinterpret_cast<float*>(w) : nullptr;
@@ -734,6 +751,7 @@ extern "C" hgd_status hgd_gemm_rows(const hgd_gemm_rows_desc* descs, int32_t cou
     p.ldy2 = d.ldy2;
     p.binarize_a = d.binarize_a;
     p.row_inv = d.row_inv;
+    p.b_row_count = d.b_row_count;
   }
   g.count = count;
   return row_gemm_group(g, as_stream(stream), "hgd_gemm_rows");

@@ -208,15 +208,21 @@ class HCCFDiffusionEncoder(HCCFEncoder):
         gcn_hidden, hgnn_hidden = [], []
         hyper_uu = linear(e['user_emb'], e['user_w'].t())
         hyper_ii = linear(e['item_emb'], e['item_w'].t())
+        blk = self.edhnnlayer
         for _ in range(self.n_layers):
             gcn_emb = self.gcnlayer(self.edgeDropper(self.sparse_norm_adj, keep_rate), hidden[-1])
-            hyper_uemb = self.edhnnlayer(hidden[-1][:nu], self.drop_out(hyper_uu),
-                                         self.edhnn_user_n)
-            hyper_iemb = self.edhnnlayer(hidden[-1][nu:], self.drop_out(hyper_ii),
-                                         self.edhnn_item_n)
+            hu = self.drop_out(hyper_uu)
+            if blk.dense_pair_ok(hidden[-1], hu, hyper_ii):
+                # the user and the item call of the block as one pass over all rows
+                # (EquivSetGNN.forward_dense_pair: grouped mean two-hops, no cat)
+                hyp = blk.forward_dense_pair(hidden[-1], hu, self.drop_out(hyper_ii))
+            else:
+                hyper_uemb = blk(hidden[-1][:nu], hu, self.edhnn_user_n)
+                hyper_iemb = blk(hidden[-1][nu:], self.drop_out(hyper_ii), self.edhnn_item_n)
+                hyp = torch.cat([hyper_uemb, hyper_iemb], 0)
             gcn_hidden += [gcn_emb]
-            hgnn_hidden += [torch.cat([hyper_uemb, hyper_iemb], 0)]
-            hidden += [gcn_emb + hgnn_hidden[-1]]
+            hgnn_hidden += [hyp]
+            hidden += [gcn_emb + hyp]
         emb = sum(hidden)
         return emb[:nu], emb[nu:], gcn_hidden, hgnn_hidden
 

@@ -1247,74 +1247,96 @@ def bpr_loss_rows(user_emb: torch.Tensor, item_emb: torch.Tensor, uid: torch.Ten
     return loss, anc, pos
 
 
-def _bin_tn(H: torch.Tensor, B: torch.Tensor, colsum: Optional[torch.Tensor]):
-    """(H > 0)ᵀ·B [K, d] (split-K over the n rows, binarized A) and, optionally, the column
-    counts of (H > 0)."""
+def _bin_tn(parts, K: int, d: int, dev, colsum: Optional[torch.Tensor],
+            b_scale: Optional[torch.Tensor]) -> torch.Tensor:
+    """(H_g > 0)ᵀ·B_g [K, d] for each (H_g, B_g, row offset) of ``parts`` (one or two products,
+    one split-K launch + one reduction) → [G, K, d]; ``colsum`` [G, K] receives the column counts
+    of (H_g > 0), ``b_scale`` scales B's rows as they are loaded (rows at the part's offset)."""
     lib = nat.load()
-    dev = H.device
-    n, K = H.shape
-    d = B.shape[1]
-    C = torch.empty((K, d), dtype=torch.float32, device=dev)
-    t = nat.GemmTnDesc()
-    t.A, t.lda, t.B, t.ldb = H.data_ptr(), H.stride(0), B.data_ptr(), B.stride(0)
-    t.rows, t.M, t.N, t.C = n, K, d, C.data_ptr()
-    t.colsum_A = nat.ptr(colsum)
-    t.binarize_a = 1
-    arr = (nat.GemmTnDesc * 1)(t)
-    wsb = lib.hgd_gemm_tn_workspace_size(arr, 1)
+    C = torch.empty((len(parts), K, d), dtype=torch.float32, device=dev)
+    arr = (nat.GemmTnDesc * len(parts))()
+    for g, (H, B, off) in enumerate(parts):
+        t = arr[g]
+        t.A, t.lda, t.B, t.ldb = H.data_ptr(), H.stride(0), B.data_ptr(), B.stride(0)
+        t.rows, t.M, t.N, t.C = H.shape[0], K, d, C[g].data_ptr()
+        t.colsum_A = nat.ptr(colsum[g]) if colsum is not None else None
+        t.binarize_a = 1
+        t.b_row_scale = nat.ptr(b_scale[off:]) if b_scale is not None else None
+    wsb = lib.hgd_gemm_tn_workspace_size(arr, len(parts))
     ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
-    nat.check(lib.hgd_gemm_tn(arr, 1, ws.data_ptr(), wsb,
+    nat.check(lib.hgd_gemm_tn(arr, len(parts), ws.data_ptr(), wsb,
                               torch.cuda.current_stream(dev).cuda_stream), "hgd_gemm_tn")
     return C
 
 
-def _bin_rows(H: torch.Tensor, M: torch.Tensor, row_inv: Optional[torch.Tensor]):
-    """(H > 0)·M [n, d] (row GEMM, binarized A); with ``row_inv`` the rows are divided by
-    max(their nonzero count, 1), which is stored there."""
-    n, K = H.shape
-    d = M.shape[1]
-    Y = torch.empty((n, d), dtype=torch.float32, device=H.device)
-    desc = _rows_desc(H, M, M.stride(0), 1, K, d, Y)
-    desc.binarize_a = 1
-    desc.row_inv = nat.ptr(row_inv)
-    _gemm_rows([desc], H.device)
-    return Y
+def _bin_rows(parts, M: torch.Tensor, count: torch.Tensor, Y: torch.Tensor,
+              row_inv: Optional[torch.Tensor]) -> None:
+    """Y[off : off + n_g] = (H_g > 0)·(D_g^-1·M[g]) for each (H_g, off) of ``parts`` (one row-GEMM
+    launch), D_g = diag(max(count[g], 1)); with ``row_inv`` each row is divided by max(its
+    nonzero count, 1), which is stored there."""
+    K, d = M.shape[1], M.shape[2]
+    descs = []
+    for g, (H, off) in enumerate(parts):
+        n = H.shape[0]
+        desc = _rows_desc(H, M[g], d, 1, K, d, Y[off:off + n])
+        desc.binarize_a = 1
+        desc.b_row_count = count[g].data_ptr()
+        desc.row_inv = nat.ptr(row_inv[off:off + n]) if row_inv is not None else None
+        descs.append(desc)
+    _gemm_rows(descs, Y.device)
 
 
 class _DenseMeanTwoHop(torch.autograd.Function):
     """The ED-HNN scatter-mean pair over V/E = nonzero(H > 0) of a DENSE learned hypergraph
     H [n, K] (HCCF_diffusion.py:205-206 → EquivSetGNN.generate_V_E :382-402, EquivSetConv
     :291-308, torch_scatter means): Xv = D_v^-1·B·D_e^-1·Bᵀ·X with B = (H > 0), empty means 0.
-    Bᵀ·X is a split-K product that counts B's columns as it goes, B·Xe a row GEMM that divides
-    each row by its own count (both read H and binarize it on load): no nonzero list, no
-    structure build, no host read — the same means as the sparse V/E path."""
+    Bᵀ·X is a split-K product that counts B's columns as it goes, B·(D_e^-1·Xe) a row GEMM that
+    scales Xe's rows by the counts as it stages them and divides each output row by its own count
+    (both read H and binarize it on load): no nonzero list, no structure build, no host read —
+    the same means as the sparse V/E path.
+
+    Two hypergraphs over the row blocks [0, nu) and [nu, N) of one X (HCCF_diffusion's user and
+    item calls of the block, :213-216) run as one grouped product per stage: 3 launches forward
+    (split-K, reduction, rows) and 3 backward, whatever the pairing."""
 
     @staticmethod
-    def forward(ctx, H, X):
-        H, X = H.contiguous(), X.contiguous()
-        n, K = H.shape
+    def forward(ctx, X, nu, H0, H1):
+        X = X.contiguous()
+        N, d = X.shape
+        K = H0.shape[1]
+        parts = [(H0.contiguous(), 0)] + ([(H1.contiguous(), nu)] if H1 is not None else [])
         f = dict(dtype=torch.float32, device=X.device)
-        cnt = torch.empty(K, **f)
-        Xe = _bin_tn(H, X, cnt)
-        inv_e = 1.0 / cnt.clamp_min(1.0)
-        row_inv = torch.empty(n, **f)
-        Y = _bin_rows(H, Xe * inv_e[:, None], row_inv)
-        ctx.save_for_backward(H, inv_e, row_inv)
+        cnt = torch.empty((len(parts), K), **f)
+        Xe = _bin_tn([(H, X[off:off + H.shape[0]], off) for H, off in parts], K, d, X.device,
+                     cnt, None)
+        row_inv = torch.empty(N, **f)
+        Y = torch.empty((N, d), **f)
+        _bin_rows(parts, Xe, cnt, Y, row_inv)
+        ctx.parts = [off for _, off in parts]
+        ctx.save_for_backward(cnt, row_inv, *[H for H, _ in parts])
         return Y
 
     @staticmethod
     def backward(ctx, dY):
-        H, inv_e, row_inv = ctx.saved_tensors
-        dM = _bin_tn(H, dY.contiguous() * row_inv[:, None], None)
-        dX = _bin_rows(H, dM * inv_e[:, None], None)
-        return None, dX  # the structure carries no gradient (nonzero(H > 0) is integer)
+        cnt, row_inv, *Hs = ctx.saved_tensors
+        parts = list(zip(Hs, ctx.parts))
+        dY = dY.contiguous()
+        N, d = dY.shape
+        K = cnt.shape[1]
+        dM = _bin_tn([(H, dY[off:off + H.shape[0]], off) for H, off in parts], K, d, dY.device,
+                     None, row_inv)
+        dX = torch.empty_like(dY)
+        _bin_rows(parts, dM, cnt, dX, None)
+        # the structure carries no gradient (nonzero(H > 0) is integer)
+        return dX, None, None, None
 
 
 def dense_mean_two_hop_ok(H, X) -> bool:
     return (H.is_cuda and X.is_cuda and H.dim() == 2 and X.dim() == 2
             and H.dtype == X.dtype == torch.float32 and H.shape[0] == X.shape[0]
             and H.shape[1] % 16 == 0 and 16 <= H.shape[1] <= 128
-            and X.shape[1] % 16 == 0 and X.shape[1] >= 16 and H.shape[0] > 0)
+            and X.shape[1] % 16 == 0 and X.shape[1] >= 16 and H.shape[0] > 0
+            and X.stride(1) == 1 and X.stride(0) % 4 == 0 and X.data_ptr() % 16 == 0)
 
 
 def dense_mean_two_hop(H: torch.Tensor, X: torch.Tensor) -> torch.Tensor:
@@ -1323,4 +1345,15 @@ def dense_mean_two_hop(H: torch.Tensor, X: torch.Tensor) -> torch.Tensor:
     if not dense_mean_two_hop_ok(H, X):
         raise ValueError("dense_mean_two_hop: needs device fp32 H [n, K] (K % 16 == 0, <= 128) "
                          "and X [n, d] (d % 16 == 0)")
-    return _DenseMeanTwoHop.apply(H.detach(), X)
+    return _DenseMeanTwoHop.apply(X, X.shape[0], H.detach(), None)
+
+
+def dense_mean_two_hop_pair(H_u: torch.Tensor, H_i: torch.Tensor, X: torch.Tensor) -> torch.Tensor:
+    """``cat([dense_mean_two_hop(H_u, X[:nu]), dense_mean_two_hop(H_i, X[nu:])])`` with
+    nu = H_u.shape[0] — both halves in the same launches, the output written whole."""
+    nu = H_u.shape[0]
+    if not (H_i.shape[1] == H_u.shape[1] and H_i.shape[0] == X.shape[0] - nu
+            and dense_mean_two_hop_ok(H_u, X[:nu]) and dense_mean_two_hop_ok(H_i, X[nu:])):
+        raise ValueError("dense_mean_two_hop_pair: needs H_u [nu, K], H_i [N - nu, K] and X [N, d] "
+                         "(device fp32, K % 16 == 0, <= 128, d % 16 == 0)")
+    return _DenseMeanTwoHop.apply(X, nu, H_u.detach(), H_i.detach())

@@ -30,7 +30,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .functional import (dense_mean_two_hop, dense_mean_two_hop_ok, dense_two_hop, dropout,
+from .functional import (dense_mean_two_hop, dense_mean_two_hop_ok,
+                         dense_mean_two_hop_pair, dense_two_hop, dropout,
                          dropout_seed, layer_norm, linear, linear_relu_dropout, spmm, two_hop,
                          two_hop_fused)
 from .incidence import (CSR, Incidence, MaskedIncidence, dense_threshold, drop_edges,
@@ -545,6 +546,32 @@ class EquivSetGNN(nn.Module):
                 x = self.act(x)
         x = self.dropout(x)
         return x if residual is None else x + residual
+
+    def dense_pair_ok(self, x, H_u, H_i) -> bool:
+        """:meth:`forward_dense_pair` applies: the fused block, dense device hypergraphs over the
+        two row blocks of ``x``."""
+        return (self._fused_dropout_ok() and torch.is_tensor(H_u) and torch.is_tensor(H_i)
+                and H_u.layout == torch.strided and H_i.layout == torch.strided
+                and H_u.shape[0] + H_i.shape[0] == x.shape[0] and H_u.shape[1] == H_i.shape[1]
+                and x.is_contiguous() and x.shape[0] * x.shape[1] < 2 ** 32
+                and dense_mean_two_hop_ok(H_u, x[:H_u.shape[0]])
+                and dense_mean_two_hop_ok(H_i, x[H_u.shape[0]:]))
+
+    def forward_dense_pair(self, x, H_u, H_i):
+        """``cat([self(x[:nu], H_u, ·), self(x[nu:], H_i, ·)])`` (HCCF_diffusion.py:213-218: the
+        block on the user rows with the user hypergraph, on the item rows with the item one) as
+        ONE pass over all N rows: the row-wise stages (dropouts, lin_in, W1, LayerNorm, the last
+        Linear) are one launch each on [N, d] and the two mean two-hops one grouped op
+        (functional.dense_mean_two_hop_pair), the output written whole (no cat, no split of its
+        gradient). Each dropout is one library-RNG mask over the [N, d] rows (same distribution
+        as two per-half masks)."""
+        p = self.dropout.p if self.training else 0.0
+        seeds = [dropout_seed(x.device) for _ in range(3)] if p > 0.0 else [None] * 3
+        x = dropout(x, p, seeds[0])
+        x = linear_relu_dropout(x, self.lin_in.weight, self.lin_in.bias, p, seed=seeds[1])
+        ln, lin = input_norm_linear(self.conv.W)
+        y = layer_norm(dense_mean_two_hop_pair(H_u, H_i, self.conv.W1(x)), ln)
+        return linear_relu_dropout(y, lin.weight, lin.bias, p, seed=seeds[2])
 
     def _fused_dropout_ok(self) -> bool:
         # exactly nn.Dropout (a test's recorded-mask dropout takes the module path), one conv

@@ -291,6 +291,10 @@ typedef struct hgd_gemm_rows_desc {
    * EquivSetGNN2.py:105-133); binarize_a: A' = (A > 0 ? 1 : 0) instead of A */
   float* row_inv;
   int32_t binarize_a;
+  /* b_row_count (NULL = off): row k of B scaled by 1 / max(b_row_count[k], 1) as it is staged —
+   * the hyperedge means D_e^-1·Xe of the mean two-hop from the raw column counts colsum_A of the
+   * split-K product that made Xe (same product as scaling B beforehand) */
+  const float* b_row_count;
 } hgd_gemm_rows_desc;
 hgd_status hgd_gemm_rows(const hgd_gemm_rows_desc* descs, int32_t count, void* stream);
 
@@ -307,6 +311,8 @@ typedef struct hgd_gemm_tn_desc {
   float* C;               /* [M, N] */
   float* colsum_A;        /* [M] or NULL */
   int32_t binarize_a;     /* A' = (A > 0 ? 1 : 0) instead of A (colsum_A then counts nonzeros) */
+  const float* b_row_scale; /* [rows] or NULL: B's row r × b_row_scale[r] as it is loaded (the
+                             * vertex means D_v^-1 of the mean two-hop's backward) */
 } hgd_gemm_tn_desc;
 size_t hgd_gemm_tn_workspace_size(const hgd_gemm_tn_desc* descs, int32_t count);
 hgd_status hgd_gemm_tn(const hgd_gemm_tn_desc* descs, int32_t count, void* workspace,

@@ -140,6 +140,17 @@ def test_module_path_unchanged_under_recorded_dropout(dev):
     assert err <= 1e-6 * float(b.abs().max()), err
 
 
+def _mean_pair64(H, X, G):
+    """Float64 restatement of the scatter-mean pair over nonzero(H > 0) and its backward."""
+    B = (H > 0).double().cpu()
+    ce = B.sum(0).clamp_min(1.0)
+    cv = B.sum(1).clamp_min(1.0)
+    Xe = (B.t() @ X.detach().double().cpu()) / ce[:, None]
+    Y = (B @ Xe) / cv[:, None]
+    dX = B @ ((B.t() @ (G.double().cpu() / cv[:, None])) / ce[:, None])
+    return Y, dX
+
+
 @pytest.mark.parametrize("n,K,d", [(3000, 32, 64), (517, 16, 32), (2048, 128, 128)])
 def test_dense_mean_two_hop_matches_the_vertex_edge_means(dev, n, K, d):
     """functional.dense_mean_two_hop (V/E = nonzero(H > 0) of a dense learned hypergraph,
@@ -155,19 +166,35 @@ def test_dense_mean_two_hop_matches_the_vertex_edge_means(dev, n, K, d):
     Y = dense_mean_two_hop(H, X)
     G = torch.randn(n, d, device=dev, generator=g)
     (dX,) = torch.autograd.grad(Y, X, G)
-    B = (H > 0).double().cpu()
-    ce = B.sum(0).clamp_min(1.0)
-    cv = B.sum(1).clamp_min(1.0)
-    Xd = X.detach().double().cpu()
-    Xe = (B.t() @ Xd) / ce[:, None]
-    Yr = (B @ Xe) / cv[:, None]
-    dXr = B @ ((B.t() @ (G.double().cpu() / cv[:, None])) / ce[:, None])
+    Yr, dXr = _mean_pair64(H, X, G)
     R.check_rows(Y, Yr, "Y")
     R.check_rows(dX, dXr, "dX")
     assert not Y[:7].any()
 
 
-def test_hccf_diffusion_dense_fused_train_matches_reference(dev, monkeypatch):
+@pytest.mark.parametrize("nu,ni,K,d", [(3000, 2500, 32, 64), (17, 700, 16, 32), (1024, 64, 128, 16)])
+def test_dense_mean_two_hop_pair_is_the_two_halves(dev, nu, ni, K, d):
+    """dense_mean_two_hop_pair (HCCF_diffusion's user and item calls of the block as one grouped
+    op over one [N, d] table) against the float64 restatement of each half, forward and
+    backward."""
+    from hypergraph_diffusion_for_recommendation_amd.functional import dense_mean_two_hop_pair
+    g = torch.Generator(device=dev).manual_seed(nu + ni)
+    Hu = torch.randn(nu, K, device=dev, generator=g)
+    Hi = torch.randn(ni, K, device=dev, generator=g)
+    Hu[:3] = -1.0
+    Hi[:, 1] = -1.0
+    X = torch.randn(nu + ni, d, device=dev, generator=g).requires_grad_(True)
+    Y = dense_mean_two_hop_pair(Hu, Hi, X)
+    G = torch.randn(nu + ni, d, device=dev, generator=g)
+    (dX,) = torch.autograd.grad(Y, X, G)
+    Yu, dXu = _mean_pair64(Hu, X[:nu], G[:nu])
+    Yi, dXi = _mean_pair64(Hi, X[nu:], G[nu:])
+    R.check_rows(Y, torch.cat([Yu, Yi]), "Y")
+    R.check_rows(dX, torch.cat([dXu, dXi]), "dX")
+
+
+@pytest.mark.parametrize("pair", [True, False])
+def test_hccf_diffusion_dense_fused_train_matches_reference(dev, monkeypatch, pair):
     """HCCFDiffusionEncoder (HCCF_diffusion.py:131-215), train mode, on the fused path: the ED-HNN
     block on the dense learned hypergraph through dense_mean_two_hop, its dropouts on the
     library RNG (masks rebuilt from the recorded seeds), against the float64 reference."""
@@ -191,6 +218,8 @@ def test_hccf_diffusion_dense_fused_train_matches_reference(dev, monkeypatch):
     torch.manual_seed(61)
     enc = HCCFDiffusionEncoder(kw, data, device=dev).train()
     assert enc.edhnnlayer._fused_dropout_ok()
+    if not pair:  # the per-call path (one block call per row block, three seeds each)
+        monkeypatch.setattr(enc.edhnnlayer, "dense_pair_ok", lambda *a: False)
     enc.drop_out = R.FixedDropout(0.2, 62)
     enc.edgeDropper = R.DropRecorder(enc.edgeDropper)
     torch.manual_seed(64)
@@ -202,11 +231,17 @@ def test_hccf_diffusion_dense_fused_train_matches_reference(dev, monkeypatch):
     for layer in range(L):
         tot = tot + (hyps[layer] * Gh[layer].to(dev)).sum()
     tot.backward()
-    assert len(seeds) == 3 * 2 * L
     blk_masks = []
-    for k, s in enumerate(seeds):
-        rows = U if (k // 3) % 2 == 0 else I
-        blk_masks.append(_mask(s, (rows, d), 0.5))
+    if pair:  # three [N, d] masks per layer: their user rows, then their item rows
+        assert len(seeds) == 3 * L
+        for layer in range(L):
+            ms = [_mask(s, (N, d), 0.5) for s in seeds[3 * layer:3 * layer + 3]]
+            blk_masks += [m[:U] for m in ms] + [m[U:] for m in ms]
+    else:
+        assert len(seeds) == 3 * 2 * L
+        for k, s in enumerate(seeds):
+            rows = U if (k // 3) % 2 == 0 else I
+            blk_masks.append(_mask(s, (rows, d), 0.5))
 
     P = R.leaves(enc)
     idx, vals = _coo_host(enc.sparse_norm_adj)
@@ -234,4 +269,4 @@ def test_hccf_diffusion_dense_fused_train_matches_reference(dev, monkeypatch):
         assert gradsR[k] is None and (got[k] is None or not got[k].any()), k
         got[k] = gradsR[k] = None
     worst = max(worst, _check_params(got, gradsR, probe))
-    print(f"HCCF_diffusion dense fused: worst row ratio {worst:.2e}")
+    print(f"HCCF_diffusion dense fused (pair={pair}): worst row ratio {worst:.2e}")
