@@ -101,6 +101,7 @@ class GemmRowsDesc(ctypes.Structure):
         ("row_inv", c_void_p),
         ("binarize_a", c_i32),
         ("b_row_count", c_void_p),
+        ("b_scale", ctypes.c_float),
     ]
 
 
@@ -121,6 +122,7 @@ class GemmTnDesc(ctypes.Structure):
         ("colsum_A", c_void_p),
         ("binarize_a", c_i32),
         ("b_row_scale", c_void_p),
+        ("c_scale", ctypes.c_float),
     ]
 
 

@@ -65,6 +65,7 @@ struct SumRowsJob {
   const float* P;
   int64_t S, W;
   float* out;
+  float scale;  // 0 = off: out = sum × scale
 };
 hgd_status sum_rows_jobs(const SumRowsJob* jobs, int n, hipStream_t st);
 

@@ -66,6 +66,7 @@ struct RowGemm {
   int32_t binarize_a;
   float* row_inv;
   const float* b_row_count;  // Bm row k × 1 / max(b_row_count[k], 1) (hyperedge means)
+  float b_scale;             // 0 = off: Bm × b_scale (fl(W · s), as a pre-scaled W)
 };
 
 // Up to two independent products of the same K, N and mask mode in ONE launch (HCCF's user and
@@ -162,6 +163,14 @@ __global__ __launch_bounds__(256) void k_row_gemm(RowGemmGroup grp) {
 #pragma unroll
         for (int t = 0; t < NT; ++t) bf[q][c][t] *= inv;
       }
+  }
+  if (p.b_scale != 0.f) {
+#pragma unroll
+    for (int q = 0; q < KQ; ++q)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) bf[q][c][t] *= p.b_scale;
   }
   float bias_v[NT];
 #pragma unroll
@@ -710,9 +719,11 @@ extern "C" hgd_status hgd_gemm_tn(const hgd_gemm_tn_desc* descs, int32_t count, 
   SumRowsJob jobs[4];
   int nj = 0;
   for (int i = 0; i < live; ++i) {
+    const float sc = ld[i]->c_scale;
     jobs[nj++] = SumRowsJob{g.p[i].part, Sl[i], static_cast<int64_t>(g.p[i].M) * g.p[i].N,
-                            ld[i]->C};
-    if (ld[i]->colsum_A) jobs[nj++] = SumRowsJob{g.p[i].part_bias, Sl[i], g.p[i].M, ld[i]->colsum_A};
+                            ld[i]->C, sc};
+    if (ld[i]->colsum_A)
+      jobs[nj++] = SumRowsJob{g.p[i].part_bias, Sl[i], g.p[i].M, ld[i]->colsum_A, sc};
   }
   return sum_rows_jobs(jobs, nj, st);
 }
@@ -752,6 +763,7 @@ extern "C" hgd_status hgd_gemm_rows(const hgd_gemm_rows_desc* descs, int32_t cou
     p.binarize_a = d.binarize_a;
     p.row_inv = d.row_inv;
     p.b_row_count = d.b_row_count;
+    p.b_scale = d.b_scale;
   }
   g.count = count;
   return row_gemm_group(g, as_stream(stream), "hgd_gemm_rows");

@@ -49,7 +49,7 @@ __global__ __launch_bounds__(kWaves * 64) void k_sum_rows(Jobs jobs) {
   float t = s_part[0][lane];
 #pragma unroll
   for (int k = 1; k < kWaves; ++k) t += s_part[k][lane];
-  out[c] = t;
+  out[c] = J.scale != 0.f ? t * J.scale : t;
 }
 
 }  // namespace
@@ -71,7 +71,7 @@ hgd_status sum_rows_jobs(const SumRowsJob* js, int n, hipStream_t st) {
 }
 
 hgd_status sum_rows(const float* P, int64_t S, int64_t W, float* out, hipStream_t st) {
-  const SumRowsJob j{P, S, W, out};
+  const SumRowsJob j{P, S, W, out, 0.f};
   return sum_rows_jobs(&j, 1, st);
 }
 

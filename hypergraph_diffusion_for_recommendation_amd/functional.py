@@ -385,9 +385,9 @@ def dropout(x: torch.Tensor, p: float, seed: Optional[torch.Tensor] = None) -> t
 class _LinearReluDrop(torch.autograd.Function):
     """``dropout(relu(X·Wᵀ + b), p) (+ res)`` in the row GEMM's store (hgd_gemm_rows: the
     ReLU, the dropout mask of the library RNG and its 1/(1-p), the residual as a second
-    output). Backward on the two hgd_linear_backward kernels with the stored dropped activation
-    as the mask (it is > 0 exactly where the ReLU passed and the element was kept) and 1/(1-p)
-    folded into W for dX and into dW / db."""
+    output). Backward: a row GEMM (dX) and a split-K product (dW, db) with the stored dropped
+    activation as the mask (it is > 0 exactly where the ReLU passed and the element was kept) and
+    1/(1-p) folded into W as it is staged and into the dW / db reduction's store."""
 
     @staticmethod
     def forward(ctx, X, weight, bias, res, p: float, seed):
@@ -422,29 +422,31 @@ class _LinearReluDrop(torch.autograd.Function):
         dY = dout.contiguous()
         n, in_f = X.shape
         out_f = W.shape[0]
-        st = torch.cuda.current_stream(dY.device).cuda_stream
+        dev = dY.device
         s = ctx.scale
         dX = dW = db = None
         if ctx.needs_input_grad[0]:
-            Ws = W * s if s != 1.0 else W
+            # dX = (dY ⊙ [Y > 0])·(W·s): the 1/(1-p) scales W as the row GEMM stages it
             dX = torch.empty_like(X)
-            nat.check(lib.hgd_linear_backward_data(
-                dY.data_ptr(), dY.stride(0), Y.data_ptr(), Y.stride(0), n, out_f, Ws.data_ptr(),
-                Ws.stride(0), in_f, dX.data_ptr(), dX.stride(0), st), "hgd_linear_backward_data")
+            d = _rows_desc(dY, W, W.stride(0), 1, out_f, in_f, dX)
+            d.relu_mask, d.ldm = Y.data_ptr(), Y.stride(0)
+            d.b_scale = s if s != 1.0 else 0.0
+            _gemm_rows([d], dev)
         want_b = ctx.has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1] or want_b:
-            dW = torch.empty((out_f, in_f), dtype=torch.float32, device=dY.device)
-            db = torch.empty(out_f, dtype=torch.float32, device=dY.device) if want_b else None
-            wsb = lib.hgd_linear_backward_weight_workspace_size(n, out_f, in_f)
-            ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dY.device)
-            nat.check(lib.hgd_linear_backward_weight(
-                dY.data_ptr(), dY.stride(0), Y.data_ptr(), Y.stride(0), X.data_ptr(),
-                X.stride(0), n, out_f, in_f, dW.data_ptr(), nat.ptr(db), ws.data_ptr(), wsb, st),
-                "hgd_linear_backward_weight")
-            if s != 1.0:
-                dW.mul_(s)
-                if db is not None:
-                    db.mul_(s)
+            # dW = s·(dY ⊙ [Y > 0])ᵀ·X, db = s·Σ_rows (dY ⊙ [Y > 0]): s applied in the reduction
+            dW = torch.empty((out_f, in_f), dtype=torch.float32, device=dev)
+            db = torch.empty(out_f, dtype=torch.float32, device=dev) if want_b else None
+            t = nat.GemmTnDesc()
+            t.A, t.lda, t.relu_mask, t.ldm = dY.data_ptr(), dY.stride(0), Y.data_ptr(), Y.stride(0)
+            t.B, t.ldb, t.rows, t.M, t.N = X.data_ptr(), X.stride(0), n, out_f, in_f
+            t.C, t.colsum_A = dW.data_ptr(), nat.ptr(db)
+            t.c_scale = s if s != 1.0 else 0.0
+            arr = (nat.GemmTnDesc * 1)(t)
+            wsb = lib.hgd_gemm_tn_workspace_size(arr, 1)
+            ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+            nat.check(lib.hgd_gemm_tn(arr, 1, ws.data_ptr(), wsb,
+                                      torch.cuda.current_stream(dev).cuda_stream), "hgd_gemm_tn")
             if not ctx.needs_input_grad[1]:
                 dW = None
         dres = dY if ctx.has_res and ctx.needs_input_grad[3] else None

@@ -295,6 +295,7 @@ typedef struct hgd_gemm_rows_desc {
    * the hyperedge means D_e^-1·Xe of the mean two-hop from the raw column counts colsum_A of the
    * split-K product that made Xe (same product as scaling B beforehand) */
   const float* b_row_count;
+  float b_scale;          /* 0 = off: B × b_scale as it is staged (a Dropout's 1/(1-p) in dX) */
 } hgd_gemm_rows_desc;
 hgd_status hgd_gemm_rows(const hgd_gemm_rows_desc* descs, int32_t count, void* stream);
 
@@ -313,6 +314,7 @@ typedef struct hgd_gemm_tn_desc {
   int32_t binarize_a;     /* A' = (A > 0 ? 1 : 0) instead of A (colsum_A then counts nonzeros) */
   const float* b_row_scale; /* [rows] or NULL: B's row r × b_row_scale[r] as it is loaded (the
                              * vertex means D_v^-1 of the mean two-hop's backward) */
+  float c_scale;          /* 0 = off: C and colsum_A × c_scale as they are stored */
 } hgd_gemm_tn_desc;
 size_t hgd_gemm_tn_workspace_size(const hgd_gemm_tn_desc* descs, int32_t count);
 hgd_status hgd_gemm_tn(const hgd_gemm_tn_desc* descs, int32_t count, void* workspace,

@@ -199,9 +199,13 @@ def test_fused_rejects_bad_descriptor(dev):
 
 @pytest.mark.parametrize("d", [3, 16, 64, 100, 256])
 def test_layer_norm_module_matches_torch(dev, d):
-    """layers.LayerNorm (hgd_row_epilogue_forward/backward) vs nn.LayerNorm: output and the
-    input / γ / β gradients."""
+    """layers.LayerNorm (hgd_row_epilogue_forward/backward) vs nn.LayerNorm in float64: output
+    rows within 1e-5 of the row's scale (tests/_ref64.check_rows); everything else element-wise
+    within 1e-5·Σ|terms| — dx_i = (g_i - mean(g) - x̂_i·mean(g⊙x̂)) / σ with g = γ⊙dY (the
+    terms |g_i|, mean|g|, |x̂_i|·mean|g⊙x̂|, over σ: at d = 3 a row's dx is mostly cancellation,
+    far below its terms), dγ_j = Σ_n dY_nj·x̂_nj and dβ_j = Σ_n dY_nj over the 5003 rows."""
     from hypergraph_diffusion_for_recommendation_amd.layers import LayerNorm
+    from tests import _ref64 as R
     torch.manual_seed(d)
     ref = torch.nn.LayerNorm(d).to(dev)
     with torch.no_grad():
@@ -211,16 +215,27 @@ def test_layer_norm_module_matches_torch(dev, d):
     ours.load_state_dict(ref.state_dict())
     x = (torch.randn(5003, d, device=dev) * 3 + 1)
     dY = torch.randn(5003, d, device=dev)
-    outs = []
-    for m in (ours, ref):
-        xx = x.clone().requires_grad_(True)
-        y = m(xx)
-        g = torch.autograd.grad(y, (xx, m.weight, m.bias), dY)
-        outs.append((y.detach(),) + tuple(g))
-    for name, a, b in zip(("y", "dx", "dgamma", "dbeta"), *outs):
-        s = b.abs().max().item()
-        tol = 2e-5 if name in ("y", "dx") else 2e-5 * 50
-        assert (a - b).abs().max().item() <= tol * s, name
+    xx = x.clone().requires_grad_(True)
+    y = ours(xx)
+    gx, gw, gb = torch.autograd.grad(y, (xx, ours.weight, ours.bias), dY)
+    ref64 = torch.nn.LayerNorm(d).double().cpu()
+    ref64.load_state_dict({k: v.double().cpu() for k, v in ref.state_dict().items()})
+    x64 = x.double().cpu().requires_grad_(True)
+    y64 = ref64(x64)
+    rx, rw, rb = torch.autograd.grad(y64, (x64, ref64.weight, ref64.bias), dY.double().cpu())
+    R.check_rows(y, y64, "y")
+    with torch.no_grad():
+        xhat = (y64 - ref64.bias) / ref64.weight
+        d64 = dY.double().cpu()
+        sigma = (x64.var(1, unbiased=False, keepdim=True) + ref64.eps).sqrt()
+        g = d64 * ref64.weight
+        dx_terms = (g.abs() + g.abs().mean(1, keepdim=True)
+                    + xhat.abs() * (g * xhat).abs().mean(1, keepdim=True)) / sigma
+        for name, got, exp, terms in (("dx", gx, rx, dx_terms),
+                                      ("dgamma", gw, rw, (d64 * xhat).abs().sum(0)),
+                                      ("dbeta", gb, rb, d64.abs().sum(0))):
+            err = (got.double().cpu() - exp).abs()
+            assert bool((err <= 1e-5 * terms).all()), (name, float((err / terms).max()))
 
 
 def test_row_epilogue_standalone_vs_oracle(dev):

@@ -10,8 +10,10 @@ reference's torch calls and the same parameters (deep-copied modules on the host
 * SelfAwareEncoderHD (HD.py:461-487): edhnn_layers[0] for layers 0..L-2, edhnn_layers[1] for the
   last, each on V/E = nonzero(norm_adj > 0) plus the layer-0 residual, eval mode.
 
-Tolerance: 2e-5 relative to the output's magnitude (fp32 sums in a different order); 1e-4 with
-the UGformer (the library's attention on both sides, different kernels)."""
+The restatements run in float64 (deep-copied modules cast to double). Bound: tests/_ref64.check_rows
+— every row (an embedding, a gradient row, a whole γ/β gradient vector) within 1e-5 of that row's
+largest |ref|, no absolute floor; 1e-4 with the UGformer (its attention is the library's
+float32 kernel on our side, float64 on the reference side)."""
 import copy
 from types import SimpleNamespace
 
@@ -21,6 +23,7 @@ import torch
 
 from oracle import hgd_oracle as O
 from oracle import ref_cpu
+from tests import _ref64 as R
 from tests._util import random_coo
 
 pytestmark = pytest.mark.gpu
@@ -42,11 +45,8 @@ def _dropped_cpu(A, keep, seed):
     return ref_cpu.coo_tensor(idx[0][m], idx[1][m], np.asarray(vals)[m] / keep, A.shape)
 
 
-def _close(got, ref, tol=2e-5):
-    got, ref = np.asarray(got), np.asarray(ref)
-    assert got.shape == ref.shape, (got.shape, ref.shape)
-    assert np.abs(got - ref).max() <= tol * max(1.0, np.abs(ref).max()), \
-        np.abs(got - ref).max()
+def _close(got, ref, tol=R.TOL, what="value"):
+    R.check_rows(torch.as_tensor(got), torch.as_tensor(ref), what, tol)
 
 
 def _ln(x, ln):
@@ -80,19 +80,19 @@ def test_self_aware_encoder_fwd_bwd(dev):
     ue, ie = enc(xg, adj_c.to(dev))
     (torch.cat([ue, ie]) * w.to(dev)).sum().backward()
 
-    ec = copy.deepcopy(enc).cpu()
+    ec = copy.deepcopy(enc).cpu().double()
     for p in ec.parameters():
         p.grad = None
-    xc = ego.clone().requires_grad_(True)
-    ref = _self_aware_ref(ec, xc, adj_c, xc)
-    (ref * w).sum().backward()
+    xc = ego.double().requires_grad_(True)
+    ref = _self_aware_ref(ec, xc, adj_c.double(), xc)
+    (ref * w.double()).sum().backward()
     _close(torch.cat([ue, ie]).detach().cpu(), ref.detach())
     _close(xg.grad.cpu(), xc.grad)
     n_checked = 0
     for (n, p), (_, pc) in zip(enc.named_parameters(), ec.named_parameters()):
         if pc.grad is not None:
             assert p.grad is not None, n
-            _close(p.grad.cpu(), pc.grad)
+            _close(p.grad.cpu(), pc.grad, what=f"d {n}")
             n_checked += 1
     assert n_checked == 2 * 3  # γ and β of every layer's LayerNorm
 
@@ -108,7 +108,8 @@ def test_self_aware_encoder_ugformer_eval(dev):
     ego = torch.randn(data.n_users + data.n_items, d)
     with torch.no_grad():
         ue, ie = enc(ego.to(dev), adj_c.to(dev))
-        ref = _self_aware_ref(copy.deepcopy(enc).cpu().eval(), ego, adj_c, ego)
+        ref = _self_aware_ref(copy.deepcopy(enc).cpu().double().eval(), ego.double(),
+                              adj_c.double(), ego.double())
     _close(torch.cat([ue, ie]).cpu(), ref, tol=1e-4)
 
 
@@ -126,12 +127,12 @@ def test_relational_aware_encoder(dev):
     xg = x.to(dev).requires_grad_(True)
     out = enc(xg, kg_c.to(dev), None)
     (out * w.to(dev)).sum().backward()
-    ec = copy.deepcopy(enc).cpu()
-    xc = x.clone().requires_grad_(True)
+    ec = copy.deepcopy(enc).cpu().double()
+    xc = x.double().requires_grad_(True)
     y = xc
     for k in range(2):
-        y = _ln(ref_cpu.hgcn_conv(kg_c, y, act=k != 1, slope=0.2), ec.lns[k]) + xc
-    (y * w).sum().backward()
+        y = _ln(ref_cpu.hgcn_conv(kg_c.double(), y, act=k != 1, slope=0.2), ec.lns[k]) + xc
+    (y * w.double()).sum().backward()
     _close(out.detach().cpu(), y.detach())
     _close(xg.grad.cpu(), xc.grad)
 
@@ -145,12 +146,12 @@ def test_self_aware_encoder_hd_eval(dev):
     ego = torch.randn(data.n_users + data.n_items, d)
     with torch.no_grad():
         ue, ie = enc(ego.to(dev), enc.sparse_norm_adj)
-    ec = copy.deepcopy(enc).cpu().eval()
+    ec = copy.deepcopy(enc).cpu().double().eval()
     idx, vals = O.coo_of(data.norm_adj)
-    adj = ref_cpu.coo_tensor(idx[0], idx[1], vals, data.norm_adj.shape).coalesce()
+    adj = ref_cpu.coo_tensor(idx[0], idx[1], vals, data.norm_adj.shape).coalesce().double()
     keep = adj._values() > 0  # nonzero(norm_adj > 0), row-major
     V, E = adj._indices()[0][keep], adj._indices()[1][keep]
-    x = ego
+    x = ego = ego.double()
     with torch.no_grad():
         for k in range(3):
             blk = ec.edhnn_layers[0 if k != 2 else 1]
