@@ -69,4 +69,7 @@ struct SumRowsJob {
 };
 hgd_status sum_rows_jobs(const SumRowsJob* jobs, int n, hipStream_t st);
 
+// HGD_TUNE_ROWGEMM_BLOCKS (linear.hip): 0 restores the default.
+void set_row_gemm_max_blocks(int blocks);
+
 }  // namespace hgd

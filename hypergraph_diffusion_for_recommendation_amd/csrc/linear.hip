@@ -33,7 +33,8 @@ __device__ __forceinline__ f32x4 relu_mask(f32x4 v, f32x4 m) {
                m.w > 0.f ? v.w : 0.f};
 }
 
-constexpr int kRowGemmMaxBlocks = 512;
+constexpr int kRowGemmMaxBlocks = 512;  // default of HGD_TUNE_ROWGEMM_BLOCKS
+int g_row_gemm_max_blocks = kRowGemmMaxBlocks;
 constexpr int kSplitKResident = 512;
 
 struct RowGemm {
@@ -440,7 +441,8 @@ void blocks_for(const int64_t* rows, int count, int64_t* bx) {
   }
   for (int i = 0; i < count; ++i) {
     bx[i] = want[i];
-    if (total > kRowGemmMaxBlocks) bx[i] = std::max<int64_t>(1, want[i] * kRowGemmMaxBlocks / total);
+    if (total > g_row_gemm_max_blocks)
+      bx[i] = std::max<int64_t>(1, want[i] * g_row_gemm_max_blocks / total);
   }
 }
 
@@ -561,6 +563,10 @@ hgd_status check_rows(const hgd_gemm_rows_desc& d, const char* fn) {
 }
 
 }  // namespace
+
+void set_row_gemm_max_blocks(int blocks) {
+  g_row_gemm_max_blocks = blocks > 0 ? blocks : kRowGemmMaxBlocks;
+}
 }  // namespace hgd
 
 extern "C" hgd_status hgd_linear_forward(const float* X, int64_t ldx, int64_t n_rows,

@@ -741,6 +741,11 @@ extern "C" hgd_status hgd_set_tuning(int32_t key, int32_t value) {
                   "hgd_set_tuning: pass columns must be 0 (auto), 64, 128 or 256");
       g_pass_cols = value;
       return HGD_OK;
+    case HGD_TUNE_ROWGEMM_BLOCKS:
+      HGD_REQUIRE(value == 0 || (value >= 64 && value <= 8192),
+                  "hgd_set_tuning: row-GEMM blocks must be 0 (default) or in [64, 8192]");
+      set_row_gemm_max_blocks(value);
+      return HGD_OK;
     default:
       return fail(HGD_ERR_INVALID_ARG, "hgd_set_tuning: unknown key %d", key);
   }

@@ -62,11 +62,15 @@ typedef enum hgd_epilogue {
  *                         batches (default), 9 both
  *   HGD_TUNE_SPMM_PASS_COLS: widest column pass of a hop without a fused row epilogue
  *                         (64, 128 or 256 fp32 columns; wider rows run as several passes;
- *                         0 = auto, the default: one pass up to 128 columns, else 64) */
+ *                         0 = auto, the default: one pass up to 128 columns, else 64)
+ *   HGD_TUNE_ROWGEMM_BLOCKS: most workgroups of a row-GEMM launch (hgd_gemm_rows, hgd_linear_*;
+ *                         0 = default 512, else 64..8192; each wave takes 16-row tiles at a
+ *                         stride of 4·blocks) */
 typedef enum hgd_tune_key {
   HGD_TUNE_SPMM_UNROLL = 1,
   HGD_TUNE_SPMM_POLICY = 2,
-  HGD_TUNE_SPMM_PASS_COLS = 3
+  HGD_TUNE_SPMM_PASS_COLS = 3,
+  HGD_TUNE_ROWGEMM_BLOCKS = 4
 } hgd_tune_key;
 hgd_status hgd_set_tuning(int32_t key, int32_t value);
 

@@ -2,7 +2,9 @@
 """Microbenchmark of the skinny Linear kernels (hgd_linear_*) against the library GEMMs torch
 uses for the same products, at ED-HNN shapes: rows × d → d. Prints one JSON line per case with
 device times from HIP events (median of --reps) and the achieved HBM rate on the algorithmic
-bytes (inputs read once, outputs written once)."""
+bytes (inputs read once, outputs written once). Each timing brackets --inner back-to-back
+launches (kernel time without the per-launch host gap); HGD_ROWGEMM_BLOCKS sets the row-GEMM
+workgroup cap (hgd_set_tuning key 4) for a sweep."""
 import argparse
 import json
 import os
@@ -17,7 +19,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, nargs="+", default=[69_716, 2_200_000])
     ap.add_argument("--dim", type=int, default=64)
-    ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--reps", type=int, default=30)
+    ap.add_argument("--inner", type=int, default=20)
     args = ap.parse_args()
     import torch
 
@@ -35,10 +38,11 @@ def main():
         for _ in range(args.reps):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            fn()
+            for _ in range(args.inner):
+                fn()
             e1.record()
             e1.synchronize()
-            ts.append(e0.elapsed_time(e1) * 1e3)
+            ts.append(e0.elapsed_time(e1) * 1e3 / args.inner)
         return statistics.median(ts)
 
     for n in args.rows:
@@ -53,7 +57,15 @@ def main():
         wsb = lib.hgd_linear_backward_weight_workspace_size(n, d, d)
         ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
         st = torch.cuda.current_stream().cuda_stream
+        seed = torch.tensor([12345], dtype=torch.int64, device=dev)
+        drop = nat.GemmRowsDesc()
+        drop.A, drop.lda, drop.B, drop.bsk, drop.bsn = X.data_ptr(), d, W.data_ptr(), 1, d
+        drop.bias, drop.relu, drop.Y, drop.ldy, drop.rows, drop.K, drop.N = (
+            b.data_ptr(), 1, Y.data_ptr(), d, n, d, d)
+        drop.drop_seed, drop.drop_keep, drop.drop_scale = seed.data_ptr(), 0.5, 2.0
+        drop_arr = (nat.GemmRowsDesc * 1)(drop)
         cases = {
+            "fwd_drop_hgd": lambda: lib.hgd_gemm_rows(drop_arr, 1, st),
             "fwd_hgd": lambda: lib.hgd_linear_forward(X.data_ptr(), d, n, d, W.data_ptr(), d, d,
                                                       b.data_ptr(), 1, Y.data_ptr(), d, st),
             "fwd_torch": lambda: torch.relu(torch.nn.functional.linear(X, W, b)),
@@ -66,11 +78,12 @@ def main():
                 db.data_ptr(), ws.data_ptr(), wsb, st),
             "bwd_weight_torch": lambda: (torch.mm(dY.t(), X), dY.sum(0)),
         }
-        algo = {"fwd": 2 * n * d * 4, "bwd_data": 3 * n * d * 4, "bwd_weight": 2 * n * d * 4}
+        algo = {"fwd": 2 * n * d * 4, "fwd_drop": 2 * n * d * 4, "bwd_data": 3 * n * d * 4, "bwd_weight": 2 * n * d * 4}
         for name, fn in cases.items():
             us = timed(fn)
             kind = name.rsplit("_", 1)[0]
             print(json.dumps({"case": name, "rows": n, "d": d, "us": round(us, 2),
+                              "rowgemm_blocks": os.environ.get("HGD_ROWGEMM_BLOCKS", "512"),
                               "alg_GBps": round(algo[kind] / us / 1e3, 1)}), flush=True)
 
 
