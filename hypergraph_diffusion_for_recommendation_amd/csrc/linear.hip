@@ -81,8 +81,10 @@ struct RowGemmGroup {
 };
 
 // K = 16·KQ; NT = live 16-column tiles of a 64-column slice (N < 64: no MFMAs on zero columns);
-// MASK: A ⊙ (mask > 0)
-template <int KQ, int NT, bool MASK>
+// MASK: A ⊙ (mask > 0). BLDS: the B fragments are read from LDS (k-contiguous, one 16-byte read
+// per 4 MFMAs) instead of being held in registers — at K = 128 the register copy (128 VGPRs)
+// left one wave per SIMD and the 144 k × 128 × 128 forward ran at 0.32 of the f32 MFMA peak
+template <int KQ, int NT, bool MASK, bool BLDS>
 __global__ __launch_bounds__(256) void k_row_gemm(RowGemmGroup grp) {
   const bool second = grp.count > 1 && static_cast<int>(blockIdx.x) >= grp.nb0;
   const RowGemm p = second ? grp.p[1] : grp.p[0];
@@ -96,7 +98,8 @@ __global__ __launch_bounds__(256) void k_row_gemm(RowGemmGroup grp) {
   // held 64-128 VGPRs and the 69,716 × 64 forward ran 18.4 µs against 16.8 µs for the masked
   // backward-data form with one, which moves 1.5× the bytes (profiles/r02_small_kernels)
   constexpr int SUB = 1;
-  __shared__ float sB[K * LDB];      // Bm[k][n0 + nl], zero past N
+  constexpr int LDK = K + 4;         // BLDS row of 64 + K floats: 16-byte reads spread banks
+  __shared__ float sB[BLDS ? 64 * LDK : K * LDB];  // Bm[k][n0 + nl] (BLDS: at nl·LDK + k)
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int i16 = lane & 15;
@@ -144,11 +147,20 @@ __global__ __launch_bounds__(256) void k_row_gemm(RowGemmGroup grp) {
       const int e = threadIdx.x + 256 * j;
       const int k = p.bsk == 1 ? e % K : e / 64;
       const int nl = p.bsk == 1 ? e / K : e % 64;
-      sB[k * LDB + nl] = tmp[j];
+      if constexpr (BLDS) {
+        // the operand scales as in the register path: × 1/max(count, 1), then × b_scale
+        float v = tmp[j];
+        if (p.b_row_count) v *= 1.f / fmaxf(p.b_row_count[k], 1.f);
+        if (p.b_scale != 0.f) v *= p.b_scale;
+        sB[nl * LDK + k] = v;
+      } else {
+        sB[k * LDB + nl] = tmp[j];
+      }
     }
   }
   __syncthreads();
-  float bf[KQ][4][NT];
+  float bf[BLDS ? 1 : KQ][4][NT];
+  if constexpr (!BLDS) {
 #pragma unroll
   for (int q = 0; q < KQ; ++q)
 #pragma unroll
@@ -173,6 +185,7 @@ __global__ __launch_bounds__(256) void k_row_gemm(RowGemmGroup grp) {
 #pragma unroll
         for (int t = 0; t < NT; ++t) bf[q][c][t] *= p.b_scale;
   }
+  }
   float bias_v[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) bias_v[t] = (p.bias && t < nt) ? p.bias[n0 + 16 * t + i16] : 0.f;
@@ -194,12 +207,26 @@ __global__ __launch_bounds__(256) void k_row_gemm(RowGemmGroup grp) {
       f32x4 acc[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (BLDS) {
 #pragma unroll
-      for (int q = 0; q < KQ; ++q)
+        for (int q = 0; q < KQ; ++q) {
+          f32x4 bq[NT];
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
+          for (int t = 0; t < NT; ++t)
+            bq[t] = *reinterpret_cast<const f32x4*>(&sB[(16 * t + i16) * LDK + 4 * h + 16 * q]);
 #pragma unroll
-          for (int t = 0; t < NT; ++t) acc[t] = mfma4(a[s][q][c], bf[q][c][t], acc[t]);
+          for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int t = 0; t < NT; ++t) acc[t] = mfma4(a[s][q][c], bq[t][c], acc[t]);
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < KQ; ++q)
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int t = 0; t < NT; ++t) acc[t] = mfma4(a[s][q][c], bf[q][c][t], acc[t]);
+      }
       const int64_t r0 = tile * 16 * SUB + 16 * s;
       if (p.row_inv) {
         // Σ_k A[row i16][k]: this lane's 4·KQ columns, then the four lanes h of the row
@@ -470,9 +497,9 @@ hgd_status row_gemm_group(RowGemmGroup g, hipStream_t st, const char* fn) {
 #define HGD_CASE_NT(Q, T)                                                              \
     case Q * 8 + T:                                                                    \
       if (g.p[0].mask)                                                                 \
-        hipLaunchKernelGGL((k_row_gemm<Q, T, true>), grid, dim3(256), 0, st, g);       \
+        hipLaunchKernelGGL((k_row_gemm<Q, T, true, (Q > 4)>), grid, dim3(256), 0, st, g); \
       else                                                                             \
-        hipLaunchKernelGGL((k_row_gemm<Q, T, false>), grid, dim3(256), 0, st, g);      \
+        hipLaunchKernelGGL((k_row_gemm<Q, T, false, (Q > 4)>), grid, dim3(256), 0, st, g); \
       break;
 #define HGD_CASE(Q) HGD_CASE_NT(Q, 1) HGD_CASE_NT(Q, 2) HGD_CASE_NT(Q, 3) HGD_CASE_NT(Q, 4)
     HGD_CASE(1) HGD_CASE(2) HGD_CASE(3) HGD_CASE(4) HGD_CASE(5) HGD_CASE(6) HGD_CASE(7)
