@@ -497,9 +497,9 @@ hgd_status row_gemm_group(RowGemmGroup g, hipStream_t st, const char* fn) {
 #define HGD_CASE_NT(Q, T)                                                              \
     case Q * 8 + T:                                                                    \
       if (g.p[0].mask)                                                                 \
-        hipLaunchKernelGGL((k_row_gemm<Q, T, true, (Q > 4)>), grid, dim3(256), 0, st, g); \
+        hipLaunchKernelGGL((k_row_gemm<Q, T, true, (Q > 1)>), grid, dim3(256), 0, st, g); \
       else                                                                             \
-        hipLaunchKernelGGL((k_row_gemm<Q, T, false, (Q > 4)>), grid, dim3(256), 0, st, g); \
+        hipLaunchKernelGGL((k_row_gemm<Q, T, false, (Q > 1)>), grid, dim3(256), 0, st, g); \
       break;
 #define HGD_CASE(Q) HGD_CASE_NT(Q, 1) HGD_CASE_NT(Q, 2) HGD_CASE_NT(Q, 3) HGD_CASE_NT(Q, 4)
     HGD_CASE(1) HGD_CASE(2) HGD_CASE(3) HGD_CASE(4) HGD_CASE(5) HGD_CASE(6) HGD_CASE(7)
@@ -520,13 +520,17 @@ hgd_status row_gemm(const RowGemm& p, hipStream_t st, const char* fn) {
   return row_gemm_group(g, st, fn);
 }
 
-int64_t splits_for(int64_t rows) {
+int64_t splits_for(int64_t rows, int64_t out_tiles) {
   // ≥ 128 rows per workgroup (two 64-row batches of 4 waves × 16 rows): ≈ 250 workgroups at 32 K
   // rows (the Yelp-shaped learned-hypergraph products), where 512-row splits left 3/4 of the CUs
   // idle; at most 512 workgroups (two per CU at the kernel's two waves per SIMD), so a mid-sized
   // problem runs in one round instead of a full second round for a few leftover workgroups
   int64_t s = (rows + 127) / 128;
-  if (s > kSplitKResident) s = kSplitKResident;
+  // the budget counts workgroups, not slices: each slice is out_tiles workgroups (64 × 64 output
+  // tiles), and the partials written and re-read are S · M · N floats — at M = N = 128, 512
+  // slices were 2,048 workgroups and 34 MB of partials each way
+  const int64_t cap = std::max<int64_t>(1, kSplitKResident / std::max<int64_t>(1, out_tiles));
+  if (s > cap) s = cap;
   return s < 1 ? 1 : s;
 }
 
@@ -534,12 +538,14 @@ int64_t splits_for(int64_t rows) {
 void tn_splits(const hgd_gemm_tn_desc* d, int count, int64_t* S, int64_t* per) {
   int64_t total = 0;
   for (int i = 0; i < count; ++i) {
-    S[i] = splits_for(d[i].rows);
+    S[i] = splits_for(d[i].rows, static_cast<int64_t>((d[i].M + 63) / 64) * ((d[i].N + 63) / 64));
     total += S[i];
   }
   for (int i = 0; i < count; ++i) {
-    if (count > 1 && total > kSplitKResident)
-      S[i] = std::max<int64_t>(1, S[i] * kSplitKResident / total);
+    const int64_t tiles = static_cast<int64_t>((d[0].M + 63) / 64) * ((d[0].N + 63) / 64);
+    const int64_t budget = std::max<int64_t>(1, kSplitKResident / tiles);
+    if (count > 1 && total > budget)
+      S[i] = std::max<int64_t>(1, S[i] * budget / total);
     const int64_t rows = d[i].rows > 0 ? d[i].rows : 1;
     int64_t pr = (rows + S[i] - 1) / S[i];
     per[i] = (pr + 63) / 64 * 64;  // whole 64-row batches
