@@ -64,8 +64,14 @@ def main():
             b.data_ptr(), 1, Y.data_ptr(), d, n, d, d)
         drop.drop_seed, drop.drop_keep, drop.drop_scale = seed.data_ptr(), 0.5, 2.0
         drop_arr = (nat.GemmRowsDesc * 1)(drop)
+        R = torch.randn(n, d, device=dev)
+        Y2 = torch.empty(n, d, device=dev)
+        dres = nat.GemmRowsDesc.from_buffer_copy(drop)
+        dres.res, dres.ldres, dres.Y2, dres.ldy2 = R.data_ptr(), d, Y2.data_ptr(), d
+        dres_arr = (nat.GemmRowsDesc * 1)(dres)
         cases = {
             "fwd_drop_hgd": lambda: lib.hgd_gemm_rows(drop_arr, 1, st),
+            "fwd_drop_res_hgd": lambda: lib.hgd_gemm_rows(dres_arr, 1, st),
             "fwd_hgd": lambda: lib.hgd_linear_forward(X.data_ptr(), d, n, d, W.data_ptr(), d, d,
                                                       b.data_ptr(), 1, Y.data_ptr(), d, st),
             "fwd_torch": lambda: torch.relu(torch.nn.functional.linear(X, W, b)),
@@ -78,7 +84,7 @@ def main():
                 db.data_ptr(), ws.data_ptr(), wsb, st),
             "bwd_weight_torch": lambda: (torch.mm(dY.t(), X), dY.sum(0)),
         }
-        algo = {"fwd": 2 * n * d * 4, "fwd_drop": 2 * n * d * 4, "bwd_data": 3 * n * d * 4, "bwd_weight": 2 * n * d * 4}
+        algo = {"fwd": 2 * n * d * 4, "fwd_drop": 2 * n * d * 4, "fwd_drop_res": 4 * n * d * 4, "bwd_data": 3 * n * d * 4, "bwd_weight": 2 * n * d * 4}
         for name, fn in cases.items():
             us = timed(fn)
             kind = name.rsplit("_", 1)[0]
