@@ -8,6 +8,7 @@ import torch
 
 from oracle import hgd_oracle as O
 from oracle import ref_cpu
+from tests import _ref64 as R
 
 pytestmark = pytest.mark.gpu
 
@@ -37,15 +38,22 @@ def test_infonce_matches_reference_formula(dev, N, d, B, temp):
     ref = ref_cpu.contrast_loss(c1, c2, torch.from_numpy(nodes), temp)
     ref.backward()
     assert abs(ref.item() - O.contrast_loss(E1, E2, nodes, temp)) < 1e-9 * max(1, abs(ref.item()))
-    # loss: a mean of B log-ratios of sums of B exps (|logit| <= 1/temp): fp32 rounding bound
-    assert abs(loss.item() - ref.item()) <= 1e-5 * (abs(ref.item()) + 1.0 / temp)
+    # loss: north_star's 1e-5 relative (measured ≤ 1.4e-7)
+    assert abs(loss.item() - ref.item()) <= 1e-5 * abs(ref.item())
+    batch = torch.unique(torch.from_numpy(nodes))
+    live = batch[batch != 0]
     for got, want in ((g1.grad, c1.grad), (g2.grad, c2.grad)):
         got = got.double().cpu()
+        if live.numel() > 1:
+            # every batch row within 1e-5 of its own largest |gradient| (tests/_ref64.check_rows;
+            # measured ≤ 1.7e-6 over these cases)
+            R.check_rows(got[live], want[live], "dE rows")
+        # the zero row's gradient is the 1/‖x + 1e-8‖-amplified dp, and a batch of one repeated
+        # node has a true gradient of O(1e-8·coef) that fp32 rounds to 0 (in the reference's fp32
+        # run too): those are held to the largest gradient, with a floor at fp32 resolution of
+        # the per-row softmax weights (coef = 1/(B·τ))
         scale = want.abs().max().item() + 1e-30
         err = (got - want).abs().max().item()
-        # relative to the largest gradient, with a floor at fp32 resolution of the per-row
-        # softmax weights (coef = 1/(B·τ)): a batch of one repeated node has a true gradient
-        # of O(1e-8·coef) that fp32 rounds to 0, in the reference's fp32 run too
         assert err <= 1e-4 * scale + 1e-7 / (B * temp), (err, scale)
         # rows outside the batch get exactly zero gradient
         outside = torch.ones(N, dtype=torch.bool)
@@ -104,8 +112,10 @@ def test_infonce_torch_index_semantics(dev):
     c2 = E2.detach().double().cpu().requires_grad_(True)
     ref = ref_cpu.contrast_loss(c1, c2, nodes.cpu(), 0.2)
     ref.backward()
-    assert abs(loss.item() - ref.item()) <= 1e-5 * (abs(ref.item()) + 5.0)
-    assert (E1.grad.double().cpu() - c1.grad).abs().max().item() <= 1e-4 * c1.grad.abs().max().item()
+    assert abs(loss.item() - ref.item()) <= 1e-5 * abs(ref.item())
+    rows = torch.unique(nodes.cpu() % 50)
+    R.check_rows(E1.grad.double().cpu()[rows], c1.grad[rows], "dE1 rows")
+    R.check_rows(E2.grad.double().cpu()[rows], c2.grad[rows], "dE2 rows")
     with pytest.raises(IndexError):
         contrast_loss(E1, E2, torch.tensor([0, 50], device=dev), 0.2)
     with pytest.raises(IndexError):
