@@ -403,5 +403,28 @@ def ptr(t) -> int | None:
 
 
 def stream_handle(device=None) -> int:
+    """The raw ``hipStream_t`` of torch's current stream on ``device`` (a torch.device, an index
+    or None for the current device). torch's ``current_stream(device).cuda_stream`` builds a
+    Stream object per call (≈ 10 µs — a quarter of an eager hop's host time at dataset sizes);
+    the raw getter returns the same handle in well under a microsecond."""
     import torch
+    if _RAW_STREAM is not None:
+        if device is None:
+            idx = torch.cuda.current_device()
+        elif isinstance(device, int):
+            idx = device
+        else:
+            idx = device.index if device.index is not None else torch.cuda.current_device()
+        return _RAW_STREAM(idx)
     return torch.cuda.current_stream(device).cuda_stream
+
+
+def _raw_stream_getter():
+    try:
+        import torch
+        return getattr(torch._C, "_cuda_getCurrentRawStream", None)
+    except Exception:  # pragma: no cover - torch without the HIP module
+        return None
+
+
+_RAW_STREAM = _raw_stream_getter()

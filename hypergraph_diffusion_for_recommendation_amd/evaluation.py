@@ -43,7 +43,7 @@ def topk_rows(scores: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]
     vals = torch.empty((n, k), dtype=torch.float32, device=scores.device)
     nat.check(nat.load().hgd_topk_rows(scores.data_ptr(), n, m, scores.stride(0), int(k),
                                        ids.data_ptr(), vals.data_ptr(),
-                                       torch.cuda.current_stream(scores.device).cuda_stream),
+                                       nat.stream_handle(scores.device)),
               "hgd_topk_rows")
     return ids, vals
 
@@ -55,7 +55,7 @@ def mask_scores(scores: torch.Tensor, rated: CSR, users: torch.Tensor,
     nat.check(nat.load().hgd_mask_scores(
         scores.data_ptr(), scores.shape[0], scores.stride(0), rated.rowptr.data_ptr(),
         rated.col.data_ptr() if rated.nnz else None, row_map.data_ptr(), float(value),
-        torch.cuda.current_stream(scores.device).cuda_stream), "hgd_mask_scores")
+        nat.stream_handle(scores.device)), "hgd_mask_scores")
     return scores
 
 
@@ -141,7 +141,7 @@ def rank_metrics(ids: torch.Tensor, tests: TestLists, cutoffs: Sequence[int],
         ids.data_ptr(), n, ids.stride(0), k, tests.rowptr.data_ptr(),
         tests.cols.data_ptr() if tests.cols.numel() else None, carr, len(cut),
         discount.data_ptr(), hits.data_ptr(), dcg.data_ptr(),
-        torch.cuda.current_stream(ids.device).cuda_stream), "hgd_rank_metrics")
+        nat.stream_handle(ids.device)), "hgd_rank_metrics")
     return hits.cpu().numpy(), dcg.cpu().numpy()
 
 

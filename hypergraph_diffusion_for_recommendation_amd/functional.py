@@ -41,7 +41,7 @@ def _epilogue_backward(ref: torch.Tensor, dy: torch.Tensor, epi: int, slope: flo
     dz = torch.empty_like(dy)
     nat.check(nat.load().hgd_epilogue_backward(ref.data_ptr(), dy.data_ptr(), dy.numel(), epi,
                                                float(slope), dz.data_ptr(),
-                                               torch.cuda.current_stream(dy.device).cuda_stream),
+                                               nat.stream_handle(dy.device)),
               "hgd_epilogue_backward")
     return dz
 
@@ -50,7 +50,7 @@ def _epilogue_apply(z: torch.Tensor, epi: int, slope: float):
     y = torch.empty_like(z)
     nat.check(nat.load().hgd_epilogue_apply(z.data_ptr(), z.numel(), epi, float(slope),
                                             y.data_ptr(),
-                                            torch.cuda.current_stream(z.device).cuda_stream),
+                                            nat.stream_handle(z.device)),
               "hgd_epilogue_apply")
     return y
 
@@ -209,7 +209,7 @@ class _FusedTwoHop(torch.autograd.Function):
             dY.data_ptr(), dY.stride(0), nat.ptr(A), 0 if A is None else A.stride(0),
             nat.ptr(stats), nat.ptr(gamma), n, d, epi, float(slope), int(ln), float(out_scale),
             dZ.data_ptr(), dZ.stride(0), nat.ptr(dgamma), nat.ptr(dbeta), nat.ptr(ws), wsb,
-            torch.cuda.current_stream(dev).cuda_stream), "hgd_row_epilogue_backward")
+            nat.stream_handle(dev)), "hgd_row_epilogue_backward")
         dX = None
         if ctx.needs_input_grad[0]:
             q = inc.scale("col", Q)
@@ -280,7 +280,7 @@ class _Linear(torch.autograd.Function):
         n, in_f = X.shape
         out_f = W.shape[0]
         Y = torch.empty((n, out_f), dtype=torch.float32, device=X.device)
-        st = torch.cuda.current_stream(X.device).cuda_stream
+        st = nat.stream_handle(X.device)
         nat.check(lib.hgd_linear_forward(X.data_ptr(), X.stride(0), n, in_f, W.data_ptr(),
                                          W.stride(0), out_f, nat.ptr(bias), int(relu),
                                          Y.data_ptr(), Y.stride(0), st), "hgd_linear_forward")
@@ -296,7 +296,7 @@ class _Linear(torch.autograd.Function):
         dY = dY.contiguous()
         n, in_f = X.shape
         out_f = W.shape[0]
-        st = torch.cuda.current_stream(dY.device).cuda_stream
+        st = nat.stream_handle(dY.device)
         dX = dW = db = None
         if ctx.needs_input_grad[0]:
             dX = torch.empty_like(X)
@@ -347,7 +347,7 @@ def _dropout_call(x: torch.Tensor, p: float, seed: torch.Tensor) -> torch.Tensor
     y = torch.empty_like(x)
     nat.check(nat.load().hgd_dropout_apply(x.data_ptr(), x.numel(), seed.data_ptr(), keep, scale,
                                            y.data_ptr(),
-                                           torch.cuda.current_stream(x.device).cuda_stream),
+                                           nat.stream_handle(x.device)),
               "hgd_dropout_apply")
     return y
 
@@ -446,7 +446,7 @@ class _LinearReluDrop(torch.autograd.Function):
             wsb = lib.hgd_gemm_tn_workspace_size(arr, 1)
             ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
             nat.check(lib.hgd_gemm_tn(arr, 1, ws.data_ptr(), wsb,
-                                      torch.cuda.current_stream(dev).cuda_stream), "hgd_gemm_tn")
+                                      nat.stream_handle(dev)), "hgd_gemm_tn")
             if not ctx.needs_input_grad[1]:
                 dW = None
         dres = dY if ctx.has_res and ctx.needs_input_grad[3] else None
@@ -498,7 +498,7 @@ class _RowEpilogue(torch.autograd.Function):
         Y = torch.empty_like(Z)
         nat.check(nat.load().hgd_row_epilogue_forward(
             Z.data_ptr(), Z.stride(0), n, d, ctypes.byref(ex), Y.data_ptr(), Y.stride(0),
-            torch.cuda.current_stream(dev).cuda_stream), "hgd_row_epilogue_forward")
+            nat.stream_handle(dev)), "hgd_row_epilogue_forward")
         ctx.cfg = cfg
         ctx.has_res = (res1 is not None, res2 is not None)
         ctx.save_for_backward(A, stats, gamma if ln else None)
@@ -525,7 +525,7 @@ class _RowEpilogue(torch.autograd.Function):
                 dY.data_ptr(), dY.stride(0), nat.ptr(A), 0 if A is None else A.stride(0),
                 nat.ptr(stats), nat.ptr(gamma), n, d, epi, float(slope), int(ln),
                 float(out_scale), dZ.data_ptr(), dZ.stride(0), nat.ptr(dgamma), nat.ptr(dbeta),
-                nat.ptr(ws), wsb, torch.cuda.current_stream(dev).cuda_stream),
+                nat.ptr(ws), wsb, nat.stream_handle(dev)),
                 "hgd_row_epilogue_backward")
 
         def res_grad(k, s):
@@ -585,7 +585,7 @@ class _ContrastLoss(torch.autograd.Function):
         loss = torch.empty((), **f)
         wsb = lib.hgd_infonce_workspace_size(B, d)
         ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
-        st = torch.cuda.current_stream(dev).cuda_stream
+        st = nat.stream_handle(dev)
         if count is None:
             nat.check(lib.hgd_infonce_forward(
                 E1c.data_ptr(), E1c.stride(0), E2c.data_ptr(), E2c.stride(0), E1.shape[0],
@@ -613,7 +613,7 @@ class _ContrastLoss(torch.autograd.Function):
         g = g.to(dtype=torch.float32).reshape(1).contiguous()
         wsb = lib.hgd_infonce_workspace_size(B, d)
         ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
-        st = torch.cuda.current_stream(dev).cuda_stream
+        st = nat.stream_handle(dev)
         dE1 = dE2 = None
         if ctx.has_count:
             # the scatter into the table gradients runs inside the backward kernel (live rows
@@ -683,7 +683,7 @@ class _ContrastLossPair(torch.autograd.Function):
             saved += [P1, P2, inv1, inv2, deno, nodes, count]
             keep.append(ws)
         nat.check(lib.hgd_infonce_forward_group(terms, 2, d, float(temp),
-                                                torch.cuda.current_stream(dev).cuda_stream),
+                                                nat.stream_handle(dev)),
                   "hgd_infonce_forward_group")
         ctx.temp = float(temp)
         ctx.nu, ctx.N, ctx.d = nu, N, d
@@ -723,7 +723,7 @@ class _ContrastLossPair(torch.autograd.Function):
                 t.dE2, t.ldE2 = dE2.data_ptr() + off, d
             t.workspace, t.workspace_bytes = ws.data_ptr(), wsb
         nat.check(lib.hgd_infonce_backward_group(terms, 2, d, ctx.temp, g.data_ptr(),
-                                                 torch.cuda.current_stream(dev).cuda_stream),
+                                                 nat.stream_handle(dev)),
                   "hgd_infonce_backward_group")
         return dE1, dE2, None, None, None, None, None, None
 
@@ -799,7 +799,7 @@ def unique_long(x: torch.Tensor) -> torch.Tensor:
     # [count | pad | workspace]: the workspace starts with the kernels' (min, max) state, so one
     # 272-byte copy returns the count and the range
     buf = torch.empty(_UQ_HEAD + max(wsb, 1), dtype=torch.uint8, device=dev)
-    st = torch.cuda.current_stream(dev).cuda_stream
+    st = nat.stream_handle(dev)
     f = x.dtype == torch.float32
     fast = lib.hgd_unique_trunc_f32 if f else lib.hgd_unique_i64
     base = buf.data_ptr()
@@ -842,7 +842,7 @@ def unique_long_n(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     base = buf.data_ptr()
     fn = lib.hgd_unique_dev_trunc_f32 if x.dtype == torch.float32 else lib.hgd_unique_dev_i64
     nat.check(fn(x.data_ptr(), n, out.data_ptr(), base, base + _UQ_HEAD, wsb,
-                 torch.cuda.current_stream(dev).cuda_stream), "hgd_unique_dev")
+                 nat.stream_handle(dev)), "hgd_unique_dev")
     count = buf[:8].view(torch.int64)
     live = torch.arange(n, device=dev) < count
     return torch.where(live, out, torch.zeros((), dtype=torch.int64, device=dev)), count
@@ -866,7 +866,7 @@ def _tn(A: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
     ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=A.device)
     nat.check(lib.hgd_linear_backward_weight(
         A.data_ptr(), A.stride(0), None, 0, B.data_ptr(), B.stride(0), n, m, k, C.data_ptr(),
-        None, ws.data_ptr(), wsb, torch.cuda.current_stream(A.device).cuda_stream),
+        None, ws.data_ptr(), wsb, nat.stream_handle(A.device)),
         "hgd_linear_backward_weight")
     return C
 
@@ -879,7 +879,7 @@ def _nn(A: torch.Tensor, M: torch.Tensor) -> torch.Tensor:
     Y = torch.empty((n, k), dtype=torch.float32, device=A.device)
     nat.check(lib.hgd_linear_backward_data(
         A.data_ptr(), A.stride(0), None, 0, n, m, M.data_ptr(), M.stride(0), k, Y.data_ptr(),
-        Y.stride(0), torch.cuda.current_stream(A.device).cuda_stream), "hgd_linear_backward_data")
+        Y.stride(0), nat.stream_handle(A.device)), "hgd_linear_backward_data")
     return Y
 
 
@@ -891,7 +891,7 @@ def _nt(A: torch.Tensor, M: torch.Tensor) -> torch.Tensor:
     Y = torch.empty((n, m), dtype=torch.float32, device=A.device)
     nat.check(lib.hgd_linear_forward(A.data_ptr(), A.stride(0), n, k, M.data_ptr(), M.stride(0),
                                      m, None, 0, Y.data_ptr(), Y.stride(0),
-                                     torch.cuda.current_stream(A.device).cuda_stream),
+                                     nat.stream_handle(A.device)),
               "hgd_linear_forward")
     return Y
 
@@ -944,7 +944,7 @@ def _rows_desc(A, B, bsk, bsn, K, N, Y, accumulate=False):
 def _gemm_rows(descs, device):
     arr = (nat.GemmRowsDesc * len(descs))(*descs)
     nat.check(nat.load().hgd_gemm_rows(arr, len(descs),
-                                       torch.cuda.current_stream(device).cuda_stream),
+                                       nat.stream_handle(device)),
               "hgd_gemm_rows")
 
 
@@ -965,7 +965,7 @@ def _gemm_tn_pair(pairs, device):
     wsb = lib.hgd_gemm_tn_workspace_size(arr, len(descs))
     ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=device)
     nat.check(lib.hgd_gemm_tn(arr, len(descs), ws.data_ptr(), wsb,
-                              torch.cuda.current_stream(device).cuda_stream), "hgd_gemm_tn")
+                              nat.stream_handle(device)), "hgd_gemm_tn")
     return outs
 
 
@@ -1085,7 +1085,7 @@ class _HCCFLayers(torch.autograd.Function):
             Ms += [M_u, M_i]
         E = torch.empty((N, d), **f)
         nat.check(nat.load().hgd_sum_slices(hid.data_ptr(), L + 1, N * d, N * d, E.data_ptr(),
-                                            torch.cuda.current_stream(dev).cuda_stream),
+                                            nat.stream_handle(dev)),
                   "hgd_sum_slices")
         ctx.adjs, ctx.nu, ctx.L, ctx.K = adjs, nu, L, K
         ctx.save_for_backward(hid, *Hs, *Ms)
@@ -1190,7 +1190,7 @@ class _BPRTable(torch.autograd.Function):
         nat.check(lib.hgd_bpr_forward(
             E.data_ptr(), E.stride(0), nu, N - nu, d, uid.data_ptr(), pid.data_ptr(),
             nid.data_ptr(), B, anc.data_ptr(), pos.data_ptr(), coef.data_ptr(), loss.data_ptr(),
-            ws.data_ptr(), wsb, torch.cuda.current_stream(dev).cuda_stream), "hgd_bpr_forward")
+            ws.data_ptr(), wsb, nat.stream_handle(dev)), "hgd_bpr_forward")
         ctx.nu = nu
         ctx.save_for_backward(E, uid, pid, nid, coef)
         ctx.mark_non_differentiable(anc, pos)
@@ -1210,7 +1210,7 @@ class _BPRTable(torch.autograd.Function):
         nat.check(lib.hgd_bpr_backward(
             E.data_ptr(), E.stride(0), ctx.nu, N - ctx.nu, d, uid.data_ptr(), pid.data_ptr(),
             nid.data_ptr(), B, coef.data_ptr(), g.data_ptr(), dE.data_ptr(), dE.stride(0),
-            ws.data_ptr(), wsb, torch.cuda.current_stream(dev).cuda_stream), "hgd_bpr_backward")
+            ws.data_ptr(), wsb, nat.stream_handle(dev)), "hgd_bpr_backward")
         return dE, None, None, None, None
 
 
@@ -1267,7 +1267,7 @@ def _bin_tn(parts, K: int, d: int, dev, colsum: Optional[torch.Tensor],
     wsb = lib.hgd_gemm_tn_workspace_size(arr, len(parts))
     ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
     nat.check(lib.hgd_gemm_tn(arr, len(parts), ws.data_ptr(), wsb,
-                              torch.cuda.current_stream(dev).cuda_stream), "hgd_gemm_tn")
+                              nat.stream_handle(dev)), "hgd_gemm_tn")
     return C
 
 

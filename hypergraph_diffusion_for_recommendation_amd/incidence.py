@@ -52,7 +52,7 @@ def _ws(nbytes: int, device) -> torch.Tensor:
 
 
 def _stream(device) -> int:
-    return torch.cuda.current_stream(device).cuda_stream
+    return nat.stream_handle(device)
 
 
 class CSR:
@@ -64,6 +64,7 @@ class CSR:
                  split_chunk: int = DEFAULT_SPLIT_CHUNK, plan_counts: Optional[Tuple] = None):
         self.rowptr = rowptr
         self.col = col
+        self._ws_bytes: Dict[int, int] = {}  # hgd_spmm_workspace_size per width (spmm_csr)
         self.n_rows = int(n_rows)
         self.n_cols = int(n_cols)
         self.nnz = int(col.numel())
@@ -88,6 +89,7 @@ class CSR:
         return counts
 
     def _build_plan(self, n_heavy: int, n_chunks: int) -> None:
+        self._ws_bytes = {}
         n_heavy, n_chunks = int(n_heavy), int(n_chunks)
         if n_heavy == 0:
             self.plan.threshold = 0
@@ -125,6 +127,7 @@ class CSR:
             segmented = False
         short = (self.n_rows > 0 and self.nnz < SEGMENTED_MAX_AVG_DEGREE * self.n_rows)
         self.plan.flags = 1 if (segmented and short and self.n_heavy == 0) else 0
+        self._ws_bytes = {}
 
     @property
     def segmented(self) -> bool:
@@ -175,7 +178,10 @@ def spmm_csr(csr: CSR, X: torch.Tensor, val: Optional[torch.Tensor] = None,
         raise ValueError("spmm: row_scale size mismatch")
     lib = nat.load()
     plan_ptr = ctypes.byref(csr.plan)
-    wsb = lib.hgd_spmm_workspace_size(plan_ptr, d)
+    # the plan is immutable once built: its workspace size per width is asked for once
+    wsb = csr._ws_bytes.get(d)
+    if wsb is None:
+        wsb = csr._ws_bytes[d] = lib.hgd_spmm_workspace_size(plan_ptr, d)
     ws = _ws(wsb, X.device) if wsb else None
     timer = profiling.active()
     if timer is not None:

@@ -214,7 +214,7 @@ class SpAdjDropEdge(nn.Module):
             if mask.numel():
                 nat.check(nat.load().hgd_bernoulli_mask(
                     seed, mask.numel(), float(keepRate), mask.data_ptr(),
-                    torch.cuda.current_stream(device).cuda_stream), "hgd_bernoulli_mask")
+                    nat.stream_handle(device)), "hgd_bernoulli_mask")
             count = None
         else:
             mask, count = torch_cpu_keep_mask(vals.numel(), keepRate)
@@ -246,7 +246,7 @@ class SpAdjDropEdge(nn.Module):
         if parent.nnz:
             nat.check(nat.load().hgd_bernoulli_mask_dev_pair(
                 self._seed.data_ptr(), parent.perm_t.data_ptr(), parent.nnz, keep,
-                mask.data_ptr(), mask_t.data_ptr(), torch.cuda.current_stream(dev).cuda_stream),
+                mask.data_ptr(), mask_t.data_ptr(), nat.stream_handle(dev)),
                 "hgd_bernoulli_mask_dev_pair")
         self._seed.add_(1)
         return parent.masked(mask, keep, mask_t)

@@ -294,7 +294,7 @@ def _fold(base: Optional[torch.Tensor], scale: torch.Tensor, col: torch.Tensor, 
     if nnz:
         nat.check(nat.load().hgd_edge_values(
             nat.ptr(base), None, scale.data_ptr(), col.data_ptr(), nnz, out.data_ptr(),
-            torch.cuda.current_stream(scale.device).cuda_stream), "hgd_edge_values")
+            nat.stream_handle(scale.device)), "hgd_edge_values")
     return out
 
 
@@ -433,7 +433,7 @@ class ShardedBipartite:
             if inc.nnz:
                 nat.check(lib.hgd_bernoulli_mask(
                     (int(seed) * 2 + k) & ((1 << 62) - 1), inc.nnz, float(keep), m.data_ptr(),
-                    torch.cuda.current_stream(inc.device).cuda_stream), "hgd_bernoulli_mask")
+                    nat.stream_handle(inc.device)), "hgd_bernoulli_mask")
             masks.append(m)
         return self.drop(keep, masks[0], masks[1])
 
@@ -546,7 +546,7 @@ class _BipartiteHopFused(torch.autograd.Function):
             ex = ex_rows(n)
             nat.check(nat.load().hgd_row_epilogue_forward(
                 Zi.data_ptr(), Zi.stride(0), sh.n_items, d, ctypes.byref(ex), Y[n:].data_ptr(),
-                Y.stride(0), torch.cuda.current_stream(dev).cuda_stream),
+                Y.stride(0), nat.stream_handle(dev)),
                 "hgd_row_epilogue_forward")
         ctx.sh, ctx.kind, ctx.cfg = sh, kind, cfg
         ctx.has_res = (res1 is not None, res2 is not None)
@@ -575,7 +575,7 @@ class _BipartiteHopFused(torch.autograd.Function):
                 dY.data_ptr(), dY.stride(0), nat.ptr(A), 0 if A is None else A.stride(0),
                 nat.ptr(stats), nat.ptr(gamma), N, d, epi, float(slope), int(ln),
                 float(out_scale), dZ.data_ptr(), dZ.stride(0), nat.ptr(dgamma), nat.ptr(dbeta),
-                nat.ptr(ws), wsb, torch.cuda.current_stream(dev).cuda_stream),
+                nat.ptr(ws), wsb, nat.stream_handle(dev)),
                 "hgd_row_epilogue_backward")
         dX = _bipartite_backward(ctx.sh, ctx.kind, dZ) if ctx.needs_input_grad[0] else None
 
