@@ -82,7 +82,29 @@ struct RowGemmGroup {
   RowGemm p[2];
   int32_t count;
   int32_t nb0;
+  int32_t nbt;  // row-block workgroups of the group (nb0 + the second's); a multiple of 8 when
+                // ny > 1
+  int32_t ny;   // 64-column slices of N
 };
+
+// Workgroup → (row block, column slice). With one slice it is blockIdx.x. With ny > 1 the slices
+// of a row block get flat ids f, f + 8, …: the dispatcher places consecutive ids on consecutive
+// XCDs, so ids 8 apart share one XCD's L2 and start together — the slices walk the same row tiles
+// in the same order, so the other slices' A tile (and ReLU mask) reads hit that L2. At
+// 144,242 × 128 → 128: forward 53.4 → 52.3 µs, backward-data 78.1 → 75.3 µs against the
+// slice-major order (profiles/r02_linear/xcd_pairing_ab.txt); the second read was mostly served
+// by the Infinity Cache already — these products are bound by the MFMA issue, not by A.
+__device__ __forceinline__ void row_block_of(const RowGemmGroup& g, int& bxg, int& y) {
+  const int f = static_cast<int>(blockIdx.x);
+  if (g.ny == 1) {
+    bxg = f;
+    y = 0;
+    return;
+  }
+  const int grp = f / (8 * g.ny), r = f % (8 * g.ny);
+  y = r / 8;
+  bxg = grp * 8 + r % 8;
+}
 
 // K = 16·KQ; NT = live 16-column tiles of a 64-column slice (N < 64: no MFMAs on zero columns);
 // MASK: A ⊙ (mask > 0). BLDS: the B fragments are read from LDS (k-contiguous, one 16-byte read
@@ -90,11 +112,12 @@ struct RowGemmGroup {
 // left one wave per SIMD and the 144 k × 128 × 128 forward ran at 0.32 of the f32 MFMA peak
 template <int KQ, int NT, bool MASK, bool BLDS>
 __global__ __launch_bounds__(256) void k_row_gemm(RowGemmGroup grp) {
-  const bool second = grp.count > 1 && static_cast<int>(blockIdx.x) >= grp.nb0;
+  int bxg, ys;
+  row_block_of(grp, bxg, ys);
+  const bool second = grp.count > 1 && bxg >= grp.nb0;
   const RowGemm p = second ? grp.p[1] : grp.p[0];
-  const int bx = static_cast<int>(blockIdx.x) - (second ? grp.nb0 : 0);
-  const int nbx = grp.count > 1 ? (second ? static_cast<int>(gridDim.x) - grp.nb0 : grp.nb0)
-                                : static_cast<int>(gridDim.x);
+  const int bx = bxg - (second ? grp.nb0 : 0);
+  const int nbx = grp.count > 1 ? (second ? grp.nbt - grp.nb0 : grp.nb0) : grp.nbt;
   constexpr int K = 16 * KQ;
   constexpr int LDB = 65;           // padded row: the k-contiguous staging writes spread banks
   constexpr int PER = K * 64 / 256;  // staged floats per thread
@@ -112,7 +135,7 @@ __global__ __launch_bounds__(256) void k_row_gemm(RowGemmGroup grp) {
   const int wave = threadIdx.x >> 6;
   const int i16 = lane & 15;
   const int h = lane >> 4;
-  const int n0 = blockIdx.y * 64;
+  const int n0 = ys * 64;
   const int nt = min(NT, (p.N - n0) / 16);  // live 16-column tiles of this slice (uniform)
   const int64_t tiles = (p.rows + 16 * SUB - 1) / (16 * SUB);  // super-tiles
   const int64_t stride = static_cast<int64_t>(nbx) * 4;
@@ -540,8 +563,12 @@ hgd_status row_gemm_group(RowGemmGroup g, hipStream_t st, const char* fn) {
   const int64_t rows[2] = {g.p[0].rows, g.count > 1 ? g.p[1].rows : 0};
   int64_t bx[2] = {0, 0};
   blocks_for(rows, g.count, bx);
+  g.ny = (p.N + 63) / 64;
+  if (g.ny > 1)  // whole groups of 8 row blocks per product (row_block_of's XCD pairing)
+    for (int i = 0; i < g.count; ++i) bx[i] = (bx[i] + 7) / 8 * 8;
   g.nb0 = static_cast<int32_t>(bx[0]);
-  const dim3 grid(static_cast<unsigned>(bx[0] + bx[1]), static_cast<unsigned>((p.N + 63) / 64));
+  g.nbt = static_cast<int32_t>(bx[0] + bx[1]);
+  const dim3 grid(static_cast<unsigned>(g.nbt) * static_cast<unsigned>(g.ny));
   // 16-column tiles per slice: 4 for N >= 64, else N / 16 (the slice is the whole N)
   const int ntiles = g.p[0].N >= 64 ? 4 : g.p[0].N / 16;
   switch ((g.p[0].K / 16) * 8 + ntiles) {
