@@ -111,7 +111,7 @@ __device__ __forceinline__ void row_block_of(const RowGemmGroup& g, int& bxg, in
 // per 4 MFMAs) instead of being held in registers — at K = 128 the register copy (128 VGPRs)
 // left one wave per SIMD and the 144 k × 128 × 128 forward ran at 0.32 of the f32 MFMA peak
 template <int KQ, int NT, bool MASK, bool BLDS>
-__global__ __launch_bounds__(256) void k_row_gemm(RowGemmGroup grp) {
+__device__ __forceinline__ void row_gemm_body(const RowGemmGroup& grp) {
   int bxg, ys;
   row_block_of(grp, bxg, ys);
   const bool second = grp.count > 1 && bxg >= grp.nb0;
@@ -149,7 +149,7 @@ __global__ __launch_bounds__(256) void k_row_gemm(RowGemmGroup grp) {
   float rv0[NT][4], rv1[NT][4];
   auto load = [&](int64_t tl, f32x4 (&a)[SUB][KQ], f32x4 (&m)[SUB][KQ], float (&rv)[NT][4]) {
     tl = tl < tiles ? tl : tiles - 1;
-    if (p.Y2) {
+    if (!MASK && p.Y2) {
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -245,7 +245,7 @@ __global__ __launch_bounds__(256) void k_row_gemm(RowGemmGroup grp) {
 #pragma unroll
         for (int q = 0; q < KQ; ++q) a[s][q] = relu_mask(a[s][q], m[s][q]);
       }
-      if (p.binarize_a) {
+      if (!MASK && p.binarize_a) {
 #pragma unroll
         for (int q = 0; q < KQ; ++q)
 #pragma unroll
@@ -275,7 +275,7 @@ __global__ __launch_bounds__(256) void k_row_gemm(RowGemmGroup grp) {
             for (int t = 0; t < NT; ++t) acc[t] = mfma4(a[s][q][c], bf[q][c][t], acc[t]);
       }
       const int64_t r0 = tile * 16 * SUB + 16 * s;
-      if (p.row_inv) {
+      if (!MASK && p.row_inv) {
         // Σ_k A[row i16][k]: this lane's 4·KQ columns, then the four lanes h of the row
         float rs = 0.f;
 #pragma unroll
@@ -298,7 +298,7 @@ __global__ __launch_bounds__(256) void k_row_gemm(RowGemmGroup grp) {
           const float v = acc[t][r] + bias_v[t];
           acc[t][r] = (p.relu && v < 0.f) ? 0.f : v;
         }
-      if (p.drop_seed) {
+      if (!MASK && p.drop_seed) {
 #pragma unroll
         for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -359,7 +359,7 @@ __global__ __launch_bounds__(256) void k_row_gemm(RowGemmGroup grp) {
             if (t < nt && r0 + 4 * h + r < p.rows)
               yb[(r0 + 4 * h + r) * p.ldy + 16 * t] = acc[t][r];
       }
-      if (p.Y2) {
+      if (!MASK && p.Y2) {
         float* y2 = p.Y2 + n0 + i16;
 #pragma unroll
         for (int t = 0; t < NT; ++t)
@@ -385,6 +385,21 @@ __global__ __launch_bounds__(256) void k_row_gemm(RowGemmGroup grp) {
     __builtin_amdgcn_sched_barrier(0);
     tile += stride;
   }
+}
+
+// Unmasked (forward) products: the compiler's own register budget (2-3 waves per SIMD).
+template <int KQ, int NT, bool BLDS>
+__global__ __launch_bounds__(256) void k_row_gemm(RowGemmGroup grp) {
+  row_gemm_body<KQ, NT, false, BLDS>(grp);
+}
+
+// Masked (backward-data) products: held to two waves per SIMD. At K = 128 the operand and mask
+// ping-pong took 259 registers (one wave per SIMD) and dX = (dY ⊙ [Y > 0])·W at 144,242 × 128
+// ran 75 µs; at two waves it runs 61 µs (profiles/r02_linear/occupancy_masked.txt).
+template <int KQ, int NT, bool BLDS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_row_gemm_masked(
+    RowGemmGroup grp) {
+  row_gemm_body<KQ, NT, true, BLDS>(grp);
 }
 
 struct SplitK {
@@ -575,9 +590,9 @@ hgd_status row_gemm_group(RowGemmGroup g, hipStream_t st, const char* fn) {
 #define HGD_CASE_NT(Q, T)                                                              \
     case Q * 8 + T:                                                                    \
       if (g.p[0].mask)                                                                 \
-        hipLaunchKernelGGL((k_row_gemm<Q, T, true, (Q > 1)>), grid, dim3(256), 0, st, g); \
+        hipLaunchKernelGGL((k_row_gemm_masked<Q, T, (Q > 1)>), grid, dim3(256), 0, st, g); \
       else                                                                             \
-        hipLaunchKernelGGL((k_row_gemm<Q, T, false, (Q > 1)>), grid, dim3(256), 0, st, g); \
+        hipLaunchKernelGGL((k_row_gemm<Q, T, (Q > 1)>), grid, dim3(256), 0, st, g);     \
       break;
 #define HGD_CASE(Q) HGD_CASE_NT(Q, 1) HGD_CASE_NT(Q, 2) HGD_CASE_NT(Q, 3) HGD_CASE_NT(Q, 4)
     HGD_CASE(1) HGD_CASE(2) HGD_CASE(3) HGD_CASE(4) HGD_CASE(5) HGD_CASE(6) HGD_CASE(7)
@@ -665,6 +680,10 @@ hgd_status check_rows(const hgd_gemm_rows_desc& d, const char* fn) {
   HGD_REQUIRE(!d.drop_seed || d.rows * static_cast<int64_t>(d.N) <= 0xffffffffLL,
               "%s: dropout needs rows·N < 2^32 (32-bit element counter)", fn);
   HGD_REQUIRE((d.res == nullptr) == (d.Y2 == nullptr), "%s: res and Y2 go together", fn);
+  // the masked form is the backward-data product: its kernel carries none of the forward
+  // epilogues (their registers kept it at one wave per SIMD)
+  HGD_REQUIRE(!d.relu_mask || (!d.drop_seed && !d.Y2 && !d.row_inv && !d.binarize_a),
+              "%s: relu_mask excludes the dropout, residual, row_inv and binarize_a epilogues", fn);
   HGD_REQUIRE(!d.Y2 || (d.ldres >= d.N && d.ldy2 >= d.N), "%s: ldres / ldy2 too small", fn);
   if (d.rows == 0) return HGD_OK;
   HGD_REQUIRE(d.A && d.B && d.Y, "%s: null pointer", fn);

@@ -257,7 +257,9 @@ hgd_status hgd_linear_backward_weight(const float* dY, int64_t ldy, const float*
  * independent products of equal shape class, which is what bounds these ~10 MB products.
  *   hgd_gemm_rows: Y = relu?((A ⊙ [relu_mask > 0])·B + bias) (+ Y when accumulate), A [rows, K]
  *     (16-byte aligned rows), B[k][n] = B[k·bsk + n·bsn]; K a multiple of 16 in [16, 128], N a
- *     multiple of 16; the two products must share K, N and mask presence.
+ *     multiple of 16; the two products must share K, N and mask presence. The masked form
+ *     (relu_mask set: the backward-data product) takes none of the drop / res / row_inv /
+ *     binarize_a epilogues below (HGD_ERR_INVALID_ARG).
  *   hgd_gemm_tn: C [M, N] = (A ⊙ [relu_mask > 0])ᵀ·B over `rows` rows (split-K, partials summed
  *     in slice order: deterministic), colsum_A [M] = Σ_rows A ⊙ mask when non-NULL; the two
  *     products must share M, N and mask presence. Workspace: hgd_gemm_tn_workspace_size. */
