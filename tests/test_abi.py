@@ -54,6 +54,22 @@ def test_product_path_has_no_cpu_fallback():
         spmm_csr(csr, torch.ones(1, 4))
 
 
+def test_masked_row_gemm_rejects_forward_epilogues():
+    """Argument validation only (returns before any HIP call): the masked (backward-data) form
+    of hgd_gemm_rows takes none of the forward epilogues its kernel no longer carries."""
+    import ctypes
+    from hypergraph_diffusion_for_recommendation_amd import _native
+    lib = _native.load()
+    d = _native.GemmRowsDesc()
+    d.A, d.lda, d.relu_mask, d.ldm = 16, 64, 16, 64
+    d.B, d.bsk, d.bsn, d.Y, d.ldy = 16, 64, 1, 16, 64
+    d.rows, d.K, d.N = 1000, 64, 64
+    d.res, d.ldres, d.Y2, d.ldy2 = 16, 64, 16, 64
+    arr = (_native.GemmRowsDesc * 1)(d)
+    assert lib.hgd_gemm_rows(arr, 1, None) == 1  # HGD_ERR_INVALID_ARG
+    assert b"relu_mask excludes" in lib.hgd_get_last_error_string()
+
+
 def test_package_never_imports_oracle():
     pkg = os.path.join(ROOT, "hypergraph_diffusion_for_recommendation_amd")
     for path in glob.glob(os.path.join(pkg, "**", "*.py"), recursive=True):
