@@ -375,9 +375,10 @@ def load() -> ctypes.CDLL:
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        # optional process-wide tuning overrides (hgd_set_tuning keys 1 / 2 / 3 / 4)
+        # optional process-wide tuning overrides (hgd_set_tuning keys 1 / 2 / 3 / 4 / 5)
         for key, env in ((1, "HGD_SPMM_UNROLL"), (2, "HGD_SPMM_POLICY"),
-                         (3, "HGD_SPMM_PASS_COLS"), (4, "HGD_ROWGEMM_BLOCKS")):
+                         (3, "HGD_SPMM_PASS_COLS"), (4, "HGD_ROWGEMM_BLOCKS"),
+                         (5, "HGD_SPLITK_ROWS")):
             if os.environ.get(env):
                 st = lib.hgd_set_tuning(key, int(os.environ[env]))
                 if st != HGD_OK:

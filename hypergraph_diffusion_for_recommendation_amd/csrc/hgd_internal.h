@@ -71,5 +71,7 @@ hgd_status sum_rows_jobs(const SumRowsJob* jobs, int n, hipStream_t st);
 
 // HGD_TUNE_ROWGEMM_BLOCKS (linear.hip): 0 restores the default.
 void set_row_gemm_max_blocks(int blocks);
+// HGD_TUNE_SPLITK_ROWS (linear.hip): rows per split-K slice, 0 restores the sizing rule.
+void set_splitk_rows(int rows);
 
 }  // namespace hgd

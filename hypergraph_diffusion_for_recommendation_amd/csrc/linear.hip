@@ -36,6 +36,7 @@ __device__ __forceinline__ f32x4 relu_mask(f32x4 v, f32x4 m) {
 constexpr int kRowGemmMaxBlocks = 512;  // default of HGD_TUNE_ROWGEMM_BLOCKS
 int g_row_gemm_max_blocks = kRowGemmMaxBlocks;
 constexpr int kSplitKResident = 512;
+int g_splitk_rows = 0;  // HGD_TUNE_SPLITK_ROWS (0: sized by splits_for / tn_splits)
 
 __device__ __forceinline__ bool al16_dev(const float* p, int64_t ld) {
   return (reinterpret_cast<uintptr_t>(p) & 15) == 0 && ld % 4 == 0;
@@ -629,6 +630,13 @@ int64_t splits_for(int64_t rows, int64_t out_tiles) {
 
 // Row slices of each product of a split-K group (the pair shares the resident budget).
 void tn_splits(const hgd_gemm_tn_desc* d, int count, int64_t* S, int64_t* per) {
+  if (g_splitk_rows > 0) {  // HGD_TUNE_SPLITK_ROWS: fixed rows per slice
+    for (int i = 0; i < count; ++i) {
+      per[i] = g_splitk_rows;
+      S[i] = std::max<int64_t>(1, (std::max<int64_t>(d[i].rows, 1) + per[i] - 1) / per[i]);
+    }
+    return;
+  }
   int64_t total = 0;
   for (int i = 0; i < count; ++i) {
     S[i] = splits_for(d[i].rows, static_cast<int64_t>((d[i].M + 63) / 64) * ((d[i].N + 63) / 64));
@@ -697,6 +705,7 @@ hgd_status check_rows(const hgd_gemm_rows_desc& d, const char* fn) {
 void set_row_gemm_max_blocks(int blocks) {
   g_row_gemm_max_blocks = blocks > 0 ? blocks : kRowGemmMaxBlocks;
 }
+void set_splitk_rows(int rows) { g_splitk_rows = rows > 0 ? rows : 0; }
 }  // namespace hgd
 
 extern "C" hgd_status hgd_linear_forward(const float* X, int64_t ldx, int64_t n_rows,

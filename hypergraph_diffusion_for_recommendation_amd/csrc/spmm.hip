@@ -746,6 +746,12 @@ extern "C" hgd_status hgd_set_tuning(int32_t key, int32_t value) {
                   "hgd_set_tuning: row-GEMM blocks must be 0 (default) or in [64, 8192]");
       set_row_gemm_max_blocks(value);
       return HGD_OK;
+    case HGD_TUNE_SPLITK_ROWS:
+      HGD_REQUIRE(value == 0 || (value >= 64 && value <= 65536 && value % 64 == 0),
+                  "hgd_set_tuning: split-K rows must be 0 (default) or a multiple of 64 in "
+                  "[64, 65536]");
+      set_splitk_rows(value);
+      return HGD_OK;
     default:
       return fail(HGD_ERR_INVALID_ARG, "hgd_set_tuning: unknown key %d", key);
   }

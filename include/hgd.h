@@ -65,12 +65,16 @@ typedef enum hgd_epilogue {
  *                         0 = auto, the default: one pass up to 128 columns, else 64)
  *   HGD_TUNE_ROWGEMM_BLOCKS: most workgroups of a row-GEMM launch (hgd_gemm_rows, hgd_linear_*;
  *                         0 = default 512, else 64..8192; each wave takes 16-row tiles at a
- *                         stride of 4·blocks) */
+ *                         stride of 4·blocks)
+ *   HGD_TUNE_SPLITK_ROWS: rows per slice of the split-K products (hgd_gemm_tn,
+ *                         hgd_linear_backward_weight; 0 = default sizing, else a multiple of 64
+ *                         in [64, 65536]; the workspace size follows it) */
 typedef enum hgd_tune_key {
   HGD_TUNE_SPMM_UNROLL = 1,
   HGD_TUNE_SPMM_POLICY = 2,
   HGD_TUNE_SPMM_PASS_COLS = 3,
-  HGD_TUNE_ROWGEMM_BLOCKS = 4
+  HGD_TUNE_ROWGEMM_BLOCKS = 4,
+  HGD_TUNE_SPLITK_ROWS = 5
 } hgd_tune_key;
 hgd_status hgd_set_tuning(int32_t key, int32_t value);
 

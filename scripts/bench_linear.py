@@ -90,6 +90,7 @@ def main():
             kind = name.rsplit("_", 1)[0]
             print(json.dumps({"case": name, "rows": n, "d": d, "us": round(us, 2),
                               "rowgemm_blocks": os.environ.get("HGD_ROWGEMM_BLOCKS", "512"),
+                              "splitk_rows": os.environ.get("HGD_SPLITK_ROWS", "auto"),
                               "alg_GBps": round(algo[kind] / us / 1e3, 1)}), flush=True)
 
 
