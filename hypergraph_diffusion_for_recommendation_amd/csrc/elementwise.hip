@@ -78,6 +78,35 @@ __global__ void k_sum_slices(const float* __restrict__ P, int64_t S, int64_t str
   }
 }
 
+// out = ((a_0 + a_1) + a_2) + … over up to kMaxSumArrays separate arrays (one pass: n + 1 array
+// streams instead of the 3·(n − 1) of a chain of binary adds)
+constexpr int kMaxSumArrays = 8;
+struct SumArrays {
+  const float* a[kMaxSumArrays];
+  int32_t n;
+};
+
+__global__ void k_sum_arrays(SumArrays A, int64_t count, float* out) {  // out may alias a[0]
+  const int64_t i4 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) * 4;
+  if (i4 + 3 < count) {
+    float4 acc = *reinterpret_cast<const float4*>(A.a[0] + i4);
+    for (int s = 1; s < A.n; ++s) {
+      const float4 v = *reinterpret_cast<const float4*>(A.a[s] + i4);
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
+    }
+    *reinterpret_cast<float4*>(out + i4) = acc;
+  } else {
+    for (int64_t i = i4; i < count; ++i) {
+      float acc = A.a[0][i];
+      for (int s = 1; s < A.n; ++s) acc += A.a[s][i];
+      out[i] = acc;
+    }
+  }
+}
+
 // nn.Dropout on the device RNG of dropout_keep (device_util.h): y[i] = keep(i) ? x[i]·scale : 0.
 // The same call on the upstream gradient with the same seed is the backward (no stored mask).
 __global__ void k_dropout(const float* __restrict__ x, int64_t n, const uint64_t* __restrict__ seed_p,
@@ -138,6 +167,24 @@ extern "C" hgd_status hgd_sum_slices(const float* P, int64_t n_slices, int64_t s
   hipLaunchKernelGGL(k_sum_slices, dim3(grid_for((n + 3) / 4)), dim3(kBlock), 0,
                      as_stream(stream), P, n_slices, slice_stride, n, out);
   return check_launch("hgd_sum_slices");
+}
+
+extern "C" hgd_status hgd_sum_arrays(const float* const* arrays, int32_t n_arrays,
+                                     int64_t count, float* out, void* stream) {
+  clear_error();
+  HGD_REQUIRE(arrays && n_arrays >= 1 && n_arrays <= kMaxSumArrays && count >= 0,
+              "hgd_sum_arrays: 1..%d arrays, count >= 0", kMaxSumArrays);
+  if (count == 0) return HGD_OK;
+  SumArrays A{};
+  A.n = n_arrays;
+  for (int s = 0; s < n_arrays; ++s) {
+    HGD_REQUIRE(arrays[s] && aligned16(arrays[s]), "hgd_sum_arrays: array %d null/unaligned", s);
+    A.a[s] = arrays[s];
+  }
+  HGD_REQUIRE(out && aligned16(out), "hgd_sum_arrays: out null/unaligned");
+  hipLaunchKernelGGL(k_sum_arrays, dim3(grid_for((count + 3) / 4)), dim3(kBlock), 0,
+                     as_stream(stream), A, count, out);
+  return check_launch("hgd_sum_arrays");
 }
 
 extern "C" hgd_status hgd_dropout_apply(const float* x, int64_t n, const uint64_t* seed,

@@ -24,7 +24,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from .functional import (dense_two_hop_pair, hccf_layers, hccf_layers_supported, linear,
+from .functional import (dense_two_hop_pair, fan, hccf_layers, hccf_layers_supported, linear,
                          two_hop_fused)
 from .incidence import Incidence, incidence_of
 from .layers import EquivSetGNN, GCNLayer, HGCNConv, HGNNLayer, LayerNorm, SpAdjDropEdge
@@ -168,17 +168,21 @@ class LocalAwareEncoder(nn.Module):
         self.to(self.device)  # the reference moves it with HGNNModel.to(device)
 
     def forward(self, ego_embeddings, sparse_norm_adj):
-        res = ego_embeddings
+        # res is read by every layer (and is layer 0's input): its gradients meet in one n-ary
+        # sum (functional.fan) instead of a chain of full-table accumulations
+        uses = fan(ego_embeddings, self.layers + 1)
+        res = uses[1:]
+        ego_embeddings = uses[0]
         all_embeddings = []
         for k in range(self.layers):
             if k != self.layers - 1:
                 # the "+ res" rides in the block's last Linear store when its fused path runs
                 ego_embeddings = self.edhnn_layers[k](ego_embeddings, self.hypergraph,
-                                                      self.edhnn_ui_n, residual=res)
+                                                      self.edhnn_ui_n, residual=res[k])
             else:
                 # LN0(HGCNConv(Â, x, act=False)) + res in one fused hop store
                 ego_embeddings = two_hop_fused(incidence_of(sparse_norm_adj), ego_embeddings,
-                                               norm=self.lns[0], res1=res, res1_scale=1.0)
+                                               norm=self.lns[0], res1=res[k], res1_scale=1.0)
             all_embeddings += [ego_embeddings]
         nu = self.data.n_users
         return all_embeddings[-1][:nu], all_embeddings[-1][nu:]

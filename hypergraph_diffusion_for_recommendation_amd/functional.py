@@ -382,6 +382,38 @@ def dropout(x: torch.Tensor, p: float, seed: Optional[torch.Tensor] = None) -> t
     return _Dropout.apply(x, float(p), seed)
 
 
+class _Fan(torch.autograd.Function):
+    """``n`` aliases of one table whose gradients meet in ONE n-ary sum (hgd_sum_arrays) instead
+    of autograd's chain of n − 1 binary accumulations (each a full read-read-write of the table)."""
+
+    @staticmethod
+    def forward(ctx, x, n: int):
+        return tuple(x.view_as(x) for _ in range(n))
+
+    @staticmethod
+    def backward(ctx, *grads):
+        gs = [g.contiguous() for g in grads if g is not None]
+        if not gs:
+            return None, None
+        if len(gs) == 1:
+            return gs[0], None
+        out = torch.empty_like(gs[0])
+        ptrs = (ctypes.c_void_p * len(gs))(*[g.data_ptr() for g in gs])
+        nat.check(nat.load().hgd_sum_arrays(ptrs, len(gs), out.numel(), out.data_ptr(),
+                                            nat.stream_handle(out.device)), "hgd_sum_arrays")
+        return out, None
+
+
+def fan(x: torch.Tensor, n: int):
+    """``n`` uses of ``x`` (e.g. HGNN_HD4's layer-0 residual ``res``, read by every layer,
+    HGNN_HD4.py:390-405) whose gradients are summed in one pass. Off the device path (or for
+    more than 8 uses) the plain tensor is returned n times."""
+    if (n < 2 or n > 8 or not x.is_cuda or x.dtype != torch.float32 or not x.requires_grad
+            or not torch.is_grad_enabled()):
+        return (x,) * n
+    return _Fan.apply(x, int(n))
+
+
 class _LinearReluDrop(torch.autograd.Function):
     """``dropout(relu(X·Wᵀ + b), p) (+ res)`` in the row GEMM's store (hgd_gemm_rows: the
     ReLU, the dropout mask of the library RNG and its 1/(1-p), the residual as a second

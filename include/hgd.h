@@ -676,6 +676,13 @@ hgd_status hgd_dropout_apply(const float* x, int64_t n, const uint64_t* seed, fl
  * tables kept as slices of one buffer. P, out 16-byte aligned, slice_stride % 4 == 0. */
 hgd_status hgd_sum_slices(const float* P, int64_t n_slices, int64_t slice_stride, int64_t n,
                           float* out, void* stream);
+/* out[i] = ((a_0[i] + a_1[i]) + a_2[i]) + … over n_arrays (1..8) separate device arrays of
+ * `count` floats, in array order, one pass: the gradient of a table used by several layers
+ * (HGNN_HD4.py:390-405's residual `res`, read by every layer) as one sum instead of a chain of
+ * binary accumulations. `arrays` is a HOST array of device pointers; all 16-byte aligned; out
+ * may alias a_0. */
+hgd_status hgd_sum_arrays(const float* const* arrays, int32_t n_arrays, int64_t count,
+                          float* out, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Incidence objects (SURVEY.md §8b "C ABI libhgd"): the library-owned form of the structure the

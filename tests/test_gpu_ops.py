@@ -119,3 +119,41 @@ def test_hgconv2_large_adjoint_property(dev):
     a = (hgconv2(inc, X1).double() * X2.double()).sum()
     b = (X1.double() * hgconv2(inc, X2).double()).sum()
     assert abs(float(a - b)) <= 1e-5 * float(a.abs() + b.abs()) + 1e-3
+
+
+@pytest.mark.parametrize("n,count", [(2, 1000), (4, 144_242 * 128 + 3), (8, 7)])
+def test_sum_arrays_is_the_binary_chain(dev, n, count):
+    """hgd_sum_arrays: bitwise ((a_0 + a_1) + a_2) + … (torch's fp32 adds in the same order),
+    including a ragged tail past the float4 body and out aliasing a_0."""
+    import ctypes
+    from hypergraph_diffusion_for_recommendation_amd import _native as nat
+    g = torch.Generator(device=dev).manual_seed(count + n)
+    arrs = [torch.randn(count, device=dev, generator=g) for _ in range(n)]
+    want = arrs[0].clone()
+    for a in arrs[1:]:
+        want = want + a
+    ptrs = (ctypes.c_void_p * n)(*[a.data_ptr() for a in arrs])
+    out = arrs[0]  # in place over a_0
+    nat.check(nat.load().hgd_sum_arrays(ptrs, n, count, out.data_ptr(), nat.stream_handle(dev)),
+              "hgd_sum_arrays")
+    assert torch.equal(out, want)
+
+
+def test_fan_gradient_is_the_sum_of_its_uses(dev):
+    """functional.fan: n aliases of x; x.grad = Σ of the uses' gradients (one n-ary pass), equal
+    to autograd's own accumulation within fp32 reassociation (1e-6 of Σ|terms|)."""
+    from hypergraph_diffusion_for_recommendation_amd.functional import fan
+    g = torch.Generator(device=dev).manual_seed(5)
+    x0 = torch.randn(3000, 64, device=dev, generator=g)
+    ws = [torch.randn(3000, 64, device=dev, generator=g) for _ in range(4)]
+
+    def loss(uses):
+        return sum((u * w).sum() * (k + 1) for k, (u, w) in enumerate(zip(uses, ws)))
+
+    x = x0.clone().requires_grad_(True)
+    uses = fan(x, 4)
+    assert all(u.data_ptr() == x.data_ptr() for u in uses)
+    loss(uses).backward()
+    ref = sum(w.double() * (k + 1) for k, w in enumerate(ws))
+    mag = sum(w.double().abs() * (k + 1) for k, w in enumerate(ws))
+    assert ((x.grad.double() - ref).abs() <= 1e-6 * mag).all()
