@@ -264,14 +264,15 @@ class LocalAwareEncoderHD3(nn.Module):
         self.to(self.device)
 
     def forward(self, ego_embeddings, sparse_norm_adj):
-        res = ego_embeddings
+        uses = fan(ego_embeddings, self.layers + 1)  # one n-ary gradient sum of the residual
+        ego_embeddings, res = uses[0], uses[1:]
         for k in range(self.layers):
             if k != self.layers - 1:
                 ego_embeddings = self.edhnn_layers[k](ego_embeddings, sparse_norm_adj,
-                                                      self.edhnn_ui_n) + res
+                                                      self.edhnn_ui_n) + res[k]
             else:
                 ego_embeddings = two_hop_fused(incidence_of(self.sparse_norm_adj), ego_embeddings,
-                                               norm=self.lns[k], res1=res, res1_scale=1.0)
+                                               norm=self.lns[k], res1=res[k], res1_scale=1.0)
         nu = self.data.n_users
         return ego_embeddings[:nu], ego_embeddings[nu:]
 

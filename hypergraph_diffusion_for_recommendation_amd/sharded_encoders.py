@@ -29,7 +29,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .encoders import edhnn_config
-from .functional import dense_two_hop, linear
+from .functional import dense_two_hop, fan, linear
 from .layers import EquivSetGNN, LayerNorm, input_norm_linear
 from .sharded import (ShardedBipartite, bipartite_hop, bipartite_hop_fused,  # noqa: F401
                       shard_bounds, sharded_dense_two_hop, sharded_mean_two_hop)
@@ -253,15 +253,17 @@ class ShardedLocalAwareEncoder(nn.Module):
         """``sparse_norm_adj``: None (the full ``norm_adj``) or a :meth:`dropped` shard, which the
         last layer's HGCNConv uses as the reference's does (HGNN_HD4.py:399)."""
         norm = sparse_norm_adj if isinstance(sparse_norm_adj, ShardedBipartite) else self.norm
-        res = ego_embeddings
+        # layer 0's input and every layer's residual: one n-ary gradient sum (functional.fan)
+        uses = fan(ego_embeddings, self.layers + 1)
+        ego_embeddings, res = uses[0], uses[1:]
         for k in range(self.layers):
             if k != self.layers - 1:
-                ego_embeddings = self._edhnn(self.edhnn_layers[k], ego_embeddings) + res
+                ego_embeddings = self._edhnn(self.edhnn_layers[k], ego_embeddings) + res[k]
             else:
                 # LN0(A·(Aᵀ·x)) + res, the LayerNorm and residual in the second hop's store
                 ego_embeddings = bipartite_hop_fused(
                     norm, bipartite_hop(norm.transpose(), ego_embeddings), norm=self.lns[0],
-                    res1=res)
+                    res1=res[k])
         nl = self.n_local
         return ego_embeddings[:nl], ego_embeddings[nl:]
 
@@ -332,14 +334,15 @@ class ShardedLocalAwareEncoderHD3(ShardedLocalAwareEncoder):
         """``sparse_norm_adj``: None (the full ``norm_adj``) or a :meth:`dropped` shard, which
         the ED-HNN blocks use (HGNN_HD3.py:416-418); the last layer uses the full one (:420)."""
         dropped = sparse_norm_adj if isinstance(sparse_norm_adj, ShardedBipartite) else self.norm
-        res = ego_embeddings
+        uses = fan(ego_embeddings, self.layers + 1)  # one n-ary gradient sum of the residual
+        ego_embeddings, res = uses[0], uses[1:]
         for k in range(self.layers):
             if k != self.layers - 1:
                 ego_embeddings = self._edhnn_spmm(self.edhnn_layers[k], ego_embeddings,
-                                                  dropped) + res
+                                                  dropped) + res[k]
             else:
                 ego_embeddings = bipartite_hop_fused(
                     self.norm, bipartite_hop(self.norm.transpose(), ego_embeddings),
-                    norm=self.lns[k], res1=res)
+                    norm=self.lns[k], res1=res[k])
         nl = self.n_local
         return ego_embeddings[:nl], ego_embeddings[nl:]
