@@ -25,7 +25,7 @@ import torch
 import torch.nn as nn
 
 from .functional import (dense_two_hop_pair, fan, hccf_layers, hccf_layers_supported, linear,
-                         two_hop_fused)
+                         sum_n, two_hop_fused)
 from .incidence import Incidence, incidence_of
 from .layers import EquivSetGNN, GCNLayer, HGCNConv, HGNNLayer, LayerNorm, SpAdjDropEdge
 
@@ -213,21 +213,26 @@ class HCCFDiffusionEncoder(HCCFEncoder):
         hyper_uu = linear(e['user_emb'], e['user_w'].t())
         hyper_ii = linear(e['item_emb'], e['item_w'].t())
         blk = self.edhnnlayer
+        terms = []  # the sum(hidden) operands
         for _ in range(self.n_layers):
-            gcn_emb = self.gcnlayer(self.edgeDropper(self.sparse_norm_adj, keep_rate), hidden[-1])
+            # hidden[-1] feeds the GCN hop, the block and the layer sum: its three gradients
+            # meet in one n-ary pass (functional.fan)
+            h_gcn, h_blk, h_sum = fan(hidden[-1], 3)
+            terms.append(h_sum)
+            gcn_emb = self.gcnlayer(self.edgeDropper(self.sparse_norm_adj, keep_rate), h_gcn)
             hu = self.drop_out(hyper_uu)
-            if blk.dense_pair_ok(hidden[-1], hu, hyper_ii):
+            if blk.dense_pair_ok(h_blk, hu, hyper_ii):
                 # the user and the item call of the block as one pass over all rows
                 # (EquivSetGNN.forward_dense_pair: grouped mean two-hops, no cat)
-                hyp = blk.forward_dense_pair(hidden[-1], hu, self.drop_out(hyper_ii))
+                hyp = blk.forward_dense_pair(h_blk, hu, self.drop_out(hyper_ii))
             else:
-                hyper_uemb = blk(hidden[-1][:nu], hu, self.edhnn_user_n)
-                hyper_iemb = blk(hidden[-1][nu:], self.drop_out(hyper_ii), self.edhnn_item_n)
+                hyper_uemb = blk(h_blk[:nu], hu, self.edhnn_user_n)
+                hyper_iemb = blk(h_blk[nu:], self.drop_out(hyper_ii), self.edhnn_item_n)
                 hyp = torch.cat([hyper_uemb, hyper_iemb], 0)
             gcn_hidden += [gcn_emb]
             hgnn_hidden += [hyp]
             hidden += [gcn_emb + hyp]
-        emb = sum(hidden)
+        emb = sum_n(terms + [hidden[-1]])  # sum(hidden), same order, one pass
         return emb[:nu], emb[nu:], gcn_hidden, hgnn_hidden
 
 

@@ -414,6 +414,35 @@ def fan(x: torch.Tensor, n: int):
     return _Fan.apply(x, int(n))
 
 
+class _SumN(torch.autograd.Function):
+    """``((t_0 + t_1) + t_2) + …`` of equal-shape tables in one pass (hgd_sum_arrays); the
+    backward hands the output gradient to every input (no kernels)."""
+
+    @staticmethod
+    def forward(ctx, *ts):
+        ts = [t.contiguous() for t in ts]
+        out = torch.empty_like(ts[0])
+        ptrs = (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
+        nat.check(nat.load().hgd_sum_arrays(ptrs, len(ts), out.numel(), out.data_ptr(),
+                                            nat.stream_handle(out.device)), "hgd_sum_arrays")
+        ctx.n = len(ts)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        return (g,) * ctx.n
+
+
+def sum_n(ts):
+    """``sum(ts)`` (e.g. HCCF's ``sum(hidden)``, HCCF.py:188 / HCCF_diffusion.py:221) as one
+    n-ary pass on the device, in list order; Python's ``sum`` elsewhere."""
+    ts = list(ts)
+    if (2 <= len(ts) <= 8 and all(t.is_cuda and t.dtype == torch.float32 for t in ts)
+            and all(t.shape == ts[0].shape for t in ts)):
+        return _SumN.apply(*ts)
+    return sum(ts)
+
+
 class _LinearReluDrop(torch.autograd.Function):
     """``dropout(relu(X·Wᵀ + b), p) (+ res)`` in the row GEMM's store (hgd_gemm_rows: the
     ReLU, the dropout mask of the library RNG and its 1/(1-p), the residual as a second
