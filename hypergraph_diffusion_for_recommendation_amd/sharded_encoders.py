@@ -29,7 +29,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .encoders import edhnn_config
-from .functional import dense_two_hop, fan, linear
+from .functional import dense_two_hop, fan, linear, sum_n
 from .layers import EquivSetGNN, LayerNorm, input_norm_linear
 from .sharded import (ShardedBipartite, bipartite_hop, bipartite_hop_fused,  # noqa: F401
                       shard_bounds, sharded_dense_two_hop, sharded_mean_two_hop)
@@ -156,15 +156,19 @@ class ShardedHCCFEncoder(nn.Module):
         gcn_hidden, hgnn_hidden = [], []
         hyper_uu = linear(e['user_emb'], e['user_w'].t())
         hyper_ii = linear(e['item_emb'], e['item_w'].t())
+        terms = []  # the sum(hidden) operands
         for _ in range(self.n_layers):
-            gcn_emb = bipartite_hop(self._dropped(keep_rate), hidden[-1])
-            hyper_u = sharded_dense_two_hop(self.rep_drop(hyper_uu, nl), hidden[-1][:nl],
-                                            self.group)
-            hyper_i = dense_two_hop(self.rep_drop(hyper_ii, 0), hidden[-1][nl:])
+            # hidden[-1] feeds the hop, the learned-hypergraph pair and the layer sum: one n-ary
+            # gradient pass (functional.fan)
+            h_hop, h_hyp, h_sum = fan(hidden[-1], 3)
+            terms.append(h_sum)
+            gcn_emb = bipartite_hop(self._dropped(keep_rate), h_hop)
+            hyper_u = sharded_dense_two_hop(self.rep_drop(hyper_uu, nl), h_hyp[:nl], self.group)
+            hyper_i = dense_two_hop(self.rep_drop(hyper_ii, 0), h_hyp[nl:])
             gcn_hidden += [gcn_emb]
             hgnn_hidden += [torch.cat([hyper_u, hyper_i], 0)]
             hidden += [gcn_emb + hgnn_hidden[-1]]
-        embeddings = sum(hidden)
+        embeddings = sum_n(terms + [hidden[-1]])  # sum(hidden), same order, one pass
         return embeddings[:nl], embeddings[nl:], gcn_hidden, hgnn_hidden
 
 
