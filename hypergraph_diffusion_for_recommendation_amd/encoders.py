@@ -304,11 +304,18 @@ def _hgcn_ln_res_stack(inc, x, lns, slope, res, attend=None):
     :428-433): one fused two-hop per layer whose store applies the LeakyReLU, the LayerNorm
     and the residual; ``attend[k]`` (the UGformer blocks) first when given."""
     L = len(lns)
+    # every layer reads res (and layer 0 reads x, the same table at the call sites): one n-ary
+    # gradient pass instead of a chain of full-table accumulations (functional.fan)
+    if res is x:
+        uses = fan(x, L + 1)
+        x, ress = uses[0], uses[1:]
+    else:
+        ress = fan(res, L)
     for k in range(L):
         if attend is not None:
             x = _self_attend(attend[k], x)
         x = two_hop_fused(inc, x, epilogue=None if k == L - 1 else "leaky_relu", slope=slope,
-                          norm=lns[k], res1=res, res1_scale=1.0)
+                          norm=lns[k], res1=ress[k], res1_scale=1.0)
     return x
 
 
@@ -415,11 +422,12 @@ class SelfAwareEncoderHD(nn.Module):
         self.to(self.device)
 
     def forward(self, ego_embeddings, sparse_norm_adj=None):
-        res = ego_embeddings
+        uses = fan(ego_embeddings, self.layers + 1)  # one n-ary gradient sum of the residual
+        ego_embeddings, res = uses[0], uses[1:]
         for k in range(self.layers):
             if self.use_self_att:
                 ego_embeddings = _self_attend(self.ugformer_layers[k], ego_embeddings)
             blk = self.edhnn_layers[0 if k != self.layers - 1 else 1]
-            ego_embeddings = blk(ego_embeddings, self.sparse_norm_adj, self.edhnn_ui_n) + res
+            ego_embeddings = blk(ego_embeddings, self.sparse_norm_adj, self.edhnn_ui_n) + res[k]
         nu = self.data.n_users
         return ego_embeddings[:nu], ego_embeddings[nu:]
