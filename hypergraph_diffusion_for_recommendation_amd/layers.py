@@ -514,7 +514,7 @@ class EquivSetGNN(nn.Module):
     def forward(self, x, hypergraph, n_nodes, residual=None):
         """``residual``: added to the block's output (LocalAwareEncoder's ``+ res``,
         HGNN_HD4.py:399) — in the last Linear's store when the fused path runs."""
-        if (self._fused_dropout_ok() and torch.is_tensor(hypergraph)
+        if (self._fused_dropout_ok() and self.conv.aggr == 'mean' and torch.is_tensor(hypergraph)
                 and hypergraph.layout == torch.strided and dense_mean_two_hop_ok(hypergraph, x)
                 and hypergraph.shape[0] == x.shape[0]):
             # a dense learned hypergraph (HCCF_diffusion.py:205-206): the mean pair straight
@@ -549,8 +549,10 @@ class EquivSetGNN(nn.Module):
 
     def dense_pair_ok(self, x, H_u, H_i) -> bool:
         """:meth:`forward_dense_pair` applies: the fused block, dense device hypergraphs over the
-        two row blocks of ``x``."""
-        return (self._fused_dropout_ok() and torch.is_tensor(H_u) and torch.is_tensor(H_i)
+        two row blocks of ``x``; the dense pair computes the MEAN two-hop, so only a 'mean'
+        aggregation takes it (an 'add' / 'sum' block runs the V/E path)."""
+        return (self._fused_dropout_ok() and self.conv.aggr == 'mean'
+                and torch.is_tensor(H_u) and torch.is_tensor(H_i)
                 and H_u.layout == torch.strided and H_i.layout == torch.strided
                 and H_u.shape[0] + H_i.shape[0] == x.shape[0] and H_u.shape[1] == H_i.shape[1]
                 and x.is_contiguous() and x.shape[0] * x.shape[1] < 2 ** 32

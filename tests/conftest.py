@@ -31,6 +31,18 @@ def pytest_configure(config):
     config._hgd_build = _ensure_built()
 
 
+# BASELINE configs' shape-level parity first: under ``pytest -x`` a failure anywhere else must
+# not leave these unreached. Files not listed keep their collection order after them.
+_FIRST = ("test_gpu_config_parity.py", "test_gpu_configs.py")
+
+
+def pytest_collection_modifyitems(session, config, items):
+    def rank(item):
+        name = os.path.basename(str(item.fspath))
+        return _FIRST.index(name) if name in _FIRST else len(_FIRST)
+    items[:] = sorted(items, key=rank)  # stable: order inside each group is unchanged
+
+
 def pytest_report_header(config):
     sha = "missing"
     if os.path.exists(LIB):

@@ -4,6 +4,8 @@ and backward, against the reference restated in float64 with its own torch calls
 
 * configs[0] LastFM HCCF, 1 layer, d = 32: 1,891 users × 14,777 items (HCCF_diffusion.py:140-141
   sizes), BPR + per-layer InfoNCE (HCCF.py:61-97, 173-191);
+* configs[1] MovieLens-1M HGNN, 2 layers, d = 64: the HGNN carrier's SelfAwareEncoder
+  (HGNN_cp.py:368-411) at 6,040 × 3,706 on the edge-dropped norm_adj, UGformer off and on;
 * configs[2] Yelp2018 HCCF, 3 layers, d = 64, with drop-edge and InfoNCE: 31,668 × 38,048;
 * configs[3] Amazon-Book "hypergraph diffusion" (HGNN_HD4 local encoder, HGNN_HD4.py:390-405),
   3 layers, d = 128: 52,643 × 91,599, single GPU and user-row sharded over 2 ranks;
@@ -22,6 +24,7 @@ fp32 derivative (the reference's own fp32 run could take either branch; at 10^7 
 few such elements occur): there the reference replays the device's decision, after checking
 that every disagreement is such an element (tests/_ref64.py ReluMasks).
 """
+import copy
 import os
 import socket
 from types import SimpleNamespace
@@ -126,6 +129,116 @@ def test_hccf_lastfm_1layer_d32_train_step(dev):
 def test_hccf_yelp_3layer_d64_infonce_train_step(dev):
     """configs[2]: Yelp2018 HCCF, 3 layers, d = 64, drop-edge + InfoNCE."""
     _hccf_case(dev, YELP, 64, 3, seed=20)
+
+
+# ---------------------------------------------------------------------------------------------
+# the HGNN carrier's encoder (configs[1])
+# ---------------------------------------------------------------------------------------------
+class _Replay(torch.nn.Module):
+    """The reference side of an R.FixedDropout: its recorded masks, in call order."""
+
+    def __init__(self, masks, p):
+        super().__init__()
+        self.masks, self.p, self.pos = masks, p, 0
+
+    def forward(self, x):
+        m = self.masks[self.pos]
+        self.pos += 1
+        return x * m.to(x.dtype) / (1.0 - self.p)
+
+
+def _ugformer_fixed_dropouts(blocks, p, seed):
+    """Every dropout of the UGformer blocks (TransformerEncoderLayer's dropout / dropout1 /
+    dropout2; the attention-weight dropout is a float inside MultiheadAttention, set to 0 on
+    both sides) as recorded draws, so both sides see the same masks."""
+    fixed = []
+    for b, blk in enumerate(blocks):
+        for layer in blk.layers:
+            for j, name in enumerate(("dropout", "dropout1", "dropout2")):
+                fd = R.FixedDropout(p, seed + 10 * b + j)
+                setattr(layer, name, fd)
+                fixed.append((b, name, fd))
+            layer.self_attn.dropout = 0.0
+    return fixed
+
+
+@pytest.mark.parametrize("self_att", [False, True], ids=["ugformer_off", "ugformer_on"])
+def test_hgnn_self_aware_ml1m_2layer_d64_train(dev, self_att):
+    """configs[1]: the HGNN carrier's CF encoder, SelfAwareEncoder (HGNN_cp.py:368-411), at the
+    MovieLens-1M shape (6,040 users × 3,706 items, 750 k interactions), d = 64, 2 layers,
+    LeakyReLU --p 0.3, train mode, on the edge-dropped norm_adj the carrier passes in
+    (calculate_cf_embeddings, HGNN_cp.py:278-283: keep = 1 − --drop_rate 0.2, the reference's
+    CPU mask). Output rows, d ego and the LayerNorm γ/β gradients against float64.
+    ``ugformer_on`` (HGNN_cp's default use_self_att=True): the UGformer block before each hop is
+    the library's full-sequence attention over all 9,746 nodes (fp32 on the device, float64 on
+    the reference side, same recorded dropout masks); its outputs and d ego are held to 1e-4 of
+    the row scale, since the attention is not an op of this path and its fp32 softmax over
+    9,746 keys is not a 1e-5 computation; the path's own layers (the hops + LeakyReLU + LN +
+    residual) are the same fused kernels as ``ugformer_off``, held there to 1e-5."""
+    from hypergraph_diffusion_for_recommendation_amd.encoders import (SelfAwareEncoder,
+                                                                      sparse_tensor_of)
+    from hypergraph_diffusion_for_recommendation_amd.layers import SpAdjDropEdge
+    U, I, nnz = 6_040, 3_706, 750_000
+    N, d, L, slope, p_drop = U + I, 64, 2, 0.3, 0.2
+    ui, A = _graph(U, I, nnz, seed=60)
+    data = SimpleNamespace(n_users=U, n_items=I, norm_adj=A, ui_adj=ui)
+    torch.manual_seed(61)
+    enc = SelfAwareEncoder(data, d, d, L, slope, p_drop, device=dev,
+                           use_self_att=self_att).train()
+    with torch.no_grad():  # non-trivial affine so the γ/β gradients carry information
+        for ln in enc.lns:
+            ln.weight.uniform_(0.5, 1.5)
+            ln.bias.uniform_(-0.2, 0.2)
+    ref_blocks = copy.deepcopy(enc.ugformer_layers).cpu().double()
+    fixed = _ugformer_fixed_dropouts(enc.ugformer_layers, p_drop, 62) if self_att else []
+    g = torch.Generator().manual_seed(63)
+    bound = (6.0 / (N + d)) ** 0.5
+    ego = (torch.rand(N, d, generator=g) * 2 - 1) * bound
+    G = torch.randn(N, d, generator=g)
+    sparse_norm_adj = sparse_tensor_of(A, dev)  # HGNN_cp.py:234
+    torch.manual_seed(64)
+    dropped = SpAdjDropEdge()(sparse_norm_adj, 1.0 - p_drop)
+    x = ego.to(dev).requires_grad_(True)
+    ue, ie = enc(x, dropped)
+    out = torch.cat([ue, ie])
+    out.backward(G.to(dev))
+
+    idx, vals = _coo_host(sparse_norm_adj)
+    torch.manual_seed(64)
+    di, dv = R.drop_edge_reference(idx, vals, 1.0 - p_drop)
+    gi, gv = _coo_host(dropped)
+    assert torch.equal(di, gi) and torch.equal(dv, gv), "drop-edge structure"
+    adj = R.sparse(di, dv, (N, N))
+    adj_t = adj.t().coalesce()
+    if self_att:
+        for b, name, fd in fixed:
+            for layer in ref_blocks[b].layers:
+                setattr(layer, name, _Replay(fd.masks, p_drop))
+                layer.self_attn.dropout = 0.0
+        ref_blocks.train()
+    P = {k: v for k, v in R.leaves(enc).items() if k.startswith("lns.")}
+    xr = ego.double().requires_grad_(True)
+    probe = R.Probe()
+    h = xr
+    for k in range(L):  # HGNN_cp.py:394-411
+        if self_att:
+            h = ref_blocks[k](h.unsqueeze(1)).squeeze(1)
+        z = torch.sparse.mm(adj, torch.sparse.mm(adj_t, h))
+        if k != L - 1:
+            z = torch.nn.functional.leaky_relu(z, slope)
+        h = R._ln(z, P, f"lns.{k}", 1e-5, probe) + xr
+    h.backward(G.double())
+    tol = 1e-4 if self_att else R.TOL
+    worst = R.check_rows(out, h, "output", tol)
+    worst = max(worst, R.check_rows(x.grad, xr.grad, "d ego", tol))
+    got = {k: p.grad for k, p in enc.named_parameters() if k.startswith("lns.")}
+    gradsR = {k: v.grad for k, v in P.items()}
+    if self_att:
+        for k, gv_ in got.items():
+            worst = max(worst, R.check_rows(gv_, gradsR[k], f"d {k}", tol))
+    else:
+        worst = max(worst, _check_params(got, gradsR, probe))
+    print(f"SelfAware ML-1M d=64 L=2 ugformer={self_att}: worst row ratio {worst:.2e}")
 
 
 # ---------------------------------------------------------------------------------------------

@@ -140,6 +140,31 @@ def test_module_path_unchanged_under_recorded_dropout(dev):
     assert err <= 1e-6 * float(b.abs().max()), err
 
 
+@pytest.mark.parametrize("aggr", ["add", "mean"])
+def test_dense_hypergraph_block_respects_aggr(dev, aggr):
+    """A block on a DENSE hypergraph (HCCF_diffusion.py:205-206) takes the dense mean fast path
+    only for aggr='mean'; with 'add' (EquivSetConv's default) it must sum, as the module path
+    over V/E = nonzero(H > 0) does. Eval mode: both paths deterministic."""
+    from hypergraph_diffusion_for_recommendation_amd.layers import EquivSetGNN
+    from hypergraph_diffusion_for_recommendation_amd.encoders import edhnn_config
+    n, K, d = 700, 32, 32
+    args = dict(edhnn_config(d), aggregate=aggr)
+    torch.manual_seed(52)
+    blk = EquivSetGNN(d, args).to(dev).eval()
+    g = torch.Generator().manual_seed(53)
+    H = torch.randn(n, K, generator=g).to(dev)
+    x = torch.randn(n, d, generator=g).to(dev)
+    Hu, Hi = H[:300].contiguous(), H[300:].contiguous()
+    with torch.no_grad():
+        fast = blk(x, H, n)
+        pair_ok = blk.dense_pair_ok(x, Hu, Hi)
+        blk.fused_dropout = False
+        ref = blk(x, H, n)
+    assert pair_ok == (aggr == "mean")
+    err = float((fast - ref).abs().max())
+    assert err <= 1e-5 * float(ref.abs().max()), (aggr, err)
+
+
 def _mean_pair64(H, X, G):
     """Float64 restatement of the scatter-mean pair over nonzero(H > 0) and its backward."""
     B = (H > 0).double().cpu()
