@@ -72,6 +72,10 @@ def parse():
     ap.add_argument("--slice-width", type=int, default=None,
                     help="embedding columns per pipelined all-reduce block (N > 1; default 32 "
                          "for d <= 128, else 64)")
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "p2p"],
+                    help="N > 1: the item-message all-reduce over RCCL (torch.distributed "
+                         "'nccl') or the direct xGMI peer exchange (hgd_p2p: two-shot mesh "
+                         "reduce over IPC-mapped buffers, sharded.P2PExchange)")
     ap.add_argument("--check", action="store_true",
                     help="after timing, compare the sharded Y / dX with the single-GPU conv of "
                          "the global graph (strong scaling) at the 1e-5 relative bound")
@@ -255,6 +259,32 @@ def launch_ranks(args) -> int:
     return subprocess.call(cmd)
 
 
+ROW_BLOCK = 1 << 20
+
+
+def table_rows(u0, u1, d, seed, device, bound=None):
+    """Rows [u0, u1) of a synthetic [U, d] table: uniform(-bound, bound) (xavier_uniform_ on the
+    global table, HCCF.py:164-169) or N(0, 1) when ``bound`` is None, generated in blocks of
+    2^20 rows with one generator per block (seed, block), so a rank draws only its own rows and
+    every rank sees the same global table."""
+    import torch
+    out = torch.empty(max(0, u1 - u0), d, device=device)
+    b = u0 // ROW_BLOCK
+    while b * ROW_BLOCK < u1:
+        r0, r1 = b * ROW_BLOCK, (b + 1) * ROW_BLOCK
+        g = torch.Generator(device=device).manual_seed(seed * 1_000_003 + b)
+        blk = torch.empty(ROW_BLOCK, d, device=device)
+        if bound is None:
+            blk.normal_(generator=g)
+        else:
+            blk.uniform_(-bound, bound, generator=g)
+        a, z = max(r0, u0), min(r1, u1)
+        out[a - u0:z - u0] = blk[a - r0:z - r0]
+        del blk
+        b += 1
+    return out
+
+
 def check_against_single_gpu(idx, U, I, X_global, dY_global, Y, dX, u0, u1):
     """Strong scaling: this rank's sharded Y / dX rows against the single-GPU hgconv2 of the
     global graph (functional.hgconv2, no exchange) at |err| <= 1e-5 · (the same conv of |X|)."""
@@ -309,7 +339,8 @@ def main():
     import torch.distributed as dist
 
     from hypergraph_diffusion_for_recommendation_amd import Incidence, profiling
-    from hypergraph_diffusion_for_recommendation_amd.sharded import (ShardedIncidence,
+    from hypergraph_diffusion_for_recommendation_amd.sharded import (ExchangeTimer,
+                                                                       ShardedIncidence,
                                                                        init_process_group,
                                                                        sharded_two_hop)
 
@@ -323,7 +354,7 @@ def main():
         init_process_group(device, dist_backend)
 
     shard_kw = dict(n_chunks=args.chunks, P="sym", Q="mean", R="sym",
-                    slice_width=args.slice_width)
+                    slice_width=args.slice_width, transport=args.transport)
     bound = (6.0 / (U + d)) ** 0.5  # xavier_uniform_ on the global [U, d] (HCCF.py:164-169)
     keep_global = args.check and strong and world > 1
     idx = make_graph(U, I, E, seed=0 if strong else rank, zipf=zipf, device=device)
@@ -339,15 +370,9 @@ def main():
     if not keep_global:
         del idx
     nnz = inc.nnz
-    g = torch.Generator(device=device).manual_seed(1000 + (0 if strong else rank))
-    X_global = torch.empty(U, d, device=device).uniform_(-bound, bound, generator=g)
-    dY_global = torch.randn(U, d, device=device, generator=g)
-    if (u0, u1) == (0, U):
-        X, dY = X_global, dY_global
-    else:
-        X, dY = X_global[u0:u1].clone(), dY_global[u0:u1].clone()
-    if not keep_global:
-        del X_global, dY_global
+    seed_x = 1000 + (0 if strong else rank)
+    X = table_rows(u0, u1, d, seed_x, device, bound)
+    dY = table_rows(u0, u1, d, seed_x + 1, device)
     X.requires_grad_(True)
     # warm the scale / edge-value caches outside the timed region
     inc.scale("row", "sym"), inc.edge_values("csc", "sym")
@@ -390,6 +415,7 @@ def main():
     # region (two event records per hop, a few µs on a ~16 ms step); a captured graph cannot
     # record them, so with --graph on the same steps are re-run eagerly afterwards for them
     timer = profiling.HopTimer()
+    xtimer = ExchangeTimer()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -398,7 +424,7 @@ def main():
         for _ in range(args.steps):
             step()
     else:
-        with timer:
+        with timer, xtimer:
             for _ in range(args.steps):
                 step()
     torch.cuda.synchronize()
@@ -412,15 +438,31 @@ def main():
         torch.cuda.synchronize()
     hop = timer.summary()
     hop_ms_step = hop["total_ms"] / args.steps
+    exposed_ms_step = xtimer.total_ms() / args.steps
+    if sh.transport == "p2p" and world > 1:
+        sh._p2p.check()  # no exchange timed out
     check = None
     if args.check and not args.pmc_child:
         Y, dX = eager_step()
+        Y = Y.detach()
+        torch.cuda.synchronize()
         if keep_global:
-            check = check_against_single_gpu(idx, U, I, X_global, dY_global, Y.detach(), dX,
-                                             u0, u1)
-            del idx, X_global, dY_global
+            # one rank at a time: the single-GPU reference of the global graph needs the whole
+            # [U, d] tables (10 GB each at d = 256), too much for N ranks sharing one device
+            for r in range(world):
+                if r == rank:
+                    X_global = table_rows(0, U, d, seed_x, device, bound)
+                    dY_global = table_rows(0, U, d, seed_x + 1, device)
+                    check = check_against_single_gpu(idx, U, I, X_global, dY_global, Y, dX,
+                                                     u0, u1)
+                    del X_global, dY_global
+                    torch.cuda.synchronize()
+                    torch.cuda.empty_cache()
+                dist.barrier()
+            del idx
     per_rank = [{"rank": rank, "users": [u0, u1], "nnz": nnz, "hop_ms_per_step":
-                 round(hop_ms_step, 4)}]
+                 round(hop_ms_step, 4), "exposed_exchange_ms_per_step":
+                 round(exposed_ms_step, 4)}]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -444,6 +486,7 @@ def main():
     if rank != 0:
         if world > 1:
             dist.barrier()
+            sh.close()
             dist.destroy_process_group()
         return
 
@@ -492,6 +535,11 @@ def main():
 
     if world == 1:
         parallelism = "single GPU"
+    elif args.transport == "p2p":
+        parallelism = (f"user-row shards x{world} ({'one global graph' if strong else 'a graph per rank'}), "
+                       f"direct xGMI peer all-reduce (hgd_p2p two-shot mesh reduce, "
+                       f"{dist_backend} for setup) of item messages in {len(sh.slices(d))} "
+                       f"column slices, pipelined with the hops on a high-priority side stream")
     else:
         parallelism = (f"user-row shards x{world} ({'one global graph' if strong else 'a graph per rank'}), "
                        f"{'RCCL' if dist_backend == 'nccl' else dist_backend} all-reduce of item "
@@ -526,11 +574,17 @@ def main():
     if world > 1:
         out["ranks"] = per_rank
         out["exchange_bytes_per_step"] = 2 * sh.exchange_bytes(d)
+        out["transport"] = args.transport
+        # the time the compute stream waited for the all-reduces (HIP events around every hop-2
+        # wait), max over ranks: 0 = the exchange was hidden behind the hops
+        out["exposed_exchange_ms_per_step"] = max(r["exposed_exchange_ms_per_step"]
+                                                  for r in per_rank)
     if check is not None:
         out["check"] = check
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
+        sh.close()
         dist.destroy_process_group()
     if check is not None and not check["ok"]:
         sys.exit(1)

@@ -178,6 +178,7 @@ SCALE_KINDS = {None: SCALE_NONE, "mean": SCALE_MEAN, "sym": SCALE_SYM, "wmean": 
                "wsym": SCALE_WSYM}
 SIDE_ROWS, SIDE_COLS = 0, 1
 COMM_ID_BYTES = 128
+P2P_HANDLE_BYTES = 128
 _PP = ctypes.POINTER(c_void_p)
 
 # name -> (restype, argtypes); every symbol of include/hgd.h appears here.
@@ -344,6 +345,14 @@ _SIGNATURES = {
     "hgd_comm_destroy": (None, [c_void_p]),
     "hgd_comm_set_chunks": (c_i32, [c_void_p, c_i32]),
     "hgd_exchange_allreduce": (c_i32, [c_void_p, c_void_p, c_i64, c_void_p]),
+    "hgd_p2p_create": (c_i32, [c_i32, c_i32, c_i64, c_i32, _PP]),
+    "hgd_p2p_destroy": (None, [c_void_p]),
+    "hgd_p2p_export": (c_i32, [c_void_p, c_void_p]),
+    "hgd_p2p_open": (c_i32, [c_void_p, c_void_p]),
+    "hgd_p2p_slot": (c_void_p, [c_void_p, c_i32]),
+    "hgd_p2p_set_timeout": (c_i32, [c_void_p, ctypes.c_double]),
+    "hgd_p2p_allreduce": (c_i32, [c_void_p, c_i32, c_i64, c_void_p, c_void_p]),
+    "hgd_p2p_check": (c_i32, [c_void_p]),
     "hgd_incidence_globalize_columns": (c_i32, [c_void_p, c_void_p, c_void_p]),
     "hgd_conv2hop_workspace_size": (c_size, [c_void_p, c_i32, c_i32]),
     "hgd_conv2hop_forward": (c_i32, [c_void_p, c_i32, c_i32, c_i32, c_void_p, c_i64, c_i32,
@@ -430,3 +439,65 @@ def _raw_stream_getter():
 
 
 _RAW_STREAM = _raw_stream_getter()
+
+
+# ---------------------------------------------------------------------------------------------
+# Views of library-owned device memory as torch tensors (DLPack, no copy): the send slots of an
+# hgd_p2p exchange are written directly by the hop kernels through such views.
+# ---------------------------------------------------------------------------------------------
+class _DLDevice(ctypes.Structure):
+    _fields_ = [("device_type", ctypes.c_int32), ("device_id", ctypes.c_int32)]
+
+
+class _DLDataType(ctypes.Structure):
+    _fields_ = [("code", ctypes.c_uint8), ("bits", ctypes.c_uint8), ("lanes", ctypes.c_uint16)]
+
+
+class _DLTensor(ctypes.Structure):
+    _fields_ = [("data", c_void_p), ("device", _DLDevice), ("ndim", ctypes.c_int32),
+                ("dtype", _DLDataType), ("shape", ctypes.POINTER(c_i64)),
+                ("strides", ctypes.POINTER(c_i64)), ("byte_offset", ctypes.c_uint64)]
+
+
+class _DLManagedTensor(ctypes.Structure):
+    _fields_ = [("dl_tensor", _DLTensor), ("manager_ctx", c_void_p), ("deleter", c_void_p)]
+
+
+_DL_CPU, _DL_ROCM = 1, 10
+_PyCapsule_New = ctypes.pythonapi.PyCapsule_New
+_PyCapsule_New.restype = ctypes.py_object
+_PyCapsule_New.argtypes = [c_void_p, ctypes.c_char_p, c_void_p]
+
+
+def float_view(address: int, shape, device, owner) -> "torch.Tensor":
+    """A contiguous float32 tensor over ``address`` (device memory the library owns, or host
+    memory for ``device`` = cpu) without copying. ``owner`` (the object whose lifetime bounds the
+    memory) is kept alive by the returned tensor's DLPack record; no deleter is called."""
+    import torch
+    device = torch.device(device)
+    shape = tuple(int(s) for s in shape)
+    rec = _DLManagedTensor()
+    shp = (c_i64 * len(shape))(*shape)
+    rec.dl_tensor.data = address
+    if device.type == "cpu":
+        rec.dl_tensor.device = _DLDevice(_DL_CPU, 0)
+    else:
+        rec.dl_tensor.device = _DLDevice(_DL_ROCM, device.index if device.index is not None
+                                         else torch.cuda.current_device())
+    rec.dl_tensor.ndim = len(shape)
+    rec.dl_tensor.dtype = _DLDataType(2, 32, 1)  # kDLFloat, 32 bits
+    rec.dl_tensor.shape = ctypes.cast(shp, ctypes.POINTER(c_i64))
+    rec.dl_tensor.strides = None  # compact row-major
+    rec.dl_tensor.byte_offset = 0
+    rec.manager_ctx = None
+    rec.deleter = None
+    cap = _PyCapsule_New(ctypes.addressof(rec), b"dltensor", None)
+    t = torch.utils.dlpack.from_dlpack(cap)
+    # the DLPack record, its shape array and the owner live as long as the tensor object
+    _KEEP[id(t)] = (rec, shp, owner)
+    import weakref
+    weakref.finalize(t, _KEEP.pop, id(t), None)
+    return t
+
+
+_KEEP = {}

@@ -96,21 +96,133 @@ def shard_rows_of_sorted_coo(indices: torch.Tensor, n_users: int, world: int, ra
     return u0, u1, loc
 
 
+TRANSPORTS = ("rccl", "p2p")
+
+
+class P2PExchange:
+    """The direct xGMI peer transport (``hgd_p2p_*``, csrc/p2p.hip): every rank exposes one
+    uncached buffer of ``n_slots`` send slots to its peers; an all-reduce of a slot is a two-shot
+    reduce over the mesh (rank r sums block r of every rank's slot, reading the N-1 peers at once,
+    then gathers the other blocks from the peers). Construction is collective over ``group``
+    (the IPC handles travel by ``all_gather_object``)."""
+
+    def __init__(self, max_count: int, n_slots: int, device: torch.device, group=None,
+                 timeout_s: float = 30.0):
+        self.lib = nat.load()
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.device = torch.device(device)
+        self.max_count = int(-(-int(max_count) // 4) * 4)
+        self.n_slots = int(n_slots)
+        h = ctypes.c_void_p()
+        nat.check(self.lib.hgd_p2p_create(self.world, self.rank, self.max_count, self.n_slots,
+                                          ctypes.byref(h)), "hgd_p2p_create")
+        self.h = h
+        nat.check(self.lib.hgd_p2p_set_timeout(h, float(timeout_s)), "hgd_p2p_set_timeout")
+        mine = ctypes.create_string_buffer(nat.P2P_HANDLE_BYTES)
+        nat.check(self.lib.hgd_p2p_export(h, mine), "hgd_p2p_export")
+        handles = [None] * self.world
+        if self.world > 1:
+            dist.all_gather_object(handles, mine.raw, group=group)
+        else:
+            handles = [mine.raw]
+        blob = ctypes.create_string_buffer(b"".join(handles), nat.P2P_HANDLE_BYTES * self.world)
+        nat.check(self.lib.hgd_p2p_open(h, blob), "hgd_p2p_open")
+        self._views = {}
+
+    def slot(self, k: int, rows: int, cols: int) -> torch.Tensor:
+        """Send slot ``k`` as a [rows, cols] float32 view (the hop kernels write into it)."""
+        if rows * cols > self.max_count:
+            raise ValueError(f"P2PExchange: slot of {rows}x{cols} > {self.max_count} floats")
+        key = (k, rows, cols)
+        v = self._views.get(key)
+        if v is None:
+            addr = self.lib.hgd_p2p_slot(self.h, int(k))
+            if not addr:
+                raise ValueError(f"P2PExchange: no slot {k}")
+            v = self._views[key] = nat.float_view(addr, (rows, cols), self.device, self)
+        return v
+
+    def allreduce(self, k: int, count: int, out: torch.Tensor, stream_handle: int) -> None:
+        """out[:count] = Σ_ranks slot k[:count], ordered on the given raw stream."""
+        nat.check(self.lib.hgd_p2p_allreduce(self.h, int(k), int(count), out.data_ptr(),
+                                             stream_handle), "hgd_p2p_allreduce")
+
+    def check(self) -> None:
+        nat.check(self.lib.hgd_p2p_check(self.h), "hgd_p2p")
+
+    def close(self) -> None:
+        """Collective: every rank's peers stop reading before the buffers go."""
+        if self.h is None:
+            return
+        torch.cuda.synchronize(self.device)
+        if self.world > 1:
+            dist.barrier(group=self.group)
+        self._views.clear()
+        self.lib.hgd_p2p_destroy(self.h)
+        self.h = None
+
+
+class ExchangeTimer:
+    """Exposed exchange time of the sharded hops: while active, each hop 2 records an event on
+    the compute stream just before it waits for its slice's exchange and one right after; the
+    pair's interval is the time the compute stream sat idle waiting for the all-reduce (0 when
+    the exchange was hidden behind the preceding hop-1 kernels)."""
+
+    def __init__(self):
+        self.pairs: List[Tuple] = []
+
+    def __enter__(self):
+        global _XTIMER
+        self._prev, _XTIMER = _XTIMER, self
+        return self
+
+    def __exit__(self, *exc):
+        global _XTIMER
+        _XTIMER = self._prev
+        return False
+
+    def mark(self):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+
+    def add(self, a, b):
+        self.pairs.append((a, b))
+
+    def total_ms(self) -> float:
+        torch.cuda.synchronize()
+        return float(sum(a.elapsed_time(b) for a, b in self.pairs))
+
+
+_XTIMER: Optional[ExchangeTimer] = None
+
+
 class ShardedIncidence:
     """One rank's slice of H (users [u0,u1) × all items) plus global item scales.
 
     ``slice_width``: embedding columns per pipelined exchange block (None: 32 for d ≤ 128, else
-    64; a multiple of 4 keeps the float4 gathers). ``n_chunks``: item-row chunks per slice."""
+    64; a multiple of 4 keeps the float4 gathers). ``n_chunks``: item-row chunks per slice (RCCL
+    transport). ``transport``: 'rccl' (torch.distributed all-reduce, backend "nccl" = RCCL) or
+    'p2p' (:class:`P2PExchange`: hop 1 writes each slice straight into an exposed send slot and
+    the slice's two-shot mesh reduce runs on a high-priority side stream)."""
 
     def __init__(self, inc: Incidence, group=None, n_chunks: int = 1,
                  P: Optional[str] = "sym", Q: Optional[str] = "mean", R: Optional[str] = "sym",
-                 slice_width: Optional[int] = None):
+                 slice_width: Optional[int] = None, transport: str = "rccl"):
+        if transport not in TRANSPORTS:
+            raise ValueError(f"ShardedIncidence: transport must be one of {TRANSPORTS}")
         self.inc = inc
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.P, self.R = P, R
+        self.transport = transport
         self.n_chunks = max(1, int(n_chunks)) if self.world > 1 else 1
         self.slice_width = slice_width
+        self._p2p = None
+        self._side = None
+        self._calls = 0
         self.q = self._global_col_scale(Q)
         # item-row chunk boundaries for the overlapped exchange
         n_items = inc.n_cols
@@ -158,6 +270,24 @@ class ShardedIncidence:
         s = torch.where(deg > 0, deg.pow(p), torch.zeros_like(deg))
         return s.to(torch.float32)
 
+    def p2p(self, d: int) -> P2PExchange:
+        """The peer transport for width ``d`` (created on first use: collective)."""
+        sl = self.slices(d)
+        need = self.inc.n_cols * max(c1 - c0 for c0, c1 in sl)
+        if self._p2p is None or self._p2p.max_count < need or self._p2p.n_slots < 2 * len(sl):
+            if self._p2p is not None:
+                self._p2p.close()
+            self._p2p = P2PExchange(need, 2 * len(sl), self.inc.device, group=self.group)
+        if self._side is None:
+            lo, _hi = torch.cuda.Stream.priority_range()
+            self._side = torch.cuda.Stream(self.inc.device, priority=min(lo, _hi))
+        return self._p2p
+
+    def close(self) -> None:
+        if self._p2p is not None:
+            self._p2p.close()
+            self._p2p = None
+
     def two_hop(self, X: torch.Tensor, src_kind: Optional[str],
                 dst_kind: Optional[str]) -> torch.Tensor:
         """``S_dst·H_g·Σ_ranks(Q·H_gᵀ·S_src·X_g)`` with the slice pipeline described above."""
@@ -166,21 +296,49 @@ class ShardedIncidence:
         Y = torch.empty((inc.n_rows, d), dtype=torch.float32, device=X.device)
         val_t = inc.edge_values("csc", src_kind)
         row_scale = inc.scale("row", dst_kind)
+        use_p2p = self.transport == "p2p" and self.world > 1
+        sl = self.slices(d)
+        if use_p2p:
+            ex = self.p2p(d)
+            parity = self._calls % 2
+            self._calls += 1
+            cur = torch.cuda.current_stream(X.device)
+            side_h = self._side.cuda_stream
         pieces = []
-        for c0, c1 in self.slices(d):
+        for s, (c0, c1) in enumerate(sl):
             w = c1 - c0
             Xs = X if w == d else X[:, c0:c1]
-            Ms = torch.empty((inc.n_cols, w), dtype=torch.float32, device=X.device)
             works: List = []
-            for a, b in self.bounds:
-                spmm_csr(inc.csc, Xs, val=val_t, row_scale=self.q, out=Ms, row_begin=a,
-                         row_end=b)
-                if self.world > 1:
-                    works.append(dist.all_reduce(Ms[a:b], group=self.group, async_op=True))
+            if use_p2p:
+                k = parity * len(sl) + s
+                send = ex.slot(k, inc.n_cols, w)
+                spmm_csr(inc.csc, Xs, val=val_t, row_scale=self.q, out=send)
+                Ms = torch.empty((inc.n_cols, w), dtype=torch.float32, device=X.device)
+                ready = torch.cuda.Event()
+                ready.record(cur)
+                self._side.wait_event(ready)
+                ex.allreduce(k, inc.n_cols * w, Ms, side_h)
+                done = torch.cuda.Event()
+                done.record(self._side)
+                works.append(done)
+            else:
+                Ms = torch.empty((inc.n_cols, w), dtype=torch.float32, device=X.device)
+                for a, b in self.bounds:
+                    spmm_csr(inc.csc, Xs, val=val_t, row_scale=self.q, out=Ms, row_begin=a,
+                             row_end=b)
+                    if self.world > 1:
+                        works.append(dist.all_reduce(Ms[a:b], group=self.group, async_op=True))
             pieces.append((c0, c1, Ms, works))
+        xt = _XTIMER if self.world > 1 else None
         for c0, c1, Ms, works in pieces:
+            before = xt.mark() if xt is not None else None
             for wk in works:
-                wk.wait()
+                if use_p2p:
+                    torch.cuda.current_stream(X.device).wait_event(wk)
+                else:
+                    wk.wait()
+            if xt is not None:
+                xt.add(before, xt.mark())
             out = Y if c1 - c0 == d else Y[:, c0:c1]
             spmm_csr(inc.csr, Ms, val=inc.val, row_scale=row_scale, out=out)
         return Y

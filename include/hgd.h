@@ -791,6 +791,38 @@ hgd_status hgd_exchange_allreduce(hgd_comm* comm, float* buf, int64_t count, voi
  * synchronises `stream`. */
 hgd_status hgd_incidence_globalize_columns(hgd_incidence* inc, hgd_comm* comm, void* stream);
 
+/* Direct xGMI peer exchange (SURVEY.md §8e "mesh … direct hipIpc peer kernel"), an alternative
+ * transport to RCCL for the same all-reduce of the item messages: a two-shot reduce over the
+ * mesh — rank r sums block r of every rank's send slot (reading the N-1 peers over their own
+ * xGMI links at once, ranks summed in ascending order), then gathers the other blocks from the
+ * peers' reduced slots. Every rank exposes one uncached allocation (flags + n_slots send slots
+ * + n_slots reduced slots of max_count floats) through hipIpcGetMemHandle. Setup is
+ * collective out of band: create, export, exchange the handles (e.g. all_gather), open.
+ * Waits are bounded (hgd_p2p_set_timeout, default 30 s): a timeout sets a device error flag,
+ * reported by hgd_p2p_check, and later exchanges become no-ops instead of hanging the GPU.
+ * A slot used by exchange i may be rewritten once any later exchange j > i has completed on
+ * this rank's stream; every rank must issue the same exchanges in the same order.
+ * Replaces: nothing in the reference (no distributed code, HCCF.py:24); the design's own. */
+typedef struct hgd_p2p hgd_p2p;
+#define HGD_P2P_HANDLE_BYTES 128
+/* nranks 1..8; max_count a positive multiple of 4 (floats per slot); n_slots 1..1024. */
+hgd_status hgd_p2p_create(int32_t nranks, int32_t rank, int64_t max_count, int32_t n_slots,
+                          hgd_p2p** out);
+void hgd_p2p_destroy(hgd_p2p* p2p);
+/* This rank's handle (HGD_P2P_HANDLE_BYTES host bytes) for its peers. */
+hgd_status hgd_p2p_export(const hgd_p2p* p2p, void* handle_out);
+/* `handles`: nranks × HGD_P2P_HANDLE_BYTES in rank order (this rank's own entry included). */
+hgd_status hgd_p2p_open(hgd_p2p* p2p, const void* handles);
+/* Device pointer of this rank's send slot (max_count floats; write the partial sums here). */
+float* hgd_p2p_slot(hgd_p2p* p2p, int32_t slot);
+hgd_status hgd_p2p_set_timeout(hgd_p2p* p2p, double seconds);
+/* out[0:count) = Σ_ranks send_slot[0:count), ordered on `stream`; count a multiple of 4 and
+ * out 16-byte aligned. */
+hgd_status hgd_p2p_allreduce(hgd_p2p* p2p, int32_t slot, int64_t count, float* out,
+                             void* stream);
+/* Synchronous: HGD_OK, or HGD_ERR_HIP if any exchange timed out. */
+hgd_status hgd_p2p_check(hgd_p2p* p2p);
+
 /* The two-hop conv over the object, Y = epi(P·A·Q·Aᵀ·R·X) with P, R row scales and Q a column
  * scale (hgd_scale each):
  *   HGCNConv (HGNN_HD4.py:455-462)        P = Q = R = NONE on the weighted norm_adj
