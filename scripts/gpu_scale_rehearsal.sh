@@ -1,0 +1,41 @@
+#!/bin/bash
+# Multi-rank rehearsals of the strong-scaling bench on ONE MI355X (VERDICT r2 "next" 2a): N ranks
+# share the device, the exchange runs over gloo (RCCL needs one device per rank) or the direct
+# peer transport (hgd_p2p over same-device IPC, gloo for setup). Each run is `bench.py --check`:
+# Σ per-rank nnz must equal the global graph's 99,999,492 and every rank's Y / dX rows must match
+# the single-GPU conv of the global graph at 1e-5 · conv(|x|). Correctness, not speed: gloo
+# stages every all-reduce through host memory. Records under gpurun_out/r03_scale/.
+#   gpurun --timeout 1200 -- 'bash scripts/gpu_scale_rehearsal.sh'
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+O=gpurun_out/r03_scale
+mkdir -p $O
+export TMPDIR=/tmp
+# progress line for the runner while a rehearsal runs silently (each step has its own limit)
+( while sleep 50; do echo "[rehearsal] $(date +%T) running"; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
+run() {  # name, time limit, bench args...
+  local name=$1 lim=$2
+  shift 2
+  echo "[rehearsal] $name: bench.py $*"
+  timeout -k 10 "$lim" python bench.py --check --steps 2 --warmup 1 --no-cpu-baseline --pmc off \
+    "$@" > $O/$name.json 2> $O/$name.err || { echo "FAILED rc=$? $name"; tail -20 $O/$name.err; exit 1; }
+  python - "$O/$name.json" <<'EOF'
+import json, sys
+line = [l for l in open(sys.argv[1]) if l.startswith("{")][-1]
+r = json.loads(line)
+nnz = sum(x["nnz"] for x in r["ranks"])
+print(f"  n={r['n_gpus']} d={r['config']['emb_dim']} transport={r['transport']} "
+      f"sum_nnz={nnz} edges={r['config']['edges']} check={r['check']}")
+assert nnz == r["config"]["edges"] == 99_999_492 and r["check"]["ok"]
+EOF
+  [ $? -eq 0 ] || exit 1
+}
+HGD_DIST_BACKEND=gloo run gloo_n4_d64 420 --gpus 4
+HGD_DIST_BACKEND=gloo run gloo_n8_d64 540 --gpus 8
+HGD_DIST_BACKEND=gloo run p2p_n4_d64 420 --gpus 4 --transport p2p
+HGD_DIST_BACKEND=gloo run p2p_n8_d64 540 --gpus 8 --transport p2p
+HGD_DIST_BACKEND=gloo run gloo_n4_d256 600 --gpus 4 --dim 256
+HGD_DIST_BACKEND=gloo run p2p_n8_d256 600 --gpus 8 --dim 256 --transport p2p
+echo "[rehearsal] all ok"
