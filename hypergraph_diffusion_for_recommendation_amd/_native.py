@@ -102,6 +102,9 @@ class GemmRowsDesc(ctypes.Structure):
         ("binarize_a", c_i32),
         ("b_row_count", c_void_p),
         ("b_scale", ctypes.c_float),
+        ("a_drop_seed", c_void_p),
+        ("a_drop_keep", c_f32),
+        ("a_drop_scale", c_f32),
     ]
 
 
@@ -123,6 +126,9 @@ class GemmTnDesc(ctypes.Structure):
         ("binarize_a", c_i32),
         ("b_row_scale", c_void_p),
         ("c_scale", ctypes.c_float),
+        ("b_drop_seed", c_void_p),
+        ("b_drop_keep", c_f32),
+        ("b_drop_scale", c_f32),
     ]
 
 
@@ -311,7 +317,7 @@ _SIGNATURES = {
     "hgd_bpr_workspace_size": (c_size, [c_i64, c_i64]),
     "hgd_bpr_forward": (c_i32, [c_void_p, c_i64, c_i64, c_i64, c_i32, c_void_p, c_void_p,
                                 c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_void_p,
-                                c_void_p, c_size, c_void_p]),
+                                c_void_p, c_void_p, c_size, c_void_p]),
     "hgd_bpr_backward": (c_i32, [c_void_p, c_i64, c_i64, c_i64, c_i32, c_void_p, c_void_p,
                                  c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_i64, c_void_p,
                                  c_size, c_void_p]),
@@ -385,10 +391,10 @@ def load() -> ctypes.CDLL:
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        # optional process-wide tuning overrides (hgd_set_tuning keys 1 / 2 / 3 / 4 / 5)
+        # optional process-wide tuning overrides (hgd_set_tuning keys 1 .. 6)
         for key, env in ((1, "HGD_SPMM_UNROLL"), (2, "HGD_SPMM_POLICY"),
                          (3, "HGD_SPMM_PASS_COLS"), (4, "HGD_ROWGEMM_BLOCKS"),
-                         (5, "HGD_SPLITK_ROWS")):
+                         (5, "HGD_SPLITK_ROWS"), (6, "HGD_GEMM_EXACT")):
             if os.environ.get(env):
                 st = lib.hgd_set_tuning(key, int(os.environ[env]))
                 if st != HGD_OK:

@@ -29,7 +29,10 @@ struct BprArgs {
 };
 
 // torch indexing semantics for a valid index (negatives wrap); out-of-range ids are clamped so
-// a bad batch can never fault (the sampler never produces them)
+// a bad batch can never fault — the forward counts them into the caller's bad_index word (the
+// reference's E[idx] gather raises; the host checks the count, functional.bpr_index_errors)
+__device__ __forceinline__ bool index_ok(int64_t i, int64_t n) { return i >= -n && i < n; }
+
 __device__ __forceinline__ int64_t fix_index(int64_t i, int64_t n) {
   if (i < 0) i += n;
   return i < 0 ? 0 : (i >= n ? n - 1 : i);
@@ -44,7 +47,7 @@ __device__ __forceinline__ int64_t dest_row(const BprArgs& a, int64_t q) {
 
 template <int G>
 __global__ __launch_bounds__(kBlock) void k_bpr_rows(BprArgs a, float* anc_out, float* pos_out,
-                                                    float* term, float* coef) {
+                                                    float* term, float* coef, int* bad) {
   constexpr int GPB = kBlock / G;
   const int l = threadIdx.x % G;
   const int64_t k = static_cast<int64_t>(blockIdx.x) * GPB + threadIdx.x / G;
@@ -67,6 +70,8 @@ __global__ __launch_bounds__(kBlock) void k_bpr_rows(BprArgs a, float* anc_out, 
   sp = group_sum<G>(sp);
   sn = group_sum<G>(sn);
   if (l == 0) {
+    if (bad && !(index_ok(a.uid[k], a.nu) && index_ok(a.pid[k], a.ni) && index_ok(a.nid[k], a.ni)))
+      atomicAdd(bad, 1);
     const float s = sp - sn;
     const float sig = 1.f / (1.f + expf(-s));
     const float den = 1e-5f + sig;
@@ -111,9 +116,13 @@ __global__ void k_bpr_bwd_link(BprArgs a, int* head, int* next, int* dst) {
 }
 
 // One lane group per position; the position left at the head of each destination row's list
-// writes that row: the contributions of all its positions, summed in ascending position order
-// (the list is walked once into the group's lanes and ranked there; a list longer than the
-// group — only with tables much smaller than the batch — is summed by repeated minimum walks).
+// writes that row: the contributions of all its positions, summed in ascending position order.
+// The list is walked ONCE into the group's LDS slots (up to CAP positions), ranked there (each
+// lane counts the smaller entries of its slots) and added in rank order. Repeats are routine in
+// real batches — a popular item is the positive of tens of batch rows, and at d = 32 a group is
+// 4 lanes — so the ranking must not chase the list per element; only a list longer than CAP
+// (more repeats of one row than CAP, far beyond any real batch) falls back to repeated minimum
+// walks.
 template <int G>
 __global__ __launch_bounds__(kBlock) void k_bpr_bwd_rows(BprArgs a, const float* coef,
                                                         const float* grad, const int* head,
@@ -123,6 +132,10 @@ __global__ __launch_bounds__(kBlock) void k_bpr_bwd_rows(BprArgs a, const float*
   const int l = threadIdx.x % G;
   const int64_t q = static_cast<int64_t>(blockIdx.x) * GPB + threadIdx.x / G;
   if (q >= 3 * a.B) return;
+  constexpr int CAP = G >= 4 ? 64 : 16;
+  __shared__ int s_list[GPB][CAP];
+  __shared__ int s_sorted[GPB][CAP];
+  const int grp = threadIdx.x / G;
   const int r = dst[q];
   if (head[r] != static_cast<int>(q)) return;  // group-uniform
   const float gB = -(*grad) / static_cast<float>(a.B);
@@ -154,23 +167,29 @@ __global__ __launch_bounds__(kBlock) void k_bpr_bwd_rows(BprArgs a, const float*
       }
     }
   };
-  // walk the list: its length, and element t held by lane t (t < G)
-  int n_pos = 0, mine = 0x7fffffff;
+  // walk the list once: its length, and entry t in slot t (written by lane t mod G)
+  int n_pos = 0;
   for (int e = static_cast<int>(q); e >= 0; e = next[e]) {
-    if (n_pos == l) mine = e;
+    if (n_pos < CAP && n_pos % G == l) s_list[grp][n_pos] = e;
     ++n_pos;
   }
-  if (n_pos <= G) {
-    int rank = 0;  // elements smaller than this lane's
-    for (int t = 0; t < n_pos; ++t) rank += __shfl(mine, t, G) < mine ? 1 : 0;
-    for (int t = 0; t < n_pos; ++t) {
-      int pos = 0;
-      for (int s = 0; s < n_pos; ++s) {
-        const int rs = __shfl(rank, s, G), ms = __shfl(mine, s, G);
-        pos = rs == t ? ms : pos;
-      }
-      add(pos);
+  if (n_pos == 1) {
+    add(q);
+  } else if (n_pos <= CAP) {
+    // the group's lanes are one wave's: order the LDS writes before the other lanes' reads
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int i = l; i < n_pos; i += G) {
+      const int v = s_list[grp][i];
+      int rank = 0;  // entries smaller than v (positions are distinct)
+      for (int j = 0; j < n_pos; ++j) rank += s_list[grp][j] < v ? 1 : 0;
+      s_sorted[grp][rank] = v;
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int t = 0; t < n_pos; ++t) add(s_sorted[grp][t]);
   } else {
     int last = -1;
     for (int t = 0; t < n_pos; ++t) {
@@ -222,7 +241,8 @@ extern "C" hgd_status hgd_bpr_forward(const float* E, int64_t lde, int64_t n_use
                                       int64_t n_items, int32_t d, const int64_t* uid,
                                       const int64_t* pid, const int64_t* nid, int64_t batch,
                                       float* anc_out, float* pos_out, float* coef, float* loss,
-                                      void* workspace, size_t workspace_bytes, void* stream) {
+                                      int32_t* bad_index, void* workspace,
+                                      size_t workspace_bytes, void* stream) {
   clear_error();
   BprArgs a{E, lde, n_users, n_items, uid, pid, nid, batch, d};
   const hgd_status c = check(a, "hgd_bpr_forward");
@@ -240,10 +260,10 @@ extern "C" hgd_status hgd_bpr_forward(const float* E, int64_t lde, int64_t n_use
   const int G = group_for(d);
   const unsigned blocks = static_cast<unsigned>((batch + kBlock / G - 1) / (kBlock / G));
   switch (G) {
-    case 64: hipLaunchKernelGGL(k_bpr_rows<64>, dim3(blocks), dim3(kBlock), 0, st, a, anc_out, pos_out, term, coef); break;
-    case 16: hipLaunchKernelGGL(k_bpr_rows<16>, dim3(blocks), dim3(kBlock), 0, st, a, anc_out, pos_out, term, coef); break;
-    case 4: hipLaunchKernelGGL(k_bpr_rows<4>, dim3(blocks), dim3(kBlock), 0, st, a, anc_out, pos_out, term, coef); break;
-    default: hipLaunchKernelGGL(k_bpr_rows<1>, dim3(blocks), dim3(kBlock), 0, st, a, anc_out, pos_out, term, coef); break;
+    case 64: hipLaunchKernelGGL(k_bpr_rows<64>, dim3(blocks), dim3(kBlock), 0, st, a, anc_out, pos_out, term, coef, bad_index); break;
+    case 16: hipLaunchKernelGGL(k_bpr_rows<16>, dim3(blocks), dim3(kBlock), 0, st, a, anc_out, pos_out, term, coef, bad_index); break;
+    case 4: hipLaunchKernelGGL(k_bpr_rows<4>, dim3(blocks), dim3(kBlock), 0, st, a, anc_out, pos_out, term, coef, bad_index); break;
+    default: hipLaunchKernelGGL(k_bpr_rows<1>, dim3(blocks), dim3(kBlock), 0, st, a, anc_out, pos_out, term, coef, bad_index); break;
   }
   hgd_status s = check_launch("hgd_bpr_forward rows");
   if (s != HGD_OK) return s;

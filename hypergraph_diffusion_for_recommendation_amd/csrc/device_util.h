@@ -72,15 +72,39 @@ __device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
   return x;
 }
 
-// Dropout keep-bit of element i (< 2^32) of a draw (nn.Dropout(p): keep with probability
-// keep = 1 - p): h = lowbias32(lowbias32(i + lo32(seed)) ^ hi32(seed)), u = (h >> 8)·2^-24,
-// kept iff floor(u + keep) != 0 — 32-bit arithmetic only, so it costs a few VALU slots beside
-// the MFMAs of the Linear it rides in (oracle: hgd_oracle.dropout_keep_mask).
-__device__ __forceinline__ bool dropout_keep(uint64_t seed, uint32_t i, float keep) {
-  const uint32_t h = lowbias32(lowbias32(i + static_cast<uint32_t>(seed)) ^
-                               static_cast<uint32_t>(seed >> 32));
-  const float u = static_cast<float>(h >> 8) * (1.0f / 16777216.0f);
-  return floorf(u + keep) != 0.f;
+// Dropout keep-bits (nn.Dropout(p): keep with probability keep = 1 - p), counter-based and drawn
+// for four consecutive elements at once — elements 4c .. 4c + 3 of a draw (c < 2^30) take the
+// four 16-bit halves of h1 = lowbias32(lowbias32(c + lo32(seed)) ^ hi32(seed)) and
+// h2 = lowbias32(h1 ^ 0x9E3779B9) (low half first); an element is kept iff its half is below
+// thr = dropout_threshold(keep) = ⌊keep·2^16 + 1/2⌋ (f32 arithmetic). Three 32-bit finalisers per
+// four elements (the per-element form took two per element, up to 60 % of a d = 128 Linear
+// with the dropout in its store); bit s of the result is element 4c + s (oracle:
+// hgd_oracle.dropout_keep_mask).
+__device__ __forceinline__ uint32_t dropout_threshold(float keep) {
+  return static_cast<uint32_t>(keep * 65536.0f + 0.5f);
+}
+
+__device__ __forceinline__ uint32_t dropout_keep4(uint64_t seed, uint32_t c, uint32_t thr) {
+  const uint32_t h1 = lowbias32(lowbias32(c + static_cast<uint32_t>(seed)) ^
+                                static_cast<uint32_t>(seed >> 32));
+  const uint32_t h2 = lowbias32(h1 ^ 0x9E3779B9u);
+  return static_cast<uint32_t>((h1 & 0xffffu) < thr) |
+         (static_cast<uint32_t>((h1 >> 16) < thr) << 1) |
+         (static_cast<uint32_t>((h2 & 0xffffu) < thr) << 2) |
+         (static_cast<uint32_t>((h2 >> 16) < thr) << 3);
+}
+
+// Keep-bit of one element i (< 2^32) of the same draw.
+__device__ __forceinline__ bool dropout_keep(uint64_t seed, uint32_t i, uint32_t thr) {
+  return (dropout_keep4(seed, i >> 2, thr) >> (i & 3u)) & 1u;
+}
+
+// v ⊙ keep-bits × scale for the four elements 4c .. 4c + 3 held in v
+__device__ __forceinline__ f32x4 dropout_apply4(f32x4 v, uint64_t seed, uint32_t c, uint32_t thr,
+                                                float scale) {
+  const uint32_t k = dropout_keep4(seed, c, thr);
+  return f32x4{(k & 1u) ? v.x * scale : 0.f, (k & 2u) ? v.y * scale : 0.f,
+               (k & 4u) ? v.z * scale : 0.f, (k & 8u) ? v.w * scale : 0.f};
 }
 
 inline int next_pow2(int x) {

@@ -107,23 +107,21 @@ __global__ void k_sum_arrays(SumArrays A, int64_t count, float* out) {  // out m
   }
 }
 
-// nn.Dropout on the device RNG of dropout_keep (device_util.h): y[i] = keep(i) ? x[i]·scale : 0.
-// The same call on the upstream gradient with the same seed is the backward (no stored mask).
+// nn.Dropout on the device RNG of dropout_keep4 (device_util.h): y[i] = keep(i) ? x[i]·scale : 0,
+// one draw per float4 (its four elements are one keep group). The same call on the upstream
+// gradient with the same seed is the backward (no stored mask).
 __global__ void k_dropout(const float* __restrict__ x, int64_t n, const uint64_t* __restrict__ seed_p,
                           float keep, float scale, float* __restrict__ y) {
   const uint64_t seed = *seed_p;
+  const uint32_t thr = dropout_threshold(keep);
   const int64_t i4 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) * 4;
   if (i4 + 3 < n) {
-    float4 v = *reinterpret_cast<const float4*>(x + i4);
-    const uint32_t j = static_cast<uint32_t>(i4);
-    v.x = dropout_keep(seed, j, keep) ? v.x * scale : 0.f;
-    v.y = dropout_keep(seed, j + 1, keep) ? v.y * scale : 0.f;
-    v.z = dropout_keep(seed, j + 2, keep) ? v.z * scale : 0.f;
-    v.w = dropout_keep(seed, j + 3, keep) ? v.w * scale : 0.f;
-    *reinterpret_cast<float4*>(y + i4) = v;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(x + i4);
+    *reinterpret_cast<f32x4*>(y + i4) =
+        dropout_apply4(v, seed, static_cast<uint32_t>(i4 >> 2), thr, scale);
   } else {
     for (int64_t i = i4; i < n; ++i)
-      y[i] = dropout_keep(seed, static_cast<uint32_t>(i), keep) ? x[i] * scale : 0.f;
+      y[i] = dropout_keep(seed, static_cast<uint32_t>(i), thr) ? x[i] * scale : 0.f;
   }
 }
 

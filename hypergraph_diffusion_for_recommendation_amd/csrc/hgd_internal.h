@@ -73,5 +73,7 @@ hgd_status sum_rows_jobs(const SumRowsJob* jobs, int n, hipStream_t st);
 void set_row_gemm_max_blocks(int blocks);
 // HGD_TUNE_SPLITK_ROWS (linear.hip): rows per split-K slice, 0 restores the sizing rule.
 void set_splitk_rows(int rows);
+// HGD_TUNE_GEMM_EXACT (linear.hip): 1 = the exact f32-MFMA products only (no split-bf16).
+void set_gemm_exact(int exact);
 
 }  // namespace hgd

@@ -57,7 +57,7 @@ struct RowGemm {
   int32_t K, N;
   int32_t accumulate;  // Y += product (the bias / ReLU apply to the product alone)
   // forward epilogue after the bias / ReLU: nn.Dropout on the product (keep-bit of element
-  // row·N + col from dropout_keep(*drop_seed, ·, drop_keep), kept values × drop_scale), and a
+  // row·N + col from dropout_keep4(*drop_seed, ·), kept values × drop_scale), and a
   // second store Y2 = Y + res (the residual add after an ED-HNN block)
   const uint64_t* drop_seed;
   float drop_keep;
@@ -73,6 +73,11 @@ struct RowGemm {
   float* row_inv;
   const float* b_row_count;  // Bm row k × 1 / max(b_row_count[k], 1) (hyperedge means)
   float b_scale;             // 0 = off: Bm × b_scale (fl(W · s), as a pre-scaled W)
+  // nn.Dropout on A as it is loaded (element row·K + k of the a_drop_seed draw, kept × scale):
+  // the ED-HNN block's input dropout inside lin_in (EquivSetGNN2.py:91-92)
+  const uint64_t* a_drop_seed;
+  float a_drop_keep;
+  float a_drop_scale;
 };
 
 // Up to two independent products of the same K, N and mask mode in ONE launch (HCCF's user and
@@ -238,10 +243,21 @@ __device__ __forceinline__ void row_gemm_body(const RowGemmGroup& grp) {
   for (int t = 0; t < NT; ++t) bias_v[t] = (p.bias && t < nt) ? p.bias[n0 + 16 * t + i16] : 0.f;
 
   const uint64_t drop_seed = p.drop_seed ? *p.drop_seed : 0ull;
+  const uint32_t drop_thr = dropout_threshold(p.drop_keep);
+  const uint64_t a_seed = p.a_drop_seed ? *p.a_drop_seed : 0ull;
+  const uint32_t a_thr = dropout_threshold(p.a_drop_keep);
   auto compute = [&](int64_t tile, f32x4 (&a)[SUB][KQ], const f32x4 (&m)[SUB][KQ],
                      const float (&rv)[NT][4]) {
 #pragma unroll
     for (int s = 0; s < SUB; ++s) {
+      if (p.a_drop_seed) {  // the float4 at k = 4h + 16q is one keep group (K % 16 == 0)
+        const uint32_t e0 = static_cast<uint32_t>(tile * 16 * SUB + 16 * s + i16) *
+                            static_cast<uint32_t>(p.K);
+#pragma unroll
+        for (int q = 0; q < KQ; ++q)
+          a[s][q] = dropout_apply4(a[s][q], a_seed, (e0 + 4 * h + 16 * q) >> 2, a_thr,
+                                   p.a_drop_scale);
+      }
       if constexpr (MASK) {
 #pragma unroll
         for (int q = 0; q < KQ; ++q) a[s][q] = relu_mask(a[s][q], m[s][q]);
@@ -299,14 +315,14 @@ __device__ __forceinline__ void row_gemm_body(const RowGemmGroup& grp) {
           const float v = acc[t][r] + bias_v[t];
           acc[t][r] = (p.relu && v < 0.f) ? 0.f : v;
         }
-      if (!MASK && p.drop_seed) {
+      if (p.drop_seed) {
 #pragma unroll
         for (int t = 0; t < NT; ++t)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const uint32_t e = static_cast<uint32_t>(r0 + 4 * h + r) * static_cast<uint32_t>(p.N) +
                                static_cast<uint32_t>(n0 + 16 * t + i16);
-            acc[t][r] = dropout_keep(drop_seed, e, p.drop_keep) ? acc[t][r] * p.drop_scale : 0.f;
+            acc[t][r] = dropout_keep(drop_seed, e, drop_thr) ? acc[t][r] * p.drop_scale : 0.f;
           }
       }
       // (the masked backward-data form keeps the direct stores: 7 % slower at d = 64 through LDS)
@@ -403,6 +419,258 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   row_gemm_body<KQ, NT, true, BLDS>(grp);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Split-bf16 row GEMM (the default for K a multiple of 32). The f32-input MFMA runs at 1/16 of
+// the bf16 rate, so at d = 128 the exact-f32 row GEMM is bound by the MFMA (4.73 GFLOP at
+// 157 TF = 30 µs for 144 k rows) and not by its 148 MB of HBM traffic (18.5 µs). Here every f32
+// operand is cut EXACTLY into three bf16 terms, x = x0 + x1 + x2 (round-to-nearest, each
+// residual exact in f32: 8 + 8 + 8 significant bits cover the 24 of an f32), and
+// a·b = Σ_{i+j ≤ 2} a_i·b_j takes six v_mfma_f32_16x16x32_bf16 (bf16 products are exact in f32,
+// accumulated in f32; the dropped a1·b2 + a2·b1 + a2·b2 are < 2^-23·|a·b|): 2.7× the f32 MFMA
+// rate, error ≈ that of the f32 fmaf chain (1e-7 of Σ|a·b|; not bitwise the same sums, so
+// hgd_set_tuning(HGD_TUNE_GEMM_EXACT, 1) keeps the f32-MFMA kernel for bitwise fmaf chains).
+// Non-finite operands (and |x| within 2^-9 of FLT_MAX, whose bf16 rounding overflows) give NaN.
+//
+// Layout: W's slice (K × up to 128 columns) is split once per workgroup into three bf16 planes
+// in LDS, each 16-byte fragment where the lane that feeds it to the MFMA reads it
+// (ds_read_b128, conflict-free). The MFMA takes W as its A operand and the activation rows as
+// its B operand, so the 16 × 16 result tile holds one ROW per lane (column l & 15 of D) and four
+// consecutive output columns per lane (rows 4(l >> 4) + r of D): every lane stores float4 pieces
+// of its own row — the epilogue (bias, ReLU, dropout, residual, row_inv) needs no transpose.
+// A wave owns 16-row tiles over ALL ≤ 128 columns, so every activation row is read once.
+// Lane (i, g) loads row i's floats [32q + 4g, +4) and [32q + 16 + 4g, +4) for k step q: MFMA k
+// index 8g + j is that permutation of the true k, which the W fragments follow.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+int g_gemm_exact = 0;  // HGD_TUNE_GEMM_EXACT
+
+__device__ __forceinline__ f32x4 mfma_bf16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// x = hi + mid + lo exactly: hi = bf16_rn(x), mid = bf16_rn(x - hi), lo = bf16_rn(x - hi - mid)
+__device__ __forceinline__ void split3(const float (&v)[8], bf16x8& hi, bf16x8& mid, bf16x8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 a = static_cast<__bf16>(v[j]);
+    const float r1 = v[j] - static_cast<float>(a);
+    const __bf16 b = static_cast<__bf16>(r1);
+    const float r2 = r1 - static_cast<float>(b);
+    hi[j] = a;
+    mid[j] = b;
+    lo[j] = static_cast<__bf16>(r2);
+  }
+}
+
+// acc += W·x over one k step: small terms first (they are added to the running sum while it is
+// small); with hi-only x (binarized 0/1 rows) the mid / lo products are zero and skipped
+__device__ __forceinline__ f32x4 mfma_x3(const bf16x8& w0, const bf16x8& w1, const bf16x8& w2,
+                                         const bf16x8& x0, const bf16x8& x1, const bf16x8& x2,
+                                         f32x4 acc, bool x_hi_only) {
+  acc = mfma_bf16(w2, x0, acc);
+  if (!x_hi_only) {
+    acc = mfma_bf16(w1, x1, acc);
+    acc = mfma_bf16(w0, x2, acc);
+  }
+  acc = mfma_bf16(w1, x0, acc);
+  if (!x_hi_only) acc = mfma_bf16(w0, x1, acc);
+  return mfma_bf16(w0, x0, acc);
+}
+
+constexpr int kX3Threads = 512;  // 8 waves: two per SIMD even when W's planes fill the LDS
+constexpr int kX3SliceCols = 128;
+
+// NT: 16-column tiles of a ≤ 128-column slice (1, 2, 4 or 8). Tiles past the live nt (N not a
+// multiple of 16·NT) are staged as zeros and computed like the others — only their stores are
+// skipped — so the MFMA stream has no branches; binarized rows likewise run all six products.
+template <int KQ, int NT, bool MASK>
+__global__ __launch_bounds__(kX3Threads) void k_row_gemm_x3(RowGemmGroup grp) {
+  extern __shared__ __attribute__((aligned(16))) char x3_smem[];
+  bf16x8* sW = reinterpret_cast<bf16x8*>(x3_smem);  // [3][NT][KQ][64]
+  float* sBias = reinterpret_cast<float*>(sW + 3 * NT * KQ * 64);  // [NT·16]
+  int bxg, ys;
+  row_block_of(grp, bxg, ys);
+  const bool second = grp.count > 1 && bxg >= grp.nb0;
+  const RowGemm p = second ? grp.p[1] : grp.p[0];  // a copy: its fields live in registers
+  const int bx = bxg - (second ? grp.nb0 : 0);
+  const int nbx = grp.count > 1 ? (second ? grp.nbt - grp.nb0 : grp.nb0) : grp.nbt;
+  constexpr int WAVES = kX3Threads / 64;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int i16 = lane & 15;
+  const int g = lane >> 4;
+  const int n0 = ys * kX3SliceCols;
+  const int nt = min(NT, (p.N - n0) / 16);
+  const int64_t tiles = (p.rows + 15) / 16;
+  const int64_t stride = static_cast<int64_t>(nbx) * WAVES;
+  int64_t tile = static_cast<int64_t>(bx) * WAVES + wave;
+
+  // activation rows of a tile (+ its mask rows)
+  auto load = [&](int64_t tl, f32x4 (&a)[KQ][2], f32x4 (&m)[KQ][2]) {
+    tl = tl < tiles ? tl : tiles - 1;
+    int64_t row = tl * 16 + i16;
+    row = row < p.rows ? row : p.rows - 1;
+    const float* ar = p.A + row * p.lda + 4 * g;
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      a[q][0] = ld4(ar + 32 * q);
+      a[q][1] = ld4(ar + 32 * q + 16);
+    }
+    if constexpr (MASK) {
+      const float* mr = p.mask + row * p.ldm + 4 * g;
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) {
+        m[q][0] = ld4(mr + 32 * q);
+        m[q][1] = ld4(mr + 32 * q + 16);
+      }
+    }
+  };
+  f32x4 a0[KQ][2], a1[KQ][2], m0v[KQ][2], m1v[KQ][2];
+  if (tile < tiles) load(tile, a0, m0v);
+
+  // W's slice → three bf16 planes in fragment order (+ the bias slice): every fragment's eight
+  // loads first (in flight together), then the splits and the LDS stores
+  {
+    constexpr int FRAGS = NT * KQ * 64;
+    constexpr int FR = (FRAGS + kX3Threads - 1) / kX3Threads;
+    float v[FR][8];
+#pragma unroll
+    for (int r = 0; r < FR; ++r) {
+      const int f = threadIdx.x + kX3Threads * r;
+      const int L = f & 63, q = (f >> 6) % KQ, t = (f >> 6) / KQ;
+      const int gg = L >> 4;
+      const bool live = f < FRAGS && t < nt;
+      const int n = live ? n0 + 16 * t + (L & 15) : 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 32 * (live ? q : 0) + (j < 4 ? 4 * gg + j : 16 + 4 * gg + (j - 4));
+        v[r][j] = p.B[static_cast<int64_t>(k) * p.bsk + static_cast<int64_t>(n) * p.bsn];
+        if (p.b_row_count) v[r][j] *= 1.f / fmaxf(p.b_row_count[k], 1.f);
+        if (p.b_scale != 0.f) v[r][j] *= p.b_scale;
+        if (!live) v[r][j] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < FR; ++r) {
+      const int f = threadIdx.x + kX3Threads * r;
+      if (f < FRAGS) {
+        const int L = f & 63, q = (f >> 6) % KQ, t = (f >> 6) / KQ;
+        bf16x8 h, md, lo;
+        split3(v[r], h, md, lo);
+        sW[((0 * NT + t) * KQ + q) * 64 + L] = h;
+        sW[((1 * NT + t) * KQ + q) * 64 + L] = md;
+        sW[((2 * NT + t) * KQ + q) * 64 + L] = lo;
+      }
+    }
+  }
+  for (int c = threadIdx.x; c < NT * 16; c += kX3Threads)
+    sBias[c] = (p.bias && c < nt * 16) ? p.bias[n0 + c] : 0.f;
+  __syncthreads();
+  if (tile >= tiles) return;  // after the block's barrier
+
+  const uint64_t drop_seed = p.drop_seed ? *p.drop_seed : 0ull;
+  const uint32_t drop_thr = dropout_threshold(p.drop_keep);
+  const uint64_t a_seed = p.a_drop_seed ? *p.a_drop_seed : 0ull;
+  const uint32_t a_thr = dropout_threshold(p.a_drop_keep);
+  auto compute = [&](int64_t tl, const f32x4 (&a)[KQ][2], const f32x4 (&m)[KQ][2]) {
+    const int64_t row = tl * 16 + i16;
+    const bool live = row < p.rows;
+    // the residual pieces of the Y2 store, requested before this tile's MFMAs (≈ 1 µs of them)
+    f32x4 rv[NT];
+    if (!MASK && p.Y2) {
+      const float* rr = p.res + (live ? row : p.rows - 1) * p.ldres + n0 + 4 * g;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) rv[t] = ld4(rr + 16 * (t < nt ? t : 0));
+    }
+    f32x4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float rs = 0.f;
+    // W fragments double-buffered: group (q, t + 1)'s three LDS reads are issued before group
+    // (q, t)'s six MFMAs, so the reads' latency hides behind them
+    bf16x8 wf[2][3];
+    auto read_w = [&](int q, int t, bf16x8 (&w)[3]) {
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) w[pl] = sW[((pl * NT + t) * KQ + q) * 64 + lane];
+    };
+    read_w(0, 0, wf[0]);
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      f32x4 x0 = a[q][0], x1 = a[q][1];
+      if (p.a_drop_seed) {  // each float4 piece is one keep group of the input dropout
+        const uint32_t e0 = static_cast<uint32_t>(row) * static_cast<uint32_t>(p.K) + 32 * q + 4 * g;
+        x0 = dropout_apply4(x0, a_seed, e0 >> 2, a_thr, p.a_drop_scale);
+        x1 = dropout_apply4(x1, a_seed, (e0 + 16) >> 2, a_thr, p.a_drop_scale);
+      }
+      if constexpr (MASK) {
+        x0 = relu_mask(x0, m[q][0]);
+        x1 = relu_mask(x1, m[q][1]);
+      } else {
+        if (p.binarize_a) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            x0[c] = x0[c] > 0.f ? 1.f : 0.f;
+            x1[c] = x1[c] > 0.f ? 1.f : 0.f;
+          }
+        }
+        if (p.row_inv) rs += ((x0.x + x0.y) + (x0.z + x0.w)) + ((x1.x + x1.y) + (x1.z + x1.w));
+      }
+      const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+      bf16x8 xh, xm, xl;
+      split3(v, xh, xm, xl);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int cur = (q * NT + t) & 1;
+        if (t + 1 < NT) read_w(q, t + 1, wf[cur ^ 1]);
+        else if (q + 1 < KQ) read_w(q + 1, 0, wf[cur ^ 1]);
+        acc[t] = mfma_x3(wf[cur][0], wf[cur][1], wf[cur][2], xh, xm, xl, acc[t], false);
+      }
+    }
+    // lane (i16, g): row r0 + i16, columns n0 + 16t + 4g + c in acc[t][c]
+    if (!MASK && p.row_inv) {
+      rs += __shfl_xor(rs, 16);
+      rs += __shfl_xor(rs, 32);
+      const float inv = 1.f / fmaxf(rs, 1.f);
+      if (g == 0 && n0 == 0 && live) p.row_inv[row] = inv;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] *= inv;
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const f32x4 b4 = *reinterpret_cast<const f32x4*>(&sBias[16 * t + 4 * g]);
+      const int col = n0 + 16 * t + 4 * g;
+      f32x4 v = acc[t] + b4;
+      if (p.relu) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c] = v[c] < 0.f ? 0.f : v[c];
+      }
+      if (p.drop_seed) {  // the lane's four columns are one keep group (N % 16 == 0)
+        const uint32_t e = static_cast<uint32_t>(row) * static_cast<uint32_t>(p.N) +
+                           static_cast<uint32_t>(col);
+        v = dropout_apply4(v, drop_seed, e >> 2, drop_thr, p.drop_scale);
+      }
+      if (!live || t >= nt) continue;
+      float* y = p.Y + row * p.ldy + col;
+      if (p.accumulate) v += ld4(y);
+      *reinterpret_cast<f32x4*>(y) = v;
+      if (!MASK && p.Y2) *reinterpret_cast<f32x4*>(p.Y2 + row * p.ldy2 + col) = v + rv[t];
+    }
+  };
+  while (tile < tiles) {
+    load(tile + stride, a1, m1v);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(tile, a0, m0v);
+    __builtin_amdgcn_sched_barrier(0);
+    tile += stride;
+    if (tile >= tiles) break;
+    load(tile + stride, a0, m0v);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(tile, a1, m1v);
+    __builtin_amdgcn_sched_barrier(0);
+    tile += stride;
+  }
+}
+
 struct SplitK {
   const float* A;  // [rows, M] (dY)
   int64_t lda;
@@ -417,6 +685,9 @@ struct SplitK {
   float* part_bias;  // [S, M] or NULL
   int32_t binarize_a;  // A as its nonzero pattern (a > 0 ? 1 : 0)
   const float* b_row_scale;  // [rows] or NULL: B row × scale on load
+  const uint64_t* b_drop_seed;  // nn.Dropout on B as it is loaded (element row·N + n), before
+  float b_drop_keep;            // b_row_scale
+  float b_drop_scale;
 };
 
 struct SplitKGroup {  // as RowGemmGroup: blocks [0, nb0) along x are p[0]'s row slices
@@ -451,6 +722,8 @@ __global__ __launch_bounds__(256) void k_splitk_tn(SplitKGroup grp) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) acc[t][u] = f32x4{0.f, 0.f, 0.f, 0.f};
   float bsum[4] = {0.f, 0.f, 0.f, 0.f};
+  const uint64_t b_seed = p.b_drop_seed ? *p.b_drop_seed : 0ull;
+  const uint32_t b_thr = dropout_threshold(p.b_drop_keep);
 
   // 4-row steps per wave per batch (loads of batch b+1 overlap b's MFMAs); 8 steps held 212-256
   // VGPRs (one wave per SIMD), 4 steps allow two
@@ -465,6 +738,9 @@ __global__ __launch_bounds__(256) void k_splitk_tn(SplitKGroup grp) {
       a[s] = ld4(p.A + kr * p.lda + mc);
       if constexpr (MASK) m[s] = ld4(p.mask + kr * p.ldm + mc);
       b[s] = ld4(p.B + kr * p.ldb + nc);
+      if (p.b_drop_seed)  // the float4 at column nc is one keep group (N % 16 == 0)
+        b[s] = dropout_apply4(b[s], b_seed,
+                              static_cast<uint32_t>(kr * p.N + nc) >> 2, b_thr, p.b_drop_scale);
       if (p.b_row_scale) {  // fl(B · scale), as a pre-scaled B would hold it
         const float sc = p.b_row_scale[kr];
         b[s] = f32x4{b[s].x * sc, b[s].y * sc, b[s].z * sc, b[s].w * sc};
@@ -543,6 +819,171 @@ __global__ __launch_bounds__(256) void k_splitk_tn(SplitKGroup grp) {
   }
 }
 
+// Split-bf16 form of k_splitk_tn (see k_row_gemm_x3 for the numerics). The reduction runs over
+// rows, so an MFMA's k index is a row: lane (i16, g) loads rows 8g + j (j < 8) of a 32-row step
+// as float4 pieces of A at columns 4·i16 and float2 pieces of B at columns 2·i16; component t of
+// its eight A pieces is the A fragment of MFMA (t, u) (output m = 4·i + t), component u of the B
+// pieces its B fragment (n = 2·i16 + u): 4 × 2 products × 6 split terms give a 64 × 32 tile per
+// 32 rows. A workgroup of 8 waves covers up to eight such tiles of the output at once (all of a
+// 128 × 128 weight gradient), so every row of A and B is read from HBM once per slice — the
+// 64 × 64-tile grid re-read each operand once per tile of the other (296 MB for a 148 MB
+// product at d = 128); with fewer tiles than waves the rows are dealt to P = 8 / tiles phases,
+// combined in LDS in phase order. Every operand of a step is split before the next step's loads
+// are issued, so those loads fly during this step's MFMAs.
+constexpr int kX3SplitKThreads = 512;
+constexpr int kX3SplitKResident = 256;  // workgroups of one resident round (one per CU)
+
+__host__ __device__ constexpr int x3_tiles_per_wg(int tiles) {
+  return tiles % 8 == 0 ? 8 : (tiles % 4 == 0 ? 4 : (tiles % 2 == 0 ? 2 : 1));
+}
+
+template <bool MASK>
+__global__ __launch_bounds__(kX3SplitKThreads) void k_splitk_tn_x3(SplitKGroup grp) {
+  const bool second = grp.count > 1 && static_cast<int>(blockIdx.x) >= grp.nb0;
+  const SplitK p = second ? grp.p[1] : grp.p[0];
+  const int64_t bx = static_cast<int64_t>(blockIdx.x) - (second ? grp.nb0 : 0);
+  constexpr int WAVES = kX3SplitKThreads / 64;
+  __shared__ float s_acc[WAVES][64 * 32];
+  __shared__ float s_bias[WAVES][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int i16 = lane & 15;
+  const int g = lane >> 4;
+  const int tiles_h = (p.N + 31) / 32;
+  const int Qg = x3_tiles_per_wg(((p.M + 63) / 64) * tiles_h);
+  const int P = WAVES / Qg;
+  const int slot = wave % Qg, phase = wave / Qg;
+  const int tile = static_cast<int>(blockIdx.y) * Qg + slot;
+  const int m0 = (tile / tiles_h) * 64;
+  const int n0 = (tile % tiles_h) * 32;
+  const int64_t k_begin = bx * p.rows_per_split;
+  const int64_t k_end = min(p.rows, k_begin + p.rows_per_split);
+  const bool mcol = m0 + 4 * i16 < p.M;
+  const bool ncol = n0 + 2 * i16 < p.N;
+  const int mc = mcol ? m0 + 4 * i16 : m0;
+  const int nc = ncol ? n0 + 2 * i16 : n0;
+  const bool want_bias = p.part_bias != nullptr && n0 == 0;
+  const bool hi_only = p.binarize_a != 0;
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) acc[t][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bsum[4] = {0.f, 0.f, 0.f, 0.f};
+  const uint64_t b_seed = p.b_drop_seed ? *p.b_drop_seed : 0ull;
+  const uint32_t b_thr = dropout_threshold(p.b_drop_keep);
+
+  f32x4 a[8], m[8];
+  f32x2 b[8];
+  float sc[8];
+  auto load = [&](int64_t kb) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      int64_t kr = kb + 8 * g + j;
+      kr = kr < k_end ? kr : k_begin;
+      a[j] = ld4(p.A + kr * p.lda + mc);
+      if constexpr (MASK) m[j] = ld4(p.mask + kr * p.ldm + mc);
+      b[j] = *reinterpret_cast<const f32x2*>(p.B + kr * p.ldb + nc);
+      if (p.b_row_scale) sc[j] = p.b_row_scale[kr];
+    }
+  };
+  const int64_t step = 32 * P;
+  int64_t kb = k_begin + 32 * phase;
+  if (kb < k_end) load(kb);
+  while (kb < k_end) {
+    bool ok[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ok[j] = kb + 8 * g + j < k_end;
+    bf16x8 bs[2][3], as[4][3];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float x = b[j][u];
+        if (p.b_drop_seed) {  // elements nc, nc + 1 are half of one keep group
+          const uint32_t e = static_cast<uint32_t>((kb + 8 * g + j) * p.N + nc + u);
+          x = dropout_keep(b_seed, e, b_thr) ? x * p.b_drop_scale : 0.f;
+        }
+        if (p.b_row_scale) x *= sc[j];  // fl(B · scale), as a pre-scaled B would hold it
+        v[j] = (ok[j] && ncol) ? x : 0.f;
+      }
+      split3(v, bs[u][0], bs[u][1], bs[u][2]);
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float x = a[j][t];
+        if constexpr (MASK) x = m[j][t] > 0.f ? x : 0.f;
+        if (hi_only) x = x > 0.f ? 1.f : 0.f;
+        v[j] = (ok[j] && mcol) ? x : 0.f;
+      }
+      if (want_bias) bsum[t] += ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+      split3(v, as[t][0], as[t][1], as[t][2]);
+    }
+    kb += step;
+    if (kb < k_end) load(kb);  // in flight during this step's MFMAs
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        // D = A·B (rows m, columns n); binarized A: its mid / lo products are zero, skipped
+        f32x4 c = acc[t][u];
+        if (!hi_only) {
+          c = mfma_bf16(as[t][2], bs[u][0], c);
+          c = mfma_bf16(as[t][1], bs[u][1], c);
+        }
+        c = mfma_bf16(as[t][0], bs[u][2], c);
+        if (!hi_only) c = mfma_bf16(as[t][1], bs[u][0], c);
+        c = mfma_bf16(as[t][0], bs[u][1], c);
+        acc[t][u] = mfma_bf16(as[t][0], bs[u][0], c);
+      }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // acc[t][u] lane (i16, g) reg r: m_local = 4·(4g + r) + t, n_local = 2·i16 + u
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        s_acc[wave][(4 * (4 * g + r) + t) * 32 + 2 * i16 + u] = acc[t][u][r];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    bsum[t] += __shfl_xor(bsum[t], 16);
+    bsum[t] += __shfl_xor(bsum[t], 32);
+    if (g == 0) s_bias[wave][4 * i16 + t] = bsum[t];
+  }
+  __syncthreads();
+  const int64_t MN = static_cast<int64_t>(p.M) * p.N;
+  for (int e = threadIdx.x; e < Qg * 64 * 32; e += kX3SplitKThreads) {
+    const int q = e / (64 * 32), el = e % (64 * 32);
+    const int tq = static_cast<int>(blockIdx.y) * Qg + q;
+    const int mq = (tq / tiles_h) * 64 + el / 32, nq = (tq % tiles_h) * 32 + el % 32;
+    if (mq < p.M && nq < p.N) {
+      float v = s_acc[q][el];
+      for (int ph = 1; ph < P; ++ph) v += s_acc[ph * Qg + q][el];
+      p.part[bx * MN + static_cast<int64_t>(mq) * p.N + nq] = v;
+    }
+  }
+  if (p.part_bias != nullptr) {
+    for (int e = threadIdx.x; e < Qg * 64; e += kX3SplitKThreads) {
+      const int q = e / 64, ml = e % 64;
+      const int tq = static_cast<int>(blockIdx.y) * Qg + q;
+      const int mq = (tq / tiles_h) * 64 + ml;
+      if (tq % tiles_h == 0 && mq < p.M) {
+        float v = s_bias[q][ml];
+        for (int ph = 1; ph < P; ++ph) v += s_bias[ph * Qg + q][ml];
+        p.part_bias[bx * p.M + mq] = v;
+      }
+    }
+  }
+}
+
 bool al16(const void* p, int64_t ld) {
   return p == nullptr || (reinterpret_cast<uintptr_t>(p) % 16 == 0 && ld % 4 == 0);
 }
@@ -563,6 +1004,73 @@ void blocks_for(const int64_t* rows, int count, int64_t* bx) {
   }
 }
 
+constexpr size_t x3_lds_bytes(int KQ, int NT) {
+  return static_cast<size_t>(3 * NT * KQ * 64) * 16 + static_cast<size_t>(NT) * 16 * 4;
+}
+
+// One split-bf16 launch: as many workgroups as the tiles want, at most one resident round (the
+// occupancy of this instantiation at its LDS size × the CUs), shared by a group's products in
+// proportion to their rows; column slices XCD-paired as in row_block_of.
+template <int KQ, int NT, bool MASK>
+hgd_status launch_x3(RowGemmGroup g, hipStream_t st, const char* fn) {
+  const void* kern = reinterpret_cast<const void*>(&k_row_gemm_x3<KQ, NT, MASK>);
+  constexpr size_t lds = x3_lds_bytes(KQ, NT);
+  static int resident = 0;
+  if (resident == 0) {
+    if (lds > 65536)
+      HGD_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  static_cast<int>(lds)));
+    int nb = 0, dev = 0, cus = 0;
+    HGD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, kX3Threads, lds));
+    HGD_HIP(hipGetDevice(&dev));
+    HGD_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    resident = std::max(1, nb) * std::max(1, cus);
+  }
+  constexpr int64_t kRowsPerBlock = 16 * (kX3Threads / 64);
+  int64_t want[2] = {0, 0}, total = 0;
+  for (int i = 0; i < g.count; ++i) {
+    want[i] = (g.p[i].rows + kRowsPerBlock - 1) / kRowsPerBlock;
+    total += want[i];
+  }
+  g.ny = (g.p[0].N + kX3SliceCols - 1) / kX3SliceCols;
+  const int64_t cap = std::max<int64_t>(1, resident / g.ny);
+  int64_t bx[2] = {0, 0};
+  for (int i = 0; i < g.count; ++i) {
+    bx[i] = total > cap ? std::max<int64_t>(1, want[i] * cap / total) : want[i];
+    if (g.ny > 1) bx[i] = (bx[i] + 7) / 8 * 8;
+  }
+  g.nb0 = static_cast<int32_t>(bx[0]);
+  g.nbt = static_cast<int32_t>(bx[0] + bx[1]);
+  const dim3 grid(static_cast<unsigned>(g.nbt) * static_cast<unsigned>(g.ny));
+  hipLaunchKernelGGL((k_row_gemm_x3<KQ, NT, MASK>), grid, dim3(kX3Threads), lds, st, g);
+  return check_launch(fn);
+}
+
+template <int KQ, int NT>
+hgd_status launch_x3_mask(const RowGemmGroup& g, hipStream_t st, const char* fn) {
+  return g.p[0].mask ? launch_x3<KQ, NT, true>(g, st, fn) : launch_x3<KQ, NT, false>(g, st, fn);
+}
+
+template <int KQ>
+hgd_status launch_x3_nt(const RowGemmGroup& g, hipStream_t st, const char* fn) {
+  const int N = g.p[0].N;
+  if (N <= 16) return launch_x3_mask<KQ, 1>(g, st, fn);
+  if (N <= 32) return launch_x3_mask<KQ, 2>(g, st, fn);
+  if (N <= 64) return launch_x3_mask<KQ, 4>(g, st, fn);
+  return launch_x3_mask<KQ, 8>(g, st, fn);
+}
+
+// The split-bf16 kernel takes K a multiple of 32 and 16-byte aligned output rows (it stores
+// float4 pieces of a row); everything else, and HGD_TUNE_GEMM_EXACT, runs the f32-MFMA kernel.
+bool x3_eligible(const RowGemmGroup& g) {
+  if (g_gemm_exact || g.p[0].K % 32 != 0) return false;
+  for (int i = 0; i < g.count; ++i) {
+    const RowGemm& p = g.p[i];
+    if (!al16(p.Y, p.ldy) || !al16(p.Y2, p.ldy2) || !al16(p.res, p.ldres)) return false;
+  }
+  return true;
+}
+
 hgd_status row_gemm_group(RowGemmGroup g, hipStream_t st, const char* fn) {
   const RowGemm& p = g.p[0];
   if (g.count == 2) {
@@ -576,6 +1084,15 @@ hgd_status row_gemm_group(RowGemmGroup g, hipStream_t st, const char* fn) {
     }
   }
   if (g.count == 0 || g.p[0].rows == 0) return HGD_OK;
+  if (x3_eligible(g)) {
+    switch (g.p[0].K / 32) {
+      case 1: return launch_x3_nt<1>(g, st, fn);
+      case 2: return launch_x3_nt<2>(g, st, fn);
+      case 3: return launch_x3_nt<3>(g, st, fn);
+      case 4: return launch_x3_nt<4>(g, st, fn);
+      default: break;
+    }
+  }
   const int64_t rows[2] = {g.p[0].rows, g.count > 1 ? g.p[1].rows : 0};
   int64_t bx[2] = {0, 0};
   blocks_for(rows, g.count, bx);
@@ -637,19 +1154,32 @@ void tn_splits(const hgd_gemm_tn_desc* d, int count, int64_t* S, int64_t* per) {
     }
     return;
   }
+  // workgroups per slice and the resident budget: 64 × 64 tiles of 256 threads (f32 MFMA), or
+  // groups of up to eight 64 × 32 tiles of 512 threads (split-bf16)
+  const bool x3 = !g_gemm_exact;
+  auto wg_per_slice = [&](const hgd_gemm_tn_desc& e) -> int64_t {
+    if (!x3) return static_cast<int64_t>((e.M + 63) / 64) * ((e.N + 63) / 64);
+    const int t = ((e.M + 63) / 64) * ((e.N + 31) / 32);
+    return t / x3_tiles_per_wg(t);
+  };
+  const int64_t resident = x3 ? kX3SplitKResident : kSplitKResident;
   int64_t total = 0;
   for (int i = 0; i < count; ++i) {
-    S[i] = splits_for(d[i].rows, static_cast<int64_t>((d[i].M + 63) / 64) * ((d[i].N + 63) / 64));
+    if (x3) {  // ≥ 256 rows per workgroup (8 waves × 32-row steps), one resident round at most
+      S[i] = std::min<int64_t>(std::max<int64_t>(1, (d[i].rows + 255) / 256),
+                               std::max<int64_t>(1, resident / wg_per_slice(d[i])));
+    } else {
+      S[i] = splits_for(d[i].rows, wg_per_slice(d[i]));
+    }
     total += S[i];
   }
   for (int i = 0; i < count; ++i) {
-    const int64_t tiles = static_cast<int64_t>((d[0].M + 63) / 64) * ((d[0].N + 63) / 64);
-    const int64_t budget = std::max<int64_t>(1, kSplitKResident / tiles);
+    const int64_t budget = std::max<int64_t>(1, resident / wg_per_slice(d[0]));
     if (count > 1 && total > budget)
       S[i] = std::max<int64_t>(1, S[i] * budget / total);
     const int64_t rows = d[i].rows > 0 ? d[i].rows : 1;
     int64_t pr = (rows + S[i] - 1) / S[i];
-    per[i] = (pr + 63) / 64 * 64;  // whole 64-row batches
+    per[i] = (pr + 127) / 128 * 128;  // whole 128-row steps (4 waves × 32 rows of the x3 form)
     S[i] = (rows + per[i] - 1) / per[i];
   }
 }
@@ -668,6 +1198,10 @@ hgd_status check_tn(const hgd_gemm_tn_desc& d, const char* fn) {
   HGD_REQUIRE(d.lda >= d.M && d.ldb >= d.N && (!d.relu_mask || d.ldm >= d.M),
               "%s: leading dimension too small", fn);
   HGD_REQUIRE(d.C, "%s: null C", fn);
+  HGD_REQUIRE(!d.b_drop_seed || (d.b_drop_keep > 0.f && d.b_drop_keep <= 1.f),
+              "%s: B dropout keep must be in (0, 1]", fn);
+  HGD_REQUIRE(!d.b_drop_seed || d.rows * static_cast<int64_t>(d.N) <= 0xffffffffLL,
+              "%s: B dropout needs rows·N < 2^32 (32-bit element counter)", fn);
   if (d.rows == 0) return HGD_OK;
   HGD_REQUIRE(d.A && d.B, "%s: null A / B", fn);
   HGD_REQUIRE(al16(d.A, d.lda) && al16(d.B, d.ldb) && al16(d.relu_mask, d.ldm),
@@ -690,8 +1224,12 @@ hgd_status check_rows(const hgd_gemm_rows_desc& d, const char* fn) {
   HGD_REQUIRE((d.res == nullptr) == (d.Y2 == nullptr), "%s: res and Y2 go together", fn);
   // the masked form is the backward-data product: its kernel carries none of the forward
   // epilogues (their registers kept it at one wave per SIMD)
-  HGD_REQUIRE(!d.relu_mask || (!d.drop_seed && !d.Y2 && !d.row_inv && !d.binarize_a),
-              "%s: relu_mask excludes the dropout, residual, row_inv and binarize_a epilogues", fn);
+  HGD_REQUIRE(!d.relu_mask || (!d.Y2 && !d.row_inv && !d.binarize_a),
+              "%s: relu_mask excludes the residual, row_inv and binarize_a epilogues", fn);
+  HGD_REQUIRE(!d.a_drop_seed || (d.a_drop_keep > 0.f && d.a_drop_keep <= 1.f),
+              "%s: A dropout keep must be in (0, 1]", fn);
+  HGD_REQUIRE(!d.a_drop_seed || d.rows * static_cast<int64_t>(d.K) <= 0xffffffffLL,
+              "%s: A dropout needs rows·K < 2^32 (32-bit element counter)", fn);
   HGD_REQUIRE(!d.Y2 || (d.ldres >= d.N && d.ldy2 >= d.N), "%s: ldres / ldy2 too small", fn);
   if (d.rows == 0) return HGD_OK;
   HGD_REQUIRE(d.A && d.B && d.Y, "%s: null pointer", fn);
@@ -706,6 +1244,7 @@ void set_row_gemm_max_blocks(int blocks) {
   g_row_gemm_max_blocks = blocks > 0 ? blocks : kRowGemmMaxBlocks;
 }
 void set_splitk_rows(int rows) { g_splitk_rows = rows > 0 ? rows : 0; }
+void set_gemm_exact(int exact) { g_gemm_exact = exact != 0; }
 }  // namespace hgd
 
 extern "C" hgd_status hgd_linear_forward(const float* X, int64_t ldx, int64_t n_rows,
@@ -833,6 +1372,9 @@ extern "C" hgd_status hgd_gemm_tn(const hgd_gemm_tn_desc* descs, int32_t count, 
     p.rows_per_split = per[i];
     p.binarize_a = d.binarize_a;
     p.b_row_scale = d.b_row_scale;
+    p.b_drop_seed = d.b_drop_seed;
+    p.b_drop_keep = d.b_drop_keep;
+    p.b_drop_scale = d.b_drop_scale;
     p.part = reinterpret_cast<float*>(w);
     w += tn_part_bytes(d, S[i]);
     p.part_bias = d.colsum_A ? reinterpret_cast<float*>(w) : nullptr;
@@ -854,10 +1396,19 @@ extern "C" hgd_status hgd_gemm_tn(const hgd_gemm_tn_desc* descs, int32_t count, 
     }
   const dim3 grid(static_cast<unsigned>(Stot), static_cast<unsigned>((g.p[0].M + 63) / 64),
                   static_cast<unsigned>((g.p[0].N + 63) / 64));
-  if (g.p[0].mask)
+  if (!g_gemm_exact) {
+    const int tiles = ((g.p[0].M + 63) / 64) * ((g.p[0].N + 31) / 32);
+    const dim3 gx(static_cast<unsigned>(Stot),
+                  static_cast<unsigned>(tiles / x3_tiles_per_wg(tiles)));
+    if (g.p[0].mask)
+      hipLaunchKernelGGL((k_splitk_tn_x3<true>), gx, dim3(kX3SplitKThreads), 0, st, g);
+    else
+      hipLaunchKernelGGL((k_splitk_tn_x3<false>), gx, dim3(kX3SplitKThreads), 0, st, g);
+  } else if (g.p[0].mask) {
     hipLaunchKernelGGL((k_splitk_tn<true>), grid, dim3(256), 0, st, g);
-  else
+  } else {
     hipLaunchKernelGGL((k_splitk_tn<false>), grid, dim3(256), 0, st, g);
+  }
   hgd_status s = check_launch("hgd_gemm_tn");
   if (s != HGD_OK) return s;
   // the slice partials in slice order: all sums of the group in one launch
@@ -909,6 +1460,9 @@ extern "C" hgd_status hgd_gemm_rows(const hgd_gemm_rows_desc* descs, int32_t cou
     p.row_inv = d.row_inv;
     p.b_row_count = d.b_row_count;
     p.b_scale = d.b_scale;
+    p.a_drop_seed = d.a_drop_seed;
+    p.a_drop_keep = d.a_drop_keep;
+    p.a_drop_scale = d.a_drop_scale;
   }
   g.count = count;
   return row_gemm_group(g, as_stream(stream), "hgd_gemm_rows");

@@ -752,6 +752,10 @@ extern "C" hgd_status hgd_set_tuning(int32_t key, int32_t value) {
                   "[64, 65536]");
       set_splitk_rows(value);
       return HGD_OK;
+    case HGD_TUNE_GEMM_EXACT:
+      HGD_REQUIRE(value == 0 || value == 1, "hgd_set_tuning: gemm exact must be 0 or 1");
+      set_gemm_exact(value);
+      return HGD_OK;
     default:
       return fail(HGD_ERR_INVALID_ARG, "hgd_set_tuning: unknown key %d", key);
   }

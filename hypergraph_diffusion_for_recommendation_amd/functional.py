@@ -388,6 +388,8 @@ class _Fan(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, n: int):
+        # an alias whose output gets no gradient arrives as None (no zero table to read)
+        ctx.set_materialize_grads(False)
         return tuple(x.view_as(x) for _ in range(n))
 
     @staticmethod
@@ -397,6 +399,8 @@ class _Fan(torch.autograd.Function):
             return None, None
         if len(gs) == 1:
             return gs[0], None
+        # hgd_sum_arrays reads 16-byte pieces: a contiguous view at an odd offset is copied
+        gs = [g if g.data_ptr() % 16 == 0 else g.clone() for g in gs]
         out = torch.empty_like(gs[0])
         ptrs = (ctypes.c_void_p * len(gs))(*[g.data_ptr() for g in gs])
         nat.check(nat.load().hgd_sum_arrays(ptrs, len(gs), out.numel(), out.data_ptr(),
@@ -444,14 +448,16 @@ def sum_n(ts):
 
 
 class _LinearReluDrop(torch.autograd.Function):
-    """``dropout(relu(X·Wᵀ + b), p) (+ res)`` in the row GEMM's store (hgd_gemm_rows: the
-    ReLU, the dropout mask of the library RNG and its 1/(1-p), the residual as a second
-    output). Backward: a row GEMM (dX) and a split-K product (dW, db) with the stored dropped
-    activation as the mask (it is > 0 exactly where the ReLU passed and the element was kept) and
-    1/(1-p) folded into W as it is staged and into the dW / db reduction's store."""
+    """``dropout(relu(dropout(X, in_p)·Wᵀ + b), p) (+ res)`` in the row GEMM (hgd_gemm_rows: the
+    input dropout as X is loaded, the ReLU, the dropout mask of the library RNG and its 1/(1-p)
+    in the store, the residual as a second output). Backward: a row GEMM (dX, with the input
+    dropout's mask and scale in its store) and a split-K product (dW, db; the input dropout
+    re-applied as X is loaded) with the stored dropped activation as the mask (it is > 0 exactly
+    where the ReLU passed and the element was kept) and 1/(1-p) folded into W as it is staged
+    and into the dW / db reduction's store. The dropped input is never materialised."""
 
     @staticmethod
-    def forward(ctx, X, weight, bias, res, p: float, seed):
+    def forward(ctx, X, weight, bias, res, p: float, seed, in_p: float, in_seed):
         X = X.contiguous()
         W = weight.contiguous()
         n, in_f = X.shape
@@ -460,6 +466,10 @@ class _LinearReluDrop(torch.autograd.Function):
         Y = torch.empty((n, out_f), dtype=torch.float32, device=dev)
         d = _rows_desc(X, W, 1, W.stride(0), in_f, out_f, Y)
         d.bias, d.relu = nat.ptr(bias), 1
+        in_keep = in_scale = 1.0
+        if in_p > 0.0:
+            in_keep, in_scale = _drop_consts(in_p)
+            d.a_drop_seed, d.a_drop_keep, d.a_drop_scale = in_seed.data_ptr(), in_keep, in_scale
         scale = 1.0
         if p > 0.0:
             keep, scale = _drop_consts(p)
@@ -472,14 +482,15 @@ class _LinearReluDrop(torch.autograd.Function):
                 out.stride(0)
         _gemm_rows([d], dev)
         ctx.scale = scale
+        ctx.in_drop = (in_keep, in_scale) if in_p > 0.0 else None
         ctx.has_bias, ctx.has_res = bias is not None, res is not None
-        ctx.save_for_backward(X, W, Y)
+        ctx.save_for_backward(X, W, Y, in_seed if in_p > 0.0 else None)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         lib = nat.load()
-        X, W, Y = ctx.saved_tensors
+        X, W, Y, in_seed = ctx.saved_tensors
         dY = dout.contiguous()
         n, in_f = X.shape
         out_f = W.shape[0]
@@ -487,11 +498,14 @@ class _LinearReluDrop(torch.autograd.Function):
         s = ctx.scale
         dX = dW = db = None
         if ctx.needs_input_grad[0]:
-            # dX = (dY ⊙ [Y > 0])·(W·s): the 1/(1-p) scales W as the row GEMM stages it
+            # dX = (dY ⊙ [Y > 0])·(W·s): the 1/(1-p) scales W as the row GEMM stages it; the
+            # input dropout's backward (its keep-bits × 1/(1-in_p)) in the store
             dX = torch.empty_like(X)
             d = _rows_desc(dY, W, W.stride(0), 1, out_f, in_f, dX)
             d.relu_mask, d.ldm = Y.data_ptr(), Y.stride(0)
             d.b_scale = s if s != 1.0 else 0.0
+            if ctx.in_drop is not None:
+                d.drop_seed, d.drop_keep, d.drop_scale = (in_seed.data_ptr(),) + ctx.in_drop
             _gemm_rows([d], dev)
         want_b = ctx.has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1] or want_b:
@@ -503,6 +517,8 @@ class _LinearReluDrop(torch.autograd.Function):
             t.B, t.ldb, t.rows, t.M, t.N = X.data_ptr(), X.stride(0), n, out_f, in_f
             t.C, t.colsum_A = dW.data_ptr(), nat.ptr(db)
             t.c_scale = s if s != 1.0 else 0.0
+            if ctx.in_drop is not None:  # dropout(X) re-drawn as X is loaded
+                t.b_drop_seed, t.b_drop_keep, t.b_drop_scale = (in_seed.data_ptr(),) + ctx.in_drop
             arr = (nat.GemmTnDesc * 1)(t)
             wsb = lib.hgd_gemm_tn_workspace_size(arr, 1)
             ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
@@ -511,26 +527,32 @@ class _LinearReluDrop(torch.autograd.Function):
             if not ctx.needs_input_grad[1]:
                 dW = None
         dres = dY if ctx.has_res and ctx.needs_input_grad[3] else None
-        return dX, dW, db, dres, None, None
+        return dX, dW, db, dres, None, None, None, None
 
 
 def linear_relu_dropout(X: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
                         p: float, res: Optional[torch.Tensor] = None,
-                        seed: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``F.dropout(F.relu(F.linear(X, weight, bias)), p) + res`` (the ED-HNN block's lin_in →
-    dropout and W → ReLU → dropout → + residual, layers2/EquivSetGNN2.py:91-101 and
-    HGNN_HD4.py:399) with everything after the product in the row GEMM's store. ``p = 0``:
-    no dropout; ``res`` None: no residual. Shapes outside the kernels run the torch ops (with
-    the library dropout)."""
+                        seed: Optional[torch.Tensor] = None, in_p: float = 0.0,
+                        in_seed: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``F.dropout(F.relu(F.linear(F.dropout(X, in_p), weight, bias)), p) + res`` (the ED-HNN
+    block's dropout → lin_in → ReLU and W → ReLU → dropout → + residual,
+    layers2/EquivSetGNN2.py:91-101 and HGNN_HD4.py:399) with the input dropout in the row GEMM's
+    operand load and everything after the product in its store. ``p`` / ``in_p = 0``: no
+    dropout; ``res`` None: no residual. Bitwise ``linear_relu_dropout(dropout(X, in_p, in_seed),
+    …)``. Shapes outside the kernels run the torch ops (with the library dropout)."""
     if res is not None and tuple(res.shape) != (X.shape[0], weight.shape[0]):
         raise ValueError("linear_relu_dropout: residual shape mismatch")
+    if in_p > 0.0 and in_seed is None:
+        in_seed = dropout_seed(X.device)
     if not (_linear_native_ok(X, weight) and X.dim() == 2
-            and X.shape[0] * weight.shape[0] <= 0xFFFFFFFF):
+            and X.shape[0] * max(weight.shape[0], weight.shape[1]) <= 0xFFFFFFFF):
+        if in_p > 0.0:
+            X = dropout(X, in_p, in_seed)
         y = dropout(linear(X, weight, bias, relu=True), p, seed)
         return y if res is None else y + res
     if p > 0.0 and seed is None:
         seed = dropout_seed(X.device)
-    return _LinearReluDrop.apply(X, weight, bias, res, float(p), seed)
+    return _LinearReluDrop.apply(X, weight, bias, res, float(p), seed, float(in_p), in_seed)
 
 
 class _RowEpilogue(torch.autograd.Function):
@@ -883,12 +905,18 @@ def unique_long(x: torch.Tensor) -> torch.Tensor:
 _UQ_HEAD = 256  # bytes before the unique workspace (count at 0; 256-byte aligned workspace)
 
 
-def unique_long_n(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+def unique_long_n(x: torch.Tensor, n_rows: Optional[int] = None
+                  ) -> Tuple[torch.Tensor, torch.Tensor]:
     """:func:`unique_long` without the device→host read, for a captured training step:
-    ``(nodes, count)`` with ``nodes`` int64 capacity-sized (x.numel()), its first ``count[0]``
-    entries the sorted unique values of ``x.long()`` and the rest 0, ``count`` an int64 [1]
-    device tensor (hgd_unique_dev_*: the range bitmap with the far keys merged on the device, so
-    no host decision). Feed both to :func:`contrast_loss`."""
+    ``(nodes, count)`` with ``nodes`` int64 capacity-sized, its first ``count[0]`` entries the
+    sorted unique values of ``x.long()`` and the rest 0, ``count`` an int64 [1] device tensor
+    (hgd_unique_dev_*: the range bitmap with the far keys merged on the device, so no host
+    decision). Feed both to :func:`contrast_loss`. The capacity is x.numel(), or at most
+    2·n_rows when the ids index a table of ``n_rows`` rows: valid torch indices lie in
+    [-n_rows, n_rows), so no valid list is longer (HCCF's ``torch.unique(anchor_emb.long())``,
+    HCCF.py:65-66, reads a [B, d] table of a handful of distinct ints — B·d capacity made every
+    InfoNCE buffer and grid that size); a list of out-of-range ids is cut to the capacity, and
+    such ids are the caller's error either way (the reference's gather raises)."""
     if not x.is_cuda or x.dtype not in (torch.float32, torch.int64):
         raise ValueError("unique_long_n: needs a float32 or int64 device tensor")
     x = x.detach().contiguous().view(-1)
@@ -905,7 +933,11 @@ def unique_long_n(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     nat.check(fn(x.data_ptr(), n, out.data_ptr(), base, base + _UQ_HEAD, wsb,
                  nat.stream_handle(dev)), "hgd_unique_dev")
     count = buf[:8].view(torch.int64)
-    live = torch.arange(n, device=dev) < count
+    cap = n if n_rows is None else max(1, min(n, 2 * int(n_rows)))
+    if cap < n:
+        out = out[:cap]
+        count = torch.clamp_max(count, cap)
+    live = torch.arange(cap, device=dev) < count
     return torch.where(live, out, torch.zeros((), dtype=torch.int64, device=dev)), count
 
 
@@ -1232,6 +1264,31 @@ def hccf_layers(adjs, user_emb: torch.Tensor, item_emb: torch.Tensor, hypers_u, 
     return out[0], list(out[1:1 + L]), list(out[1 + L:])
 
 
+_BPR_BAD = {}
+
+
+def _bpr_bad_word(dev: torch.device) -> torch.Tensor:
+    """The per-device int32 word every fused BPR forward adds its out-of-range id count to (a
+    fixed address, so captured steps keep counting into it)."""
+    key = (dev.type, dev.index if dev.index is not None else torch.cuda.current_device())
+    w = _BPR_BAD.get(key)
+    if w is None:
+        w = _BPR_BAD[key] = torch.zeros(1, dtype=torch.int32, device=dev)
+    return w
+
+
+def bpr_index_errors(dev: torch.device, reset: bool = True) -> int:
+    """Batch rows with an out-of-range uid / pid / nid seen by :func:`bpr_loss_rows` on ``dev``
+    since the last reset (one device→host read). The kernels clamp such ids where the
+    reference's ``E[idx]`` gather raises (HCCF.py:84-86); the training loops call this once per
+    epoch and raise IndexError on a non-zero count."""
+    w = _bpr_bad_word(dev)
+    n = int(w.item())
+    if reset and n:
+        w.zero_()
+    return n
+
+
 class _BPRTable(torch.autograd.Function):
     """bpr_loss(E[uid], E[nu + pid], E[nu + nid]) (util/loss_torch.py:5-9) on one [N, d] table
     (hgd_bpr_forward / hgd_bpr_backward); also returns the gathered anchor and positive rows
@@ -1251,7 +1308,8 @@ class _BPRTable(torch.autograd.Function):
         nat.check(lib.hgd_bpr_forward(
             E.data_ptr(), E.stride(0), nu, N - nu, d, uid.data_ptr(), pid.data_ptr(),
             nid.data_ptr(), B, anc.data_ptr(), pos.data_ptr(), coef.data_ptr(), loss.data_ptr(),
-            ws.data_ptr(), wsb, nat.stream_handle(dev)), "hgd_bpr_forward")
+            _bpr_bad_word(dev).data_ptr(), ws.data_ptr(), wsb, nat.stream_handle(dev)),
+            "hgd_bpr_forward")
         ctx.nu = nu
         ctx.save_for_backward(E, uid, pid, nid, coef)
         ctx.mark_non_differentiable(anc, pos)

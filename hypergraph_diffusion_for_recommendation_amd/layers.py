@@ -31,7 +31,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .functional import (dense_mean_two_hop, dense_mean_two_hop_ok,
-                         dense_mean_two_hop_pair, dense_two_hop, dropout,
+                         dense_mean_two_hop_pair, dense_two_hop,
                          dropout_seed, layer_norm, linear, linear_relu_dropout, spmm, two_hop,
                          two_hop_fused)
 from .incidence import (CSR, Incidence, MaskedIncidence, dense_threshold, drop_edges,
@@ -521,8 +521,9 @@ class EquivSetGNN(nn.Module):
             # from H (functional.dense_mean_two_hop), no V/E lists and no host read
             p = self.dropout.p if self.training else 0.0
             seeds = [dropout_seed(x.device) for _ in range(3)] if p > 0.0 else [None] * 3
-            x = dropout(x, p, seeds[0])
-            x = linear_relu_dropout(x, self.lin_in.weight, self.lin_in.bias, p, seed=seeds[1])
+            # the input dropout rides in lin_in's operand load (never materialised)
+            x = linear_relu_dropout(x, self.lin_in.weight, self.lin_in.bias, p, seed=seeds[1],
+                                    in_p=p, in_seed=seeds[0])
             ln, lin = input_norm_linear(self.conv.W)
             y = layer_norm(dense_mean_two_hop(hypergraph, self.conv.W1(x)), ln)
             return linear_relu_dropout(y, lin.weight, lin.bias, p, res=residual, seed=seeds[2])
@@ -532,8 +533,9 @@ class EquivSetGNN(nn.Module):
             # second one in lin_in's store, the last one and the residual in W's store
             p = self.dropout.p if self.training else 0.0
             seeds = [dropout_seed(x.device) for _ in range(3)] if p > 0.0 else [None] * 3
-            x = dropout(x, p, seeds[0])
-            x = linear_relu_dropout(x, self.lin_in.weight, self.lin_in.bias, p, seed=seeds[1])
+            # the input dropout rides in lin_in's operand load (never materialised)
+            x = linear_relu_dropout(x, self.lin_in.weight, self.lin_in.bias, p, seed=seeds[1],
+                                    in_p=p, in_seed=seeds[0])
             return self.conv.forward_tail(x, V, E, p, residual=residual, seed=seeds[2])
         x = self.dropout(x)
         x = self.lin_in(x, relu=True)  # F.relu(lin_in(x)) fused
@@ -569,8 +571,8 @@ class EquivSetGNN(nn.Module):
         as two per-half masks)."""
         p = self.dropout.p if self.training else 0.0
         seeds = [dropout_seed(x.device) for _ in range(3)] if p > 0.0 else [None] * 3
-        x = dropout(x, p, seeds[0])
-        x = linear_relu_dropout(x, self.lin_in.weight, self.lin_in.bias, p, seed=seeds[1])
+        x = linear_relu_dropout(x, self.lin_in.weight, self.lin_in.bias, p, seed=seeds[1],
+                                in_p=p, in_seed=seeds[0])
         ln, lin = input_norm_linear(self.conv.W)
         y = layer_norm(dense_mean_two_hop_pair(H_u, H_i, self.conv.W1(x)), ln)
         return linear_relu_dropout(y, lin.weight, lin.bias, p, seed=seeds[2])

@@ -45,7 +45,8 @@ from torch.optim.lr_scheduler import ReduceLROnPlateau
 
 from .encoders import (HCCFDiffusionEncoder, HCCFEncoder, LocalAwareEncoder,
                        LocalAwareEncoderHD3, sparse_tensor_of)
-from .functional import (bpr_loss_rows, contrast_loss, contrast_loss_pair, unique_long,
+from .functional import (bpr_index_errors, bpr_loss_rows, contrast_loss, contrast_loss_pair,
+                         unique_long,
                          unique_long_n)
 from .layers import HGCNConv, SpAdjDropEdge
 from .sampler import next_batch_pairwise
@@ -137,7 +138,8 @@ class HCCF(GraphRecommender):
         # and with device drop-edge masks, capacity-sized with the count kept on the device)
         dropper = getattr(getattr(self, "model", None), "edgeDropper", None)
         if getattr(self, "graph_mode", False) or getattr(dropper, "capture_safe", False):
-            (u_nodes, u_cnt), (p_nodes, p_cnt) = unique_long_n(ancs), unique_long_n(poss)
+            (u_nodes, u_cnt) = unique_long_n(ancs, nu)
+            (p_nodes, p_cnt) = unique_long_n(poss, self.data.n_items)
         else:
             u_nodes, p_nodes = unique_long(ancs), unique_long(poss)
             u_cnt = p_cnt = None
@@ -199,6 +201,12 @@ class HCCF(GraphRecommender):
                 user_idx, pos_idx, neg_idx = batch
                 batch_loss = self.graph_step(user_idx, pos_idx, neg_idx)
                 train_losses.append(batch_loss.item())
+            # the fused BPR clamps out-of-range ids where the reference's gather raises: one
+            # read of its device count per epoch
+            bad = bpr_index_errors(self.device)
+            if bad:
+                raise IndexError(f"HCCF: {bad} batch rows held a user / item id out of range "
+                                 f"(epoch {ep})")
             tr_time = time.time() - s_train
             model.eval()
             with torch.no_grad():

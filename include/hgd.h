@@ -68,13 +68,19 @@ typedef enum hgd_epilogue {
  *                         stride of 4·blocks)
  *   HGD_TUNE_SPLITK_ROWS: rows per slice of the split-K products (hgd_gemm_tn,
  *                         hgd_linear_backward_weight; 0 = default sizing, else a multiple of 64
- *                         in [64, 65536]; the workspace size follows it) */
+ *                         in [64, 65536]; the workspace size follows it)
+ *   HGD_TUNE_GEMM_EXACT:  0 (default) = the dense products with K (row GEMM) or the row count's
+ *                         reduction (split-K) eligible run as split-bf16 MFMAs (every f32
+ *                         operand cut exactly into three bf16 terms, six products: error
+ *                         ≈ 1e-7·Σ|a·b| like the f32 fmaf chain, not bitwise equal to it);
+ *                         1 = the exact f32-input MFMA kernels only (bitwise k-ordered fmaf) */
 typedef enum hgd_tune_key {
   HGD_TUNE_SPMM_UNROLL = 1,
   HGD_TUNE_SPMM_POLICY = 2,
   HGD_TUNE_SPMM_PASS_COLS = 3,
   HGD_TUNE_ROWGEMM_BLOCKS = 4,
-  HGD_TUNE_SPLITK_ROWS = 5
+  HGD_TUNE_SPLITK_ROWS = 5,
+  HGD_TUNE_GEMM_EXACT = 6
 } hgd_tune_key;
 hgd_status hgd_set_tuning(int32_t key, int32_t value);
 
@@ -306,6 +312,14 @@ typedef struct hgd_gemm_rows_desc {
    * split-K product that made Xe (same product as scaling B beforehand) */
   const float* b_row_count;
   float b_scale;          /* 0 = off: B × b_scale as it is staged (a Dropout's 1/(1-p) in dX) */
+  /* a_drop_seed (NULL = off): nn.Dropout on A as it is loaded — element (row, k) kept as
+   * hgd_dropout_apply keeps element row·K + k (rows·K < 2^32) for seed *a_drop_seed, kept values
+   * × a_drop_scale, before relu_mask / binarize_a: the ED-HNN block's input dropout inside
+   * lin_in (EquivSetGNN2.py:91-92). With relu_mask set, drop_seed is the backward of such an
+   * input dropout: the masked product's output × its keep-bits × drop_scale. */
+  const uint64_t* a_drop_seed;
+  float a_drop_keep;
+  float a_drop_scale;
 } hgd_gemm_rows_desc;
 hgd_status hgd_gemm_rows(const hgd_gemm_rows_desc* descs, int32_t count, void* stream);
 
@@ -325,6 +339,12 @@ typedef struct hgd_gemm_tn_desc {
   const float* b_row_scale; /* [rows] or NULL: B's row r × b_row_scale[r] as it is loaded (the
                              * vertex means D_v^-1 of the mean two-hop's backward) */
   float c_scale;          /* 0 = off: C and colsum_A × c_scale as they are stored */
+  /* b_drop_seed (NULL = off): nn.Dropout on B as it is loaded (element row·N + n kept as
+   * hgd_dropout_apply keeps it, rows·N < 2^32, kept × b_drop_scale; before b_row_scale) — the
+   * weight gradient of a Linear whose input dropout ran inside its forward */
+  const uint64_t* b_drop_seed;
+  float b_drop_keep;
+  float b_drop_scale;
 } hgd_gemm_tn_desc;
 size_t hgd_gemm_tn_workspace_size(const hgd_gemm_tn_desc* descs, int32_t count);
 hgd_status hgd_gemm_tn(const hgd_gemm_tn_desc* descs, int32_t count, void* workspace,
@@ -636,7 +656,9 @@ hgd_status hgd_unique_dev_trunc_f32(const float* x, int64_t n, int64_t* out, int
  * BPR loss from the embedding table (util/loss_torch.py:5-9 over the rows HCCF.py:84-86
  * gathers): E [n_users + n_items, lde] (users first, 16-byte aligned rows, d % 4 == 0,
  * d <= 256); anc = E[uid], pos = E[n_users + pid], neg = E[n_users + nid] (int64 ids, torch
- * indexing semantics; out-of-range ids are clamped, never dereferenced);
+ * indexing semantics; out-of-range ids are clamped, never dereferenced, and the forward adds
+ * the number of batch rows holding one to *bad_index when it is non-NULL — a device word the
+ * caller zeroes and reads when it chooses: the reference's gather raises on such an id);
  *   loss = mean_k −log(1e-5 + σ(⟨anc_k,pos_k⟩ − ⟨anc_k,neg_k⟩)), coef_k = σ(1−σ)/(1e-5+σ).
  * anc_out / pos_out ([batch, d], optional) receive the gathered rows (HCCF's InfoNCE node lists
  * are taken from them). Backward: dE = ∂(grad·loss)/∂E written in full (zero rows included;
@@ -646,7 +668,8 @@ size_t hgd_bpr_workspace_size(int64_t batch, int64_t n_rows);
 hgd_status hgd_bpr_forward(const float* E, int64_t lde, int64_t n_users, int64_t n_items,
                            int32_t d, const int64_t* uid, const int64_t* pid, const int64_t* nid,
                            int64_t batch, float* anc_out, float* pos_out, float* coef,
-                           float* loss, void* workspace, size_t workspace_bytes, void* stream);
+                           float* loss, int32_t* bad_index, void* workspace,
+                           size_t workspace_bytes, void* stream);
 hgd_status hgd_bpr_backward(const float* E, int64_t lde, int64_t n_users, int64_t n_items,
                             int32_t d, const int64_t* uid, const int64_t* pid,
                             const int64_t* nid, int64_t batch, const float* coef,
@@ -665,10 +688,12 @@ hgd_status hgd_epilogue_backward(const float* ref, const float* dy, int64_t n, i
                                  float slope, float* dz, void* stream);
 /* nn.Dropout(p) on the library's counter-based RNG (the ED-HNN block's dropouts,
  * layers2/EquivSetGNN2.py:91-101, when they run in its Linear stores or alone): y[i] = x[i]·scale
- * if element i (< 2^32) is kept, else 0 — kept iff floor(u + keep) != 0 with
- * u = (h >> 8)·2^-24, h = lowbias32(lowbias32(i + lo32(s)) ^ hi32(s)), s = *seed (a device
- * value). keep = 1 - p, scale = 1 / (1 - p). The backward is the same call on the gradient with
- * the same seed (no mask is stored). x, y 16-byte aligned; y may alias x. */
+ * if element i (< 2^32) is kept, else 0. Elements 4c .. 4c + 3 share one draw:
+ * h1 = lowbias32(lowbias32(c + lo32(s)) ^ hi32(s)), h2 = lowbias32(h1 ^ 0x9E3779B9), s = *seed
+ * (a device value); element 4c + j is kept iff the j-th 16-bit half of (h1, h2), low half
+ * first, is below floor(keep·65536 + 0.5) (f32). keep = 1 - p, scale = 1 / (1 - p). The
+ * backward is the same call on the gradient with the same seed (no mask is stored). x, y
+ * 16-byte aligned; y may alias x. */
 hgd_status hgd_dropout_apply(const float* x, int64_t n, const uint64_t* seed, float keep,
                              float scale, float* y, void* stream);
 /* out[i] = Σ_s P[s·slice_stride + i] over s = 0..n_slices-1, summed in slice order (bitwise the

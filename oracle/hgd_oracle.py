@@ -558,9 +558,11 @@ def dropout_keep_mask(seed, n, keep):
     dropout epilogue, hgd_gemm_rows_desc.drop_*: the build's own counter-based RNG for the
     ED-HNN block's nn.Dropout, layers2/EquivSetGNN2.py:91-101; the reference draws torch's
     CUDA philox stream, which no test can share, so the parity tests rebuild these masks here
-    and feed them to the float64 reference). For element i < 2^32:
-    h = lowbias32(lowbias32(i + lo32(seed)) ^ hi32(seed)), u = (h >> 8) / 2^24, kept iff
-    floor(u + keep) != 0 in float32. Bit-exact restatement for testing."""
+    and feed them to the float64 reference). Elements 4c .. 4c + 3 (c < 2^30) share one draw:
+    h1 = lowbias32(lowbias32(c + lo32(seed)) ^ hi32(seed)), h2 = lowbias32(h1 ^ 0x9E3779B9);
+    element 4c + s takes the s-th 16-bit half of (h1, h2), low half first, and is kept iff that
+    half is below thr = floor(keep·2^16 + 1/2) computed in float32 (device_util.h
+    dropout_keep4). Bit-exact restatement for testing."""
     m32 = np.uint32(0xFFFFFFFF)
 
     def lowbias32(x):
@@ -572,11 +574,15 @@ def dropout_keep_mask(seed, n, keep):
 
     seed = int(seed) & 0xFFFFFFFFFFFFFFFF
     lo, hi = np.uint32(seed & 0xFFFFFFFF), np.uint32(seed >> 32)
+    thr = np.uint32(np.float32(keep) * np.float32(65536.0) + np.float32(0.5))
+    groups = (int(n) + 3) // 4
     with np.errstate(over="ignore"):
-        i = np.arange(n, dtype=np.uint32)
-        h = lowbias32(lowbias32((i + lo) & m32) ^ hi)
-    u = (h >> np.uint32(8)).astype(np.float32) * np.float32(1.0 / 16777216.0)
-    return np.floor(u + np.float32(keep)) != 0
+        c = np.arange(groups, dtype=np.uint32)
+        h1 = lowbias32(lowbias32((c + lo) & m32) ^ hi)
+        h2 = lowbias32(h1 ^ np.uint32(0x9E3779B9))
+    halves = np.stack([h1 & np.uint32(0xFFFF), h1 >> np.uint32(16),
+                       h2 & np.uint32(0xFFFF), h2 >> np.uint32(16)], axis=1).reshape(-1)
+    return (halves < thr)[:int(n)]
 
 
 def device_keep_mask(seed, n, keep):

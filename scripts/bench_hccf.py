@@ -80,10 +80,10 @@ def main():
                 bpr = R.bpr_loss(anc, pos, neg)
             ssl = 0
             # the reference recomputes torch.unique(·.long()) per layer; ours hoists it (same value)
-            un = (unique(anc), unique(pos)) if hoist else None
+            un = (unique(anc, nu), unique(pos, ni)) if hoist else None
             for layer in range(args.layers):
                 e1, e2 = gcn[layer].detach(), hyp[layer]
-                nu_nodes, np_nodes = un if hoist else (unique(anc), unique(pos))
+                nu_nodes, np_nodes = un if hoist else (unique(anc, nu), unique(pos, ni))
                 if counted:  # (nodes, device count) pairs: both halves in one op
                     ssl = ssl + contrast_loss_pair(e1, e2, nu, nu_nodes[0], np_nodes[0], temp,
                                                    nu_nodes[1], np_nodes[1])
@@ -131,10 +131,10 @@ def main():
     out = []
     want = args.variants.split(",")
     if "hgd_cpu_mask" in want:
-        out.append(("hgd_cpu_mask", timed(make_step(ours, contrast_loss, unique_long))))
+        out.append(("hgd_cpu_mask", timed(make_step(ours, contrast_loss, lambda t, n: unique_long(t)))))
     if "hgd_device_mask" in want:
         ours.edgeDropper.device_rng = True
-        out.append(("hgd_device_mask", timed(make_step(ours, contrast_loss, unique_long))))
+        out.append(("hgd_device_mask", timed(make_step(ours, contrast_loss, lambda t, n: unique_long(t)))))
     if "hgd_graph" in want:
         torch.manual_seed(0)
         g_model = HCCFEncoder(conf, data, dev)
@@ -152,7 +152,7 @@ def main():
         out.append(("hgd_capture_safe_eager", timed(make_step(e_model, contrast_loss,
                                                               unique_long_n, counted=True))))
     if "reference_ops" in want:
-        out.append(("reference_ops", timed(make_step(ref, R.contrast_loss, lambda t: torch.unique(t.long()), hoist=False))))
+        out.append(("reference_ops", timed(make_step(ref, R.contrast_loss, lambda t, n: torch.unique(t.long()), hoist=False))))
     for name, ms in out:
         print(json.dumps({"variant": name, "ms_per_step": round(ms, 3), "users": nu,
                           "items": ni, "edges": len(u), "d": args.dim, "layers": args.layers,

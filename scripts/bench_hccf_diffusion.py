@@ -115,7 +115,7 @@ def main():
             ue, ie, gcn, hyp = fwd(keep)
             if graph:  # HCCF_diffusion(hgd_graph=True)'s train_step
                 bpr, anc, pos = bpr_loss_rows(ue, ie, uid, pid, nid)
-                (un, uc), (pn, pc) = unique_long_n(anc), unique_long_n(pos)
+                (un, uc), (pn, pc) = unique_long_n(anc, nu), unique_long_n(pos, ni)
                 ssl = 0
                 for layer in range(L):
                     ssl = ssl + contrast_loss_pair(gcn[layer].detach(), hyp[layer], nu, un, pn,

@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--dim", type=int, default=64)
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--inner", type=int, default=20)
+    ap.add_argument("--cases", nargs="*", default=None,
+                    help="only these case names (e.g. fwd_hgd bwd_weight_hgd), for profiling")
     args = ap.parse_args()
     import torch
 
@@ -86,6 +88,8 @@ def main():
         }
         algo = {"fwd": 2 * n * d * 4, "fwd_drop": 2 * n * d * 4, "fwd_drop_res": 4 * n * d * 4, "bwd_data": 3 * n * d * 4, "bwd_weight": 2 * n * d * 4}
         for name, fn in cases.items():
+            if args.cases and name not in args.cases:
+                continue
             us = timed(fn)
             kind = name.rsplit("_", 1)[0]
             print(json.dumps({"case": name, "rows": n, "d": d, "us": round(us, 2),

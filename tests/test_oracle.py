@@ -222,8 +222,9 @@ def test_ranking_evaluation_known_answer():
 
 def test_dropout_keep_mask_restatement():
     """oracle.dropout_keep_mask (the library dropout's RNG, hgd_dropout_apply): the numpy form
-    equals a scalar Python restatement of the two lowbias32 rounds, and keeps about keep·n
-    elements; successive seeds give uncorrelated masks."""
+    equals a scalar Python restatement of the grouped draw (two lowbias32 rounds per group of
+    four elements, a third for the second pair of 16-bit halves), keeps about keep·n elements;
+    successive seeds give uncorrelated masks."""
     import numpy as np
     from oracle import hgd_oracle as O
     M = 0xFFFFFFFF
@@ -236,11 +237,16 @@ def test_dropout_keep_mask_restatement():
         return x ^ (x >> 16)
 
     seed, keep = 0x123456789ABCDEF, 0.7
-    got = O.dropout_keep_mask(seed, 300, keep)
-    for i in range(300):
-        h = lb(lb((i + (seed & M)) & M) ^ (seed >> 32))
-        u = np.float32(h >> 8) * np.float32(1 / 16777216)
-        assert got[i] == (np.floor(u + np.float32(keep)) != 0)
+    thr = int(np.float32(keep) * np.float32(65536.0) + np.float32(0.5))
+    assert thr == 45875
+    got = O.dropout_keep_mask(seed, 301, keep)
+    assert got.shape == (301,)
+    for i in range(301):
+        h1 = lb(lb(((i >> 2) + (seed & M)) & M) ^ (seed >> 32))
+        h2 = lb(h1 ^ 0x9E3779B9)
+        half = [h1 & 0xFFFF, h1 >> 16, h2 & 0xFFFF, h2 >> 16][i & 3]
+        assert got[i] == (half < thr)
+    assert O.dropout_keep_mask(seed, 1000, 1.0).all()
     a = O.dropout_keep_mask(7, 1_000_000, 0.5)
     b = O.dropout_keep_mask(8, 1_000_000, 0.5)
     assert abs(a.mean() - 0.5) < 0.003
