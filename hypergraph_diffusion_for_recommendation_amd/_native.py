@@ -359,6 +359,10 @@ _SIGNATURES = {
     "hgd_p2p_set_timeout": (c_i32, [c_void_p, ctypes.c_double]),
     "hgd_p2p_allreduce": (c_i32, [c_void_p, c_i32, c_i64, c_void_p, c_void_p]),
     "hgd_p2p_check": (c_i32, [c_void_p]),
+    "hgd_p2p_block_range": (c_i32, [c_i64, c_i32, c_i32, ctypes.POINTER(c_i64),
+                                    ctypes.POINTER(c_i64)]),
+    "hgd_p2p_gather_index": (c_i32, [c_i64, c_i32, c_i32, c_i64, ctypes.POINTER(c_i64),
+                                     ctypes.POINTER(c_i32)]),
     "hgd_incidence_globalize_columns": (c_i32, [c_void_p, c_void_p, c_void_p]),
     "hgd_conv2hop_workspace_size": (c_size, [c_void_p, c_i32, c_i32]),
     "hgd_conv2hop_forward": (c_i32, [c_void_p, c_i32, c_i32, c_i32, c_void_p, c_i64, c_i32,
@@ -391,10 +395,11 @@ def load() -> ctypes.CDLL:
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        # optional process-wide tuning overrides (hgd_set_tuning keys 1 .. 6)
+        # optional process-wide tuning overrides (hgd_set_tuning keys 1 .. 8)
         for key, env in ((1, "HGD_SPMM_UNROLL"), (2, "HGD_SPMM_POLICY"),
                          (3, "HGD_SPMM_PASS_COLS"), (4, "HGD_ROWGEMM_BLOCKS"),
-                         (5, "HGD_SPLITK_ROWS"), (6, "HGD_GEMM_EXACT")):
+                         (5, "HGD_SPLITK_ROWS"), (6, "HGD_GEMM_EXACT"),
+                         (7, "HGD_X3_COLS"), (8, "HGD_X3_SPLITK")):
             if os.environ.get(env):
                 st = lib.hgd_set_tuning(key, int(os.environ[env]))
                 if st != HGD_OK:

@@ -75,5 +75,10 @@ void set_row_gemm_max_blocks(int blocks);
 void set_splitk_rows(int rows);
 // HGD_TUNE_GEMM_EXACT (linear.hip): 1 = the exact f32-MFMA products only (no split-bf16).
 void set_gemm_exact(int exact);
+// HGD_TUNE_X3_COLS (linear.hip): column-slice width of the split-bf16 row GEMM (0, 64 or 128).
+void set_x3_cols(int cols);
+// HGD_TUNE_X3_SPLITK (linear.hip): 0 = the f32-MFMA split-K weight gradient even when split-bf16
+// products are on.
+void set_x3_splitk(int on);
 
 }  // namespace hgd

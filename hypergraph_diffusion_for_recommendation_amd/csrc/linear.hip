@@ -477,14 +477,17 @@ __device__ __forceinline__ f32x4 mfma_x3(const bf16x8& w0, const bf16x8& w1, con
   return mfma_bf16(w0, x0, acc);
 }
 
-constexpr int kX3Threads = 512;  // 8 waves: two per SIMD even when W's planes fill the LDS
-constexpr int kX3SliceCols = 128;
+// Column slices of 16·NT columns: 128 (NT = 8, 512-thread workgroups: two waves per SIMD with
+// W's 96 KB of planes filling the LDS) or 64 (NT = 4, 256 threads, 48 KB of planes: several
+// workgroups per CU; the second slice's A reads hit the XCD's L2, row_block_of). HGD_TUNE_X3_COLS.
+int g_x3_cols = 0;  // 0: default
+int g_x3_splitk = 1;  // HGD_TUNE_X3_SPLITK: the split-bf16 weight-gradient kernel (0: f32 MFMA)
 
 // NT: 16-column tiles of a ≤ 128-column slice (1, 2, 4 or 8). Tiles past the live nt (N not a
 // multiple of 16·NT) are staged as zeros and computed like the others — only their stores are
 // skipped — so the MFMA stream has no branches; binarized rows likewise run all six products.
-template <int KQ, int NT, bool MASK>
-__global__ __launch_bounds__(kX3Threads) void k_row_gemm_x3(RowGemmGroup grp) {
+template <int KQ, int NT, bool MASK, int THREADS>
+__global__ __launch_bounds__(THREADS) void k_row_gemm_x3(RowGemmGroup grp) {
   extern __shared__ __attribute__((aligned(16))) char x3_smem[];
   bf16x8* sW = reinterpret_cast<bf16x8*>(x3_smem);  // [3][NT][KQ][64]
   float* sBias = reinterpret_cast<float*>(sW + 3 * NT * KQ * 64);  // [NT·16]
@@ -494,12 +497,12 @@ __global__ __launch_bounds__(kX3Threads) void k_row_gemm_x3(RowGemmGroup grp) {
   const RowGemm p = second ? grp.p[1] : grp.p[0];  // a copy: its fields live in registers
   const int bx = bxg - (second ? grp.nb0 : 0);
   const int nbx = grp.count > 1 ? (second ? grp.nbt - grp.nb0 : grp.nb0) : grp.nbt;
-  constexpr int WAVES = kX3Threads / 64;
+  constexpr int WAVES = THREADS / 64;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int i16 = lane & 15;
   const int g = lane >> 4;
-  const int n0 = ys * kX3SliceCols;
+  const int n0 = ys * 16 * NT;
   const int nt = min(NT, (p.N - n0) / 16);
   const int64_t tiles = (p.rows + 15) / 16;
   const int64_t stride = static_cast<int64_t>(nbx) * WAVES;
@@ -532,11 +535,11 @@ __global__ __launch_bounds__(kX3Threads) void k_row_gemm_x3(RowGemmGroup grp) {
   // loads first (in flight together), then the splits and the LDS stores
   {
     constexpr int FRAGS = NT * KQ * 64;
-    constexpr int FR = (FRAGS + kX3Threads - 1) / kX3Threads;
+    constexpr int FR = (FRAGS + THREADS - 1) / THREADS;
     float v[FR][8];
 #pragma unroll
     for (int r = 0; r < FR; ++r) {
-      const int f = threadIdx.x + kX3Threads * r;
+      const int f = threadIdx.x + THREADS * r;
       const int L = f & 63, q = (f >> 6) % KQ, t = (f >> 6) / KQ;
       const int gg = L >> 4;
       const bool live = f < FRAGS && t < nt;
@@ -552,7 +555,7 @@ __global__ __launch_bounds__(kX3Threads) void k_row_gemm_x3(RowGemmGroup grp) {
     }
 #pragma unroll
     for (int r = 0; r < FR; ++r) {
-      const int f = threadIdx.x + kX3Threads * r;
+      const int f = threadIdx.x + THREADS * r;
       if (f < FRAGS) {
         const int L = f & 63, q = (f >> 6) % KQ, t = (f >> 6) / KQ;
         bf16x8 h, md, lo;
@@ -563,7 +566,7 @@ __global__ __launch_bounds__(kX3Threads) void k_row_gemm_x3(RowGemmGroup grp) {
       }
     }
   }
-  for (int c = threadIdx.x; c < NT * 16; c += kX3Threads)
+  for (int c = threadIdx.x; c < NT * 16; c += THREADS)
     sBias[c] = (p.bias && c < nt * 16) ? p.bias[n0 + c] : 0.f;
   __syncthreads();
   if (tile >= tiles) return;  // after the block's barrier
@@ -1013,7 +1016,8 @@ constexpr size_t x3_lds_bytes(int KQ, int NT) {
 // proportion to their rows; column slices XCD-paired as in row_block_of.
 template <int KQ, int NT, bool MASK>
 hgd_status launch_x3(RowGemmGroup g, hipStream_t st, const char* fn) {
-  const void* kern = reinterpret_cast<const void*>(&k_row_gemm_x3<KQ, NT, MASK>);
+  constexpr int kX3Threads = NT == 8 ? 512 : 256;
+  const void* kern = reinterpret_cast<const void*>(&k_row_gemm_x3<KQ, NT, MASK, kX3Threads>);
   constexpr size_t lds = x3_lds_bytes(KQ, NT);
   static int resident = 0;
   if (resident == 0) {
@@ -1032,7 +1036,7 @@ hgd_status launch_x3(RowGemmGroup g, hipStream_t st, const char* fn) {
     want[i] = (g.p[i].rows + kRowsPerBlock - 1) / kRowsPerBlock;
     total += want[i];
   }
-  g.ny = (g.p[0].N + kX3SliceCols - 1) / kX3SliceCols;
+  g.ny = (g.p[0].N + 16 * NT - 1) / (16 * NT);
   const int64_t cap = std::max<int64_t>(1, resident / g.ny);
   int64_t bx[2] = {0, 0};
   for (int i = 0; i < g.count; ++i) {
@@ -1042,7 +1046,8 @@ hgd_status launch_x3(RowGemmGroup g, hipStream_t st, const char* fn) {
   g.nb0 = static_cast<int32_t>(bx[0]);
   g.nbt = static_cast<int32_t>(bx[0] + bx[1]);
   const dim3 grid(static_cast<unsigned>(g.nbt) * static_cast<unsigned>(g.ny));
-  hipLaunchKernelGGL((k_row_gemm_x3<KQ, NT, MASK>), grid, dim3(kX3Threads), lds, st, g);
+  hipLaunchKernelGGL((k_row_gemm_x3<KQ, NT, MASK, kX3Threads>), grid, dim3(kX3Threads), lds, st,
+                     g);
   return check_launch(fn);
 }
 
@@ -1056,7 +1061,7 @@ hgd_status launch_x3_nt(const RowGemmGroup& g, hipStream_t st, const char* fn) {
   const int N = g.p[0].N;
   if (N <= 16) return launch_x3_mask<KQ, 1>(g, st, fn);
   if (N <= 32) return launch_x3_mask<KQ, 2>(g, st, fn);
-  if (N <= 64) return launch_x3_mask<KQ, 4>(g, st, fn);
+  if (N <= 64 || g_x3_cols == 64) return launch_x3_mask<KQ, 4>(g, st, fn);
   return launch_x3_mask<KQ, 8>(g, st, fn);
 }
 
@@ -1156,7 +1161,7 @@ void tn_splits(const hgd_gemm_tn_desc* d, int count, int64_t* S, int64_t* per) {
   }
   // workgroups per slice and the resident budget: 64 × 64 tiles of 256 threads (f32 MFMA), or
   // groups of up to eight 64 × 32 tiles of 512 threads (split-bf16)
-  const bool x3 = !g_gemm_exact;
+  const bool x3 = !g_gemm_exact && g_x3_splitk;
   auto wg_per_slice = [&](const hgd_gemm_tn_desc& e) -> int64_t {
     if (!x3) return static_cast<int64_t>((e.M + 63) / 64) * ((e.N + 63) / 64);
     const int t = ((e.M + 63) / 64) * ((e.N + 31) / 32);
@@ -1245,6 +1250,8 @@ void set_row_gemm_max_blocks(int blocks) {
 }
 void set_splitk_rows(int rows) { g_splitk_rows = rows > 0 ? rows : 0; }
 void set_gemm_exact(int exact) { g_gemm_exact = exact != 0; }
+void set_x3_cols(int cols) { g_x3_cols = cols; }
+void set_x3_splitk(int on) { g_x3_splitk = on != 0; }
 }  // namespace hgd
 
 extern "C" hgd_status hgd_linear_forward(const float* X, int64_t ldx, int64_t n_rows,
@@ -1396,7 +1403,7 @@ extern "C" hgd_status hgd_gemm_tn(const hgd_gemm_tn_desc* descs, int32_t count, 
     }
   const dim3 grid(static_cast<unsigned>(Stot), static_cast<unsigned>((g.p[0].M + 63) / 64),
                   static_cast<unsigned>((g.p[0].N + 63) / 64));
-  if (!g_gemm_exact) {
+  if (!g_gemm_exact && g_x3_splitk) {
     const int tiles = ((g.p[0].M + 63) / 64) * ((g.p[0].N + 31) / 32);
     const dim3 gx(static_cast<unsigned>(Stot),
                   static_cast<unsigned>(tiles / x3_tiles_per_wg(tiles)));

@@ -68,10 +68,26 @@ __global__ void k_signal_wait(uint64_t* const* flags, int kind, int rank, int nr
   }
 }
 
+// The block arithmetic of an exchange (host and device share it; hgd_p2p_block_range and
+// hgd_p2p_gather_index expose it to the CPU tests): rank q reduces float4s [lo(q), hi(q)), the
+// last blocks may be short or empty; gather element i < n4 - |own block| is float4 j of rank
+// q's block, the own block skipped.
 struct Blocks {
   int64_t n4, b4;  // float4s in the exchange, float4s per rank block
-  __device__ int64_t lo(int q) const { int64_t v = q * b4; return v < n4 ? v : n4; }
-  __device__ int64_t hi(int q) const { int64_t v = (q + 1) * b4; return v < n4 ? v : n4; }
+  __host__ __device__ static Blocks of(int64_t count, int nranks) {
+    Blocks b;
+    b.n4 = count / 4;
+    b.b4 = (b.n4 + nranks - 1) / nranks;
+    return b;
+  }
+  __host__ __device__ int64_t lo(int q) const { int64_t v = q * b4; return v < n4 ? v : n4; }
+  __host__ __device__ int64_t hi(int q) const { int64_t v = (q + 1) * b4; return v < n4 ? v : n4; }
+  __host__ __device__ int64_t gather_count(int rank) const { return n4 - (hi(rank) - lo(rank)); }
+  __host__ __device__ int64_t gather_j(int rank, int64_t i) const {
+    const int64_t own_lo = lo(rank), own_len = hi(rank) - own_lo;
+    return i < own_lo ? i : i + own_len;
+  }
+  __host__ __device__ int gather_owner(int64_t j) const { return static_cast<int>(j / b4); }
 };
 
 // out[block r] = reduced_r[block r] = Σ_q send_q[block r], q ascending
@@ -104,14 +120,12 @@ __global__ void k_reduce(char* const* base, size_t send_off, size_t red_off, Blo
 __global__ void k_gather(char* const* base, size_t red_off, Blocks bl, int rank,
                          float4* __restrict__ out, const int* err) {
   if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
-  const int64_t own_lo = bl.lo(rank), own_len = bl.hi(rank) - own_lo;
-  const int64_t n = bl.n4 - own_len;
+  const int64_t n = bl.gather_count(rank);
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
        i += stride) {
-    const int64_t j = i < own_lo ? i : i + own_len;
-    const int q = static_cast<int>(j / bl.b4);
-    out[j] = reinterpret_cast<const float4*>(base[q] + red_off)[j];
+    const int64_t j = bl.gather_j(rank, i);
+    out[j] = reinterpret_cast<const float4*>(base[bl.gather_owner(j)] + red_off)[j];
   }
 }
 
@@ -269,9 +283,7 @@ extern "C" hgd_status hgd_p2p_allreduce(hgd_p2p* h, int32_t slot, int64_t count,
   hipStream_t st = hgd::as_stream(stream);
   const uint64_t seq = ++h->seq;
   const uint64_t tmo = static_cast<uint64_t>(h->timeout_s * static_cast<double>(h->ticks_per_s));
-  Blocks bl;
-  bl.n4 = count / 4;
-  bl.b4 = (bl.n4 + h->nranks - 1) / h->nranks;
+  const Blocks bl = Blocks::of(count, h->nranks);
   float4* o = reinterpret_cast<float4*>(out);
   hipLaunchKernelGGL(k_signal_wait, dim3(1), dim3(64), 0, st, h->d_flags, kSent, h->rank,
                      h->nranks, seq, tmo, h->err);
@@ -284,8 +296,7 @@ extern "C" hgd_status hgd_p2p_allreduce(hgd_p2p* h, int32_t slot, int64_t count,
     hipLaunchKernelGGL(k_signal_wait, dim3(1), dim3(64), 0, st, h->d_flags, kReduced, h->rank,
                        h->nranks, seq, tmo, h->err);
     if (hgd_status r = hgd::check_launch("hgd_p2p_allreduce (signal)"); r != HGD_OK) return r;
-    const int64_t rest = bl.n4 - (std::min(bl.n4, (h->rank + 1) * bl.b4) -
-                                  std::min(bl.n4, h->rank * bl.b4));
+    const int64_t rest = bl.gather_count(h->rank);
     if (rest > 0) {
       const unsigned g2 = std::min<unsigned>(2048, hgd::grid_for(rest));
       hipLaunchKernelGGL(k_gather, dim3(g2), dim3(hgd::kBlock), 0, st, h->d_bases,
@@ -309,3 +320,28 @@ extern "C" hgd_status hgd_p2p_check(hgd_p2p* h) {
 }
 
 extern "C" void hgd_p2p_destroy(hgd_p2p* h) { delete h; }
+
+extern "C" hgd_status hgd_p2p_block_range(int64_t count, int32_t nranks, int32_t q, int64_t* lo,
+                                          int64_t* hi) {
+  hgd::clear_error();
+  HGD_REQUIRE(count >= 0 && count % 4 == 0 && nranks >= 1 && nranks <= kMaxRanks && q >= 0 &&
+                  q < nranks && lo && hi,
+              "hgd_p2p_block_range: bad arguments");
+  const Blocks b = Blocks::of(count, nranks);
+  *lo = 4 * b.lo(q);
+  *hi = 4 * b.hi(q);
+  return HGD_OK;
+}
+
+extern "C" hgd_status hgd_p2p_gather_index(int64_t count, int32_t nranks, int32_t rank,
+                                           int64_t i, int64_t* j, int32_t* owner) {
+  hgd::clear_error();
+  HGD_REQUIRE(count >= 0 && count % 4 == 0 && nranks >= 1 && nranks <= kMaxRanks && rank >= 0 &&
+                  rank < nranks && j && owner,
+              "hgd_p2p_gather_index: bad arguments");
+  const Blocks b = Blocks::of(count, nranks);
+  HGD_REQUIRE(i >= 0 && i < b.gather_count(rank), "hgd_p2p_gather_index: i out of range");
+  *j = b.gather_j(rank, i);
+  *owner = b.gather_owner(*j);
+  return HGD_OK;
+}

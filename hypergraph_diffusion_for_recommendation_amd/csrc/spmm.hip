@@ -756,6 +756,15 @@ extern "C" hgd_status hgd_set_tuning(int32_t key, int32_t value) {
       HGD_REQUIRE(value == 0 || value == 1, "hgd_set_tuning: gemm exact must be 0 or 1");
       set_gemm_exact(value);
       return HGD_OK;
+    case HGD_TUNE_X3_COLS:
+      HGD_REQUIRE(value == 0 || value == 64 || value == 128,
+                  "hgd_set_tuning: x3 columns must be 0 (default), 64 or 128");
+      set_x3_cols(value);
+      return HGD_OK;
+    case HGD_TUNE_X3_SPLITK:
+      HGD_REQUIRE(value == 0 || value == 1, "hgd_set_tuning: x3 split-K must be 0 or 1");
+      set_x3_splitk(value);
+      return HGD_OK;
     default:
       return fail(HGD_ERR_INVALID_ARG, "hgd_set_tuning: unknown key %d", key);
   }

@@ -73,14 +73,20 @@ typedef enum hgd_epilogue {
  *                         reduction (split-K) eligible run as split-bf16 MFMAs (every f32
  *                         operand cut exactly into three bf16 terms, six products: error
  *                         ≈ 1e-7·Σ|a·b| like the f32 fmaf chain, not bitwise equal to it);
- *                         1 = the exact f32-input MFMA kernels only (bitwise k-ordered fmaf) */
+ *                         1 = the exact f32-input MFMA kernels only (bitwise k-ordered fmaf)
+ *   HGD_TUNE_X3_COLS:     output columns per workgroup of the split-bf16 row GEMM (64 or 128;
+ *                         0 = default)
+ *   HGD_TUNE_X3_SPLITK:   1 (default) = the split-bf16 split-K weight gradient when
+ *                         HGD_TUNE_GEMM_EXACT is 0; 0 = the f32-MFMA split-K kernel */
 typedef enum hgd_tune_key {
   HGD_TUNE_SPMM_UNROLL = 1,
   HGD_TUNE_SPMM_POLICY = 2,
   HGD_TUNE_SPMM_PASS_COLS = 3,
   HGD_TUNE_ROWGEMM_BLOCKS = 4,
   HGD_TUNE_SPLITK_ROWS = 5,
-  HGD_TUNE_GEMM_EXACT = 6
+  HGD_TUNE_GEMM_EXACT = 6,
+  HGD_TUNE_X3_COLS = 7,
+  HGD_TUNE_X3_SPLITK = 8
 } hgd_tune_key;
 hgd_status hgd_set_tuning(int32_t key, int32_t value);
 
@@ -847,6 +853,13 @@ hgd_status hgd_p2p_allreduce(hgd_p2p* p2p, int32_t slot, int64_t count, float* o
                              void* stream);
 /* Synchronous: HGD_OK, or HGD_ERR_HIP if any exchange timed out. */
 hgd_status hgd_p2p_check(hgd_p2p* p2p);
+/* The block arithmetic of hgd_p2p_allreduce (host only, no device calls): rank q reduces floats
+ * [*lo, *hi) of a `count`-float exchange over `nranks` ranks; gather step i of `rank` copies
+ * float4 *j from rank *owner's reduced block (its own block is skipped). */
+hgd_status hgd_p2p_block_range(int64_t count, int32_t nranks, int32_t q, int64_t* lo,
+                               int64_t* hi);
+hgd_status hgd_p2p_gather_index(int64_t count, int32_t nranks, int32_t rank, int64_t i,
+                                int64_t* j, int32_t* owner);
 
 /* The two-hop conv over the object, Y = epi(P·A·Q·Aᵀ·R·X) with P, R row scales and Q a column
  * scale (hgd_scale each):

@@ -49,7 +49,7 @@ def toy_hgconv2():
 
 
 def interactions(rng, n_users, n_items, n):
-    """A training list in file order (with repeats), remapped like data/ui_graph.py:107-125."""
+    """A training list in file order (with repeats), remapped like data/ui_graph.py:43-68."""
     raw_u = rng.integers(1000, 1000 + n_users, size=n)
     raw_i = rng.integers(50, 50 + n_items, size=n)
     user, item = O.remap_ids(zip(raw_u.tolist(), raw_i.tolist()))

@@ -56,7 +56,8 @@ def test_product_path_has_no_cpu_fallback():
 
 def test_masked_row_gemm_rejects_forward_epilogues():
     """Argument validation only (returns before any HIP call): the masked (backward-data) form
-    of hgd_gemm_rows takes none of the forward epilogues its kernel no longer carries."""
+    of hgd_gemm_rows takes none of the forward epilogues its kernel no longer carries (the
+    output dropout is allowed: it is the backward of an input dropout fused into the forward)."""
     import ctypes
     from hypergraph_diffusion_for_recommendation_amd import _native
     lib = _native.load()
