@@ -564,15 +564,22 @@ class _ShardedPlugin:
     def _rows(self, table_local: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
         """table[ids] for GLOBAL user ids (negative ids wrap, as torch indexing) of a user table
         sharded by rows: each owner contributes its rows, the rest zeros, summed over ranks."""
+        return self._rows_multi([table_local], ids)[0]
+
+    def _rows_multi(self, tables_local, ids: torch.Tensor):
+        """``[t[ids] for t in tables_local]`` for several user tables sharded alike, with ONE
+        (differentiable) all-reduce of the stacked owner parts instead of one per table."""
         n = self.data.n_users
+        d = tables_local[0].shape[1]
         if self.u1 == self.u0:  # a rank without users contributes nothing
-            return self._all_reduce_sum(torch.zeros(ids.numel(), table_local.shape[1],
-                                                    device=ids.device))
-        g = torch.where(ids < 0, ids + n, ids)
-        own = (g >= self.u0) & (g < self.u1)
-        loc = (g - self.u0).clamp(0, max(self.u1 - self.u0 - 1, 0))
-        part = torch.where(own[:, None], table_local[loc], torch.zeros((), device=ids.device))
-        return self._all_reduce_sum(part)
+            part = torch.zeros(len(tables_local) * ids.numel(), d, device=ids.device)
+        else:
+            g = torch.where(ids < 0, ids + n, ids)
+            own = (g >= self.u0) & (g < self.u1)
+            loc = (g - self.u0).clamp(0, max(self.u1 - self.u0 - 1, 0))
+            zero = torch.zeros((), device=ids.device)
+            part = torch.cat([torch.where(own[:, None], t[loc], zero) for t in tables_local], 0)
+        return list(self._all_reduce_sum(part).split(ids.numel(), 0))
 
     def _full_user_table(self, user_local: torch.Tensor) -> torch.Tensor:
         full = torch.zeros(self.data.n_users, user_local.shape[1], device=user_local.device)
@@ -656,11 +663,17 @@ class HCCF_sharded(_ShardedPlugin, HCCF):
         bprLoss = bpr_loss(anchor_emb, pos_emb, neg_emb)
         u_nodes, p_nodes = unique_long(anchor_emb), unique_long(pos_emb)
         k = torch.arange(u_nodes.numel(), device=u_nodes.device)
+        # the InfoNCE user rows of every layer (both tables) in ONE all-reduce: 2 exchanges per
+        # step (the anchor rows, then these) instead of 1 + 2L. Not one: the node list is
+        # torch.unique(anchor_emb.long()) (HCCF.py:65), which needs the gathered anchor rows
+        e1s = [gcnEmbedsLst[i].detach() for i in range(self.nLayers)]
+        e2s = list(hyperEmbedsLst[:self.nLayers])
+        rows = self._rows_multi([e[:nl] for e in e1s] + [e[:nl] for e in e2s], u_nodes)
+        L = self.nLayers
         sslLoss = 0
-        for i in range(self.nLayers):
-            e1, e2 = gcnEmbedsLst[i].detach(), hyperEmbedsLst[i]
-            sslLoss += contrast_loss(self._rows(e1[:nl], u_nodes), self._rows(e2[:nl], u_nodes),
-                                     k, self.temp) \
+        for i in range(L):
+            e1, e2 = e1s[i], e2s[i]
+            sslLoss += contrast_loss(rows[i], rows[L + i], k, self.temp) \
                 + contrast_loss(e1[nl:], e2[nl:], p_nodes, self.temp)
         batch_loss = bprLoss + sslLoss * self.ss_rate
         self.optimizer.zero_grad()

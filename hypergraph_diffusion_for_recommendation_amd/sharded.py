@@ -853,3 +853,157 @@ def sharded_dense_two_hop(H_local: torch.Tensor, X_local: torch.Tensor,
         from .functional import dense_two_hop
         return dense_two_hop(H_local, X_local)
     return _ShardedDenseTwoHop.apply(H_local, X_local, group)
+
+
+class _ShardedHCCFLayers(torch.autograd.Function):
+    """HCCF's layer loop (model/graph/HCCF.py:173-191) on user-row shards as ONE op — the sharded
+    counterpart of functional._HCCFLayers, on the local layout ``[h_u (local users); h_i (items,
+    replicated)]``. Per layer k, forward:
+
+    * hypergraph pair: ``M_u = Σ_ranks H_uᵀ·h_u`` (grouped split-K with the replicated
+      ``M_i = H_iᵀ·h_i``, then an all-reduce of the [K, d] user part), ``Hh = [H_u·M_u; H_i·M_i]``;
+    * GCN hop over the edge-dropped shard: the user rows ``B_g·h_i`` are complete locally, so
+      their store writes ``gcn_k`` (act_out) and ``h_{k+1} = gcn_k + Hh`` (res1) as on one GPU;
+      the item rows ``Σ_g C_g·h_u`` are written straight into ``gcn_k`` in chunks, each chunk
+      all-reduced behind its kernel, and ``h_{k+1}`` of the items is one add after the exchange
+      (fused into the store too on a single rank);
+    * ``sum(hidden)`` is one slice-sum pass.
+
+    Backward, layer k (item-row gradients are per-rank partials, as everywhere in this module):
+    ``dM_u`` all-reduced, the grouped ``H·dM`` store, then the two transposed block hops whose
+    stores add it and dE and write the next layer's ``dhgnn`` (sum_out); the item part of
+    ``dgcn`` is all-reduced while the into-items hop ``B_gᵀ·dgcn_u`` runs. Exchanges per layer:
+    forward [K, d] + [I, d], backward [K, d] + [I, d] — the same as the per-layer module graph,
+    with none of its adds and accumulations."""
+
+    @staticmethod
+    def forward(ctx, shs, group, user_local, item, *Hs):
+        from .functional import _gemm_rows, _gemm_tn_pair, _res_epilogue, _rows_desc
+        L = len(shs)
+        dev = user_local.device
+        nl, I = user_local.shape[0], item.shape[0]
+        N, d = nl + I, user_local.shape[1]
+        K = Hs[0].shape[1]
+        world = dist.get_world_size(group) if dist.is_initialized() else 1
+        f = dict(dtype=torch.float32, device=dev)
+        hid = torch.empty((L + 1, N, d), **f)
+        torch.cat([user_local, item], 0, out=hid[0])
+        Hs = [H.contiguous() for H in Hs]
+        gcn, hgnn, Ms = [], [], []
+        for k in range(L):
+            sh = shs[k]
+            H_u, H_i = Hs[2 * k], Hs[2 * k + 1]
+            h = hid[k]
+            M_u, M_i = _gemm_tn_pair([(H_u, h[:nl]), (H_i, h[nl:])], dev)
+            if world > 1:
+                dist.all_reduce(M_u, group=group)
+            Hh = torch.empty((N, d), **f)
+            _gemm_rows([_rows_desc(H_u, M_u, d, 1, K, d, Hh[:nl]),
+                        _rows_desc(H_i, M_i, d, 1, K, d, Hh[nl:])], dev)
+            G = torch.empty((N, d), **f)
+            out = hid[k + 1]
+            works: List = []
+            if world > 1:
+                for a, b in sh.bounds:  # item rows: partial sums, chunk by chunk into G
+                    if b > a:
+                        spmm_csr(sh.C.csr, h[:nl], val=sh.C.val, out=G[nl:], row_begin=a,
+                                 row_end=b)
+                    works.append(dist.all_reduce(G[nl:][a:b], group=group, async_op=True))
+            else:
+                spmm_csr(sh.C.csr, h[:nl], val=sh.C.val,
+                         ex=_res_epilogue(Hh[nl:], act_out=G[nl:]), out=out[nl:])
+            spmm_csr(sh.B.csr, h[nl:], val=sh.B.val, ex=_res_epilogue(Hh[:nl], act_out=G[:nl]),
+                     out=out[:nl])
+            for w in works:
+                w.wait()
+            if world > 1:
+                torch.add(G[nl:], Hh[nl:], out=out[nl:])
+            gcn.append(G)
+            hgnn.append(Hh)
+            Ms += [M_u, M_i]
+        E = torch.empty((N, d), **f)
+        nat.check(nat.load().hgd_sum_slices(hid.data_ptr(), L + 1, N * d, N * d, E.data_ptr(),
+                                            nat.stream_handle(dev)), "hgd_sum_slices")
+        ctx.shs, ctx.group, ctx.world, ctx.nl, ctx.L, ctx.K = shs, group, world, nl, L, K
+        ctx.save_for_backward(hid, *Hs, *Ms)
+        ctx.set_materialize_grads(False)
+        return (E, *gcn, *hgnn)
+
+    @staticmethod
+    def backward(ctx, dE, *grads):
+        from .functional import _gemm_rows, _gemm_tn_pair, _res_epilogue, _rows_desc
+        L, nl, K, world, group = ctx.L, ctx.nl, ctx.K, ctx.world, ctx.group
+        saved = ctx.saved_tensors
+        hid = saved[0]
+        Hs = saved[1:1 + 2 * L]
+        Ms = saved[1 + 2 * L:]
+        dgcn, dhgnn = grads[:L], grads[L:]
+        _, N, d = hid.shape
+        dev = hid.device
+        f = dict(dtype=torch.float32, device=dev)
+        if dE is not None:
+            dE = dE.contiguous()
+        dh = dE if dE is not None else torch.zeros((N, d), **f)
+        dHh = dh if dhgnn[L - 1] is None else dh + dhgnn[L - 1].contiguous()
+        want_emb = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
+        dHs = [None] * (2 * L)
+        for k in reversed(range(L)):
+            sh = ctx.shs[k]
+            H_u, H_i = Hs[2 * k], Hs[2 * k + 1]
+            M_u, M_i = Ms[2 * k], Ms[2 * k + 1]
+            h = hid[k]
+            dG = dh if dgcn[k] is None else dh + dgcn[k]
+            dG = dG.contiguous()
+            dM_u, dM_i = _gemm_tn_pair([(H_u, dHh[:nl]), (H_i, dHh[nl:])], dev)
+            if world > 1:  # M_u was all-reduced: its gradient is summed too
+                dist.all_reduce(dM_u, group=group)
+            if ctx.needs_input_grad[4 + 2 * k] or ctx.needs_input_grad[5 + 2 * k]:
+                dH_u, dH_i = torch.empty_like(H_u), torch.empty_like(H_i)
+                _gemm_rows([_rows_desc(dHh[:nl], M_u, 1, d, d, K, dH_u),
+                            _rows_desc(dHh[nl:], M_i, 1, d, d, K, dH_i)], dev)
+                _gemm_rows([_rows_desc(h[:nl], dM_u, 1, d, d, K, dH_u, accumulate=True),
+                            _rows_desc(h[nl:], dM_i, 1, d, d, K, dH_i, accumulate=True)], dev)
+                dHs[2 * k], dHs[2 * k + 1] = dH_u, dH_i
+            if k == 0 and not want_emb:
+                break
+            dh_new = torch.empty((N, d), **f)
+            _gemm_rows([_rows_desc(H_u, dM_u, d, 1, K, d, dh_new[:nl]),
+                        _rows_desc(H_i, dM_i, d, 1, K, d, dh_new[nl:])], dev)
+            nxt = dhgnn[k - 1].contiguous() if k > 0 and dhgnn[k - 1] is not None else None
+            dHh_new = torch.empty((N, d), **f) if nxt is not None else None
+
+            def ex(r0, r1):
+                return _res_epilogue(None if dE is None else dE[r0:r1], res2=dh_new[r0:r1],
+                                     sum_res=None if nxt is None else nxt[r0:r1],
+                                     sum_out=None if dHh_new is None else dHh_new[r0:r1])
+
+            dZi, work = dG[nl:], None
+            if world > 1:  # the items' gradient summed while the into-items hop runs
+                dZi = dZi.clone()
+                work = dist.all_reduce(dZi, group=group, async_op=True)
+            spmm_csr(sh.B.csc, dG[:nl], val=sh.B.val_t, ex=ex(nl, N), out=dh_new[nl:])
+            if work is not None:
+                work.wait()
+            spmm_csr(sh.C.csc, dZi, val=sh.C.val_t, ex=ex(0, nl), out=dh_new[:nl])
+            dh = dh_new
+            dHh = dHh_new if nxt is not None else dh_new
+        d_u = dh[:nl] if ctx.needs_input_grad[2] else None
+        d_i = dh[nl:] if ctx.needs_input_grad[3] else None
+        return (None, None, d_u, d_i, *dHs)
+
+
+def sharded_hccf_layers(shs, user_local: torch.Tensor, item: torch.Tensor, hypers_u, hypers_i,
+                        group=None):
+    """HCCF's propagation (HCCF.py:173-191) over per-layer edge-dropped shards ``shs``
+    (:class:`ShardedBipartite`) and per-layer dropped hypergraphs (user rows local, item rows
+    replicated): ``(sum(hidden), gcn_hidden, hgnn_hidden)`` on the local layout
+    (:class:`_ShardedHCCFLayers`)."""
+    L = len(shs)
+    for sh in shs:
+        if sh.n_local != user_local.shape[0] or sh.n_items != item.shape[0]:
+            raise ValueError("sharded_hccf_layers: shard shape does not match the tables")
+    Hs = []
+    for Hu, Hi in zip(hypers_u, hypers_i):
+        Hs += [Hu, Hi]
+    out = _ShardedHCCFLayers.apply(list(shs), group, user_local, item, *Hs)
+    return out[0], list(out[1:1 + L]), list(out[1 + L:])

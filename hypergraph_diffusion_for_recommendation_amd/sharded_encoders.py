@@ -29,10 +29,11 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .encoders import edhnn_config
-from .functional import dense_two_hop, fan, linear, sum_n
+from .functional import dense_two_hop, fan, hccf_layers_supported, linear, sum_n
 from .layers import EquivSetGNN, LayerNorm, input_norm_linear
 from .sharded import (ShardedBipartite, bipartite_hop, bipartite_hop_fused,  # noqa: F401
-                      shard_bounds, sharded_dense_two_hop, sharded_mean_two_hop)
+                      shard_bounds, sharded_dense_two_hop, sharded_hccf_layers,
+                      sharded_mean_two_hop)
 
 
 def _coo_tensor(mat, binary: bool = False):
@@ -124,6 +125,8 @@ class ShardedHCCFEncoder(nn.Module):
         })
         self.rep_gen, self.loc_gen = _rank_generators(self.device, seed, group)
         self.rep_drop = _SplitDropout(self.drop_rate, self.rep_gen, self.loc_gen)
+        # False: the per-layer module graph (bipartite hops, dense two-hops, torch adds)
+        self.fused_layers = True
 
     @torch.no_grad()
     def load_global(self, embedding_dict) -> None:
@@ -151,11 +154,22 @@ class ShardedHCCFEncoder(nn.Module):
     def forward(self, keep_rate=0.5):
         nl = self.n_local
         e = self.embedding_dict
+        hyper_uu = linear(e['user_emb'], e['user_w'].t())
+        hyper_ii = linear(e['item_emb'], e['item_w'].t())
+        if self.fused_layers and hccf_layers_supported(e['user_emb'], e['item_emb'], hyper_ii):
+            # the whole loop as one op (sharded.sharded_hccf_layers, the counterpart of the
+            # single-GPU encoder's hccf_layers); same draws in the same order as the loop below
+            shs, hus, his = [], [], []
+            for _ in range(self.n_layers):
+                shs.append(self._dropped(keep_rate))
+                hus.append(self.rep_drop(hyper_uu, nl))
+                his.append(self.rep_drop(hyper_ii, 0))
+            embeddings, gcn_hidden, hgnn_hidden = sharded_hccf_layers(
+                shs, e['user_emb'], e['item_emb'], hus, his, self.group)
+            return embeddings[:nl], embeddings[nl:], gcn_hidden, hgnn_hidden
         embeddings = torch.cat([e['user_emb'], e['item_emb']], 0)
         hidden = [embeddings]
         gcn_hidden, hgnn_hidden = [], []
-        hyper_uu = linear(e['user_emb'], e['user_w'].t())
-        hyper_ii = linear(e['item_emb'], e['item_w'].t())
         terms = []  # the sum(hidden) operands
         for _ in range(self.n_layers):
             # hidden[-1] feeds the hop, the learned-hypergraph pair and the layer sum: one n-ary

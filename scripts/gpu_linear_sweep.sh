@@ -7,7 +7,11 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/linsweep
 mkdir -p $O
 export TMPDIR=/tmp
-for cfg in "HGD_GEMM_EXACT=1" "HGD_X3_COLS=128" "HGD_X3_COLS=64" "HGD_X3_SPLITK=0"; do
+if [ "${SWEEP_TESTS:-1}" = 1 ]; then
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_linear.py tests/test_gpu_fused_dropout.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+  tail -1 $O/pytest.log
+fi
+for cfg in ${SWEEP_CFGS:-"HGD_GEMM_EXACT=1" "HGD_X3_COLS=0" "HGD_X3_COLS=128" "HGD_X3_SPLITK=0"}; do
   tag=$(echo $cfg | tr '=' '_')
   env $cfg timeout -k 10 120 python scripts/bench_linear.py --rows 144242 --dim 128 > $O/d128_$tag.jsonl 2>&1 || { cat $O/d128_$tag.jsonl; exit 1; }
   env $cfg timeout -k 10 120 python scripts/bench_linear.py --rows 69716 31668 --dim 64 > $O/d64_$tag.jsonl 2>&1 || { cat $O/d64_$tag.jsonl; exit 1; }

@@ -19,7 +19,7 @@ run() {  # name, time limit, bench args...
   local name=$1 lim=$2
   shift 2
   echo "[rehearsal] $name: bench.py $*"
-  timeout -k 10 "$lim" python bench.py --check --steps 2 --warmup 1 --no-cpu-baseline --pmc off \
+  timeout -k 10 "$lim" python bench.py --check --no-cpu-baseline --pmc off \
     "$@" > $O/$name.json 2> $O/$name.err || { echo "FAILED rc=$? $name"; tail -20 $O/$name.err; exit 1; }
   python - "$O/$name.json" <<'EOF'
 import json, sys
@@ -32,10 +32,15 @@ assert nnz == r["config"]["edges"] == 99_999_492 and r["check"]["ok"]
 EOF
   [ $? -eq 0 ] || exit 1
 }
-HGD_DIST_BACKEND=gloo run gloo_n4_d64 420 --gpus 4
-HGD_DIST_BACKEND=gloo run gloo_n8_d64 540 --gpus 8
-HGD_DIST_BACKEND=gloo run p2p_n4_d64 420 --gpus 4 --transport p2p
-HGD_DIST_BACKEND=gloo run p2p_n8_d64 540 --gpus 8 --transport p2p
-HGD_DIST_BACKEND=gloo run gloo_n4_d256 600 --gpus 4 --dim 256
-HGD_DIST_BACKEND=gloo run p2p_n8_d256 600 --gpus 8 --dim 256 --transport p2p
+# gloo stages each 256 MB all-reduce through host TCP: 21 s per step at N = 4 (run once:
+# profiles/r03_scale/bench_strong_4ranks_gloo_d64_check.json); N = 8 over gloo does not finish a
+# step within 9 minutes on one box, so the larger rehearsals use the peer transport (same sharding,
+# same check; gloo only for setup)
+STEPS="--steps ${REH_STEPS:-1} --warmup ${REH_WARMUP:-1}"
+for spec in ${REH_RUNS:-"p2p:4:64 p2p:8:64 p2p:4:256 p2p:8:256"}; do
+  IFS=: read tr n d <<< "$spec"
+  extra=""
+  [ "$tr" = p2p ] && extra="--transport p2p"
+  HGD_DIST_BACKEND=gloo run ${tr}_n${n}_d${d} 420 --gpus $n --dim $d $extra $STEPS
+done
 echo "[rehearsal] all ok"

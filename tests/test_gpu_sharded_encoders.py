@@ -57,11 +57,13 @@ def _worker(rank, world, port, which):
         data = _data()
         u0, u1 = SE.shard_bounds(U, world, rank)
         Gu, Gi_tot, Gi_mine = _grads(world, rank, dev)
-        if which == "hccf":
+        if which.startswith("hccf"):
             torch.manual_seed(0)
             ref = HCCFEncoder(HCCF_KW, data, device=dev)
             sh = SE.ShardedHCCFEncoder(HCCF_KW, data, u0, u1, device=dev, n_chunks=3,
                                        device_rng=False)
+            # "hccf": the layer loop as one op (sharded_hccf_layers); "hccf_module": per layer
+            sh.fused_layers = which == "hccf"
             sh.load_global(ref.embedding_dict)
             torch.manual_seed(123)
             ue, ie, _, _ = ref(keep_rate=0.7)
@@ -119,7 +121,7 @@ def _free_port():
 
 
 @pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("which", ["hccf", "local_aware"])
+@pytest.mark.parametrize("which", ["hccf", "hccf_module", "local_aware"])
 def test_sharded_encoder_matches_single_gpu(dev, world, which):
     mp.start_processes(_worker, args=(world, _free_port(), which), nprocs=world, join=True,
                        start_method="spawn")
