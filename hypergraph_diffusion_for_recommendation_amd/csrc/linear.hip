@@ -733,7 +733,9 @@ struct X3S {
   static constexpr int D = F >= 8 ? 1 : 8 / F;
   static constexpr int LPR = K / 4;                          // lanes holding one row
   static constexpr size_t PLANE_BYTES = static_cast<size_t>(RT) * KQ * 1024;  // one plane, one stage
-  static constexpr size_t LDS = 2 * 3 * PLANE_BYTES + 2 * R * 4;
+  static constexpr size_t PLANES_LDS = 2 * 3 * PLANE_BYTES + 2 * R * 4;
+  static constexpr size_t W_LDS = static_cast<size_t>(K) * (16 * CG * NTW + 4) * 4;  // staging
+  static constexpr size_t LDS = PLANES_LDS > W_LDS ? PLANES_LDS : W_LDS;
 };
 
 template <int KQ, int NTW, int CG, int RT, bool MASK, int EPI>
@@ -759,68 +761,8 @@ __global__ __launch_bounds__(64 * CG * RT) void k_row_gemm_x3s(RowGemmGroup grp)
   const int nt = min(NTS, (p.N - n0) / 16);  // live tiles of this slice
   const int64_t stages = (p.rows + C::R - 1) / C::R;
 
-  // ---- this wave's W fragments: tile t = cg·NTW + tw, k step q, planes 0..2 (registers). All
-  // loads of a kind are issued before any is used (a load under a runtime condition inside the
-  // element loop made hipcc wait vmcnt(0) after each one: 64 serial round trips)
-  bf16x8 wf[NTW][KQ][3];
-  f32x4 bias4[NTW];
-  {
-    float wv[NTW][KQ][8];
-#pragma unroll
-    for (int tw = 0; tw < NTW; ++tw) {
-      const int t = cg * NTW + tw;
-      const int n = t < nt ? n0 + 16 * t + i16 : n0;
-#pragma unroll
-      for (int q = 0; q < KQ; ++q)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int k = 32 * q + (j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4));
-          wv[tw][q][j] = p.B[static_cast<int64_t>(k) * p.bsk + static_cast<int64_t>(n) * p.bsn];
-        }
-    }
-    if (p.b_row_count) {
-      float cnt[KQ][8];
-#pragma unroll
-      for (int q = 0; q < KQ; ++q)
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          cnt[q][j] = p.b_row_count[32 * q + (j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4))];
-#pragma unroll
-      for (int tw = 0; tw < NTW; ++tw)
-#pragma unroll
-        for (int q = 0; q < KQ; ++q)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) wv[tw][q][j] *= 1.f / fmaxf(cnt[q][j], 1.f);
-    }
-#pragma unroll
-    for (int tw = 0; tw < NTW; ++tw) {
-      const bool tl = cg * NTW + tw < nt;
-#pragma unroll
-      for (int q = 0; q < KQ; ++q) {
-        float v[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          float w = wv[tw][q][j];
-          if (p.b_scale != 0.f) w *= p.b_scale;
-          v[j] = tl ? w : 0.f;
-        }
-        split3(v, wf[tw][q][0], wf[tw][q][1], wf[tw][q][2]);
-      }
-    }
-    float bv[NTW][4];
-#pragma unroll
-    for (int tw = 0; tw < NTW; ++tw) {
-      const int t = cg * NTW + tw;
-      const int c0 = n0 + 16 * (t < nt ? t : 0) + 4 * g;
-#pragma unroll
-      for (int cc = 0; cc < 4; ++cc) bv[tw][cc] = p.bias ? p.bias[c0 + cc] : 0.f;
-      const bool tl = t < nt;
-      bias4[tw] = tl ? f32x4{bv[tw][0], bv[tw][1], bv[tw][2], bv[tw][3]}
-                     : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  }
-
-  // ---- the ring: stage i of this workgroup is row block bx + i·nbx
+  // ---- the ring: stage i of this workgroup is row block bx + i·nbx. Its first D stages are
+  // requested before W is staged, so the two latencies overlap.
   f32x4 raw[C::D][C::F], rawm[C::D][C::F];
   auto ring_load = [&](int64_t i, f32x4 (&a)[C::F], f32x4 (&m)[C::F]) {
     int64_t sb = static_cast<int64_t>(bx) + i * nbx;
@@ -838,6 +780,70 @@ __global__ __launch_bounds__(64 * CG * RT) void k_row_gemm_x3s(RowGemmGroup grp)
   };
 #pragma unroll
   for (int d = 0; d < C::D; ++d) ring_load(d, raw[d], rawm[d]);
+
+  // ---- W's slice → LDS (coalesced along whichever of k / n is contiguous in memory, scaled
+  // there), then each wave's fragments (tile t = cg·NTW + tw, k step q, planes 0..2) → registers.
+  // All loads of a kind are issued before any is used: a load under a runtime condition inside
+  // an element loop made hipcc wait vmcnt(0) after each one.
+  bf16x8 wf[NTW][KQ][3];
+  f32x4 bias4[NTW];
+  {
+    constexpr int NSL = 16 * NTS;                 // slice columns
+    constexpr int LDW = NSL + 4;                  // padded LDS row of k
+    constexpr int EW = (C::K * NSL + C::THREADS - 1) / C::THREADS;
+    static_assert(C::K * LDW * 4 <= C::LDS, "W staging must fit the kernel's LDS");
+    float* sWt = reinterpret_cast<float*>(x3s_smem);  // [K][LDW], before the planes are used
+    const bool kfast = p.bsk == 1;
+    float wv[EW];
+    int ek[EW], en[EW];
+#pragma unroll
+    for (int r = 0; r < EW; ++r) {
+      int e = tid + C::THREADS * r;
+      e = e < C::K * NSL ? e : C::K * NSL - 1;
+      ek[r] = kfast ? e % C::K : e / NSL;
+      en[r] = kfast ? e / C::K : e % NSL;
+      const int n = n0 + en[r] < p.N ? n0 + en[r] : p.N - 1;
+      wv[r] = p.B[static_cast<int64_t>(ek[r]) * p.bsk + static_cast<int64_t>(n) * p.bsn];
+    }
+    if (p.b_row_count) {
+      float cnt[EW];
+#pragma unroll
+      for (int r = 0; r < EW; ++r) cnt[r] = p.b_row_count[ek[r]];
+#pragma unroll
+      for (int r = 0; r < EW; ++r) wv[r] *= 1.f / fmaxf(cnt[r], 1.f);
+    }
+#pragma unroll
+    for (int r = 0; r < EW; ++r) {
+      float w = wv[r];
+      if (p.b_scale != 0.f) w *= p.b_scale;
+      if (n0 + en[r] >= p.N) w = 0.f;
+      if (tid + C::THREADS * r < C::K * NSL) sWt[ek[r] * LDW + en[r]] = w;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int tw = 0; tw < NTW; ++tw) {
+      const int col = 16 * (cg * NTW + tw) + i16;
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          v[j] = sWt[(32 * q + (j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4))) * LDW + col];
+        split3(v, wf[tw][q][0], wf[tw][q][1], wf[tw][q][2]);
+      }
+    }
+    float bv[NTW][4];
+#pragma unroll
+    for (int tw = 0; tw < NTW; ++tw) {
+      const int t = cg * NTW + tw;
+      const int c0 = n0 + 16 * (t < nt ? t : 0) + 4 * g;
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) bv[tw][cc] = p.bias ? p.bias[c0 + cc] : 0.f;
+      bias4[tw] = t < nt ? f32x4{bv[tw][0], bv[tw][1], bv[tw][2], bv[tw][3]}
+                         : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    __syncthreads();  // the staging region becomes plane buffers
+  }
 
   const uint64_t drop_seed = p.drop_seed ? *p.drop_seed : 0ull;
   const uint32_t drop_thr = dropout_threshold(p.drop_keep);
