@@ -399,7 +399,7 @@ def load() -> ctypes.CDLL:
         for key, env in ((1, "HGD_SPMM_UNROLL"), (2, "HGD_SPMM_POLICY"),
                          (3, "HGD_SPMM_PASS_COLS"), (4, "HGD_ROWGEMM_BLOCKS"),
                          (5, "HGD_SPLITK_ROWS"), (6, "HGD_GEMM_EXACT"),
-                         (7, "HGD_X3_COLS"), (8, "HGD_X3_SPLITK")):
+                         (7, "HGD_X3_COLS"), (8, "HGD_X3_SPLITK"), (9, "HGD_X3S_TILES")):
             if os.environ.get(env):
                 st = lib.hgd_set_tuning(key, int(os.environ[env]))
                 if st != HGD_OK:

@@ -80,5 +80,7 @@ void set_x3_cols(int cols);
 // HGD_TUNE_X3_SPLITK (linear.hip): 0 = the f32-MFMA split-K weight gradient even when split-bf16
 // products are on.
 void set_x3_splitk(int on);
+// HGD_TUNE_X3S_TILES (linear.hip): 16-column tiles per wave of the staged row GEMM (0 = default).
+void set_x3s_tiles(int tiles);
 
 }  // namespace hgd

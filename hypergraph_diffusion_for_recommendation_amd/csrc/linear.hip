@@ -375,6 +375,7 @@ int g_gemm_exact = 0;  // HGD_TUNE_GEMM_EXACT
 // W's 96 KB of planes filling the LDS) or 64 (NT = 4, 256 threads, 48 KB of planes: several
 // workgroups per CU; the second slice's A reads hit the XCD's L2, row_block_of). HGD_TUNE_X3_COLS.
 int g_x3_cols = 0;  // 0: default
+int g_x3s_tiles = 0;  // HGD_TUNE_X3S_TILES (0: default)
 int g_x3_splitk = 1;  // HGD_TUNE_X3_SPLITK: the split-bf16 weight-gradient kernel (0: f32 MFMA)
 
 // NT: 16-column tiles of a ≤ 128-column slice (1, 2, 4 or 8). Tiles past the live nt (N not a
@@ -971,6 +972,11 @@ bool x3_eligible(const RowGemmGroup& g) {
   for (int i = 0; i < g.count; ++i) {
     const RowGemm& p = g.p[i];
     if (!al16(p.Y, p.ldy) || !al16(p.Y2, p.ldy2) || !al16(p.res, p.ldres)) return false;
+    // the staged kernel addresses a ≤ 64-row block through 32-bit byte offsets
+    constexpr int64_t kLdMax = int64_t{1} << 22;
+    if (p.lda >= kLdMax || p.ldm >= kLdMax || p.ldy >= kLdMax || p.ldy2 >= kLdMax ||
+        p.ldres >= kLdMax)
+      return false;
   }
   return true;
 }
@@ -990,10 +996,10 @@ hgd_status row_gemm_group(RowGemmGroup g, hipStream_t st, const char* fn) {
   if (g.count == 0 || g.p[0].rows == 0) return HGD_OK;
   if (x3_eligible(g) && g_x3_cols == 0) {
     switch (g.p[0].K / 32) {
-      case 1: return launch_x3s_k<1>(g, st, fn);
-      case 2: return launch_x3s_k<2>(g, st, fn);
-      case 3: return launch_x3s_k<3>(g, st, fn);
-      case 4: return launch_x3s_k<4>(g, st, fn);
+      case 1: return launch_x3s_k<1>(g, g_x3s_tiles, st, fn);
+      case 2: return launch_x3s_k<2>(g, g_x3s_tiles, st, fn);
+      case 3: return launch_x3s_k<3>(g, g_x3s_tiles, st, fn);
+      case 4: return launch_x3s_k<4>(g, g_x3s_tiles, st, fn);
       default: break;
     }
   }
@@ -1160,6 +1166,7 @@ void set_splitk_rows(int rows) { g_splitk_rows = rows > 0 ? rows : 0; }
 void set_gemm_exact(int exact) { g_gemm_exact = exact != 0; }
 void set_x3_cols(int cols) { g_x3_cols = cols; }
 void set_x3_splitk(int on) { g_x3_splitk = on != 0; }
+void set_x3s_tiles(int tiles) { g_x3s_tiles = tiles; }
 }  // namespace hgd
 
 extern "C" hgd_status hgd_linear_forward(const float* X, int64_t ldx, int64_t n_rows,

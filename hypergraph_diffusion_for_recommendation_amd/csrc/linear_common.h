@@ -143,13 +143,32 @@ __device__ __forceinline__ f32x4 mfma_x3(const bf16x8& w0, const bf16x8& w1, con
   return mfma_bf16(w0, x0, acc);
 }
 
+// Buffer-resource access (raw buffer, byte range [0, bytes) from base): an offset at or past the
+// range reads zeros without touching memory and drops a store. The staged kernel addresses a row
+// block through one resource per stage (base = the block's first row) with per-lane offsets that
+// do not change from stage to stage: no 64-bit address arithmetic or row clamps per access, and
+// no store under a branch (hipcc's vmcnt accounting then stays exact across the ring).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr uint32_t kBufOff = 0x80000000u;  // an offset outside every range used here
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, static_cast<int>(bytes),
+                                           0x00020000);
+}
+__device__ __forceinline__ f32x4 buf_ld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ __forceinline__ void buf_st4(__amdgpu_buffer_rsrc_t r, uint32_t off, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 0);
+}
+
 // row GEMM epilogue kinds of the staged split-bf16 kernel (linear_x3s.hip)
 constexpr int kEpiPlain = 0, kEpiRes = 1, kEpiAcc = 2;
 
 // The staged split-bf16 row GEMM for K = 32·KQ (linear_x3s.hip, one translation unit per KQ so
 // that the instantiations compile in parallel).
+// tiles: 16-column tiles per wave (HGD_TUNE_X3S_TILES; 0 = default)
 template <int KQ>
-hgd_status launch_x3s_k(const RowGemmGroup& g, hipStream_t st, const char* fn);
+hgd_status launch_x3s_k(const RowGemmGroup& g, int tiles, hipStream_t st, const char* fn);
 
 }  // namespace lin
 }  // namespace hgd

@@ -765,6 +765,10 @@ extern "C" hgd_status hgd_set_tuning(int32_t key, int32_t value) {
       HGD_REQUIRE(value == 0 || value == 1, "hgd_set_tuning: x3 split-K must be 0 or 1");
       set_x3_splitk(value);
       return HGD_OK;
+    case HGD_TUNE_X3S_TILES:
+      HGD_REQUIRE(value >= 0 && value <= 2, "hgd_set_tuning: x3s tiles must be 0, 1 or 2");
+      set_x3s_tiles(value);
+      return HGD_OK;
     default:
       return fail(HGD_ERR_INVALID_ARG, "hgd_set_tuning: unknown key %d", key);
   }

@@ -77,7 +77,10 @@ typedef enum hgd_epilogue {
  *   HGD_TUNE_X3_COLS:     output columns per workgroup of the split-bf16 row GEMM (64 or 128;
  *                         0 = default)
  *   HGD_TUNE_X3_SPLITK:   1 (default) = the split-bf16 split-K weight gradient when
- *                         HGD_TUNE_GEMM_EXACT is 0; 0 = the f32-MFMA split-K kernel */
+ *                         HGD_TUNE_GEMM_EXACT is 0; 0 = the f32-MFMA split-K kernel
+ *   HGD_TUNE_X3S_TILES:   16-column tiles per wave of the staged split-bf16 row GEMM at N > 32
+ *                         (1 or 2; 0 = default: 1 for masked products and N ≤ 64, else 2): 1
+ *                         holds half the W registers, two workgroups per CU */
 typedef enum hgd_tune_key {
   HGD_TUNE_SPMM_UNROLL = 1,
   HGD_TUNE_SPMM_POLICY = 2,
@@ -86,7 +89,8 @@ typedef enum hgd_tune_key {
   HGD_TUNE_SPLITK_ROWS = 5,
   HGD_TUNE_GEMM_EXACT = 6,
   HGD_TUNE_X3_COLS = 7,
-  HGD_TUNE_X3_SPLITK = 8
+  HGD_TUNE_X3_SPLITK = 8,
+  HGD_TUNE_X3S_TILES = 9
 } hgd_tune_key;
 hgd_status hgd_set_tuning(int32_t key, int32_t value);
 

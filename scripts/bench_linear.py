@@ -85,8 +85,10 @@ def main():
                 dY.data_ptr(), d, None, 0, X.data_ptr(), d, n, d, d, dW.data_ptr(),
                 db.data_ptr(), ws.data_ptr(), wsb, st),
             "bwd_weight_torch": lambda: (torch.mm(dY.t(), X), dY.sum(0)),
+            # the HBM reference point: one read and one write of the same bytes as the forward
+            "copy_torch": lambda: Y.copy_(X),
         }
-        algo = {"fwd": 2 * n * d * 4, "fwd_drop": 2 * n * d * 4, "fwd_drop_res": 4 * n * d * 4, "bwd_data": 3 * n * d * 4, "bwd_weight": 2 * n * d * 4}
+        algo = {"fwd": 2 * n * d * 4, "fwd_drop": 2 * n * d * 4, "fwd_drop_res": 4 * n * d * 4, "bwd_data": 3 * n * d * 4, "bwd_weight": 2 * n * d * 4, "copy": 2 * n * d * 4}
         for name, fn in cases.items():
             if args.cases and name not in args.cases:
                 continue

@@ -1,0 +1,34 @@
+#!/bin/bash
+# PMC passes of the staged split-bf16 row GEMM forward at 144,242 × 128 → 128 (one counter group
+# per pass), for each HGD_X3S_TILES setting in PROF_TILES. Records under gpurun_out/profx3s/.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+O=gpurun_out/profx3s
+mkdir -p $O
+export TMPDIR=/tmp
+CASES=${PROF_CASES:-fwd_hgd}
+CMD="python scripts/bench_linear.py --rows 144242 --dim 128 --reps 5 --inner 4 --cases $CASES"
+for t in ${PROF_TILES:-2 1}; do
+  n=0
+  for pmc in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
+      "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \
+      "SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INST_CYCLES_VMEM SQ_VALU_MFMA_BUSY_CYCLES" \
+      "FETCH_SIZE" "WRITE_SIZE"; do
+    n=$((n+1))
+    HGD_X3S_TILES=$t timeout -s KILL 90 rocprofv3 --pmc $pmc --output-format csv -d $O/t${t}_pmc$n -o run -- $CMD \
+      > $O/t${t}_pmc$n.log 2>&1 || { echo "pmc pass $n failed"; tail -5 $O/t${t}_pmc$n.log; exit 1; }
+  done
+done
+python3 - $O <<'PY'
+import csv, glob, collections, sys, os
+O = sys.argv[1]
+for d in sorted(glob.glob(os.path.join(O, "t*_pmc*"))):
+    for f in glob.glob(os.path.join(d, "run_counter_collection.csv")):
+        per = collections.defaultdict(lambda: collections.defaultdict(float))
+        for r in csv.DictReader(open(f)):
+            if "x3s" not in r["Kernel_Name"]:
+                continue
+            per[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
+        for k, v in sorted(per.items()):
+            print(os.path.basename(d), k, round(sum(v.values()) / len(v)))
+PY
