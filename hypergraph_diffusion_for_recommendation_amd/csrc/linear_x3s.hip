@@ -40,17 +40,20 @@ namespace {
 // R = 16·RT rows per stage; K = 32·KQ; THREADS = 64·CG·RT. EPI: 0 plain store, 1 the second
 // store Y2 = Y + res, 2 accumulate (Y += product) — template arguments, so that no load of the
 // stage sits in a runtime branch (hipcc then waits vmcnt(0) at the join, draining the ring).
-template <int KQ, int NTW, int CG, int RT, bool MASK>
+template <int KQ, int NTW, int CG, int RT, bool MASK, int PW>
 struct X3S {
   static constexpr int K = 32 * KQ;
   static constexpr int R = 16 * RT;
-  static constexpr int WAVES = CG * RT;
+  static constexpr int CWAVES = CG * RT;                     // waves computing tiles
+  static constexpr int WAVES = CWAVES + PW;                  // + producer waves (PW > 0)
   static constexpr int THREADS = 64 * WAVES;
+  static constexpr int STHREADS = PW > 0 ? 64 * PW : THREADS;  // threads loading and splitting
   static constexpr int F4 = R * K / 4;                       // float4 pieces of a stage
-  static constexpr int F = (F4 + THREADS - 1) / THREADS;     // per thread
+  static constexpr int F = (F4 + STHREADS - 1) / STHREADS;   // per loading thread
   // ring depth: 8 float4 pieces (128 B) per thread in flight — 64 KB per 8-wave workgroup; with
-  // one column tile per wave (two workgroups per CU in 128 registers) 4 pieces, 2 with a mask
-  static constexpr int RING = NTW == 1 ? (MASK ? 2 : 6) : 8;
+  // one column tile per wave (two workgroups per CU in 128 registers) 6 pieces, 2 with a mask;
+  // producer waves (no W registers) 12, 4 with a mask — 48 KB per workgroup
+  static constexpr int RING = PW > 0 ? (MASK ? 4 : 12) : NTW == 1 ? (MASK ? 2 : 6) : 8;
   static constexpr int D = F >= RING ? 1 : RING / F;
   static constexpr int LPR = K / 4;                          // lanes holding one row
   static constexpr size_t PLANE_BYTES = static_cast<size_t>(RT) * KQ * 1024;  // one plane, one stage
@@ -66,10 +69,14 @@ struct X3S {
 // dropout, kSplAny the runtime flags (dropout, binarization, row_inv) in branches
 constexpr int kSplPlain = 0, kSplDrop = 1, kSplAny = 2;
 
-template <int KQ, int NTW, int CG, int RT, bool MASK, int EPI, int SPL>
-__global__ __launch_bounds__(64 * CG * RT) __attribute__((amdgpu_waves_per_eu(NTW == 1 && CG >= 4 ? 4 : 1)))
+// PW > 0: PW producer waves load the row blocks and split them into the planes while the CG·RT
+// consumer waves run the MFMAs and epilogues of the previous stage (one barrier per stage); the
+// two phases then overlap across waves instead of alternating inside every wave.
+template <int KQ, int NTW, int CG, int RT, bool MASK, int EPI, int SPL, int PW>
+__global__ __launch_bounds__(64 * (CG * RT + PW))
+__attribute__((amdgpu_waves_per_eu(PW > 0 ? 3 : NTW == 1 && CG >= 4 ? 4 : 1)))
 void k_row_gemm_x3s(RowGemmGroup grp) {
-  using C = X3S<KQ, NTW, CG, RT, MASK>;
+  using C = X3S<KQ, NTW, CG, RT, MASK, PW>;
   extern __shared__ __attribute__((aligned(16))) char x3s_smem[];
   char* planes = x3s_smem;                                            // [2][3][RT][KQ][1 KB]
   float* s_inv = reinterpret_cast<float*>(x3s_smem + 2 * 3 * C::PLANE_BYTES);  // [2][R]
@@ -84,7 +91,9 @@ void k_row_gemm_x3s(RowGemmGroup grp) {
   const int wave = tid >> 6;
   const int i16 = lane & 15;
   const int g = lane >> 4;
-  const int rt = wave % RT, cg = wave / RT;
+  const int rt = wave % RT, cg = (wave / RT) % CG;
+  const bool producer = PW > 0 && wave >= C::CWAVES;
+  const int stid = PW > 0 ? tid - 64 * C::CWAVES : tid;  // index among the loading threads
   constexpr int NTS = CG * NTW;  // 16-column tiles per slice
   const int n0 = ys * 16 * NTS;
   const int nt = min(NTS, (p.N - n0) / 16);  // live tiles of this slice
@@ -96,7 +105,7 @@ void k_row_gemm_x3s(RowGemmGroup grp) {
   uint32_t aoff[C::F], moff[C::F];
 #pragma unroll
   for (int u = 0; u < C::F; ++u) {
-    const int f = tid + C::THREADS * u;
+    const int f = stid + C::STHREADS * u;
     const uint32_t rl = f / C::LPR, c = f % C::LPR;
     aoff[u] = f < C::F4 ? (rl * static_cast<uint32_t>(p.lda) + 4 * c) * 4 : kBufOff;
     moff[u] = f < C::F4 ? (rl * static_cast<uint32_t>(p.ldm) + 4 * c) * 4 : kBufOff;
@@ -119,8 +128,10 @@ void k_row_gemm_x3s(RowGemmGroup grp) {
       for (int u = 0; u < C::F; ++u) m[u] = buf_ld4(rm, moff[u]);
     }
   };
+  if (PW == 0 || producer) {
 #pragma unroll
-  for (int d = 0; d < C::D; ++d) ring_load(d, raw[d], rawm[d]);
+    for (int d = 0; d < C::D; ++d) ring_load(d, raw[d], rawm[d]);
+  }
 
   // ---- W's slice → LDS (coalesced along whichever of k / n is contiguous in memory, scaled
   // there), then each wave's fragments (tile t = cg·NTW + tw, k step q, planes 0..2) → registers.
@@ -128,6 +139,7 @@ void k_row_gemm_x3s(RowGemmGroup grp) {
   // an element loop made hipcc wait vmcnt(0) after each one.
   bf16x8 wf[NTW][KQ][3];
   f32x4 bias4[NTW];
+  bool w_nk;  // W staged as [n][k] (else [k][n])
   {
     constexpr int NSL = 16 * NTS;                 // slice columns
     constexpr int LDW = NSL + 4;                  // [k][n] layout: padded row of k
@@ -144,6 +156,7 @@ void k_row_gemm_x3s(RowGemmGroup grp) {
     // fragment is two 16-byte reads (LDK ≡ 8 mod 64: the 16 lanes of a ds_read_b128 group on
     // distinct banks). Otherwise sW[k][n] with scalar fragment reads.
     const bool nk = vec && kfast;
+    w_nk = nk;
     if (vec) {
       // float4 pieces along the contiguous dimension, all in flight at once: one round trip
       // (8 pieces per thread at K = 128 and 128 columns)
@@ -219,6 +232,15 @@ void k_row_gemm_x3s(RowGemmGroup grp) {
       }
     }
     __syncthreads();
+  }
+
+  // each computing wave's W fragments (tile t = cg·NTW + tw, k step q, planes 0..2) and bias
+  auto load_w_frags = [&]() {
+    constexpr int NSL = 16 * NTS;
+    constexpr int LDW = NSL + 4;
+    constexpr int LDK = C::K + ((8 - C::K) % 64 + 64) % 64;
+    const float* sW = reinterpret_cast<const float*>(x3s_smem);
+    const bool nk = w_nk;
 #pragma unroll
     for (int tw = 0; tw < NTW; ++tw) {
       const int col = 16 * (cg * NTW + tw) + i16;
@@ -251,8 +273,7 @@ void k_row_gemm_x3s(RowGemmGroup grp) {
       bias4[tw] = t < nt ? f32x4{bv[tw][0], bv[tw][1], bv[tw][2], bv[tw][3]}
                          : f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    __syncthreads();  // the staging region becomes plane buffers
-  }
+  };
 
   const uint64_t drop_seed = p.drop_seed ? *p.drop_seed : 0ull;
   const uint32_t drop_thr = dropout_threshold(p.drop_keep);
@@ -266,8 +287,8 @@ void k_row_gemm_x3s(RowGemmGroup grp) {
     char* pb = planes + static_cast<size_t>(buf) * 3 * C::PLANE_BYTES;
 #pragma unroll
     for (int u = 0; u < C::F; ++u) {
-      const int f = tid + C::THREADS * u;
-      if (C::F4 % C::THREADS != 0 && f >= C::F4) continue;
+      const int f = stid + C::STHREADS * u;
+      if (C::F4 % C::STHREADS != 0 && f >= C::F4) continue;
       const int rl = f / C::LPR, c = f % C::LPR;
       f32x4 x = a[u];
       const uint32_t e = static_cast<uint32_t>(r0 + rl) * static_cast<uint32_t>(C::K) + 4 * c;
@@ -306,8 +327,9 @@ void k_row_gemm_x3s(RowGemmGroup grp) {
   // with stage i + 1 + D, then stage i's epilogue. The split's vector work sits in the same
   // basic block as the MFMAs (SPL: no runtime branch in it), so the scheduler can interleave it
   // with the matrix instructions instead of running the two phases in turn.
-  auto step = [&](int64_t i, int buf, bool has_next, f32x4 (&a)[C::F], f32x4 (&m)[C::F]) {
-    __syncthreads();
+  // consume(i, buf, mid): stage i's MFMAs from plane buffer buf, mid() (the cooperative form's
+  // split of the next stage), then the epilogue
+  auto consume = [&](int64_t i, int buf, auto&& mid) {
     const int64_t sb = static_cast<int64_t>(bx) + i * nbx;
     const int64_t r0 = sb * C::R;
     const uint32_t nr = block_rows(sb);
@@ -361,19 +383,7 @@ void k_row_gemm_x3s(RowGemmGroup grp) {
       for (int tw = 0; tw < NTW; ++tw)
         acc[tw] = mfma_x3(wf[tw][q][0], wf[tw][q][1], wf[tw][q][2], xh, xm, xl, acc[tw], false);
     }
-    // stage i + 1 into the other buffer (its last reads, stage i - 1's, were before the barrier)
-    // and the slot's refill: independent of the MFMAs above, in the same basic block
-    if (has_next) {
-      split_stage(i + 1, buf ^ 1, a, m);
-      ring_load(i + 1 + C::D, a, m);
-    }
-    // issue order of the block: each MFMA followed by two vector instructions (the split's),
-    // which run while the matrix core works (an MFMA holds vector issue for 8 of its 16 cycles)
-#pragma unroll
-    for (int k = 0; k < KQ * NTW * 6; ++k) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
-    }
+    mid();
     // epilogue: lane (i16, g) holds row orow, columns n0 + 16t + 4g + 0..3; the scale and bias
     // unconditionally (inv = 1 without row_inv: bitwise the unscaled sum) and at once
     mfma_drain();
@@ -408,33 +418,97 @@ void k_row_gemm_x3s(RowGemmGroup grp) {
   };
   // stages of this workgroup; stage s lives in ring slot s % D (static: D steps unrolled)
   const int64_t my_stages = bx < stages ? (stages - bx + nbx - 1) / nbx : 0;
-  if (my_stages == 0) return;  // no barrier below is reached by part of the workgroup only
-  split_stage(0, 0, raw[0], rawm[0]);
-  ring_load(C::D, raw[0], rawm[0]);
-  // Whole groups of D steps that all have a next stage run without a condition, the rest after
-  // the loop: with a per-step condition inside the loop, the path that skipped steps left the
-  // latest ring load last in the queue, and hipcc's merge at the loop header waited vmcnt(0) —
-  // the whole ring drained once per group
-  int64_t i0 = 0;
-  for (; i0 + C::D < my_stages; i0 += C::D) {
+  if (my_stages == 0) return;  // (uniform: no barrier below is reached by part of the workgroup)
+  if constexpr (PW == 0) {
+    load_w_frags();
+    __syncthreads();  // the staging region becomes plane buffers
+    split_stage(0, 0, raw[0], rawm[0]);
+    ring_load(C::D, raw[0], rawm[0]);
+    // One pipeline step: stage i's planes (buffer i & 1) are complete after the barrier; its MFMAs
+    // run, stage i + 1 is split from ring slot a / m into the other buffer (its last reads, stage
+    // i - 1's, were before the barrier) and the slot refilled with stage i + 1 + D, then stage
+    // i's epilogue. The split's vector work sits in the same basic block as the MFMAs (SPL: no
+    // runtime branch in it), so the scheduler can interleave it with the matrix instructions.
+    auto step = [&](int64_t i, int buf, bool has_next, f32x4 (&a)[C::F], f32x4 (&m)[C::F]) {
+      __syncthreads();
+      consume(i, buf, [&]() {
+        if (has_next) {
+          split_stage(i + 1, buf ^ 1, a, m);
+          ring_load(i + 1 + C::D, a, m);
+        }
+        // issue order: each MFMA followed by two vector instructions (the split's), which run
+        // while the matrix core works (an MFMA holds vector issue for 8 of its 16 cycles)
 #pragma unroll
-    for (int d = 0; d < C::D; ++d)
-      step(i0 + d, static_cast<int>((i0 + d) & 1), true, raw[(d + 1) % C::D], rawm[(d + 1) % C::D]);
-  }
+        for (int k = 0; k < KQ * NTW * 6; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+        }
+      });
+    };
+    // Whole groups of D steps that all have a next stage run without a condition, the rest
+    // after the loop: with a per-step condition inside the loop, the path that skipped steps left
+    // the latest ring load last in the queue, and hipcc's merge at the loop header waited
+    // vmcnt(0) — the whole ring drained once per group
+    int64_t i0 = 0;
+    for (; i0 + C::D < my_stages; i0 += C::D) {
 #pragma unroll
-  for (int d = 0; d < C::D; ++d) {
-    if (i0 + d < my_stages)
-      step(i0 + d, static_cast<int>((i0 + d) & 1), i0 + d + 1 < my_stages, raw[(d + 1) % C::D],
-           rawm[(d + 1) % C::D]);
+      for (int d = 0; d < C::D; ++d)
+        step(i0 + d, static_cast<int>((i0 + d) & 1), true, raw[(d + 1) % C::D],
+             rawm[(d + 1) % C::D]);
+    }
+#pragma unroll
+    for (int d = 0; d < C::D; ++d) {
+      if (i0 + d < my_stages)
+        step(i0 + d, static_cast<int>((i0 + d) & 1), i0 + d + 1 < my_stages, raw[(d + 1) % C::D],
+             rawm[(d + 1) % C::D]);
+    }
+  } else if (producer) {
+    // producers: stage i + 1 into the buffer the consumers left before this barrier
+    __syncthreads();  // the consumers have their W fragments: the staging region is free
+    split_stage(0, 0, raw[0], rawm[0]);
+    ring_load(C::D, raw[0], rawm[0]);
+    auto pstep = [&](int64_t i, bool has_next, f32x4 (&a)[C::F], f32x4 (&m)[C::F]) {
+      __syncthreads();
+      if (has_next) {
+        split_stage(i + 1, static_cast<int>((i + 1) & 1), a, m);
+        ring_load(i + 1 + C::D, a, m);
+      }
+    };
+    int64_t i0 = 0;
+    for (; i0 + C::D < my_stages; i0 += C::D) {
+#pragma unroll
+      for (int d = 0; d < C::D; ++d) pstep(i0 + d, true, raw[(d + 1) % C::D], rawm[(d + 1) % C::D]);
+    }
+#pragma unroll
+    for (int d = 0; d < C::D; ++d) {
+      if (i0 + d < my_stages)
+        pstep(i0 + d, i0 + d + 1 < my_stages, raw[(d + 1) % C::D], rawm[(d + 1) % C::D]);
+    }
+  } else {
+    // consumers: W fragments, then one stage per barrier
+    load_w_frags();
+    __syncthreads();
+    for (int64_t i = 0; i < my_stages; ++i) {
+      __syncthreads();
+      consume(i, static_cast<int>(i & 1), []() {
+        // fragment reads one k step ahead of the MFMAs (not all hoisted: registers)
+        __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+#pragma unroll
+        for (int q = 0; q < KQ; ++q) {
+          if (q + 1 < KQ) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, NTW * 6, 0);
+        }
+      });
+    }
   }
 }
 // One staged split-bf16 launch (k_row_gemm_x3s): persistent workgroups, at most one resident
 // round, shared by a group's products in proportion to their rows; column slices XCD-paired.
-template <int KQ, int NTW, int CG, bool MASK, int EPI, int SPL>
+template <int KQ, int NTW, int CG, bool MASK, int EPI, int SPL, int PW>
 hgd_status launch_x3s(RowGemmGroup g, hipStream_t st, const char* fn) {
   constexpr int RT = (8 / CG) < (16 / KQ) ? (8 / CG) : (16 / KQ) >= 4 ? 4 : 2;
-  using C = X3S<KQ, NTW, CG, RT, MASK>;
-  const void* kern = reinterpret_cast<const void*>(&k_row_gemm_x3s<KQ, NTW, CG, RT, MASK, EPI, SPL>);
+  using C = X3S<KQ, NTW, CG, RT, MASK, PW>;
+  const void* kern = reinterpret_cast<const void*>(&k_row_gemm_x3s<KQ, NTW, CG, RT, MASK, EPI, SPL, PW>);
   static int resident = 0;
   if (resident == 0) {
     if (C::LDS > 65536)
@@ -461,7 +535,7 @@ hgd_status launch_x3s(RowGemmGroup g, hipStream_t st, const char* fn) {
   g.nb0 = static_cast<int32_t>(bx[0]);
   g.nbt = static_cast<int32_t>(bx[0] + bx[1]);
   const dim3 grid(static_cast<unsigned>(g.nbt) * static_cast<unsigned>(g.ny));
-  hipLaunchKernelGGL((k_row_gemm_x3s<KQ, NTW, CG, RT, MASK, EPI, SPL>), grid, dim3(C::THREADS), C::LDS,
+  hipLaunchKernelGGL((k_row_gemm_x3s<KQ, NTW, CG, RT, MASK, EPI, SPL, PW>), grid, dim3(C::THREADS), C::LDS,
                      st, g);
   return check_launch(fn);
 }
@@ -481,16 +555,16 @@ int x3s_split_kind(const RowGemmGroup& g, int epi) {
   return kSplAny;
 }
 
-template <int KQ, int NTW, int CG, bool MASK, int EPI>
+template <int KQ, int NTW, int CG, int PW, bool MASK, int EPI>
 hgd_status launch_x3s_spl(const RowGemmGroup& g, int spl, hipStream_t st, const char* fn) {
-  if (spl == kSplPlain) return launch_x3s<KQ, NTW, CG, MASK, EPI, kSplPlain>(g, st, fn);
+  if (spl == kSplPlain) return launch_x3s<KQ, NTW, CG, MASK, EPI, kSplPlain, PW>(g, st, fn);
   if constexpr (!MASK && EPI != kEpiAcc) {
-    if (spl == kSplDrop) return launch_x3s<KQ, NTW, CG, MASK, EPI, kSplDrop>(g, st, fn);
+    if (spl == kSplDrop) return launch_x3s<KQ, NTW, CG, MASK, EPI, kSplDrop, PW>(g, st, fn);
   }
-  return launch_x3s<KQ, NTW, CG, MASK, EPI, kSplAny>(g, st, fn);
+  return launch_x3s<KQ, NTW, CG, MASK, EPI, kSplAny, PW>(g, st, fn);
 }
 
-template <int KQ, int NTW, int CG>
+template <int KQ, int NTW, int CG, int PW = 0>
 hgd_status launch_x3s_epi(const RowGemmGroup& g, hipStream_t st, const char* fn) {
   // every product of a group has the same mask mode; the epilogue kind must match too
   const RowGemm& p = g.p[0];
@@ -502,21 +576,24 @@ hgd_status launch_x3s_epi(const RowGemmGroup& g, hipStream_t st, const char* fn)
   }
   const int spl = x3s_split_kind(g, epi);
   if (p.mask) {
-    if (epi == kEpiAcc) return launch_x3s_spl<KQ, NTW, CG, true, kEpiAcc>(g, spl, st, fn);
-    return launch_x3s_spl<KQ, NTW, CG, true, kEpiPlain>(g, spl, st, fn);
+    if (epi == kEpiAcc) return launch_x3s_spl<KQ, NTW, CG, PW, true, kEpiAcc>(g, spl, st, fn);
+    return launch_x3s_spl<KQ, NTW, CG, PW, true, kEpiPlain>(g, spl, st, fn);
   }
-  if (epi == kEpiRes) return launch_x3s_spl<KQ, NTW, CG, false, kEpiRes>(g, spl, st, fn);
-  if (epi == kEpiAcc) return launch_x3s_spl<KQ, NTW, CG, false, kEpiAcc>(g, spl, st, fn);
-  return launch_x3s_spl<KQ, NTW, CG, false, kEpiPlain>(g, spl, st, fn);
+  if (epi == kEpiRes) return launch_x3s_spl<KQ, NTW, CG, PW, false, kEpiRes>(g, spl, st, fn);
+  if (epi == kEpiAcc) return launch_x3s_spl<KQ, NTW, CG, PW, false, kEpiAcc>(g, spl, st, fn);
+  return launch_x3s_spl<KQ, NTW, CG, PW, false, kEpiPlain>(g, spl, st, fn);
 }
 
 template <int KQ>
 hgd_status launch_x3s_shape(const RowGemmGroup& g, int tiles, hipStream_t st, const char* fn) {
   const int nt = (std::min(g.p[0].N, 128) + 15) / 16;
-  // default (measured at 144,242 × 128 and 69,716 × 64, profiles/r03_linear): one tile per wave
-  // for the masked backward-data product and up to 64 columns, two for the unmasked forward at
-  // 128 (its W registers then serve twice the MFMAs per fragment read)
-  if (tiles == 0) tiles = g.p[0].mask || nt <= 4 ? 1 : 2;
+  // default (measured at 144,242 × 128 and 69,716 / 31,668 × 64, profiles/r03_linear): one
+  // tile per wave for the masked backward-data product, two tiles + producer waves otherwise
+  if (tiles == 0) tiles = g.p[0].mask ? 1 : 3;
+  if (tiles == 3 && nt > 2) {  // two tiles per wave + 4 producer waves
+    if (nt <= 4) return launch_x3s_epi<KQ, 2, 2, 4>(g, st, fn);
+    return launch_x3s_epi<KQ, 2, 4, 4>(g, st, fn);
+  }
   if (tiles == 1 && nt > 2) {  // one column tile per wave, ≤ 128 registers: 2 workgroups per CU
     if (nt <= 4) return launch_x3s_epi<KQ, 1, 4>(g, st, fn);
     return launch_x3s_epi<KQ, 1, 8>(g, st, fn);

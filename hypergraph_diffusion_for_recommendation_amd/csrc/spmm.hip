@@ -766,7 +766,7 @@ extern "C" hgd_status hgd_set_tuning(int32_t key, int32_t value) {
       set_x3_splitk(value);
       return HGD_OK;
     case HGD_TUNE_X3S_TILES:
-      HGD_REQUIRE(value >= 0 && value <= 2, "hgd_set_tuning: x3s tiles must be 0, 1 or 2");
+      HGD_REQUIRE(value >= 0 && value <= 3, "hgd_set_tuning: x3s tiles must be 0, 1, 2 or 3");
       set_x3s_tiles(value);
       return HGD_OK;
     default:

@@ -78,9 +78,10 @@ typedef enum hgd_epilogue {
  *                         0 = default)
  *   HGD_TUNE_X3_SPLITK:   1 (default) = the split-bf16 split-K weight gradient when
  *                         HGD_TUNE_GEMM_EXACT is 0; 0 = the f32-MFMA split-K kernel
- *   HGD_TUNE_X3S_TILES:   16-column tiles per wave of the staged split-bf16 row GEMM at N > 32
- *                         (1 or 2; 0 = default: 1 for masked products and N ≤ 64, else 2): 1
- *                         holds half the W registers, two workgroups per CU */
+ *   HGD_TUNE_X3S_TILES:   form of the staged split-bf16 row GEMM at N > 32: 1 or 2 16-column
+ *                         tiles per wave (1: half the W registers, two workgroups per CU), 3 =
+ *                         two tiles + 4 producer waves that load and split the rows while the
+ *                         others multiply; 0 = default (1 for masked products, else 3) */
 typedef enum hgd_tune_key {
   HGD_TUNE_SPMM_UNROLL = 1,
   HGD_TUNE_SPMM_POLICY = 2,
