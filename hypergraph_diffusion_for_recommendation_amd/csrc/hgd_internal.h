@@ -78,8 +78,8 @@ void set_gemm_exact(int exact);
 // HGD_TUNE_X3_COLS (linear.hip): column-slice width of the split-bf16 row GEMM (0, 64 or 128).
 void set_x3_cols(int cols);
 // HGD_TUNE_X3_SPLITK (linear.hip): 0 = the f32-MFMA split-K weight gradient even when split-bf16
-// products are on.
-void set_x3_splitk(int on);
+// products are on, 1 = split-bf16, 2 = by shape (default).
+void set_x3_splitk(int mode);
 // HGD_TUNE_X3S_TILES (linear.hip): 16-column tiles per wave of the staged row GEMM (0 = default).
 void set_x3s_tiles(int tiles);
 

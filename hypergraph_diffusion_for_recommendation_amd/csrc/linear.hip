@@ -376,7 +376,23 @@ int g_gemm_exact = 0;  // HGD_TUNE_GEMM_EXACT
 // workgroups per CU; the second slice's A reads hit the XCD's L2, row_block_of). HGD_TUNE_X3_COLS.
 int g_x3_cols = 0;  // 0: default
 int g_x3s_tiles = 0;  // HGD_TUNE_X3S_TILES (0: default)
-int g_x3_splitk = 1;  // HGD_TUNE_X3_SPLITK: the split-bf16 weight-gradient kernel (0: f32 MFMA)
+int g_x3_splitk = 2;  // HGD_TUNE_X3_SPLITK: 1 split-bf16 weight gradient, 0 f32 MFMA, 2 auto
+
+// The split-bf16 split-K kernel pays for its six products with one k step in flight per slice:
+// at 144,242 × 128 it ran 79 µs against the f32-MFMA kernel's 59 µs; at 69,716 × 64 19.9 against
+// 21.1, at 31,668 × 64 16.0 against 13.1 (profiles/r03_linear). Auto: split-bf16 for outputs of
+// at most 64 × 64 over at least 49,152 rows. The same rule sizes the workspace and launches.
+bool use_x3_splitk(const hgd_gemm_tn_desc* d, int count) {
+  if (g_gemm_exact || g_x3_splitk == 0) return false;
+  if (g_x3_splitk == 1) return true;
+  int64_t rows = 0;
+  for (int i = 0; i < count; ++i) {
+    if (d[i].rows <= 0) continue;
+    if (d[i].M > 64 || d[i].N > 64) return false;
+    rows += d[i].rows;
+  }
+  return rows >= 49152;
+}
 
 // NT: 16-column tiles of a ≤ 128-column slice (1, 2, 4 or 8). Tiles past the live nt (N not a
 // multiple of 16·NT) are staged as zeros and computed like the others — only their stores are
@@ -1066,6 +1082,7 @@ int64_t splits_for(int64_t rows, int64_t out_tiles) {
 
 // Row slices of each product of a split-K group (the pair shares the resident budget).
 void tn_splits(const hgd_gemm_tn_desc* d, int count, int64_t* S, int64_t* per) {
+  const bool x3 = use_x3_splitk(d, count);
   if (g_splitk_rows > 0) {  // HGD_TUNE_SPLITK_ROWS: fixed rows per slice
     for (int i = 0; i < count; ++i) {
       per[i] = g_splitk_rows;
@@ -1075,7 +1092,6 @@ void tn_splits(const hgd_gemm_tn_desc* d, int count, int64_t* S, int64_t* per) {
   }
   // workgroups per slice and the resident budget: 64 × 64 tiles of 256 threads (f32 MFMA), or
   // groups of up to eight 64 × 32 tiles of 512 threads (split-bf16)
-  const bool x3 = !g_gemm_exact && g_x3_splitk;
   auto wg_per_slice = [&](const hgd_gemm_tn_desc& e) -> int64_t {
     if (!x3) return static_cast<int64_t>((e.M + 63) / 64) * ((e.N + 63) / 64);
     const int t = ((e.M + 63) / 64) * ((e.N + 31) / 32);
@@ -1165,7 +1181,7 @@ void set_row_gemm_max_blocks(int blocks) {
 void set_splitk_rows(int rows) { g_splitk_rows = rows > 0 ? rows : 0; }
 void set_gemm_exact(int exact) { g_gemm_exact = exact != 0; }
 void set_x3_cols(int cols) { g_x3_cols = cols; }
-void set_x3_splitk(int on) { g_x3_splitk = on != 0; }
+void set_x3_splitk(int mode) { g_x3_splitk = mode; }
 void set_x3s_tiles(int tiles) { g_x3s_tiles = tiles; }
 }  // namespace hgd
 
@@ -1318,7 +1334,7 @@ extern "C" hgd_status hgd_gemm_tn(const hgd_gemm_tn_desc* descs, int32_t count, 
     }
   const dim3 grid(static_cast<unsigned>(Stot), static_cast<unsigned>((g.p[0].M + 63) / 64),
                   static_cast<unsigned>((g.p[0].N + 63) / 64));
-  if (!g_gemm_exact && g_x3_splitk) {
+  if (use_x3_splitk(descs, count)) {
     const int tiles = ((g.p[0].M + 63) / 64) * ((g.p[0].N + 31) / 32);
     const dim3 gx(static_cast<unsigned>(Stot),
                   static_cast<unsigned>(tiles / x3_tiles_per_wg(tiles)));

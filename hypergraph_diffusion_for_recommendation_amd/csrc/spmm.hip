@@ -762,7 +762,7 @@ extern "C" hgd_status hgd_set_tuning(int32_t key, int32_t value) {
       set_x3_cols(value);
       return HGD_OK;
     case HGD_TUNE_X3_SPLITK:
-      HGD_REQUIRE(value == 0 || value == 1, "hgd_set_tuning: x3 split-K must be 0 or 1");
+      HGD_REQUIRE(value >= 0 && value <= 2, "hgd_set_tuning: x3 split-K must be 0, 1 or 2");
       set_x3_splitk(value);
       return HGD_OK;
     case HGD_TUNE_X3S_TILES:

@@ -95,3 +95,20 @@ def test_linear_abi_checks(dev):
                                         db.data_ptr(), None, 0, None)
     torch.cuda.synchronize()
     assert st == 0 and dW.abs().sum().item() == 0 and db.abs().sum().item() == 0
+
+
+@pytest.mark.parametrize("tiles,splitk", [(1, 1), (2, 0), (3, 1), (3, 0)])
+def test_linear_kernel_forms(dev, tiles, splitk):
+    """Every form of the split-bf16 products (HGD_TUNE_X3S_TILES: one or two column tiles per
+    wave, producer waves; HGD_TUNE_X3_SPLITK: split-bf16 or f32 weight gradient) against float64,
+    at both ED-HNN widths, masked and unmasked."""
+    from hypergraph_diffusion_for_recommendation_amd import _native as nat
+    lib = nat.load()
+    try:
+        assert lib.hgd_set_tuning(9, tiles) == 0 and lib.hgd_set_tuning(8, splitk) == 0
+        for rows, d in ((70_001, 64), (20_011, 128), (4_999, 96)):
+            for relu in (False, True):
+                test_linear_fwd_bwd(dev, rows, d, d, relu)
+    finally:
+        lib.hgd_set_tuning(9, 0)
+        lib.hgd_set_tuning(8, 2)
