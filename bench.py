@@ -326,6 +326,12 @@ def main():
               f"mislabelled run", file=sys.stderr)
         sys.exit(2)
     strong = args.scaling == "strong"
+    t_launch = time.perf_counter()
+
+    def phase(msg):  # multi-rank progress on stderr (rehearsals of N ranks on one device)
+        if world > 1:
+            print(f"[bench rank {rank}] {time.perf_counter() - t_launch:7.1f} s {msg}",
+                  file=sys.stderr, flush=True)
 
     pmc = None
     pmc_note = None
@@ -349,9 +355,11 @@ def main():
     device = torch.device(f"cuda:{dev_index}")
     torch.cuda.set_device(device)
     dist_backend = None
+    phase("torch imported")
     if world > 1:
         dist_backend = os.environ.get("HGD_DIST_BACKEND", "nccl")  # nccl == RCCL
         init_process_group(device, dist_backend)
+        phase("process group up")
 
     shard_kw = dict(n_chunks=args.chunks, P="sym", Q="mean", R="sym",
                     slice_width=args.slice_width, transport=args.transport)
@@ -359,6 +367,7 @@ def main():
     keep_global = args.check and strong and world > 1
     idx = make_graph(U, I, E, seed=0 if strong else rank, zipf=zipf, device=device)
     nnz_graph = int(idx.shape[1])
+    phase(f"graph built ({nnz_graph} edges)")
     u0, u1 = 0, U
     if strong and world > 1:
         sh, u0, u1 = ShardedIncidence.from_global(idx, U, I, device=device, **shard_kw)
@@ -370,6 +379,7 @@ def main():
     if not keep_global:
         del idx
     nnz = inc.nnz
+    phase(f"shard ready ({nnz} edges, users [{u0}, {u1}))")
     seed_x = 1000 + (0 if strong else rank)
     X = table_rows(u0, u1, d, seed_x, device, bound)
     dY = table_rows(u0, u1, d, seed_x + 1, device)
@@ -409,6 +419,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    phase("warm")
     if world > 1:
         dist.barrier()
     # roofline: HIP events around every hop launch on its stream, recorded inside the timed
@@ -458,6 +469,7 @@ def main():
                     del X_global, dY_global
                     torch.cuda.synchronize()
                     torch.cuda.empty_cache()
+                    phase(f"checked: {check}")
                 dist.barrier()
             del idx
     per_rank = [{"rank": rank, "users": [u0, u1], "nnz": nnz, "hop_ms_per_step":

@@ -12,15 +12,16 @@ O=gpurun_out/r03_scale
 mkdir -p $O
 export TMPDIR=/tmp
 # progress line for the runner while a rehearsal runs silently (each step has its own limit)
-( while sleep 50; do echo "[rehearsal] $(date +%T) running"; done ) &
+( while sleep 50; do echo "[rehearsal] $(date +%T) running: $(grep -h '^\[bench rank' $O/$(cat $O/current 2>/dev/null).err 2>/dev/null | tail -1)"; done ) &
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
 run() {  # name, time limit, bench args...
   local name=$1 lim=$2
   shift 2
   echo "[rehearsal] $name: bench.py $*"
+  echo $name > $O/current
   timeout -k 10 "$lim" python bench.py --check --no-cpu-baseline --pmc off \
-    "$@" > $O/$name.json 2> $O/$name.err || { echo "FAILED rc=$? $name"; tail -20 $O/$name.err; exit 1; }
+    "$@" > $O/$name.json 2> $O/$name.err || { echo "FAILED rc=$? $name"; grep '^\[bench rank' $O/$name.err | tail -20; tail -5 $O/$name.err; exit 1; }
   python - "$O/$name.json" <<'EOF'
 import json, sys
 line = [l for l in open(sys.argv[1]) if l.startswith("{")][-1]
@@ -41,6 +42,6 @@ for spec in ${REH_RUNS:-"p2p:4:64 p2p:8:64 p2p:4:256 p2p:8:256"}; do
   IFS=: read tr n d <<< "$spec"
   extra=""
   [ "$tr" = p2p ] && extra="--transport p2p"
-  HGD_DIST_BACKEND=gloo run ${tr}_n${n}_d${d} 420 --gpus $n --dim $d $extra $STEPS
+  HGD_DIST_BACKEND=gloo run ${tr}_n${n}_d${d} ${REH_LIMIT:-420} --gpus $n --dim $d $extra $STEPS
 done
 echo "[rehearsal] all ok"
