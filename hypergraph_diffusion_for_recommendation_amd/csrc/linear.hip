@@ -21,6 +21,7 @@
 //    permuted; the 4 waves are combined in LDS in wave order, the S slice partials by sum_rows in
 //    slice order. No atomics: results are bitwise reproducible.
 #include <algorithm>
+#include <type_traits>
 
 #include "linear_common.h"
 
@@ -902,6 +903,212 @@ __global__ __launch_bounds__(kX3SplitKThreads) void k_splitk_tn_x3(SplitKGroup g
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Weight gradient with producer waves (dW = (dY ⊙ mask)ᵀ·X, db = Σ dY ⊙ mask; M = N = 128): the
+// row-GEMM's structure applied to split-K. A workgroup owns one row slice and the whole 128 × 128
+// output, so each operand row is read ONCE (the 64 × 64-tile f32 kernel read both twice: 2.0× the
+// algorithmic bytes, profiles/r03_linear/pmc). 16 waves:
+//
+//  * 8 producer waves stream 32-row stages of both operands (waves 8–11 dY and its ReLU mask,
+//    12–15 X) through a register ring two stages deep: each thread loads a 4-row × 4-column
+//    block (float4 per row; a wave instruction covers two full 512-B rows), applies the mask /
+//    binarization (dY) or the input dropout and row scale (X), splits every column's four values
+//    into the three bf16 terms and writes them as 8-byte halves of the MFMA fragments, both
+//    operands TRANSPOSED in LDS (fragment (column c, k-group g) = rows 8g .. 8g + 7 of column c);
+//  * 8 consumer waves multiply the previous stage: wave (mp, nq) owns output tiles 2mp .. 2mp + 1
+//    × 4nq .. 4nq + 3 (16 × 16 each) and runs 6 split-bf16 MFMAs per tile per stage;
+//  * fragment unit (c, g) sits at 16-B unit c·4 + (g ^ ((c >> 1) & 3)) and producer b writes
+//    its columns in the order (c + (cb >> 1)) & 3: conflict-free ds_read_b128 (lane groups
+//    {0–3,12–15,20–27}, …) and ds_write_b64 (16 consecutive lanes) on gfx950 (searched
+//    exhaustively over the candidate swizzles);
+//  * the slice's partial tile and column sums go to `part` / `part_bias` as the other split-K
+//    kernels' (summed by sum_rows in slice order).
+constexpr int kX3pThreads = 1024;
+constexpr int kX3pResident = 256;  // one workgroup per CU
+constexpr size_t kX3pPlane = 128 * 4 * 16;         // one operand, one bf16 term: 8 KB
+constexpr size_t kX3pLds = 2 * 2 * 3 * kX3pPlane;  // [buffer][operand][term] = 96 KB
+
+__device__ __forceinline__ int x3p_unit(int c, int g) { return c * 4 + (g ^ ((c >> 1) & 3)); }
+
+template <bool MASK>
+__global__ __launch_bounds__(kX3pThreads) void k_splitk_x3p(SplitKGroup grp) {
+  extern __shared__ __attribute__((aligned(16))) char x3p_smem[];
+  const bool second = grp.count > 1 && static_cast<int>(blockIdx.x) >= grp.nb0;
+  const SplitK p = second ? grp.p[1] : grp.p[0];
+  const int64_t bx = static_cast<int64_t>(blockIdx.x) - (second ? grp.nb0 : 0);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int i16 = lane & 15;
+  const int g = lane >> 4;
+  const int64_t k_begin = bx * p.rows_per_split;
+  const int64_t k_end = min(p.rows, k_begin + p.rows_per_split);
+  const int64_t n_st = k_end > k_begin ? (k_end - k_begin + 31) / 32 : 0;
+  auto plane = [&](int buf, int op, int term) -> char* {
+    return x3p_smem + static_cast<size_t>((buf * 2 + op) * 3 + term) * kX3pPlane;
+  };
+  float bsum[4] = {0.f, 0.f, 0.f, 0.f};  // dY producers: column sums of their block
+  const int pt = tid - 512;              // producer thread index
+  const int pb = pt & 255, gq = pb >> 6, hh = pb & 1, cb = (pb >> 1) & 31;
+
+  // one producer role (OP 0: dY [+ mask], 1: X): a loop of exactly n_st barriers
+  auto produce = [&](auto op_tag) {
+    constexpr int OP = decltype(op_tag)::value;
+    const float* base = OP == 0 ? p.A : p.B;
+    const int64_t ld = OP == 0 ? p.lda : p.ldb;
+    uint32_t off[4], moff[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t r = 8 * gq + 4 * hh + j;
+      off[j] = (r * static_cast<uint32_t>(ld) + 4 * cb) * 4;
+      moff[j] = (r * static_cast<uint32_t>(p.ldm) + 4 * cb) * 4;
+    }
+    const uint64_t seed = p.b_drop_seed ? *p.b_drop_seed : 0ull;
+    const uint32_t thr = dropout_threshold(p.b_drop_keep);
+    constexpr int D = 2;
+    f32x4 raw[D][4], rawm[D][4];
+    auto load = [&](int64_t s, f32x4 (&a)[4], f32x4 (&m)[4]) {
+      const int64_t r0 = k_begin + 32 * s;
+      const uint32_t nr = s < n_st ? static_cast<uint32_t>(min<int64_t>(32, k_end - r0)) : 0u;
+      const int64_t rb0 = nr ? r0 : 0;
+      const auto rs = buf_rsrc(base + rb0 * ld, nr * static_cast<uint32_t>(ld) * 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] = buf_ld4(rs, off[j]);
+      if constexpr (OP == 0 && MASK) {
+        const auto rm = buf_rsrc(p.mask + rb0 * p.ldm, nr * static_cast<uint32_t>(p.ldm) * 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) m[j] = buf_ld4(rm, moff[j]);
+      }
+    };
+    auto split = [&](int64_t s, int buf, const f32x4 (&a)[4], const f32x4 (&m)[4]) {
+      const int64_t r0 = k_begin + 32 * s + 8 * gq + 4 * hh;  // this block's first row
+      f32x4 v[4];                                              // v[j] = row j, columns 0..3
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        f32x4 x = a[j];
+        if constexpr (OP == 0) {
+          if constexpr (MASK) x = relu_mask(x, m[j]);
+          if (p.binarize_a) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) x[c] = x[c] > 0.f ? 1.f : 0.f;
+          }
+#pragma unroll
+          for (int c = 0; c < 4; ++c) bsum[c] += x[c];
+        } else {
+          if (p.b_drop_seed) {  // keep group of elements row·N + 4cb .. + 3
+            const uint32_t e = static_cast<uint32_t>((r0 + j) * p.N + 4 * cb);
+            x = dropout_apply4(x, seed, e >> 2, thr, p.b_drop_scale);
+          }
+        }
+        v[j] = x;
+      }
+      if constexpr (OP == 1) {
+        if (p.b_row_scale) {  // fl(B · scale), as a pre-scaled B would hold it
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int64_t r = r0 + j < k_end ? r0 + j : k_begin;
+            v[j] *= p.b_row_scale[r];
+          }
+        }
+      }
+#pragma unroll
+      for (int c0 = 0; c0 < 4; ++c0) {
+        const int c = (c0 + (cb >> 1)) & 3;
+        const f32x4 col{v[0][c], v[1][c], v[2][c], v[3][c]};
+        bf16x4 t0, t1, t2;
+        split3x4(col, t0, t1, t2);
+        const size_t o = static_cast<size_t>(x3p_unit(4 * cb + c, gq)) * 16 + 8 * hh;
+        *reinterpret_cast<bf16x4*>(plane(buf, OP, 0) + o) = t0;
+        *reinterpret_cast<bf16x4*>(plane(buf, OP, 1) + o) = t1;
+        *reinterpret_cast<bf16x4*>(plane(buf, OP, 2) + o) = t2;
+      }
+    };
+#pragma unroll
+    for (int d = 0; d < D; ++d) load(d, raw[d], rawm[d]);
+    if (n_st > 0) {
+      split(0, 0, raw[0], rawm[0]);
+      load(D, raw[0], rawm[0]);
+    }
+    auto pstep = [&](int64_t i, bool has_next, f32x4 (&a)[4], f32x4 (&m)[4]) {
+      __syncthreads();
+      if (has_next) {
+        split(i + 1, static_cast<int>((i + 1) & 1), a, m);
+        load(i + 1 + D, a, m);
+      }
+    };
+    int64_t i0 = 0;
+    for (; i0 + D < n_st; i0 += D) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) pstep(i0 + d, true, raw[(d + 1) % D], rawm[(d + 1) % D]);
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      if (i0 + d < n_st) pstep(i0 + d, i0 + d + 1 < n_st, raw[(d + 1) % D], rawm[(d + 1) % D]);
+    }
+  };
+
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[t][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int mp = wave & 3, nq = (wave >> 2) & 1;
+  if (wave >= 12) {
+    produce(std::integral_constant<int, 1>{});
+  } else if (wave >= 8) {
+    produce(std::integral_constant<int, 0>{});
+  } else {
+    for (int64_t i = 0; i < n_st; ++i) {
+      __syncthreads();
+      const int buf = static_cast<int>(i & 1);
+      bf16x8 af[2][3];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int tm = 0; tm < 3; ++tm)
+          af[t][tm] = *reinterpret_cast<const bf16x8*>(
+              plane(buf, 0, tm) + static_cast<size_t>(x3p_unit(16 * (2 * mp + t) + i16, g)) * 16);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        bf16x8 bf[3];
+#pragma unroll
+        for (int tm = 0; tm < 3; ++tm)
+          bf[tm] = *reinterpret_cast<const bf16x8*>(
+              plane(buf, 1, tm) + static_cast<size_t>(x3p_unit(16 * (4 * nq + u) + i16, g)) * 16);
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          acc[t][u] = mfma_x3(af[t][0], af[t][1], af[t][2], bf[0], bf[1], bf[2], acc[t][u], false);
+      }
+    }
+  }
+  mfma_drain();
+  __syncthreads();  // the planes are free: column sums of the dY producers through LDS
+  float* s_b = reinterpret_cast<float*>(x3p_smem);  // [4 k-groups · 2 halves][128]
+  if (wave >= 8 && wave < 12) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) s_b[(2 * gq + hh) * 128 + 4 * cb + c] = bsum[c];
+  }
+  const int64_t MN = static_cast<int64_t>(p.M) * p.N;
+  if (wave < 8) {
+    // acc[t][u] lane (i16, g) register r: m = 16(2mp + t) + 4g + r, n = 16(4nq + u) + i16
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = 16 * (2 * mp + t) + 4 * g + r, n = 16 * (4 * nq + u) + i16;
+          p.part[bx * MN + static_cast<int64_t>(m) * p.N + n] = acc[t][u][r];
+        }
+  }
+  __syncthreads();
+  if (p.part_bias != nullptr && tid < 128) {
+    float v = 0.f;
+    for (int q = 0; q < 8; ++q) v += s_b[q * 128 + tid];
+    p.part_bias[bx * p.M + tid] = v;
+  }
+}
+
 bool al16(const void* p, int64_t ld) {
   return p == nullptr || (reinterpret_cast<uintptr_t>(p) % 16 == 0 && ld % 4 == 0);
 }
@@ -1080,6 +1287,23 @@ int64_t splits_for(int64_t rows, int64_t out_tiles) {
   return s < 1 ? 1 : s;
 }
 
+// The producer-wave weight gradient (k_splitk_x3p): 128 × 128 outputs whose operand rows are
+// 16-byte aligned and addressable in 32-bit block offsets, by default (HGD_TUNE_X3_SPLITK = 2)
+bool use_x3p_splitk(const hgd_gemm_tn_desc* d, int count) {
+  if (g_gemm_exact || g_x3_splitk != 2) return false;
+  int64_t rows = 0;
+  constexpr int64_t kLdMax = int64_t{1} << 22;
+  for (int i = 0; i < count; ++i) {
+    if (d[i].rows <= 0) continue;
+    if (d[i].M != 128 || d[i].N != 128) return false;
+    if (!al16(d[i].A, d[i].lda) || !al16(d[i].B, d[i].ldb) || !al16(d[i].relu_mask, d[i].ldm))
+      return false;
+    if (d[i].lda >= kLdMax || d[i].ldb >= kLdMax || d[i].ldm >= kLdMax) return false;
+    rows += d[i].rows;
+  }
+  return rows >= 4096;
+}
+
 // Row slices of each product of a split-K group (the pair shares the resident budget).
 void tn_splits(const hgd_gemm_tn_desc* d, int count, int64_t* S, int64_t* per) {
   const bool x3 = use_x3_splitk(d, count);
@@ -1087,6 +1311,22 @@ void tn_splits(const hgd_gemm_tn_desc* d, int count, int64_t* S, int64_t* per) {
     for (int i = 0; i < count; ++i) {
       per[i] = g_splitk_rows;
       S[i] = std::max<int64_t>(1, (std::max<int64_t>(d[i].rows, 1) + per[i] - 1) / per[i]);
+    }
+    return;
+  }
+  if (use_x3p_splitk(d, count)) {  // one 1024-thread workgroup per slice, ≥ 64 rows each
+    int64_t total = 0;
+    for (int i = 0; i < count; ++i) {
+      S[i] = std::min<int64_t>(std::max<int64_t>(1, (std::max<int64_t>(d[i].rows, 1) + 63) / 64),
+                               kX3pResident);
+      total += S[i];
+    }
+    for (int i = 0; i < count; ++i) {
+      if (count > 1 && total > kX3pResident)
+        S[i] = std::max<int64_t>(1, S[i] * kX3pResident / total);
+      const int64_t rows = d[i].rows > 0 ? d[i].rows : 1;
+      per[i] = ((rows + S[i] - 1) / S[i] + 31) / 32 * 32;  // whole 32-row stages
+      S[i] = (rows + per[i] - 1) / per[i];
     }
     return;
   }
@@ -1334,7 +1574,22 @@ extern "C" hgd_status hgd_gemm_tn(const hgd_gemm_tn_desc* descs, int32_t count, 
     }
   const dim3 grid(static_cast<unsigned>(Stot), static_cast<unsigned>((g.p[0].M + 63) / 64),
                   static_cast<unsigned>((g.p[0].N + 63) / 64));
-  if (use_x3_splitk(descs, count)) {
+  if (use_x3p_splitk(descs, count)) {
+    const void* kern = g.p[0].mask ? reinterpret_cast<const void*>(&k_splitk_x3p<true>)
+                                   : reinterpret_cast<const void*>(&k_splitk_x3p<false>);
+    static bool lds_set[2] = {false, false};
+    if (!lds_set[g.p[0].mask ? 1 : 0]) {
+      HGD_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  static_cast<int>(kX3pLds)));
+      lds_set[g.p[0].mask ? 1 : 0] = true;
+    }
+    if (g.p[0].mask)
+      hipLaunchKernelGGL((k_splitk_x3p<true>), dim3(static_cast<unsigned>(Stot)), dim3(kX3pThreads),
+                         kX3pLds, st, g);
+    else
+      hipLaunchKernelGGL((k_splitk_x3p<false>), dim3(static_cast<unsigned>(Stot)),
+                         dim3(kX3pThreads), kX3pLds, st, g);
+  } else if (use_x3_splitk(descs, count)) {
     const int tiles = ((g.p[0].M + 63) / 64) * ((g.p[0].N + 31) / 32);
     const dim3 gx(static_cast<unsigned>(Stot),
                   static_cast<unsigned>(tiles / x3_tiles_per_wg(tiles)));

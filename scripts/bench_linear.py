@@ -85,10 +85,15 @@ def main():
                 dY.data_ptr(), d, None, 0, X.data_ptr(), d, n, d, d, dW.data_ptr(),
                 db.data_ptr(), ws.data_ptr(), wsb, st),
             "bwd_weight_torch": lambda: (torch.mm(dY.t(), X), dY.sum(0)),
+            # the ED-HNN weight gradient: dY masked by the forward's ReLU output
+            "bwd_weight_mask_hgd": lambda: lib.hgd_linear_backward_weight(
+                dY.data_ptr(), d, Y.data_ptr(), d, X.data_ptr(), d, n, d, d, dW.data_ptr(),
+                db.data_ptr(), ws.data_ptr(), wsb, st),
             # the HBM reference point: one read and one write of the same bytes as the forward
             "copy_torch": lambda: Y.copy_(X),
         }
-        algo = {"fwd": 2 * n * d * 4, "fwd_drop": 2 * n * d * 4, "fwd_drop_res": 4 * n * d * 4, "bwd_data": 3 * n * d * 4, "bwd_weight": 2 * n * d * 4, "copy": 2 * n * d * 4}
+        algo = {"fwd": 2 * n * d * 4, "fwd_drop": 2 * n * d * 4, "fwd_drop_res": 4 * n * d * 4, "bwd_data": 3 * n * d * 4, "bwd_weight": 2 * n * d * 4, "bwd_weight_mask": 3 * n * d * 4,
+                "copy": 2 * n * d * 4}
         for name, fn in cases.items():
             if args.cases and name not in args.cases:
                 continue
