@@ -25,7 +25,7 @@ import torch
 import torch.nn as nn
 
 from .functional import (dense_two_hop_pair, fan, hccf_layers, hccf_layers_supported, linear,
-                         sum_n, two_hop_fused)
+                         split_rows, sum_n, two_hop_fused)
 from .incidence import Incidence, incidence_of
 from .layers import EquivSetGNN, GCNLayer, HGCNConv, HGNNLayer, LayerNorm, SpAdjDropEdge
 
@@ -185,7 +185,7 @@ class LocalAwareEncoder(nn.Module):
                                                norm=self.lns[0], res1=res[k], res1_scale=1.0)
             all_embeddings += [ego_embeddings]
         nu = self.data.n_users
-        return all_embeddings[-1][:nu], all_embeddings[-1][nu:]
+        return split_rows(all_embeddings[-1], nu)
 
 
 class HCCFDiffusionEncoder(HCCFEncoder):
@@ -233,7 +233,7 @@ class HCCFDiffusionEncoder(HCCFEncoder):
             hgnn_hidden += [hyp]
             hidden += [gcn_emb + hyp]
         emb = sum_n(terms + [hidden[-1]])  # sum(hidden), same order, one pass
-        return emb[:nu], emb[nu:], gcn_hidden, hgnn_hidden
+        return (*split_rows(emb, nu), gcn_hidden, hgnn_hidden)
 
 
 class LocalAwareEncoderHD3(nn.Module):
@@ -279,7 +279,7 @@ class LocalAwareEncoderHD3(nn.Module):
                 ego_embeddings = two_hop_fused(incidence_of(self.sparse_norm_adj), ego_embeddings,
                                                norm=self.lns[k], res1=res[k], res1_scale=1.0)
         nu = self.data.n_users
-        return ego_embeddings[:nu], ego_embeddings[nu:]
+        return split_rows(ego_embeddings, nu)
 
 
 def ugformer_layers(hyper_size, n_layers, drop_rate, device=None) -> nn.ModuleList:
@@ -356,7 +356,7 @@ class SelfAwareEncoder(nn.Module):
         ego_embeddings = _hgcn_ln_res_stack(inc, ego_embeddings, list(self.lns), self.leaky,
                                             ego_embeddings, attend)
         nu = self.data.n_users
-        return ego_embeddings[:nu], ego_embeddings[nu:]
+        return split_rows(ego_embeddings, nu)
 
 
 class RelationalAwareEncoder(nn.Module):
@@ -430,4 +430,4 @@ class SelfAwareEncoderHD(nn.Module):
             blk = self.edhnn_layers[0 if k != self.layers - 1 else 1]
             ego_embeddings = blk(ego_embeddings, self.sparse_norm_adj, self.edhnn_ui_n) + res[k]
         nu = self.data.n_users
-        return ego_embeddings[:nu], ego_embeddings[nu:]
+        return split_rows(ego_embeddings, nu)

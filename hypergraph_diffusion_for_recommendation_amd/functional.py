@@ -408,6 +408,14 @@ class _Fan(torch.autograd.Function):
         return out, None
 
 
+def split_rows(x: torch.Tensor, nu: int):
+    """``(x[:nu], x[nu:])`` (the encoders' user / item halves of the node table) as one split:
+    its backward is ONE cat of the two gradients, where two slicing views each materialise a
+    zero-filled full table, copy their half into it and add the two (≈ 90 µs per LocalAware step
+    at 144 k × 128: two fills, two copies and a full-table add)."""
+    return torch.split(x, [nu, x.shape[0] - nu], dim=0)
+
+
 def fan(x: torch.Tensor, n: int):
     """``n`` uses of ``x`` (e.g. HGNN_HD4's layer-0 residual ``res``, read by every layer,
     HGNN_HD4.py:390-405) whose gradients are summed in one pass. Off the device path (or for

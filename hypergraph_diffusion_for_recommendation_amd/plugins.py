@@ -46,8 +46,7 @@ from torch.optim.lr_scheduler import ReduceLROnPlateau
 from .encoders import (HCCFDiffusionEncoder, HCCFEncoder, LocalAwareEncoder,
                        LocalAwareEncoderHD3, sparse_tensor_of)
 from .functional import (bpr_index_errors, bpr_loss_rows, contrast_loss, contrast_loss_pair,
-                         unique_long,
-                         unique_long_n)
+                         split_rows, unique_long, unique_long_n)
 from .layers import HGCNConv, SpAdjDropEdge
 from .sampler import next_batch_pairwise
 from .selfrec import GraphRecommender, early_stopping
@@ -442,7 +441,7 @@ class HGCN_Encoder(nn.Module):
             all_embeddings += [ego]
         all_embeddings[-1] = all_embeddings[-1] + res
         nu = self.data.n_users
-        return all_embeddings[-1][:nu], all_embeddings[-1][nu:]
+        return split_rows(all_embeddings[-1], nu)
 
 
 class HGCN(GraphRecommender):
