@@ -907,31 +907,42 @@ __global__ __launch_bounds__(kX3SplitKThreads) void k_splitk_tn_x3(SplitKGroup g
 // Weight gradient with producer waves (dW = (dY ⊙ mask)ᵀ·X, db = Σ dY ⊙ mask; M = N = 128): the
 // row-GEMM's structure applied to split-K. A workgroup owns one row slice and the whole 128 × 128
 // output, so each operand row is read ONCE (the 64 × 64-tile f32 kernel read both twice: 2.0× the
-// algorithmic bytes, profiles/r03_linear/pmc). 16 waves:
+// algorithmic bytes, profiles/r03_linear/pmc). At 128 × 128, 16 waves (at 64 × 64, 12):
 //
-//  * 8 producer waves stream 32-row stages of both operands (waves 8–11 dY and its ReLU mask,
-//    12–15 X) through a register ring two stages deep: each thread loads a 4-row × 4-column
+//  * 8 (4) producer waves stream 32-row stages of both operands (the first half dY and its ReLU
+//    mask, the second X) through a register ring two stages deep: each thread loads a 4-row × 4-column
 //    block (float4 per row; a wave instruction covers two full 512-B rows), applies the mask /
 //    binarization (dY) or the input dropout and row scale (X), splits every column's four values
 //    into the three bf16 terms and writes them as 8-byte halves of the MFMA fragments, both
 //    operands TRANSPOSED in LDS (fragment (column c, k-group g) = rows 8g .. 8g + 7 of column c);
-//  * 8 consumer waves multiply the previous stage: wave (mp, nq) owns output tiles 2mp .. 2mp + 1
-//    × 4nq .. 4nq + 3 (16 × 16 each) and runs 6 split-bf16 MFMAs per tile per stage;
+//  * 8 consumer waves multiply the previous stage: wave (mp, nq) owns output tiles
+//    TM·mp .. + TM - 1 × TN·nq .. + TN - 1 (16 × 16 each; TM × TN = 2 × 4 at 128, 1 × 2 at 64)
+//    and runs 6 split-bf16 MFMAs per tile per stage;
 //  * fragment unit (c, g) sits at 16-B unit c·4 + (g ^ ((c >> 1) & 3)) and producer b writes
 //    its columns in the order (c + (cb >> 1)) & 3: conflict-free ds_read_b128 (lane groups
 //    {0–3,12–15,20–27}, …) and ds_write_b64 (16 consecutive lanes) on gfx950 (searched
 //    exhaustively over the candidate swizzles);
 //  * the slice's partial tile and column sums go to `part` / `part_bias` as the other split-K
 //    kernels' (summed by sum_rows in slice order).
-constexpr int kX3pThreads = 1024;
+// MT = 16-column output tiles per side (8: 128 × 128, 16 waves; 4: 64 × 64, 8 consumer + 4
+// producer waves, each consumer two tiles).
 constexpr int kX3pResident = 256;  // one workgroup per CU
-constexpr size_t kX3pPlane = 128 * 4 * 16;         // one operand, one bf16 term: 8 KB
-constexpr size_t kX3pLds = 2 * 2 * 3 * kX3pPlane;  // [buffer][operand][term] = 96 KB
+template <int MT>
+struct X3P {
+  static constexpr int C4 = 4 * MT;                     // 4-column blocks of an operand row
+  static constexpr int PROD = 2 * 8 * C4;               // producer threads (both operands)
+  static constexpr int THREADS = 512 + PROD;            // + 8 consumer waves
+  static constexpr int TM = MT / 4, TN = MT / 2;        // output tiles of a consumer wave
+  static constexpr size_t PLANE = static_cast<size_t>(MT) * 16 * 4 * 16;  // one operand, one term
+  static constexpr size_t LDS = 2 * 2 * 3 * PLANE;      // [buffer][operand][term]
+};
 
 __device__ __forceinline__ int x3p_unit(int c, int g) { return c * 4 + (g ^ ((c >> 1) & 3)); }
 
-template <bool MASK>
-__global__ __launch_bounds__(kX3pThreads) void k_splitk_x3p(SplitKGroup grp) {
+template <int MT, bool MASK>
+__global__ __launch_bounds__(X3P<MT>::THREADS) void k_splitk_x3p(SplitKGroup grp) {
+  using C = X3P<MT>;
+  constexpr size_t kX3pPlane = C::PLANE;
   extern __shared__ __attribute__((aligned(16))) char x3p_smem[];
   const bool second = grp.count > 1 && static_cast<int>(blockIdx.x) >= grp.nb0;
   const SplitK p = second ? grp.p[1] : grp.p[0];
@@ -949,7 +960,7 @@ __global__ __launch_bounds__(kX3pThreads) void k_splitk_x3p(SplitKGroup grp) {
   };
   float bsum[4] = {0.f, 0.f, 0.f, 0.f};  // dY producers: column sums of their block
   const int pt = tid - 512;              // producer thread index
-  const int pb = pt & 255, gq = pb >> 6, hh = pb & 1, cb = (pb >> 1) & 31;
+  const int pb = pt % (8 * C::C4), gq = pb / (2 * C::C4), hh = pb & 1, cb = (pb >> 1) % C::C4;
 
   // one producer role (OP 0: dY [+ mask], 1: X): a loop of exactly n_st barriers
   auto produce = [&](auto op_tag) {
@@ -1047,13 +1058,13 @@ __global__ __launch_bounds__(kX3pThreads) void k_splitk_x3p(SplitKGroup grp) {
     }
   };
 
-  f32x4 acc[2][4];
+  f32x4 acc[C::TM][C::TN];
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < C::TM; ++t)
 #pragma unroll
-    for (int u = 0; u < 4; ++u) acc[t][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < C::TN; ++u) acc[t][u] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int mp = wave & 3, nq = (wave >> 2) & 1;
-  if (wave >= 12) {
+  if (tid >= 512 + 8 * C::C4) {
     produce(std::integral_constant<int, 1>{});
   } else if (wave >= 8) {
     produce(std::integral_constant<int, 0>{});
@@ -1061,50 +1072,53 @@ __global__ __launch_bounds__(kX3pThreads) void k_splitk_x3p(SplitKGroup grp) {
     for (int64_t i = 0; i < n_st; ++i) {
       __syncthreads();
       const int buf = static_cast<int>(i & 1);
-      bf16x8 af[2][3];
+      bf16x8 af[C::TM][3];
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < C::TM; ++t)
 #pragma unroll
         for (int tm = 0; tm < 3; ++tm)
           af[t][tm] = *reinterpret_cast<const bf16x8*>(
-              plane(buf, 0, tm) + static_cast<size_t>(x3p_unit(16 * (2 * mp + t) + i16, g)) * 16);
+              plane(buf, 0, tm) +
+              static_cast<size_t>(x3p_unit(16 * (C::TM * mp + t) + i16, g)) * 16);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < C::TN; ++u) {
         bf16x8 bf[3];
 #pragma unroll
         for (int tm = 0; tm < 3; ++tm)
           bf[tm] = *reinterpret_cast<const bf16x8*>(
-              plane(buf, 1, tm) + static_cast<size_t>(x3p_unit(16 * (4 * nq + u) + i16, g)) * 16);
+              plane(buf, 1, tm) +
+              static_cast<size_t>(x3p_unit(16 * (C::TN * nq + u) + i16, g)) * 16);
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+        for (int t = 0; t < C::TM; ++t)
           acc[t][u] = mfma_x3(af[t][0], af[t][1], af[t][2], bf[0], bf[1], bf[2], acc[t][u], false);
       }
     }
   }
   mfma_drain();
   __syncthreads();  // the planes are free: column sums of the dY producers through LDS
-  float* s_b = reinterpret_cast<float*>(x3p_smem);  // [4 k-groups · 2 halves][128]
-  if (wave >= 8 && wave < 12) {
+  constexpr int M = 16 * MT;
+  float* s_b = reinterpret_cast<float*>(x3p_smem);  // [4 k-groups · 2 halves][M]
+  if (tid >= 512 && tid < 512 + 8 * C::C4) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c) s_b[(2 * gq + hh) * 128 + 4 * cb + c] = bsum[c];
+    for (int c = 0; c < 4; ++c) s_b[(2 * gq + hh) * M + 4 * cb + c] = bsum[c];
   }
   const int64_t MN = static_cast<int64_t>(p.M) * p.N;
   if (wave < 8) {
-    // acc[t][u] lane (i16, g) register r: m = 16(2mp + t) + 4g + r, n = 16(4nq + u) + i16
+    // acc[t][u] lane (i16, g) register r: m = 16(TM·mp + t) + 4g + r, n = 16(TN·nq + u) + i16
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < C::TM; ++t)
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < C::TN; ++u)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int m = 16 * (2 * mp + t) + 4 * g + r, n = 16 * (4 * nq + u) + i16;
+          const int m = 16 * (C::TM * mp + t) + 4 * g + r, n = 16 * (C::TN * nq + u) + i16;
           p.part[bx * MN + static_cast<int64_t>(m) * p.N + n] = acc[t][u][r];
         }
   }
   __syncthreads();
-  if (p.part_bias != nullptr && tid < 128) {
+  if (p.part_bias != nullptr && tid < M) {
     float v = 0.f;
-    for (int q = 0; q < 8; ++q) v += s_b[q * 128 + tid];
+    for (int q = 0; q < 8; ++q) v += s_b[q * M + tid];
     p.part_bias[bx * p.M + tid] = v;
   }
 }
@@ -1287,7 +1301,28 @@ int64_t splits_for(int64_t rows, int64_t out_tiles) {
   return s < 1 ? 1 : s;
 }
 
-// The producer-wave weight gradient (k_splitk_x3p): 128 × 128 outputs whose operand rows are
+template <int MT>
+hgd_status launch_x3p(const SplitKGroup& g, int64_t Stot, hipStream_t st) {
+  using C = X3P<MT>;
+  static bool lds_set[2] = {false, false};
+  const int mi = g.p[0].mask ? 1 : 0;
+  if (!lds_set[mi]) {
+    const void* kern = mi ? reinterpret_cast<const void*>(&k_splitk_x3p<MT, true>)
+                          : reinterpret_cast<const void*>(&k_splitk_x3p<MT, false>);
+    if (C::LDS > 65536)
+      HGD_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  static_cast<int>(C::LDS)));
+    lds_set[mi] = true;
+  }
+  const dim3 grid(static_cast<unsigned>(Stot));
+  if (mi)
+    hipLaunchKernelGGL((k_splitk_x3p<MT, true>), grid, dim3(C::THREADS), C::LDS, st, g);
+  else
+    hipLaunchKernelGGL((k_splitk_x3p<MT, false>), grid, dim3(C::THREADS), C::LDS, st, g);
+  return HGD_OK;
+}
+
+// The producer-wave weight gradient (k_splitk_x3p): 128 × 128 or 64 × 64 outputs whose operand rows are
 // 16-byte aligned and addressable in 32-bit block offsets, by default (HGD_TUNE_X3_SPLITK = 2)
 bool use_x3p_splitk(const hgd_gemm_tn_desc* d, int count) {
   if (g_gemm_exact || g_x3_splitk != 2) return false;
@@ -1295,7 +1330,7 @@ bool use_x3p_splitk(const hgd_gemm_tn_desc* d, int count) {
   constexpr int64_t kLdMax = int64_t{1} << 22;
   for (int i = 0; i < count; ++i) {
     if (d[i].rows <= 0) continue;
-    if (d[i].M != 128 || d[i].N != 128) return false;
+    if (d[i].M != d[i].N || (d[i].M != 128 && d[i].M != 64) || d[i].M != d[0].M) return false;
     if (!al16(d[i].A, d[i].lda) || !al16(d[i].B, d[i].ldb) || !al16(d[i].relu_mask, d[i].ldm))
       return false;
     if (d[i].lda >= kLdMax || d[i].ldb >= kLdMax || d[i].ldm >= kLdMax) return false;
@@ -1575,20 +1610,8 @@ extern "C" hgd_status hgd_gemm_tn(const hgd_gemm_tn_desc* descs, int32_t count, 
   const dim3 grid(static_cast<unsigned>(Stot), static_cast<unsigned>((g.p[0].M + 63) / 64),
                   static_cast<unsigned>((g.p[0].N + 63) / 64));
   if (use_x3p_splitk(descs, count)) {
-    const void* kern = g.p[0].mask ? reinterpret_cast<const void*>(&k_splitk_x3p<true>)
-                                   : reinterpret_cast<const void*>(&k_splitk_x3p<false>);
-    static bool lds_set[2] = {false, false};
-    if (!lds_set[g.p[0].mask ? 1 : 0]) {
-      HGD_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  static_cast<int>(kX3pLds)));
-      lds_set[g.p[0].mask ? 1 : 0] = true;
-    }
-    if (g.p[0].mask)
-      hipLaunchKernelGGL((k_splitk_x3p<true>), dim3(static_cast<unsigned>(Stot)), dim3(kX3pThreads),
-                         kX3pLds, st, g);
-    else
-      hipLaunchKernelGGL((k_splitk_x3p<false>), dim3(static_cast<unsigned>(Stot)),
-                         dim3(kX3pThreads), kX3pLds, st, g);
+    hgd_status ls = g.p[0].M == 128 ? launch_x3p<8>(g, Stot, st) : launch_x3p<4>(g, Stot, st);
+    if (ls != HGD_OK) return ls;
   } else if (use_x3_splitk(descs, count)) {
     const int tiles = ((g.p[0].M + 63) / 64) * ((g.p[0].N + 31) / 32);
     const dim3 gx(static_cast<unsigned>(Stot),
