@@ -76,9 +76,12 @@ typedef enum hgd_epilogue {
  *                         1 = the exact f32-input MFMA kernels only (bitwise k-ordered fmaf)
  *   HGD_TUNE_X3_COLS:     output columns per workgroup of the split-bf16 row GEMM (64 or 128;
  *                         0 = default)
- *   HGD_TUNE_X3_SPLITK:   1 = the split-bf16 split-K weight gradient when HGD_TUNE_GEMM_EXACT
- *                         is 0; 0 = the f32-MFMA split-K kernel; 2 (default) = split-bf16 for
- *                         outputs ≤ 64 × 64 over ≥ 49,152 rows, else f32 MFMA
+ *   HGD_TUNE_X3_SPLITK:   weight-gradient (split-K) kernel when HGD_TUNE_GEMM_EXACT is 0:
+ *                         2 (default) = by shape: the producer-wave split-bf16 kernel for
+ *                         64 × 64 and 128 × 128 outputs (16-byte aligned rows, ≥ 4,096 rows),
+ *                         the one-wave-per-tile split-bf16 kernel for other outputs ≤ 64 × 64
+ *                         over ≥ 49,152 rows, else the f32-MFMA kernel; 1 = always the
+ *                         one-wave-per-tile split-bf16 kernel; 0 = always f32 MFMA
  *   HGD_TUNE_X3S_TILES:   form of the staged split-bf16 row GEMM at N > 32: 1 or 2 16-column
  *                         tiles per wave (1: half the W registers, two workgroups per CU), 3 =
  *                         two tiles + 4 producer waves that load and split the rows while the
