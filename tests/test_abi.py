@@ -120,3 +120,27 @@ def test_c_host_example_compiles_against_the_header(tmp_path):
         if exe is None:
             pytest.skip("gcc not available")
         assert os.path.exists(exe)
+
+
+def test_tuning_keys_validate_their_values():
+    """hgd_set_tuning (host-side globals, no device work): every documented key takes its
+    documented values, rejects others with HGD_ERR_INVALID_ARG, and the defaults restore."""
+    from hypergraph_diffusion_for_recommendation_amd import _native
+    lib = _native.load()
+    good = {1: [8, 16], 2: [0, 1, 8, 9], 3: [0, 64, 128, 256], 4: [0, 64, 8192],
+            5: [0, 64, 65536], 6: [0, 1], 7: [0, 64, 128], 8: [0, 1, 2], 9: [0, 1, 2, 3]}
+    bad = {2: [3], 3: [32], 4: [63], 5: [65], 6: [2], 7: [32], 8: [3, -1], 9: [4, -1]}
+    defaults = {1: 8, 2: 8, 3: 0, 4: 0, 5: 0, 6: 0, 7: 0, 8: 2, 9: 0}
+    try:
+        for key, vals in good.items():
+            for v in vals:
+                assert lib.hgd_set_tuning(key, v) == 0, (key, v)
+        for key, vals in bad.items():
+            for v in vals:
+                assert lib.hgd_set_tuning(key, v) == 1, (key, v)
+        assert lib.hgd_set_tuning(99, 0) == 1
+    finally:
+        for key, v in defaults.items():
+            lib.hgd_set_tuning(key, v)
+    # leave no error text behind for later tests that read hgd_get_last_error_string
+    assert lib.hgd_set_tuning(8, 2) == 0
