@@ -361,8 +361,15 @@ def main():
         init_process_group(device, dist_backend)
         phase("process group up")
 
+    if world > 1:
+        # a rank that stops making progress prints every thread's Python stack (the line it is
+        # blocked in) instead of dying silently at the launcher's limit
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ.get("HGD_STALL_DUMP_S", "600")),
+                                          exit=False)
     shard_kw = dict(n_chunks=args.chunks, P="sym", Q="mean", R="sym",
-                    slice_width=args.slice_width, transport=args.transport)
+                    slice_width=args.slice_width, transport=args.transport,
+                    trace=phase if world > 1 else None)
     bound = (6.0 / (U + d)) ** 0.5  # xavier_uniform_ on the global [U, d] (HCCF.py:164-169)
     keep_global = args.check and strong and world > 1
     # N ranks rehearsed on fewer devices: the graph builds (a 100 M-key sort each) run one rank
@@ -425,8 +432,12 @@ def main():
             graph.replay()
             return static_out
 
-    for _ in range(args.warmup):
+    for k in range(args.warmup):
         step()
+        phase(f"warm-up step {k} issued")
+        if sh.transport == "p2p" and world > 1:
+            sh._p2p.wait()  # bounded: a stalled exchange raises here instead of hanging
+            sh._p2p.check()
     torch.cuda.synchronize()
     phase("warm")
     if world > 1:

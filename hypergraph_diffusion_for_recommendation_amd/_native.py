@@ -184,7 +184,7 @@ SCALE_KINDS = {None: SCALE_NONE, "mean": SCALE_MEAN, "sym": SCALE_SYM, "wmean": 
                "wsym": SCALE_WSYM}
 SIDE_ROWS, SIDE_COLS = 0, 1
 COMM_ID_BYTES = 128
-P2P_HANDLE_BYTES = 128
+P2P_HANDLE_BYTES = 4096
 _PP = ctypes.POINTER(c_void_p)
 
 # name -> (restype, argtypes); every symbol of include/hgd.h appears here.
@@ -306,6 +306,7 @@ _SIGNATURES = {
                                     c_void_p, c_void_p, c_i64, c_i64, c_i32, c_void_p, c_void_p,
                                     c_void_p]),
     "hgd_torch_cpu_state_bytes": (c_size, []),
+    "hgd_torch_cpu_jump_selfcheck": (c_i32, [c_i64]),
     "hgd_torch_cpu_keep_mask": (c_i32, [c_void_p, c_i64, c_i64, c_f32, c_void_p,
                                         ctypes.POINTER(c_i64)]),
     "hgd_epilogue_apply":(c_i32, [c_void_p, c_i64, c_i32, c_f32, c_void_p, c_void_p]),
@@ -359,6 +360,11 @@ _SIGNATURES = {
     "hgd_p2p_set_timeout": (c_i32, [c_void_p, ctypes.c_double]),
     "hgd_p2p_allreduce": (c_i32, [c_void_p, c_i32, c_i64, c_void_p, c_void_p]),
     "hgd_p2p_check": (c_i32, [c_void_p]),
+    "hgd_comm_create_p2p": (c_i32, [c_void_p, c_i32, c_i32, _PP]),
+    "hgd_comm_set_slice_width": (c_i32, [c_void_p, c_i32]),
+    "hgd_p2p_poll": (c_i32, [c_void_p]),
+    "hgd_p2p_n_slots": (c_i32, [c_void_p]),
+    "hgd_p2p_max_count": (c_i64, [c_void_p]),
     "hgd_p2p_block_range": (c_i32, [c_i64, c_i32, c_i32, ctypes.POINTER(c_i64),
                                     ctypes.POINTER(c_i64)]),
     "hgd_p2p_gather_index": (c_i32, [c_i64, c_i32, c_i32, c_i64, ctypes.POINTER(c_i64),
@@ -399,7 +405,9 @@ def load() -> ctypes.CDLL:
         for key, env in ((1, "HGD_SPMM_UNROLL"), (2, "HGD_SPMM_POLICY"),
                          (3, "HGD_SPMM_PASS_COLS"), (4, "HGD_ROWGEMM_BLOCKS"),
                          (5, "HGD_SPLITK_ROWS"), (6, "HGD_GEMM_EXACT"),
-                         (7, "HGD_X3_COLS"), (8, "HGD_X3_SPLITK"), (9, "HGD_X3S_TILES")):
+                         (7, "HGD_X3_COLS"), (8, "HGD_X3_SPLITK"), (9, "HGD_X3S_TILES"),
+                         (10, "HGD_P2P_SEGMENT_MB"), (11, "HGD_P2P_CACHED"),
+                         (12, "HGD_CPU_RNG_THREADS")):
             if os.environ.get(env):
                 st = lib.hgd_set_tuning(key, int(os.environ[env]))
                 if st != HGD_OK:
@@ -504,11 +512,16 @@ def float_view(address: int, shape, device, owner) -> "torch.Tensor":
     rec.deleter = None
     cap = _PyCapsule_New(ctypes.addressof(rec), b"dltensor", None)
     t = torch.utils.dlpack.from_dlpack(cap)
-    # the DLPack record, its shape array and the owner live as long as the tensor object
-    _KEEP[id(t)] = (rec, shp, owner)
+    # torch reads the record (its deleter field) when the STORAGE is released, which any view
+    # of the tensor can delay past the tensor object: the record and its shape array are never
+    # freed (~100 bytes; callers cache their views, e.g. P2PExchange.slot). The owner is kept
+    # alive as long as the tensor object.
+    _RECORDS.append((rec, shp))
+    _KEEP[id(t)] = owner
     import weakref
     weakref.finalize(t, _KEEP.pop, id(t), None)
     return t
 
 
 _KEEP = {}
+_RECORDS = []

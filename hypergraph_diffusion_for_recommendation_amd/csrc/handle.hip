@@ -8,10 +8,16 @@
 // (HGNN_HD4.py:455-462). The compute is the flat ABI's kernels (spmm.hip, structure.hip); this
 // file only sequences them and owns memory.
 //
-// Multi-GPU: one process per GPU, users (rows of H) sharded, items replicated. Hop 1's partial
-// item sums are all-reduced in item chunks on the communicator's side stream, each chunk's
-// ncclAllReduce queued behind the hop kernel that produced it (event), so RCCL moves chunk k
-// over xGMI while the CUs gather chunk k+1.
+// Multi-GPU: one process per GPU, users (rows of H) sharded, items replicated. Two transports
+// for the all-reduce of hop 1's partial item sums, both on the communicator's side stream:
+//  * RCCL (hgd_comm_create): item chunks, each chunk's ncclAllReduce queued behind the hop kernel
+//    that produced it (event), so RCCL moves chunk k over xGMI while the CUs gather chunk k+1;
+//  * the direct peer exchange (hgd_comm_create_p2p over an opened hgd_p2p): the embedding
+//    COLUMNS are cut into slices (32 columns for d <= 128, else 64; hgd_comm_set_slice_width),
+//    hop 1 of slice s writes straight into a send slot of the exchange, the slot's two-shot mesh
+//    reduce runs on the side stream behind it, and hop 2 of slice s waits only for that slice —
+//    the same pipeline, kernels and slot alternation as sharded.ShardedIncidence (transport
+//    'p2p'), so the two give the same bits.
 
 #include <rccl/rccl.h>
 
@@ -75,15 +81,39 @@ __global__ void k_degree_f64(const int64_t* __restrict__ ptr, int64_t n, double*
   if (i < n) deg[i] = static_cast<double>(ptr[i + 1] - ptr[i]);
 }
 
-// Global column scales from the all-reduced degrees: deg^p in float64, inf→0, rounded to fp32
-// (the same arithmetic as sharded.ShardedIncidence._global_col_scale).
+// Global column scales from the all-reduced degrees: 1/deg and 1/sqrt(deg) in float64 (both
+// correctly rounded steps), 0 for an empty column, rounded to fp32 — the arithmetic of
+// hgd_degree_scale and of sharded.ShardedIncidence._global_col_scale, so every path gives the
+// same bits.
 __global__ void k_scale_from_f64(const double* __restrict__ deg, int64_t n,
                                  float* __restrict__ mean, float* __restrict__ sym) {
   const int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
   if (i >= n) return;
   const double g = deg[i];
   mean[i] = g > 0 ? static_cast<float>(1.0 / g) : 0.f;
-  sym[i] = g > 0 ? static_cast<float>(pow(g, -0.5)) : 0.f;
+  sym[i] = g > 0 ? static_cast<float>(1.0 / sqrt(g)) : 0.f;
+}
+
+// Integer degrees as three 16-bit limbs in fp32 (limb k of column i at k·n + i): a sum over <= 8
+// ranks of limbs < 2^16 stays below 2^24, so the peer exchange's fp32 sum is exact.
+__global__ void k_degree_limbs(const int64_t* __restrict__ ptr, int64_t n, int64_t count4,
+                               float* __restrict__ out) {
+  const int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  if (i < n) {
+    const uint64_t g = static_cast<uint64_t>(ptr[i + 1] - ptr[i]);
+    out[i] = static_cast<float>(g & 0xffff);
+    out[n + i] = static_cast<float>((g >> 16) & 0xffff);
+    out[2 * n + i] = static_cast<float>(g >> 32);
+  } else if (i < count4 - 2 * n) {  // zero the padding to a multiple of 4 floats
+    out[2 * n + i] = 0.f;
+  }
+}
+
+__global__ void k_limbs_to_f64(const float* __restrict__ sum, int64_t n, double* __restrict__ deg) {
+  const int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  if (i < n)
+    deg[i] = static_cast<double>(sum[i]) + 65536.0 * static_cast<double>(sum[n + i]) +
+             4294967296.0 * static_cast<double>(sum[2 * n + i]);
 }
 
 unsigned capped_grid(int64_t n) { return std::min<unsigned>(grid_for(n), 4096u); }
@@ -123,13 +153,18 @@ struct hgd_incidence {
 };
 
 struct hgd_comm {
-  ncclComm_t comm = nullptr;
-  int32_t nranks = 1, rank = 0, n_chunks = 4;
+  ncclComm_t comm = nullptr;  // RCCL transport (NULL for a peer-exchange communicator)
+  hgd_p2p* p2p = nullptr;     // peer-exchange transport (not owned)
+  int32_t nranks = 1, rank = 0, n_chunks = 4, slice_width = 0;
   int device = 0;
+  uint64_t p2p_calls = 0;     // exchanges of conv hops issued: alternates the two slot sets
   hipStream_t side = nullptr;
   hipEvent_t ev[65] = {};
+  hipEvent_t done[64] = {};
   ~hgd_comm() {
     for (hipEvent_t e : ev)
+      if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : done)
       if (e) (void)hipEventDestroy(e);
     if (side) (void)hipStreamDestroy(side);
     if (comm) (void)ncclCommDestroy(comm);
@@ -359,6 +394,66 @@ hgd_status check_conv(const hgd_incidence* o, int32_t P, int32_t Q, int32_t R, i
                                         o->global_cols),
                 "%s: with a communicator Q must be NONE or a global MEAN/SYM "
                 "(hgd_incidence_globalize_columns)", fn);
+  }
+  return HGD_OK;
+}
+
+// Column slice width of the peer-exchange pipeline (sharded.ShardedIncidence.slices).
+int p2p_slice_width(const hgd_comm* c, int32_t d) {
+  int w = c->slice_width > 0 ? c->slice_width : (d <= 128 ? 32 : 64);
+  w = std::max(4, (w / 4) * 4);
+  return std::min<int>(w, d);
+}
+
+// The two hops over the peer exchange, slice by slice (see the file header):
+//   hop 1  slot = Q·Aᵀ·(S_src·X[:, c0:c1])   into send slot (parity·n_sl + s), compute stream
+//          M_s  = Σ_ranks slot              hgd_p2p_allreduce on the side stream
+//   hop 2  out[:, c0:c1] = epi(S_dst·A·M_s) after slice s's exchange only
+// M holds the slices as contiguous [n_cols, w] blocks; saved_M (optional) gets them as [n_cols, d].
+hgd_status two_hop_p2p(const hgd_incidence* o, int32_t Q, int32_t S_src, const float* X,
+                       int64_t ldx, int32_t d, int32_t S_dst, float* out, int64_t ldo,
+                       int32_t epilogue, float slope, float* saved_M, hgd_comm* c, float* M,
+                       void* ws, size_t wsb, hipStream_t st, const char* fn) {
+  HGD_REQUIRE(c->device == o->device, "%s: communicator and incidence on different devices", fn);
+  HGD_REQUIRE(d % 4 == 0, "%s: the peer exchange needs d %% 4 == 0 (got %d)", fn, d);
+  const int w = p2p_slice_width(c, d);
+  const int n_sl = (d + w - 1) / w;
+  const int64_t I = o->n_cols;
+  HGD_REQUIRE(n_sl <= 64, "%s: %d column slices (at most 64)", fn, n_sl);
+  HGD_REQUIRE(hgd_p2p_n_slots(c->p2p) >= 2 * n_sl && hgd_p2p_max_count(c->p2p) >= I * w,
+              "%s: the exchange needs %d slots of %lld floats (has %d of %lld)", fn, 2 * n_sl,
+              static_cast<long long>(I * w), hgd_p2p_n_slots(c->p2p),
+              static_cast<long long>(hgd_p2p_max_count(c->p2p)));
+  hgd_status r = hgd_p2p_poll(c->p2p);  // an earlier exchange timed out: stop here
+  if (r != HGD_OK) return r;
+  const float* wt = nullptr;
+  if ((r = csc_weights(o, S_src, &wt, st)) != HGD_OK) return r;
+  const float* q = Q == HGD_SCALE_NONE ? nullptr : o->scale[HGD_SIDE_COLS][Q];
+  const float* p = S_dst == HGD_SCALE_NONE ? nullptr : o->scale[HGD_SIDE_ROWS][S_dst];
+  const int parity = static_cast<int>(c->p2p_calls++ % 2);
+  for (int s = 0; s < n_sl; ++s) {
+    const int c0 = s * w, ws_ = std::min(w, d - c0);
+    const int slot = parity * n_sl + s;
+    float* send = hgd_p2p_slot(c->p2p, slot);
+    if (I > 0 && (r = hgd_spmm(o->colptr, o->row_t, wt, q, I, o->n_rows, 0, I, X + c0, ldx, send,
+                               ws_, ws_, HGD_EPI_NONE, 0.f, &o->plan[1], ws, wsb, st)) != HGD_OK)
+      return r;
+    HGD_HIP(hipEventRecord(c->ev[s], st));
+    HGD_HIP(hipStreamWaitEvent(c->side, c->ev[s], 0));
+    if ((r = hgd_p2p_allreduce(c->p2p, slot, I * ws_, M + I * c0, c->side)) != HGD_OK) return r;
+    HGD_HIP(hipEventRecord(c->done[s], c->side));
+  }
+  for (int s = 0; s < n_sl; ++s) {
+    const int c0 = s * w, ws_ = std::min(w, d - c0);
+    const float* Ms = M + I * c0;
+    HGD_HIP(hipStreamWaitEvent(st, c->done[s], 0));
+    if (saved_M && I > 0)
+      HGD_HIP(hipMemcpy2DAsync(saved_M + c0, static_cast<size_t>(d) * 4, Ms,
+                               static_cast<size_t>(ws_) * 4, static_cast<size_t>(ws_) * 4, I,
+                               hipMemcpyDeviceToDevice, st));
+    if ((r = hgd_spmm(o->rowptr, o->col, o->val, p, o->n_rows, I, 0, o->n_rows, Ms, ws_,
+                      out + c0, ldo, ws_, epilogue, slope, &o->plan[0], ws, wsb, st)) != HGD_OK)
+      return r;
   }
   return HGD_OK;
 }
@@ -618,6 +713,15 @@ extern "C" hgd_status hgd_conv2hop_forward(const hgd_incidence* o, int32_t P, in
   float* M = static_cast<float*>(ws);
   char* sws = static_cast<char*>(ws) + (need - spmm_ws(o, d));
   const size_t swsb = spmm_ws(o, d);
+  if (comm && comm->p2p) {
+    if (fuse)
+      return two_hop_p2p(o, Q, R, X, ldx, d, P, Y, ldy, epilogue, slope, saved_M, comm, M, sws,
+                         swsb, st, fn);
+    r = two_hop_p2p(o, Q, R, X, ldx, d, P, pre_act, d, HGD_EPI_NONE, 0.f, saved_M, comm, M, sws,
+                    swsb, st, fn);
+    if (r != HGD_OK) return r;
+    return hgd_epilogue_apply(pre_act, o->n_rows * d, epilogue, slope, Y, st);
+  }
   if ((r = hop_to_items(o, Q, R, X, ldx, d, M, comm, sws, swsb, st, fn)) != HGD_OK) return r;
   if (saved_M && o->n_cols)
     HGD_HIP(hipMemcpyAsync(saved_M, M, static_cast<size_t>(o->n_cols) * d * 4,
@@ -661,6 +765,9 @@ extern "C" hgd_status hgd_conv2hop_backward(const hgd_incidence* o, int32_t P, i
     g = dZ;
     ldg = d;
   }
+  if (comm && comm->p2p)
+    return two_hop_p2p(o, Q, P, g, ldg, d, R, dX, ldx, HGD_EPI_NONE, 0.f, nullptr, comm, dM, sws,
+                       swsb, st, fn);
   if ((r = hop_to_items(o, Q, P, g, ldg, d, dM, comm, sws, swsb, st, fn)) != HGD_OK) return r;
   const float* rs = R == HGD_SCALE_NONE ? nullptr : o->scale[HGD_SIDE_ROWS][R];
   return hgd_spmm(o->rowptr, o->col, o->val, rs, o->n_rows, o->n_cols, 0, o->n_rows, dM, d, dX,
@@ -709,6 +816,47 @@ extern "C" hgd_status hgd_comm_create(const void* id, int32_t nranks, int32_t ra
   return HGD_OK;
 }
 
+extern "C" hgd_status hgd_comm_create_p2p(hgd_p2p* p2p, int32_t nranks, int32_t rank,
+                                          hgd_comm** out) {
+  clear_error();
+  HGD_REQUIRE(p2p && out, "hgd_comm_create_p2p: null pointer");
+  HGD_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, "hgd_comm_create_p2p: bad rank %d of %d",
+              rank, nranks);
+  *out = nullptr;
+  auto* c = new hgd_comm();
+  c->p2p = p2p;
+  c->nranks = nranks;
+  c->rank = rank;
+  auto bail = [&](hgd_status s) {
+    delete c;
+    return s;
+  };
+  // the exchange's waits run on the side stream at high priority, as in sharded.py: its few
+  // workgroups are placed as soon as a CU frees instead of behind the queued hop grid
+  int lo = 0, hi = 0;
+  if (hipGetDevice(&c->device) != hipSuccess ||
+      hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, std::min(lo, hi)) != hipSuccess)
+    return bail(fail(HGD_ERR_HIP, "hgd_comm_create_p2p: stream creation failed"));
+  for (hipEvent_t& e : c->ev)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+      return bail(fail(HGD_ERR_HIP, "hgd_comm_create_p2p: event creation failed"));
+  for (hipEvent_t& e : c->done)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+      return bail(fail(HGD_ERR_HIP, "hgd_comm_create_p2p: event creation failed"));
+  *out = c;
+  return HGD_OK;
+}
+
+extern "C" hgd_status hgd_comm_set_slice_width(hgd_comm* comm, int32_t width) {
+  clear_error();
+  HGD_REQUIRE(comm, "hgd_comm_set_slice_width: null comm");
+  HGD_REQUIRE(width == 0 || (width >= 4 && width % 4 == 0),
+              "hgd_comm_set_slice_width: width must be 0 (default) or a multiple of 4");
+  comm->slice_width = width;
+  return HGD_OK;
+}
+
 extern "C" void hgd_comm_destroy(hgd_comm* comm) {
   if (comm && comm->side) (void)hipStreamSynchronize(comm->side);
   delete comm;
@@ -728,6 +876,17 @@ extern "C" hgd_status hgd_exchange_allreduce(hgd_comm* comm, float* buf, int64_t
   HGD_REQUIRE(comm, "hgd_exchange_allreduce: null comm");
   HGD_REQUIRE(count >= 0 && (count == 0 || buf), "hgd_exchange_allreduce: bad buffer");
   if (count == 0) return HGD_OK;
+  if (comm->p2p) {  // through send slot 0 of the exchange (the conv hops alternate all slots)
+    HGD_REQUIRE(count % 4 == 0 && reinterpret_cast<uintptr_t>(buf) % 16 == 0,
+                "hgd_exchange_allreduce: over the peer exchange count must be a multiple of 4 "
+                "and buf 16-byte aligned");
+    HGD_REQUIRE(count <= hgd_p2p_max_count(comm->p2p),
+                "hgd_exchange_allreduce: %lld floats exceed the exchange's slots",
+                static_cast<long long>(count));
+    HGD_HIP(hipMemcpyAsync(hgd_p2p_slot(comm->p2p, 0), buf, static_cast<size_t>(count) * 4,
+                           hipMemcpyDeviceToDevice, as_stream(stream)));
+    return hgd_p2p_allreduce(comm->p2p, 0, count, buf, stream);
+  }
   HGD_NCCL(ncclAllReduce(buf, buf, static_cast<size_t>(count), ncclFloat32, ncclSum, comm->comm,
                          as_stream(stream)));
   return HGD_OK;
@@ -748,9 +907,29 @@ extern "C" hgd_status hgd_incidence_globalize_columns(hgd_incidence* o, hgd_comm
   double* deg = nullptr;
   hgd_status r = temp_alloc(reinterpret_cast<void**>(&deg), n * sizeof(double), t.p);
   if (r != HGD_OK) return r;
-  hipLaunchKernelGGL(k_degree_f64, dim3(grid_for(n)), dim3(kBlock), 0, st, o->colptr, n, deg);
-  if ((r = check_launch("hgd_incidence_globalize_columns")) != HGD_OK) return r;
-  HGD_NCCL(ncclAllReduce(deg, deg, static_cast<size_t>(n), ncclFloat64, ncclSum, comm->comm, st));
+  if (comm->p2p) {
+    // exact integer sums over the fp32 exchange: three 16-bit limbs per degree
+    const int64_t count4 = (3 * n + 3) / 4 * 4;
+    HGD_REQUIRE(count4 <= hgd_p2p_max_count(comm->p2p),
+                "hgd_incidence_globalize_columns: %lld limbs exceed the exchange's slots",
+                static_cast<long long>(count4));
+    float* sum = nullptr;
+    if ((r = temp_alloc(reinterpret_cast<void**>(&sum), count4 * sizeof(float), t.p)) != HGD_OK)
+      return r;
+    hipLaunchKernelGGL(k_degree_limbs, dim3(grid_for(count4 - 2 * n)), dim3(kBlock), 0, st,
+                       o->colptr, n, count4, hgd_p2p_slot(comm->p2p, 0));
+    if ((r = check_launch("hgd_incidence_globalize_columns")) != HGD_OK) return r;
+    if ((r = hgd_p2p_allreduce(comm->p2p, 0, count4, sum, st)) != HGD_OK) return r;
+    hipLaunchKernelGGL(k_limbs_to_f64, dim3(grid_for(n)), dim3(kBlock), 0, st, sum, n, deg);
+    if ((r = check_launch("hgd_incidence_globalize_columns")) != HGD_OK) return r;
+    HGD_HIP(hipStreamSynchronize(st));
+    if ((r = hgd_p2p_check(comm->p2p)) != HGD_OK) return r;
+  } else {
+    hipLaunchKernelGGL(k_degree_f64, dim3(grid_for(n)), dim3(kBlock), 0, st, o->colptr, n, deg);
+    if ((r = check_launch("hgd_incidence_globalize_columns")) != HGD_OK) return r;
+    HGD_NCCL(ncclAllReduce(deg, deg, static_cast<size_t>(n), ncclFloat64, ncclSum, comm->comm,
+                           st));
+  }
   hipLaunchKernelGGL(k_scale_from_f64, dim3(grid_for(n)), dim3(kBlock), 0, st, deg, n,
                      o->scale[HGD_SIDE_COLS][HGD_SCALE_MEAN],
                      o->scale[HGD_SIDE_COLS][HGD_SCALE_SYM]);

@@ -1,9 +1,12 @@
 // Direct xGMI peer exchange: the all-reduce of the item messages without RCCL.
 //
-// Every rank exposes ONE uncached device allocation to its peers (hipIpcGetMemHandle, opened by
-// the others with hipIpcOpenMemHandle):
-//
-//   [ flags: 2 kinds × 64 uint64 | send slots: n_slots × max_count f32 | reduced slots: same ]
+// Every rank exposes uncached device memory to its peers (hipIpcGetMemHandle, opened by the
+// others with hipIpcOpenMemHandle): a 4 KiB flag page and 2·n_slots slots of max_count floats
+// (n_slots send slots, then n_slots reduced slots), packed whole into SEGMENTS — separate
+// allocations of at most 1 GiB each (HGD_TUNE_P2P_SEGMENT_MB). One allocation per rank is not
+// possible at the configs[4] sizes: on the ROCm 7.2 box, hipIpcOpenMemHandle of a 3.5 GiB or
+// 4 GiB uncached allocation never returns (every rank of a 4-process rehearsal blocked inside
+// it for 100 s, profiles/r04_scale/p2p_stall/), while 1 GiB imports open in milliseconds.
 //
 // An exchange of `count` floats in send slot k is a two-shot all-reduce over the mesh:
 //   1. signal/wait "sent":   this rank stores seq into flags[SENT][rank] of every peer, then
@@ -14,17 +17,33 @@
 //   3. signal/wait "reduced";
 //   4. gather:               the other N-1 blocks are read from the peers' reduced slots into out.
 // Each rank moves 2·(N-1)/N·count·4 bytes over its links, all N-1 at once (a ring moves the same
-// volume one link at a time). Memory is uncached (hipDeviceMallocUncached) so a peer's reads
-// see the owner's stores without cache maintenance; the flags are system-scope release /
-// acquire atomics; every wait is bounded (wall clock) and a timeout sets a device error flag
-// that turns the remaining exchanges into no-ops instead of hanging the GPU.
+// volume one link at a time).
+//
+// Memory ordering (the argument does not depend on how the importing GPU caches a peer's
+// memory: whether the dmabuf import keeps the exporter's uncached MTYPE or maps it
+// non-coherent-cacheable is the driver's choice, so both must be correct):
+//   * writer side: the owner's slot stores (hop 1 into a send slot, k_reduce into a reduced
+//     slot) go to uncached memory, and are complete when their kernel ends. k_reduce also ends
+//     with a system-scope release per workgroup. The flag that announces them is stored by a
+//     LATER kernel of the same stream with release semantics at system scope (L2 write-back,
+//     then the store), so no announced byte can still sit in a cache of the writer;
+//   * reader side: the flag is read with a system-scope acquire by the wait kernel, and every
+//     workgroup of k_reduce / k_gather starts with a system-scope acquire fence, which
+//     invalidates its CU's L1 and the non-coherent lines of its L2 before the first peer load.
+//     A slot is reused every second exchange of a stream (sharded.py alternates two slot sets),
+//     so without that fence a non-coherent L2 line of the previous exchange could be read back;
+//   * flags are only touched by system-scope atomics (never cached).
+// Every wait is bounded (wall clock). A timeout sets a device error flag and its host-visible
+// copy (hgd_p2p_poll reads it without a sync): the remaining exchanges then write NaN into
+// their output instead of summing, so a failed exchange never passes for data.
 //
 // Slot reuse: the buffers of an exchange i may be rewritten once any later exchange j > i has
 // completed on this rank's stream — a peer signals "sent" for j only after its own stream has
 // finished every read of i (exchanges are issued in the same order on every rank, on one
-// stream per rank). The sharded hop alternates two sets of slots per call (sharded.py).
+// stream per rank).
 #include "hgd_internal.h"
 
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
@@ -34,26 +53,38 @@ constexpr int kMaxRanks = 8;
 constexpr int kFlagSlots = 64;
 constexpr size_t kFlagsBytes = 4096;  // 2 × 64 × 8 = 1 KiB, padded to a page
 constexpr int kSent = 0, kReduced = 1;
+constexpr int kMaxSegments = 62;      // handles per rank record (HGD_P2P_HANDLE_BYTES)
+size_t g_segment_bytes = size_t(1) << 30;  // HGD_TUNE_P2P_SEGMENT_MB
+int g_cached = 0;                          // HGD_TUNE_P2P_CACHED
 
-struct Packed {  // the exported handle (HGD_P2P_HANDLE_BYTES)
-  hipIpcMemHandle_t ipc;
-  int64_t total_bytes;
-  int64_t max_count;
-  int32_t n_slots;
-  int32_t rank;
-  int32_t nranks;
-  int32_t magic;
+struct Packed {  // one rank's record in the handle exchange (HGD_P2P_HANDLE_BYTES)
+  int32_t magic, rank, nranks, n_slots;
+  int64_t max_count, slot_bytes;
+  int32_t n_segments, slots_per_segment;
+  int32_t cached, pad;
+  hipIpcMemHandle_t flags;
+  hipIpcMemHandle_t seg[kMaxSegments];
 };
 static_assert(sizeof(Packed) <= HGD_P2P_HANDLE_BYTES, "handle too large");
-constexpr int32_t kMagic = 0x68676470;  // "hgdp"
+constexpr int32_t kMagic = 0x68676471;  // "hgdq" (segmented layout)
+
+// System-scope fences (see "Memory ordering" above): the acquire invalidates this CU's vector L1
+// and the non-coherent lines of the L2, so the loads after it fetch peer memory afresh; the
+// release waits for this wave's stores and writes dirty L2 lines back to memory.
+__device__ __forceinline__ void acquire_system() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); }
+__device__ __forceinline__ void release_system() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, ""); }
+
+__device__ __forceinline__ bool failed(const int* err) {
+  return __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+}
 
 __global__ void k_signal_wait(uint64_t* const* flags, int kind, int rank, int nranks,
-                              uint64_t seq, uint64_t timeout_ticks, int* err) {
+                              uint64_t seq, uint64_t timeout_ticks, int* err, int* host_err) {
   const int t = threadIdx.x;
   if (t >= nranks) return;
-  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
-  // publish: peer t's slot for this rank (the previous kernels of this stream are complete, and
-  // their stores to the uncached slots are in memory)
+  if (failed(err)) return;
+  // publish: peer t's slot for this rank. The release orders every earlier kernel of this stream
+  // (complete before this one started) before the flag: its stores are in memory.
   __hip_atomic_store(flags[t] + kind * kFlagSlots + rank, seq, __ATOMIC_RELEASE,
                      __HIP_MEMORY_SCOPE_SYSTEM);
   // wait for peer t's store into this rank's slot
@@ -63,6 +94,8 @@ __global__ void k_signal_wait(uint64_t* const* flags, int kind, int rank, int nr
     __builtin_amdgcn_s_sleep(8);
     if (static_cast<uint64_t>(wall_clock64()) - t0 > timeout_ticks) {
       __hip_atomic_store(err, 1 + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // the host-visible copy hgd_p2p_poll reads without synchronising
+      __hip_atomic_store(host_err, 1 + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return;
     }
   }
@@ -90,23 +123,35 @@ struct Blocks {
   __host__ __device__ int gather_owner(int64_t j) const { return static_cast<int>(j / b4); }
 };
 
+// Every rank's address of one slot (kernel argument, by value).
+struct SlotPtrs {
+  const float4* p[kMaxRanks];
+};
+
+// After a timed-out wait the exchange's output is NaN, never stale or uninitialised memory.
+__device__ __forceinline__ float4 nan4() {
+  const float n = __builtin_nanf("");
+  return make_float4(n, n, n, n);
+}
+
 // out[block r] = reduced_r[block r] = Σ_q send_q[block r], q ascending
-__global__ void k_reduce(char* const* base, size_t send_off, size_t red_off, Blocks bl,
-                         int rank, int nranks, float4* __restrict__ out, const int* err) {
-  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
-  const int64_t lo = bl.lo(rank), hi = bl.hi(rank);
-  const float4* src[kMaxRanks];
-#pragma unroll
-  for (int q = 0; q < kMaxRanks; ++q)
-    src[q] = reinterpret_cast<const float4*>(base[q < nranks ? q : 0] + send_off);
-  float4* red = reinterpret_cast<float4*>(base[rank] + red_off);
+__global__ void k_reduce(SlotPtrs send, float4* red, Blocks bl, int rank, int nranks,
+                         float4* __restrict__ out, const int* err) {
+  const int64_t hi = bl.hi(rank);
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-  for (int64_t i = lo + blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < hi;
-       i += stride) {
+  const int64_t first = bl.lo(rank) + blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  if (failed(err)) {
+    for (int64_t i = first; i < hi; i += stride) out[i] = nan4();
+    return;
+  }
+  // the "sent" flags were acquired by the wait kernel before this one: drop any copy of a
+  // peer's slot a cache may still hold from an earlier exchange of the same slot
+  acquire_system();
+  for (int64_t i = first; i < hi; i += stride) {
     float4 v[kMaxRanks];
 #pragma unroll
     for (int q = 0; q < kMaxRanks; ++q)  // all loads in flight before the first add
-      if (q < nranks) v[q] = src[q][i];
+      if (q < nranks) v[q] = send.p[q][i];
     float4 a = v[0];
 #pragma unroll
     for (int q = 1; q < kMaxRanks; ++q)
@@ -114,18 +159,26 @@ __global__ void k_reduce(char* const* base, size_t send_off, size_t red_off, Blo
     red[i] = a;
     out[i] = a;
   }
+  // the peers read red[] after the "reduced" flag: this workgroup's stores are performed at
+  // system scope before the kernel ends (one release per workgroup, after all its waves' stores)
+  __syncthreads();
+  if (threadIdx.x == 0) release_system();
 }
 
 // out[block q] = reduced_q[block q] for every q != rank
-__global__ void k_gather(char* const* base, size_t red_off, Blocks bl, int rank,
-                         float4* __restrict__ out, const int* err) {
-  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+__global__ void k_gather(SlotPtrs red, Blocks bl, int rank, float4* __restrict__ out,
+                         const int* err) {
   const int64_t n = bl.gather_count(rank);
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
-       i += stride) {
+  const int64_t first = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  if (failed(err)) {
+    for (int64_t i = first; i < n; i += stride) out[bl.gather_j(rank, i)] = nan4();
+    return;
+  }
+  acquire_system();  // the "reduced" flags were acquired by the wait kernel before this one
+  for (int64_t i = first; i < n; i += stride) {
     const int64_t j = bl.gather_j(rank, i);
-    out[j] = reinterpret_cast<const float4*>(base[bl.gather_owner(j)] + red_off)[j];
+    out[j] = red.p[bl.gather_owner(j)][j];
   }
 }
 
@@ -135,32 +188,53 @@ struct hgd_p2p {
   int device = -1;
   int32_t nranks = 0, rank = 0, n_slots = 0;
   int64_t max_count = 0;
-  size_t slot_bytes = 0, total_bytes = 0;
-  char* base = nullptr;               // own exposed allocation
-  std::vector<char*> bases;           // every rank's mapping (own = base), host copy
-  char** d_bases = nullptr;           // the same on the device
-  uint64_t** d_flags = nullptr;       // every rank's flag array on the device
+  size_t slot_bytes = 0;
+  int n_segments = 0, per_segment = 0;  // slots per segment (2·n_slots slots in all)
+  int cached = 0;
+  char* flags_own = nullptr;
+  std::vector<char*> segs_own;
+  // every rank's mappings (own entries are the own allocations), host copies
+  std::vector<char*> flags;                // [rank]
+  std::vector<std::vector<char*>> segs;    // [rank][segment]
+  uint64_t** d_flags = nullptr;       // every rank's flag page on the device
   int* err = nullptr;                 // device error flag (0 = ok, q+1 = timed out on rank q)
+  int* host_err = nullptr;            // its host-visible copy (pinned, coherent), host address
+  int* host_err_dev = nullptr;        // ... and its device address
   uint64_t seq = 0;                   // exchanges issued
   uint64_t ticks_per_s = 100000000;
   double timeout_s = 30.0;
   bool opened = false;
 
-  size_t send_off(int slot) const { return kFlagsBytes + static_cast<size_t>(slot) * slot_bytes; }
-  size_t red_off(int slot) const {
-    return kFlagsBytes + static_cast<size_t>(n_slots + slot) * slot_bytes;
+  // slot g of rank q: send slots are g = 0 .. n_slots-1, reduced slots n_slots .. 2·n_slots-1
+  char* slot(int q, int g) const {
+    return segs[q][g / per_segment] + static_cast<size_t>(g % per_segment) * slot_bytes;
+  }
+  size_t segment_bytes(int s) const {
+    const int first = s * per_segment;
+    return static_cast<size_t>(std::min(per_segment, 2 * n_slots - first)) * slot_bytes;
   }
   ~hgd_p2p() {
     if (device >= 0) (void)hipSetDevice(device);
     (void)hipDeviceSynchronize();
-    for (int q = 0; q < static_cast<int>(bases.size()); ++q)
-      if (q != rank && bases[q]) (void)hipIpcCloseMemHandle(bases[q]);
-    if (d_bases) (void)hipFree(d_bases);
+    for (int q = 0; q < static_cast<int>(flags.size()); ++q) {
+      if (q == rank) continue;
+      if (flags[q]) (void)hipIpcCloseMemHandle(flags[q]);
+      for (char* p : segs[q])
+        if (p) (void)hipIpcCloseMemHandle(p);
+    }
     if (d_flags) (void)hipFree(d_flags);
     if (err) (void)hipFree(err);
-    if (base) (void)hipFree(base);
+    if (host_err) (void)hipHostFree(host_err);
+    for (char* p : segs_own)
+      if (p) (void)hipFree(p);
+    if (flags_own) (void)hipFree(flags_own);
   }
 };
+
+namespace hgd {
+void set_p2p_segment_mb(int mb) { g_segment_bytes = (mb > 0 ? size_t(mb) : 1024) << 20; }
+void set_p2p_cached(int cached) { g_cached = cached; }
+}  // namespace hgd
 
 using hgd::fail;
 
@@ -175,6 +249,16 @@ extern "C" hgd_status hgd_p2p_create(int32_t nranks, int32_t rank, int64_t max_c
               "hgd_p2p_create: max_count must be a positive multiple of 4, got %lld",
               static_cast<long long>(max_count));
   HGD_REQUIRE(n_slots >= 1 && n_slots <= 1024, "hgd_p2p_create: n_slots in [1, 1024]");
+  const size_t slot_bytes = hgd::align_up(static_cast<size_t>(max_count) * 4, 4096);
+  HGD_REQUIRE(slot_bytes <= g_segment_bytes,
+              "hgd_p2p_create: a slot of %lld floats exceeds the %zu MiB segment limit",
+              static_cast<long long>(max_count), g_segment_bytes >> 20);
+  const int per_segment =
+      static_cast<int>(std::min<size_t>(g_segment_bytes / slot_bytes, 2 * size_t(n_slots)));
+  const int n_segments = (2 * n_slots + per_segment - 1) / per_segment;
+  HGD_REQUIRE(n_segments <= kMaxSegments,
+              "hgd_p2p_create: %d slots of %zu bytes need %d segments (at most %d)", 2 * n_slots,
+              slot_bytes, n_segments, kMaxSegments);
   auto* h = new hgd_p2p();
   auto bail = [&](hgd_status s) { delete h; return s; };
   if (hipGetDevice(&h->device) != hipSuccess) return bail(fail(HGD_ERR_HIP, "hgd_p2p_create: no device"));
@@ -182,27 +266,43 @@ extern "C" hgd_status hgd_p2p_create(int32_t nranks, int32_t rank, int64_t max_c
   h->rank = rank;
   h->n_slots = n_slots;
   h->max_count = max_count;
-  h->slot_bytes = hgd::align_up(static_cast<size_t>(max_count) * 4, 4096);
-  h->total_bytes = kFlagsBytes + 2 * static_cast<size_t>(n_slots) * h->slot_bytes;
+  h->slot_bytes = slot_bytes;
+  h->per_segment = per_segment;
+  h->n_segments = n_segments;
+  h->cached = g_cached;
+  const unsigned flag = g_cached ? hipDeviceMallocDefault : hipDeviceMallocUncached;
   void* p = nullptr;
-  hipError_t e = hipExtMallocWithFlags(&p, h->total_bytes, hipDeviceMallocUncached);
-  if (e != hipSuccess)
-    return bail(fail(HGD_ERR_HIP, "hgd_p2p_create: uncached allocation of %zu bytes: %s",
-                     h->total_bytes, hipGetErrorString(e)));
-  h->base = static_cast<char*>(p);
-  if (hipMemset(h->base, 0, kFlagsBytes) != hipSuccess ||
+  if (hipExtMallocWithFlags(&p, kFlagsBytes, hipDeviceMallocUncached) != hipSuccess)
+    return bail(fail(HGD_ERR_HIP, "hgd_p2p_create: flag page allocation failed"));
+  h->flags_own = static_cast<char*>(p);
+  h->segs_own.assign(n_segments, nullptr);
+  for (int s = 0; s < n_segments; ++s) {
+    p = nullptr;
+    hipError_t e = hipExtMallocWithFlags(&p, h->segment_bytes(s), flag);
+    if (e != hipSuccess)
+      return bail(fail(HGD_ERR_HIP, "hgd_p2p_create: segment %d of %zu bytes: %s", s,
+                       h->segment_bytes(s), hipGetErrorString(e)));
+    h->segs_own[s] = static_cast<char*>(p);
+  }
+  if (hipMemset(h->flags_own, 0, kFlagsBytes) != hipSuccess ||
       hipMalloc(reinterpret_cast<void**>(&h->err), sizeof(int)) != hipSuccess ||
       hipMemset(h->err, 0, sizeof(int)) != hipSuccess ||
-      hipMalloc(reinterpret_cast<void**>(&h->d_bases), kMaxRanks * sizeof(char*)) != hipSuccess ||
       hipMalloc(reinterpret_cast<void**>(&h->d_flags), kMaxRanks * sizeof(uint64_t*)) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&h->host_err), sizeof(int),
+                    hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&h->host_err_dev), h->host_err, 0) !=
+          hipSuccess ||
       hipDeviceSynchronize() != hipSuccess)
     return bail(fail(HGD_ERR_HIP, "hgd_p2p_create: setup failed"));
+  *h->host_err = 0;
   int khz = 0;
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->device) == hipSuccess &&
       khz > 0)
     h->ticks_per_s = static_cast<uint64_t>(khz) * 1000;
-  h->bases.assign(nranks, nullptr);
-  h->bases[rank] = h->base;
+  h->flags.assign(nranks, nullptr);
+  h->segs.assign(nranks, std::vector<char*>(n_segments, nullptr));
+  h->flags[rank] = h->flags_own;
+  h->segs[rank] = h->segs_own;
   *out = h;
   return HGD_OK;
 }
@@ -213,17 +313,43 @@ extern "C" hgd_status hgd_p2p_export(const hgd_p2p* h, void* handle_out) {
   Packed pk;
   std::memset(&pk, 0, sizeof(pk));
   HGD_HIP(hipSetDevice(h->device));
-  HGD_HIP(hipIpcGetMemHandle(&pk.ipc, h->base));
-  pk.total_bytes = static_cast<int64_t>(h->total_bytes);
-  pk.max_count = h->max_count;
-  pk.n_slots = h->n_slots;
+  HGD_HIP(hipIpcGetMemHandle(&pk.flags, h->flags_own));
+  for (int s = 0; s < h->n_segments; ++s) HGD_HIP(hipIpcGetMemHandle(&pk.seg[s], h->segs_own[s]));
+  pk.magic = kMagic;
   pk.rank = h->rank;
   pk.nranks = h->nranks;
-  pk.magic = kMagic;
+  pk.n_slots = h->n_slots;
+  pk.max_count = h->max_count;
+  pk.slot_bytes = static_cast<int64_t>(h->slot_bytes);
+  pk.n_segments = h->n_segments;
+  pk.slots_per_segment = h->per_segment;
+  pk.cached = h->cached;
   std::memset(handle_out, 0, HGD_P2P_HANDLE_BYTES);
   std::memcpy(handle_out, &pk, sizeof(pk));
   return HGD_OK;
 }
+
+namespace {
+// Opens one peer allocation and checks that the mapping spans all of it (a short import would
+// fault, or read another object, at the first slot past its end).
+hgd_status open_one(const hipIpcMemHandle_t& ipc, size_t bytes, int q, char** out) {
+  void* p = nullptr;
+  HGD_HIP(hipIpcOpenMemHandle(&p, ipc, hipIpcMemLazyEnablePeerAccess));
+  *out = static_cast<char*>(p);
+  hipDeviceptr_t mb = nullptr;
+  size_t msz = 0;
+  if (hipMemGetAddressRange(&mb, &msz, p) == hipSuccess) {
+    const char* lo = static_cast<const char*>(mb);
+    const char* at = static_cast<const char*>(p);
+    if (at < lo || static_cast<size_t>(lo + msz - at) < bytes)
+      return fail(HGD_ERR_HIP, "hgd_p2p_open: rank %d's mapping covers %zu of %zu bytes", q,
+                  at < lo ? size_t(0) : static_cast<size_t>(lo + msz - at), bytes);
+  } else {
+    (void)hipGetLastError();
+  }
+  return HGD_OK;
+}
+}  // namespace
 
 extern "C" hgd_status hgd_p2p_open(hgd_p2p* h, const void* handles) {
   hgd::clear_error();
@@ -235,22 +361,21 @@ extern "C" hgd_status hgd_p2p_open(hgd_p2p* h, const void* handles) {
     Packed pk;
     std::memcpy(&pk, in + static_cast<size_t>(q) * HGD_P2P_HANDLE_BYTES, sizeof(pk));
     HGD_REQUIRE(pk.magic == kMagic && pk.rank == q && pk.nranks == h->nranks &&
-                    pk.total_bytes == static_cast<int64_t>(h->total_bytes) &&
-                    pk.max_count == h->max_count && pk.n_slots == h->n_slots,
+                    pk.max_count == h->max_count && pk.n_slots == h->n_slots &&
+                    pk.slot_bytes == static_cast<int64_t>(h->slot_bytes) &&
+                    pk.n_segments == h->n_segments && pk.slots_per_segment == h->per_segment &&
+                    pk.cached == h->cached,
                 "hgd_p2p_open: handle %d does not match this exchange (rank %d, %d ranks, "
-                "%lld bytes)", q, pk.rank, pk.nranks, static_cast<long long>(pk.total_bytes));
+                "%lld floats x %d slots in %d segments)", q, pk.rank, pk.nranks,
+                static_cast<long long>(pk.max_count), pk.n_slots, pk.n_segments);
     if (q == h->rank) continue;
-    void* p = nullptr;
-    HGD_HIP(hipIpcOpenMemHandle(&p, pk.ipc, hipIpcMemLazyEnablePeerAccess));
-    h->bases[q] = static_cast<char*>(p);
+    if (hgd_status r = open_one(pk.flags, kFlagsBytes, q, &h->flags[q]); r != HGD_OK) return r;
+    for (int s = 0; s < h->n_segments; ++s)
+      if (hgd_status r = open_one(pk.seg[s], h->segment_bytes(s), q, &h->segs[q][s]); r != HGD_OK)
+        return r;
   }
-  std::vector<char*> b(kMaxRanks, h->base);
-  std::vector<uint64_t*> f(kMaxRanks, reinterpret_cast<uint64_t*>(h->base));
-  for (int q = 0; q < h->nranks; ++q) {
-    b[q] = h->bases[q];
-    f[q] = reinterpret_cast<uint64_t*>(h->bases[q]);
-  }
-  HGD_HIP(hipMemcpy(h->d_bases, b.data(), kMaxRanks * sizeof(char*), hipMemcpyHostToDevice));
+  std::vector<uint64_t*> f(kMaxRanks, reinterpret_cast<uint64_t*>(h->flags_own));
+  for (int q = 0; q < h->nranks; ++q) f[q] = reinterpret_cast<uint64_t*>(h->flags[q]);
   HGD_HIP(hipMemcpy(h->d_flags, f.data(), kMaxRanks * sizeof(uint64_t*), hipMemcpyHostToDevice));
   h->opened = true;
   return HGD_OK;
@@ -258,7 +383,7 @@ extern "C" hgd_status hgd_p2p_open(hgd_p2p* h, const void* handles) {
 
 extern "C" float* hgd_p2p_slot(hgd_p2p* h, int32_t slot) {
   if (!h || slot < 0 || slot >= h->n_slots) return nullptr;
-  return reinterpret_cast<float*>(h->base + h->send_off(slot));
+  return reinterpret_cast<float*>(h->slot(h->rank, slot));
 }
 
 extern "C" hgd_status hgd_p2p_set_timeout(hgd_p2p* h, double seconds) {
@@ -284,23 +409,30 @@ extern "C" hgd_status hgd_p2p_allreduce(hgd_p2p* h, int32_t slot, int64_t count,
   const uint64_t seq = ++h->seq;
   const uint64_t tmo = static_cast<uint64_t>(h->timeout_s * static_cast<double>(h->ticks_per_s));
   const Blocks bl = Blocks::of(count, h->nranks);
+  SlotPtrs send{}, red{};
+  for (int q = 0; q < kMaxRanks; ++q) {
+    const int qq = q < h->nranks ? q : h->rank;
+    send.p[q] = reinterpret_cast<const float4*>(h->slot(qq, slot));
+    red.p[q] = reinterpret_cast<const float4*>(h->slot(qq, h->n_slots + slot));
+  }
   float4* o = reinterpret_cast<float4*>(out);
   hipLaunchKernelGGL(k_signal_wait, dim3(1), dim3(64), 0, st, h->d_flags, kSent, h->rank,
-                     h->nranks, seq, tmo, h->err);
+                     h->nranks, seq, tmo, h->err, h->host_err_dev);
   if (hgd_status r = hgd::check_launch("hgd_p2p_allreduce (signal)"); r != HGD_OK) return r;
   const unsigned g1 = std::min<unsigned>(1024, hgd::grid_for(std::max<int64_t>(bl.b4, 1)));
-  hipLaunchKernelGGL(k_reduce, dim3(g1), dim3(hgd::kBlock), 0, st, h->d_bases,
-                     h->send_off(slot), h->red_off(slot), bl, h->rank, h->nranks, o, h->err);
+  hipLaunchKernelGGL(k_reduce, dim3(g1), dim3(hgd::kBlock), 0, st, send,
+                     reinterpret_cast<float4*>(h->slot(h->rank, h->n_slots + slot)), bl, h->rank,
+                     h->nranks, o, h->err);
   if (hgd_status r = hgd::check_launch("hgd_p2p_allreduce (reduce)"); r != HGD_OK) return r;
   if (h->nranks > 1) {
     hipLaunchKernelGGL(k_signal_wait, dim3(1), dim3(64), 0, st, h->d_flags, kReduced, h->rank,
-                       h->nranks, seq, tmo, h->err);
+                       h->nranks, seq, tmo, h->err, h->host_err_dev);
     if (hgd_status r = hgd::check_launch("hgd_p2p_allreduce (signal)"); r != HGD_OK) return r;
     const int64_t rest = bl.gather_count(h->rank);
     if (rest > 0) {
       const unsigned g2 = std::min<unsigned>(2048, hgd::grid_for(rest));
-      hipLaunchKernelGGL(k_gather, dim3(g2), dim3(hgd::kBlock), 0, st, h->d_bases,
-                         h->red_off(slot), bl, h->rank, o, h->err);
+      hipLaunchKernelGGL(k_gather, dim3(g2), dim3(hgd::kBlock), 0, st, red, bl, h->rank, o,
+                         h->err);
       if (hgd_status r = hgd::check_launch("hgd_p2p_allreduce (gather)"); r != HGD_OK) return r;
     }
   }
@@ -318,6 +450,19 @@ extern "C" hgd_status hgd_p2p_check(hgd_p2p* h) {
                 e - 1, h->timeout_s);
   return HGD_OK;
 }
+
+extern "C" hgd_status hgd_p2p_poll(const hgd_p2p* h) {
+  hgd::clear_error();
+  HGD_REQUIRE(h, "hgd_p2p_poll: null handle");
+  const int e = __atomic_load_n(h->host_err, __ATOMIC_ACQUIRE);
+  if (e != 0)
+    return fail(HGD_ERR_HIP, "hgd_p2p: an exchange timed out waiting for rank %d after %.1f s",
+                e - 1, h->timeout_s);
+  return HGD_OK;
+}
+
+extern "C" int32_t hgd_p2p_n_slots(const hgd_p2p* h) { return h ? h->n_slots : 0; }
+extern "C" int64_t hgd_p2p_max_count(const hgd_p2p* h) { return h ? h->max_count : 0; }
 
 extern "C" void hgd_p2p_destroy(hgd_p2p* h) { delete h; }
 

@@ -769,6 +769,19 @@ extern "C" hgd_status hgd_set_tuning(int32_t key, int32_t value) {
       HGD_REQUIRE(value >= 0 && value <= 3, "hgd_set_tuning: x3s tiles must be 0, 1, 2 or 3");
       set_x3s_tiles(value);
       return HGD_OK;
+    case HGD_TUNE_P2P_SEGMENT_MB:
+      HGD_REQUIRE(value >= 0 && value <= 65536,
+                  "hgd_set_tuning: p2p segment must be 0 (default) or 1..65536 MiB");
+      set_p2p_segment_mb(value);
+      return HGD_OK;
+    case HGD_TUNE_P2P_CACHED:
+      HGD_REQUIRE(value == 0 || value == 1, "hgd_set_tuning: p2p cached must be 0 or 1");
+      set_p2p_cached(value);
+      return HGD_OK;
+    case HGD_TUNE_CPU_RNG_THREADS:
+      HGD_REQUIRE(value >= 0 && value <= 64, "hgd_set_tuning: cpu rng threads must be 0..64");
+      set_cpu_rng_threads(value);
+      return HGD_OK;
     default:
       return fail(HGD_ERR_INVALID_ARG, "hgd_set_tuning: unknown key %d", key);
   }

@@ -507,7 +507,7 @@ size_t excl_scan_bytes(int64_t n) {
 
 using namespace hgd;
 
-extern "C" int hgd_version(void) { return 100; }  // 0.1.0
+extern "C" int hgd_version(void) { return 400; }  // 0.4.0
 
 extern "C" const char* hgd_get_last_error_string(void) { return g_last_error; }
 

@@ -15,9 +15,15 @@
 // POD with the 624 MT words as uint64, then the float-normal cache), read and written in place
 // so the caller hands it back with torch.set_rng_state; the Python side checks the layout once
 // against torch.rand itself before using this path.
-#include <cstdint>
 #include <algorithm>
+#include <condition_variable>
+#include <cstdint>
 #include <cstring>
+#include <functional>
+#include <map>
+#include <mutex>
+#include <thread>
+#include <vector>
 
 #include "../../include/hgd.h"
 #include "hgd_internal.h"
@@ -117,10 +123,315 @@ int64_t draw_mask_base(Draws& g, int64_t n, float keep, uint8_t* mask) {
   return draw_mask(g, n, keep, mask);
 }
 
+int64_t draw_any(Draws& g, int64_t n, float keep, uint8_t* mask) {
+  static const bool avx2 = __builtin_cpu_supports("avx2");
+  if (n == 0) return 0;
+  return avx2 ? draw_mask_avx2(g, n, keep, mask) : draw_mask_base(g, n, keep, mask);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Jump-ahead: the draws split over threads, each starting from the generator state T refills
+// ahead, computed in GF(2) (no draws skipped by stepping).
+//
+// Let w_0, w_1, … be the raw (untempered) words in output order; the array after r refills holds
+// w_{624r} … w_{624r+623} (r = 0: the current array). The generator's linear state is the upper
+// bit of w_t plus w_{t+1} … w_{t+623} (19,937 bits), so every bit of u_t = w_{t+1} satisfies the
+// recurrence with MT19937's characteristic polynomial φ (degree 19,937): with
+// x^N mod φ = Σ c_i x^i, u_{t+N} = ⊕_{c_i = 1} u_{t+i} for all t >= 0. The array after R refills
+// is then word j = w_{624R+j} = u_{624R-1+j} = ⊕_{c_i = 1} u_{i+j} (N = 624R - 1): a XOR of
+// shifted windows of the next 19,937 + 623 words, which one thread generates by plain refills.
+// φ comes from Berlekamp–Massey on one bit of a generated sequence (once per process); x^N mod φ
+// by square-and-multiply, cached per N (the split of a draw depends only on its length).
+// ---------------------------------------------------------------------------------------------
+constexpr int kDeg = 19937;
+constexpr int kPhiWords = (kDeg + 1 + 63) / 64;  // 312
+using Poly = std::vector<uint64_t>;
+
+inline bool bit(const Poly& p, int64_t i) { return (p[i >> 6] >> (i & 63)) & 1u; }
+inline void flip(Poly& p, int64_t i) { p[i >> 6] ^= uint64_t(1) << (i & 63); }
+
+struct Gf2 {
+  Poly phi;                      // φ, kDeg + 1 coefficients
+  std::vector<Poly> phi_sh;      // φ·x^s for s = 0..63 (kPhiWords + 1 words each)
+  uint16_t spread[256];          // bit i of a byte → bit 2i
+  bool ok = false;
+};
+
+// at::mt19937's seeding (init_genrand) of a plain array
+void seed_array(uint32_t* s, uint32_t seed) {
+  s[0] = seed;
+  for (int i = 1; i < kN; ++i) s[i] = 1812433253u * (s[i - 1] ^ (s[i - 1] >> 30)) + i;
+}
+
+// Berlekamp–Massey over GF(2) on bit 0 of 2·kDeg + 64 generated words: returns φ (the
+// reciprocal of the connection polynomial), degree L.
+Poly berlekamp_massey(int* L_out) {
+  const int n_bits = 2 * kDeg + 64;
+  std::vector<uint8_t> seq(n_bits);
+  uint32_t s[kN];
+  seed_array(s, 5489u);
+  for (int k = 0; k < n_bits; k += kN) {
+    next_state(s);
+    for (int i = 0; i < kN && k + i < n_bits; ++i) seq[k + i] = s[i] & 1u;
+  }
+  const int W = (n_bits + 63) / 64 + 1;
+  Poly C(W, 0), B(W, 0), win(W, 0);  // win bit i = seq[n - i]
+  C[0] = B[0] = 1;
+  int L = 0, m = 1;
+  auto xor_shifted = [&](Poly& dst, const Poly& src, int sh) {  // dst ^= src << sh
+    const int ws = sh >> 6, bs = sh & 63;
+    for (int i = W - 1; i >= ws; --i) {
+      uint64_t v = src[i - ws] << bs;
+      if (bs && i - ws - 1 >= 0) v |= src[i - ws - 1] >> (64 - bs);
+      dst[i] ^= v;
+    }
+  };
+  for (int n = 0; n < n_bits; ++n) {
+    // window ← window·x + seq[n]
+    for (int i = W - 1; i > 0; --i) win[i] = (win[i] << 1) | (win[i - 1] >> 63);
+    win[0] = (win[0] << 1) | seq[n];
+    int d = 0;
+    const int lw = (L >> 6) + 1;
+    for (int i = 0; i < lw && i < W; ++i) d ^= __builtin_parityll(C[i] & win[i]);
+    if (d == 0) {
+      ++m;
+    } else if (2 * L <= n) {
+      Poly T = C;
+      xor_shifted(C, B, m);
+      L = n + 1 - L;
+      B.swap(T);
+      m = 1;
+    } else {
+      xor_shifted(C, B, m);
+      ++m;
+    }
+  }
+  Poly phi(kPhiWords, 0);
+  if (L <= kDeg)
+    for (int i = 0; i <= L; ++i)
+      if (bit(C, i)) flip(phi, L - i);
+  *L_out = L;
+  return phi;
+}
+
+const Gf2& gf2() {
+  static Gf2 g;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    int L = 0;
+    g.phi = berlekamp_massey(&L);
+    g.ok = L == kDeg && bit(g.phi, kDeg) && bit(g.phi, 0);
+    g.phi_sh.assign(64, Poly(kPhiWords + 1, 0));
+    for (int s = 0; s < 64; ++s)
+      for (int i = 0; i <= kDeg; ++i)
+        if (bit(g.phi, i)) flip(g.phi_sh[s], i + s);
+    for (int b = 0; b < 256; ++b) {
+      uint16_t v = 0;
+      for (int i = 0; i < 8; ++i) v |= static_cast<uint16_t>(((b >> i) & 1) << (2 * i));
+      g.spread[b] = v;
+    }
+  });
+  return g;
+}
+
+// a mod φ in place (a has at most 2·kDeg bits); returns kPhiWords words
+void reduce(const Gf2& g, Poly& a) {
+  for (int64_t p = static_cast<int64_t>(a.size()) * 64 - 1; p >= kDeg; --p) {
+    if (!bit(a, p)) continue;
+    const int64_t sh = p - kDeg;
+    const Poly& f = g.phi_sh[sh & 63];
+    const int64_t w0 = sh >> 6;
+    for (int i = 0; i <= kPhiWords && w0 + i < static_cast<int64_t>(a.size()); ++i)
+      a[w0 + i] ^= f[i];
+  }
+  a.resize(kPhiWords);
+}
+
+// x^N mod φ
+Poly x_pow_mod(const Gf2& g, int64_t N) {
+  Poly r(kPhiWords, 0);
+  r[0] = 1;
+  int top = 63;
+  while (top > 0 && !((N >> top) & 1)) --top;
+  for (int b = top; b >= 0; --b) {
+    Poly sq(2 * kPhiWords + 1, 0);  // r², spread bits
+    for (int i = 0; i < kPhiWords; ++i) {
+      uint64_t lo = 0, hi = 0;
+      for (int k = 0; k < 4; ++k) {
+        lo |= static_cast<uint64_t>(g.spread[(r[i] >> (8 * k)) & 0xff]) << (16 * k);
+        hi |= static_cast<uint64_t>(g.spread[(r[i] >> (8 * k + 32)) & 0xff]) << (16 * k);
+      }
+      sq[2 * i] = lo;
+      sq[2 * i + 1] = hi;
+    }
+    if ((N >> b) & 1) {  // ·x
+      for (int i = static_cast<int>(sq.size()) - 1; i > 0; --i)
+        sq[i] = (sq[i] << 1) | (sq[i - 1] >> 63);
+      sq[0] <<= 1;
+    }
+    reduce(g, sq);
+    r.swap(sq);
+  }
+  return r;
+}
+
+// Set coefficients of x^N mod φ (cached: a draw of a given length uses the same jumps).
+const std::vector<int32_t>& jump_terms(int64_t N) {
+  static std::mutex mu;
+  static std::map<int64_t, std::vector<int32_t>> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(N);
+  if (it != cache.end()) return it->second;
+  if (cache.size() > 256) cache.clear();
+  const Poly c = x_pow_mod(gf2(), N);
+  std::vector<int32_t> terms;
+  for (int i = 0; i < kDeg; ++i)
+    if (bit(c, i)) terms.push_back(i);
+  return cache.emplace(N, std::move(terms)).first->second;
+}
+
+// The array after R >= 1 refills of the array `cur` (w_0 … w_623).
+__attribute__((target("avx2"))) void jump_array_avx2(const uint32_t* cur, int64_t R,
+                                                     const std::vector<int32_t>& terms,
+                                                     uint32_t* out) {
+  constexpr int kU = kDeg + kN;  // u_0 … u_{kDeg+623}
+  std::vector<uint32_t> u(kU + kN);
+  uint32_t work[kN];
+  std::memcpy(work, cur, sizeof(work));
+  std::memcpy(u.data(), cur + 1, (kN - 1) * sizeof(uint32_t));
+  for (int k = kN - 1; k < kU; k += kN) {
+    next_state(work);
+    std::memcpy(u.data() + k, work, sizeof(work));
+  }
+  uint32_t acc[kN] = {};
+  for (const int32_t i : terms) {
+    const uint32_t* src = u.data() + i;
+    for (int j = 0; j < kN; ++j) acc[j] ^= src[j];
+  }
+  (void)R;
+  std::memcpy(out, acc, sizeof(acc));
+}
+
+// A small persistent pool for the split draws (one call at a time).
+class Pool {
+ public:
+  static Pool& get() {  // never destroyed: its detached workers wait on it until the process ends
+    static Pool* p = new Pool;
+    return *p;
+  }
+  std::mutex call_mu;  // serialises whole calls
+  void run(int n_tasks, const std::function<void(int)>& fn) {
+    ensure(n_tasks - 1);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      fn_ = &fn;
+      n_tasks_ = n_tasks;
+      pending_ = n_tasks - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    fn(0);
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return pending_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  void ensure(int workers) {
+    while (static_cast<int>(threads_.size()) < workers) {
+      const int idx = static_cast<int>(threads_.size()) + 1;
+      threads_.emplace_back([this, idx] { loop(idx); });
+      threads_.back().detach();
+    }
+  }
+  void loop(int idx) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(int)>* fn = nullptr;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (idx < n_tasks_) fn = fn_;
+      }
+      if (!fn) continue;
+      (*fn)(idx);
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--pending_ == 0) done_cv_.notify_all();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  std::vector<std::thread> threads_;
+  const std::function<void(int)>* fn_ = nullptr;
+  int n_tasks_ = 0, pending_ = 0;
+  uint64_t gen_ = 0;
+};
+
+int g_rng_threads = 0;  // HGD_TUNE_CPU_RNG_THREADS: 0 = auto, 1 = serial
+
+int rng_threads() {
+  if (g_rng_threads > 0) return g_rng_threads;
+  const unsigned hw = std::thread::hardware_concurrency();
+  return static_cast<int>(std::max(1u, std::min(8u, hw)));
+}
+
+// The split draw: thread 0 continues the real state over the head of the current block and the
+// first Q refills; thread t >= 1 starts at refill 1 + t·Q from a jumped array. The last thread
+// with draws leaves the final state.
+int64_t draw_split(Draws& g, int64_t n, float keep, uint8_t* mask, int T) {
+  const int64_t Q = ((n + kN - 1) / kN + T - 1) / T;  // refills per thread (from n alone)
+  const int64_t head = std::min<int64_t>(n, g.left - 1);
+  const int64_t rest = n - head;
+  const int64_t r_tot = (rest + kN - 1) / kN;
+  const int used = static_cast<int>(std::max<int64_t>(1, (r_tot + Q - 1) / Q));
+  std::vector<int64_t> counts(used, 0);
+  std::vector<Draws> st(used);
+  st[0] = g;
+  std::vector<const std::vector<int32_t>*> terms(used, nullptr);
+  for (int t = 1; t < used; ++t) terms[t] = &jump_terms(kN * (1 + t * Q) - 1);
+  auto task = [&](int t) {
+    if (t >= used) return;
+    const int64_t lo = t == 0 ? 0 : head + t * Q * kN;
+    const int64_t hi = std::min<int64_t>(n, head + (t + 1) * Q * kN);
+    if (t > 0) {
+      jump_array_avx2(g.s, 1 + t * Q, *terms[t], st[t].s);
+      st[t].left = kN + 1;
+      st[t].next = 0;
+    }
+    counts[t] = draw_any(st[t], hi - lo, keep, mask + lo);
+  };
+  Pool::get().run(used, task);
+  g = st[used - 1];
+  int64_t cnt = 0;
+  for (int64_t c : counts) cnt += c;
+  return cnt;
+}
+
 }  // namespace
+
+void set_cpu_rng_threads(int threads) { g_rng_threads = threads; }
+
+// Self-check of the jump (tests): the array after R refills of the seeded state, by stepping
+// and by the GF(2) jump, must be equal.
+bool cpu_rng_jump_selfcheck(int64_t R) {
+  if (!gf2().ok) return false;
+  uint32_t s[kN], a[kN], b[kN];
+  seed_array(s, 1234u);
+  next_state(s);
+  std::memcpy(a, s, sizeof(a));
+  for (int64_t r = 0; r < R; ++r) next_state(a);
+  jump_array_avx2(s, R, jump_terms(kN * R - 1), b);
+  return std::memcmp(a, b, sizeof(a)) == 0;
+}
+
 }  // namespace hgd
 
 extern "C" size_t hgd_torch_cpu_state_bytes(void) { return sizeof(hgd::TorchCpuState); }
+
+extern "C" int32_t hgd_torch_cpu_jump_selfcheck(int64_t refills) {
+  return refills >= 1 && hgd::cpu_rng_jump_selfcheck(refills) ? 1 : 0;
+}
 
 extern "C" hgd_status hgd_torch_cpu_keep_mask(uint8_t* torch_state, int64_t state_bytes,
                                               int64_t n, float keep, uint8_t* mask,
@@ -141,9 +452,17 @@ extern "C" hgd_status hgd_torch_cpu_keep_mask(uint8_t* torch_state, int64_t stat
   for (int i = 0; i < kN; ++i) g.s[i] = static_cast<uint32_t>(L.state[i]);
   g.left = L.left;
   g.next = static_cast<uint32_t>(L.next);
+  // long draws split over threads from jumped states (bitwise the serial draw); short ones, a
+  // serial tuning or a CPU without AVX2 run the one-thread loop
   static const bool avx2 = __builtin_cpu_supports("avx2");
-  const int64_t cnt = n == 0 ? 0 : (avx2 ? draw_mask_avx2(g, n, keep, mask)
-                                         : draw_mask_base(g, n, keep, mask));
+  const int T = rng_threads();
+  int64_t cnt;
+  if (T > 1 && avx2 && n >= static_cast<int64_t>(T) * 64 * kN && gf2().ok) {
+    std::lock_guard<std::mutex> lk(Pool::get().call_mu);
+    cnt = draw_split(g, n, keep, mask, T);
+  } else {
+    cnt = draw_any(g, n, keep, mask);
+  }
   for (int i = 0; i < kN; ++i) L.state[i] = g.s[i];
   L.left = g.left;
   L.next = g.next;

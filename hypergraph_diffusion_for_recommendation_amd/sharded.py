@@ -26,6 +26,7 @@ The reference has no distributed code at all; this is new desi
 from __future__ import annotations
 
 import ctypes
+import time
 from typing import List, Optional, Tuple
 
 import numpy as np
@@ -99,6 +100,14 @@ def shard_rows_of_sorted_coo(indices: torch.Tensor, n_users: int, world: int, ra
 TRANSPORTS = ("rccl", "p2p")
 
 
+def _scale_of_degrees(deg: torch.Tensor, kind: str) -> torch.Tensor:
+    """1/deg ('mean') or 1/sqrt(deg) ('sym') of float64 degrees, 0 where deg = 0, rounded to
+    fp32: every step correctly rounded, so it is bitwise the library's hgd_degree_scale and the
+    native communicator's global scales (handle.hip k_scale_from_f64)."""
+    inv = deg if kind == "mean" else deg.sqrt()
+    return torch.where(deg > 0, 1.0 / inv, torch.zeros_like(deg)).to(torch.float32)
+
+
 class P2PExchange:
     """The direct xGMI peer transport (``hgd_p2p_*``, csrc/p2p.hip): every rank exposes one
     uncached buffer of ``n_slots`` send slots to its peers; an all-reduce of a slot is a two-shot
@@ -107,7 +116,7 @@ class P2PExchange:
     (the IPC handles travel by ``all_gather_object``)."""
 
     def __init__(self, max_count: int, n_slots: int, device: torch.device, group=None,
-                 timeout_s: float = 30.0):
+                 timeout_s: float = 30.0, trace=None):
         self.lib = nat.load()
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -115,20 +124,26 @@ class P2PExchange:
         self.device = torch.device(device)
         self.max_count = int(-(-int(max_count) // 4) * 4)
         self.n_slots = int(n_slots)
+        self.timeout_s = float(timeout_s)
+        trace = trace or (lambda msg: None)
         h = ctypes.c_void_p()
         nat.check(self.lib.hgd_p2p_create(self.world, self.rank, self.max_count, self.n_slots,
                                           ctypes.byref(h)), "hgd_p2p_create")
         self.h = h
-        nat.check(self.lib.hgd_p2p_set_timeout(h, float(timeout_s)), "hgd_p2p_set_timeout")
+        trace("p2p: created")
+        nat.check(self.lib.hgd_p2p_set_timeout(h, self.timeout_s), "hgd_p2p_set_timeout")
         mine = ctypes.create_string_buffer(nat.P2P_HANDLE_BYTES)
         nat.check(self.lib.hgd_p2p_export(h, mine), "hgd_p2p_export")
+        trace("p2p: exported")
         handles = [None] * self.world
         if self.world > 1:
             dist.all_gather_object(handles, mine.raw, group=group)
         else:
             handles = [mine.raw]
+        trace("p2p: handles gathered")
         blob = ctypes.create_string_buffer(b"".join(handles), nat.P2P_HANDLE_BYTES * self.world)
         nat.check(self.lib.hgd_p2p_open(h, blob), "hgd_p2p_open")
+        trace("p2p: peers opened")
         self._views = {}
 
     def slot(self, k: int, rows: int, cols: int) -> torch.Tensor:
@@ -151,6 +166,29 @@ class P2PExchange:
 
     def check(self) -> None:
         nat.check(self.lib.hgd_p2p_check(self.h), "hgd_p2p")
+
+    def poll(self) -> None:
+        """Raises if a wait that has already run timed out (a host-visible flag: no sync)."""
+        nat.check(self.lib.hgd_p2p_poll(self.h), "hgd_p2p")
+
+    def wait(self, stream: Optional[torch.cuda.Stream] = None,
+             timeout_s: Optional[float] = None) -> None:
+        """Waits on the host until the work queued so far on ``stream`` (default: the current
+        stream) has finished, for at most ``timeout_s`` (default: twice the device wait bound
+        plus a minute); raises TimeoutError instead of blocking forever, so a stall anywhere in
+        the device queue — not only in a wait kernel that is running — surfaces as an error."""
+        stream = stream or torch.cuda.current_stream(self.device)
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        limit = timeout_s if timeout_s is not None else 2.0 * self.timeout_s + 60.0
+        t0 = time.perf_counter()
+        pause = 1e-4
+        while not ev.query():
+            if time.perf_counter() - t0 > limit:
+                raise TimeoutError(f"hgd_p2p rank {self.rank}: device queue not drained after "
+                                   f"{limit:.0f} s (device-side wait bound {self.timeout_s} s)")
+            time.sleep(pause)
+            pause = min(2 * pause, 0.05)
 
     def close(self) -> None:
         """Collective: every rank's peers stop reading before the buffers go."""
@@ -210,7 +248,8 @@ class ShardedIncidence:
 
     def __init__(self, inc: Incidence, group=None, n_chunks: int = 1,
                  P: Optional[str] = "sym", Q: Optional[str] = "mean", R: Optional[str] = "sym",
-                 slice_width: Optional[int] = None, transport: str = "rccl"):
+                 slice_width: Optional[int] = None, transport: str = "rccl",
+                 p2p_timeout_s: float = 30.0, trace=None):
         if transport not in TRANSPORTS:
             raise ValueError(f"ShardedIncidence: transport must be one of {TRANSPORTS}")
         self.inc = inc
@@ -218,6 +257,8 @@ class ShardedIncidence:
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.P, self.R = P, R
         self.transport = transport
+        self.p2p_timeout_s = float(p2p_timeout_s)
+        self.trace = trace
         self.n_chunks = max(1, int(n_chunks)) if self.world > 1 else 1
         self.slice_width = slice_width
         self._p2p = None
@@ -266,9 +307,7 @@ class ShardedIncidence:
             raise ValueError(f"sharded: unsupported item scale {kind!r}")
         deg = (self.inc.csc.rowptr[1:] - self.inc.csc.rowptr[:-1]).to(torch.float64)
         dist.all_reduce(deg, group=self.group)
-        p = -1.0 if kind == "mean" else -0.5
-        s = torch.where(deg > 0, deg.pow(p), torch.zeros_like(deg))
-        return s.to(torch.float32)
+        return _scale_of_degrees(deg, kind)
 
     def p2p(self, d: int) -> P2PExchange:
         """The peer transport for width ``d`` (created on first use: collective)."""
@@ -277,7 +316,8 @@ class ShardedIncidence:
         if self._p2p is None or self._p2p.max_count < need or self._p2p.n_slots < 2 * len(sl):
             if self._p2p is not None:
                 self._p2p.close()
-            self._p2p = P2PExchange(need, 2 * len(sl), self.inc.device, group=self.group)
+            self._p2p = P2PExchange(need, 2 * len(sl), self.inc.device, group=self.group,
+                                    timeout_s=self.p2p_timeout_s, trace=self.trace)
         if self._side is None:
             lo, _hi = torch.cuda.Stream.priority_range()
             self._side = torch.cuda.Stream(self.inc.device, priority=min(lo, _hi))
@@ -300,6 +340,9 @@ class ShardedIncidence:
         sl = self.slices(d)
         if use_p2p:
             ex = self.p2p(d)
+            # an earlier exchange that timed out leaves NaN in its output; stop at the next call
+            # instead of propagating it (the flag is host-visible, no synchronisation)
+            ex.poll()
             parity = self._calls % 2
             self._calls += 1
             cur = torch.cuda.current_stream(X.device)
@@ -547,8 +590,7 @@ class ShardedBipartite:
         deg = (o.rowptr[1:] - o.rowptr[:-1]).to(torch.float64)
         if side == "item" and self.world > 1:
             dist.all_reduce(deg, group=self.group)
-        p = -1.0 if kind == "mean" else -0.5
-        s = torch.where(deg > 0, deg.pow(p), torch.zeros_like(deg)).to(torch.float32)
+        s = _scale_of_degrees(deg, kind)
         self._scales[key] = s
         return s
 

@@ -85,7 +85,16 @@ typedef enum hgd_epilogue {
  *   HGD_TUNE_X3S_TILES:   form of the staged split-bf16 row GEMM at N > 32: 1 or 2 16-column
  *                         tiles per wave (1: half the W registers, two workgroups per CU), 3 =
  *                         two tiles + 4 producer waves that load and split the rows while the
- *                         others multiply; 0 = default (1 for masked products, else 3) */
+ *                         others multiply; 0 = default (1 for masked products, else 3)
+ *   HGD_TUNE_P2P_SEGMENT_MB: largest allocation hgd_p2p_create exposes to its peers, in MiB
+ *                         (0 = default 1024; slots are packed whole into segments of at most
+ *                         this size, each imported separately: a single 3.5 GiB import never
+ *                         returned on the ROCm 7.2 box); applies to later hgd_p2p_create calls
+ *   HGD_TUNE_P2P_CACHED:  0 (default) = uncached segments (hipDeviceMallocUncached); 1 = plain
+ *                         device memory (the exchange's fences keep it correct either way; the
+ *                         knob prices what uncached hop-1 stores cost)
+ *   HGD_TUNE_CPU_RNG_THREADS: host threads of hgd_torch_cpu_keep_mask's split draw (0 = default
+ *                         min(8, hardware threads); 1 = one thread) */
 typedef enum hgd_tune_key {
   HGD_TUNE_SPMM_UNROLL = 1,
   HGD_TUNE_SPMM_POLICY = 2,
@@ -95,7 +104,10 @@ typedef enum hgd_tune_key {
   HGD_TUNE_GEMM_EXACT = 6,
   HGD_TUNE_X3_COLS = 7,
   HGD_TUNE_X3_SPLITK = 8,
-  HGD_TUNE_X3S_TILES = 9
+  HGD_TUNE_X3S_TILES = 9,
+  HGD_TUNE_P2P_SEGMENT_MB = 10,
+  HGD_TUNE_P2P_CACHED = 11,
+  HGD_TUNE_CPU_RNG_THREADS = 12
 } hgd_tune_key;
 hgd_status hgd_set_tuning(int32_t key, int32_t value);
 
@@ -634,10 +646,14 @@ hgd_status hgd_sample_pairwise(uint32_t* mt_state, const int64_t* order, int64_t
 /* SpAdjDropEdge's CPU keep-mask (HCCF.py:223: floor(torch.rand(nnz) + keepRate).bool()) from
  * torch's default CPU generator, bit for bit, in one host pass (HOST function). torch_state =
  * the bytes of torch.get_rng_state() (hgd_torch_cpu_state_bytes(), 5056 on x86-64), advanced in
- * place by n draws for torch.set_rng_state; mask uint8 [n] (host); *kept = number of ones. */
+ * place by n draws for torch.set_rng_state; mask uint8 [n] (host); *kept = number of ones.
+ * Long draws are split over host threads (HGD_TUNE_CPU_RNG_THREADS), each starting from the
+ * MT19937 state its first draw sees, computed by a GF(2) jump-ahead: the same bits as one thread. */
 size_t hgd_torch_cpu_state_bytes(void);
 hgd_status hgd_torch_cpu_keep_mask(uint8_t* torch_state, int64_t state_bytes, int64_t n,
                                    float keep, uint8_t* mask, int64_t* kept);
+/* Test hook: 1 if the jump-ahead reproduces `refills` MT19937 refills of a seeded state. */
+int32_t hgd_torch_cpu_jump_selfcheck(int64_t refills);
 
 /* ------------------------------------------------------------------------------------------
  * Sorted unique of integer keys — torch.unique(t.long()) as HCCF's loss calls it every step on
@@ -822,9 +838,10 @@ hgd_status hgd_comm_get_unique_id(void* id_out);
 /* Collective over the nranks processes; binds the communicator to the current HIP device. */
 hgd_status hgd_comm_create(const void* id, int32_t nranks, int32_t rank, hgd_comm** out);
 void hgd_comm_destroy(hgd_comm* comm);
-/* Item chunks per exchange for the overlapped hop (default 4, 1..64). */
+/* Item chunks per exchange for the overlapped hop (default 4, 1..64; RCCL transport). */
 hgd_status hgd_comm_set_chunks(hgd_comm* comm, int32_t n_chunks);
-/* In-place sum of a device fp32 buffer over the ranks, ordered on `stream`. */
+/* In-place sum of a device fp32 buffer over the ranks, ordered on `stream` (over the peer
+ * exchange: count a multiple of 4 <= its max_count, buf 16-byte aligned; uses send slot 0). */
 hgd_status hgd_exchange_allreduce(hgd_comm* comm, float* buf, int64_t count, void* stream);
 /* Replaces the object's column degrees by their sum over the ranks (each rank holds a user
  * shard of the same item set), so column scales — the Q of conv2hop — are global. Collective;
@@ -835,26 +852,45 @@ hgd_status hgd_incidence_globalize_columns(hgd_incidence* inc, hgd_comm* comm, v
  * transport to RCCL for the same all-reduce of the item messages: a two-shot reduce over the
  * mesh — rank r sums block r of every rank's send slot (reading the N-1 peers over their own
  * xGMI links at once, ranks summed in ascending order), then gathers the other blocks from the
- * peers' reduced slots. Every rank exposes one uncached allocation (flags + n_slots send slots
- * + n_slots reduced slots of max_count floats) through hipIpcGetMemHandle. Setup is
- * collective out of band: create, export, exchange the handles (e.g. all_gather), open.
- * Waits are bounded (hgd_p2p_set_timeout, default 30 s): a timeout sets a device error flag,
- * reported by hgd_p2p_check, and later exchanges become no-ops instead of hanging the GPU.
+ * peers' reduced slots. Every rank exposes a flag page and 2·n_slots slots of max_count floats
+ * (send, then reduced) in uncached segments of at most 1 GiB (HGD_TUNE_P2P_SEGMENT_MB), each
+ * through hipIpcGetMemHandle. Setup is collective out of band: create, export, exchange the
+ * handles (e.g. all_gather), open. Peer reads follow a system-scope acquire and announced
+ * stores a system-scope release, so correctness does not depend on how the importing device
+ * caches peer memory (csrc/p2p.hip, "Memory ordering").
+ * Waits are bounded (hgd_p2p_set_timeout, default 30 s): a timeout sets a device error flag
+ * and a host-visible copy; hgd_p2p_poll reports it without synchronising, hgd_p2p_check after
+ * a sync, and every later exchange writes NaN into its output instead of summing.
  * A slot used by exchange i may be rewritten once any later exchange j > i has completed on
  * this rank's stream; every rank must issue the same exchanges in the same order.
  * Replaces: nothing in the reference (no distributed code, HCCF.py:24); the design's own. */
 typedef struct hgd_p2p hgd_p2p;
-#define HGD_P2P_HANDLE_BYTES 128
-/* nranks 1..8; max_count a positive multiple of 4 (floats per slot); n_slots 1..1024. */
+#define HGD_P2P_HANDLE_BYTES 4096
+/* A communicator whose exchanges run over an OPENED peer exchange instead of RCCL (no RCCL
+ * communicator; `p2p` must outlive it and is not destroyed with it). conv2hop over it pipelines
+ * column slices: hop 1 of a slice writes straight into a send slot, the slot's mesh reduce runs
+ * on the communicator's high-priority side stream, hop 2 of the slice waits only for it (the
+ * same slices, slots and kernels as sharded.ShardedIncidence with transport 'p2p'). Needs
+ * d % 4 == 0 and 2·ceil(d / width) slots of n_cols·width floats. hgd_incidence_globalize_columns
+ * over it sums the degrees exactly (16-bit limbs). */
+hgd_status hgd_comm_create_p2p(hgd_p2p* p2p, int32_t nranks, int32_t rank, hgd_comm** out);
+/* Column-slice width of the peer-exchange pipeline: 0 = default (32 for d <= 128, else 64),
+ * else a multiple of 4. */
+hgd_status hgd_comm_set_slice_width(hgd_comm* comm, int32_t width);
+/* nranks 1..8; max_count a positive multiple of 4 (floats per slot, at most one segment);
+ * n_slots 1..1024 (at most 62 segments in all). */
 hgd_status hgd_p2p_create(int32_t nranks, int32_t rank, int64_t max_count, int32_t n_slots,
                           hgd_p2p** out);
 void hgd_p2p_destroy(hgd_p2p* p2p);
 /* This rank's handle (HGD_P2P_HANDLE_BYTES host bytes) for its peers. */
 hgd_status hgd_p2p_export(const hgd_p2p* p2p, void* handle_out);
-/* `handles`: nranks × HGD_P2P_HANDLE_BYTES in rank order (this rank's own entry included). */
+/* `handles`: nranks × HGD_P2P_HANDLE_BYTES in rank order (this rank's own entry included).
+ * Checks that every imported mapping spans the peer's whole allocation. */
 hgd_status hgd_p2p_open(hgd_p2p* p2p, const void* handles);
 /* Device pointer of this rank's send slot (max_count floats; write the partial sums here). */
 float* hgd_p2p_slot(hgd_p2p* p2p, int32_t slot);
+int32_t hgd_p2p_n_slots(const hgd_p2p* p2p);
+int64_t hgd_p2p_max_count(const hgd_p2p* p2p);
 hgd_status hgd_p2p_set_timeout(hgd_p2p* p2p, double seconds);
 /* out[0:count) = Σ_ranks send_slot[0:count), ordered on `stream`; count a multiple of 4 and
  * out 16-byte aligned. */
@@ -862,6 +898,8 @@ hgd_status hgd_p2p_allreduce(hgd_p2p* p2p, int32_t slot, int64_t count, float* o
                              void* stream);
 /* Synchronous: HGD_OK, or HGD_ERR_HIP if any exchange timed out. */
 hgd_status hgd_p2p_check(hgd_p2p* p2p);
+/* Non-blocking: HGD_ERR_HIP if a wait that has already run timed out (host-visible flag). */
+hgd_status hgd_p2p_poll(const hgd_p2p* p2p);
 /* The block arithmetic of hgd_p2p_allreduce (host only, no device calls): rank q reduces floats
  * [*lo, *hi) of a `count`-float exchange over `nranks` ranks; gather step i of `rank` copies
  * float4 *j from rank *owner's reduced block (its own block is skipped). */
@@ -881,7 +919,8 @@ hgd_status hgd_p2p_gather_index(int64_t count, int32_t nranks, int32_t rank, int
  * Backward: dZ = epi'(dY) (act_ref = the forward Y when slope >= 0, else pre_act; NULL without
  * an epilogue), dM = Q·Aᵀ·(P·dZ), dX = R·A·dM — the same hops with P and R swapped.
  * comm != NULL: this rank's A is a user shard; hop 1's item sums are all-reduced (chunked and
- * overlapped on the communicator's stream) before hop 2; Q must be NONE or the global
+ * overlapped on the communicator's stream over RCCL, or column-sliced over the peer exchange of
+ * hgd_comm_create_p2p) before hop 2; Q must be NONE or the global
  * MEAN / SYM of hgd_incidence_globalize_columns. Epilogues with slope < 0 or dY with ldy != d
  * need contiguous rows. Workspace: hgd_conv2hop_workspace_size. */
 size_t hgd_conv2hop_workspace_size(const hgd_incidence* inc, int32_t d, int32_t epilogue);

@@ -33,10 +33,11 @@ assert nnz == r["config"]["edges"] == 99_999_492 and r["check"]["ok"]
 EOF
   [ $? -eq 0 ] || exit 1
 }
-# gloo stages each 256 MB all-reduce through host TCP: 21 s per step at N = 4 (run once:
-# profiles/r03_scale/bench_strong_4ranks_gloo_d64_check.json); N = 8 over gloo does not finish a
-# step within 9 minutes on one box, so the larger rehearsals use the peer transport (same sharding,
-# same check; gloo only for setup)
+# gloo stages each all-reduce through host TCP (21 s per step at N = 4, d = 64:
+# profiles/r03_scale/bench_strong_4ranks_gloo_d64_check.json; N = 8 at d = 256 reached "warm" at
+# 7.4 s, profiles/r03_scale/gloo_n8_d256.phases.txt). The default runs use the peer transport
+# (same sharding, same check; gloo only for setup): since round 4 its slots are exposed in
+# <= 1 GiB segments, and d = 256 runs at N = 4 and 8 (profiles/r04_scale/).
 STEPS="--steps ${REH_STEPS:-1} --warmup ${REH_WARMUP:-1}"
 for spec in ${REH_RUNS:-"p2p:4:64 p2p:8:64 p2p:4:256 p2p:8:256"}; do
   IFS=: read tr n d <<< "$spec"

@@ -37,10 +37,12 @@ def _partial(rank, count, rnd):
     return torch.randn(count, generator=g)
 
 
-def _allreduce_worker(rank, world, port, counts, outdir):
+def _allreduce_worker(rank, world, port, counts, outdir, seg_mb=0):
     dev = _init(rank, world, port)
     try:
+        from hypergraph_diffusion_for_recommendation_amd import _native as nat
         from hypergraph_diffusion_for_recommendation_amd.sharded import P2PExchange
+        nat.check(nat.load().hgd_set_tuning(10, seg_mb), "hgd_set_tuning")  # P2P_SEGMENT_MB
         ex = P2PExchange(max(counts), 4, dev, timeout_s=60.0)
         side = torch.cuda.Stream(dev)
         bad = []
@@ -59,6 +61,7 @@ def _allreduce_worker(rank, world, port, counts, outdir):
             if not torch.equal(got, ref):
                 bad.append((rnd, count, float((got - ref).abs().max())))
         ex.check()
+        ex.poll()
         torch.save(bad, os.path.join(outdir, f"r{rank}.pt"))
         ex.close()
     finally:
@@ -69,6 +72,18 @@ def _allreduce_worker(rank, world, port, counts, outdir):
 def test_p2p_allreduce_is_the_rank_ordered_sum(dev, tmp_path, world):
     counts = [4, 1 << 16, 12_345 * 4, (1 << 20) + 36, 8]
     mp.start_processes(_allreduce_worker, args=(world, _free_port(), counts, str(tmp_path)),
+                       nprocs=world, join=True, start_method="spawn")
+    for r in range(world):
+        assert torch.load(str(tmp_path / f"r{r}.pt"), weights_only=True) == [], r
+
+
+def test_p2p_allreduce_over_several_segments(dev, tmp_path):
+    """1 MiB segments: the 4 send + 4 reduced slots of 400 KB each live two to a segment, so the exchange addresses slots across four separately imported allocations (the
+    layout that keeps each import under the size at which hipIpcOpenMemHandle stalled)."""
+    world = 3
+    counts = [100_000, 4, 99_996, 65_536, 100_000, 40]
+    mp.start_processes(_allreduce_worker,
+                       args=(world, _free_port(), counts, str(tmp_path), 1),
                        nprocs=world, join=True, start_method="spawn")
     for r in range(world):
         assert torch.load(str(tmp_path / f"r{r}.pt"), weights_only=True) == [], r
@@ -137,14 +152,23 @@ def _timeout_worker(rank, world, port, outdir):
         ex = P2PExchange(1024, 2, dev, timeout_s=1.0)
         msg = "no error"
         if rank == 0:  # rank 1 never exchanges: rank 0's wait must give up after ~1 s
-            out = torch.empty(1024, device=dev)
+            out = torch.zeros(1024, device=dev)
             ex.allreduce(0, 1024, out, torch.cuda.current_stream(dev).cuda_stream)
-            ex.allreduce(1, 1024, out, torch.cuda.current_stream(dev).cuda_stream)  # a no-op now
-            torch.cuda.synchronize(dev)
+            out2 = torch.zeros(1024, device=dev)
+            ex.allreduce(1, 1024, out2, torch.cuda.current_stream(dev).cuda_stream)  # NaN now
+            ex.wait(timeout_s=30.0)
+            polled = "no error"
+            try:
+                ex.poll()  # host-visible flag, no sync
+            except HGDNativeError as e:
+                polled = str(e)
             try:
                 ex.check()
             except HGDNativeError as e:
                 msg = str(e)
+            # a failed exchange never passes for data: every element of both outputs is NaN
+            nan_out = bool(torch.isnan(out).all()) and bool(torch.isnan(out2).all())
+            msg = f"{msg}|poll: {polled}|nan: {nan_out}"
         with open(os.path.join(outdir, f"r{rank}.txt"), "w") as f:
             f.write(msg)
         dist.barrier()
@@ -157,4 +181,92 @@ def test_p2p_wait_is_bounded(dev, tmp_path):
     mp.start_processes(_timeout_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2,
                        join=True, start_method="spawn")
     msg = (tmp_path / "r0.txt").read_text()
-    assert "timed out waiting for rank 1" in msg, msg
+    check, polled, nan = msg.split("|")
+    assert "timed out waiting for rank 1" in check, msg
+    assert "timed out waiting for rank 1" in polled, msg
+    assert nan == "nan: True", msg
+
+
+def _native_conv_worker(rank, world, port, outdir):
+    """The sharded conv through the C ABI over a peer-exchange communicator
+    (hgd_comm_create_p2p, hgd_incidence_globalize_columns, hgd_conv2hop_forward / _backward)
+    against the Python ShardedIncidence on transport 'p2p', same shard, same inputs."""
+    import ctypes
+    dev = _init(rank, world, port)
+    try:
+        from hypergraph_diffusion_for_recommendation_amd import _native as nat
+        from hypergraph_diffusion_for_recommendation_amd.sharded import (P2PExchange,
+                                                                           ShardedIncidence,
+                                                                           sharded_two_hop)
+        from oracle import hgd_oracle as O
+        lib = nat.load()
+        U, I, d = 20_000, 3_000, 96  # d = 96: three 32-column slices, six slots
+        rows, cols = O.synthetic_incidence(U, I, 200_000, seed=5)
+        idx = torch.from_numpy(np.stack([rows, cols])).to(dev)
+        sh, u0, u1 = ShardedIncidence.from_global(idx, U, I, device=dev, transport="p2p")
+        g = torch.Generator().manual_seed(6)
+        X = torch.randn(U, d, generator=g)[u0:u1].to(dev)
+        G = torch.randn(U, d, generator=g)[u0:u1].to(dev)
+        st = torch.cuda.current_stream(dev).cuda_stream
+        # the native objects: the same local CSR, its own exchange and communicator
+        inc = sh.inc
+        h = ctypes.c_void_p()
+        nat.check(lib.hgd_incidence_create(inc.csr.rowptr.data_ptr(), inc.csr.col.data_ptr(),
+                                           None, inc.n_rows, I, inc.nnz, ctypes.byref(h), st),
+                  "hgd_incidence_create")
+        ex = P2PExchange(I * 32, 6, dev)
+        comm = ctypes.c_void_p()
+        nat.check(lib.hgd_comm_create_p2p(ex.h, world, rank, ctypes.byref(comm)),
+                  "hgd_comm_create_p2p")
+        nat.check(lib.hgd_incidence_globalize_columns(h, comm, st), "globalize")
+        q = ctypes.c_void_p()
+        nat.check(lib.hgd_incidence_scale(h, 1, 1, ctypes.byref(q)), "scale")  # cols, MEAN
+        q_nat = torch.empty(I, device=dev)
+        hip = ctypes.CDLL("libamdhip64.so")
+        assert hip.hipMemcpy(ctypes.c_void_p(q_nat.data_ptr()), q, ctypes.c_size_t(4 * I), 3) == 0
+        res = {"scale_equal": bool(torch.equal(q_nat, sh.q))}
+        ws = torch.empty(lib.hgd_conv2hop_workspace_size(h, d, 0), dtype=torch.uint8, device=dev)
+        same = []
+        for _ in range(3):  # both slot sets of both transports, reused
+            x = X.clone().requires_grad_(True)
+            y = sharded_two_hop(sh, x)
+            (dx,) = torch.autograd.grad(y, x, G)
+            Y = torch.empty(inc.n_rows, d, device=dev)
+            M = torch.empty(I, d, device=dev)
+            nat.check(lib.hgd_conv2hop_forward(h, 2, 1, 2, X.data_ptr(), d, d, Y.data_ptr(), d, 0,
+                                               0.0, M.data_ptr(), None, comm, ws.data_ptr(),
+                                               ws.numel(), st), "hgd_conv2hop_forward")
+            dX = torch.empty(inc.n_rows, d, device=dev)
+            nat.check(lib.hgd_conv2hop_backward(h, 2, 1, 2, G.data_ptr(), d, d, None, 0, 0.0,
+                                                dX.data_ptr(), d, comm, ws.data_ptr(), ws.numel(),
+                                                st), "hgd_conv2hop_backward")
+            torch.cuda.synchronize(dev)
+            same.append(bool(torch.equal(Y, y.detach())) and bool(torch.equal(dX, dx)))
+        res["conv_equal"] = same
+        # hgd_exchange_allreduce over the peer exchange: the rank-ordered sum, bitwise
+        buf = _partial(rank, 4096, 7).to(dev)
+        nat.check(lib.hgd_exchange_allreduce(comm, buf.data_ptr(), 4096, st), "allreduce")
+        ref = _partial(0, 4096, 7).clone()
+        for r in range(1, world):
+            ref += _partial(r, 4096, 7)
+        res["allreduce_equal"] = bool(torch.equal(buf.cpu(), ref))
+        ex.check()
+        sh._p2p.check()
+        torch.save(res, os.path.join(outdir, f"r{rank}.pt"))
+        lib.hgd_comm_destroy(comm)
+        lib.hgd_incidence_destroy(h)
+        dist.barrier()
+        ex.close()
+        sh.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_native_conv2hop_over_p2p_equals_python_p2p_conv(dev, tmp_path):
+    world = 2
+    mp.start_processes(_native_conv_worker, args=(world, _free_port(), str(tmp_path)),
+                       nprocs=world, join=True, start_method="spawn")
+    for r in range(world):
+        res = torch.load(str(tmp_path / f"r{r}.pt"), weights_only=True)
+        assert res == {"scale_equal": True, "conv_equal": [True] * 3,
+                       "allreduce_equal": True}, (r, res)
