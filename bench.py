@@ -22,8 +22,8 @@ touches the GPU) and exits with its status; under a launcher WORLD_SIZE must equ
 Rank 0 prints ONE JSON line. ``roofline`` prices the dominant kernel (hgd_spmm) from HIP events
 recorded around every hop launch on its stream during the timed steps, with SURVEY.md §8d's
 algorithmic bytes; ``cpu_baseline`` times the reference's own library calls (torch.sparse.mm +
-autograd on CPU, oracle/ref_cpu.py) on a bounded sample of the same generator, on this box's
-host cores.
+autograd on CPU, oracle/ref_cpu.py) on the same graph and tables as the GPU run (copied to the
+host), on this box's host cores.
 """
 from __future__ import annotations
 
@@ -79,8 +79,8 @@ def parse():
     ap.add_argument("--check", action="store_true",
                     help="after timing, compare the sharded Y / dX with the single-GPU conv of "
                          "the global graph (strong scaling) at the 1e-5 relative bound")
-    ap.add_argument("--cpu-sample-edges", type=int, default=10_000_000)
-    ap.add_argument("--cpu-budget-s", type=float, default=25.0)
+    ap.add_argument("--cpu-budget-s", type=float, default=60.0,
+                    help="wall-clock budget of the CPU baseline's timed runs (after one warm-up)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc", default="auto", choices=["auto", "on", "off"],
                     help="measure HBM traffic with rocprofv3 PMC passes in a child process")
@@ -108,63 +108,50 @@ def make_graph(U, I, E, seed, zipf, device):
     return torch.stack([key // I, key % I])
 
 
-def cpu_baseline(U, I, E, zipf, sample_edges, budget_s, d):
-    """oracle/ref_cpu.py (torch.sparse.mm + autograd, the reference's own calls) on a bounded,
-    proportionally scaled sample of the same generator; median M-edges/s."""
-    import numpy as np
+def cpu_baseline(idx, X, dY, U, I, budget_s, d, label):
+    """oracle/ref_cpu.py (torch.sparse.mm + autograd, the reference's own calls) on the SAME
+    inputs as the GPU run — the headline graph and the X / dY tables, copied to the host
+    (SURVEY.md §8d "same run, same inputs"): one warm-up, then timed runs while the budget lasts
+    (at least one), median M-edges/s at torch's host threads; then one run at one thread."""
+    import psutil
     import torch
 
-    from oracle import hgd_oracle as O
     from oracle import ref_cpu
-
-    f = min(1.0, sample_edges / E)
-    u_s, i_s, e_s = max(1, int(U * f)), max(1, int(I * f)), max(1, int(E * f))
-    rows, cols = O.synthetic_incidence(u_s, i_s, e_s, seed=0, zipf=zipf)
-    H = ref_cpu.coo_tensor(rows, cols, None, (u_s, i_s))
-    g = torch.Generator().manual_seed(1)
-    X = torch.empty(u_s, d)
-    torch.nn.init.xavier_uniform_(X, generator=g)
-    dY = torch.randn(u_s, d, generator=g)
+    nnz = int(idx.shape[1])
+    t_setup = time.perf_counter()
+    H = torch.sparse_coo_tensor(idx, torch.ones(nnz, dtype=torch.float32), (U, I))
+    setup_s = time.perf_counter() - t_setup
     times = []
     t_start = time.perf_counter()
     ref_cpu.hgconv2_fwd_bwd(H, X, dY)  # warm-up
-    while len(times) < 5 and (time.perf_counter() - t_start) < budget_s or len(times) < 1:
+    while not times or (len(times) < 5 and time.perf_counter() - t_start < budget_s):
         t0 = time.perf_counter()
         ref_cpu.hgconv2_fwd_bwd(H, X, dY)
         times.append(time.perf_counter() - t0)
     t = statistics.median(times)
+    ram = psutil.virtual_memory().total / 2**30
     out = {
-        "value": round(len(rows) / t / 1e6, 3),
+        "value": round(nnz / t / 1e6, 3),
         "unit": "M-edges/s",
         "cores": torch.get_num_threads(),
         "kind": "port",
-        "sample": (f"{u_s}x{i_s} graph, {len(rows)} edges (same generator scaled by {f:.3g}), "
-                   f"d={d}, torch.sparse.mm fwd+bwd (oracle/ref_cpu.py), median of "
-                   f"{len(times)} runs, {t:.3f} s/run"),
+        "sample": (f"the headline workload itself ({label}: {U}x{I} graph, {nnz} edges, d={d}, "
+                   f"the GPU run's graph and X / dY copied to the host), torch.sparse.mm fwd+bwd "
+                   f"(oracle/ref_cpu.py), median of {len(times)} runs after one warm-up, "
+                   f"{t:.2f} s/run; host RAM {ram:.0f} GiB"),
     }
-    # SURVEY.md §8d: also a 1-thread figure, on a 10x smaller sample of the same generator
-    f1 = f / 10
-    u1, i1, e1 = max(1, int(U * f1)), max(1, int(I * f1)), max(1, int(E * f1))
-    r1, c1 = O.synthetic_incidence(u1, i1, e1, seed=0, zipf=zipf)
-    H1 = ref_cpu.coo_tensor(r1, c1, None, (u1, i1))
-    X1 = torch.empty(u1, d)
-    torch.nn.init.xavier_uniform_(X1, generator=g)
-    dY1 = torch.randn(u1, d, generator=g)
+    # SURVEY.md §8d: also a 1-thread figure — one run of the same workload
     threads = torch.get_num_threads()
     torch.set_num_threads(1)
     try:
-        ref_cpu.hgconv2_fwd_bwd(H1, X1, dY1)  # warm-up
-        t1s = []
-        for _ in range(3):
-            t0 = time.perf_counter()
-            ref_cpu.hgconv2_fwd_bwd(H1, X1, dY1)
-            t1s.append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        ref_cpu.hgconv2_fwd_bwd(H, X, dY)
+        t1 = time.perf_counter() - t0
     finally:
         torch.set_num_threads(threads)
-    t1 = statistics.median(t1s)
-    out["single_thread"] = {"value": round(len(r1) / t1 / 1e6, 3), "cores": 1,
-                            "sample": f"{u1}x{i1} graph, {len(r1)} edges, median of 3, "
-                                      f"{t1:.3f} s/run"}
+    out["single_thread"] = {"value": round(nnz / t1 / 1e6, 3), "cores": 1,
+                            "sample": f"the same workload, one run, {t1:.2f} s"}
+    out["setup_s"] = round(setup_s, 2)
     return out
 
 
@@ -392,6 +379,8 @@ def main():
         inc = Incidence.from_coo(idx, None, (U, I), device=device, validate=False,
                                  rows_sorted=True)
         sh = ShardedIncidence(inc, **shard_kw)
+    want_cpu = not args.no_cpu_baseline and world == 1 and not args.pmc_child
+    idx_host = idx.cpu() if want_cpu else None  # the CPU baseline runs on the same graph
     if not keep_global:
         del idx
     nnz = inc.nnz
@@ -570,8 +559,13 @@ def main():
                                             4)
 
     cpu = None
-    if not args.no_cpu_baseline and world == 1:
-        cpu = cpu_baseline(U, I, E, zipf, args.cpu_sample_edges, args.cpu_budget_s, d)
+    if want_cpu:
+        Xh, dYh = X.detach().cpu(), dY.cpu()
+        del X, dY
+        torch.cuda.empty_cache()
+        cpu = cpu_baseline(idx_host, Xh, dYh, U, I, args.cpu_budget_s, d,
+                           f"{args.workload}-{U}x{I}x{E}-d{d}")
+        del idx_host, Xh, dYh
 
     if world == 1:
         parallelism = "single GPU"

@@ -2,11 +2,14 @@
  * A plain-C host of the incidence-object ABI (include/hgd.h, "Incidence objects"): the HGNN
  * two-hop Y = D_v^-1/2·H·D_e^-1·Hᵀ·D_v^-1/2·X (data/graph.py:28-42) and its backward through
  * hgd_incidence_create + hgd_conv2hop_forward/backward, on user-row shards with the RCCL
- * exchange (hgd_comm_*) — what a native host would write in place of the reference's
- * torch.sparse.mm calls (HGNN_HD4.py:455-462).
+ * exchange (hgd_comm_*) or the direct peer exchange (hgd_p2p_* + hgd_comm_create_p2p) — what a
+ * native host would write in place of the reference's torch.sparse.mm calls
+ * (HGNN_HD4.py:455-462).
  *
  * One process per GPU. WORLD_SIZE / RANK (default 1 / 0) pick this process's user shard;
- * with WORLD_SIZE > 1, rank 0 writes the RCCL id to $HGD_COMM_ID_FILE and the others read it.
+ * HGD_TRANSPORT=p2p selects the peer exchange (default rccl). With WORLD_SIZE > 1 the setup
+ * travels through files next to $HGD_COMM_ID_FILE: rank 0 writes the RCCL id there, or every
+ * rank writes its hgd_p2p handle to $HGD_COMM_ID_FILE.<rank> and reads the others'.
  * Every rank builds the same deterministic graph, keeps its contiguous user range, runs the
  * sharded conv and checks its rows of Y and dX against a float64 host computation over the
  * whole graph (dX = the same operator applied to dY: the op is self-adjoint).
@@ -76,6 +79,52 @@ static int exchange_id(int world, int rank, void* id) {
   return 1;
 }
 
+static int read_file(const char* path, void* buf, size_t n) {
+  for (int tries = 0; tries < 6000; ++tries) { /* up to 60 s */
+    FILE* f = fopen(path, "rb");
+    if (f) {
+      size_t got = fread(buf, 1, n, f);
+      fclose(f);
+      if (got == n) return 0;
+    }
+    struct timespec ts = {0, 10 * 1000 * 1000};
+    nanosleep(&ts, NULL);
+  }
+  return 1;
+}
+
+/* The peer exchange: create, export, all-gather the handles through files, open. */
+static int open_p2p(int world, int rank, int64_t max_count, int32_t n_slots, hgd_p2p** out) {
+  static unsigned char handles[8 * HGD_P2P_HANDLE_BYTES];
+  if (world > 8) return 1;
+  if (hgd_p2p_create(world, rank, max_count, n_slots, out) != HGD_OK) return 1;
+  unsigned char* mine = handles + (size_t)rank * HGD_P2P_HANDLE_BYTES;
+  if (hgd_p2p_export(*out, mine) != HGD_OK) return 1;
+  if (world > 1) {
+    const char* path = getenv("HGD_COMM_ID_FILE");
+    if (!path) {
+      fprintf(stderr, "WORLD_SIZE > 1 needs HGD_COMM_ID_FILE\n");
+      return 1;
+    }
+    char name[4096], tmp[4200];
+    snprintf(name, sizeof name, "%s.%d", path, rank);
+    snprintf(tmp, sizeof tmp, "%s.tmp", name);
+    FILE* f = fopen(tmp, "wb");
+    if (!f || fwrite(mine, 1, HGD_P2P_HANDLE_BYTES, f) != HGD_P2P_HANDLE_BYTES) return 1;
+    fclose(f);
+    if (rename(tmp, name) != 0) return 1;
+    for (int q = 0; q < world; ++q) {
+      if (q == rank) continue;
+      snprintf(name, sizeof name, "%s.%d", path, q);
+      if (read_file(name, handles + (size_t)q * HGD_P2P_HANDLE_BYTES, HGD_P2P_HANDLE_BYTES)) {
+        fprintf(stderr, "rank %d: no p2p handle in %s\n", rank, name);
+        return 1;
+      }
+    }
+  }
+  return hgd_p2p_open(*out, handles) == HGD_OK ? 0 : 1;
+}
+
 int main(void) {
   const int world = getenv("WORLD_SIZE") ? atoi(getenv("WORLD_SIZE")) : 1;
   const int rank = getenv("RANK") ? atoi(getenv("RANK")) : 0;
@@ -125,10 +174,24 @@ int main(void) {
   /* object + communicator; item scales made global before the conv */
   hgd_incidence* H = NULL;
   CHECK_HGD(hgd_incidence_create(d_rowptr, d_col, NULL, Us, I, nnz_s, &H, st));
-  unsigned char id[HGD_COMM_ID_BYTES];
-  if (exchange_id(world, rank, id)) return 1;
+  const char* transport = getenv("HGD_TRANSPORT");
+  const int use_p2p = transport && strcmp(transport, "p2p") == 0;
   hgd_comm* comm = NULL;
-  CHECK_HGD(hgd_comm_create(id, world, rank, &comm));
+  hgd_p2p* p2p = NULL;
+  if (use_p2p) {
+    /* two sets of ceil(d / 32) column slices of the [I, 32] item messages (d <= 128) */
+    const int32_t n_slices = (d + 31) / 32;
+    if (open_p2p(world, rank, I * 32, 2 * n_slices, &p2p)) {
+      fprintf(stderr, "rank %d: peer exchange setup failed: %s\n", rank,
+              hgd_get_last_error_string());
+      return 1;
+    }
+    CHECK_HGD(hgd_comm_create_p2p(p2p, world, rank, &comm));
+  } else {
+    unsigned char id[HGD_COMM_ID_BYTES];
+    if (exchange_id(world, rank, id)) return 1;
+    CHECK_HGD(hgd_comm_create(id, world, rank, &comm));
+  }
   CHECK_HGD(hgd_incidence_globalize_columns(H, comm, st));
   CHECK_HGD(hgd_incidence_prepare(H, 1u << HGD_SCALE_SYM, st));
   const size_t wsb = hgd_conv2hop_workspace_size(H, d, HGD_EPI_NONE);
@@ -178,9 +241,27 @@ int main(void) {
     free(M);
     free(Ma);
   }
-  printf("rank %d/%d: users [%lld,%lld), nnz %lld, max |err| / magnitude = %.3e\n", rank, world,
-         (long long)u0, (long long)u1, (long long)nnz_s, worst);
+  printf("rank %d/%d (%s): users [%lld,%lld), nnz %lld, max |err| / magnitude = %.3e\n", rank,
+         world, use_p2p ? "p2p" : "rccl", (long long)u0, (long long)u1, (long long)nnz_s, worst);
   hgd_comm_destroy(comm);
+  if (p2p) {
+    CHECK_HGD(hgd_p2p_check(p2p));
+    if (world > 1) { /* the peers stop reading before the buffers go: a file barrier */
+      const char* path = getenv("HGD_COMM_ID_FILE");
+      char name[4096];
+      snprintf(name, sizeof name, "%s.done.%d", path, rank);
+      FILE* f = fopen(name, "wb");
+      if (!f) return 1;
+      fputc(1, f);
+      fclose(f);
+      for (int q = 0; q < world; ++q) {
+        unsigned char b;
+        snprintf(name, sizeof name, "%s.done.%d", path, q);
+        if (read_file(name, &b, 1)) return 1;
+      }
+    }
+    hgd_p2p_destroy(p2p);
+  }
   hgd_incidence_destroy(H);
   if (worst > 1e-5) {
     fprintf(stderr, "conv2hop_objects: mismatch\n");

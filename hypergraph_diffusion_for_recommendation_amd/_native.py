@@ -360,6 +360,8 @@ _SIGNATURES = {
     "hgd_p2p_set_timeout": (c_i32, [c_void_p, ctypes.c_double]),
     "hgd_p2p_allreduce": (c_i32, [c_void_p, c_i32, c_i64, c_void_p, c_void_p]),
     "hgd_p2p_check": (c_i32, [c_void_p]),
+    "hgd_p2p_price_local": (c_i32, [c_i32, c_i64, c_i32, c_i32, ctypes.POINTER(c_f32),
+                                    ctypes.POINTER(c_f32), c_void_p]),
     "hgd_comm_create_p2p": (c_i32, [c_void_p, c_i32, c_i32, _PP]),
     "hgd_comm_set_slice_width": (c_i32, [c_void_p, c_i32]),
     "hgd_p2p_poll": (c_i32, [c_void_p]),
@@ -407,7 +409,7 @@ def load() -> ctypes.CDLL:
                          (5, "HGD_SPLITK_ROWS"), (6, "HGD_GEMM_EXACT"),
                          (7, "HGD_X3_COLS"), (8, "HGD_X3_SPLITK"), (9, "HGD_X3S_TILES"),
                          (10, "HGD_P2P_SEGMENT_MB"), (11, "HGD_P2P_CACHED"),
-                         (12, "HGD_CPU_RNG_THREADS")):
+                         (12, "HGD_CPU_RNG_THREADS"), (13, "HGD_X3P_QUEUE")):
             if os.environ.get(env):
                 st = lib.hgd_set_tuning(key, int(os.environ[env]))
                 if st != HGD_OK:

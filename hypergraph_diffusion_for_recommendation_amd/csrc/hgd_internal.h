@@ -82,6 +82,8 @@ void set_x3_cols(int cols);
 void set_x3_splitk(int mode);
 // HGD_TUNE_X3S_TILES (linear.hip): 16-column tiles per wave of the staged row GEMM (0 = default).
 void set_x3s_tiles(int tiles);
+// HGD_TUNE_X3P_QUEUE (linear.hip): 1 = k_splitk_x3p's queue form (per-buffer counters).
+void set_x3p_queue(int queue);
 // HGD_TUNE_P2P_SEGMENT_MB / HGD_TUNE_P2P_CACHED (p2p.hip): layout of later hgd_p2p_create calls.
 void set_p2p_segment_mb(int mb);
 void set_p2p_cached(int cached);

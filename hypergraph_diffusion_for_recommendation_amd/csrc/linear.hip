@@ -378,6 +378,7 @@ int g_gemm_exact = 0;  // HGD_TUNE_GEMM_EXACT
 int g_x3_cols = 0;  // 0: default
 int g_x3s_tiles = 0;  // HGD_TUNE_X3S_TILES (0: default)
 int g_x3_splitk = 2;  // HGD_TUNE_X3_SPLITK: 1 split-bf16 weight gradient, 0 f32 MFMA, 2 auto
+int g_x3p_queue = 0;  // HGD_TUNE_X3P_QUEUE: 1 = the queue form of k_splitk_x3p
 
 // The split-bf16 split-K kernel pays for its six products with one k step in flight per slice:
 // at 144,242 × 128 it ran 79 µs against the f32-MFMA kernel's 59 µs; at 69,716 × 64 19.9 against
@@ -935,11 +936,19 @@ struct X3P {
   static constexpr int TM = MT / 4, TN = MT / 2;        // output tiles of a consumer wave
   static constexpr size_t PLANE = static_cast<size_t>(MT) * 16 * 4 * 16;  // one operand, one term
   static constexpr size_t LDS = 2 * 2 * 3 * PLANE;      // [buffer][operand][term]
+  // the queue form: three buffers and, after them, the stage counters full[3] / empty[3]
+  static constexpr size_t LDS_Q = 3 * 2 * 3 * PLANE + 64;
+  static constexpr uint32_t PROD_WAVES = PROD / 64;
 };
 
 __device__ __forceinline__ int x3p_unit(int c, int g) { return c * 4 + (g ^ ((c >> 1) & 3)); }
 
-template <int MT, bool MASK>
+// QUEUE: the producer and consumer sides meet through per-buffer counters instead of one
+// workgroup barrier per stage (three LDS buffers; a producer wave waits only until the consumers
+// have READ the stage three back, a consumer wave only until the 8 producer waves have written its
+// stage — the sides drift by up to two stages). The barrier form couples all 16 waves every 32
+// rows: PMC put them 49 % parked at that barrier (profiles/r03_linear/pmc).
+template <int MT, bool MASK, bool QUEUE>
 __global__ __launch_bounds__(X3P<MT>::THREADS) void k_splitk_x3p(SplitKGroup grp) {
   using C = X3P<MT>;
   constexpr size_t kX3pPlane = C::PLANE;
@@ -960,6 +969,26 @@ __global__ __launch_bounds__(X3P<MT>::THREADS) void k_splitk_x3p(SplitKGroup grp
   };
   float bsum[4] = {0.f, 0.f, 0.f, 0.f};  // dY producers: column sums of their block
   const int pt = tid - 512;              // producer thread index
+  // queue form: full[b] counts producer-wave arrivals at buffer b, empty[b] consumer-wave
+  // departures (monotone over the slice: stage i uses buffer i % 3 for the (i / 3)-th time)
+  uint32_t* const full = reinterpret_cast<uint32_t*>(x3p_smem + 3 * 2 * 3 * kX3pPlane);
+  uint32_t* const empty = full + 3;
+  if constexpr (QUEUE) {
+    if (tid < 6) full[tid] = 0u;
+    __syncthreads();
+  }
+  // bounded: every wave leaves the loop (the counts are reached within microseconds; a wrong
+  // count would give wrong sums, which the tests catch, never a grid that does not drain)
+  auto spin_until = [&](const uint32_t* c, uint32_t target) {
+    for (uint32_t n = 0; n < (1u << 22); ++n) {
+      if (__hip_atomic_load(c, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+  };
+  auto arrive = [&](uint32_t* c) {  // after this wave's LDS accesses of the stage
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
   const int pb = pt % (8 * C::C4), gq = pb / (2 * C::C4), hh = pb & 1, cb = (pb >> 1) % C::C4;
 
   // one producer role (OP 0: dY [+ mask], 1: X): a loop of exactly n_st barriers
@@ -1036,6 +1065,26 @@ __global__ __launch_bounds__(X3P<MT>::THREADS) void k_splitk_x3p(SplitKGroup grp
     };
 #pragma unroll
     for (int d = 0; d < D; ++d) load(d, raw[d], rawm[d]);
+    if constexpr (QUEUE) {
+      // stage i: wait until buffer i % 3 is free (its previous stage read), split, arrive, then
+      // refill the ring slot with stage i + D
+      auto qstep = [&](int64_t i, f32x4 (&a)[4], f32x4 (&m)[4]) {
+        const int b = static_cast<int>(i % 3);
+        if (i >= 3) spin_until(empty + b, 8u * static_cast<uint32_t>(i / 3));
+        split(i, b, a, m);
+        arrive(full + b);
+        load(i + D, a, m);
+      };
+      int64_t i0 = 0;
+      for (; i0 + D <= n_st; i0 += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) qstep(i0 + d, raw[d], rawm[d]);
+      }
+#pragma unroll
+      for (int d = 0; d < D; ++d)
+        if (i0 + d < n_st) qstep(i0 + d, raw[d], rawm[d]);
+      return;
+    }
     if (n_st > 0) {
       split(0, 0, raw[0], rawm[0]);
       load(D, raw[0], rawm[0]);
@@ -1068,6 +1117,33 @@ __global__ __launch_bounds__(X3P<MT>::THREADS) void k_splitk_x3p(SplitKGroup grp
     produce(std::integral_constant<int, 1>{});
   } else if (wave >= 8) {
     produce(std::integral_constant<int, 0>{});
+  } else if constexpr (QUEUE) {
+    for (int64_t i = 0; i < n_st; ++i) {
+      const int b = static_cast<int>(i % 3);
+      spin_until(full + b, C::PROD_WAVES * static_cast<uint32_t>(i / 3 + 1));
+      bf16x8 af[C::TM][3], bfr[C::TN][3];
+#pragma unroll
+      for (int t = 0; t < C::TM; ++t)
+#pragma unroll
+        for (int tm = 0; tm < 3; ++tm)
+          af[t][tm] = *reinterpret_cast<const bf16x8*>(
+              plane(b, 0, tm) +
+              static_cast<size_t>(x3p_unit(16 * (C::TM * mp + t) + i16, g)) * 16);
+#pragma unroll
+      for (int u = 0; u < C::TN; ++u)
+#pragma unroll
+        for (int tm = 0; tm < 3; ++tm)
+          bfr[u][tm] = *reinterpret_cast<const bf16x8*>(
+              plane(b, 1, tm) +
+              static_cast<size_t>(x3p_unit(16 * (C::TN * nq + u) + i16, g)) * 16);
+      arrive(empty + b);  // the fragments are in registers: the buffer may be refilled
+#pragma unroll
+      for (int u = 0; u < C::TN; ++u)
+#pragma unroll
+        for (int t = 0; t < C::TM; ++t)
+          acc[t][u] = mfma_x3(af[t][0], af[t][1], af[t][2], bfr[u][0], bfr[u][1], bfr[u][2],
+                              acc[t][u], false);
+    }
   } else {
     for (int64_t i = 0; i < n_st; ++i) {
       __syncthreads();
@@ -1301,25 +1377,31 @@ int64_t splits_for(int64_t rows, int64_t out_tiles) {
   return s < 1 ? 1 : s;
 }
 
+template <int MT, bool MASK, bool QUEUE>
+hgd_status launch_x3p_form(const SplitKGroup& g, int64_t Stot, hipStream_t st) {
+  using C = X3P<MT>;
+  constexpr size_t lds = QUEUE ? C::LDS_Q : C::LDS;
+  static bool lds_set = false;
+  const void* kern = reinterpret_cast<const void*>(&k_splitk_x3p<MT, MASK, QUEUE>);
+  if (!lds_set) {
+    if (lds > 65536)
+      HGD_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  static_cast<int>(lds)));
+    lds_set = true;
+  }
+  hipLaunchKernelGGL((k_splitk_x3p<MT, MASK, QUEUE>), dim3(static_cast<unsigned>(Stot)),
+                     dim3(C::THREADS), lds, st, g);
+  return HGD_OK;
+}
+
 template <int MT>
 hgd_status launch_x3p(const SplitKGroup& g, int64_t Stot, hipStream_t st) {
-  using C = X3P<MT>;
-  static bool lds_set[2] = {false, false};
-  const int mi = g.p[0].mask ? 1 : 0;
-  if (!lds_set[mi]) {
-    const void* kern = mi ? reinterpret_cast<const void*>(&k_splitk_x3p<MT, true>)
-                          : reinterpret_cast<const void*>(&k_splitk_x3p<MT, false>);
-    if (C::LDS > 65536)
-      HGD_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  static_cast<int>(C::LDS)));
-    lds_set[mi] = true;
-  }
-  const dim3 grid(static_cast<unsigned>(Stot));
-  if (mi)
-    hipLaunchKernelGGL((k_splitk_x3p<MT, true>), grid, dim3(C::THREADS), C::LDS, st, g);
-  else
-    hipLaunchKernelGGL((k_splitk_x3p<MT, false>), grid, dim3(C::THREADS), C::LDS, st, g);
-  return HGD_OK;
+  const bool mask = g.p[0].mask != nullptr;
+  if (g_x3p_queue)
+    return mask ? launch_x3p_form<MT, true, true>(g, Stot, st)
+                : launch_x3p_form<MT, false, true>(g, Stot, st);
+  return mask ? launch_x3p_form<MT, true, false>(g, Stot, st)
+              : launch_x3p_form<MT, false, false>(g, Stot, st);
 }
 
 // The producer-wave weight gradient (k_splitk_x3p): 128 × 128 or 64 × 64 outputs whose operand rows are
@@ -1458,6 +1540,7 @@ void set_gemm_exact(int exact) { g_gemm_exact = exact != 0; }
 void set_x3_cols(int cols) { g_x3_cols = cols; }
 void set_x3_splitk(int mode) { g_x3_splitk = mode; }
 void set_x3s_tiles(int tiles) { g_x3s_tiles = tiles; }
+void set_x3p_queue(int queue) { g_x3p_queue = queue; }
 }  // namespace hgd
 
 extern "C" hgd_status hgd_linear_forward(const float* X, int64_t ldx, int64_t n_rows,

@@ -461,6 +461,84 @@ extern "C" hgd_status hgd_p2p_poll(const hgd_p2p* h) {
   return HGD_OK;
 }
 
+// Pricing hook (profiles/r04_scale): the exchange's two data kernels at the block sizes of an
+// `nranks`-way exchange, with every "peer" slot a separate LOCAL allocation (uncached unless
+// `cached`): k_reduce of rank 0's block over nranks sources, then k_gather of the other
+// nranks - 1 blocks; mean ms per launch over `iters` launches each (HIP events on `stream`).
+// Local HBM stands in for the xGMI peers, so this prices the kernels' own cost, not the links.
+extern "C" hgd_status hgd_p2p_price_local(int32_t nranks, int64_t count, int32_t cached,
+                                          int32_t iters, float* ms_reduce, float* ms_gather,
+                                          void* stream) {
+  hgd::clear_error();
+  HGD_REQUIRE(nranks >= 1 && nranks <= kMaxRanks && count > 0 && count % 4 == 0 && iters >= 1 &&
+                  ms_reduce && ms_gather,
+              "hgd_p2p_price_local: bad arguments");
+  hipStream_t st = hgd::as_stream(stream);
+  const size_t bytes = static_cast<size_t>(count) * 4;
+  std::vector<void*> send(nranks, nullptr), red(nranks, nullptr);
+  void* out = nullptr;
+  int* err = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  auto cleanup = [&] {
+    for (void* p : send) if (p) (void)hipFree(p);
+    for (void* p : red) if (p) (void)hipFree(p);
+    if (out) (void)hipFree(out);
+    if (err) (void)hipFree(err);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+  };
+  const unsigned flag = cached ? hipDeviceMallocDefault : hipDeviceMallocUncached;
+  bool ok = hipMalloc(&out, bytes) == hipSuccess && hipMalloc(reinterpret_cast<void**>(&err),
+                                                              sizeof(int)) == hipSuccess &&
+            hipMemsetAsync(err, 0, sizeof(int), st) == hipSuccess &&
+            hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess;
+  for (int q = 0; ok && q < nranks; ++q)
+    ok = hipExtMallocWithFlags(&send[q], bytes, flag) == hipSuccess &&
+         hipExtMallocWithFlags(&red[q], bytes, flag) == hipSuccess &&
+         hipMemsetAsync(send[q], 0, bytes, st) == hipSuccess &&
+         hipMemsetAsync(red[q], 0, bytes, st) == hipSuccess;
+  if (!ok) {
+    cleanup();
+    return fail(HGD_ERR_HIP, "hgd_p2p_price_local: allocation of %d x 2 x %zu bytes failed",
+                nranks, bytes);
+  }
+  SlotPtrs sp{}, rp{};
+  for (int q = 0; q < kMaxRanks; ++q) {
+    sp.p[q] = static_cast<const float4*>(send[q < nranks ? q : 0]);
+    rp.p[q] = static_cast<const float4*>(red[q < nranks ? q : 0]);
+  }
+  const Blocks bl = Blocks::of(count, nranks);
+  float4* o = static_cast<float4*>(out);
+  const unsigned g1 = std::min<unsigned>(1024, hgd::grid_for(std::max<int64_t>(bl.b4, 1)));
+  const int64_t rest = bl.gather_count(0);
+  const unsigned g2 = std::min<unsigned>(2048, hgd::grid_for(std::max<int64_t>(rest, 1)));
+  auto reduce = [&] {
+    hipLaunchKernelGGL(k_reduce, dim3(g1), dim3(hgd::kBlock), 0, st, sp,
+                       const_cast<float4*>(rp.p[0]), bl, 0, nranks, o, err);
+  };
+  auto gather = [&] {
+    if (rest > 0) hipLaunchKernelGGL(k_gather, dim3(g2), dim3(hgd::kBlock), 0, st, rp, bl, 0, o, err);
+  };
+  float t = 0.f;
+  reduce();
+  gather();
+  ok = hipEventRecord(e0, st) == hipSuccess;
+  for (int i = 0; i < iters; ++i) reduce();
+  ok = ok && hipEventRecord(e1, st) == hipSuccess && hipEventSynchronize(e1) == hipSuccess &&
+       hipEventElapsedTime(&t, e0, e1) == hipSuccess;
+  *ms_reduce = t / iters;
+  ok = ok && hipEventRecord(e0, st) == hipSuccess;
+  for (int i = 0; i < iters; ++i) gather();
+  ok = ok && hipEventRecord(e1, st) == hipSuccess && hipEventSynchronize(e1) == hipSuccess &&
+       hipEventElapsedTime(&t, e0, e1) == hipSuccess;
+  *ms_gather = rest > 0 ? t / iters : 0.f;
+  const hipError_t le = hipGetLastError();
+  cleanup();
+  if (!ok || le != hipSuccess)
+    return fail(HGD_ERR_HIP, "hgd_p2p_price_local: timing failed: %s", hipGetErrorString(le));
+  return HGD_OK;
+}
+
 extern "C" int32_t hgd_p2p_n_slots(const hgd_p2p* h) { return h ? h->n_slots : 0; }
 extern "C" int64_t hgd_p2p_max_count(const hgd_p2p* h) { return h ? h->max_count : 0; }
 

@@ -20,6 +20,7 @@
 #include <cstdint>
 #include <cstring>
 #include <functional>
+#include <immintrin.h>
 #include <map>
 #include <mutex>
 #include <thread>
@@ -275,8 +276,9 @@ Poly x_pow_mod(const Gf2& g, int64_t N) {
   return r;
 }
 
-// Set coefficients of x^N mod φ (cached: a draw of a given length uses the same jumps).
-const std::vector<int32_t>& jump_terms(int64_t N) {
+// x^N mod φ as its nonzero 4-bit windows, (k << 4) | m for coefficient bits 4k + b, b in m
+// (cached: a draw of a given length uses the same jumps).
+const std::vector<int32_t>& jump_windows(int64_t N) {
   static std::mutex mu;
   static std::map<int64_t, std::vector<int32_t>> cache;
   std::lock_guard<std::mutex> lk(mu);
@@ -284,18 +286,41 @@ const std::vector<int32_t>& jump_terms(int64_t N) {
   if (it != cache.end()) return it->second;
   if (cache.size() > 256) cache.clear();
   const Poly c = x_pow_mod(gf2(), N);
-  std::vector<int32_t> terms;
-  for (int i = 0; i < kDeg; ++i)
-    if (bit(c, i)) terms.push_back(i);
-  return cache.emplace(N, std::move(terms)).first->second;
+  std::vector<int32_t> win;
+  for (int k = 0; 4 * k < kDeg; ++k) {
+    const int m = static_cast<int>((c[(4 * k) >> 6] >> ((4 * k) & 63)) & 15);
+    if (m) win.push_back((k << 4) | m);
+  }
+  return cache.emplace(N, std::move(win)).first->second;
 }
 
-// The array after R >= 1 refills of the array `cur` (w_0 … w_623).
-__attribute__((target("avx2"))) void jump_array_avx2(const uint32_t* cur, int64_t R,
-                                                     const std::vector<int32_t>& terms,
+// acc[j0 .. j0 + 8·NR) = ⊕ over windows (k, m) of V_m[4k + j0 ..]: NR ymm accumulators
+template <int NR>
+__attribute__((target("avx2"))) inline void xor_windows(const uint32_t* const* V,
+                                                        const std::vector<int32_t>& win, int j0,
+                                                        uint32_t* out) {
+  __m256i a[NR];
+  for (int r = 0; r < NR; ++r) a[r] = _mm256_setzero_si256();
+  for (const int32_t e : win) {
+    const uint32_t* src = V[e & 15] + 4 * (e >> 4) + j0;
+    for (int r = 0; r < NR; ++r)
+      a[r] = _mm256_xor_si256(a[r], _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src) + r));
+  }
+  for (int r = 0; r < NR; ++r) _mm256_storeu_si256(reinterpret_cast<__m256i*>(out + j0) + r, a[r]);
+}
+
+// The array after R >= 1 refills of the array `cur` (w_0 … w_623) from the windows of
+// x^(624R-1) mod φ: u_t = w_{t+1} for t < kDeg + 627 by plain refills, the 15 window tables
+// V_m[t] = ⊕_{b in m} u_{t+b}, then word j = ⊕_{(k,m)} V_m[4k + j] (4-bit windows halve the XORs
+// of the bit-by-bit sum; the accumulators stay in registers, 64 words at a time).
+__attribute__((target("avx2"))) void jump_array_avx2(const uint32_t* cur,
+                                                     const std::vector<int32_t>& win,
                                                      uint32_t* out) {
-  constexpr int kU = kDeg + kN;  // u_0 … u_{kDeg+623}
-  std::vector<uint32_t> u(kU + kN);
+  constexpr int kV = kDeg + kN;  // V_m[t] for t < kV (4k + j <= 19,936 + 623)
+  constexpr int kU = kV + 4;     // u_t for t < kV + 3
+  thread_local std::vector<uint32_t> u, tab;
+  u.resize(kU + kN);
+  tab.resize(16 * static_cast<size_t>(kV));
   uint32_t work[kN];
   std::memcpy(work, cur, sizeof(work));
   std::memcpy(u.data(), cur + 1, (kN - 1) * sizeof(uint32_t));
@@ -303,13 +328,23 @@ __attribute__((target("avx2"))) void jump_array_avx2(const uint32_t* cur, int64_
     next_state(work);
     std::memcpy(u.data() + k, work, sizeof(work));
   }
-  uint32_t acc[kN] = {};
-  for (const int32_t i : terms) {
-    const uint32_t* src = u.data() + i;
-    for (int j = 0; j < kN; ++j) acc[j] ^= src[j];
+  const uint32_t* V[16];
+  for (int m = 1; m < 16; ++m) {
+    uint32_t* v = tab.data() + static_cast<size_t>(m) * kV;
+    const int b = __builtin_ctz(m);
+    const uint32_t* sh = u.data() + b;
+    if (m == (1 << b)) {
+      std::memcpy(v, sh, kV * sizeof(uint32_t));
+    } else {
+      const uint32_t* prev = tab.data() + static_cast<size_t>(m & (m - 1)) * kV;
+      for (int t = 0; t < kV; ++t) v[t] = prev[t] ^ sh[t];
+    }
+    V[m] = v;
   }
-  (void)R;
-  std::memcpy(out, acc, sizeof(acc));
+  V[0] = nullptr;
+  static_assert(kN == 9 * 64 + 48, "block split of the 624 state words");
+  for (int j0 = 0; j0 < 9 * 64; j0 += 64) xor_windows<8>(V, win, j0, out);
+  xor_windows<6>(V, win, 9 * 64, out);
 }
 
 // A small persistent pool for the split draws (one call at a time).
@@ -388,14 +423,14 @@ int64_t draw_split(Draws& g, int64_t n, float keep, uint8_t* mask, int T) {
   std::vector<int64_t> counts(used, 0);
   std::vector<Draws> st(used);
   st[0] = g;
-  std::vector<const std::vector<int32_t>*> terms(used, nullptr);
-  for (int t = 1; t < used; ++t) terms[t] = &jump_terms(kN * (1 + t * Q) - 1);
+  std::vector<const std::vector<int32_t>*> wins(used, nullptr);
+  for (int t = 1; t < used; ++t) wins[t] = &jump_windows(kN * (1 + t * Q) - 1);
   auto task = [&](int t) {
     if (t >= used) return;
     const int64_t lo = t == 0 ? 0 : head + t * Q * kN;
     const int64_t hi = std::min<int64_t>(n, head + (t + 1) * Q * kN);
     if (t > 0) {
-      jump_array_avx2(g.s, 1 + t * Q, *terms[t], st[t].s);
+      jump_array_avx2(g.s, *wins[t], st[t].s);
       st[t].left = kN + 1;
       st[t].next = 0;
     }
@@ -421,7 +456,7 @@ bool cpu_rng_jump_selfcheck(int64_t R) {
   next_state(s);
   std::memcpy(a, s, sizeof(a));
   for (int64_t r = 0; r < R; ++r) next_state(a);
-  jump_array_avx2(s, R, jump_terms(kN * R - 1), b);
+  jump_array_avx2(s, jump_windows(kN * R - 1), b);
   return std::memcmp(a, b, sizeof(a)) == 0;
 }
 

@@ -40,10 +40,23 @@ class CapturedStep:
         # thread-local capture: a host thread of the harness (e.g. a keep-mask prefetch worker
         # allocating pinned memory) must not invalidate the capture
         with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
-            self.out = step(*self.static)
+            out = step(*self.static)
+        # keep the outputs' storage, not their autograd graph: a captured loss would hold the
+        # parameters' AccumulateGrad nodes (bound to the capture stream) alive, and a later eager
+        # step (a short last batch) would accumulate through them from another stream — torch's
+        # "AccumulateGrad node's stream does not match" warning and an extra sync
+        self.out = _detached(out)
 
     def __call__(self, *inputs: torch.Tensor):
         for dst, src in zip(self.static, inputs):
             dst.copy_(src)
         self.graph.replay()
         return self.out
+
+
+def _detached(x):
+    if isinstance(x, torch.Tensor):
+        return x.detach()
+    if isinstance(x, (tuple, list)):
+        return type(x)(_detached(v) for v in x)
+    return x

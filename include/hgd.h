@@ -94,7 +94,9 @@ typedef enum hgd_epilogue {
  *                         device memory (the exchange's fences keep it correct either way; the
  *                         knob prices what uncached hop-1 stores cost)
  *   HGD_TUNE_CPU_RNG_THREADS: host threads of hgd_torch_cpu_keep_mask's split draw (0 = default
- *                         min(8, hardware threads); 1 = one thread) */
+ *                         min(8, hardware threads); 1 = one thread)
+ *   HGD_TUNE_X3P_QUEUE:   form of the producer-wave weight gradient: 0 = one workgroup barrier
+ *                         per 32-row stage, 1 = three LDS buffers with full / empty counters */
 typedef enum hgd_tune_key {
   HGD_TUNE_SPMM_UNROLL = 1,
   HGD_TUNE_SPMM_POLICY = 2,
@@ -107,7 +109,8 @@ typedef enum hgd_tune_key {
   HGD_TUNE_X3S_TILES = 9,
   HGD_TUNE_P2P_SEGMENT_MB = 10,
   HGD_TUNE_P2P_CACHED = 11,
-  HGD_TUNE_CPU_RNG_THREADS = 12
+  HGD_TUNE_CPU_RNG_THREADS = 12,
+  HGD_TUNE_X3P_QUEUE = 13
 } hgd_tune_key;
 hgd_status hgd_set_tuning(int32_t key, int32_t value);
 
@@ -900,6 +903,12 @@ hgd_status hgd_p2p_allreduce(hgd_p2p* p2p, int32_t slot, int64_t count, float* o
 hgd_status hgd_p2p_check(hgd_p2p* p2p);
 /* Non-blocking: HGD_ERR_HIP if a wait that has already run timed out (host-visible flag). */
 hgd_status hgd_p2p_poll(const hgd_p2p* p2p);
+/* Pricing hook: k_reduce (rank 0's block over nranks sources) and k_gather (the other blocks) of
+ * a `count`-float exchange with every peer slot a separate LOCAL allocation (uncached unless
+ * `cached`), mean ms per launch over `iters` launches; synchronises `stream`. Prices the
+ * kernels, not xGMI (profiles/r04_scale). */
+hgd_status hgd_p2p_price_local(int32_t nranks, int64_t count, int32_t cached, int32_t iters,
+                               float* ms_reduce, float* ms_gather, void* stream);
 /* The block arithmetic of hgd_p2p_allreduce (host only, no device calls): rank q reduces floats
  * [*lo, *hi) of a `count`-float exchange over `nranks` ranks; gather step i of `rank` copies
  * float4 *j from rank *owner's reduced block (its own block is skipped). */

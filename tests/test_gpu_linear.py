@@ -112,3 +112,34 @@ def test_linear_kernel_forms(dev, tiles, splitk):
     finally:
         lib.hgd_set_tuning(9, 0)
         lib.hgd_set_tuning(8, 2)
+
+
+@pytest.mark.parametrize("d", [64, 128])
+@pytest.mark.parametrize("relu", [False, True])
+def test_x3p_queue_form_equals_barrier_form(dev, d, relu):
+    """k_splitk_x3p's queue form (HGD_TUNE_X3P_QUEUE = 1: three LDS buffers, full / empty
+    counters instead of a workgroup barrier per stage) runs the same MFMAs in the same order as
+    the barrier form: bitwise the same dW / db, ragged slices included, and within the float64
+    bound."""
+    from hypergraph_diffusion_for_recommendation_amd import _native as nat
+    from hypergraph_diffusion_for_recommendation_amd.functional import linear
+    lib = nat.load()
+    g = torch.Generator(device=dev).manual_seed(d + relu)
+    for rows in (144_242, 4_099, 20_011):
+        X = torch.randn(rows, d, device=dev, generator=g)
+        W = (torch.randn(d, d, device=dev, generator=g) / d ** 0.5).requires_grad_(True)
+        b = torch.randn(d, device=dev, generator=g).requires_grad_(True)
+        dY = torch.randn(rows, d, device=dev, generator=g)
+        outs = []
+        try:
+            for q in (0, 1):
+                assert lib.hgd_set_tuning(13, q) == 0
+                outs.append(torch.autograd.grad(linear(X, W, b, relu=relu), (W, b), dY))
+        finally:
+            lib.hgd_set_tuning(13, 0)
+        (gW0, gb0), (gW1, gb1) = outs
+        assert torch.equal(gW0, gW1) and torch.equal(gb0, gb1), rows
+        if not relu:
+            ref = dY.double().T @ X.double()
+            mag = dY.double().abs().T @ X.double().abs()
+            assert ((gW1.double() - ref).abs() <= 1e-5 * mag).all()
