@@ -72,10 +72,12 @@ def parse():
     ap.add_argument("--slice-width", type=int, default=None,
                     help="embedding columns per pipelined all-reduce block (N > 1; default 32 "
                          "for d <= 128, else 64)")
-    ap.add_argument("--transport", default="rccl", choices=["rccl", "p2p"],
+    ap.add_argument("--transport", default="auto", choices=["auto", "rccl", "p2p"],
                     help="N > 1: the item-message all-reduce over RCCL (torch.distributed "
                          "'nccl') or the direct xGMI peer exchange (hgd_p2p: two-shot mesh "
-                         "reduce over IPC-mapped buffers, sharded.P2PExchange)")
+                         "reduce over IPC-mapped buffers, sharded.P2PExchange); auto (default) "
+                         "times both after the warm-up and runs the timed steps on the faster "
+                         "(RCCL if the peer exchange fails or disagrees with it)")
     ap.add_argument("--check", action="store_true",
                     help="after timing, compare the sharded Y / dX with the single-GPU conv of "
                          "the global graph (strong scaling) at the 1e-5 relative bound")
@@ -233,6 +235,70 @@ def copy_peak_gbps(device, n_bytes=1 << 30, reps=10):
     return max(rates.values()), rates
 
 
+def choose_transport(sh, eager_step, device, phase, n=3):
+    """--transport auto: after the warm-up, n steps over RCCL and n over the peer exchange (its
+    first step compared with RCCL's result), max over ranks; the timed steps then run on the
+    faster. Any failure of the peer exchange on any rank — setup, a bounded wait, a timed-out
+    exchange, a result off by more than 1e-5 of max |Y| — keeps RCCL on every rank."""
+    import torch
+    import torch.distributed as dist
+
+    def timed():
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            eager_step()
+        if sh.transport == "p2p":
+            sh._p2p.wait()
+        torch.cuda.synchronize()
+        dist.barrier()
+        t = torch.tensor([(time.perf_counter() - t0) / n * 1e3], dtype=torch.float64,
+                         device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    out = {"steps_each": n}
+    sh.transport = "rccl"
+    Y_r, dX_r = eager_step()
+    Y_r, dX_r = Y_r.detach(), dX_r.detach()
+    out["rccl_ms_per_step"] = round(timed(), 4)
+    def agree(err):  # every rank learns whether any rank failed
+        flag = torch.tensor([0 if err is None else 1], dtype=torch.int32, device=device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        if err is not None:
+            out["p2p_error"] = err
+        return int(flag.item()) == 0
+
+    err = None
+    try:  # one step, checked against RCCL's, before any collective timing
+        sh.transport = "p2p"
+        Y_p, dX_p = eager_step()
+        sh._p2p.wait()
+        sh._p2p.check()
+        rel = max(float((Y_p.detach() - Y_r).abs().max() / Y_r.abs().max().clamp_min(1e-30)),
+                  float((dX_p - dX_r).abs().max() / dX_r.abs().max().clamp_min(1e-30)))
+        out["p2p_vs_rccl_max_rel_diff"] = rel
+        if not rel <= 1e-5:
+            raise RuntimeError(f"peer exchange differs from RCCL by {rel:.3e} of max |Y|")
+    except Exception as e:  # noqa: BLE001 — any failure keeps RCCL, reported in the line
+        err = repr(e)[:400]
+    ok = agree(err)
+    if ok:
+        try:
+            out["p2p_ms_per_step"] = round(timed(), 4)
+            sh._p2p.check()
+        except Exception as e:  # noqa: BLE001
+            err = repr(e)[:400]
+        ok = agree(err)
+    use_p2p = ok and out.get("p2p_ms_per_step", float("inf")) < out["rccl_ms_per_step"]
+    sh.transport = "p2p" if use_p2p else "rccl"
+    out["chosen"] = sh.transport
+    if not ok:
+        out["p2p_failed_on_some_rank"] = True
+    return out
+
+
 def launch_ranks(args) -> int:
     """Starts ``--gpus`` ranks of this script under torch.distributed.run as a CHILD process (no
     exec: this process has not touched the GPU and never will) and returns its exit status."""
@@ -355,7 +421,8 @@ def main():
         faulthandler.dump_traceback_later(float(os.environ.get("HGD_STALL_DUMP_S", "600")),
                                           exit=False)
     shard_kw = dict(n_chunks=args.chunks, P="sym", Q="mean", R="sym",
-                    slice_width=args.slice_width, transport=args.transport,
+                    slice_width=args.slice_width,
+                    transport="rccl" if args.transport == "auto" else args.transport,
                     trace=phase if world > 1 else None)
     bound = (6.0 / (U + d)) ** 0.5  # xavier_uniform_ on the global [U, d] (HCCF.py:164-169)
     keep_global = args.check and strong and world > 1
@@ -431,6 +498,10 @@ def main():
     phase("warm")
     if world > 1:
         dist.barrier()
+    probe = None
+    if world > 1 and args.transport == "auto":
+        probe = choose_transport(sh, eager_step, device, phase)
+        phase(f"transport: {probe}")
     # roofline: HIP events around every hop launch on its stream, recorded inside the timed
     # region (two event records per hop, a few µs on a ~16 ms step); a captured graph cannot
     # record them, so with --graph on the same steps are re-run eagerly afterwards for them
@@ -569,7 +640,7 @@ def main():
 
     if world == 1:
         parallelism = "single GPU"
-    elif args.transport == "p2p":
+    elif sh.transport == "p2p":
         parallelism = (f"user-row shards x{world} ({'one global graph' if strong else 'a graph per rank'}), "
                        f"direct xGMI peer all-reduce (hgd_p2p two-shot mesh reduce, "
                        f"{dist_backend} for setup) of item messages in {len(sh.slices(d))} "
@@ -608,7 +679,9 @@ def main():
     if world > 1:
         out["ranks"] = per_rank
         out["exchange_bytes_per_step"] = 2 * sh.exchange_bytes(d)
-        out["transport"] = args.transport
+        out["transport"] = sh.transport
+        if probe is not None:
+            out["transport_probe"] = probe
         # the time the compute stream waited for the all-reduces (HIP events around every hop-2
         # wait), max over ranks: 0 = the exchange was hidden behind the hops
         out["exposed_exchange_ms_per_step"] = max(r["exposed_exchange_ms_per_step"]

@@ -126,25 +126,53 @@ class P2PExchange:
         self.n_slots = int(n_slots)
         self.timeout_s = float(timeout_s)
         trace = trace or (lambda msg: None)
-        h = ctypes.c_void_p()
-        nat.check(self.lib.hgd_p2p_create(self.world, self.rank, self.max_count, self.n_slots,
-                                          ctypes.byref(h)), "hgd_p2p_create")
-        self.h = h
-        trace("p2p: created")
-        nat.check(self.lib.hgd_p2p_set_timeout(h, self.timeout_s), "hgd_p2p_set_timeout")
-        mine = ctypes.create_string_buffer(nat.P2P_HANDLE_BYTES)
-        nat.check(self.lib.hgd_p2p_export(h, mine), "hgd_p2p_export")
-        trace("p2p: exported")
-        handles = [None] * self.world
-        if self.world > 1:
-            dist.all_gather_object(handles, mine.raw, group=group)
-        else:
-            handles = [mine.raw]
-        trace("p2p: handles gathered")
-        blob = ctypes.create_string_buffer(b"".join(handles), nat.P2P_HANDLE_BYTES * self.world)
-        nat.check(self.lib.hgd_p2p_open(h, blob), "hgd_p2p_open")
-        trace("p2p: peers opened")
+        self.h = None
         self._views = {}
+        # every step that can fail locally is followed by an agreement among the ranks, so a
+        # failure on one rank raises on all of them (none is left waiting in a collective)
+        h = ctypes.c_void_p()
+        mine = ctypes.create_string_buffer(nat.P2P_HANDLE_BYTES)
+        err = self._try(lambda: self.lib.hgd_p2p_create(self.world, self.rank, self.max_count,
+                                                        self.n_slots, ctypes.byref(h)),
+                        "hgd_p2p_create")
+        if err is None:
+            self.h = h
+            err = self._try(lambda: self.lib.hgd_p2p_set_timeout(h, self.timeout_s),
+                            "hgd_p2p_set_timeout") or self._try(
+                lambda: self.lib.hgd_p2p_export(h, mine), "hgd_p2p_export")
+        trace("p2p: created and exported" if err is None else f"p2p: {err}")
+        entries = [None] * self.world
+        if self.world > 1:
+            dist.all_gather_object(entries, (mine.raw if err is None else None, err),
+                                   group=group)
+        else:
+            entries = [(mine.raw, err)]
+        self._agree([e[1] for e in entries])
+        trace("p2p: handles gathered")
+        blob = ctypes.create_string_buffer(b"".join(e[0] for e in entries),
+                                           nat.P2P_HANDLE_BYTES * self.world)
+        err = self._try(lambda: self.lib.hgd_p2p_open(h, blob), "hgd_p2p_open")
+        errs = [err]
+        if self.world > 1:
+            errs = [None] * self.world
+            dist.all_gather_object(errs, err, group=group)
+        self._agree(errs)
+        trace("p2p: peers opened")
+
+    def _try(self, call, what):
+        st = call()
+        if st == nat.HGD_OK:
+            return None
+        return f"{what}: {self.lib.hgd_get_last_error_string().decode(errors='replace')}"
+
+    def _agree(self, errs):
+        bad = [(q, e) for q, e in enumerate(errs) if e is not None]
+        if bad:
+            if self.h is not None:
+                self.lib.hgd_p2p_destroy(self.h)
+                self.h = None
+            raise nat.HGDNativeError("P2PExchange: " + "; ".join(f"rank {q}: {e}"
+                                                                  for q, e in bad))
 
     def slot(self, k: int, rows: int, cols: int) -> torch.Tensor:
         """Send slot ``k`` as a [rows, cols] float32 view (the hop kernels write into it)."""
