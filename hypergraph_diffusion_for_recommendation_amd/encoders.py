@@ -41,6 +41,14 @@ def sparse_tensor_of(mat, device) -> torch.Tensor:
     return t
 
 
+def _begin_step(dropper) -> None:
+    """A step boundary for SpAdjDropEdge's per-call mask slots (a wrapped or foreign dropper
+    without them is left alone)."""
+    begin = getattr(dropper, "begin_step", None)
+    if begin is not None:
+        begin()
+
+
 class HCCFEncoder(nn.Module):
     """HCCF propagation: per layer a GCN hop on the (edge-dropped) normalised bipartite graph plus
     the dense learned-hypergraph hop for users and items; outputs the layer sum and the per-layer
@@ -86,6 +94,7 @@ class HCCFEncoder(nn.Module):
 
     def forward(self, keep_rate=0.5):
         nu = self.data.n_users
+        _begin_step(self.edgeDropper)
         # E·W [n, d]·[d, K] on the skinny MFMA Linear (functional.linear takes W as [out, in])
         hyper_uu = linear(self.embedding_dict['user_emb'], self.embedding_dict['user_w'].t())
         hyper_ii = linear(self.embedding_dict['item_emb'], self.embedding_dict['item_w'].t())
@@ -207,6 +216,7 @@ class HCCFDiffusionEncoder(HCCFEncoder):
 
     def forward(self, keep_rate=0.5):
         nu = self.data.n_users
+        _begin_step(self.edgeDropper)
         e = self.embedding_dict
         hidden = [torch.cat([e['user_emb'], e['item_emb']], 0)]
         gcn_hidden, hgnn_hidden = [], []

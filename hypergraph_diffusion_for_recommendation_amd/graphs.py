@@ -30,7 +30,11 @@ class CapturedStep:
     logging keeps the parameters' AccumulateGrad nodes, bound to the eager stream, alive into
     the capture, where they break it: keep ``loss.detach()``)."""
 
-    def __init__(self, step: Callable, example_inputs: Sequence[torch.Tensor]):
+    def __init__(self, step: Callable, example_inputs: Sequence[torch.Tensor],
+                 before_replay: Callable = None):
+        # before_replay: host work each replay needs first, e.g. SpAdjDropEdge.refill (the
+        # reference's CPU keep-masks of the step, drawn into the buffers the graph reads)
+        self.before_replay = before_replay
         self.static = [t.detach().clone() for t in example_inputs]
         # free eager autograd graphs still held by reference cycles: their AccumulateGrad nodes
         # would otherwise carry the eager stream into the capture
@@ -50,6 +54,8 @@ class CapturedStep:
     def __call__(self, *inputs: torch.Tensor):
         for dst, src in zip(self.static, inputs):
             dst.copy_(src)
+        if self.before_replay is not None:
+            self.before_replay()
         self.graph.replay()
         return self.out
 

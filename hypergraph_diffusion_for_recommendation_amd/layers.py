@@ -189,13 +189,37 @@ class SpAdjDropEdge(nn.Module):
     def __init__(self, device_rng: bool = False, capture_safe: bool = False):
         super().__init__()
         self.device_rng = device_rng
-        # capture_safe: device mask from a device-side seed counter, returned as a masked VIEW of
-        # the parent (Incidence.masked: the hops skip the dropped edges, no compaction) — no
-        # host read, no host RNG, so the step can be replayed from a HIP graph (fresh masks
-        # every replay). The return value is then an Incidence (what GCNLayer / HGCNConv
-        # consume), not a torch sparse COO.
+        # capture_safe: the result is a masked VIEW of the parent (Incidence.masked: the hops
+        # skip the dropped edges, no compaction) and nothing is read back to the host, so the
+        # step can be replayed from a HIP graph. The return value is then an Incidence (what
+        # GCNLayer / HGCNConv consume), not a torch sparse COO. The mask comes either from a
+        # device-side seed counter (device_rng: fresh masks every replay, a different stream)
+        # or — the reference's own CPU torch.rand stream — from a static device buffer per call
+        # of the step ("slot"), filled from the host: drawn inline on eager steps, and by
+        # refill() before each replay once host_fed(True) is set.
         self.capture_safe = capture_safe
         self._seed = None
+        self._slots = []       # [(nnz, keep, device uint8 buffer)] per call of a step
+        self._slot_i = 0
+        self._prefilled = False
+
+    def begin_step(self):
+        """A step boundary: the next drop uses the first slot (encoders call it per forward)."""
+        self._slot_i = 0
+
+    def host_fed(self, on: bool = True):
+        """capture_safe masks on the reference's CPU stream drawn ahead by :meth:`refill` (for a
+        captured step, whose replays do not run Python) instead of inside the step."""
+        self._prefilled = bool(on)
+
+    def refill(self):
+        """Draws the next step's masks from the CPU generator — the same draws, in the same
+        order, as the step's drop calls would make — into the slots' device buffers (copies
+        ordered on the current stream before the step that reads them)."""
+        for n, keep, buf in self._slots:
+            mask, _ = torch_cpu_keep_mask(n, keep)
+            buf.copy_(mask, non_blocking=True)
+        self._slot_i = 0
 
     def forward(self, adj, keepRate):
         if keepRate == 1.0:
@@ -237,6 +261,22 @@ class SpAdjDropEdge(nn.Module):
         if not (parent.coo_sorted and parent.perm_t is not None):
             raise RuntimeError("SpAdjDropEdge(capture_safe): needs a row-sorted base adjacency")
         dev = parent.device
+        if not self.device_rng:  # the reference's CPU stream through this call's slot
+            i = self._slot_i
+            self._slot_i += 1
+            if i == len(self._slots):
+                if self._prefilled:
+                    raise RuntimeError("SpAdjDropEdge: more drop calls in this step than the "
+                                       "refilled slots (call begin_step per step)")
+                self._slots.append((parent.nnz, keep,
+                                    torch.empty(parent.nnz, dtype=torch.uint8, device=dev)))
+            n, k, buf = self._slots[i]
+            if n != parent.nnz or k != keep:
+                raise RuntimeError("SpAdjDropEdge: a step's drop calls changed size or rate")
+            if not self._prefilled:
+                mask, _ = torch_cpu_keep_mask(n, keep)
+                buf.copy_(mask, non_blocking=True)
+            return parent.masked(buf, keep)
         if self._seed is None or self._seed.device != dev:
             # drawn once from the CPU generator (torch.manual_seed fixes the stream); advanced
             # on the device afterwards

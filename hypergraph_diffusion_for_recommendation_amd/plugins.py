@@ -97,7 +97,10 @@ class HCCF(GraphRecommender):
         self.graph_mode = bool(kwargs.get('hgd_graph', False))
         self._captured = None
         if self.graph_mode:
-            self.model.edgeDropper.device_rng = True
+            # the drop-edge masks stay the reference's CPU torch.rand stream (drawn on the host
+            # before each replay into the buffers the graph reads) unless hgd_device_rng asks
+            # for device draws
+            self.model.edgeDropper.device_rng = bool(kwargs.get('hgd_device_rng', False))
             self.model.edgeDropper.capture_safe = True
             lr = torch.tensor(self.lRate, dtype=torch.float32, device=self.device)
             # fused: one multi-tensor kernel per step instead of the ~15 foreach passes
@@ -177,11 +180,20 @@ class HCCF(GraphRecommender):
             return self.train_step(user_idx, pos_idx, neg_idx)
         full = user_idx.numel() == self.batchSize
         cap = self._captured
+        if cap is not None and not full:  # a short last batch runs eagerly: masks drawn inline
+            self.model.edgeDropper.host_fed(False)
+            out = self.train_step(user_idx, pos_idx, neg_idx).detach()
+            self.model.edgeDropper.host_fed(not self.model.edgeDropper.device_rng)
+            return out
         if cap is not None and full:
             return cap(user_idx, pos_idx, neg_idx).detach().clone()
         if cap is None and full and getattr(self, "_eager_steps", 0) >= 1:
             from .graphs import CapturedStep
-            self._captured = CapturedStep(self.train_step, (user_idx, pos_idx, neg_idx))
+            dropper = self.model.edgeDropper
+            host_fed = not dropper.device_rng
+            dropper.host_fed(host_fed)  # the capture records the slots; refill() fills them
+            self._captured = CapturedStep(self.train_step, (user_idx, pos_idx, neg_idx),
+                                          before_replay=dropper.refill if host_fed else None)
             return self._captured(user_idx, pos_idx, neg_idx).detach().clone()
         self._eager_steps = getattr(self, "_eager_steps", 0) + 1
         # detached: a caller holding the loss would keep the eager autograd graph — and with it

@@ -10,6 +10,8 @@ reference calls it) and Adam. Variants:
 * hgd_device_mask  — the same with SpAdjDropEdge(device_rng=True);
 * hgd_graph        — the device-mask step replayed from one HIP graph (graphs.CapturedStep:
                      capture-safe drop-edge, device-side InfoNCE node counts, capturable Adam);
+* hgd_graph_cpu_mask — the same replay with the masks of the reference's CPU torch.rand stream,
+                     drawn on the host before each replay (SpAdjDropEdge.refill);
 * reference_ops    — scripts/refops.HCCFEncoderRef + the reference's losses (torch.sparse.mm,
                      torch.mm, F.normalize …) on the same GPU, same parameters.
 
@@ -62,7 +64,7 @@ def main():
                 torch.randint(0, ni, (args.batch,), device=dev, generator=g),
                 torch.randint(0, ni, (args.batch,), device=dev, generator=g)) for _ in range(8)]
 
-    def make_step(model, loss_fn, unique, hoist=True, graph=False, counted=None):
+    def make_step(model, loss_fn, unique, hoist=True, graph=False, counted=None, host_fed=None):
         counted = graph if counted is None else counted
         if counted:
             lr = torch.tensor(conf["lrate"], dtype=torch.float32, device=dev)
@@ -105,7 +107,11 @@ def main():
             if state["cap"] is None:
                 if state["k"] == 1:
                     return body(uid, pid, nid)  # one eager step: optimizer state, handles
-                state["cap"] = CapturedStep(body, (uid, pid, nid))
+                if host_fed is not None:  # the reference's CPU mask stream, drawn per replay
+                    host_fed.host_fed(True)
+                state["cap"] = CapturedStep(body, (uid, pid, nid),
+                                            before_replay=None if host_fed is None
+                                            else host_fed.refill)
             return state["cap"](uid, pid, nid)
         return step
 
@@ -143,6 +149,15 @@ def main():
         g_model.edgeDropper.capture_safe = True
         out.append(("hgd_graph", timed(make_step(g_model, contrast_loss, unique_long_n,
                                                  graph=True))))
+    if "hgd_graph_cpu_mask" in want:  # graph replay, masks from the reference's CPU stream
+        torch.manual_seed(0)
+        c_model = HCCFEncoder(conf, data, dev)
+        c_model.load_state_dict(ours.state_dict())
+        c_model.edgeDropper.device_rng = False
+        c_model.edgeDropper.capture_safe = True
+        out.append(("hgd_graph_cpu_mask", timed(make_step(c_model, contrast_loss, unique_long_n,
+                                                          graph=True,
+                                                          host_fed=c_model.edgeDropper))))
     if "hgd_capture_safe_eager" in want:  # the graph variant's ops, launched eagerly
         torch.manual_seed(0)
         e_model = HCCFEncoder(conf, data, dev)
