@@ -1,0 +1,81 @@
+"""sharded.P2PExchange's setup is collective: a failure on ONE rank — creating or exporting its
+buffers, or opening a peer's — must raise on EVERY rank, so none is left waiting in a
+collective (the round-3 stall left four ranks blocked with no error). Two gloo ranks on the CPU
+with a stand-in for libhgd's hgd_p2p_* calls that fails where the test says."""
+import os
+import socket
+
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class _FakeLib:
+    """hgd_p2p_* with the ABI's return codes; fails at `fail_at` on rank `fail_rank`."""
+
+    def __init__(self, rank, fail_rank, fail_at):
+        self.rank, self.fail_rank, self.fail_at = rank, fail_rank, fail_at
+        self.destroyed = 0
+
+    def _st(self, what):
+        return 2 if (self.rank == self.fail_rank and what == self.fail_at) else 0
+
+    def hgd_p2p_create(self, world, rank, count, slots, out):
+        return self._st("create")
+
+    def hgd_p2p_set_timeout(self, h, t):
+        return 0
+
+    def hgd_p2p_export(self, h, buf):
+        return self._st("export")
+
+    def hgd_p2p_open(self, h, blob):
+        return self._st("open")
+
+    def hgd_p2p_destroy(self, h):
+        self.destroyed += 1
+
+    def hgd_get_last_error_string(self):
+        return f"injected failure on rank {self.rank}".encode()
+
+
+def _worker(rank, world, port, fail_rank, fail_at, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from hypergraph_diffusion_for_recommendation_amd import _native as nat
+        from hypergraph_diffusion_for_recommendation_amd import sharded
+        fake = _FakeLib(rank, fail_rank, fail_at)
+        nat_load = nat.load
+        nat.load = lambda: fake
+        try:
+            sharded.P2PExchange(1024, 2, "cpu")
+            q.put((rank, "no error", fake.destroyed))
+        except nat.HGDNativeError as e:
+            q.put((rank, str(e), fake.destroyed))
+        finally:
+            nat.load = nat_load
+        dist.barrier()  # every rank got here: nobody is stuck in the setup's collectives
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail_rank,fail_at", [(1, "create"), (0, "export"), (0, "open"),
+                                               (1, "open")])
+def test_p2p_setup_failure_raises_on_every_rank(fail_rank, fail_at):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    mp.start_processes(_worker, args=(2, _free_port(), fail_rank, fail_at, q), nprocs=2,
+                       join=True, start_method="spawn")
+    got = sorted(q.get(timeout=30) for _ in range(2))
+    for rank, msg, destroyed in got:
+        assert f"rank {fail_rank}: hgd_p2p_{fail_at}" in msg, (rank, msg)
+        # a rank whose own create succeeded releases its buffers when the setup fails
+        created = not (fail_at == "create" and rank == fail_rank)
+        assert destroyed == (1 if created else 0), (rank, destroyed)
