@@ -309,6 +309,8 @@ _SIGNATURES = {
     "hgd_torch_cpu_jump_selfcheck": (c_i32, [c_i64]),
     "hgd_torch_cpu_keep_mask": (c_i32, [c_void_p, c_i64, c_i64, c_f32, c_void_p,
                                         ctypes.POINTER(c_i64)]),
+    "hgd_torch_cpu_keep_mask_threads": (c_i32, [c_void_p, c_i64, c_i64, c_f32, c_void_p,
+                                                ctypes.POINTER(c_i64), c_i32]),
     "hgd_epilogue_apply":(c_i32, [c_void_p, c_i64, c_i32, c_f32, c_void_p, c_void_p]),
     "hgd_epilogue_backward": (c_i32, [c_void_p, c_void_p, c_i64, c_i32, c_f32, c_void_p,
                                       c_void_p]),

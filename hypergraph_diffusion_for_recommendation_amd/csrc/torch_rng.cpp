@@ -476,11 +476,12 @@ extern "C" int32_t hgd_torch_cpu_jump_selfcheck(int64_t refills) {
   return refills >= 1 && hgd::cpu_rng_jump_selfcheck(refills) ? 1 : 0;
 }
 
-extern "C" hgd_status hgd_torch_cpu_keep_mask(uint8_t* torch_state, int64_t state_bytes,
-                                              int64_t n, float keep, uint8_t* mask,
-                                              int64_t* kept) {
+extern "C" hgd_status hgd_torch_cpu_keep_mask_threads(uint8_t* torch_state, int64_t state_bytes,
+                                                      int64_t n, float keep, uint8_t* mask,
+                                                      int64_t* kept, int32_t threads) {
   using namespace hgd;
   clear_error();
+  HGD_REQUIRE(threads >= 0 && threads <= 64, "hgd_torch_cpu_keep_mask: threads in [0, 64]");
   HGD_REQUIRE(torch_state && state_bytes == static_cast<int64_t>(sizeof(TorchCpuState)),
               "hgd_torch_cpu_keep_mask: state must be the %zu bytes of torch.get_rng_state()",
               sizeof(TorchCpuState));
@@ -498,7 +499,7 @@ extern "C" hgd_status hgd_torch_cpu_keep_mask(uint8_t* torch_state, int64_t stat
   // long draws split over threads from jumped states (bitwise the serial draw); short ones, a
   // serial tuning or a CPU without AVX2 run the one-thread loop
   static const bool avx2 = __builtin_cpu_supports("avx2");
-  const int T = rng_threads();
+  const int T = threads > 0 ? threads : rng_threads();
   int64_t cnt;
   if (T > 1 && avx2 && n >= static_cast<int64_t>(T) * 64 * kN && gf2().ok) {
     std::lock_guard<std::mutex> lk(Pool::get().call_mu);
@@ -512,4 +513,10 @@ extern "C" hgd_status hgd_torch_cpu_keep_mask(uint8_t* torch_state, int64_t stat
   std::memcpy(torch_state, &st, sizeof(st));
   if (kept) *kept = cnt;
   return HGD_OK;
+}
+
+extern "C" hgd_status hgd_torch_cpu_keep_mask(uint8_t* torch_state, int64_t state_bytes,
+                                              int64_t n, float keep, uint8_t* mask,
+                                              int64_t* kept) {
+  return hgd_torch_cpu_keep_mask_threads(torch_state, state_bytes, n, keep, mask, kept, 0);
 }

@@ -23,6 +23,7 @@ device :class:`~.incidence.Incidence` (also accepted directly).
 """
 from __future__ import annotations
 
+import os
 import weakref
 from typing import Optional
 
@@ -107,7 +108,13 @@ def _native_cpu_mask_ok() -> bool:
     return _NATIVE_CPU_MASK
 
 
-def _draw_keep_mask(state: torch.Tensor, n: int, keep: float):
+# Host threads of a draw made ahead beside an eager step: the step's own launches are host-bound
+# and need their core (16 draw threads on the GPU box's 16-CPU share took the HCCF eager step
+# from 3.8 to 5.7 ms, profiles/r04_hccf/). Draws the caller waits for use the library default.
+_EAGER_RNG_THREADS = int(os.environ.get("HGD_EAGER_RNG_THREADS", "8"))
+
+
+def _draw_keep_mask(state: torch.Tensor, n: int, keep: float, threads: int = 0):
     """hgd_torch_cpu_keep_mask on a private copy of the generator state (advanced in place);
     ctypes drops the GIL for the call, so it can run on the prefetch thread."""
     import ctypes
@@ -115,10 +122,31 @@ def _draw_keep_mask(state: torch.Tensor, n: int, keep: float):
     from . import _native as nat
     mask = torch.empty(n, dtype=torch.uint8, pin_memory=torch.cuda.is_available())
     kept = ctypes.c_int64(0)
-    nat.check(nat.load().hgd_torch_cpu_keep_mask(state.data_ptr(), state.numel(), n, float(keep),
-                                                 mask.data_ptr() if n else None,
-                                                 ctypes.byref(kept)), "hgd_torch_cpu_keep_mask")
+    nat.check(nat.load().hgd_torch_cpu_keep_mask_threads(
+        state.data_ptr(), state.numel(), n, float(keep), mask.data_ptr() if n else None,
+        ctypes.byref(kept), int(threads)), "hgd_torch_cpu_keep_mask")
     return mask, int(kept.value), state
+
+
+def _draw_step_masks(state: torch.Tensor, spec, threads: int = 0):
+    """The masks of one step's drop calls ((n, keep) each, in order) from one generator state,
+    advanced in place: [mask], state."""
+    masks = []
+    for n, keep in spec:
+        mask, _, state = _draw_keep_mask(state, n, keep, threads)
+        masks.append(mask)
+    return masks, state
+
+
+_STEP_POOL = None
+
+
+def _step_pool():
+    global _STEP_POOL
+    if _STEP_POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+        _STEP_POOL = ThreadPoolExecutor(max_workers=1, thread_name_prefix="hgd-step-masks")
+    return _STEP_POOL
 
 
 def _native_keep_mask(n: int, keep: float):
@@ -150,7 +178,8 @@ class _KeepMaskPrefetcher:
             mask, kept, end = _draw_keep_mask(st, n, keep)
         torch.set_rng_state(end)
         self._pending = (end.clone(), n, keep,
-                         self._pool.submit(_draw_keep_mask, end.clone(), n, keep))
+                         self._pool.submit(_draw_keep_mask, end.clone(), n, keep,
+                                           _EAGER_RNG_THREADS))
         return mask, kept
 
 
@@ -202,6 +231,7 @@ class SpAdjDropEdge(nn.Module):
         self._slots = []       # [(nnz, keep, device uint8 buffer)] per call of a step
         self._slot_i = 0
         self._prefilled = False
+        self._step_job = None  # (start state, spec, future) of the next step's masks
 
     def begin_step(self):
         """A step boundary: the next drop uses the first slot (encoders call it per forward)."""
@@ -215,9 +245,26 @@ class SpAdjDropEdge(nn.Module):
     def refill(self):
         """Draws the next step's masks from the CPU generator — the same draws, in the same
         order, as the step's drop calls would make — into the slots' device buffers (copies
-        ordered on the current stream before the step that reads them)."""
-        for n, keep, buf in self._slots:
-            mask, _ = torch_cpu_keep_mask(n, keep)
+        ordered on the current stream before the step that reads them). The masks of the step
+        after are then drawn on a worker thread while this one runs (all library threads: a
+        replayed step leaves the host idle), and used only if nothing else moved the generator
+        in between — the stream stays the reference's either way."""
+        spec = tuple((n, keep) for n, keep, _ in self._slots)
+        if not _native_cpu_mask_ok():
+            masks = [torch_cpu_keep_mask(n, keep, prefetch=False)[0] for n, keep in spec]
+        else:
+            st = torch.get_rng_state()
+            job, self._step_job = getattr(self, "_step_job", None), None
+            if job is not None and job[1] == spec and torch.equal(job[0], st):
+                masks, end = job[2].result()
+            else:
+                if job is not None:
+                    job[2].result()  # never leave a draw running behind a discarded one
+                masks, end = _draw_step_masks(st, spec)
+            torch.set_rng_state(end)
+            self._step_job = (end.clone(), spec,
+                              _step_pool().submit(_draw_step_masks, end.clone(), spec))
+        for (n, keep, buf), mask in zip(self._slots, masks):
             buf.copy_(mask, non_blocking=True)
         self._slot_i = 0
 

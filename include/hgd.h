@@ -656,6 +656,11 @@ hgd_status hgd_sample_pairwise(uint32_t* mt_state, const int64_t* order, int64_t
 size_t hgd_torch_cpu_state_bytes(void);
 hgd_status hgd_torch_cpu_keep_mask(uint8_t* torch_state, int64_t state_bytes, int64_t n,
                                    float keep, uint8_t* mask, int64_t* kept);
+/* The same with an explicit host thread count (0 = HGD_TUNE_CPU_RNG_THREADS' default): a draw
+ * that runs beside a host-bound eager step should leave cores to it. */
+hgd_status hgd_torch_cpu_keep_mask_threads(uint8_t* torch_state, int64_t state_bytes, int64_t n,
+                                           float keep, uint8_t* mask, int64_t* kept,
+                                           int32_t threads);
 /* Test hook: 1 if the jump-ahead reproduces `refills` MT19937 refills of a seeded state. */
 int32_t hgd_torch_cpu_jump_selfcheck(int64_t refills);
 
