@@ -155,32 +155,58 @@ def _native_keep_mask(n: int, keep: float):
     return mask, kept
 
 
+# Masks of the same size and rate kept drawn ahead of the caller: the encoders make a step's
+# drop calls back to back (HCCF: one per layer, before the layers run), so one mask ahead left
+# the step's other draws in its critical path.
+_KEEP_MASK_AHEAD = int(os.environ.get("HGD_KEEP_MASK_AHEAD", "3"))
+
+
 class _KeepMaskPrefetcher:
-    """Draws the NEXT mask of the same size and rate on a worker thread, from the generator state
-    the current draw leaves behind, while the caller launches the layer's device work. It is used
-    only if the default generator is still exactly in that state when the next mask is asked for
-    (nothing else drew from it in between) — otherwise it is discarded and the mask drawn there
-    and then — so the stream stays the reference's either way."""
+    """Keeps the next ``_KEEP_MASK_AHEAD`` masks of the same size and rate drawn on a worker
+    thread — a chain, each from the generator state the previous one leaves behind — while the
+    caller launches its device work. A drawn-ahead mask is used only if the default generator is
+    still exactly in the state it was drawn from (nothing else drew in between); otherwise the
+    chain is discarded and the mask drawn there and then — so the stream stays the reference's
+    either way."""
 
     def __init__(self):
         from concurrent.futures import ThreadPoolExecutor
         self._pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="hgd-keep-mask")
-        self._pending = None  # (start state, n, keep, future)
+        self._chain = []     # futures of (start state, mask, kept, end state), in draw order
+        self._key = None     # (n, keep) of the chain
+        self._tail = None    # the state the last queued draw starts from: [tensor], worker-owned
+
+    def _extend(self):
+        tail, (n, keep) = self._tail, self._key
+
+        def draw_next():  # jobs run in submission order on the one worker
+            start = tail[0]
+            mask, kept, end = _draw_keep_mask(start.clone(), n, keep, _EAGER_RNG_THREADS)
+            tail[0] = end
+            return start, mask, kept, end
+        self._chain.append(self._pool.submit(draw_next))
+
+    def _drop_chain(self):
+        for f in self._chain:
+            f.result()  # never leave a draw running behind a discarded one
+        self._chain = []
 
     def get(self, n: int, keep: float):
         st = torch.get_rng_state()
-        p, self._pending = self._pending, None
-        if p is not None and p[1] == n and p[2] == keep and torch.equal(p[0], st):
-            mask, kept, end = p[3].result()
-        else:
-            if p is not None:
-                p[3].result()  # never leave a draw running behind a discarded one
+        got = None
+        if self._chain and self._key == (n, keep):
+            start, mask, kept, end = self._chain.pop(0).result()
+            if torch.equal(start, st):
+                got = (mask, kept, end)
+        if got is None:
+            self._drop_chain()
             mask, kept, end = _draw_keep_mask(st, n, keep)
-        torch.set_rng_state(end)
-        self._pending = (end.clone(), n, keep,
-                         self._pool.submit(_draw_keep_mask, end.clone(), n, keep,
-                                           _EAGER_RNG_THREADS))
-        return mask, kept
+            got = (mask, kept, end)
+            self._key, self._tail = (n, keep), [end.clone()]
+        torch.set_rng_state(got[2])
+        while len(self._chain) < _KEEP_MASK_AHEAD:
+            self._extend()
+        return got[0], got[1]
 
 
 _PREFETCH: Optional[_KeepMaskPrefetcher] = None
