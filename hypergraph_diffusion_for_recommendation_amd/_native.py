@@ -411,7 +411,8 @@ def load() -> ctypes.CDLL:
                          (5, "HGD_SPLITK_ROWS"), (6, "HGD_GEMM_EXACT"),
                          (7, "HGD_X3_COLS"), (8, "HGD_X3_SPLITK"), (9, "HGD_X3S_TILES"),
                          (10, "HGD_P2P_SEGMENT_MB"), (11, "HGD_P2P_CACHED"),
-                         (12, "HGD_CPU_RNG_THREADS"), (13, "HGD_X3P_QUEUE")):
+                         (12, "HGD_CPU_RNG_THREADS"), (13, "HGD_X3P_QUEUE"),
+                         (14, "HGD_P2P_GRID")):
             if os.environ.get(env):
                 st = lib.hgd_set_tuning(key, int(os.environ[env]))
                 if st != HGD_OK:

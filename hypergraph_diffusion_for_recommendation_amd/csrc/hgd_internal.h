@@ -87,6 +87,7 @@ void set_x3p_queue(int queue);
 // HGD_TUNE_P2P_SEGMENT_MB / HGD_TUNE_P2P_CACHED (p2p.hip): layout of later hgd_p2p_create calls.
 void set_p2p_segment_mb(int mb);
 void set_p2p_cached(int cached);
+void set_p2p_grid(int grid);
 // HGD_TUNE_CPU_RNG_THREADS (torch_rng.cpp): threads of the split keep-mask draw (0 = auto).
 void set_cpu_rng_threads(int threads);
 bool cpu_rng_jump_selfcheck(int64_t refills);

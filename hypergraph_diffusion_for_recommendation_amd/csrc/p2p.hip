@@ -56,6 +56,12 @@ constexpr int kSent = 0, kReduced = 1;
 constexpr int kMaxSegments = 62;      // handles per rank record (HGD_P2P_HANDLE_BYTES)
 size_t g_segment_bytes = size_t(1) << 30;  // HGD_TUNE_P2P_SEGMENT_MB
 int g_cached = 0;                          // HGD_TUNE_P2P_CACHED
+// Workgroups of k_reduce / k_gather (HGD_TUNE_P2P_GRID). They run beside the hop kernels on a
+// high-priority stream; over xGMI the links, not the CUs, bound them (a phase moves one 16 MB
+// block per link at N = 8), and 256 workgroups keep 256 × 256 threads × 2 float4 × N loads in
+// flight — far more than the links' bandwidth-latency product — while leaving the CUs to the
+// hops the exchange overlaps.
+unsigned g_grid = 256;
 
 struct Packed {  // one rank's record in the handle exchange (HGD_P2P_HANDLE_BYTES)
   int32_t magic, rank, nranks, n_slots;
@@ -135,6 +141,10 @@ __device__ __forceinline__ float4 nan4() {
 }
 
 // out[block r] = reduced_r[block r] = Σ_q send_q[block r], q ascending
+__device__ __forceinline__ float4 add4(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
 __global__ void k_reduce(SlotPtrs send, float4* red, Blocks bl, int rank, int nranks,
                          float4* __restrict__ out, const int* err) {
   const int64_t hi = bl.hi(rank);
@@ -147,15 +157,31 @@ __global__ void k_reduce(SlotPtrs send, float4* red, Blocks bl, int rank, int nr
   // the "sent" flags were acquired by the wait kernel before this one: drop any copy of a
   // peer's slot a cache may still hold from an earlier exchange of the same slot
   acquire_system();
-  for (int64_t i = first; i < hi; i += stride) {
+  // two float4 per thread per step, all 2·N loads in flight before the first add
+  int64_t i = first;
+  for (; i + stride < hi; i += 2 * stride) {
+    float4 v[kMaxRanks], w[kMaxRanks];
+#pragma unroll
+    for (int q = 0; q < kMaxRanks; ++q)
+      if (q < nranks) { v[q] = send.p[q][i]; w[q] = send.p[q][i + stride]; }
+    float4 a = v[0], b = w[0];
+#pragma unroll
+    for (int q = 1; q < kMaxRanks; ++q)
+      if (q < nranks) { a = add4(a, v[q]); b = add4(b, w[q]); }
+    red[i] = a;
+    out[i] = a;
+    red[i + stride] = b;
+    out[i + stride] = b;
+  }
+  if (i < hi) {
     float4 v[kMaxRanks];
 #pragma unroll
-    for (int q = 0; q < kMaxRanks; ++q)  // all loads in flight before the first add
+    for (int q = 0; q < kMaxRanks; ++q)
       if (q < nranks) v[q] = send.p[q][i];
     float4 a = v[0];
 #pragma unroll
     for (int q = 1; q < kMaxRanks; ++q)
-      if (q < nranks) { a.x += v[q].x; a.y += v[q].y; a.z += v[q].z; a.w += v[q].w; }
+      if (q < nranks) a = add4(a, v[q]);
     red[i] = a;
     out[i] = a;
   }
@@ -176,9 +202,21 @@ __global__ void k_gather(SlotPtrs red, Blocks bl, int rank, float4* __restrict__
     return;
   }
   acquire_system();  // the "reduced" flags were acquired by the wait kernel before this one
-  for (int64_t i = first; i < n; i += stride) {
-    const int64_t j = bl.gather_j(rank, i);
-    out[j] = red.p[bl.gather_owner(j)][j];
+  int64_t i = first;
+  for (; i + 3 * stride < n; i += 4 * stride) {  // four loads in flight per thread
+    float4 v[4];
+    int64_t j[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      j[u] = bl.gather_j(rank, i + u * stride);
+      v[u] = red.p[bl.gather_owner(j[u])][j[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) out[j[u]] = v[u];
+  }
+  for (; i < n; i += stride) {
+    const int64_t jj = bl.gather_j(rank, i);
+    out[jj] = red.p[bl.gather_owner(jj)][jj];
   }
 }
 
@@ -234,6 +272,7 @@ struct hgd_p2p {
 namespace hgd {
 void set_p2p_segment_mb(int mb) { g_segment_bytes = (mb > 0 ? size_t(mb) : 1024) << 20; }
 void set_p2p_cached(int cached) { g_cached = cached; }
+void set_p2p_grid(int grid) { g_grid = grid > 0 ? static_cast<unsigned>(grid) : 256u; }
 }  // namespace hgd
 
 using hgd::fail;
@@ -419,7 +458,7 @@ extern "C" hgd_status hgd_p2p_allreduce(hgd_p2p* h, int32_t slot, int64_t count,
   hipLaunchKernelGGL(k_signal_wait, dim3(1), dim3(64), 0, st, h->d_flags, kSent, h->rank,
                      h->nranks, seq, tmo, h->err, h->host_err_dev);
   if (hgd_status r = hgd::check_launch("hgd_p2p_allreduce (signal)"); r != HGD_OK) return r;
-  const unsigned g1 = std::min<unsigned>(1024, hgd::grid_for(std::max<int64_t>(bl.b4, 1)));
+  const unsigned g1 = std::min<unsigned>(g_grid, hgd::grid_for(std::max<int64_t>(bl.b4, 1)));
   hipLaunchKernelGGL(k_reduce, dim3(g1), dim3(hgd::kBlock), 0, st, send,
                      reinterpret_cast<float4*>(h->slot(h->rank, h->n_slots + slot)), bl, h->rank,
                      h->nranks, o, h->err);
@@ -430,7 +469,7 @@ extern "C" hgd_status hgd_p2p_allreduce(hgd_p2p* h, int32_t slot, int64_t count,
     if (hgd_status r = hgd::check_launch("hgd_p2p_allreduce (signal)"); r != HGD_OK) return r;
     const int64_t rest = bl.gather_count(h->rank);
     if (rest > 0) {
-      const unsigned g2 = std::min<unsigned>(2048, hgd::grid_for(rest));
+      const unsigned g2 = std::min<unsigned>(g_grid, hgd::grid_for(rest));
       hipLaunchKernelGGL(k_gather, dim3(g2), dim3(hgd::kBlock), 0, st, red, bl, h->rank, o,
                          h->err);
       if (hgd_status r = hgd::check_launch("hgd_p2p_allreduce (gather)"); r != HGD_OK) return r;
@@ -509,9 +548,9 @@ extern "C" hgd_status hgd_p2p_price_local(int32_t nranks, int64_t count, int32_t
   }
   const Blocks bl = Blocks::of(count, nranks);
   float4* o = static_cast<float4*>(out);
-  const unsigned g1 = std::min<unsigned>(1024, hgd::grid_for(std::max<int64_t>(bl.b4, 1)));
+  const unsigned g1 = std::min<unsigned>(g_grid, hgd::grid_for(std::max<int64_t>(bl.b4, 1)));
   const int64_t rest = bl.gather_count(0);
-  const unsigned g2 = std::min<unsigned>(2048, hgd::grid_for(std::max<int64_t>(rest, 1)));
+  const unsigned g2 = std::min<unsigned>(g_grid, hgd::grid_for(std::max<int64_t>(rest, 1)));
   auto reduce = [&] {
     hipLaunchKernelGGL(k_reduce, dim3(g1), dim3(hgd::kBlock), 0, st, sp,
                        const_cast<float4*>(rp.p[0]), bl, 0, nranks, o, err);

@@ -782,6 +782,10 @@ extern "C" hgd_status hgd_set_tuning(int32_t key, int32_t value) {
       HGD_REQUIRE(value == 0 || value == 1, "hgd_set_tuning: x3p queue must be 0 or 1");
       set_x3p_queue(value);
       return HGD_OK;
+    case HGD_TUNE_P2P_GRID:
+      HGD_REQUIRE(value >= 0 && value <= 65536, "hgd_set_tuning: p2p grid must be 0..65536");
+      set_p2p_grid(value);
+      return HGD_OK;
     case HGD_TUNE_CPU_RNG_THREADS:
       HGD_REQUIRE(value >= 0 && value <= 64, "hgd_set_tuning: cpu rng threads must be 0..64");
       set_cpu_rng_threads(value);

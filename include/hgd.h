@@ -97,7 +97,9 @@ typedef enum hgd_epilogue {
  *                         min(16, hardware threads, OMP_NUM_THREADS); 1 = one thread)
  *   HGD_TUNE_X3P_QUEUE:   form of the producer-wave weight gradient: 0 (default) = one workgroup
  *                         barrier per 32-row stage, 1 = three LDS buffers with full / empty
- *                         counters (measured slower: 45.1 vs 41.5 µs at 144,242 x 128) */
+ *                         counters (measured slower: 45.1 vs 41.5 µs at 144,242 x 128)
+ *   HGD_TUNE_P2P_GRID:    workgroups of the peer exchange's reduce / gather kernels (0 = default
+ *                         256: the links bound them, the hops they overlap need the CUs) */
 typedef enum hgd_tune_key {
   HGD_TUNE_SPMM_UNROLL = 1,
   HGD_TUNE_SPMM_POLICY = 2,
@@ -111,7 +113,8 @@ typedef enum hgd_tune_key {
   HGD_TUNE_P2P_SEGMENT_MB = 10,
   HGD_TUNE_P2P_CACHED = 11,
   HGD_TUNE_CPU_RNG_THREADS = 12,
-  HGD_TUNE_X3P_QUEUE = 13
+  HGD_TUNE_X3P_QUEUE = 13,
+  HGD_TUNE_P2P_GRID = 14
 } hgd_tune_key;
 hgd_status hgd_set_tuning(int32_t key, int32_t value);
 
