@@ -593,7 +593,7 @@ def main():
             dist.barrier()
             sh.close()
             dist.destroy_process_group()
-        return
+        return finish(0)
 
     value = total_edges * args.steps / elapsed / 1e6
     achieved = hop["avg_bytes"] / (hop["avg_ms"] * 1e-3) / 1e9 if hop["avg_ms"] > 0 else 0.0
@@ -706,8 +706,21 @@ def main():
         dist.barrier()
         sh.close()
         dist.destroy_process_group()
-    if check is not None and not check["ok"]:
-        sys.exit(1)
+    finish(1 if check is not None and not check["ok"] else 0)
+
+
+def finish(rc: int):
+    """Exit status of a rank. A peer-exchange set-up call that never returned (the auto probe
+    then chose RCCL) is still blocked on a daemon thread, and the HIP runtime's teardown at
+    interpreter exit may wait for it: such a rank ends with os._exit once its output is out."""
+    from hypergraph_diffusion_for_recommendation_amd.sharded import p2p_setup_stuck
+    if p2p_setup_stuck():
+        print(f"bench.py: {p2p_setup_stuck()} peer-exchange set-up call(s) never returned; "
+              f"exiting without runtime teardown", file=sys.stderr, flush=True)
+        sys.stdout.flush()
+        os._exit(rc)
+    if rc:
+        sys.exit(rc)
 
 
 if __name__ == "__main__":

@@ -26,6 +26,8 @@ The reference has no distributed code at all; this is new desi
 from __future__ import annotations
 
 import ctypes
+import os
+import threading
 import time
 from typing import List, Optional, Tuple
 
@@ -108,6 +110,19 @@ def _scale_of_degrees(deg: torch.Tensor, kind: str) -> torch.Tensor:
     return torch.where(deg > 0, 1.0 / inv, torch.zeros_like(deg)).to(torch.float32)
 
 
+# Deadline of each P2PExchange set-up call (HGD_P2P_SETUP_TIMEOUT_S, seconds), and the number of
+# set-up calls that never returned in this process (p2p_setup_stuck).
+_P2P_SETUP_TIMEOUT_S = float(os.environ.get("HGD_P2P_SETUP_TIMEOUT_S", "180"))
+_P2P_STUCK = 0
+
+
+def p2p_setup_stuck() -> int:
+    """How many P2PExchange set-up calls of this process never returned. They are left running on
+    daemon threads; a process with any should end with ``os._exit`` once its output is flushed,
+    since the runtime's teardown may wait for them."""
+    return _P2P_STUCK
+
+
 class P2PExchange:
     """The direct xGMI peer transport (``hgd_p2p_*``, csrc/p2p.hip): every rank exposes one
     uncached buffer of ``n_slots`` send slots to its peers; an all-reduce of a slot is a two-shot
@@ -116,8 +131,14 @@ class P2PExchange:
     (the IPC handles travel by ``all_gather_object``)."""
 
     def __init__(self, max_count: int, n_slots: int, device: torch.device, group=None,
-                 timeout_s: float = 30.0, trace=None):
+                 timeout_s: float = 30.0, trace=None, setup_timeout_s: Optional[float] = None):
         self.lib = nat.load()
+        # the set-up calls (allocation, export, the peers' IPC opens) run on a helper thread with
+        # a deadline: one that never returns — hipIpcOpenMemHandle of a ≥ 3.5 GiB uncached
+        # allocation did that on ROCm 7.2 — becomes an error on every rank instead of a hang
+        self.setup_timeout_s = float(setup_timeout_s if setup_timeout_s is not None else
+                                     _P2P_SETUP_TIMEOUT_S)
+        self._stuck = False
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -160,17 +181,39 @@ class P2PExchange:
         trace("p2p: peers opened")
 
     def _try(self, call, what):
-        st = call()
-        if st == nat.HGD_OK:
-            return None
-        return f"{what}: {self.lib.hgd_get_last_error_string().decode(errors='replace')}"
+        """Runs one hgd_p2p_* set-up call on a helper thread (bound to this exchange's device)
+        and waits at most ``setup_timeout_s`` for it: None, or the error text. A call that has
+        not returned by then is left running; the exchange is marked stuck and its buffers are
+        never released (the call may still be using them)."""
+        if self._stuck:
+            return f"{what}: skipped after an earlier set-up call did not return"
+        box = {}
+
+        def run():
+            try:
+                if self.device.type == "cuda":
+                    torch.cuda.set_device(self.device)
+                st = call()
+                box["err"] = None if st == nat.HGD_OK else (
+                    f"{what}: {self.lib.hgd_get_last_error_string().decode(errors='replace')}")
+            except Exception as e:  # noqa: BLE001 — reported like a failed call
+                box["err"] = f"{what}: {e!r}"
+        th = threading.Thread(target=run, name=f"hgd-p2p-{what}", daemon=True)
+        th.start()
+        th.join(self.setup_timeout_s)
+        if th.is_alive():
+            global _P2P_STUCK
+            _P2P_STUCK += 1
+            self._stuck = True
+            return f"{what}: did not return within {self.setup_timeout_s:.0f} s"
+        return box["err"]
 
     def _agree(self, errs):
         bad = [(q, e) for q, e in enumerate(errs) if e is not None]
         if bad:
-            if self.h is not None:
+            if self.h is not None and not self._stuck:
                 self.lib.hgd_p2p_destroy(self.h)
-                self.h = None
+            self.h = None
             raise nat.HGDNativeError("P2PExchange: " + "; ".join(f"rank {q}: {e}"
                                                                   for q, e in bad))
 

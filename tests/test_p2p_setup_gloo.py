@@ -4,6 +4,7 @@ collective (the round-3 stall left four ranks blocked with no error). Two gloo r
 with a stand-in for libhgd's hgd_p2p_* calls that fails where the test says."""
 import os
 import socket
+import threading
 
 import pytest
 import torch.distributed as dist
@@ -22,6 +23,7 @@ class _FakeLib:
     def __init__(self, rank, fail_rank, fail_at):
         self.rank, self.fail_rank, self.fail_at = rank, fail_rank, fail_at
         self.destroyed = 0
+        self.release = threading.Event()  # a "hang" call blocks until the test releases it
 
     def _st(self, what):
         return 2 if (self.rank == self.fail_rank and what == self.fail_at) else 0
@@ -36,6 +38,9 @@ class _FakeLib:
         return self._st("export")
 
     def hgd_p2p_open(self, h, blob):
+        if self.rank == self.fail_rank and self.fail_at == "hang":
+            self.release.wait(60)  # an IPC open that does not return (the ROCm 7.2 ≥ 3.5 GiB case)
+            return 0
         return self._st("open")
 
     def hgd_p2p_destroy(self, h):
@@ -55,12 +60,13 @@ def _worker(rank, world, port, fail_rank, fail_at, q):
         nat_load = nat.load
         nat.load = lambda: fake
         try:
-            sharded.P2PExchange(1024, 2, "cpu")
-            q.put((rank, "no error", fake.destroyed))
+            sharded.P2PExchange(1024, 2, "cpu", setup_timeout_s=3.0)
+            q.put((rank, "no error", fake.destroyed, sharded.p2p_setup_stuck()))
         except nat.HGDNativeError as e:
-            q.put((rank, str(e), fake.destroyed))
+            q.put((rank, str(e), fake.destroyed, sharded.p2p_setup_stuck()))
         finally:
             nat.load = nat_load
+            fake.release.set()
         dist.barrier()  # every rank got here: nobody is stuck in the setup's collectives
     finally:
         dist.destroy_process_group()
@@ -74,8 +80,24 @@ def test_p2p_setup_failure_raises_on_every_rank(fail_rank, fail_at):
     mp.start_processes(_worker, args=(2, _free_port(), fail_rank, fail_at, q), nprocs=2,
                        join=True, start_method="spawn")
     got = sorted(q.get(timeout=30) for _ in range(2))
-    for rank, msg, destroyed in got:
+    for rank, msg, destroyed, stuck in got:
         assert f"rank {fail_rank}: hgd_p2p_{fail_at}" in msg, (rank, msg)
         # a rank whose own create succeeded releases its buffers when the setup fails
         created = not (fail_at == "create" and rank == fail_rank)
         assert destroyed == (1 if created else 0), (rank, destroyed)
+        assert stuck == 0
+
+
+def test_p2p_setup_call_that_never_returns_raises_on_every_rank():
+    """A set-up call still running at its deadline fails the set-up on every rank; the stuck
+    rank keeps its buffers (the call may still use them) and counts the call in
+    p2p_setup_stuck(), which bench.py's exit path checks."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    mp.start_processes(_worker, args=(2, _free_port(), 1, "hang", q), nprocs=2,
+                       join=True, start_method="spawn")
+    got = sorted(q.get(timeout=30) for _ in range(2))
+    for rank, msg, destroyed, stuck in got:
+        assert "rank 1: hgd_p2p_open: did not return within 3 s" in msg, (rank, msg)
+        assert destroyed == (0 if rank == 1 else 1), (rank, destroyed)
+        assert stuck == (1 if rank == 1 else 0), (rank, stuck)
