@@ -12,6 +12,10 @@ reference calls it) and Adam. Variants:
                      capture-safe drop-edge, device-side InfoNCE node counts, capturable Adam);
 * hgd_graph_cpu_mask — the same replay with the masks of the reference's CPU torch.rand stream,
                      drawn on the host before each replay (SpAdjDropEdge.refill);
+* hgd_capture_safe_eager — the graph variant's ops (device mask), launched eagerly;
+* hgd_cs_eager_cpu_mask — eager, capture-safe drop-edge views (the reference's CPU mask stream
+                     through the per-call slots), device-side InfoNCE counts, fused BPR, the
+                     reference's unfused Adam: no host read inside the step;
 * reference_ops    — scripts/refops.HCCFEncoderRef + the reference's losses (torch.sparse.mm,
                      torch.mm, F.normalize …) on the same GPU, same parameters.
 
@@ -64,9 +68,11 @@ def main():
                 torch.randint(0, ni, (args.batch,), device=dev, generator=g),
                 torch.randint(0, ni, (args.batch,), device=dev, generator=g)) for _ in range(8)]
 
-    def make_step(model, loss_fn, unique, hoist=True, graph=False, counted=None, host_fed=None):
+    def make_step(model, loss_fn, unique, hoist=True, graph=False, counted=None, host_fed=None,
+                  fused_adam=None):
         counted = graph if counted is None else counted
-        if counted:
+        fused_adam = counted if fused_adam is None else fused_adam
+        if fused_adam:
             lr = torch.tensor(conf["lrate"], dtype=torch.float32, device=dev)
             opt = torch.optim.Adam(model.parameters(), lr=lr, capturable=True, fused=True)
         else:
@@ -166,6 +172,15 @@ def main():
         e_model.edgeDropper.capture_safe = True
         out.append(("hgd_capture_safe_eager", timed(make_step(e_model, contrast_loss,
                                                               unique_long_n, counted=True))))
+    if "hgd_cs_eager_cpu_mask" in want:  # eager, capture-safe ops on the reference's CPU mask
+        torch.manual_seed(0)                # stream, the reference's (unfused) Adam
+        f_model = HCCFEncoder(conf, data, dev)
+        f_model.load_state_dict(ours.state_dict())
+        f_model.edgeDropper.device_rng = False
+        f_model.edgeDropper.capture_safe = True
+        out.append(("hgd_cs_eager_cpu_mask", timed(make_step(f_model, contrast_loss,
+                                                             unique_long_n, counted=True,
+                                                             fused_adam=False))))
     if "reference_ops" in want:
         out.append(("reference_ops", timed(make_step(ref, R.contrast_loss, lambda t, n: torch.unique(t.long()), hoist=False))))
     for name, ms in out:
