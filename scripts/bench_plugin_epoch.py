@@ -121,6 +121,30 @@ def main():
     torch.cuda.synchronize()
     out["ours_epoch_device_rng_s"] = round(time.perf_counter() - t, 3)
     rec.model.edgeDropper.device_rng = False
+    # eager, capture-safe drop-edge views on the reference's CPU mask stream (per-call slots),
+    # device-side InfoNCE node counts: no host read inside a step
+    rec.model.edgeDropper.capture_safe = True
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for u, i, j in next_batch_pairwise(rec.data, rec.batchSize, device=dev):
+        rec.train_step(u, i, j)
+    torch.cuda.synchronize()
+    out["ours_epoch_capture_safe_s"] = round(time.perf_counter() - t, 3)
+    rec.model.edgeDropper.capture_safe = False
+    # hgd_graph: full-size batches replayed from one HIP graph, the reference's CPU mask stream
+    torch.manual_seed(0)
+    rec_g = HCCF(conf, train, test, None, **dict(kw, hgd_graph=True))
+    for k, b in enumerate(next_batch_pairwise(rec_g.data, rec_g.batchSize, device=dev)):
+        rec_g.graph_step(*b)  # eager step, capture, first replays
+        if k == 3:
+            break
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for u, i, j in next_batch_pairwise(rec_g.data, rec_g.batchSize, device=dev):
+        rec_g.graph_step(u, i, j)
+    torch.cuda.synchronize()
+    out["ours_epoch_graph_s"] = round(time.perf_counter() - t, 3)
+    del rec_g
     rec.model.eval()
     with torch.no_grad():
         rec.user_emb, rec.item_emb, _, _ = rec.model(keep_rate=1)
