@@ -26,6 +26,11 @@ def main():
     ap.add_argument("--items", type=int, default=38_048)
     ap.add_argument("--train", type=int, default=1_170_000)
     ap.add_argument("--test", type=int, default=390_000)
+    ap.add_argument("--warm", action="store_true",
+                    help="one train_step on the first batch first, as bench_plugin_epoch.py")
+    ap.add_argument("--nosync", action="store_true",
+                    help="no per-step checks (the bench's timing): report the batch that raises "
+                         "and check the parameters at each epoch's end")
     args = ap.parse_args()
     import torch
 
@@ -65,7 +70,26 @@ def main():
         return names
 
     random.seed(1)
+    if args.warm:
+        b0 = next(iter(next_batch_pairwise(rec.data, rec.batchSize, device=dev)))
+        rec.train_step(*b0)
     for ep, mode in enumerate(args.modes.split(",")):
+        if args.nosync:
+            drop.device_rng = mode == "device"
+            drop.capture_safe = mode.startswith("cs")
+            b = -1
+            try:
+                for b, (u, i, j) in enumerate(next_batch_pairwise(rec.data, rec.batchSize,
+                                                                  device=dev)):
+                    rec.train_step(u, i, j)
+            except Exception as e:  # noqa: BLE001
+                print(f"mode {mode} epoch {ep}: batch {b} raised {e!r:.300}; non-finite now: "
+                      f"{bad_tensors({})}", flush=True)
+                return 1
+            torch.cuda.synchronize()
+            print(f"mode {mode}: epoch done ({b + 1} batches), non-finite: {bad_tensors({})}",
+                  flush=True)
+            continue
         drop.device_rng = mode == "device"
         drop.capture_safe = mode.startswith("cs")
         for b, (u, i, j) in enumerate(next_batch_pairwise(rec.data, rec.batchSize, device=dev)):
