@@ -113,8 +113,10 @@ def main():
                 print(f"mode {mode} epoch {ep} batch {b} size {u.numel()}: before step {pre}, "
                       f"after {post}, error {err}", flush=True)
                 return 1
-            if b % 50 == 0:
-                print(f"mode {mode} batch {b} loss {float(loss):.6f}", flush=True)
+            if b % 25 == 0 or b >= 270:
+                mags = " ".join(f"{k} {float(t.abs().max()):.3g}" for k, t in outs.items())
+                print(f"mode {mode} batch {b} loss {float(loss):.6f} max|.|: {mags}",
+                      flush=True)
         print(f"mode {mode}: epoch finite ({b + 1} batches, last size {u.numel()})", flush=True)
     return 0
 
