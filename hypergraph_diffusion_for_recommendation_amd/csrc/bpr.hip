@@ -120,9 +120,13 @@ __global__ void k_bpr_bwd_link(BprArgs a, int* head, int* next, int* dst) {
 // The list is walked ONCE into the group's LDS slots (up to CAP positions), ranked there (each
 // lane counts the smaller entries of its slots) and added in rank order. Repeats are routine in
 // real batches — a popular item is the positive of tens of batch rows, and at d = 32 a group is
-// 4 lanes — so the ranking must not chase the list per element; only a list longer than CAP
-// (more repeats of one row than CAP, far beyond any real batch) falls back to repeated minimum
-// walks.
+// 4 lanes — so the ranking must not chase the list per element. A list longer than CAP (a
+// skewed catalogue's head item: under Zipf(1.2) popularity one item is the positive of ~740 of
+// 4,096 rows) stops being walked at CAP + 1 — a dependent load per entry — and the group scans
+// the destination array instead, K positions per lane per step (independent loads), taking its
+// row's positions in ascending order from the lanes' hit masks. That scan is ≤ 3B/(K·G) steps
+// for the few such rows; the round-3 fallback (repeated minimum walks over the list, quadratic
+// in dependent loads) took 45 ms per call on that batch.
 template <int G>
 __global__ __launch_bounds__(kBlock) void k_bpr_bwd_rows(BprArgs a, const float* coef,
                                                         const float* grad, const int* head,
@@ -167,11 +171,12 @@ __global__ __launch_bounds__(kBlock) void k_bpr_bwd_rows(BprArgs a, const float*
       }
     }
   };
-  // walk the list once: its length, and entry t in slot t (written by lane t mod G)
+  // walk the list once: its length (up to CAP + 1), and entry t in slot t (written by lane
+  // t mod G)
   int n_pos = 0;
   for (int e = static_cast<int>(q); e >= 0; e = next[e]) {
     if (n_pos < CAP && n_pos % G == l) s_list[grp][n_pos] = e;
-    ++n_pos;
+    if (++n_pos > CAP) break;
   }
   if (n_pos == 1) {
     add(q);
@@ -191,12 +196,28 @@ __global__ __launch_bounds__(kBlock) void k_bpr_bwd_rows(BprArgs a, const float*
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     for (int t = 0; t < n_pos; ++t) add(s_sorted[grp][t]);
   } else {
-    int last = -1;
-    for (int t = 0; t < n_pos; ++t) {
-      int best = 0x7fffffff;
-      for (int e = static_cast<int>(q); e >= 0; e = next[e]) best = (e > last && e < best) ? e : best;
-      add(best);
-      last = best;
+    // ascending scan of dst[]: lane l tests positions base + l·K + [0, K); the group's lanes
+    // with hits are taken in lane order (ballot), each lane's hits in k order (its mask,
+    // broadcast) — i.e. ascending positions, the order of the other paths
+    constexpr int K = 16;
+    const int P = static_cast<int>(3 * a.B);
+    const int g0 = static_cast<int>(threadIdx.x & 63) - l;  // the group's first lane in the wave
+    for (int base = 0; base < P; base += K * G) {
+      unsigned hits = 0;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int e = base + l * K + k;
+        if (e < P && dst[e] == r) hits |= 1u << k;
+      }
+      unsigned long long lanes = __ballot(hits != 0u);
+      if (G < 64) lanes = (lanes >> g0) & ((1ull << G) - 1ull);
+      while (lanes) {
+        const int src = __ffsll(static_cast<unsigned long long>(lanes)) - 1;
+        lanes &= lanes - 1ull;
+        for (unsigned m = static_cast<unsigned>(__shfl(static_cast<int>(hits), g0 + src)); m;
+             m &= m - 1u)
+          add(base + src * K + (__ffs(m) - 1));
+      }
     }
   }
 #pragma unroll

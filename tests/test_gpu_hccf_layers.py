@@ -150,35 +150,72 @@ def test_bpr_loss_rows_matches_torch(dev, d):
     HCCF.py:84-86 in float64: loss within 1e-6 relative, the table gradient row-bound
     (1e-5 · Σ|terms| of each row), the gathered rows bitwise; a small table makes most rows
     repeat within the batch (the summed-duplicates path); two runs are bitwise equal."""
-    from hypergraph_diffusion_for_recommendation_amd.functional import bpr_loss_rows
     g = torch.Generator(device=dev).manual_seed(d)
     for U, I, B in ((300, 500, 4096), (31_668, 38_048, 4096), (5, 3, 64)):
-        E = (0.3 * torch.randn(U + I, d, device=dev, generator=g)).requires_grad_(True)
         uid = torch.randint(0, U, (B,), device=dev, generator=g)
         pid = torch.randint(0, I, (B,), device=dev, generator=g)
         nid = torch.randint(0, I, (B,), device=dev, generator=g)
-        ue, ie = torch.split(E, [U, I])
-        outs = []
-        for _ in range(2):
-            loss, anc, pos = bpr_loss_rows(ue, ie, uid, pid, nid)
-            (gE,) = torch.autograd.grad(2.5 * loss, E)
-            outs.append((loss.detach(), anc, pos, gE))
-        assert all(torch.equal(a, b) for a, b in zip(outs[0], outs[1]))
-        loss, anc, pos, gE = outs[0]
-        assert torch.equal(anc, E.detach()[uid]) and torch.equal(pos, E.detach()[U + pid])
-        E64 = E.detach().double().cpu().requires_grad_(True)
-        u64, i64 = torch.split(E64, [U, I])
-        a, p, n = u64[uid.cpu()], i64[pid.cpu()], i64[nid.cpu()]
-        ps, ns = (a * p).sum(1), (a * n).sum(1)
-        ref = torch.mean(-torch.log(1e-5 + torch.sigmoid(ps - ns)))
-        (gR,) = torch.autograd.grad(2.5 * ref, E64)
-        assert abs(float(loss) - float(ref)) <= 1e-6 * abs(float(ref)), (float(loss), float(ref))
-        # Σ|terms| of each gradient row: the same chain on |·| (|coef| ≤ 1/B · 2.5)
-        a_, p_, n_ = a.detach().abs(), p.detach().abs(), n.detach().abs()
-        mag = torch.zeros_like(E64)
-        w = 2.5 / B
-        mag.index_add_(0, uid.cpu(), w * (p_ + n_))
-        mag.index_add_(0, U + pid.cpu(), w * a_)
-        mag.index_add_(0, U + nid.cpu(), w * a_)
-        err = (gE.double().cpu() - gR).abs()
-        assert bool((err <= 1e-5 * mag + 1e-30).all()), float((err / (mag + 1e-30)).max())
+        _check_bpr_rows(dev, g, d, U, I, uid, pid, nid)
+
+
+@pytest.mark.parametrize("d", [12, 64, 256])
+def test_bpr_loss_rows_skewed_batch(dev, d):
+    """A skewed catalogue's batch (bench_plugin_epoch's Zipf-1.2 items: one item is the positive
+    of ~18 % of the rows, far more repeats than a row's LDS list holds): the same bounds and
+    determinism, and the backward stays a small fraction of a step (the list-scan path; the
+    round-3 fallback took 45 ms per call here)."""
+    import time
+
+    from hypergraph_diffusion_for_recommendation_amd.functional import bpr_loss_rows
+    g = torch.Generator(device=dev).manual_seed(100 + d)
+    U, I, B = 31_668, 38_048, 4096
+    uid = torch.randint(0, U, (B,), device=dev, generator=g)
+    pid = torch.randint(0, I, (B,), device=dev, generator=g)
+    hot = torch.rand(B, device=dev, generator=g) < 0.18
+    pid = torch.where(hot, torch.zeros_like(pid), pid)           # item 0: ~740 positives
+    nid = torch.randint(0, I, (B,), device=dev, generator=g)
+    nid[: B // 8] = 1                                             # item 1: 512 negatives
+    uid[B // 2: B // 2 + 300] = 7                                 # user 7: 300 anchors
+    _check_bpr_rows(dev, g, d, U, I, uid, pid, nid)
+    E = (0.3 * torch.randn(U + I, d, device=dev, generator=g)).requires_grad_(True)
+    ue, ie = torch.split(E, [U, I])
+    ts = []
+    for _ in range(6):
+        loss, _a, _p = bpr_loss_rows(ue, ie, uid, pid, nid)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        torch.autograd.grad(loss, E)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    assert sorted(ts)[3] < 5e-3, ts
+
+
+def _check_bpr_rows(dev, g, d, U, I, uid, pid, nid):
+    from hypergraph_diffusion_for_recommendation_amd.functional import bpr_loss_rows
+    B = uid.numel()
+    E = (0.3 * torch.randn(U + I, d, device=dev, generator=g)).requires_grad_(True)
+    ue, ie = torch.split(E, [U, I])
+    outs = []
+    for _ in range(2):
+        loss, anc, pos = bpr_loss_rows(ue, ie, uid, pid, nid)
+        (gE,) = torch.autograd.grad(2.5 * loss, E)
+        outs.append((loss.detach(), anc, pos, gE))
+    assert all(torch.equal(a, b) for a, b in zip(outs[0], outs[1]))
+    loss, anc, pos, gE = outs[0]
+    assert torch.equal(anc, E.detach()[uid]) and torch.equal(pos, E.detach()[U + pid])
+    E64 = E.detach().double().cpu().requires_grad_(True)
+    u64, i64 = torch.split(E64, [U, I])
+    a, p, n = u64[uid.cpu()], i64[pid.cpu()], i64[nid.cpu()]
+    ps, ns = (a * p).sum(1), (a * n).sum(1)
+    ref = torch.mean(-torch.log(1e-5 + torch.sigmoid(ps - ns)))
+    (gR,) = torch.autograd.grad(2.5 * ref, E64)
+    assert abs(float(loss) - float(ref)) <= 1e-6 * abs(float(ref)), (float(loss), float(ref))
+    # Σ|terms| of each gradient row: the same chain on |·| (|coef| ≤ 1/B · 2.5)
+    a_, p_, n_ = a.detach().abs(), p.detach().abs(), n.detach().abs()
+    mag = torch.zeros_like(E64)
+    w = 2.5 / B
+    mag.index_add_(0, uid.cpu(), w * (p_ + n_))
+    mag.index_add_(0, U + pid.cpu(), w * a_)
+    mag.index_add_(0, U + nid.cpu(), w * a_)
+    err = (gE.double().cpu() - gR).abs()
+    assert bool((err <= 1e-5 * mag + 1e-30).all()), float((err / (mag + 1e-30)).max())
