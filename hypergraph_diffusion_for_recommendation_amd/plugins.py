@@ -68,15 +68,19 @@ def l2_reg_loss(reg, *args):
 
 
 def _device_drop_edge(dropper, kwargs) -> None:
-    """``hgd_device_rng``: the drop-edge masks come from the device (same Bernoulli(keep) per
-    edge, not the reference's CPU ``torch.rand`` stream). For the HCCF encoders they are drawn
-    from a device seed counter and applied as masked views of the parent adjacency (no
-    compaction, no kept-count read), with the InfoNCE node counts kept on the device too
-    (:meth:`HCCF.ssl_loss`): an eager step then makes no host read at all (Yelp shape: 2.0 ms
-    against 3.2 ms with compacted children, ``scripts/bench_hccf.py``)."""
-    on = bool(kwargs.get('hgd_device_rng', False))
-    dropper.device_rng = on
-    dropper.capture_safe = on
+    """The drop-edge result of every step is a masked VIEW of the parent adjacency (no
+    compaction, no kept-count or split-plan read), with the InfoNCE node counts kept on the
+    device too (:meth:`HCCF.ssl_loss`): an eager step makes no host read. The masks stay the
+    reference's CPU ``torch.rand`` stream (bit-identical drops), drawn natively ahead of the
+    step into per-call slots. Yelp shape 1.93 ms per eager step against 2.9 ms with compacted
+    children (``scripts/bench_hccf.py``); on a Zipf-skewed catalogue, whose compacted children
+    re-plan their split rows every step, 2.9 against 4.8 ms (``scripts/profile_plugin_steps.py``).
+    ``hgd_compact_drop`` keeps the compacted children (the reference's sparse tensors; the
+    sums differ from the view's only in the order of split rows' partials). ``hgd_device_rng``:
+    the masks come from a device seed counter instead (same Bernoulli(keep) per edge, a
+    different stream, no host work)."""
+    dropper.device_rng = bool(kwargs.get('hgd_device_rng', False))
+    dropper.capture_safe = not bool(kwargs.get('hgd_compact_drop', False))
 
 
 class HCCF(GraphRecommender):

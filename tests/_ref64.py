@@ -65,9 +65,21 @@ class DropRecorder(nn.Module):
         self.inner = inner
         self.outputs = []
 
+    def begin_step(self):
+        begin = getattr(self.inner, "begin_step", None)
+        if begin is not None:
+            begin()
+
     def forward(self, adj, keep):
         out = self.inner(adj, keep)
-        self.outputs.append((out._indices().cpu(), out._values().cpu()))
+        if getattr(out, "parent", None) is not None and hasattr(out.csr, "mask"):
+            # a masked view (SpAdjDropEdge(capture_safe)): the kept entries of the parent COO
+            # (CSR order), values / keep in float32 — what the compacted output holds
+            m = out.csr.mask.bool().cpu()
+            idx, vals = adj._indices().cpu(), adj._values().cpu()
+            self.outputs.append((idx[:, m], vals[m] / keep))
+        else:
+            self.outputs.append((out._indices().cpu(), out._values().cpu()))
         return out
 
 

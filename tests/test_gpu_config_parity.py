@@ -58,7 +58,8 @@ def _coo_host(adj):
 # ---------------------------------------------------------------------------------------------
 # HCCF (configs[0], configs[2])
 # ---------------------------------------------------------------------------------------------
-def _hccf_case(dev, shape, d, n_layers, seed, batch=4096, temp=1.0, cl_rate=0.01):
+def _hccf_case(dev, shape, d, n_layers, seed, batch=4096, temp=1.0, cl_rate=0.01,
+               capture_safe=False):
     """One HCCF training step's forward and backward (HCCF.py:79-97): encoder with drop-edge
     (keep 1 - conf dropout 0.3) and learned-hypergraph dropout (--drop_rate 0.2), then
     HCCF.calcLosses (BPR + cl_rate · Σ_layers InfoNCE at conf temp), as the plugin computes it
@@ -74,6 +75,9 @@ def _hccf_case(dev, shape, d, n_layers, seed, batch=4096, temp=1.0, cl_rate=0.01
     torch.manual_seed(seed)
     enc = HCCFEncoder(kw, data, device=dev).train()
     enc.drop_out = R.FixedDropout(0.2, seed + 1)
+    # capture_safe: the plugins' default drop-edge — masked views of the parent on the same
+    # CPU mask stream (the recorder reads the kept entries off the view's mask)
+    enc.edgeDropper.capture_safe = capture_safe
     enc.edgeDropper = R.DropRecorder(enc.edgeDropper)
     rng = np.random.default_rng(seed + 2)
     u, i, j = (torch.from_numpy(rng.integers(0, n, batch)) for n in (U, I, I))
@@ -129,6 +133,15 @@ def test_hccf_lastfm_1layer_d32_train_step(dev):
 def test_hccf_yelp_3layer_d64_infonce_train_step(dev):
     """configs[2]: Yelp2018 HCCF, 3 layers, d = 64, drop-edge + InfoNCE."""
     _hccf_case(dev, YELP, 64, 3, seed=20)
+
+
+@pytest.mark.parametrize("shape,d,layers,seed", [("LASTFM", 32, 1, 11), ("YELP", 64, 3, 21)])
+def test_hccf_train_step_on_masked_drop_views(dev, shape, d, layers, seed):
+    """The plugins' default drop-edge (masked views of the parent, the reference's CPU mask
+    stream): the recorded drops equal the reference's compaction bit for bit, and the step's
+    outputs and gradients meet the same row bound as with compacted children."""
+    _hccf_case(dev, {"LASTFM": LASTFM, "YELP": YELP}[shape], d, layers, seed=seed,
+               capture_safe=True)
 
 
 # ---------------------------------------------------------------------------------------------
