@@ -9,14 +9,13 @@ from contextlib import redirect_stdout
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
-sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 
 def main():
     import torch
 
-    import _ref64 as R
-    import test_gpu_config_parity as T
+    from tests import _ref64 as R
+    from tests import test_gpu_config_parity as T
     R.TOL = 1.0  # report, do not assert
     rows, wgrad = R.check_rows, R.check_weight_grad
     R.check_rows = lambda g, r, what, tol=None: rows(g, r, what, 1.0)
