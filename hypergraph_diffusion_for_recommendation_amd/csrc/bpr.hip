@@ -171,6 +171,45 @@ __global__ __launch_bounds__(kBlock) void k_bpr_bwd_rows(BprArgs a, const float*
       }
     }
   };
+  // add(js[0]) … add(js[cnt-1]) in that order, the rows of all of them loaded first
+  auto add4 = [&](const int64_t (&js)[4], int cnt) {
+    float t4[4];
+    int64_t k4[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t j = js[u];
+      k4[u] = j < a.B ? j : (j < 2 * a.B ? j - a.B : j - 2 * a.B);
+      t4[u] = u < cnt ? gB * coef[k4[u]] : 0.f;
+    }
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int c = 4 * (l + v * G);
+      if (c >= a.d) break;
+      float r1[4][4], r2[4][4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (u >= cnt) continue;
+        if (js[u] < a.B) {
+          load_vec<4>(a.E + static_cast<int64_t>(dst[a.B + k4[u]]) * a.lde + c, r1[u]);
+          load_vec<4>(a.E + static_cast<int64_t>(dst[2 * a.B + k4[u]]) * a.lde + c, r2[u]);
+        } else {
+          load_vec<4>(a.E + static_cast<int64_t>(dst[k4[u]]) * a.lde + c, r1[u]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (u >= cnt) continue;
+        if (js[u] < a.B) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[v][i] += t4[u] * (r1[u][i] - r2[u][i]);
+        } else {
+          const float sg = js[u] < 2 * a.B ? t4[u] : -t4[u];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[v][i] += sg * r1[u][i];
+        }
+      }
+    }
+  };
   // walk the list once: its length (up to CAP + 1), and entry t in slot t (written by lane
   // t mod G)
   int n_pos = 0;
@@ -214,9 +253,21 @@ __global__ __launch_bounds__(kBlock) void k_bpr_bwd_rows(BprArgs a, const float*
       while (lanes) {
         const int src = __ffsll(static_cast<unsigned long long>(lanes)) - 1;
         lanes &= lanes - 1ull;
-        for (unsigned m = static_cast<unsigned>(__shfl(static_cast<int>(hits), g0 + src)); m;
-             m &= m - 1u)
-          add(base + src * K + (__ffs(m) - 1));
+        unsigned m = static_cast<unsigned>(__shfl(static_cast<int>(hits), g0 + src));
+        while (m) {  // up to four positions at a time: their loads in flight together
+          int64_t js[4];
+          int cnt = 0;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            js[u] = 0;
+            if (m) {
+              js[u] = base + src * K + (__ffs(m) - 1);
+              m &= m - 1u;
+              ++cnt;
+            }
+          }
+          add4(js, cnt);
+        }
       }
     }
   }

@@ -11,6 +11,8 @@ forward, BPR + per-layer InfoNCE, backward, Adam — the repo's "hypergraph diff
                     drop-edge as masked views, the ED-HNN block's dropouts on the library RNG,
                     fused BPR on the encoder table, device-side InfoNCE node counts, capturable
                     fused Adam) — HCCF_diffusion(hgd_graph=True);
+* hgd_plugin_eager — the plugin's eager default: masked drop-edge views on the reference's CPU
+                    mask stream, fused BPR, device-side InfoNCE node counts, the reference's Adam;
 * reference_ops   — the same step with the reference's torch calls on the same GPU and the same
                     parameters: torch.sparse.mm, torch.nonzero(H > 0), the scatter-mean pair
                     (torch_scatter's mean as index_reduce_, pytorch-scatter being absent),
@@ -102,7 +104,8 @@ def main():
         emb = sum(hidden)
         return emb[:nu], emb[nu:], gcn_l, hyp_l
 
-    def make_step(fwd, loss_fn, unique, hoist, graph=False, params=None):
+    def make_step(fwd, loss_fn, unique, hoist, graph=False, params=None, counted=None):
+        counted = graph if counted is None else counted
         params = list(model.parameters() if params is None else params)
         if graph:
             lr = torch.tensor(conf["lrate"], dtype=torch.float32, device=dev)
@@ -113,7 +116,7 @@ def main():
 
         def body(uid, pid, nid):
             ue, ie, gcn, hyp = fwd(keep)
-            if graph:  # HCCF_diffusion(hgd_graph=True)'s train_step
+            if counted:  # the plugin's train_step ops (graph mode and the eager default)
                 bpr, anc, pos = bpr_loss_rows(ue, ie, uid, pid, nid)
                 (un, uc), (pn, pc) = unique_long_n(anc, nu), unique_long_n(pos, ni)
                 ssl = 0
@@ -178,6 +181,15 @@ def main():
         g_model.train()
         out.append(("hgd_graph", timed(make_step(g_model, None, None, True, graph=True,
                                                  params=g_model.parameters()))))
+    if "hgd_plugin_eager" in want:  # the plugin's eager default: masked drop-edge views on the
+        torch.manual_seed(0)        # reference's CPU mask stream, counted ops, unfused Adam
+        p_model = HCCFDiffusionEncoder(conf, data, dev)
+        p_model.load_state_dict(model.state_dict())
+        p_model.edgeDropper.device_rng = False
+        p_model.edgeDropper.capture_safe = True
+        p_model.train()
+        out.append(("hgd_plugin_eager", timed(make_step(p_model, None, None, True, counted=True,
+                                                        params=p_model.parameters()))))
     if "reference_ops" in want:
         out.append(("reference_ops", timed(make_step(
             ref_forward, R.contrast_loss, lambda t: torch.unique(t.long()), False))))
