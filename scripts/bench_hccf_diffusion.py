@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--variants", default="hgd_device_mask,hgd_graph,reference_ops")
+    ap.add_argument("--profile", action="store_true",
+                    help="cProfile 20 steps of each variant (stderr)")
     args = ap.parse_args()
     import torch
     import torch.nn.functional as F
@@ -156,6 +158,16 @@ def main():
         for _ in range(3):
             step()
         torch.cuda.synchronize()
+        if args.profile:  # host-side cost of the variant's steps (top functions by own time)
+            import cProfile
+            import pstats
+            pr = cProfile.Profile()
+            pr.enable()
+            for _ in range(20):
+                step()
+            torch.cuda.synchronize()
+            pr.disable()
+            pstats.Stats(pr, stream=sys.stderr).sort_stats("tottime").print_stats(25)
         ts = []
         for _ in range(args.reps):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
