@@ -167,7 +167,9 @@ def main():
                 step()
             torch.cuda.synchronize()
             pr.disable()
-            pstats.Stats(pr, stream=sys.stderr).sort_stats("tottime").print_stats(25)
+            st = pstats.Stats(pr, stream=sys.stderr)
+            st.sort_stats("tottime").print_stats(25)
+            st.print_callers("item|cpu|tolist|synchronize")
         ts = []
         for _ in range(args.reps):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
