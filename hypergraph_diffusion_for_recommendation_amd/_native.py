@@ -132,6 +132,21 @@ class GemmTnDesc(ctypes.Structure):
     ]
 
 
+class UniqueJob(ctypes.Structure):
+    """Mirror of ``hgd_unique_job`` (include/hgd.h)."""
+
+    _fields_ = [
+        ("x_f32", c_void_p),
+        ("x_i64", c_void_p),
+        ("n", c_i64),
+        ("capacity", c_i64),
+        ("out", c_void_p),
+        ("n_out", c_void_p),
+        ("workspace", c_void_p),
+        ("workspace_bytes", c_size),
+    ]
+
+
 class InfonceTerm(ctypes.Structure):
     """Mirror of ``hgd_infonce_term`` (include/hgd.h)."""
 
@@ -332,6 +347,7 @@ _SIGNATURES = {
                                    c_void_p]),
     "hgd_unique_dev_trunc_f32": (c_i32, [c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_size,
                                          c_void_p]),
+    "hgd_unique_dev_group": (c_i32, [c_void_p, c_i32, c_void_p]),
     "hgd_unique_sort_i64": (c_i32, [c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_size,
                                     c_void_p]),
     "hgd_unique_sort_trunc_f32": (c_i32, [c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_size,

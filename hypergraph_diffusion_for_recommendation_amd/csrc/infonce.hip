@@ -40,8 +40,8 @@ inline float exp2_scale(float temp) {
   return static_cast<float>(1.4426950408889634 / static_cast<double>(temp));
 }
 
-// One InfoNCE term's operands (both halves of HCCF's paired terms, HCCF.py:65-66, run as ONE
-// launch per kernel: blocks [0, nb0) along x take p[0], the rest p[1]).
+// One InfoNCE term's operands. Up to kMaxTerms terms run as ONE launch per kernel (HCCF's user
+// and item terms of every layer, HCCF.py:62-67): blocks [start[i], start[i+1]) along x take p[i].
 struct NceProb {
   const float* E1;
   int64_t ld1;
@@ -71,18 +71,21 @@ struct NceProb {
   int64_t ldE2;
 };
 
+constexpr int kMaxTerms = 8;
+
 struct NceGroup {
-  NceProb p[2];
+  NceProb p[kMaxTerms];
   int32_t count;
-  int32_t nb0;  // x-blocks of p[0]
+  int32_t start[kMaxTerms];  // first x-block of each term
 };
 
 __device__ __forceinline__ NceProb pick(const NceGroup& g, int64_t& bx) {
-  if (g.count > 1 && bx >= g.nb0) {
-    bx -= g.nb0;
-    return g.p[1];
-  }
-  return g.p[0];
+  int i = 0;
+#pragma unroll
+  for (int k = 1; k < kMaxTerms; ++k)
+    if (k < g.count && bx >= g.start[k]) i = k;
+  bx -= g.start[i];
+  return g.p[i];
 }
 
 // ---- gather + normalise: one group of G = d/4 lanes per batch row ----
@@ -543,9 +546,8 @@ NceGroup group_of(const NceProb* p, int count, int64_t rows_per_block, unsigned*
   int64_t total = 0;
   for (int i = 0; i < count; ++i) {
     g.p[i] = p[i];
-    const int64_t nb = (p[i].B + rows_per_block - 1) / rows_per_block;
-    if (i == 0) g.nb0 = static_cast<int32_t>(nb);
-    total += nb;
+    g.start[i] = static_cast<int32_t>(total);
+    total += (p[i].B + rows_per_block - 1) / rows_per_block;
   }
   *grid_x = static_cast<unsigned>(total);
   return g;
@@ -553,9 +555,9 @@ NceGroup group_of(const NceProb* p, int count, int64_t rows_per_block, unsigned*
 
 hgd_status infonce_forward(const hgd_infonce_term* terms, int count, int32_t d, float temp,
                            hipStream_t st, const char* fn) {
-  HGD_REQUIRE(terms && count >= 1 && count <= 2, "%s: 1 or 2 terms", fn);
+  HGD_REQUIRE(terms && count >= 1 && count <= kMaxTerms, "%s: 1 to %d terms", fn, kMaxTerms);
   HGD_REQUIRE(temp > 0.f, "%s: temperature must be > 0", fn);
-  NceProb p[2];
+  NceProb p[kMaxTerms];
   int64_t s_max = 1;
   for (int i = 0; i < count; ++i) {
     const hgd_status c = prepare(terms[i], d, false, &p[i], fn);
@@ -597,10 +599,10 @@ hgd_status infonce_forward(const hgd_infonce_term* terms, int count, int32_t d, 
 
 hgd_status infonce_backward(const hgd_infonce_term* terms, int count, int32_t d, float temp,
                             const float* grad_loss, hipStream_t st, const char* fn) {
-  HGD_REQUIRE(terms && count >= 1 && count <= 2, "%s: 1 or 2 terms", fn);
+  HGD_REQUIRE(terms && count >= 1 && count <= kMaxTerms, "%s: 1 to %d terms", fn, kMaxTerms);
   HGD_REQUIRE(temp > 0.f, "%s: temperature must be > 0", fn);
   HGD_REQUIRE(grad_loss, "%s: null grad_loss", fn);
-  NceProb p[2];
+  NceProb p[kMaxTerms];
   int64_t s_max = 1;
   bool side1 = false, side2 = false;
   for (int i = 0; i < count; ++i) {

@@ -68,7 +68,7 @@ __device__ __forceinline__ long long wave_max(long long v) {
   return v;
 }
 
-__global__ void k_uq_init(State* st) {
+__device__ __forceinline__ void uq_init(State* st) {
   st->lo = LLONG_MAX;
   st->hi = LLONG_MIN;
   st->overflow = 0;
@@ -76,7 +76,7 @@ __global__ void k_uq_init(State* st) {
 }
 
 template <class Src>
-__global__ __launch_bounds__(256) void k_uq_minmax(Src src, int64_t n, State* st) {
+__device__ __forceinline__ void uq_minmax(Src src, int64_t n, State* st) {
   long long lo = LLONG_MAX, hi = LLONG_MIN;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
@@ -128,7 +128,7 @@ __device__ __forceinline__ bool range_words(const State* st, int64_t* words) {
 }
 
 template <bool CLAMP>
-__global__ __launch_bounds__(256) void k_uq_zero(uint32_t* bitmap, State* st) {
+__device__ __forceinline__ void uq_zero(uint32_t* bitmap, State* st) {
   int64_t words;
   if (!range_words<CLAMP>(st, &words)) {
     if (blockIdx.x == 0 && threadIdx.x == 0) st->overflow = 1;
@@ -143,8 +143,8 @@ __global__ __launch_bounds__(256) void k_uq_zero(uint32_t* bitmap, State* st) {
 // Sets every key's bit. FAR (device-complete path): keys past the kCapBits window are appended
 // to `far` (State::far_n counts them) instead.
 template <class Src, bool FAR = false>
-__global__ __launch_bounds__(256) void k_uq_mark(Src src, int64_t n, uint32_t* bitmap,
-                                                 State* st, int64_t* far = nullptr) {
+__device__ __forceinline__ void uq_mark(Src src, int64_t n, uint32_t* bitmap, State* st,
+                                        int64_t* far) {
   __shared__ uint32_t s_bits[kLdsWords];
   int64_t words;
   if (!range_words<FAR>(st, &words) || words == 0) return;  // uniform over the grid
@@ -202,8 +202,8 @@ __device__ __forceinline__ int block_exclusive_scan(int v, int* total) {
 }
 
 template <bool CLAMP>
-__global__ __launch_bounds__(kEmitThreads) void k_uq_count(const uint32_t* bitmap,
-                                                           const State* st, int* tile_cnt) {
+__device__ __forceinline__ void uq_count(const uint32_t* bitmap, const State* st,
+                                         int* tile_cnt) {
   int64_t words;
   if (!range_words<CLAMP>(st, &words)) return;
   const int64_t tiles = (words + kTileWords - 1) / kTileWords;
@@ -219,8 +219,8 @@ __global__ __launch_bounds__(kEmitThreads) void k_uq_count(const uint32_t* bitma
 }
 
 template <bool CLAMP>
-__global__ __launch_bounds__(kMaxTiles) void k_uq_scan(const int* tile_cnt, const State* st,
-                                                       int64_t* tile_off, int64_t* n_out) {
+__device__ __forceinline__ void uq_scan(const int* tile_cnt, const State* st, int64_t* tile_off,
+                                        int64_t* n_out) {
   __shared__ int64_t s[kMaxTiles];
   int64_t words;
   if (!range_words<CLAMP>(st, &words)) {
@@ -242,8 +242,8 @@ __global__ __launch_bounds__(kMaxTiles) void k_uq_scan(const int* tile_cnt, cons
 }
 
 template <bool CLAMP>
-__global__ __launch_bounds__(kEmitThreads) void k_uq_emit(const uint32_t* bitmap, const State* st,
-                                                          const int64_t* tile_off, int64_t* out) {
+__device__ __forceinline__ void uq_emit(const uint32_t* bitmap, const State* st,
+                                        const int64_t* tile_off, int64_t* out) {
   int64_t words;
   if (!range_words<CLAMP>(st, &words)) return;
   const int64_t tiles = (words + kTileWords - 1) / kTileWords;
@@ -308,9 +308,8 @@ __device__ __forceinline__ void block_bitonic(Keys& keys, int P) {
   }
 }
 
-__global__ __launch_bounds__(kFarThreads) void k_uq_far(State* st, int64_t* far, int64_t cap,
-                                                        int64_t* out, int64_t* n_out,
-                                                        int64_t n) {
+__device__ __forceinline__ void uq_far(State* st, int64_t* far, int64_t cap, int64_t* out,
+                                       int64_t* n_out, int64_t n) {
   __shared__ int64_t s_keys[kFarLds];
   __shared__ int s_wave[kFarThreads / 64];
   int64_t kk = static_cast<int64_t>(st->far_n);
@@ -360,6 +359,110 @@ __global__ __launch_bounds__(kFarThreads) void k_uq_far(State* st, int64_t* far,
     __syncthreads();
   }
   if (t == 0) *n_out = base;
+}
+
+// Single-call kernels (the bodies above) and the grouped forms of the device-complete path
+// (hgd_unique_dev_group: blockIdx.y picks the call, so several node lists share each launch).
+__global__ void k_uq_init(State* st) { uq_init(st); }
+template <class Src>
+__global__ __launch_bounds__(256) void k_uq_minmax(Src src, int64_t n, State* st) {
+  uq_minmax(src, n, st);
+}
+template <bool CLAMP>
+__global__ __launch_bounds__(256) void k_uq_zero(uint32_t* bitmap, State* st) {
+  uq_zero<CLAMP>(bitmap, st);
+}
+template <class Src, bool FAR = false>
+__global__ __launch_bounds__(256) void k_uq_mark(Src src, int64_t n, uint32_t* bitmap, State* st,
+                                                 int64_t* far = nullptr) {
+  uq_mark<Src, FAR>(src, n, bitmap, st, far);
+}
+template <bool CLAMP>
+__global__ __launch_bounds__(kEmitThreads) void k_uq_count(const uint32_t* bitmap, const State* st,
+                                                           int* tile_cnt) {
+  uq_count<CLAMP>(bitmap, st, tile_cnt);
+}
+template <bool CLAMP>
+__global__ __launch_bounds__(kMaxTiles) void k_uq_scan(const int* tile_cnt, const State* st,
+                                                       int64_t* tile_off, int64_t* n_out) {
+  uq_scan<CLAMP>(tile_cnt, st, tile_off, n_out);
+}
+template <bool CLAMP>
+__global__ __launch_bounds__(kEmitThreads) void k_uq_emit(const uint32_t* bitmap, const State* st,
+                                                          const int64_t* tile_off, int64_t* out) {
+  uq_emit<CLAMP>(bitmap, st, tile_off, out);
+}
+__global__ __launch_bounds__(kFarThreads) void k_uq_far(State* st, int64_t* far, int64_t cap,
+                                                        int64_t* out, int64_t* n_out, int64_t n) {
+  uq_far(st, far, cap, out, n_out, n);
+}
+
+// A key source of either type (a group may mix float and int64 lists).
+struct AnySrc {
+  const float* f;
+  const int64_t* i;
+  __device__ int64_t operator()(int64_t k) const {
+    return f ? TruncSrc{f}(k) : i[k];
+  }
+};
+
+constexpr int kMaxJobs = 4;
+struct UqJob {
+  AnySrc src;
+  int64_t n;
+  int64_t* out;
+  int64_t* n_out;
+  State* st;
+  int* cnt;
+  int64_t* toff;
+  uint32_t* bitmap;
+  int64_t* far;
+  int64_t far_cap;
+  int64_t cap;  // entries kept: n_out clamped to it, out[n_out, cap) zeroed
+};
+struct UqJobs {
+  UqJob j[kMaxJobs];
+};
+
+__global__ void k_uqg_init(UqJobs J) { uq_init(J.j[blockIdx.y].st); }
+__global__ __launch_bounds__(256) void k_uqg_minmax(UqJobs J) {
+  const UqJob& j = J.j[blockIdx.y];
+  uq_minmax(j.src, j.n, j.st);
+}
+__global__ __launch_bounds__(256) void k_uqg_zero(UqJobs J) {
+  const UqJob& j = J.j[blockIdx.y];
+  uq_zero<true>(j.bitmap, j.st);
+}
+__global__ __launch_bounds__(256) void k_uqg_mark(UqJobs J) {
+  const UqJob& j = J.j[blockIdx.y];
+  uq_mark<AnySrc, true>(j.src, j.n, j.bitmap, j.st, j.far);
+}
+__global__ __launch_bounds__(kEmitThreads) void k_uqg_count(UqJobs J) {
+  const UqJob& j = J.j[blockIdx.y];
+  uq_count<true>(j.bitmap, j.st, j.cnt);
+}
+__global__ __launch_bounds__(kMaxTiles) void k_uqg_scan(UqJobs J) {
+  const UqJob& j = J.j[blockIdx.y];
+  uq_scan<true>(j.cnt, j.st, j.toff, j.n_out);
+}
+__global__ __launch_bounds__(kEmitThreads) void k_uqg_emit(UqJobs J) {
+  const UqJob& j = J.j[blockIdx.y];
+  uq_emit<true>(j.bitmap, j.st, j.toff, j.out);
+}
+__global__ __launch_bounds__(kFarThreads) void k_uqg_far(UqJobs J) {
+  const UqJob& j = J.j[blockIdx.y];
+  uq_far(j.st, j.far, j.far_cap, j.out, j.n_out, j.n);
+}
+// n_out = min(n_out, cap) and out[n_out, cap) = 0. Every block derives the same clamped count
+// (min is idempotent, so reading before or after block 0's store gives the same value).
+__global__ __launch_bounds__(256) void k_uqg_tail(UqJobs J) {
+  const UqJob& j = J.j[blockIdx.y];
+  const int64_t raw = *j.n_out;
+  const int64_t c = raw < j.cap ? raw : j.cap;
+  for (int64_t i = c + blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < j.cap;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    j.out[i] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && raw > j.cap) *j.n_out = j.cap;
 }
 
 template <class Src>
@@ -465,6 +568,61 @@ hgd_status unique_sort(Src src, const int64_t* keys_in, int64_t n, int64_t* out,
   return HGD_OK;
 }
 
+// The device-complete path for several lists at once: the same kernels, one launch each for
+// all of them (grid y = the list), every list exactly as hgd_unique_dev_* would give it.
+hgd_status unique_group(const hgd_unique_job* jobs, int count, hipStream_t st, const char* fn) {
+  HGD_REQUIRE(jobs && count >= 1 && count <= kMaxJobs, "%s: 1 to %d lists", fn, kMaxJobs);
+  UqJobs J{};
+  int64_t n_max = 0;
+  for (int k = 0; k < count; ++k) {
+    const hgd_unique_job& q = jobs[k];
+    HGD_REQUIRE(q.n >= 0 && q.n < (int64_t(1) << 31), "%s: list %d: n must be in [0, 2^31)", fn, k);
+    HGD_REQUIRE(q.n_out && (q.n == 0 || q.out), "%s: list %d: null output", fn, k);
+    HGD_REQUIRE(q.n == 0 || (q.x_f32 != nullptr) != (q.x_i64 != nullptr),
+                "%s: list %d: exactly one of x_f32 / x_i64", fn, k);
+    const size_t need = dev_path_bytes(q.n);
+    if (q.workspace_bytes < need || !q.workspace)
+      return fail(HGD_ERR_WORKSPACE, "%s: list %d: workspace %zu < required %zu", fn, k,
+                  q.workspace_bytes, need);
+    char* w = static_cast<char*>(q.workspace);
+    UqJob& j = J.j[k];
+    j.src = AnySrc{q.x_f32, q.x_i64};
+    j.n = q.n;
+    j.out = q.out;
+    j.n_out = q.n_out;
+    j.st = reinterpret_cast<State*>(w + kOffState);
+    j.cnt = reinterpret_cast<int*>(w + kOffCnt);
+    j.toff = reinterpret_cast<int64_t*>(w + kOffTileOff);
+    j.bitmap = reinterpret_cast<uint32_t*>(w + kOffBitmap);
+    j.far = reinterpret_cast<int64_t*>(w + kBitmapPathBytes);
+    j.far_cap = far_capacity(q.n);
+    HGD_REQUIRE(q.capacity >= 0 && q.capacity <= q.n, "%s: list %d: capacity must be in [0, n]",
+                fn, k);
+    j.cap = q.capacity > 0 ? q.capacity : q.n;
+    n_max = std::max(n_max, q.n);
+  }
+  const unsigned y = static_cast<unsigned>(count);
+  hipLaunchKernelGGL(k_uqg_init, dim3(1, y), dim3(1), 0, st, J);
+  if (n_max > 0) {
+    const unsigned g = static_cast<unsigned>(std::min<int64_t>(kGrid, (n_max + 4095) / 4096));
+    hipLaunchKernelGGL(k_uqg_minmax, dim3(g, y), dim3(256), 0, st, J);
+  }
+  hipLaunchKernelGGL(k_uqg_zero, dim3(kGrid, y), dim3(256), 0, st, J);
+  if (n_max > 0) {
+    const unsigned g = static_cast<unsigned>(std::min<int64_t>(kGrid, (n_max + 255) / 256));
+    hipLaunchKernelGGL(k_uqg_mark, dim3(g, y), dim3(256), 0, st, J);
+  }
+  hipLaunchKernelGGL(k_uqg_count, dim3(kMaxTiles, y), dim3(kEmitThreads), 0, st, J);
+  hipLaunchKernelGGL(k_uqg_scan, dim3(1, y), dim3(kMaxTiles), 0, st, J);
+  hipLaunchKernelGGL(k_uqg_emit, dim3(kMaxTiles, y), dim3(kEmitThreads), 0, st, J);
+  hipLaunchKernelGGL(k_uqg_far, dim3(1, y), dim3(kFarThreads), 0, st, J);
+  if (n_max > 0) {
+    const unsigned g = static_cast<unsigned>(std::min<int64_t>(kGrid, (n_max + 255) / 256));
+    hipLaunchKernelGGL(k_uqg_tail, dim3(g, y), dim3(256), 0, st, J);
+  }
+  return check_launch(fn);
+}
+
 }  // namespace
 }  // namespace hgd
 
@@ -523,4 +681,10 @@ extern "C" hgd_status hgd_unique_dev_trunc_f32(const float* x, int64_t n, int64_
   HGD_REQUIRE(n == 0 || x, "hgd_unique_dev_trunc_f32: null x");
   return unique_bitmap<TruncSrc, true>(TruncSrc{x}, n, out, n_out, ws, wsb, as_stream(stream),
                                        "hgd_unique_dev_trunc_f32");
+}
+
+extern "C" hgd_status hgd_unique_dev_group(const hgd_unique_job* jobs, int32_t count,
+                                           void* stream) {
+  clear_error();
+  return unique_group(jobs, count, as_stream(stream), "hgd_unique_dev_group");
 }

@@ -24,7 +24,7 @@ diagonals swapped.
 from __future__ import annotations
 
 import ctypes
-from typing import Optional, Tuple
+from typing import List, Optional, Tuple
 
 import torch
 
@@ -734,89 +734,138 @@ class _ContrastLoss(torch.autograd.Function):
         return dE1, dE2, None, None, None
 
 
-class _ContrastLossPair(torch.autograd.Function):
-    """The user and item contrastLoss terms of one HCCF layer on the halves of the [U + I, d]
-    tables (HCCF.py:65-66), with device counts: both InfoNCE terms as ONE launch per kernel
-    (hgd_infonce_forward_group / _backward_group, each term on its row offset of the full
-    tables), and in the backward ONE zeroed [U + I, d] gradient per table that both terms'
-    scatters write into — instead of per-term launches, per-half zeroed gradients, the slice
-    backward's zeroed full table plus copy, and the add joining the halves."""
+class _ContrastLossLayers(torch.autograd.Function):
+    """The user and item contrastLoss terms of every HCCF layer on the halves of the [U + I, d]
+    tables (HCCF.py:62-67), with device counts: all 2·L InfoNCE terms as ONE launch per kernel
+    (hgd_infonce_forward_group / _backward_group, each term on its row offset of its layer's
+    tables), and in the backward ONE zeroed [U + I, d] gradient per table that both of its
+    terms' scatters write into — instead of per-term launches, per-half zeroed gradients, the
+    slice backward's zeroed full table plus copy, and the adds joining halves and layers.
+    Inputs after the scalars: E1 of layer 0, E2 of layer 0, E1 of layer 1, …; the output is
+    the sum of the 2·L term losses."""
 
     @staticmethod
-    def forward(ctx, E1, E2, nu, nodes_u, count_u, nodes_i, count_i, temp: float):
+    def forward(ctx, nu, nodes_u, count_u, nodes_i, count_i, temp: float, *tables):
         lib = nat.load()
-        dev = E1.device
-        E1c, E2c = E1.contiguous(), E2.contiguous()
-        d = E1.shape[1]
-        N = E1.shape[0]
+        L = len(tables) // 2
+        dev = tables[0].device
+        d = tables[0].shape[1]
+        N = tables[0].shape[0]
         f = dict(dtype=torch.float32, device=dev)
-        loss2 = torch.empty(2, **f)
-        terms = (nat.InfonceTerm * 2)()
+        losses = torch.empty(2 * L, **f)
+        terms = (nat.InfonceTerm * (2 * L))()
         saved, keep = [], []
-        for k, (r0, rows, nodes, count) in enumerate(((0, nu, nodes_u, count_u),
-                                                      (nu, N - nu, nodes_i, count_i))):
-            nodes = nodes.to(device=dev, dtype=torch.int64).contiguous()
-            B = nodes.numel()
-            P1, P2 = torch.empty((B, d), **f), torch.empty((B, d), **f)
-            inv1, inv2, pos, deno = (torch.empty(B, **f) for _ in range(4))
-            wsb = lib.hgd_infonce_workspace_size(B, d)
-            ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
-            t = terms[k]
-            off = r0 * d * 4
-            t.E1, t.ld1, t.E2, t.ld2 = E1c.data_ptr() + off, d, E2c.data_ptr() + off, d
-            t.n_rows, t.nodes, t.capacity, t.batch_count = rows, nodes.data_ptr(), B, \
-                count.data_ptr()
-            t.P1, t.P2, t.inv_norm1, t.inv_norm2 = (P1.data_ptr(), P2.data_ptr(),
-                                                    inv1.data_ptr(), inv2.data_ptr())
-            t.pos_logit, t.deno, t.loss = pos.data_ptr(), deno.data_ptr(), \
-                loss2.data_ptr() + 4 * k
-            t.workspace, t.workspace_bytes = ws.data_ptr(), wsb
-            saved += [P1, P2, inv1, inv2, deno, nodes, count]
-            keep.append(ws)
-        nat.check(lib.hgd_infonce_forward_group(terms, 2, d, float(temp),
+        halves = []
+        for r0, rows, nodes, count in ((0, nu, nodes_u, count_u), (nu, N - nu, nodes_i, count_i)):
+            halves.append((r0, rows, nodes.to(device=dev, dtype=torch.int64).contiguous(), count))
+        for layer in range(L):
+            E1c, E2c = tables[2 * layer].contiguous(), tables[2 * layer + 1].contiguous()
+            keep += [E1c, E2c]
+            for k, (r0, rows, nodes, count) in enumerate(halves):
+                B = nodes.numel()
+                P1, P2 = torch.empty((B, d), **f), torch.empty((B, d), **f)
+                inv1, inv2, pos, deno = (torch.empty(B, **f) for _ in range(4))
+                wsb = lib.hgd_infonce_workspace_size(B, d)
+                ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+                t = terms[2 * layer + k]
+                off = r0 * d * 4
+                t.E1, t.ld1, t.E2, t.ld2 = E1c.data_ptr() + off, d, E2c.data_ptr() + off, d
+                t.n_rows, t.nodes, t.capacity, t.batch_count = rows, nodes.data_ptr(), B, \
+                    count.data_ptr()
+                t.P1, t.P2, t.inv_norm1, t.inv_norm2 = (P1.data_ptr(), P2.data_ptr(),
+                                                        inv1.data_ptr(), inv2.data_ptr())
+                t.pos_logit, t.deno = pos.data_ptr(), deno.data_ptr()
+                t.loss = losses.data_ptr() + 4 * (2 * layer + k)
+                t.workspace, t.workspace_bytes = ws.data_ptr(), wsb
+                saved += [P1, P2, inv1, inv2, deno]
+                keep.append(ws)
+        nat.check(lib.hgd_infonce_forward_group(terms, 2 * L, d, float(temp),
                                                 nat.stream_handle(dev)),
                   "hgd_infonce_forward_group")
         ctx.temp = float(temp)
-        ctx.nu, ctx.N, ctx.d = nu, N, d
-        ctx.save_for_backward(*saved)
-        return loss2[0] + loss2[1]
+        ctx.nu, ctx.N, ctx.d, ctx.L = nu, N, d, L
+        ctx.save_for_backward(halves[0][2], count_u, halves[1][2], count_i, *saved)
+        return losses.sum() if L > 1 else losses[0] + losses[1]
 
     @staticmethod
     def backward(ctx, g):
         lib = nat.load()
-        saved = ctx.saved_tensors
+        nodes_u, count_u, nodes_i, count_i, *saved = ctx.saved_tensors
         dev = saved[0].device
-        nu, N, d = ctx.nu, ctx.N, ctx.d
+        nu, N, d, L = ctx.nu, ctx.N, ctx.d, ctx.L
         g = g.to(dtype=torch.float32).reshape(1).contiguous()
         f = dict(dtype=torch.float32, device=dev)
-        dE1 = torch.zeros((N, d), **f) if ctx.needs_input_grad[0] else None
-        dE2 = torch.zeros((N, d), **f) if ctx.needs_input_grad[1] else None
-        if dE1 is None and dE2 is None:
-            return (None,) * 8
-        terms = (nat.InfonceTerm * 2)()
+        need = ctx.needs_input_grad[6:]
+        grads = [torch.zeros((N, d), **f) if need[j] else None for j in range(2 * L)]
+        none = (None,) * 6
+        if all(x is None for x in grads):
+            return none + tuple(grads)
+        terms = (nat.InfonceTerm * (2 * L))()
         keep = []
-        for k, (r0, rows) in enumerate(((0, nu), (nu, N - nu))):
-            P1, P2, inv1, inv2, deno, nodes, count = saved[7 * k: 7 * k + 7]
-            B = P1.shape[0]
-            wsb = lib.hgd_infonce_workspace_size(B, d)
-            ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
-            keep.append(ws)
-            t = terms[k]
-            off = r0 * d * 4
-            t.n_rows, t.nodes, t.capacity, t.batch_count = rows, nodes.data_ptr(), B, \
-                count.data_ptr()
-            t.P1, t.P2, t.inv_norm1, t.inv_norm2 = (P1.data_ptr(), P2.data_ptr(),
-                                                    inv1.data_ptr(), inv2.data_ptr())
-            t.deno = deno.data_ptr()
-            if dE1 is not None:
-                t.dE1, t.ldE1 = dE1.data_ptr() + off, d
-            if dE2 is not None:
-                t.dE2, t.ldE2 = dE2.data_ptr() + off, d
-            t.workspace, t.workspace_bytes = ws.data_ptr(), wsb
-        nat.check(lib.hgd_infonce_backward_group(terms, 2, d, ctx.temp, g.data_ptr(),
+        for layer in range(L):
+            dE1, dE2 = grads[2 * layer], grads[2 * layer + 1]
+            for k, (r0, rows, nodes, count) in enumerate(((0, nu, nodes_u, count_u),
+                                                          (nu, N - nu, nodes_i, count_i))):
+                P1, P2, inv1, inv2, deno = saved[5 * (2 * layer + k): 5 * (2 * layer + k) + 5]
+                B = P1.shape[0]
+                wsb = lib.hgd_infonce_workspace_size(B, d)
+                ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+                keep.append(ws)
+                t = terms[2 * layer + k]
+                off = r0 * d * 4
+                t.n_rows, t.nodes, t.capacity, t.batch_count = rows, nodes.data_ptr(), B, \
+                    count.data_ptr()
+                t.P1, t.P2, t.inv_norm1, t.inv_norm2 = (P1.data_ptr(), P2.data_ptr(),
+                                                        inv1.data_ptr(), inv2.data_ptr())
+                t.deno = deno.data_ptr()
+                if dE1 is not None:
+                    t.dE1, t.ldE1 = dE1.data_ptr() + off, d
+                if dE2 is not None:
+                    t.dE2, t.ldE2 = dE2.data_ptr() + off, d
+                t.workspace, t.workspace_bytes = ws.data_ptr(), wsb
+        nat.check(lib.hgd_infonce_backward_group(terms, 2 * L, d, ctx.temp, g.data_ptr(),
                                                  nat.stream_handle(dev)),
                   "hgd_infonce_backward_group")
-        return dE1, dE2, None, None, None, None, None, None
+        return none + tuple(grads)
+
+
+_NCE_MAX_LAYERS = 4  # 2 terms per layer, hgd_infonce_*_group takes up to 8
+
+
+def _nce_group_ok(embeds1, embeds2, nu, nodes_u, nodes_i, count_u, count_i) -> bool:
+    d = embeds1.shape[-1]
+    return (count_u is not None and count_i is not None and embeds1.dim() == 2
+            and embeds2.shape == embeds1.shape and embeds1.is_cuda
+            and embeds1.dtype == torch.float32 and embeds2.dtype == torch.float32
+            and d % 16 == 0 and 16 <= d <= 256 and 0 < nu < embeds1.shape[0]
+            and nodes_u.numel() > 0 and nodes_i.numel() > 0)
+
+
+def contrast_loss_layers(embeds1s, embeds2s, nu: int, nodes_u: torch.Tensor,
+                         nodes_i: torch.Tensor, temp: float,
+                         count_u: Optional[torch.Tensor] = None,
+                         count_i: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``Σ_layers contrastLoss(e1[:nu], e2[:nu], nodes_u, temp) + contrastLoss(e1[nu:], e2[nu:],
+    nodes_i, temp)`` — HCCF.calcLosses' InfoNCE loop (HCCF.py:62-67) before ``ss_rate`` — as ONE
+    op over all layers when the node lists carry device counts (:func:`unique_long_n`), up to
+    four layers per launch; otherwise per-layer :func:`contrast_loss_pair` calls."""
+    e1s, e2s = list(embeds1s), list(embeds2s)
+    if len(e1s) != len(e2s) or not e1s:
+        raise ValueError("contrast_loss_layers: one embeds2 per embeds1, at least one layer")
+    ok = all(_nce_group_ok(a, b, nu, nodes_u, nodes_i, count_u, count_i) and
+             a.shape == e1s[0].shape for a, b in zip(e1s, e2s))
+    if not ok:
+        total = 0
+        for a, b in zip(e1s, e2s):
+            total = total + contrast_loss_pair(a, b, nu, nodes_u, nodes_i, temp, count_u, count_i)
+        return total
+    total = 0
+    for c0 in range(0, len(e1s), _NCE_MAX_LAYERS):
+        tables = [t for ab in zip(e1s[c0:c0 + _NCE_MAX_LAYERS], e2s[c0:c0 + _NCE_MAX_LAYERS])
+                  for t in ab]
+        total = total + _ContrastLossLayers.apply(int(nu), nodes_u, count_u, nodes_i, count_i,
+                                                  float(temp), *tables)
+    return total
 
 
 def contrast_loss_pair(embeds1: torch.Tensor, embeds2: torch.Tensor, nu: int,
@@ -826,17 +875,11 @@ def contrast_loss_pair(embeds1: torch.Tensor, embeds2: torch.Tensor, nu: int,
     """``contrastLoss(e1[:nu], e2[:nu], nodes_u, temp) + contrastLoss(e1[nu:], e2[nu:], nodes_i,
     temp)`` (HCCF.py:65-66, util/loss_torch.py:103-110) as one op when both node lists carry
     device counts (:func:`unique_long_n`); otherwise the two :func:`contrast_loss` calls."""
-    d = embeds1.shape[-1]
-    ok = (count_u is not None and count_i is not None and embeds1.dim() == 2
-          and embeds2.shape == embeds1.shape and embeds1.is_cuda
-          and embeds1.dtype == torch.float32 and embeds2.dtype == torch.float32
-          and d % 16 == 0 and 16 <= d <= 256 and 0 < nu < embeds1.shape[0]
-          and nodes_u.numel() > 0 and nodes_i.numel() > 0)
-    if not ok:
+    if not _nce_group_ok(embeds1, embeds2, nu, nodes_u, nodes_i, count_u, count_i):
         return (contrast_loss(embeds1[:nu], embeds2[:nu], nodes_u, temp, count_u)
                 + contrast_loss(embeds1[nu:], embeds2[nu:], nodes_i, temp, count_i))
-    return _ContrastLossPair.apply(embeds1, embeds2, int(nu), nodes_u, count_u, nodes_i,
-                                   count_i, float(temp))
+    return _ContrastLossLayers.apply(int(nu), nodes_u, count_u, nodes_i, count_i, float(temp),
+                                     embeds1, embeds2)
 
 
 def contrast_loss(embeds1: torch.Tensor, embeds2: torch.Tensor, nodes: torch.Tensor,
@@ -918,35 +961,57 @@ def unique_long_n(x: torch.Tensor, n_rows: Optional[int] = None
     """:func:`unique_long` without the device→host read, for a captured training step:
     ``(nodes, count)`` with ``nodes`` int64 capacity-sized, its first ``count[0]`` entries the
     sorted unique values of ``x.long()`` and the rest 0, ``count`` an int64 [1] device tensor
-    (hgd_unique_dev_*: the range bitmap with the far keys merged on the device, so no host
+    (hgd_unique_dev_group: the range bitmap with the far keys merged on the device, so no host
     decision). Feed both to :func:`contrast_loss`. The capacity is x.numel(), or at most
     2·n_rows when the ids index a table of ``n_rows`` rows: valid torch indices lie in
     [-n_rows, n_rows), so no valid list is longer (HCCF's ``torch.unique(anchor_emb.long())``,
     HCCF.py:65-66, reads a [B, d] table of a handful of distinct ints — B·d capacity made every
     InfoNCE buffer and grid that size); a list of out-of-range ids is cut to the capacity, and
     such ids are the caller's error either way (the reference's gather raises)."""
-    if not x.is_cuda or x.dtype not in (torch.float32, torch.int64):
-        raise ValueError("unique_long_n: needs a float32 or int64 device tensor")
-    x = x.detach().contiguous().view(-1)
-    n = x.numel()
-    if n == 0:
-        raise ValueError("unique_long_n: empty input")
+    return unique_long_n_group([x], [n_rows])[0]
+
+
+def unique_long_n_group(xs, n_rows=None) -> List[Tuple[torch.Tensor, torch.Tensor]]:
+    """:func:`unique_long_n` of several tensors in one launch per kernel (up to four per group;
+    HCCF's anchor and positive lists, HCCF.py:65-66): ``[(nodes, count)]`` in order, each
+    exactly as :func:`unique_long_n` gives it; ``n_rows`` a list of table sizes (or None)."""
+    xs = list(xs)
+    n_rows = list(n_rows) if n_rows is not None else [None] * len(xs)
+    if len(n_rows) != len(xs) or not xs:
+        raise ValueError("unique_long_n_group: one n_rows entry per tensor, at least one tensor")
     lib = nat.load()
-    dev = x.device
-    out = torch.empty(n, dtype=torch.int64, device=dev)
-    wsb = lib.hgd_unique_workspace_size(n)
-    buf = torch.empty(_UQ_HEAD + max(wsb, 1), dtype=torch.uint8, device=dev)
-    base = buf.data_ptr()
-    fn = lib.hgd_unique_dev_trunc_f32 if x.dtype == torch.float32 else lib.hgd_unique_dev_i64
-    nat.check(fn(x.data_ptr(), n, out.data_ptr(), base, base + _UQ_HEAD, wsb,
-                 nat.stream_handle(dev)), "hgd_unique_dev")
-    count = buf[:8].view(torch.int64)
-    cap = n if n_rows is None else max(1, min(n, 2 * int(n_rows)))
-    if cap < n:
-        out = out[:cap]
-        count = torch.clamp_max(count, cap)
-    live = torch.arange(cap, device=dev) < count
-    return torch.where(live, out, torch.zeros((), dtype=torch.int64, device=dev)), count
+    res = []
+    for c0 in range(0, len(xs), 4):
+        chunk = list(zip(xs[c0:c0 + 4], n_rows[c0:c0 + 4]))
+        jobs = (nat.UniqueJob * len(chunk))()
+        keep = []
+        dev = None
+        for q, (x, nr) in enumerate(chunk):
+            if not x.is_cuda or x.dtype not in (torch.float32, torch.int64):
+                raise ValueError("unique_long_n: needs a float32 or int64 device tensor")
+            x = x.detach().contiguous().view(-1)
+            n = x.numel()
+            if n == 0:
+                raise ValueError("unique_long_n: empty input")
+            dev = x.device
+            out = torch.empty(n, dtype=torch.int64, device=dev)
+            count = torch.empty(1, dtype=torch.int64, device=dev)
+            wsb = lib.hgd_unique_workspace_size(n)
+            ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+            cap = n if nr is None else max(1, min(n, 2 * int(nr)))
+            j = jobs[q]
+            if x.dtype == torch.float32:
+                j.x_f32 = x.data_ptr()
+            else:
+                j.x_i64 = x.data_ptr()
+            j.n, j.capacity = n, cap
+            j.out, j.n_out = out.data_ptr(), count.data_ptr()
+            j.workspace, j.workspace_bytes = ws.data_ptr(), wsb
+            keep += [x, ws]
+            res.append((out[:cap] if cap < n else out, count))
+        nat.check(lib.hgd_unique_dev_group(jobs, len(chunk), nat.stream_handle(dev)),
+                  "hgd_unique_dev_group")
+    return res
 
 
 def _mm_ok(H: torch.Tensor, X: torch.Tensor) -> bool:

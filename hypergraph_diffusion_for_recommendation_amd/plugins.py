@@ -45,8 +45,8 @@ from torch.optim.lr_scheduler import ReduceLROnPlateau
 
 from .encoders import (HCCFDiffusionEncoder, HCCFEncoder, LocalAwareEncoder,
                        LocalAwareEncoderHD3, sparse_tensor_of)
-from .functional import (bpr_index_errors, bpr_loss_rows, contrast_loss, contrast_loss_pair,
-                         split_rows, unique_long, unique_long_n)
+from .functional import (bpr_index_errors, bpr_loss_rows, contrast_loss, contrast_loss_layers,
+                         split_rows, unique_long, unique_long_n, unique_long_n_group)
 from .layers import HGCNConv, SpAdjDropEdge
 from .sampler import next_batch_pairwise
 from .selfrec import GraphRecommender, early_stopping
@@ -144,17 +144,17 @@ class HCCF(GraphRecommender):
         # and with device drop-edge masks, capacity-sized with the count kept on the device)
         dropper = getattr(getattr(self, "model", None), "edgeDropper", None)
         if getattr(self, "graph_mode", False) or getattr(dropper, "capture_safe", False):
-            (u_nodes, u_cnt) = unique_long_n(ancs, nu)
-            (p_nodes, p_cnt) = unique_long_n(poss, self.data.n_items)
+            (u_nodes, u_cnt), (p_nodes, p_cnt) = unique_long_n_group(
+                [ancs, poss], [nu, self.data.n_items])  # both lists in one launch per kernel
         else:
             u_nodes, p_nodes = unique_long(ancs), unique_long(poss)
             u_cnt = p_cnt = None
-        sslLoss = 0
-        for i in range(self.nLayers):
-            embeds1 = gcnEmbedsLst[i].detach()
-            embeds2 = hyperEmbedsLst[i]
-            sslLoss += contrast_loss_pair(embeds1, embeds2, nu, u_nodes, p_nodes, self.temp,
-                                          u_cnt, p_cnt)
+        # every layer's user and item terms (embeds1 = gcnEmbedsLst[i].detach(), embeds2 =
+        # hyperEmbedsLst[i]) as one op: one launch per kernel for the whole loop when the node
+        # counts are on the device (functional.contrast_loss_layers)
+        sslLoss = contrast_loss_layers([gcnEmbedsLst[i].detach() for i in range(self.nLayers)],
+                                       [hyperEmbedsLst[i] for i in range(self.nLayers)], nu,
+                                       u_nodes, p_nodes, self.temp, u_cnt, p_cnt)
         sslLoss *= self.ss_rate
         return sslLoss
 

@@ -438,7 +438,9 @@ hgd_status hgd_infonce_backward_n(const float* P1, const float* P2, const float*
  * (batch_count NULL = all `capacity` rows live), with its own workspace
  * (hgd_infonce_workspace_size(capacity, d)). Backward outputs: dX1 / dX2 compact [capacity, d]
  * rows, or dE1 / dE2 scatter-adds into [n_rows, ld] tables (nodes required); a side without an
- * output is skipped. count is 1 or 2; all terms share d and temp. */
+ * output is skipped. count is 1 to 8 (HCCF: the user and item terms of up to four layers, one
+ * launch per kernel for the whole step's InfoNCE); all terms share d, temp and — backward —
+ * grad_loss (the group's loss is the sum of its terms' losses). */
 typedef struct hgd_infonce_term {
   const float* E1;
   int64_t ld1;
@@ -694,6 +696,25 @@ hgd_status hgd_unique_dev_i64(const int64_t* keys, int64_t n, int64_t* out, int6
                               void* workspace, size_t workspace_bytes, void* stream);
 hgd_status hgd_unique_dev_trunc_f32(const float* x, int64_t n, int64_t* out, int64_t* n_out,
                                     void* workspace, size_t workspace_bytes, void* stream);
+
+/* Several lists through the device-complete path at once (HCCF's anchor and positive node
+ * lists, HCCF.py:65-66): one launch per kernel for all of them, each list's out / n_out exactly
+ * as hgd_unique_dev_i64 / hgd_unique_dev_trunc_f32 give it. Per list: exactly one of x_f32
+ * (truncated like Tensor.long()) and x_i64, and its own workspace of
+ * hgd_unique_workspace_size(n) bytes. `capacity` (0 = n): *n_out is clamped to it and
+ * out[*n_out, capacity) zeroed — a fixed-size list whose live count stays on the device (the
+ * capacity-sized node lists HCCF's InfoNCE reads). count is 1 to 4. */
+typedef struct hgd_unique_job {
+  const float* x_f32;
+  const int64_t* x_i64;
+  int64_t n;
+  int64_t capacity;
+  int64_t* out;
+  int64_t* n_out;
+  void* workspace;
+  size_t workspace_bytes;
+} hgd_unique_job;
+hgd_status hgd_unique_dev_group(const hgd_unique_job* jobs, int32_t count, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * BPR loss from the embedding table (util/loss_torch.py:5-9 over the rows HCCF.py:84-86

@@ -49,9 +49,10 @@ def main():
     from hypergraph_diffusion_for_recommendation_amd.encoders import HCCFEncoder
     from hypergraph_diffusion_for_recommendation_amd.functional import (bpr_loss_rows,
                                                                          contrast_loss,
-                                                                         contrast_loss_pair,
+                                                                         contrast_loss_layers,
                                                                          unique_long,
-                                                                         unique_long_n)
+                                                                         unique_long_n,
+                                                                         unique_long_n_group)
     from hypergraph_diffusion_for_recommendation_amd.graphs import CapturedStep
 
     dev = torch.device("cuda")
@@ -88,16 +89,18 @@ def main():
                 bpr = R.bpr_loss(anc, pos, neg)
             ssl = 0
             # the reference recomputes torch.unique(·.long()) per layer; ours hoists it (same value)
-            un = (unique(anc, nu), unique(pos, ni)) if hoist else None
-            for layer in range(args.layers):
+            if counted:  # both node lists in one launch per kernel (the plugin's ssl_loss)
+                un = tuple(unique_long_n_group([anc, pos], [nu, ni]))
+            else:
+                un = (unique(anc, nu), unique(pos, ni)) if hoist else None
+            if counted:  # (nodes, device count) pairs: every layer's both halves in one op
+                ssl = contrast_loss_layers([t.detach() for t in gcn], hyp, nu, un[0][0],
+                                           un[1][0], temp, un[0][1], un[1][1])
+            for layer in range(0 if counted else args.layers):
                 e1, e2 = gcn[layer].detach(), hyp[layer]
                 nu_nodes, np_nodes = un if hoist else (unique(anc, nu), unique(pos, ni))
-                if counted:  # (nodes, device count) pairs: both halves in one op
-                    ssl = ssl + contrast_loss_pair(e1, e2, nu, nu_nodes[0], np_nodes[0], temp,
-                                                   nu_nodes[1], np_nodes[1])
-                else:
-                    ssl = ssl + loss_fn(e1[:nu], e2[:nu], nu_nodes, temp) \
-                        + loss_fn(e1[nu:], e2[nu:], np_nodes, temp)
+                ssl = ssl + loss_fn(e1[:nu], e2[:nu], nu_nodes, temp) \
+                    + loss_fn(e1[nu:], e2[nu:], np_nodes, temp)
             loss = bpr + cl_rate * ssl
             opt.zero_grad()
             torch.nn.utils.clip_grad_norm_(model.parameters(), 4)  # before backward, as HCCF.py:95

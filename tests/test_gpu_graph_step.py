@@ -211,19 +211,43 @@ def test_contrast_loss_pair_equals_two_calls(dev):
     assert torch.equal(a.grad, b.grad)
 
 
+@pytest.mark.parametrize("L", [1, 3, 5])
+def test_contrast_loss_layers_equals_per_layer_pairs(dev, L):
+    """contrast_loss_layers (all 2·L InfoNCE terms of a step in one launch per kernel, up to four
+    layers per group) against the per-layer contrast_loss_pair loop it replaces: every layer's
+    table gradient bitwise, the summed loss within one rounding of each addend (the group
+    sums the 2·L term losses in one reduction)."""
+    from hypergraph_diffusion_for_recommendation_amd.functional import (contrast_loss_layers,
+                                                                         contrast_loss_pair,
+                                                                         unique_long_n)
+    g = torch.Generator(device=dev).manual_seed(20 + L)
+    U, N, d = 700, 1900, 64
+    E1s = [torch.randn(N, d, device=dev, generator=g) for _ in range(L)]
+    E2s = [torch.randn(N, d, device=dev, generator=g) for _ in range(L)]
+    un, uc = unique_long_n(torch.randint(-40, 400, (300,), device=dev, generator=g))
+    pn, pc = unique_long_n(torch.randint(0, 1200, (500,), device=dev, generator=g))
+    a = [e.clone().requires_grad_(True) for e in E2s]
+    la = contrast_loss_layers(E1s, a, U, un, pn, 0.3, uc, pc)
+    la.backward()
+    b = [e.clone().requires_grad_(True) for e in E2s]
+    terms = [contrast_loss_pair(e1, e2, U, un, pn, 0.3, uc, pc) for e1, e2 in zip(E1s, b)]
+    lb = sum(terms)
+    lb.backward()
+    assert abs(float(la) - float(lb)) <= 4 * L * 1.2e-7 * sum(abs(float(t)) for t in terms)
+    for x, y in zip(a, b):
+        assert torch.equal(x.grad, y.grad)
+
+
 def _step_fn(enc, opt, U, temp=1.0, cl=0.01):
     from hypergraph_diffusion_for_recommendation_amd.functional import (bpr_loss_rows,
-                                                                         contrast_loss_pair,
+                                                                         contrast_loss_layers,
                                                                          unique_long_n)
 
     def step(u, i, j):
         ue, ie, gcn, hyp = enc(keep_rate=0.7)
         bpr, anc, pos = bpr_loss_rows(ue, ie, u, i, j)  # the plugin's fused BPR
         (un, uc), (pn, pc) = unique_long_n(anc), unique_long_n(pos)
-        ssl = 0
-        for layer in range(enc.n_layers):
-            e1, e2 = gcn[layer].detach(), hyp[layer]
-            ssl = ssl + contrast_loss_pair(e1, e2, U, un, pn, temp, uc, pc)
+        ssl = contrast_loss_layers([t.detach() for t in gcn], hyp, U, un, pn, temp, uc, pc)
         loss = bpr + ssl * cl
         opt.zero_grad()
         loss.backward()

@@ -123,3 +123,49 @@ def test_device_complete_unique_of_floats(dev):
     want = _ref(y)  # the host cast maps NaN to INT64_MIN too
     assert want[0] == -2**63
     assert torch.equal(_dev_unique(y).cpu(), want)
+
+
+def test_device_unique_group_equals_single_lists(dev):
+    """hgd_unique_dev_group (functional.unique_long_n_group: several lists per launch, HCCF's
+    anchor and positive lists): each list's nodes and count bitwise as unique_long_n gives them
+    one at a time — float and int64 lists mixed, different sizes, a far-key list, a NaN list,
+    a capacity cut by n_rows (count clamped, tail zero) and more lists than one group holds."""
+    from hypergraph_diffusion_for_recommendation_amd.functional import (unique_long_n,
+                                                                         unique_long_n_group)
+    g = torch.Generator(device=dev).manual_seed(5)
+    emb = torch.randn(4096, 64, device=dev, generator=g) * 3.0
+    nan = emb.clone()
+    nan[1, 2] = float("nan")
+    ids = torch.randint(-50, 900, (5000,), device=dev, generator=g)
+    far = torch.tensor([3, 3 + (1 << 30), 9, -(1 << 40)], device=dev)
+    xs = [emb, ids, nan, far, emb[:100], ids[:7]]
+    rows = [None, 900, None, None, 4, None]   # emb[:100] has ~13 distinct ids > 2·4: cut to 8
+    got = unique_long_n_group(xs, rows)
+    for k, (x, r) in enumerate(zip(xs, rows)):
+        want_n, want_c = _single(x, r)
+        assert torch.equal(unique_long_n(x, r)[0], want_n), k
+        n, c = got[k]
+        assert torch.equal(n, want_n) and torch.equal(c, want_c), k
+        live = int(c)
+        assert not n[live:].any(), k
+
+
+def _single(x, n_rows):
+    """The round-3 unique_long_n: the single-list C entry point, the clamp and the zeroed tail
+    done by torch ops — the reference the grouped path must reproduce."""
+    from hypergraph_diffusion_for_recommendation_amd import _native as nat
+    lib = nat.load()
+    x = x.detach().contiguous().view(-1)
+    n = x.numel()
+    out = torch.empty(n, dtype=torch.int64, device=x.device)
+    wsb = lib.hgd_unique_workspace_size(n)
+    buf = torch.empty(256 + wsb, dtype=torch.uint8, device=x.device)
+    fn = lib.hgd_unique_dev_trunc_f32 if x.dtype == torch.float32 else lib.hgd_unique_dev_i64
+    nat.check(fn(x.data_ptr(), n, out.data_ptr(), buf.data_ptr(), buf.data_ptr() + 256, wsb,
+                 nat.stream_handle(x.device)), "hgd_unique_dev")
+    count = buf[:8].view(torch.int64).clone()
+    cap = n if n_rows is None else max(1, min(n, 2 * int(n_rows)))
+    out = out[:cap]
+    count = torch.clamp_max(count, cap)
+    live = torch.arange(cap, device=x.device) < count
+    return torch.where(live, out, torch.zeros((), dtype=torch.int64, device=x.device)), count
