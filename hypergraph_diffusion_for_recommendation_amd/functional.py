@@ -778,7 +778,7 @@ class _ContrastLossLayers(torch.autograd.Function):
                 t.loss = losses.data_ptr() + 4 * (2 * layer + k)
                 t.workspace, t.workspace_bytes = ws.data_ptr(), wsb
                 saved += [P1, P2, inv1, inv2, deno]
-                keep.append(ws)
+                keep += [ws, pos]  # alive until the launch: a later term must not reuse them
         nat.check(lib.hgd_infonce_forward_group(terms, 2 * L, d, float(temp),
                                                 nat.stream_handle(dev)),
                   "hgd_infonce_forward_group")
