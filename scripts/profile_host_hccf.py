@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
-"""cProfile of eager HCCF training steps (encoders.HCCFEncoder with the device drop-edge mask,
-fused BPR + InfoNCE, Adam) at the Yelp shape: where the host time of the eager path goes."""
+"""cProfile of eager HCCF training steps at the Yelp shape — the plugins' eager default
+(encoders.HCCFEncoder with masked drop-edge views on the reference's CPU mask stream, fused BPR,
+the grouped unique and InfoNCE with device counts, the reference's Adam): where the host time of
+the eager path goes."""
 import cProfile
 import os
 import pstats
@@ -19,8 +21,8 @@ def main():
     import refops as R
     from hypergraph_diffusion_for_recommendation_amd.encoders import HCCFEncoder
     from hypergraph_diffusion_for_recommendation_amd.functional import (bpr_loss_rows,
-                                                                         contrast_loss_pair,
-                                                                         unique_long)
+                                                                         contrast_loss_layers,
+                                                                         unique_long_n_group)
     dev = torch.device("cuda")
     nu, ni = 31_668, 38_048
     u, i = R.synthetic_incidence(nu, ni, 1_237_259, seed=0)
@@ -30,7 +32,7 @@ def main():
                 embedding_size=64, hyper_dim=32, drop_rate=0.5, p=0.1, n_layers=3)
     torch.manual_seed(0)
     model = HCCFEncoder(conf, data, dev)
-    model.edgeDropper.device_rng = True
+    model.edgeDropper.capture_safe = True  # the plugins' default (device_rng off)
     opt = torch.optim.Adam(model.parameters(), lr=0.001)
     g = torch.Generator(device=dev).manual_seed(0)
     uid, pid, nid = (torch.randint(0, n, (4096,), device=dev, generator=g) for n in (nu, ni, ni))
@@ -38,10 +40,8 @@ def main():
     def step():
         ue, ie, gcn, hyp = model(keep_rate=0.5)
         bpr, anc, pos = bpr_loss_rows(ue, ie, uid, pid, nid)
-        un, pn = unique_long(anc), unique_long(pos)
-        ssl = 0
-        for k in range(3):
-            ssl = ssl + contrast_loss_pair(gcn[k].detach(), hyp[k], nu, un, pn, 0.2)
+        (un, uc), (pn, pc) = unique_long_n_group([anc, pos], [nu, ni])
+        ssl = contrast_loss_layers([t.detach() for t in gcn], hyp, nu, un, pn, 0.2, uc, pc)
         loss = bpr + 1e-4 * ssl
         opt.zero_grad()
         torch.nn.utils.clip_grad_norm_(model.parameters(), 4)
@@ -62,7 +62,9 @@ def main():
         step()
     torch.cuda.synchronize()
     pr.disable()
-    pstats.Stats(pr).sort_stats("tottime").print_stats(30)
+    st = pstats.Stats(pr)
+    st.sort_stats("tottime").print_stats(30)
+    st.sort_stats("cumulative").print_stats(40)
 
 
 if __name__ == "__main__":
