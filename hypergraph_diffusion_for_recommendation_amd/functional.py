@@ -751,47 +751,59 @@ class _ContrastLossLayers(torch.autograd.Function):
         dev = tables[0].device
         d = tables[0].shape[1]
         N = tables[0].shape[0]
-        f = dict(dtype=torch.float32, device=dev)
-        losses = torch.empty(2 * L, **f)
-        terms = (nat.InfonceTerm * (2 * L))()
-        saved, keep = [], []
         halves = []
         for r0, rows, nodes, count in ((0, nu, nodes_u, count_u), (nu, N - nu, nodes_i, count_i)):
             halves.append((r0, rows, nodes.to(device=dev, dtype=torch.int64).contiguous(), count))
+        # every term's operands in ONE float buffer and every workspace in ONE byte buffer (an
+        # eager step otherwise made ~40 allocator calls here): the term losses first, then per
+        # term P1, P2 [B, d] and inv1, inv2, pos_logit, deno [B], each at a 256-byte boundary
+        offs, cur = [], _al64(2 * L)
+        for layer in range(L):
+            for _r0, _rows, nodes, _c in halves:
+                B = nodes.numel()
+                o = {}
+                for name, size in (("P1", B * d), ("P2", B * d), ("inv1", B), ("inv2", B),
+                                   ("pos", B), ("deno", B)):
+                    o[name] = cur
+                    cur += _al64(size)
+                offs.append(o)
+        buf = torch.empty(cur, dtype=torch.float32, device=dev)
+        wsbs = [lib.hgd_infonce_workspace_size(h[2].numel(), d) for h in halves]
+        wsbuf = torch.empty(max(1, L * sum(_al256(w) for w in wsbs)), dtype=torch.uint8,
+                            device=dev)
+        fp, wp = buf.data_ptr(), wsbuf.data_ptr()
+        terms = (nat.InfonceTerm * (2 * L))()
+        keep = []
         for layer in range(L):
             E1c, E2c = tables[2 * layer].contiguous(), tables[2 * layer + 1].contiguous()
             keep += [E1c, E2c]
             for k, (r0, rows, nodes, count) in enumerate(halves):
-                B = nodes.numel()
-                P1, P2 = torch.empty((B, d), **f), torch.empty((B, d), **f)
-                inv1, inv2, pos, deno = (torch.empty(B, **f) for _ in range(4))
-                wsb = lib.hgd_infonce_workspace_size(B, d)
-                ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+                o = offs[2 * layer + k]
                 t = terms[2 * layer + k]
                 off = r0 * d * 4
                 t.E1, t.ld1, t.E2, t.ld2 = E1c.data_ptr() + off, d, E2c.data_ptr() + off, d
-                t.n_rows, t.nodes, t.capacity, t.batch_count = rows, nodes.data_ptr(), B, \
-                    count.data_ptr()
-                t.P1, t.P2, t.inv_norm1, t.inv_norm2 = (P1.data_ptr(), P2.data_ptr(),
-                                                        inv1.data_ptr(), inv2.data_ptr())
-                t.pos_logit, t.deno = pos.data_ptr(), deno.data_ptr()
-                t.loss = losses.data_ptr() + 4 * (2 * layer + k)
-                t.workspace, t.workspace_bytes = ws.data_ptr(), wsb
-                saved += [P1, P2, inv1, inv2, deno]
-                keep += [ws, pos]  # alive until the launch: a later term must not reuse them
+                t.n_rows, t.nodes, t.capacity, t.batch_count = rows, nodes.data_ptr(), \
+                    nodes.numel(), count.data_ptr()
+                t.P1, t.P2 = fp + 4 * o["P1"], fp + 4 * o["P2"]
+                t.inv_norm1, t.inv_norm2 = fp + 4 * o["inv1"], fp + 4 * o["inv2"]
+                t.pos_logit, t.deno = fp + 4 * o["pos"], fp + 4 * o["deno"]
+                t.loss = fp + 4 * (2 * layer + k)
+                t.workspace, t.workspace_bytes = wp, wsbs[k]
+                wp += _al256(wsbs[k])
         nat.check(lib.hgd_infonce_forward_group(terms, 2 * L, d, float(temp),
                                                 nat.stream_handle(dev)),
                   "hgd_infonce_forward_group")
         ctx.temp = float(temp)
-        ctx.nu, ctx.N, ctx.d, ctx.L = nu, N, d, L
-        ctx.save_for_backward(halves[0][2], count_u, halves[1][2], count_i, *saved)
+        ctx.nu, ctx.N, ctx.d, ctx.L, ctx.offs, ctx.wsbs = nu, N, d, L, offs, wsbs
+        ctx.save_for_backward(halves[0][2], count_u, halves[1][2], count_i, buf)
+        losses = buf[:2 * L]
         return losses.sum() if L > 1 else losses[0] + losses[1]
 
     @staticmethod
     def backward(ctx, g):
         lib = nat.load()
-        nodes_u, count_u, nodes_i, count_i, *saved = ctx.saved_tensors
-        dev = saved[0].device
+        nodes_u, count_u, nodes_i, count_i, buf = ctx.saved_tensors
+        dev = buf.device
         nu, N, d, L = ctx.nu, ctx.N, ctx.d, ctx.L
         g = g.to(dtype=torch.float32).reshape(1).contiguous()
         f = dict(dtype=torch.float32, device=dev)
@@ -800,33 +812,40 @@ class _ContrastLossLayers(torch.autograd.Function):
         none = (None,) * 6
         if all(x is None for x in grads):
             return none + tuple(grads)
+        wsbuf = torch.empty(max(1, L * sum(_al256(w) for w in ctx.wsbs)), dtype=torch.uint8,
+                            device=dev)
+        fp, wp = buf.data_ptr(), wsbuf.data_ptr()
         terms = (nat.InfonceTerm * (2 * L))()
-        keep = []
         for layer in range(L):
             dE1, dE2 = grads[2 * layer], grads[2 * layer + 1]
             for k, (r0, rows, nodes, count) in enumerate(((0, nu, nodes_u, count_u),
                                                           (nu, N - nu, nodes_i, count_i))):
-                P1, P2, inv1, inv2, deno = saved[5 * (2 * layer + k): 5 * (2 * layer + k) + 5]
-                B = P1.shape[0]
-                wsb = lib.hgd_infonce_workspace_size(B, d)
-                ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
-                keep.append(ws)
+                o = ctx.offs[2 * layer + k]
                 t = terms[2 * layer + k]
                 off = r0 * d * 4
-                t.n_rows, t.nodes, t.capacity, t.batch_count = rows, nodes.data_ptr(), B, \
-                    count.data_ptr()
-                t.P1, t.P2, t.inv_norm1, t.inv_norm2 = (P1.data_ptr(), P2.data_ptr(),
-                                                        inv1.data_ptr(), inv2.data_ptr())
-                t.deno = deno.data_ptr()
+                t.n_rows, t.nodes, t.capacity, t.batch_count = rows, nodes.data_ptr(), \
+                    nodes.numel(), count.data_ptr()
+                t.P1, t.P2 = fp + 4 * o["P1"], fp + 4 * o["P2"]
+                t.inv_norm1, t.inv_norm2 = fp + 4 * o["inv1"], fp + 4 * o["inv2"]
+                t.deno = fp + 4 * o["deno"]
                 if dE1 is not None:
                     t.dE1, t.ldE1 = dE1.data_ptr() + off, d
                 if dE2 is not None:
                     t.dE2, t.ldE2 = dE2.data_ptr() + off, d
-                t.workspace, t.workspace_bytes = ws.data_ptr(), wsb
+                t.workspace, t.workspace_bytes = wp, ctx.wsbs[k]
+                wp += _al256(ctx.wsbs[k])
         nat.check(lib.hgd_infonce_backward_group(terms, 2 * L, d, ctx.temp, g.data_ptr(),
                                                  nat.stream_handle(dev)),
                   "hgd_infonce_backward_group")
         return none + tuple(grads)
+
+
+def _al64(n: int) -> int:
+    return -(-int(n) // 64) * 64
+
+
+def _al256(n: int) -> int:
+    return -(-int(n) // 256) * 256
 
 
 _NCE_MAX_LAYERS = 4  # 2 terms per layer, hgd_infonce_*_group takes up to 8
