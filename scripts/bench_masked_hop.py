@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""One drop-edge hop of HCCF's GCN layer (HCCF.py:199, torch.sparse.mm(adj, E) on the edge-dropped
+Yelp-shaped norm_adj, d = 64) three ways, event-timed medians:
+
+* full       — the parent adjacency, nothing dropped (every edge gathered);
+* masked     — the masked view (hgd_spmm_masked: every parent edge's index read, the kept ones
+               compacted per lane group and gathered) — the plugins' default;
+* compacted  — the compacted child (Incidence.drop): only kept edges stored.
+
+Prints one JSON line."""
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+
+
+def main():
+    import torch
+
+    import refops as R
+    from hypergraph_diffusion_for_recommendation_amd.incidence import Incidence, spmm_csr
+    dev = torch.device("cuda")
+    nu, ni, d, keep = 31_668, 38_048, 64, 0.5
+    u, i = R.synthetic_incidence(nu, ni, 1_237_259, seed=0)
+    A = R.normalize_graph_mat(R.bipartite_adjacency(u, i, nu, ni)).tocoo()
+    idx = torch.from_numpy(__import__("numpy").stack([A.row, A.col]).astype("int64"))
+    val = torch.from_numpy(A.data.astype("float32"))
+    inc = Incidence.from_coo(idx, val, A.shape, device=dev)
+    X = torch.randn(A.shape[1], d, device=dev)
+    g = torch.Generator(device=dev).manual_seed(0)
+    mask = (torch.rand(inc.nnz, device=dev, generator=g) < keep).to(torch.uint8)
+    view = inc.masked(mask, keep)
+    child = inc.drop(mask, keep)
+
+    def timed(fn, reps=200):
+        for _ in range(10):
+            fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1e3)
+        return round(statistics.median(ts), 2)
+
+    out = {"nnz": inc.nnz, "kept": child.nnz, "d": d}
+    for name, m in (("full", inc), ("masked", view), ("compacted", child)):
+        out[f"{name}_us"] = timed(lambda m=m: spmm_csr(m.csr, X, m.val))
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
