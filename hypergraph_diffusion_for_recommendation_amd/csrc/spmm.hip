@@ -50,6 +50,7 @@ struct SpmmArgs {
   // val[e] / keep (IEEE, as the dropped COO's values)
   const uint8_t* mask;
   float keep;
+  int32_t mask_pair;  // two-batch masked walk (HGD_TUNE_MASK_PAIR)
 };
 
 __device__ __forceinline__ float epilogue(float y, int epi, float slope) {
@@ -180,6 +181,90 @@ __device__ __forceinline__ int compact_kept(const SpmmArgs& a, int l, int keep, 
   return __popcll(gm);
 }
 
+// The masked hop's walk (MASK): TWO index batches of G edges per step (2G edges, about G kept
+// at keep = 0.5), their kept entries packed in edge order into 2G slots — slot j < G in lane j's
+// register a, slot j >= G in lane j-G's register b — so a step gathers as many rows as an
+// unmasked batch instead of half as many; the next pair of index batches is loaded before the
+// gathers are issued. Sums in edge order: bitwise the one-batch walk and the compacted matrix's.
+template <int G, int VEC, int U, bool HAS_VAL, int POL>
+__device__ __forceinline__ void gather_sum_mask2(const SpmmArgs& a, int64_t e0, int64_t e1,
+                                                 int l, bool col_ok, float (&acc)[VEC]) {
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) acc[i] = 0.f;
+  const int64_t coff = static_cast<int64_t>(a.col0) + static_cast<int64_t>(l) * VEC;
+  const int base = (static_cast<int>(threadIdx.x) & 63) & ~(G - 1);
+  auto group_bits = [&](int keep) {
+    const unsigned long long bal = __ballot(keep != 0);
+    return G == 64 ? bal : (bal >> base) & ((1ull << (G == 64 ? 0 : G)) - 1ull);
+  };
+  auto load2 = [&](int64_t eb, int& c1, float& w1, int& k1, int& c2, float& w2, int& k2) {
+    load_index<HAS_VAL, POL, true>(a, eb, static_cast<int>(min(static_cast<int64_t>(G), e1 - eb)),
+                                   l, c1, w1, k1);
+    const int64_t eb2 = eb + G;
+    if (eb2 < e1) {
+      load_index<HAS_VAL, POL, true>(
+          a, eb2, static_cast<int>(min(static_cast<int64_t>(G), e1 - eb2)), l, c2, w2, k2);
+    } else {
+      c2 = 0;
+      w2 = 1.f;
+      k2 = 0;
+    }
+  };
+  int nc1 = 0, nk1 = 0, nc2 = 0, nk2 = 0;
+  float nw1 = 1.f, nw2 = 1.f;
+  if (e0 < e1) load2(e0, nc1, nw1, nk1, nc2, nw2, nk2);
+  for (int64_t eb = e0; eb < e1; eb += 2 * G) {
+    const int c1 = nc1, k1 = nk1, c2 = nc2, k2 = nk2;
+    const float w1 = nw1, w2 = nw2;
+    if (eb + 2 * G < e1) load2(eb + 2 * G, nc1, nw1, nk1, nc2, nw2, nk2);
+    const unsigned long long gm1 = group_bits(k1), gm2 = group_bits(k2);
+    const int n1 = __popcll(gm1), n = n1 + __popcll(gm2);
+    if (n == 0) continue;  // group-uniform
+    // slot l (register a) and slot l + G (register b) of the packed pair
+    const int s1 = nth_set_bit<G>(gm1, l);
+    const int s2a = nth_set_bit<G>(gm2, l >= n1 ? l - n1 : 0);
+    const int s2b = nth_set_bit<G>(gm2, l + G - n1 < G ? l + G - n1 : 0);
+    const int ca1 = __shfl(c1, s1, G), ca2 = __shfl(c2, s2a, G), cb = __shfl(c2, s2b, G);
+    const int ca = l < n1 ? ca1 : ca2;
+    float wa = 1.f, wb = 1.f;
+    if constexpr (HAS_VAL) {
+      const float wa1 = __shfl(w1, s1, G), wa2 = __shfl(w2, s2a, G);
+      wa = __fdiv_rn(l < n1 ? wa1 : wa2, a.keep);  // vals[mask] / keepRate (HCCF.py:224)
+      wb = __fdiv_rn(__shfl(w2, s2b, G), a.keep);
+    }
+    for (int k = 0; k < n; k += U) {
+      const bool hi = k >= G;  // group-uniform: U divides G, so a step stays in one register
+      float xv[U][VEC];
+      float w[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int kk = k + u;
+        const int c = __shfl(hi ? cb : ca, kk & (G - 1), G);
+        if constexpr (HAS_VAL) w[u] = __shfl(hi ? wb : wa, kk & (G - 1), G);
+        if (kk < n && col_ok) {
+          load_vec<VEC, (POL & kPolNtGather) != 0>(a.X + static_cast<int64_t>(c) * a.ldx + coff,
+                                                   xv[u]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < VEC; ++i) xv[u][i] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (k + u < n) {
+#pragma unroll
+          for (int i = 0; i < VEC; ++i) {
+            if constexpr (HAS_VAL)
+              acc[i] = fmaf(w[u], xv[u][i], acc[i]);
+            else
+              acc[i] += xv[u][i];
+          }
+        }
+      }
+    }
+  }
+}
+
 // Σ_{e in [e0,e1)} val[e] * X[col[e], cols of this lane], in edge order. With kPolPrefetch the
 // index batch b+1 is loaded before the gathers of batch b are issued, so the dependent
 // index → gather round trip is paid once per row instead of once per batch of G nonzeros.
@@ -246,6 +331,21 @@ __device__ __forceinline__ void gather_sum(const SpmmArgs& a, int64_t e0, int64_
   }
 }
 
+int g_mask_pair = 1;  // HGD_TUNE_MASK_PAIR: the masked hop walks two index batches per step
+
+// MASK with G >= 8 lanes (U | G): the two-batch masked walk unless HGD_TUNE_MASK_PAIR is 0.
+template <int G, int VEC, int U, bool HAS_VAL, int POL, bool MASK>
+__device__ __forceinline__ void masked_or_plain_sum(const SpmmArgs& a, int64_t e0, int64_t e1,
+                                                    int l, bool col_ok, float (&acc)[VEC]) {
+  if constexpr (MASK && G >= 8 && G % U == 0) {
+    if (a.mask_pair) {
+      gather_sum_mask2<G, VEC, U, HAS_VAL, POL>(a, e0, e1, l, col_ok, acc);
+      return;
+    }
+  }
+  gather_sum<G, VEC, U, HAS_VAL, POL, MASK>(a, e0, e1, l, col_ok, acc);
+}
+
 template <int G, int VEC, int U, bool HAS_VAL, int POL, bool EX, bool MASK = false>
 __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
   constexpr int GPB = kBlock / G;
@@ -265,7 +365,7 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
     const int64_t re = a.rowptr[r + 1];
     const int64_t e0 = a.rowptr[r] + k * a.chunk;
     const int64_t e1 = min(e0 + static_cast<int64_t>(a.chunk), re);
-    gather_sum<G, VEC, U, HAS_VAL, POL, MASK>(a, e0, e1, l, col_ok, acc);
+    masked_or_plain_sum<G, VEC, U, HAS_VAL, POL, MASK>(a, e0, e1, l, col_ok, acc);
     if (col_ok) store_vec<VEC>(a.partial + t * a.d + coff, acc);
     return;
   }
@@ -276,7 +376,7 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
   const int64_t e0 = a.rowptr[r];
   const int64_t e1 = a.rowptr[r + 1];
   if (a.heavy_threshold > 0 && e1 - e0 > a.heavy_threshold) return;  // split-plan row
-  gather_sum<G, VEC, U, HAS_VAL, POL, MASK>(a, e0, e1, l, col_ok, acc);
+  masked_or_plain_sum<G, VEC, U, HAS_VAL, POL, MASK>(a, e0, e1, l, col_ok, acc);
   const float s = a.row_scale ? a.row_scale[r] : 1.f;
   finish_row<G, VEC, EX, (POL & kPolNtStore) != 0>(a, r, s, l, coff, col_ok, acc);
 }
@@ -604,6 +704,7 @@ hgd_status spmm_impl(const int64_t* rowptr, const int32_t* col, const float* val
   if (ex) a.ex = *ex;
   a.mask = mask;
   a.keep = keep;
+  a.mask_pair = g_mask_pair;
   if (plan && plan->threshold > 0 && plan->n_heavy > 0) {
     HGD_REQUIRE(plan->chunk > 0 && plan->heavy_rows && plan->heavy_cptr && plan->chunk_heavy,
                 "%s: incomplete split plan", fn);
@@ -785,6 +886,10 @@ extern "C" hgd_status hgd_set_tuning(int32_t key, int32_t value) {
     case HGD_TUNE_P2P_GRID:
       HGD_REQUIRE(value >= 0 && value <= 65536, "hgd_set_tuning: p2p grid must be 0..65536");
       set_p2p_grid(value);
+      return HGD_OK;
+    case HGD_TUNE_MASK_PAIR:
+      HGD_REQUIRE(value == 0 || value == 1, "hgd_set_tuning: mask pair must be 0 or 1");
+      g_mask_pair = value;
       return HGD_OK;
     case HGD_TUNE_CPU_RNG_THREADS:
       HGD_REQUIRE(value >= 0 && value <= 64, "hgd_set_tuning: cpu rng threads must be 0..64");

@@ -99,7 +99,9 @@ typedef enum hgd_epilogue {
  *                         barrier per 32-row stage, 1 = three LDS buffers with full / empty
  *                         counters (measured slower: 45.1 vs 41.5 µs at 144,242 x 128)
  *   HGD_TUNE_P2P_GRID:    workgroups of the peer exchange's reduce / gather kernels (0 = default
- *                         256: the links bound them, the hops they overlap need the CUs) */
+ *                         256: the links bound them, the hops they overlap need the CUs)
+ *   HGD_TUNE_MASK_PAIR:   the masked hop (hgd_spmm_masked*) walks two index batches per step
+ *                         (1, default) or one (0); the sums are the same bits either way */
 typedef enum hgd_tune_key {
   HGD_TUNE_SPMM_UNROLL = 1,
   HGD_TUNE_SPMM_POLICY = 2,
@@ -114,7 +116,8 @@ typedef enum hgd_tune_key {
   HGD_TUNE_P2P_CACHED = 11,
   HGD_TUNE_CPU_RNG_THREADS = 12,
   HGD_TUNE_X3P_QUEUE = 13,
-  HGD_TUNE_P2P_GRID = 14
+  HGD_TUNE_P2P_GRID = 14,
+  HGD_TUNE_MASK_PAIR = 15
 } hgd_tune_key;
 hgd_status hgd_set_tuning(int32_t key, int32_t value);
 
