@@ -21,9 +21,12 @@ touches the GPU) and exits with its status; under a launcher WORLD_SIZE must equ
 
 Rank 0 prints ONE JSON line. ``roofline`` prices the dominant kernel (hgd_spmm) from HIP events
 recorded around every hop launch on its stream during the timed steps, with SURVEY.md §8d's
-algorithmic bytes; ``cpu_baseline`` times the reference's own library calls (torch.sparse.mm +
-autograd on CPU, oracle/ref_cpu.py) on the same graph and tables as the GPU run (copied to the
-host), on this box's host cores.
+algorithmic bytes. At N = 1 the reference's own library calls (torch.sparse.mm + autograd on CPU,
+oracle/ref_cpu.py) run once on the FULL graph and tables of the GPU run (copied to the host):
+``parity`` compares one more GPU step with them row by row (the 1e-5 row bound; the script exits
+non-zero if it fails), and ``cpu_baseline`` times the same calls on a bounded prefix sample of
+the graph (median of 5 after 2 warm-ups) on this box's host cores. At N > 1 ``check`` compares
+every rank's rows with the single-GPU conv of the global graph (on by default).
 """
 from __future__ import annotations
 
@@ -53,7 +56,7 @@ WORKLOADS = {
 }
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -78,19 +81,22 @@ def parse():
                          "reduce over IPC-mapped buffers, sharded.P2PExchange); auto (default) "
                          "times both after the warm-up and runs the timed steps on the faster "
                          "(RCCL if the peer exchange fails or disagrees with it)")
-    ap.add_argument("--check", action="store_true",
+    ap.add_argument("--check", action=argparse.BooleanOptionalAction, default=None,
                     help="after timing, compare the sharded Y / dX with the single-GPU conv of "
-                         "the global graph (strong scaling) at the 1e-5 relative bound")
-    ap.add_argument("--cpu-budget-s", type=float, default=90.0,
-                    help="wall-clock budget of the CPU baseline's timed runs (after the warm-ups)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
+                         "the global graph (strong scaling) at the 1e-5 relative bound; on by "
+                         "default when N > 1 (--no-check to skip)")
+    ap.add_argument("--cpu-sample-frac", type=float, default=0.1,
+                    help="share of the users (a prefix of the row-sorted graph) the CPU "
+                         "baseline's timed runs cover; the parity gate always runs the full graph")
+    ap.add_argument("--no-cpu-baseline", action="store_true",
+                    help="skip the CPU reference: no cpu_baseline and no parity gate")
     ap.add_argument("--pmc", default="auto", choices=["auto", "on", "off"],
                     help="measure HBM traffic with rocprofv3 PMC passes in a child process")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--graph", default="off", choices=["on", "off"],
                     help="replay the fwd+bwd step as one captured hipGraph (measured: no gain "
                          "once the per-hop events are out of the timed loop)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def make_graph(U, I, E, seed, zipf, device):
@@ -110,63 +116,105 @@ def make_graph(U, I, E, seed, zipf, device):
     return torch.stack([key // I, key % I])
 
 
-def cpu_baseline(idx, X, dY, U, I, budget_s, d, label):
-    """oracle/ref_cpu.py (torch.sparse.mm + autograd, the reference's own calls) on the SAME
-    inputs as the GPU run — the headline graph and the X / dY tables, copied to the host
-    (SURVEY.md §8d "same run, same inputs"): one warm-up, then timed runs while the budget lasts
-    (at least one), median M-edges/s at torch's host threads; then one run at one thread."""
+def cpu_reference(idx, X, dY, U, I):
+    """The reference's own library calls (oracle/ref_cpu.py: torch.sparse.mm fwd + autograd bwd,
+    HCCF.py:199 on the data/graph.py:28-42 normalisation) on the FULL headline graph and the GPU
+    run's X / dY, copied to the host: (Y, dX, seconds). The outputs are the parity gate's
+    reference (BASELINE.md §3 "a speed-up is reported only if parity holds on the same run")."""
+    import torch
+
+    from oracle import ref_cpu
+    H = torch.sparse_coo_tensor(idx, torch.ones(int(idx.shape[1]), dtype=torch.float32), (U, I))
+    t0 = time.perf_counter()
+    Y, dX = ref_cpu.hgconv2_fwd_bwd(H, X, dY)
+    return Y, dX, time.perf_counter() - t0
+
+
+def row_parity(got, ref, block=1 << 20):
+    """The encoder-level rule of tests/_ref64.check_rows at any size: per row, max |got − ref|
+    over the row's largest |ref| (in float64, in blocks of rows); an all-zero reference row
+    must come out exactly zero. Returns (worst ratio, worst row, rows over 1e-5, zero-row
+    violations)."""
+    import torch
+    worst, where, over, zero_bad = 0.0, -1, 0, 0
+    for r0 in range(0, ref.shape[0], block):
+        g = got[r0:r0 + block].double()
+        r = ref[r0:r0 + block].double()
+        err = (g - r).abs().amax(1)
+        scale = r.abs().amax(1)
+        zero = scale == 0
+        zero_bad += int((err[zero] != 0).sum())
+        ratio = torch.where(zero, torch.zeros_like(err), err / torch.where(zero, 1.0, scale))
+        over += int((ratio > 1e-5).sum())
+        m = float(ratio.max()) if ratio.numel() else 0.0
+        if m > worst:
+            worst, where = m, r0 + int(ratio.argmax())
+    return worst, where, over, zero_bad
+
+
+def parity_gate(Y, dX, Y_ref, dX_ref, cpu_s):
+    """The GPU step's (Y, dX) — one eager step after timing, the same code the timed steps ran —
+    against the reference's torch.sparse.mm (Y, dX) on the same full-size inputs."""
+    out = {"ok": True, "bound": "per row: max|err| <= 1e-5 * max|ref| (tests/_ref64.check_rows)",
+           "reference": "oracle/ref_cpu.py torch.sparse.mm fwd+bwd, full graph, same X/dY",
+           "reference_s": round(cpu_s, 2)}
+    for name, got, ref in (("Y", Y, Y_ref), ("dX", dX, dX_ref)):
+        worst, row, over, zero_bad = row_parity(got, ref)
+        out[f"max_row_ratio_{name}"] = worst
+        out[f"rows_over_{name}"] = over + zero_bad
+        if over or zero_bad or got.shape != ref.shape:
+            out["ok"] = False
+            out[f"worst_row_{name}"] = row
+    out["rows"] = int(Y_ref.shape[0])
+    return out
+
+
+def cpu_baseline(idx, X, dY, U, I, d, label, full_s, frac=0.1):
+    """The CPU baseline's timing: the reference's calls
+    (oracle/ref_cpu.py) on a BOUNDED sample of the same workload — the users [0, U·frac) of the
+    GPU run's graph (a prefix of its row-sorted COO, every item kept) with their X / dY rows —
+    median of 5 runs after 2 warm-ups at torch's host threads, then one run at one thread. The
+    full-size run the parity gate made is reported beside it (``full_size``)."""
     import psutil
     import torch
 
     from oracle import ref_cpu
-    nnz = int(idx.shape[1])
-    t_setup = time.perf_counter()
-    H = torch.sparse_coo_tensor(idx, torch.ones(nnz, dtype=torch.float32), (U, I))
-    setup_s = time.perf_counter() - t_setup
-    # SURVEY §8d: the median of 5 after 2 warm-ups, as far as the budget allows. At the headline
-    # graph one fwd+bwd takes ≈ 50 s on the GPU box (torch.sparse.mm barely uses its threads), so
-    # there the first run is the sample (there is nothing to warm up: no JIT, no caches that
-    # outlast a 20 GB pass), which keeps the default bench.py run to a few minutes.
+    nnz_full = int(idx.shape[1])
+    Us = max(1, int(U * frac))
+    n = int(torch.searchsorted(idx[0].contiguous(), torch.tensor([Us])).item())
+    H = torch.sparse_coo_tensor(idx[:, :n], torch.ones(n, dtype=torch.float32), (Us, I))
+    Xs, dYs = X[:Us], dY[:Us]
+    for _ in range(2):
+        ref_cpu.hgconv2_fwd_bwd(H, Xs, dYs)
     times = []
-    t0 = time.perf_counter()
-    ref_cpu.hgconv2_fwd_bwd(H, X, dY)
-    first = time.perf_counter() - t0
-    if first > budget_s / 3:
-        times, warm = [first], 0
-    else:
-        warm = 1
-        if first < budget_s / 8:
-            ref_cpu.hgconv2_fwd_bwd(H, X, dY)
-            warm = 2
-        t_start = time.perf_counter()
-        while not times or (len(times) < 5 and time.perf_counter() - t_start < budget_s):
-            t0 = time.perf_counter()
-            ref_cpu.hgconv2_fwd_bwd(H, X, dY)
-            times.append(time.perf_counter() - t0)
+    for _ in range(5):
+        t0 = time.perf_counter()
+        ref_cpu.hgconv2_fwd_bwd(H, Xs, dYs)
+        times.append(time.perf_counter() - t0)
     t = statistics.median(times)
     ram = psutil.virtual_memory().total / 2**30
     out = {
-        "value": round(nnz / t / 1e6, 3),
+        "value": round(n / t / 1e6, 3),
         "unit": "M-edges/s",
         "cores": torch.get_num_threads(),
         "kind": "port",
-        "sample": (f"the headline workload itself ({label}: {U}x{I} graph, {nnz} edges, d={d}, "
-                   f"the GPU run's graph and X / dY copied to the host), torch.sparse.mm fwd+bwd "
-                   f"(oracle/ref_cpu.py), median of {len(times)} run(s) after {warm} warm-up(s), "
-                   f"{t:.2f} s/run; host RAM {ram:.0f} GiB"),
+        "sample": (f"users [0, {Us}) of the headline graph ({label}): {Us}x{I}, {n} edges, d={d}, "
+                   f"the GPU run's X / dY rows; torch.sparse.mm fwd+bwd (oracle/ref_cpu.py), "
+                   f"median of 5 after 2 warm-ups, {t:.2f} s/run; host RAM {ram:.0f} GiB"),
     }
-    # SURVEY.md §8d: also a 1-thread figure — one run of the same workload
     threads = torch.get_num_threads()
     torch.set_num_threads(1)
     try:
         t0 = time.perf_counter()
-        ref_cpu.hgconv2_fwd_bwd(H, X, dY)
+        ref_cpu.hgconv2_fwd_bwd(H, Xs, dYs)
         t1 = time.perf_counter() - t0
     finally:
         torch.set_num_threads(threads)
-    out["single_thread"] = {"value": round(nnz / t1 / 1e6, 3), "cores": 1,
-                            "sample": f"the same workload, one run, {t1:.2f} s"}
-    out["setup_s"] = round(setup_s, 2)
+    out["single_thread"] = {"value": round(n / t1 / 1e6, 3), "cores": 1,
+                            "sample": f"the same sample, one run, {t1:.2f} s"}
+    out["full_size"] = {"value": round(nnz_full / full_s / 1e6, 3), "cores": threads,
+                        "sample": f"the whole headline graph, {nnz_full} edges, one run "
+                                  f"(the parity gate's reference), {full_s:.2f} s"}
     return out
 
 
@@ -257,31 +305,48 @@ def choose_transport(sh, eager_step, device, phase, n=3):
     import torch.distributed as dist
 
     def timed():
+        """n steps between a barrier pair, max over ranks: (ms per step, error or None). A
+        failure on this rank alone (a poll that sees the error flag, a timed-out wait) is
+        recorded, never raised: every rank still reaches the same barrier and all-reduce, so
+        the collectives stay paired and agree() below decides on all ranks at once."""
+        err = None
         torch.cuda.synchronize()
         dist.barrier()
         t0 = time.perf_counter()
-        for _ in range(n):
-            eager_step()
-        if sh.transport == "p2p":
-            sh._p2p.wait()
-        torch.cuda.synchronize()
+        try:
+            for _ in range(n):
+                eager_step()
+            if sh.transport == "p2p":
+                sh._p2p.wait()
+                sh._p2p.check()
+        except Exception as e:  # noqa: BLE001 — reported through agree()
+            err = repr(e)[:400]
+        try:
+            torch.cuda.synchronize()  # a stalled exchange ends at its device wait bound
+        except Exception as e:  # noqa: BLE001
+            err = err or repr(e)[:400]
         dist.barrier()
         t = torch.tensor([(time.perf_counter() - t0) / n * 1e3], dtype=torch.float64,
                          device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
+        return float(t.item()), err
 
     out = {"steps_each": n}
-    sh.transport = "rccl"
-    Y_r, dX_r = eager_step()
-    Y_r, dX_r = Y_r.detach(), dX_r.detach()
-    out["rccl_ms_per_step"] = round(timed(), 4)
-    def agree(err):  # every rank learns whether any rank failed
+
+    def agree(err, key="p2p_error"):  # every rank learns whether any rank failed
         flag = torch.tensor([0 if err is None else 1], dtype=torch.int32, device=device)
         dist.all_reduce(flag, op=dist.ReduceOp.MAX)
         if err is not None:
-            out["p2p_error"] = err
+            out[key] = err
         return int(flag.item()) == 0
+
+    sh.transport = "rccl"
+    Y_r, dX_r = eager_step()
+    Y_r, dX_r = Y_r.detach(), dX_r.detach()
+    ms, rccl_err = timed()
+    if not agree(rccl_err, "rccl_error"):  # the all-reduce path itself failed: no fallback
+        raise RuntimeError(f"RCCL steps failed on some rank: {out.get('rccl_error')}")
+    out["rccl_ms_per_step"] = round(ms, 4)
 
     err = None
     try:  # one step, checked against RCCL's, before any collective timing
@@ -298,12 +363,10 @@ def choose_transport(sh, eager_step, device, phase, n=3):
         err = repr(e)[:400]
     ok = agree(err)
     if ok:
-        try:
-            out["p2p_ms_per_step"] = round(timed(), 4)
-            sh._p2p.check()
-        except Exception as e:  # noqa: BLE001
-            err = repr(e)[:400]
+        ms, err = timed()
         ok = agree(err)
+        if ok:
+            out["p2p_ms_per_step"] = round(ms, 4)
     use_p2p = ok and out.get("p2p_ms_per_step", float("inf")) < out["rccl_ms_per_step"]
     sh.transport = "p2p" if use_p2p else "rccl"
     out["chosen"] = sh.transport
@@ -374,6 +437,25 @@ def check_against_single_gpu(idx, U, I, X_global, dY_global, Y, dX, u0, u1):
     return out
 
 
+def check_enabled(args, world) -> bool:
+    """--check / --no-check; unset, an N > 1 record proves cross-device correctness by default."""
+    return world > 1 if args.check is None else bool(args.check)
+
+
+def gather_checks(check, world, shared_device):
+    """Every rank's check_against_single_gpu result → the line's ``check`` (on every rank)."""
+    import torch.distributed as dist
+    checks = [None] * world
+    dist.all_gather_object(checks, check)
+    return {"ok": all(c["Y"]["ok"] and c["dX"]["ok"] for c in checks),
+            "max_rel_err_Y": max(c["Y"]["max_rel_err"] for c in checks),
+            "max_rel_err_dX": max(c["dX"]["max_rel_err"] for c in checks),
+            "bound": "|err| <= 1e-5 * conv(|x|), per element",
+            "ranks_checked": world,
+            "wall_s": max(c.get("wall_s", 0.0) for c in checks),
+            "ranks_in_parallel": not shared_device}
+
+
 def main():
     args = parse()
     U0, I0, E0, zipf = WORKLOADS[args.workload]
@@ -392,12 +474,20 @@ def main():
               f"mislabelled run", file=sys.stderr)
         sys.exit(2)
     strong = args.scaling == "strong"
+    args.check = check_enabled(args, world)
     t_launch = time.perf_counter()
+
+    stall_s = float(os.environ.get("HGD_STALL_DUMP_S", "600"))
+    watchdog = [False]
 
     def phase(msg):  # multi-rank progress on stderr (rehearsals of N ranks on one device)
         if world > 1:
             print(f"[bench rank {rank}] {time.perf_counter() - t_launch:7.1f} s {msg}",
                   file=sys.stderr, flush=True)
+            if watchdog[0]:  # progress: the stall dump fires only HGD_STALL_DUMP_S after it
+                import faulthandler
+                faulthandler.cancel_dump_traceback_later()
+                faulthandler.dump_traceback_later(stall_s, exit=False)
 
     pmc = None
     pmc_note = None
@@ -429,10 +519,11 @@ def main():
 
     if world > 1:
         # a rank that stops making progress prints every thread's Python stack (the line it is
-        # blocked in) instead of dying silently at the launcher's limit
+        # blocked in) instead of dying silently at the launcher's limit; re-armed by every
+        # phase() line, so a long run that keeps reporting progress never dumps
         import faulthandler
-        faulthandler.dump_traceback_later(float(os.environ.get("HGD_STALL_DUMP_S", "600")),
-                                          exit=False)
+        faulthandler.dump_traceback_later(stall_s, exit=False)
+        watchdog[0] = True
     shard_kw = dict(n_chunks=args.chunks, P="sym", Q="mean", R="sym",
                     slice_width=args.slice_width,
                     transport="rccl" if args.transport == "auto" else args.transport,
@@ -547,13 +638,15 @@ def main():
         sh._p2p.check()  # no exchange timed out
     check = None
     if args.check and not args.pmc_child:
+        t_check = time.perf_counter()
         Y, dX = eager_step()
         Y = Y.detach()
         torch.cuda.synchronize()
         if keep_global:
-            # one rank at a time: the single-GPU reference of the global graph needs the whole
-            # [U, d] tables (10 GB each at d = 256), too much for N ranks sharing one device
-            for r in range(world):
+            # every rank recomputes the global conv on its own device at once; ranks sharing a
+            # device take turns (the single-GPU reference needs the whole [U, d] tables, 10 GB
+            # each at d = 256, too much for N ranks on one device)
+            for r in (range(world) if shared_device else [rank]):
                 if r == rank:
                     X_global = table_rows(0, U, d, seed_x, device, bound)
                     dY_global = table_rows(0, U, d, seed_x + 1, device)
@@ -563,8 +656,10 @@ def main():
                     torch.cuda.synchronize()
                     torch.cuda.empty_cache()
                     phase(f"checked: {check}")
-                dist.barrier()
+                if shared_device:
+                    dist.barrier()
             del idx
+            check["wall_s"] = round(time.perf_counter() - t_check, 2)
     per_rank = [{"rank": rank, "users": [u0, u1], "nnz": nnz, "hop_ms_per_step":
                  round(hop_ms_step, 4), "exposed_exchange_ms_per_step":
                  round(exposed_ms_step, 4)}]
@@ -576,12 +671,7 @@ def main():
         dist.all_gather_object(gathered, per_rank[0])
         per_rank = gathered
         if check is not None:
-            checks = [None] * world
-            dist.all_gather_object(checks, check)
-            check = {"ok": all(c["Y"]["ok"] and c["dX"]["ok"] for c in checks),
-                     "max_rel_err_Y": max(c["Y"]["max_rel_err"] for c in checks),
-                     "max_rel_err_dX": max(c["dX"]["max_rel_err"] for c in checks),
-                     "bound": "|err| <= 1e-5 * conv(|x|), per element"}
+            check = gather_checks(check, world, shared_device)
     total_edges = float(nnz_graph if strong else sum(r["nnz"] for r in per_rank))
     if strong and world > 1:
         assert sum(r["nnz"] for r in per_rank) == nnz_graph, "shards do not tile the graph"
@@ -642,13 +732,20 @@ def main():
         roofline["frac_by_traffic"] = round(pmc / (hop["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                                             4)
 
-    cpu = None
+    cpu = parity = None
     if want_cpu:
+        # the parity gate: one more eager step of the timed code, then the reference's own
+        # torch.sparse.mm fwd+bwd on the same full graph and tables, compared row by row
+        Yg, dXg = eager_step()
+        Yh, dXh = Yg.detach().cpu(), dXg.cpu()
         Xh, dYh = X.detach().cpu(), dY.cpu()
-        del X, dY
+        del X, dY, Yg, dXg
         torch.cuda.empty_cache()
-        cpu = cpu_baseline(idx_host, Xh, dYh, U, I, args.cpu_budget_s, d,
-                           f"{args.workload}-{U}x{I}x{E}-d{d}")
+        Y_ref, dX_ref, full_s = cpu_reference(idx_host, Xh, dYh, U, I)
+        parity = parity_gate(Yh, dXh, Y_ref, dX_ref, full_s)
+        del Yh, dXh, Y_ref, dX_ref
+        cpu = cpu_baseline(idx_host, Xh, dYh, U, I, d, f"{args.workload}-{U}x{I}x{E}-d{d}",
+                           full_s, args.cpu_sample_frac)
         del idx_host, Xh, dYh
 
     if world == 1:
@@ -701,18 +798,26 @@ def main():
                                                   for r in per_rank)
     if check is not None:
         out["check"] = check
+    if world == 1:
+        out["parity"] = parity
     print(json.dumps(out), flush=True)
+    if parity is not None and not parity["ok"]:
+        print(f"bench.py: PARITY FAILED against the reference's torch.sparse.mm on the same "
+              f"inputs: {parity}", file=sys.stderr, flush=True)
     if world > 1:
         dist.barrier()
         sh.close()
         dist.destroy_process_group()
-    finish(1 if check is not None and not check["ok"] else 0)
+    bad = (check is not None and not check["ok"]) or (parity is not None and not parity["ok"])
+    finish(1 if bad else 0)
 
 
 def finish(rc: int):
     """Exit status of a rank. A peer-exchange set-up call that never returned (the auto probe
     then chose RCCL) is still blocked on a daemon thread, and the HIP runtime's teardown at
     interpreter exit may wait for it: such a rank ends with os._exit once its output is out."""
+    import faulthandler
+    faulthandler.cancel_dump_traceback_later()
     from hypergraph_diffusion_for_recommendation_amd.sharded import p2p_setup_stuck
     if p2p_setup_stuck():
         print(f"bench.py: {p2p_setup_stuck()} peer-exchange set-up call(s) never returned; "

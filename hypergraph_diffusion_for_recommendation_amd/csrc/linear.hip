@@ -973,17 +973,21 @@ __global__ __launch_bounds__(X3P<MT>::THREADS) void k_splitk_x3p(SplitKGroup grp
   // departures (monotone over the slice: stage i uses buffer i % 3 for the (i / 3)-th time)
   uint32_t* const full = reinterpret_cast<uint32_t*>(x3p_smem + 3 * 2 * 3 * kX3pPlane);
   uint32_t* const empty = full + 3;
+  uint32_t* const stall = full + 6;  // set by any wave whose wait ran out (LDS_Q's spare words)
   if constexpr (QUEUE) {
-    if (tid < 6) full[tid] = 0u;
+    if (tid < 7) full[tid] = 0u;
     __syncthreads();
   }
-  // bounded: every wave leaves the loop (the counts are reached within microseconds; a wrong
-  // count would give wrong sums, which the tests catch, never a grid that does not drain)
+  // bounded: every wave leaves the loop (the counts are reached within microseconds). A wave
+  // descheduled past the bound (≈ 0.1 s: preemption, a shared GPU) would read a buffer not yet
+  // filled or overwrite one in use, so a wait that runs out marks the workgroup, and its whole
+  // output is written as NaN below — a loud failure, never silently wrong gradients.
   auto spin_until = [&](const uint32_t* c, uint32_t target) {
     for (uint32_t n = 0; n < (1u << 22); ++n) {
-      if (__hip_atomic_load(c, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
+      if (__hip_atomic_load(c, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) return;
       __builtin_amdgcn_s_sleep(1);
     }
+    __hip_atomic_store(stall, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   };
   auto arrive = [&](uint32_t* c) {  // after this wave's LDS accesses of the stage
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -1179,6 +1183,10 @@ __global__ __launch_bounds__(X3P<MT>::THREADS) void k_splitk_x3p(SplitKGroup grp
     for (int c = 0; c < 4; ++c) s_b[(2 * gq + hh) * M + 4 * cb + c] = bsum[c];
   }
   const int64_t MN = static_cast<int64_t>(p.M) * p.N;
+  bool poisoned = false;
+  if constexpr (QUEUE)
+    poisoned = __hip_atomic_load(stall, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u;
+  const float nan = __builtin_nanf("");
   if (wave < 8) {
     // acc[t][u] lane (i16, g) register r: m = 16(TM·mp + t) + 4g + r, n = 16(TN·nq + u) + i16
 #pragma unroll
@@ -1188,14 +1196,14 @@ __global__ __launch_bounds__(X3P<MT>::THREADS) void k_splitk_x3p(SplitKGroup grp
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int m = 16 * (C::TM * mp + t) + 4 * g + r, n = 16 * (C::TN * nq + u) + i16;
-          p.part[bx * MN + static_cast<int64_t>(m) * p.N + n] = acc[t][u][r];
+          p.part[bx * MN + static_cast<int64_t>(m) * p.N + n] = poisoned ? nan : acc[t][u][r];
         }
   }
   __syncthreads();
   if (p.part_bias != nullptr && tid < M) {
     float v = 0.f;
     for (int q = 0; q < 8; ++q) v += s_b[q * M + tid];
-    p.part_bias[bx * p.M + tid] = v;
+    p.part_bias[bx * p.M + tid] = poisoned ? nan : v;
   }
 }
 

@@ -97,7 +97,9 @@ typedef enum hgd_epilogue {
  *                         min(16, hardware threads, OMP_NUM_THREADS); 1 = one thread)
  *   HGD_TUNE_X3P_QUEUE:   form of the producer-wave weight gradient: 0 (default) = one workgroup
  *                         barrier per 32-row stage, 1 = three LDS buffers with full / empty
- *                         counters (measured slower: 45.1 vs 41.5 µs at 144,242 x 128)
+ *                         counters (measured slower: 45.1 vs 41.5 µs at 144,242 x 128); a
+ *                         counter wait that runs out (≈ 0.1 s) writes the workgroup's partial
+ *                         sums as NaN instead of reading an unfilled buffer
  *   HGD_TUNE_P2P_GRID:    workgroups of the peer exchange's reduce / gather kernels (0 = default
  *                         256: the links bound them, the hops they overlap need the CUs)
  *   HGD_TUNE_MASK_PAIR:   the masked hop (hgd_spmm_masked*) walks two index batches per step

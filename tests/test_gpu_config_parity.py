@@ -59,11 +59,17 @@ def _coo_host(adj):
 # HCCF (configs[0], configs[2])
 # ---------------------------------------------------------------------------------------------
 def _hccf_case(dev, shape, d, n_layers, seed, batch=4096, temp=1.0, cl_rate=0.01,
-               capture_safe=False):
+               capture_safe=False, fp32_bound=False):
     """One HCCF training step's forward and backward (HCCF.py:79-97): encoder with drop-edge
     (keep 1 - conf dropout 0.3) and learned-hypergraph dropout (--drop_rate 0.2), then
     HCCF.calcLosses (BPR + cl_rate · Σ_layers InfoNCE at conf temp), as the plugin computes it
-    (plugins.HCCF.calcLosses: fused InfoNCE kernel, MFMA E·W and HGNN products)."""
+    (plugins.HCCF.calcLosses: fused InfoNCE kernel, MFMA E·W and HGNN products).
+
+    Every output, the loss and every parameter gradient are held to the row bound against the
+    reference's torch calls in float64. ``fp32_bound``: per tensor the bound is instead
+    max(1e-5, the reference's own torch calls evaluated in float32, against the same float64) —
+    our step may be no worse than the reference's arithmetic where a row is ill-conditioned in
+    fp32 (§7 of DESIGN.md). Returns {tensor: (ours, reference fp32 or None)} worst row ratios."""
     from hypergraph_diffusion_for_recommendation_amd.encoders import HCCFEncoder
     from hypergraph_diffusion_for_recommendation_amd.plugins import HCCF
     U, I, nnz = shape
@@ -90,39 +96,56 @@ def _hccf_case(dev, shape, d, n_layers, seed, batch=4096, temp=1.0, cl_rate=0.01
     loss = bpr + ssl
     loss.backward()
 
-    P = R.leaves(enc)
     idx, vals = _coo_host(enc.sparse_norm_adj)
     torch.manual_seed(seed + 3)
-    adjs = []
+    drops = []
     for layer in range(n_layers):
         di, dv = R.drop_edge_reference(idx, vals, 0.7)
         gi, gv = enc.edgeDropper.outputs[layer]
         assert torch.equal(di, gi) and torch.equal(dv, gv), f"drop-edge layer {layer}"
-        adjs.append(R.sparse(di, dv, (N, N)))
+        drops.append((di, dv))
     assert len(enc.drop_out.masks) == 2 * n_layers
-    ueR, ieR, gR, hR = R.hccf_encoder(P, adjs, enc.drop_out.masks, 0.8, U, n_layers)
-    anc, pos, neg = ueR[u], ieR[i], ieR[j]
-    u_nodes, p_nodes = torch.unique(anc.long()), torch.unique(pos.long())
-    sslR = 0
-    for layer in range(n_layers):
-        e1, e2 = gR[layer].detach(), hR[layer]
-        sslR = sslR + R.contrast_loss(e1[:U], e2[:U], u_nodes, temp) \
-            + R.contrast_loss(e1[U:], e2[U:], p_nodes, temp)
-    lossR = R.bpr_loss(anc, pos, neg) + sslR * cl_rate
 
-    worst = R.check_rows(ue, ueR, "user_emb")
-    worst = max(worst, R.check_rows(ie, ieR, "item_emb"))
+    def reference(dtype):
+        P = R.leaves(enc, dtype)
+        adjs = [R.sparse(di, dv, (N, N), dtype) for di, dv in drops]
+        masks = [m.to(dtype) for m in enc.drop_out.masks[:2 * n_layers]]
+        ueR, ieR, gR, hR = R.hccf_encoder(P, adjs, masks, 0.8, U, n_layers)
+        anc, pos, neg = ueR[u], ieR[i], ieR[j]
+        u_nodes, p_nodes = torch.unique(anc.long()), torch.unique(pos.long())
+        sslR = 0
+        for layer in range(n_layers):
+            e1, e2 = gR[layer].detach(), hR[layer]
+            sslR = sslR + R.contrast_loss(e1[:U], e2[:U], u_nodes, temp) \
+                + R.contrast_loss(e1[U:], e2[U:], p_nodes, temp)
+        lossR = R.bpr_loss(anc, pos, neg) + sslR * cl_rate
+        out = {"user_emb": ueR, "item_emb": ieR, "loss": lossR.reshape(1)}
+        for layer in range(n_layers):
+            out[f"gcn[{layer}]"], out[f"hyper[{layer}]"] = gR[layer], hR[layer]
+        names = list(P)
+        gref = torch.autograd.grad(lossR, [P[k] for k in names])
+        out.update((f"d {k}", g) for k, g in zip(names, gref))
+        return out
+
+    got = {"user_emb": ue, "item_emb": ie, "loss": loss.detach().reshape(1)}
     for layer in range(n_layers):
-        worst = max(worst, R.check_rows(gcns[layer], gR[layer], f"gcn[{layer}]"),
-                    R.check_rows(hyps[layer], hR[layer], f"hyper[{layer}]"))
-    assert abs(float(loss) - float(lossR)) <= R.TOL * abs(float(lossR)), (float(loss),
-                                                                         float(lossR))
-    names = list(P)
-    gref = torch.autograd.grad(lossR, [P[k] for k in names])
-    got = dict(enc.named_parameters())
-    for k, g in zip(names, gref):
-        worst = max(worst, R.check_rows(got[k].grad, g, f"d {k}"))
-    print(f"HCCF {shape} d={d} L={n_layers}: worst row ratio {worst:.2e}")
+        got[f"gcn[{layer}]"], got[f"hyper[{layer}]"] = gcns[layer], hyps[layer]
+    got.update((f"d {k}", p.grad) for k, p in enc.named_parameters())
+    r64 = reference(torch.float64)
+    r32 = reference(torch.float32) if fp32_bound else None
+    ratios = {}
+    for k in r64:
+        # (tol 1e-2: the fp32 reference must be the same computation — e.g. the same InfoNCE
+        # node lists — or the bound it sets would be vacuous)
+        own = None if r32 is None else R.check_rows(r32[k], r64[k], f"reference fp32 {k}",
+                                                    tol=1e-2)
+        ours = R.check_rows(got[k], r64[k], k, tol=R.TOL if own is None else max(R.TOL, own))
+        ratios[k] = (ours, own)
+    worst = max(v[0] for v in ratios.values())
+    print(f"HCCF {shape} d={d} L={n_layers} seed={seed} view={capture_safe}: worst row ratio "
+          f"{worst:.2e}" + ("" if r32 is None else " | " + ", ".join(
+              f"{k} {a:.2e}/{b:.2e}" for k, (a, b) in ratios.items() if max(a, b) > R.TOL)))
+    return ratios
 
 
 def test_hccf_lastfm_1layer_d32_train_step(dev):
@@ -135,70 +158,27 @@ def test_hccf_yelp_3layer_d64_infonce_train_step(dev):
     _hccf_case(dev, YELP, 64, 3, seed=20)
 
 
-def test_hccf_ill_conditioned_rows_no_worse_than_reference_fp32(dev):
-    """LastFM seed 13: the batch's InfoNCE node lists are torch.unique(emb.long()) = [0]
-    (HCCF.py:65-66), a one-node softmax whose loss is 0 in fp32 and 2e-10 in float64, so row 0
-    of both embedding gradients is pure rounding: the reference's own torch calls evaluated in
-    float32 miss the float64 row there by 6.1e-4 (items) and 2.5e-5 (users) of its scale. The
-    row bound cannot hold for ANY fp32 evaluation of that row; what is checked is that every
-    tensor of our step is within max(1e-5, the reference-fp32 deviation) of float64 — i.e. no
-    worse than the reference's own arithmetic (scripts/diag/diag_hccf_seed.py prints the
-    breakdown: ours 2.9e-4 / 6.1e-6 there)."""
-    from hypergraph_diffusion_for_recommendation_amd.encoders import HCCFEncoder
-    from hypergraph_diffusion_for_recommendation_amd.plugins import HCCF
-    U, I, nnz = LASTFM
-    N, d, L, seed, batch, temp, cl_rate = U + I, 32, 1, 13, 4096, 1.0, 0.01
-    _, A = _graph(U, I, nnz, seed)
-    data = SimpleNamespace(n_users=U, n_items=I, norm_adj=A)
-    kw = dict(lrate=1e-3, lr_decay=0.9, max_epoch=1, batch_size=batch, reg=0.01,
-              embedding_size=d, hyper_dim=32, drop_rate=0.2, p=0.3, n_layers=L)
-    torch.manual_seed(seed)
-    enc = HCCFEncoder(kw, data, device=dev).train()
-    enc.drop_out = R.FixedDropout(0.2, seed + 1)
-    enc.edgeDropper = R.DropRecorder(enc.edgeDropper)
-    rng = np.random.default_rng(seed + 2)
-    u, i, j = (torch.from_numpy(rng.integers(0, n, batch)) for n in (U, I, I))
-    host = SimpleNamespace(data=data, nLayers=L, temp=temp, ss_rate=cl_rate)
-    torch.manual_seed(seed + 3)
-    ue, ie, gcns, hyps = enc(keep_rate=0.7)
-    bpr, ssl = HCCF.calcLosses(host, ue[u.to(dev)], ie[i.to(dev)], ie[j.to(dev)], gcns, hyps,
-                               0.01)
-    (bpr + ssl).backward()
-
-    def reference(dtype):
-        P = R.leaves(enc, dtype)
-        adjs = [R.sparse(gi, gv, (N, N), dtype) for gi, gv in enc.edgeDropper.outputs[:L]]
-        masks = [m.to(dtype) for m in enc.drop_out.masks[:2 * L]]
-        ueR, ieR, gR, hR = R.hccf_encoder(P, adjs, masks, 0.8, U, L)
-        anc, pos, neg = ueR[u], ieR[i], ieR[j]
-        un, pn = torch.unique(anc.long()), torch.unique(pos.long())
-        sslR = 0
-        for layer in range(L):
-            e1, e2 = gR[layer].detach(), hR[layer]
-            sslR = sslR + R.contrast_loss(e1[:U], e2[:U], un, temp) \
-                + R.contrast_loss(e1[U:], e2[U:], pn, temp)
-        lossR = R.bpr_loss(anc, pos, neg) + sslR * cl_rate
-        names = list(P)
-        out = {"user_emb": ueR, "item_emb": ieR, "gcn": gR[0], "hyper": hR[0]}
-        out.update(zip(names, torch.autograd.grad(lossR, [P[k] for k in names])))
-        return out
-
-    r64, r32 = reference(torch.float64), reference(torch.float32)
-    got = {"user_emb": ue, "item_emb": ie, "gcn": gcns[0], "hyper": hyps[0]}
-    got.update({k: p.grad for k, p in enc.named_parameters()})
-    for k in r64:
-        own = R.check_rows(r32[k], r64[k], f"reference fp32 {k}", tol=1.0)
-        R.check_rows(got[k], r64[k], k, tol=max(R.TOL, own))
+@pytest.mark.parametrize("view", [False, True], ids=["compacted", "view"])
+@pytest.mark.parametrize("seed", range(10, 20))
+def test_hccf_lastfm_seeds_no_worse_than_reference_fp32(dev, seed, view):
+    """configs[0] (LastFM HCCF, 1 layer, d = 32) over seeds 10-19 on both drop-edge paths (the
+    compacted children and the plugins' default masked views; the drops are bit-exact either
+    way). The batch's InfoNCE node lists are torch.unique(emb.long()) (HCCF.py:65-66): small
+    integers, sometimes just [0], so a few gradient rows are sums with heavy cancellation. E.g.
+    at seed 13 the lists are [0], a one-node softmax whose loss is 0 in fp32 and 2e-10 in
+    float64, and the reference's own torch calls evaluated in float32 miss row 0 of the item /
+    user gradients by 6.1e-4 / 2.5e-5 of its scale. The row bound cannot hold for ANY fp32
+    evaluation of such a row; every tensor of our step is held to max(1e-5, the reference's own
+    fp32 deviation from float64) — no seed is dropped (DESIGN.md §7 lists the ratios)."""
+    _hccf_case(dev, LASTFM, 32, 1, seed=seed, capture_safe=view, fp32_bound=True)
 
 
 @pytest.mark.parametrize("shape,d,layers,seed", [("LASTFM", 32, 1, 10), ("YELP", 64, 3, 20)])
 def test_hccf_train_step_on_masked_drop_views(dev, shape, d, layers, seed):
     """The plugins' default drop-edge (masked views of the parent, the reference's CPU mask
     stream): the recorded drops equal the reference's compaction bit for bit, and the step's
-    outputs and gradients meet the same row bound as with compacted children. (Same seeds as
-    the compacted cases above: the worst row ratios of the two paths are equal there, e.g.
-    3.74e-6 at LastFM seed 10; seed 11 puts an item-gradient row with heavy cancellation at
-    1.97e-5 of its scale on BOTH paths — scripts/diag/diag_view_ratio.py.)"""
+    outputs and gradients meet the 1e-5 row bound outright, as with compacted children (LastFM
+    over seeds 10-19 under the reference-fp32 bound: the sweep above)."""
     _hccf_case(dev, {"LASTFM": LASTFM, "YELP": YELP}[shape], d, layers, seed=seed,
                capture_safe=True)
 

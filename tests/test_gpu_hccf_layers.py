@@ -162,11 +162,8 @@ def test_bpr_loss_rows_matches_torch(dev, d):
 def test_bpr_loss_rows_skewed_batch(dev, d):
     """A skewed catalogue's batch (bench_plugin_epoch's Zipf-1.2 items: one item is the positive
     of ~18 % of the rows, far more repeats than a row's LDS list holds): the same bounds and
-    determinism, and the backward stays a small fraction of a step (the list-scan path; the
-    round-3 fallback took 45 ms per call here)."""
-    import time
-
-    from hypergraph_diffusion_for_recommendation_amd.functional import bpr_loss_rows
+    determinism on the list-scan path. (Its speed — the round-3 fallback took 45 ms per call
+    here — is a benchmark's business: scripts/bench_plugin_epoch.py's Zipf epoch.)"""
     g = torch.Generator(device=dev).manual_seed(100 + d)
     U, I, B = 31_668, 38_048, 4096
     uid = torch.randint(0, U, (B,), device=dev, generator=g)
@@ -177,17 +174,6 @@ def test_bpr_loss_rows_skewed_batch(dev, d):
     nid[: B // 8] = 1                                             # item 1: 512 negatives
     uid[B // 2: B // 2 + 300] = 7                                 # user 7: 300 anchors
     _check_bpr_rows(dev, g, d, U, I, uid, pid, nid)
-    E = (0.3 * torch.randn(U + I, d, device=dev, generator=g)).requires_grad_(True)
-    ue, ie = torch.split(E, [U, I])
-    ts = []
-    for _ in range(6):
-        loss, _a, _p = bpr_loss_rows(ue, ie, uid, pid, nid)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        torch.autograd.grad(loss, E)
-        torch.cuda.synchronize()
-        ts.append(time.perf_counter() - t0)
-    assert sorted(ts)[3] < 5e-3, ts
 
 
 def _check_bpr_rows(dev, g, d, U, I, uid, pid, nid):

@@ -51,10 +51,17 @@ def _worker(rank, world, port, case, q):
         sh = _FakeShard(rank, case)
         Y = torch.linspace(-1.0, 1.0, 64).reshape(8, 8)
 
+        p2p_steps = [0]
+
         def eager_step():
             if sh.transport == "p2p":
+                p2p_steps[0] += 1
                 if case == "raise" and rank == 1:
                     raise RuntimeError("P2PExchange: rank 1: hgd_p2p_open: did not return")
+                if case == "raise_timed" and rank == 1 and p2p_steps[0] == 2:
+                    # the first TIMED step (the checked step passed): the other rank is
+                    # already inside timed()'s collectives
+                    raise RuntimeError("hgd_p2p_poll: a wait timed out on this rank")
                 time.sleep(0.002 if case != "slower" else 0.02)
                 y = Y * (1.0 + 1e-3) if case == "mismatch" and rank == 0 else Y
                 return y, Y.clone()
@@ -70,7 +77,8 @@ def _worker(rank, world, port, case, q):
 
 @pytest.mark.parametrize("case,chosen,failed", [("ok", "p2p", False), ("slower", "rccl", False),
                                                 ("raise", "rccl", True), ("check", "rccl", True),
-                                                ("mismatch", "rccl", True)])
+                                                ("mismatch", "rccl", True),
+                                                ("raise_timed", "rccl", True)])
 def test_auto_transport_decision_is_agreed(case, chosen, failed):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -80,5 +88,5 @@ def test_auto_transport_decision_is_agreed(case, chosen, failed):
     for rank, ch, fail, has_err, transport in got:
         assert ch == chosen and transport == chosen, (case, rank, ch, transport)
         assert fail == failed, (case, rank, fail)
-    if case == "raise":  # the failing rank reports its error
+    if case in ("raise", "raise_timed"):  # the failing rank reports its error
         assert got[1][3]
