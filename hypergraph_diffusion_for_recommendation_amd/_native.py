@@ -509,10 +509,14 @@ _PyCapsule_New.restype = ctypes.py_object
 _PyCapsule_New.argtypes = [c_void_p, ctypes.c_char_p, c_void_p]
 
 
-def float_view(address: int, shape, device, owner) -> "torch.Tensor":
+def float_view(address: int, shape, device, on_release=None) -> "torch.Tensor":
     """A contiguous float32 tensor over ``address`` (device memory the library owns, or host
-    memory for ``device`` = cpu) without copying. ``owner`` (the object whose lifetime bounds the
-    memory) is kept alive by the returned tensor's DLPack record; no deleter is called."""
+    memory for ``device`` = cpu) without copying. ``on_release()`` runs when torch releases the
+    tensor's STORAGE — after the last tensor or view sharing it is gone, which may be well after
+    the returned tensor object — through the DLPack record's deleter: the owner of the memory
+    counts its live views this way and frees the memory only once none is left (a view can never
+    reach freed memory). Nothing here references the owner, so a view does not keep its owner's
+    Python object alive (no reference cycle through a global)."""
     import torch
     device = torch.device(device)
     shape = tuple(int(s) for s in shape)
@@ -530,19 +534,27 @@ def float_view(address: int, shape, device, owner) -> "torch.Tensor":
     rec.dl_tensor.strides = None  # compact row-major
     rec.dl_tensor.byte_offset = 0
     rec.manager_ctx = None
-    rec.deleter = None
+    rec.deleter = ctypes.cast(_DL_DELETER, c_void_p)
+    # the record and its shape array live until torch calls the deleter with the record
+    _LIVE_RECORDS[ctypes.addressof(rec)] = (rec, shp, on_release)
     cap = _PyCapsule_New(ctypes.addressof(rec), b"dltensor", None)
-    t = torch.utils.dlpack.from_dlpack(cap)
-    # torch reads the record (its deleter field) when the STORAGE is released, which any view
-    # of the tensor can delay past the tensor object: the record and its shape array are never
-    # freed (~100 bytes; callers cache their views, e.g. P2PExchange.slot). The owner is kept
-    # alive as long as the tensor object.
-    _RECORDS.append((rec, shp))
-    _KEEP[id(t)] = owner
-    import weakref
-    weakref.finalize(t, _KEEP.pop, id(t), None)
-    return t
+    return torch.utils.dlpack.from_dlpack(cap)
 
 
-_KEEP = {}
-_RECORDS = []
+_LIVE_RECORDS = {}
+
+
+@ctypes.CFUNCTYPE(None, c_void_p)
+def _DL_DELETER(address, _live=_LIVE_RECORDS):
+    """DLManagedTensor.deleter: torch released the storage of a float_view."""
+    try:
+        entry = _live.pop(address, None)
+        if entry is not None and entry[2] is not None:
+            entry[2]()
+    except Exception:  # noqa: BLE001 — never raise into torch's storage release
+        pass
+
+
+def live_views() -> int:
+    """float_view storages torch has not released yet (tests)."""
+    return len(_LIVE_RECORDS)

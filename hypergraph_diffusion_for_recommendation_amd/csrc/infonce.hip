@@ -11,6 +11,14 @@
 //     each wave owns 16 rows of p1 (fragments in registers) and streams 16-column tiles of p2,
 //     exponentiating the 16×16 logit tile in registers; the j range is split over S workgroups
 //     whose partial row sums are added in a fixed order (deterministic, no atomics);
+//   * the diagonal is kept apart: k_nce_rowsum sums the OFF-diagonal terms (off_b =
+//     Σ_{j≠b} exp(s_bj/τ) + 1e-8) and leaves exp(s_bb/τ) for the finish, which forms
+//     deno_b = off_b + exp(s_bb/τ) and keeps off_b beside it (deno holds [2, B]). The loss term
+//     log(deno_b/nume_b) is then log1p((off_b + (e_bb − nume_b))/nume_b), and the diagonal
+//     gradient weight −(1 − p_bb) is −off_b/deno_b: no cancellation of p_bb ≈ 1 against 1. That
+//     case is HCCF's (HCCF.py:65-66 passes torch.unique(emb.long()), often a list of one or two
+//     nodes: p_bb = e/(e + 1e-8) rounds to 1 in fp32, so e/deno − 1 is pure rounding noise and the
+//     reference's own fp32 autograd returns noise there — we return the float64 value's digits);
 //   * backward: G_bj = g·(exp(s_bj/τ)/deno_b − δ_bj)/(B·τ) is recomputed tile by tile, and
 //     dP1 = G·P2, dP2 = Gᵀ·P1 run on the MFMA with the logit tile's accumulator registers used
 //     directly as the next MFMA's A operand (rows of the tile on the lane, its columns in the
@@ -233,9 +241,18 @@ __global__ __launch_bounds__(256) void k_nce_rowsum(NceGroup grp, float k2) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) s = mfma4(a[q][c], f[q][c], s);
       // s[r] = <p1_{b0 + 4(l>>4) + r}, p2_{j0 + 16t + (l&15)}>
-      const bool jok = j0 + 16 * t + (lane & 15) < j_end;
+      const int64_t j = j0 + 16 * t + (lane & 15);
+      const bool jok = j < j_end;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) psum[r] += jok ? exp2_raw(s[r] * k2) : 0.f;
+      for (int r = 0; r < 4; ++r) {
+        const int64_t b = b0 + 4 * (lane >> 4) + r;
+        const float e = exp2_raw(s[r] * k2);
+        if (j == b) {  // the diagonal: exactly one lane of the grid; kept apart for the finish
+          if (jok && b < Be) p.deno[b] = e;
+        } else {
+          psum[r] += jok ? e : 0.f;
+        }
+      }
     }
     if (more) stage_store<DQ>(sm[buf ^ 1], v);
     __syncthreads();
@@ -275,9 +292,14 @@ __global__ __launch_bounds__(1024) void k_nce_finish(NceGroup grp) {
       for (int u = 0; u < 8; ++u) den += v[u];
     }
     for (; s < S; ++s) den += partial[s * B + b];
-    den += kDenoEps;
-    deno[b] = den;
-    acc += logf(expf(pos_logit[b]) / den);
+    const float off = den + kDenoEps;  // Σ_{j≠b} exp(s_bj/τ) + 1e-8
+    const float e_bb = deno[b];        // exp(s_bb/τ), left by k_nce_rowsum
+    const float nume = expf(pos_logit[b]);
+    deno[b] = off + e_bb;
+    deno[B + b] = off;
+    // log(nume / deno) = −log1p((deno − nume)/nume), deno − nume = off + (e_bb − nume): the two
+    // exps are the same logit rounded two ways, so their difference is exact-ish (Sterbenz)
+    acc -= log1pf((off + (e_bb - nume)) / nume);
   }
   red[threadIdx.x] = acc;
   __syncthreads();
@@ -291,7 +313,7 @@ __global__ __launch_bounds__(1024) void k_nce_finish(NceGroup grp) {
 // ---- backward partials ----
 // ROWS = true : part[s][b][:] = Σ_{j in slice s} G_bj p2_j       (dP1)
 // ROWS = false: part[s][j][:] = Σ_{b in slice s} G_bj p1_b       (dP2)
-// with G_bj = coef·(exp(s_bj/τ)/deno_b − δ_bj), coef = g/(B·τ).
+// with G_bj = coef·(exp(s_bj/τ)/deno_b − δ_bj), coef = g/(B·τ); the diagonal as −coef·off_b/deno_b.
 // The "other" rows of the slice stream through LDS in 32-row stages shared by the workgroup's
 // four waves (with their denominators when those index the other rows); each 16-row tile is read
 // twice from the stage: as logit fragments (row on the lane) and, transposed, as the B operand of
@@ -331,6 +353,8 @@ __global__ __launch_bounds__(256) void k_nce_bwd(NceGroup grp, float k2,
   const int64_t o_lane = o0 + i16;  // own row of this lane in the logit tile below
   float inv_own = 1.f;
   if (ROWS) inv_own = 1.f / deno[o_lane < Be ? o_lane : Be - 1];
+  // the diagonal weight −(1 − p_bb) = −off_b/deno_b of this lane's own row (off_b: deno[B + b])
+  const float off_own = deno[B + (o_lane < Be ? o_lane : Be - 1)];
   const int64_t k_begin = static_cast<int64_t>(blockIdx.y) * p.per_slice;
   const int64_t k_end = min(Be, k_begin + p.per_slice);
   f32x4 acc[DQ / 4];
@@ -374,8 +398,8 @@ __global__ __launch_bounds__(256) void k_nce_bwd(NceGroup grp, float k2,
         const int64_t k = kt + 4 * h + r;  // other index of register r
         const float e = exp2_raw(s[r] * k2);
         const float inv = ROWS ? inv_own : sinv[buf][16 * u + 4 * h + r];
-        const float delta = (k == o_lane) ? 1.f : 0.f;
-        gk[r] = (k < k_end && o_lane < Be) ? coef * (e * inv - delta) : 0.f;
+        const float w = (k == o_lane) ? -off_own * inv : e * inv;
+        gk[r] = (k < k_end && o_lane < Be) ? coef * w : 0.f;
       }
       // acc[own row][n] += Σ_k G[own][k]·oth_k[n]: A operand = gk (own row on the lane, k-step
       // r covers other rows {4(l>>4) + r}), B operand = those rows' features, read transposed

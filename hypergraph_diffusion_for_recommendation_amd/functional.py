@@ -672,7 +672,8 @@ class _ContrastLoss(torch.autograd.Function):
         B, d = nodes.numel(), E1.shape[1]
         f = dict(dtype=torch.float32, device=dev)
         P1, P2 = torch.empty((B, d), **f), torch.empty((B, d), **f)
-        inv1, inv2, pos, deno = (torch.empty(B, **f) for _ in range(4))
+        inv1, inv2, pos = (torch.empty(B, **f) for _ in range(3))
+        deno = torch.empty(2 * B, **f)  # [deno; off-diagonal part] (include/hgd.h)
         loss = torch.empty((), **f)
         wsb = lib.hgd_infonce_workspace_size(B, d)
         ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
@@ -756,14 +757,15 @@ class _ContrastLossLayers(torch.autograd.Function):
             halves.append((r0, rows, nodes.to(device=dev, dtype=torch.int64).contiguous(), count))
         # every term's operands in ONE float buffer and every workspace in ONE byte buffer (an
         # eager step otherwise made ~40 allocator calls here): the term losses first, then per
-        # term P1, P2 [B, d] and inv1, inv2, pos_logit, deno [B], each at a 256-byte boundary
+        # term P1, P2 [B, d], inv1, inv2, pos_logit [B] and deno [2, B], each at a 256-byte
+        # boundary
         offs, cur = [], _al64(2 * L)
         for layer in range(L):
             for _r0, _rows, nodes, _c in halves:
                 B = nodes.numel()
                 o = {}
                 for name, size in (("P1", B * d), ("P2", B * d), ("inv1", B), ("inv2", B),
-                                   ("pos", B), ("deno", B)):
+                                   ("pos", B), ("deno", 2 * B)):
                     o[name] = cur
                     cur += _al64(size)
                 offs.append(o)

@@ -123,6 +123,45 @@ def p2p_setup_stuck() -> int:
     return _P2P_STUCK
 
 
+class _P2PHandle:
+    """Owns one ``hgd_p2p`` handle (its exported send / reduced slots). The handle is destroyed
+    once BOTH a release was requested (:meth:`P2PExchange.close` / ``release``, or the exchange
+    was garbage-collected) AND no slot view's storage is alive (nat.float_view's deleter reports
+    each one's release, whenever torch gets to it): a slot view held past close() keeps pointing
+    at live memory, and an exchange dropped without close() still frees its segments."""
+
+    def __init__(self, lib, h):
+        self.lib, self.h = lib, h
+        self.live = 0
+        self.wanted = False
+        self.lock = threading.Lock()
+
+    def view_born(self):
+        with self.lock:
+            self.live += 1
+
+    def view_gone(self):
+        with self.lock:
+            self.live -= 1
+        self._maybe_destroy()
+
+    def release(self):
+        with self.lock:
+            self.wanted = True
+        self._maybe_destroy()
+
+    def _maybe_destroy(self):
+        with self.lock:
+            if not (self.wanted and self.live == 0 and self.h is not None):
+                return
+            h, self.h = self.h, None
+        self.lib.hgd_p2p_destroy(h)  # synchronises the device, closes the peers' mappings
+
+    @property
+    def alive(self) -> bool:
+        return self.h is not None
+
+
 class P2PExchange:
     """The direct xGMI peer transport (``hgd_p2p_*``, csrc/p2p.hip): every rank exposes one
     uncached buffer of ``n_slots`` send slots to its peers; an all-reduce of a slot is a two-shot
@@ -148,6 +187,7 @@ class P2PExchange:
         self.timeout_s = float(timeout_s)
         trace = trace or (lambda msg: None)
         self.h = None
+        self._handle = None  # _P2PHandle: the handle's lifetime (slot views may outlive close)
         self._views = {}
         # every step that can fail locally is followed by an agreement among the ranks, so a
         # failure on one rank raises on all of them (none is left waiting in a collective)
@@ -158,6 +198,7 @@ class P2PExchange:
                         "hgd_p2p_create")
         if err is None:
             self.h = h
+            self._handle = _P2PHandle(self.lib, h)
             err = self._try(lambda: self.lib.hgd_p2p_set_timeout(h, self.timeout_s),
                             "hgd_p2p_set_timeout") or self._try(
                 lambda: self.lib.hgd_p2p_export(h, mine), "hgd_p2p_export")
@@ -211,8 +252,9 @@ class P2PExchange:
     def _agree(self, errs):
         bad = [(q, e) for q, e in enumerate(errs) if e is not None]
         if bad:
-            if self.h is not None and not self._stuck:
-                self.lib.hgd_p2p_destroy(self.h)
+            if self._handle is not None and not self._stuck:
+                self._handle.release()
+            self._handle = None
             self.h = None
             raise nat.HGDNativeError("P2PExchange: " + "; ".join(f"rank {q}: {e}"
                                                                   for q, e in bad))
@@ -221,13 +263,18 @@ class P2PExchange:
         """Send slot ``k`` as a [rows, cols] float32 view (the hop kernels write into it)."""
         if rows * cols > self.max_count:
             raise ValueError(f"P2PExchange: slot of {rows}x{cols} > {self.max_count} floats")
+        if self.h is None:
+            raise RuntimeError("P2PExchange: closed")
         key = (k, rows, cols)
         v = self._views.get(key)
         if v is None:
             addr = self.lib.hgd_p2p_slot(self.h, int(k))
             if not addr:
                 raise ValueError(f"P2PExchange: no slot {k}")
-            v = self._views[key] = nat.float_view(addr, (rows, cols), self.device, self)
+            hd = self._handle
+            hd.view_born()
+            v = self._views[key] = nat.float_view(addr, (rows, cols), self.device,
+                                                  on_release=hd.view_gone)
         return v
 
     def allreduce(self, k: int, count: int, out: torch.Tensor, stream_handle: int) -> None:
@@ -262,15 +309,37 @@ class P2PExchange:
             pause = min(2 * pause, 0.05)
 
     def close(self) -> None:
-        """Collective: every rank's peers stop reading before the buffers go."""
+        """Collective: every rank's peers stop reading before the buffers go. The exchange is
+        unusable afterwards; its memory is freed as soon as no slot view handed out is alive."""
         if self.h is None:
             return
         torch.cuda.synchronize(self.device)
         if self.world > 1:
             dist.barrier(group=self.group)
-        self._views.clear()
-        self.lib.hgd_p2p_destroy(self.h)
+        self.release()
+
+    def release(self) -> None:
+        """Non-collective close (no barrier): the exchange stops being usable, and the handle
+        goes once every slot view's storage is released. What a dropped exchange does."""
         self.h = None
+        self._views.clear()
+        if self._handle is not None and not self._stuck:
+            self._handle.release()
+        self._handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None) is not None:
+                self.release()
+        except Exception:  # noqa: BLE001 — interpreter teardown
+            pass
 
 
 class ExchangeTimer:
@@ -395,9 +464,27 @@ class ShardedIncidence:
         return self._p2p
 
     def close(self) -> None:
+        """Collective when the peer transport is up (its close is)."""
         if self._p2p is not None:
             self._p2p.close()
             self._p2p = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
+
+    def __del__(self):
+        # dropped without close(): free the peer segments without a collective (the exchange's
+        # own finalizer would too; releasing here does not wait for the GC to reach it)
+        try:
+            if getattr(self, "_p2p", None) is not None:
+                self._p2p.release()
+                self._p2p = None
+        except Exception:  # noqa: BLE001 — interpreter teardown
+            pass
 
     def two_hop(self, X: torch.Tensor, src_kind: Optional[str],
                 dst_kind: Optional[str]) -> torch.Tensor:

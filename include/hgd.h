@@ -396,8 +396,12 @@ hgd_status hgd_gemm_tn(const hgd_gemm_tn_desc* descs, int32_t count, void* works
  * Only the B batch rows are gathered and normalised; the [B, B] exp-sum is never materialised.
  * nodes follow torch indexing: negative ids count from the end of the table (HCCF.py:65-66 passes
  * torch.unique(emb.long())); ids outside [-n_rows, n_rows) are the caller's error (clamped here).
- * Forward writes P1, P2 [B, d] (contiguous), inv_norm1/2 [B], pos_logit [B], deno [B] and the
- * scalar loss (all device). Backward recomputes the logits and writes dX1, dX2 [B, d] =
+ * Forward writes P1, P2 [B, d] (contiguous), inv_norm1/2 [B], pos_logit [B], deno [2, B] and
+ * the scalar loss (all device): deno[b] = Σ_j exp(<p1_b,p2_j>/τ) + 1e-8 and deno[B + b] = its
+ * off-diagonal part (Σ_{j≠b} … + 1e-8), from which the loss term and the diagonal gradient
+ * weight 1 − p_bb are formed without cancellation (p_bb rounds to 1 in fp32 for a one-node list;
+ * the reference's fp32 autograd returns rounding noise there). B is the capacity for the _n
+ * forms. Backward recomputes the logits and writes dX1, dX2 [B, d] =
  * dloss/d(E1[nodes]), dloss/d(E2[nodes]) scaled by the device scalar *grad_loss; scattering
  * them into the [N, d] table gradients (duplicate nodes add) is the caller's. d: multiple of 16
  * in [16, 256]. Deterministic (fixed-order reductions). Workspace: hgd_infonce_workspace_size.

@@ -1,0 +1,176 @@
+#!/usr/bin/env python3
+"""Is the second-epoch divergence of the HCCF plugin on a skewed catalogue the reference's own
+dynamics? (VERDICT r4 "what's weak" 2; profiles/r04_hccf/eager_views/zipf_two_epoch_divergence.txt)
+
+Same set-up, batches and modes as scripts/diag/diag_epoch_nan.py (bench_plugin_epoch's Zipf-1.2
+Yelp-shaped files, epoch 1 on the reference's CPU drop-edge stream, epoch 2 on device-drawn
+masks): the trajectory is the one that diverged. From batch ``--start`` of epoch 2 on, every step
+is teacher-forced: from the parameters the plugin holds before the step and with the step's own
+drop-edge structures and dropout masks (recorded, not re-drawn), the reference's torch calls
+(tests/_ref64.py: HCCF.py:61-97, 173-191, util/loss_torch.py) give the batch loss and every
+parameter gradient in float64 — and in float32, for the reference's own rounding — which are
+compared with what the plugin computed and its optimizer then applied. One JSON line per step:
+loss relative error, worst gradient row ratio (tests/_ref64.check_rows) against float64 and the
+reference-fp32's own, and the tables' magnitudes. Ends at the IndexError (or the epoch's end).
+
+    python scripts/diag/diag_zipf_teacher_forced.py [--start 200]
+"""
+import argparse
+import json
+import os
+import random
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--start", type=int, default=200)
+    ap.add_argument("--stop", type=int, default=10_000)
+    ap.add_argument("--users", type=int, default=31_668)
+    ap.add_argument("--items", type=int, default=38_048)
+    ap.add_argument("--train", type=int, default=1_170_000)
+    ap.add_argument("--test", type=int, default=390_000)
+    args = ap.parse_args()
+    import torch
+
+    import bench_plugin_epoch as E
+    from hypergraph_diffusion_for_recommendation_amd.plugins import HCCF
+    from hypergraph_diffusion_for_recommendation_amd.sampler import next_batch_pairwise
+    from hypergraph_diffusion_for_recommendation_amd.selfrec import (FileIO, ModelConf,
+                                                                     default_args)
+    from tests import _ref64 as R
+
+    tmp = tempfile.mkdtemp(prefix="hgd_zipf_tf_")
+    os.chdir(tmp)
+    d = os.path.join(tmp, "dataset", "yelp_synth")
+    E.write_files(d, args.users, args.items, args.train, args.test)
+    with open("HCCF.conf", "w") as f:
+        f.write(E.CONF)
+    conf = ModelConf("HCCF.conf")
+    kw = default_args(model="HCCF", dataset="yelp_synth", max_epoch=1, batch_size=4096,
+                      embedding_size=64, hyper_dim=32, n_layers=3, lrate=0.001, drop_rate=0.5,
+                      p=0.1, cl_rate=1e-4, temp=0.2, reg=0.1, item_ranking="10,20")
+    train = FileIO.load_data_set(d + "/train.txt")
+    test = FileIO.load_data_set(d + "/test.txt")
+    torch.manual_seed(0)
+    rec = HCCF(conf, train, test, None, **kw)
+    enc = rec.model
+    nu, ni, L = rec.data.n_users, rec.data.n_items, rec.nLayers
+    N = nu + ni
+    dropper = enc.edgeDropper
+    keep_h = 1 - enc.drop_rate
+
+    class DropoutRecorder(torch.nn.Module):
+        """The encoder's own nn.Dropout, its keep-masks read off its output (an element the mask
+        kept is nonzero unless its input was 0, where the mask does not matter)."""
+
+        def __init__(self, inner):
+            super().__init__()
+            self.inner, self.masks = inner, []
+
+        def forward(self, x):
+            y = self.inner(x)
+            if self.training:
+                self.masks.append((y != 0).cpu())
+            return y
+
+    enc.drop_out = DropoutRecorder(enc.drop_out)
+    enc.edgeDropper = R.DropRecorder(dropper)
+    captured = {}
+    ssl_loss = rec.ssl_loss
+
+    def ssl_capture(anchor_emb, pos_emb, *a, **k):  # the plugin's own anchor / positive rows
+        captured["anc"], captured["pos"] = anchor_emb.detach(), pos_emb.detach()
+        return ssl_loss(anchor_emb, pos_emb, *a, **k)
+
+    rec.ssl_loss = ssl_capture
+    print(json.dumps({"n_users": nu, "n_items": ni, "start": args.start}), flush=True)
+
+    def reference(P, dtype, drops, masks, u, i, j):
+        adjs = [R.sparse(di, dv, (N, N), dtype) for di, dv in drops]
+        ueR, ieR, gR, hR = R.hccf_encoder(P, adjs, [m.to(dtype) for m in masks], keep_h, nu, L)
+        anc, pos, neg = ueR[u], ieR[i], ieR[j]
+        nodes = []
+        for ref_rows, ours in ((anc, captured["anc"]), (pos, captured["pos"])):
+            mine = torch.unique(ref_rows.long())
+            theirs = torch.unique(ours.cpu().long())
+            if not torch.equal(mine, theirs):
+                # .long() of a value within rounding of an integer: take the plugin's list (as
+                # _ref64.ReluMasks does for a ReLU at 0) after checking that is the only cause
+                diff = (ref_rows.long() != ours.cpu().long())
+                gap = (ref_rows[diff] - ref_rows[diff].round()).abs().max()
+                nodes.append((theirs, float(gap)))
+            else:
+                nodes.append((mine, None))
+        ssl = 0
+        for layer in range(L):
+            e1, e2 = gR[layer].detach(), hR[layer]
+            ssl = ssl + R.contrast_loss(e1[:nu], e2[:nu], nodes[0][0], rec.temp) \
+                + R.contrast_loss(e1[nu:], e2[nu:], nodes[1][0], rec.temp)
+        loss = R.bpr_loss(anc, pos, neg) + ssl * rec.ss_rate
+        names = list(P)
+        grads = dict(zip(names, torch.autograd.grad(loss, [P[n] for n in names])))
+        mags = {"user_emb": float(ueR.abs().max()), "item_emb": float(ieR.abs().max()),
+                f"hyper[{L - 1}]": float(hR[-1].abs().max())}
+        return float(loss), grads, [g for _, g in nodes], mags
+
+    random.seed(1)
+    worst_all = 0.0
+    for ep, mode in enumerate(("cpu", "device")):
+        dropper.device_rng = mode == "device"
+        dropper.capture_safe = False
+        for b, (u, i, j) in enumerate(next_batch_pairwise(rec.data, rec.batchSize, device=rec.device)):
+            forced = ep == 1 and args.start <= b < args.stop
+            enc.drop_out.masks.clear()
+            enc.edgeDropper.outputs.clear()
+            before = ({n: p.detach().cpu().double() for n, p in enc.named_parameters()}
+                      if forced else None)
+            try:
+                got = float(rec.train_step(u, i, j).detach())
+            except Exception as e:  # noqa: BLE001
+                print(json.dumps({"epoch": ep, "batch": b, "mode": mode,
+                                  "raised": repr(e)[:300]}), flush=True)
+                print(json.dumps({"summary": "stopped at the exception", "worst_ratio_over_bound":
+                                  worst_all}), flush=True)
+                return 0
+            if not forced:
+                if b % 50 == 0:
+                    print(json.dumps({"epoch": ep, "batch": b, "mode": mode, "loss": got}),
+                          flush=True)
+                continue
+            drops = list(enc.edgeDropper.outputs[:L])
+            masks = list(enc.drop_out.masks[:2 * L])
+            assert len(drops) == L and len(masks) == 2 * L, (len(drops), len(masks))
+            uc, ic, jc = u.cpu(), i.cpu(), j.cpu()
+            P64 = {n: v.clone().requires_grad_(True) for n, v in before.items()}
+            P32 = {n: v.float().requires_grad_(True) for n, v in before.items()}
+            l64, g64, gaps, mags = reference(P64, torch.float64, drops, masks, uc, ic, jc)
+            l32, g32, _, _ = reference(P32, torch.float32, drops, masks, uc, ic, jc)
+            params = dict(enc.named_parameters())
+            rows, over = {}, 0.0
+            for n in g64:
+                own = R.check_rows(g32[n], g64[n], f"ref32 {n}", tol=1e9)
+                ours = R.check_rows(params[n].grad, g64[n], f"{n}", tol=1e9)
+                rows[n] = [ours, own]
+                over = max(over, ours / max(R.TOL, own))
+            loss_rel = abs(got - l64) / abs(l64)
+            loss_rel32 = abs(l32 - l64) / abs(l64)
+            over = max(over, loss_rel / max(R.TOL, loss_rel32))
+            worst_all = max(worst_all, over)
+            print(json.dumps({"epoch": ep, "batch": b, "mode": mode, "loss": got,
+                              "loss_ref64": l64, "loss_rel": loss_rel, "loss_rel_ref32": loss_rel32,
+                              "grad_row_ratio": rows, "ratio_over_bound": over,
+                              "within_bound": over <= 1.0, "node_list_gaps": gaps,
+                              "max_abs_ref64": mags}), flush=True)
+    print(json.dumps({"summary": "epochs finished", "worst_ratio_over_bound": worst_all}),
+          flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

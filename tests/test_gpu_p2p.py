@@ -270,3 +270,57 @@ def test_native_conv2hop_over_p2p_equals_python_p2p_conv(dev, tmp_path):
         res = torch.load(str(tmp_path / f"r{r}.pt"), weights_only=True)
         assert res == {"scale_equal": True, "conv_equal": [True] * 3,
                        "allreduce_equal": True}, (r, res)
+
+
+def _sharded_with_p2p(dev, items=1 << 20, d=64):
+    """A one-rank ShardedIncidence whose peer transport is up (4 slots of items·d floats)."""
+    from hypergraph_diffusion_for_recommendation_amd import Incidence
+    from hypergraph_diffusion_for_recommendation_amd.sharded import ShardedIncidence
+    idx = torch.tensor([[0, 1, 2, 3], [0, 5, items - 1, 7]], device=dev)
+    sh = ShardedIncidence(Incidence.from_coo(idx, None, (4, items), device=dev))
+    return sh, sh.p2p(d)
+
+
+def _free_bytes(dev):
+    import gc
+    gc.collect()
+    torch.cuda.synchronize(dev)
+    torch.cuda.empty_cache()
+    return torch.cuda.mem_get_info(dev)[0]
+
+
+def test_p2p_segments_freed_when_dropped_without_close(dev):
+    """A ShardedIncidence dropped without close() frees its exported segments (hipMemGetInfo
+    back to where it was): no global keeps the exchange alive through its cached slot views."""
+    from hypergraph_diffusion_for_recommendation_amd import _native as nat
+    items, d = 1 << 20, 64
+    slots_bytes = 4 * items * d * 4  # 2 send + 2 reduced slots of 256 MB
+    free0 = _free_bytes(dev)
+    live0 = nat.live_views()
+    sh, ex = _sharded_with_p2p(dev, items, d)
+    ex.slot(0, items, d).fill_(1.0)
+    free1 = _free_bytes(dev)
+    assert free0 - free1 >= slots_bytes, (free0, free1)
+    del sh, ex
+    free2 = _free_bytes(dev)
+    assert free0 - free2 < slots_bytes // 8, (free0, free2)
+    assert nat.live_views() == live0
+
+
+def test_p2p_slot_view_held_past_close_stays_valid(dev):
+    """close() makes the exchange unusable, but a slot view handed out before it keeps its memory
+    alive (never a view of freed memory); the memory goes with the last view's storage."""
+    items, d = 1 << 20, 64
+    slots_bytes = 4 * items * d * 4
+    free0 = _free_bytes(dev)
+    sh, ex = _sharded_with_p2p(dev, items, d)
+    v = ex.slot(1, items, d)[10:20]  # a view of the view: the storage outlives the slot tensor
+    sh.close()
+    with pytest.raises(RuntimeError, match="closed"):
+        ex.slot(1, items, d)
+    assert free0 - _free_bytes(dev) >= slots_bytes  # still mapped: v points at live memory
+    v.fill_(3.0)
+    assert bool((v == 3.0).all())
+    del v
+    assert free0 - _free_bytes(dev) < slots_bytes // 8
+    del sh, ex
