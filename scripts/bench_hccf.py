@@ -12,6 +12,8 @@ reference calls it) and Adam. Variants:
                      capture-safe drop-edge, device-side InfoNCE node counts, capturable Adam);
 * hgd_graph_cpu_mask — the same replay with the masks of the reference's CPU torch.rand stream,
                      drawn on the host before each replay (SpAdjDropEdge.refill);
+* hgd_graph_ref_adam — the hgd_graph_cpu_mask replay holding only the forward + backward, the
+                     reference's Adam (torch.optim.Adam(lr=float)) stepping eagerly after it;
 * hgd_capture_safe_eager — the graph variant's ops (device mask), launched eagerly;
 * hgd_cs_eager_cpu_mask — eager, capture-safe drop-edge views (the reference's CPU mask stream
                      through the per-call slots), device-side InfoNCE counts, fused BPR, the
@@ -70,9 +72,11 @@ def main():
                 torch.randint(0, ni, (args.batch,), device=dev, generator=g)) for _ in range(8)]
 
     def make_step(model, loss_fn, unique, hoist=True, graph=False, counted=None, host_fed=None,
-                  fused_adam=None):
+                  fused_adam=None, adam_after_replay=False):
+        # adam_after_replay: the graph holds the forward + backward only; the reference's Adam
+        # (torch.optim.Adam(lr=float), non-capturable) steps eagerly after each replay
         counted = graph if counted is None else counted
-        fused_adam = counted if fused_adam is None else fused_adam
+        fused_adam = (counted and not adam_after_replay) if fused_adam is None else fused_adam
         if fused_adam:
             lr = torch.tensor(conf["lrate"], dtype=torch.float32, device=dev)
             opt = torch.optim.Adam(model.parameters(), lr=lr, capturable=True, fused=True)
@@ -105,23 +109,33 @@ def main():
             opt.zero_grad()
             torch.nn.utils.clip_grad_norm_(model.parameters(), 4)  # before backward, as HCCF.py:95
             loss.backward()
-            opt.step()
+            if not adam_after_replay:
+                opt.step()
             return loss
 
         def step():
             uid, pid, nid = batches[state["k"] % len(batches)]
             state["k"] += 1
             if not graph:
-                return body(uid, pid, nid)
+                out = body(uid, pid, nid)
+                if adam_after_replay:
+                    opt.step()
+                return out
             if state["cap"] is None:
                 if state["k"] == 1:
-                    return body(uid, pid, nid)  # one eager step: optimizer state, handles
+                    out = body(uid, pid, nid)  # one eager step: optimizer state, handles
+                    if adam_after_replay:
+                        opt.step()
+                    return out
                 if host_fed is not None:  # the reference's CPU mask stream, drawn per replay
                     host_fed.host_fed(True)
                 state["cap"] = CapturedStep(body, (uid, pid, nid),
                                             before_replay=None if host_fed is None
                                             else host_fed.refill)
-            return state["cap"](uid, pid, nid)
+            out = state["cap"](uid, pid, nid)
+            if adam_after_replay:
+                opt.step()
+            return out
         return step
 
     def timed(step):
@@ -167,6 +181,16 @@ def main():
         out.append(("hgd_graph_cpu_mask", timed(make_step(c_model, contrast_loss, unique_long_n,
                                                           graph=True,
                                                           host_fed=c_model.edgeDropper))))
+    if "hgd_graph_ref_adam" in want:  # replayed fwd + bwd on the reference's CPU mask stream,
+        torch.manual_seed(0)             # the reference's Adam eagerly after each replay
+        a_model = HCCFEncoder(conf, data, dev)
+        a_model.load_state_dict(ours.state_dict())
+        a_model.edgeDropper.device_rng = False
+        a_model.edgeDropper.capture_safe = True
+        out.append(("hgd_graph_ref_adam", timed(make_step(a_model, contrast_loss, unique_long_n,
+                                                          graph=True,
+                                                          host_fed=a_model.edgeDropper,
+                                                          adam_after_replay=True))))
     if "hgd_capture_safe_eager" in want:  # the graph variant's ops, launched eagerly
         torch.manual_seed(0)
         e_model = HCCFEncoder(conf, data, dev)
