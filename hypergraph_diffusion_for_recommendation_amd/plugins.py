@@ -96,16 +96,22 @@ class HCCF(GraphRecommender):
 
     def _init_optimizer(self, kwargs):
         # hgd_graph: the training step replayed from one HIP graph (graphs.CapturedStep) — the
-        # device drop-edge mask from a device seed counter, device-side InfoNCE node counts and a
-        # capturable Adam (its lr a device tensor the scheduler updates in place); the same math
+        # drop-edge masks as views filled before each replay, device-side InfoNCE node counts.
+        # The optimizer is the reference's torch.optim.Adam(lr=float) (HCCF.py:33), stepping
+        # eagerly after each replay of the forward + backward, so replayed steps are bitwise the
+        # eager steps; hgd_capturable_adam=True puts a capturable fused Adam inside the graph
+        # instead (one launch less per step, but not the reference's rounding of the bias
+        # corrections: scripts/diag/diag_adam_bitwise.py)
         self.graph_mode = bool(kwargs.get('hgd_graph', False))
         self._captured = None
+        self._adam_in_graph = self.graph_mode and bool(kwargs.get('hgd_capturable_adam', False))
         if self.graph_mode:
             # the drop-edge masks stay the reference's CPU torch.rand stream (drawn on the host
             # before each replay into the buffers the graph reads) unless hgd_device_rng asks
             # for device draws
             self.model.edgeDropper.device_rng = bool(kwargs.get('hgd_device_rng', False))
             self.model.edgeDropper.capture_safe = True
+        if self._adam_in_graph:
             lr = torch.tensor(self.lRate, dtype=torch.float32, device=self.device)
             # fused: one multi-tensor kernel per step instead of the ~15 foreach passes
             self.optimizer = torch.optim.Adam(self.model.parameters(), lr=lr, capturable=True,
@@ -160,6 +166,13 @@ class HCCF(GraphRecommender):
 
     def train_step(self, user_idx, pos_idx, neg_idx) -> torch.Tensor:
         """One batch of HCCF.py:79-97; returns the (device) batch loss."""
+        batch_loss = self.forward_backward(user_idx, pos_idx, neg_idx)
+        self.optimizer.step()
+        return batch_loss
+
+    def forward_backward(self, user_idx, pos_idx, neg_idx) -> torch.Tensor:
+        """:meth:`train_step` up to the optimizer step (HCCF.py:79-95): the parameters' .grad
+        hold the batch's gradients afterwards."""
         model = self.model
         model.train()
         user_emb, item_emb, gcnEmbedsLst, hyperEmbedsLst = model(keep_rate=1 - self.dropRate)
@@ -172,7 +185,6 @@ class HCCF(GraphRecommender):
         self.optimizer.zero_grad()
         torch.nn.utils.clip_grad_norm_(model.parameters(), 4)  # before backward, as :95
         batch_loss.backward()
-        self.optimizer.step()
         return batch_loss
 
     def graph_step(self, user_idx, pos_idx, neg_idx) -> torch.Tensor:
@@ -190,19 +202,30 @@ class HCCF(GraphRecommender):
             self.model.edgeDropper.host_fed(not self.model.edgeDropper.device_rng)
             return out
         if cap is not None and full:
-            return cap(user_idx, pos_idx, neg_idx).detach().clone()
+            return self._replay(user_idx, pos_idx, neg_idx)
         if cap is None and full and getattr(self, "_eager_steps", 0) >= 1:
             from .graphs import CapturedStep
             dropper = self.model.edgeDropper
             host_fed = not dropper.device_rng
             dropper.host_fed(host_fed)  # the capture records the slots; refill() fills them
-            self._captured = CapturedStep(self.train_step, (user_idx, pos_idx, neg_idx),
+            body = self.train_step if self._adam_in_graph else self.forward_backward
+            self._captured = CapturedStep(body, (user_idx, pos_idx, neg_idx),
                                           before_replay=dropper.refill if host_fed else None)
-            return self._captured(user_idx, pos_idx, neg_idx).detach().clone()
+            # the gradient buffers the replays write (an eager short batch rebinds .grad)
+            self._graph_grads = [p.grad for p in self.model.parameters()]
+            return self._replay(user_idx, pos_idx, neg_idx)
         self._eager_steps = getattr(self, "_eager_steps", 0) + 1
         # detached: a caller holding the loss would keep the eager autograd graph — and with it
         # the parameters' AccumulateGrad nodes, bound to the eager stream — alive into the capture
         return self.train_step(user_idx, pos_idx, neg_idx).detach()
+
+    def _replay(self, user_idx, pos_idx, neg_idx) -> torch.Tensor:
+        out = self._captured(user_idx, pos_idx, neg_idx).detach().clone()
+        if not self._adam_in_graph:  # the reference's Adam on the replay's gradients
+            for p, g in zip(self.model.parameters(), self._graph_grads):
+                p.grad = g
+            self.optimizer.step()
+        return out
 
     def train(self, load_pretrained=False):  # HCCF.py:72-118
         model = self.model

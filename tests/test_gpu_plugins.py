@@ -161,6 +161,39 @@ def test_hccf_steps_match_reference_ops(dev, tmp_path, monkeypatch):
     print(f"HCCF plugin steps: worst gradient row ratio {worst:.2e}")
 
 
+@pytest.mark.parametrize("model", ["HCCF", "HCCF_diffusion"])
+def test_graph_mode_steps_equal_eager_default_steps(dev, tmp_path, monkeypatch, model):
+    """hgd_graph=True — the forward + backward replayed from one HIP graph, the reference's
+    torch.optim.Adam(lr=float) (HCCF.py:33) stepping eagerly after each replay — takes bit for
+    bit the steps of the eager default: same batches, the same CPU drop-edge stream (drawn before
+    each replay), a short last batch run eagerly in between, and parameters and losses equal
+    after two epochs' worth of steps."""
+    from hypergraph_diffusion_for_recommendation_amd import plugins
+    from hypergraph_diffusion_for_recommendation_amd.sampler import next_batch_pairwise
+    from hypergraph_diffusion_for_recommendation_amd.selfrec import FileIO
+    conf, kwargs = _setup(tmp_path, monkeypatch, model)
+    kwargs.pop('dataset_root')
+    d = str(tmp_path / "dataset" / "toy") + "/"
+    runs = []
+    for graph in (False, True):
+        torch.manual_seed(0)
+        rec = getattr(plugins, model)(conf, FileIO.load_data_set(d + "train.txt"),
+                                      FileIO.load_data_set(d + "test.txt"), None,
+                                      **dict(kwargs, hgd_graph=graph))
+        random.seed(4)
+        losses = []
+        for _ep in range(2):
+            for b in next_batch_pairwise(rec.data, rec.batchSize, device=dev):
+                losses.append(float(rec.graph_step(*b)))
+        assert (rec._captured is not None) == graph
+        runs.append((losses, [p.detach().clone() for p in rec.model.parameters()],
+                     torch.get_rng_state()))
+    (l0, p0, s0), (l1, p1, s1) = runs
+    assert l0 == l1
+    assert all(torch.equal(a, b) for a, b in zip(p0, p1))
+    assert torch.equal(s0, s1)  # the CPU generator ends where the eager draws leave it
+
+
 def test_hgnn_hd4_rejects_broken_modes(dev, tmp_path, monkeypatch):
     from hypergraph_diffusion_for_recommendation_amd.selfrec import SELFRec
     conf, kwargs = _setup(tmp_path, monkeypatch, "HGNN_HD4", mode="full")
