@@ -186,7 +186,13 @@ __device__ __forceinline__ int compact_kept(const SpmmArgs& a, int l, int keep, 
 // register a, slot j >= G in lane j-G's register b — so a step gathers as many rows as an
 // unmasked batch instead of half as many; the next pair of index batches is loaded before the
 // gathers are issued. Sums in edge order: bitwise the one-batch walk and the compacted matrix's.
-template <int G, int VEC, int U, bool HAS_VAL, int POL>
+// PUSH (HGD_TUNE_MASK_PAIR = 2, the default): the packing is ONE forward permute per value and
+// batch — each lane sends its entry to its slot (its rank among the kept entries of its batch,
+// from a popcount of the lower lanes' keep bits; the dropped entries fill the slots after the
+// kept ones, so every batch is a permutation of the group's lanes and no two lanes collide) —
+// instead of every lane pulling its slot's entry after a binary search for the j-th set bit
+// (nth_set_bit, three per step: ~4 dependent popcount rounds each). Same slots, same sums.
+template <int G, int VEC, int U, bool HAS_VAL, int POL, bool PUSH>
 __device__ __forceinline__ void gather_sum_mask2(const SpmmArgs& a, int64_t e0, int64_t e1,
                                                  int l, bool col_ok, float (&acc)[VEC]) {
 #pragma unroll
@@ -218,19 +224,44 @@ __device__ __forceinline__ void gather_sum_mask2(const SpmmArgs& a, int64_t e0, 
     const float w1 = nw1, w2 = nw2;
     if (eb + 2 * G < e1) load2(eb + 2 * G, nc1, nw1, nk1, nc2, nw2, nk2);
     const unsigned long long gm1 = group_bits(k1), gm2 = group_bits(k2);
-    const int n1 = __popcll(gm1), n = n1 + __popcll(gm2);
+    const int n1 = __popcll(gm1), n2 = __popcll(gm2), n = n1 + n2;
     if (n == 0) continue;  // group-uniform
     // slot l (register a) and slot l + G (register b) of the packed pair
-    const int s1 = nth_set_bit<G>(gm1, l);
-    const int s2a = nth_set_bit<G>(gm2, l >= n1 ? l - n1 : 0);
-    const int s2b = nth_set_bit<G>(gm2, l + G - n1 < G ? l + G - n1 : 0);
-    const int ca1 = __shfl(c1, s1, G), ca2 = __shfl(c2, s2a, G), cb = __shfl(c2, s2b, G);
-    const int ca = l < n1 ? ca1 : ca2;
+    int ca, cb;
     float wa = 1.f, wb = 1.f;
-    if constexpr (HAS_VAL) {
-      const float wa1 = __shfl(w1, s1, G), wa2 = __shfl(w2, s2a, G);
-      wa = __fdiv_rn(l < n1 ? wa1 : wa2, a.keep);  // vals[mask] / keepRate (HCCF.py:224)
-      wb = __fdiv_rn(__shfl(w2, s2b, G), a.keep);
+    if constexpr (PUSH) {
+      const unsigned long long below = (1ull << l) - 1ull;  // the group's lanes below l
+      const int r1 = __popcll(gm1 & below), r2 = __popcll(gm2 & below);
+      // batch 1 → slots [0, G) of register a; batch 2 → slot n1 + rank, i.e. register a of lane
+      // (n1 + rank) for slots < G and register b of lane (n1 + rank − G) beyond: one permute
+      // modulo G serves both, and each lane's a / b pick (l < n1) is the pull form's
+      const int d1 = k1 ? r1 : n1 + (l - r1);
+      const int d2 = ((k2 ? r2 : n2 + (l - r2)) + n1) & (G - 1);
+      const int a1 = 4 * (base + d1), a2 = 4 * (base + d2);
+      const int x1 = __builtin_amdgcn_ds_permute(a1, c1);
+      const int x2 = __builtin_amdgcn_ds_permute(a2, c2);
+      ca = l < n1 ? x1 : x2;
+      cb = x2;
+      if constexpr (HAS_VAL) {
+        // vals[mask] / keepRate (HCCF.py:224), divided before the move (same IEEE quotient)
+        const float v1 = __fdiv_rn(w1, a.keep), v2 = __fdiv_rn(w2, a.keep);
+        const float y1 = __int_as_float(__builtin_amdgcn_ds_permute(a1, __float_as_int(v1)));
+        const float y2 = __int_as_float(__builtin_amdgcn_ds_permute(a2, __float_as_int(v2)));
+        wa = l < n1 ? y1 : y2;
+        wb = y2;
+      }
+    } else {
+      const int s1 = nth_set_bit<G>(gm1, l);
+      const int s2a = nth_set_bit<G>(gm2, l >= n1 ? l - n1 : 0);
+      const int s2b = nth_set_bit<G>(gm2, l + G - n1 < G ? l + G - n1 : 0);
+      const int ca1 = __shfl(c1, s1, G), ca2 = __shfl(c2, s2a, G);
+      cb = __shfl(c2, s2b, G);
+      ca = l < n1 ? ca1 : ca2;
+      if constexpr (HAS_VAL) {
+        const float wa1 = __shfl(w1, s1, G), wa2 = __shfl(w2, s2a, G);
+        wa = __fdiv_rn(l < n1 ? wa1 : wa2, a.keep);  // vals[mask] / keepRate (HCCF.py:224)
+        wb = __fdiv_rn(__shfl(w2, s2b, G), a.keep);
+      }
     }
     for (int k = 0; k < n; k += U) {
       const bool hi = k >= G;  // group-uniform: U divides G, so a step stays in one register
@@ -331,15 +362,19 @@ __device__ __forceinline__ void gather_sum(const SpmmArgs& a, int64_t e0, int64_
   }
 }
 
-int g_mask_pair = 1;  // HGD_TUNE_MASK_PAIR: the masked hop walks two index batches per step
+int g_mask_pair = 2;  // HGD_TUNE_MASK_PAIR: the masked hop walks two index batches per step
 
 // MASK with G >= 8 lanes (U | G): the two-batch masked walk unless HGD_TUNE_MASK_PAIR is 0.
 template <int G, int VEC, int U, bool HAS_VAL, int POL, bool MASK>
 __device__ __forceinline__ void masked_or_plain_sum(const SpmmArgs& a, int64_t e0, int64_t e1,
                                                     int l, bool col_ok, float (&acc)[VEC]) {
   if constexpr (MASK && G >= 8 && G % U == 0) {
+    if (a.mask_pair == 2) {
+      gather_sum_mask2<G, VEC, U, HAS_VAL, POL, true>(a, e0, e1, l, col_ok, acc);
+      return;
+    }
     if (a.mask_pair) {
-      gather_sum_mask2<G, VEC, U, HAS_VAL, POL>(a, e0, e1, l, col_ok, acc);
+      gather_sum_mask2<G, VEC, U, HAS_VAL, POL, false>(a, e0, e1, l, col_ok, acc);
       return;
     }
   }
@@ -888,7 +923,7 @@ extern "C" hgd_status hgd_set_tuning(int32_t key, int32_t value) {
       set_p2p_grid(value);
       return HGD_OK;
     case HGD_TUNE_MASK_PAIR:
-      HGD_REQUIRE(value == 0 || value == 1, "hgd_set_tuning: mask pair must be 0 or 1");
+      HGD_REQUIRE(value >= 0 && value <= 2, "hgd_set_tuning: mask pair must be 0, 1 or 2");
       g_mask_pair = value;
       return HGD_OK;
     case HGD_TUNE_CPU_RNG_THREADS:

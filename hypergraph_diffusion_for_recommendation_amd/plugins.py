@@ -86,6 +86,11 @@ def _device_drop_edge(dropper, kwargs) -> None:
 class HCCF(GraphRecommender):
     """model/graph/HCCF.py:26-133."""
 
+    # the training loop replays its steps from a HIP graph unless hgd_graph=False (or the
+    # compacted drop-edge children are asked for): bitwise the eager steps, ~1.3 vs ~1.9 ms per
+    # Yelp-shaped step (DESIGN.md §4.11)
+    _graph_default = True
+
     def __init__(self, conf, training_set, test_set, knowledge_set, **kwargs):
         GraphRecommender.__init__(self, conf, training_set, test_set, knowledge_set, **kwargs)
         self.model = HCCFEncoder(kwargs, self.data, self.device)
@@ -102,7 +107,8 @@ class HCCF(GraphRecommender):
         # eager steps; hgd_capturable_adam=True puts a capturable fused Adam inside the graph
         # instead (one launch less per step, but not the reference's rounding of the bias
         # corrections: scripts/diag/diag_adam_bitwise.py)
-        self.graph_mode = bool(kwargs.get('hgd_graph', False))
+        default = self._graph_default and not kwargs.get('hgd_compact_drop', False)
+        self.graph_mode = bool(kwargs.get('hgd_graph', default))
         self._captured = None
         self._adam_in_graph = self.graph_mode and bool(kwargs.get('hgd_capturable_adam', False))
         if self.graph_mode:
@@ -672,6 +678,8 @@ class HCCF_sharded(_ShardedPlugin, HCCF):
     user table once per epoch and runs the single-GPU device evaluation; rank 0 writes the
     result files. With ``drop_rate`` 0 and the reference's CPU drop-edge stream it takes the
     same steps as :class:`HCCF` on one GPU (``tests/test_gpu_plugins.py``)."""
+
+    _graph_default = False  # its steps all-reduce: no graph replay
 
     def __init__(self, conf, training_set, test_set, knowledge_set, **kwargs):
         from .sharded_encoders import ShardedHCCFEncoder

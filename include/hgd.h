@@ -102,8 +102,10 @@ typedef enum hgd_epilogue {
  *                         sums as NaN instead of reading an unfilled buffer
  *   HGD_TUNE_P2P_GRID:    workgroups of the peer exchange's reduce / gather kernels (0 = default
  *                         256: the links bound them, the hops they overlap need the CUs)
- *   HGD_TUNE_MASK_PAIR:   the masked hop (hgd_spmm_masked*) walks two index batches per step
- *                         (1, default) or one (0); the sums are the same bits either way */
+ *   HGD_TUNE_MASK_PAIR:   the masked hop (hgd_spmm_masked*) walks two index batches per step,
+ *                         their kept entries packed by forward permutes (2, default) or by
+ *                         set-bit searches and pulls (1), or one batch per step (0); the sums
+ *                         are the same bits every way */
 typedef enum hgd_tune_key {
   HGD_TUNE_SPMM_UNROLL = 1,
   HGD_TUNE_SPMM_POLICY = 2,

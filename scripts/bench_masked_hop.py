@@ -4,7 +4,8 @@ Yelp-shaped norm_adj, d = 64) three ways, event-timed medians:
 
 * full       — the parent adjacency, nothing dropped (every edge gathered);
 * masked     — the masked view (hgd_spmm_masked: every parent edge's index read, the kept ones
-               compacted per lane group and gathered) — the plugins' default;
+               compacted per lane group and gathered) — the plugins' default; also timed with
+               the older packing forms (masked_pair1_us, masked_pair0_us);
 * compacted  — the compacted child (Incidence.drop): only kept edges stored.
 
 Prints one JSON line."""
@@ -50,9 +51,19 @@ def main():
             ts.append(e0.elapsed_time(e1) * 1e3)
         return round(statistics.median(ts), 2)
 
+    from hypergraph_diffusion_for_recommendation_amd import _native as nat
+    lib = nat.load()
     out = {"nnz": inc.nnz, "kept": child.nnz, "d": d}
     for name, m in (("full", inc), ("masked", view), ("compacted", child)):
         out[f"{name}_us"] = timed(lambda m=m: spmm_csr(m.csr, X, m.val))
+    # the masked walk's packing forms (HGD_TUNE_MASK_PAIR: 2 push permutes, the default; 1 pull
+    # after set-bit searches; 0 one batch per step)
+    try:
+        for pair in (1, 0):
+            nat.check(lib.hgd_set_tuning(15, pair), "hgd_set_tuning")
+            out[f"masked_pair{pair}_us"] = timed(lambda: spmm_csr(view.csr, X, view.val))
+    finally:
+        nat.check(lib.hgd_set_tuning(15, 2), "hgd_set_tuning")
     print(json.dumps(out), flush=True)
 
 

@@ -27,7 +27,7 @@ def main():
         for cs in (False, True):
             with redirect_stdout(io.StringIO()):
                 ratios = T._hccf_case(dev, T.LASTFM, 32, 1, seed=seed, capture_safe=cs,
-                                      fp32_bound=True)
+                                      fp32_record=True)
             worst_k = max(ratios, key=lambda k: ratios[k][0] / max(R.TOL, ratios[k][1]))
             print(json.dumps({
                 "seed": seed, "path": "view" if cs else "compacted",

@@ -35,6 +35,9 @@ def main():
     ap.add_argument("--items", type=int, default=38_048)
     ap.add_argument("--train", type=int, default=1_170_000)
     ap.add_argument("--test", type=int, default=390_000)
+    ap.add_argument("--analyze", type=int, default=4,
+                    help="decompose the first N steps over the bound (forward outputs, the BPR "
+                         "and InfoNCE gradients apart, a bitwise re-run of the step)")
     args = ap.parse_args()
     import torch
 
@@ -91,7 +94,7 @@ def main():
     rec.ssl_loss = ssl_capture
     print(json.dumps({"n_users": nu, "n_items": ni, "start": args.start}), flush=True)
 
-    def reference(P, dtype, drops, masks, u, i, j):
+    def reference(P, dtype, drops, masks, u, i, j, parts=False):
         adjs = [R.sparse(di, dv, (N, N), dtype) for di, dv in drops]
         ueR, ieR, gR, hR = R.hccf_encoder(P, adjs, [m.to(dtype) for m in masks], keep_h, nu, L)
         anc, pos, neg = ueR[u], ieR[i], ieR[j]
@@ -112,15 +115,102 @@ def main():
             e1, e2 = gR[layer].detach(), hR[layer]
             ssl = ssl + R.contrast_loss(e1[:nu], e2[:nu], nodes[0][0], rec.temp) \
                 + R.contrast_loss(e1[nu:], e2[nu:], nodes[1][0], rec.temp)
-        loss = R.bpr_loss(anc, pos, neg) + ssl * rec.ss_rate
+        bpr = R.bpr_loss(anc, pos, neg)
+        loss = bpr + ssl * rec.ss_rate
         names = list(P)
+        if parts:  # the encoder's outputs and the two losses' gradients apart
+            gb = dict(zip(names, torch.autograd.grad(bpr, [P[n] for n in names],
+                                                     retain_graph=True)))
+            gs = dict(zip(names, torch.autograd.grad(ssl * rec.ss_rate, [P[n] for n in names])))
+            return (ueR, ieR, gR, hR), gb, gs
         grads = dict(zip(names, torch.autograd.grad(loss, [P[n] for n in names])))
         mags = {"user_emb": float(ueR.abs().max()), "item_emb": float(ieR.abs().max()),
                 f"hyper[{L - 1}]": float(hR[-1].abs().max())}
         return float(loss), grads, [g for _, g in nodes], mags
 
+    from hypergraph_diffusion_for_recommendation_amd.functional import bpr_loss_rows
+    adj_idx = enc.sparse_norm_adj._indices()
+    node_deg = torch.bincount(adj_idx[0], minlength=N).cpu()
+
+    def worst_row(got, ref):
+        g = got.detach().cpu().double()
+        r = ref.detach().cpu().double()
+        if g.dim() == 1:
+            g, r = g[None], r[None]
+        err = (g - r).abs().amax(1)
+        scale = r.abs().amax(1)
+        ratio = torch.where(scale == 0, err, err / scale.clamp_min(1e-300))
+        k = int(ratio.argmax())
+        return {"ratio": float(ratio[k]), "row": k, "err": float(err[k]),
+                "scale": float(scale[k]), "rows_over_1e-5": int((ratio > 1e-5).sum())}
+
+    def analyze(b, u, i, j, before, pre_rng, drops, masks):
+        """Re-runs the bad step from its start: the same parameters and RNG states (so the same
+        drop-edge and dropout draws), the forward outputs and the BPR / InfoNCE gradients apart
+        against float64, and whether the re-run's total gradient is bitwise the step's."""
+        params = dict(enc.named_parameters())
+        step_grads = {n: p.grad.detach().clone() for n, p in params.items()}
+        post = {n: p.detach().clone() for n, p in params.items()}
+        post_rng = (torch.get_rng_state(), torch.cuda.get_rng_state())
+        with torch.no_grad():
+            for n, p in params.items():
+                p.copy_(before[n].to(device=p.device, dtype=p.dtype))
+        torch.set_rng_state(pre_rng[0])
+        torch.cuda.set_rng_state(pre_rng[1])
+        enc.drop_out.masks.clear()
+        enc.edgeDropper.outputs.clear()
+        enc.zero_grad(set_to_none=True)
+        ue, ie, gcn, hyp = enc(keep_rate=1 - rec.dropRate)
+        same_draws = (all(torch.equal(a[0], b_[0]) and torch.equal(a[1], b_[1])
+                          for a, b_ in zip(enc.edgeDropper.outputs[:L], drops)) and
+                      all(torch.equal(a, b_) for a, b_ in zip(enc.drop_out.masks[:2 * L], masks)))
+        bpr, anc, pos = bpr_loss_rows(ue, ie, u, i, j)
+        names = list(params)
+        gb = dict(zip(names, torch.autograd.grad(bpr, [params[n] for n in names],
+                                                 retain_graph=True, allow_unused=True)))
+        ssl = rec.ssl_loss(anc, pos, gcn, hyp)
+        gs = dict(zip(names, torch.autograd.grad(ssl, [params[n] for n in names],
+                                                 allow_unused=True)))
+        P64 = {n: v.clone().requires_grad_(True) for n, v in before.items()}
+        (ueR, ieR, gR, hR), gbR, gsR = reference(P64, torch.float64, drops, masks, u.cpu(),
+                                                 i.cpu(), j.cpu(), parts=True)
+        rep = {"batch": b, "analysis": True, "same_draws_on_rerun": same_draws,
+               "forward": {"user_emb": worst_row(ue, ueR), "item_emb": worst_row(ie, ieR)}}
+        for layer in range(L):
+            rep["forward"][f"gcn[{layer}]"] = worst_row(gcn[layer], gR[layer])
+            rep["forward"][f"hyper[{layer}]"] = worst_row(hyp[layer], hR[layer])
+        rep["bpr_grad"] = {n: worst_row(gb[n] if gb[n] is not None else torch.zeros_like(
+            params[n]), gbR[n]) for n in names}
+        rep["ssl_grad"] = {n: worst_row(gs[n] if gs[n] is not None else torch.zeros_like(
+            params[n]), gsR[n]) for n in names}
+        rerun = {n: (gb[n] if gb[n] is not None else 0) + (gs[n] if gs[n] is not None else 0)
+                 for n in names}
+        rep["rerun_total_equals_step"] = {n: bool(torch.equal(rerun[n], step_grads[n]))
+                                          for n in names}
+        rep["rerun_vs_step_max_abs"] = {n: float((rerun[n] - step_grads[n]).abs().max())
+                                        for n in names}
+        # the worst rows of the step's own gradient: how often in the batch, graph degree
+        uc, ic, jc = u.cpu(), i.cpu(), j.cpu()
+        for n, off, ids in (("embedding_dict.item_emb", nu, (ic, jc)),
+                            ("embedding_dict.user_emb", 0, (uc,))):
+            gR_tot = gbR[n] + gsR[n]
+            w = worst_row(step_grads[n], gR_tot)
+            k = w["row"]
+            w.update({"times_in_batch": [int((t == k).sum()) for t in ids],
+                      "node_degree": int(node_deg[off + k]),
+                      "max_degree": int(node_deg[off:off + (ni if off else nu)].max())})
+            rep[f"step_worst_{n[15:]}"] = w
+        print(json.dumps(rep), flush=True)
+        with torch.no_grad():
+            for n, p in params.items():
+                p.copy_(post[n])
+                p.grad = step_grads[n]
+        torch.set_rng_state(post_rng[0])
+        torch.cuda.set_rng_state(post_rng[1])
+
     random.seed(1)
     worst_all = 0.0
+    analyzed = 0
     for ep, mode in enumerate(("cpu", "device")):
         dropper.device_rng = mode == "device"
         dropper.capture_safe = False
@@ -130,6 +220,7 @@ def main():
             enc.edgeDropper.outputs.clear()
             before = ({n: p.detach().cpu().double() for n, p in enc.named_parameters()}
                       if forced else None)
+            pre_rng = (torch.get_rng_state(), torch.cuda.get_rng_state()) if forced else None
             try:
                 got = float(rec.train_step(u, i, j).detach())
             except Exception as e:  # noqa: BLE001
@@ -167,6 +258,9 @@ def main():
                               "grad_row_ratio": rows, "ratio_over_bound": over,
                               "within_bound": over <= 1.0, "node_list_gaps": gaps,
                               "max_abs_ref64": mags}), flush=True)
+            if over > 10.0 and analyzed < args.analyze:
+                analyzed += 1
+                analyze(b, u, i, j, before, pre_rng, drops, masks)
     print(json.dumps({"summary": "epochs finished", "worst_ratio_over_bound": worst_all}),
           flush=True)
     return 0

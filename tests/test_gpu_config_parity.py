@@ -59,17 +59,16 @@ def _coo_host(adj):
 # HCCF (configs[0], configs[2])
 # ---------------------------------------------------------------------------------------------
 def _hccf_case(dev, shape, d, n_layers, seed, batch=4096, temp=1.0, cl_rate=0.01,
-               capture_safe=False, fp32_bound=False):
+               capture_safe=False, fp32_record=False):
     """One HCCF training step's forward and backward (HCCF.py:79-97): encoder with drop-edge
     (keep 1 - conf dropout 0.3) and learned-hypergraph dropout (--drop_rate 0.2), then
     HCCF.calcLosses (BPR + cl_rate · Σ_layers InfoNCE at conf temp), as the plugin computes it
     (plugins.HCCF.calcLosses: fused InfoNCE kernel, MFMA E·W and HGNN products).
 
     Every output, the loss and every parameter gradient are held to the row bound against the
-    reference's torch calls in float64. ``fp32_bound``: per tensor the bound is instead
-    max(1e-5, the reference's own torch calls evaluated in float32, against the same float64) —
-    our step may be no worse than the reference's arithmetic where a row is ill-conditioned in
-    fp32 (§7 of DESIGN.md). Returns {tensor: (ours, reference fp32 or None)} worst row ratios."""
+    reference's torch calls in float64. ``fp32_record``: the reference's own torch calls are also
+    evaluated in float32 and their deviation from the same float64 is recorded beside ours (§7 of
+    DESIGN.md). Returns {tensor: (ours, reference fp32 or None)} worst row ratios."""
     from hypergraph_diffusion_for_recommendation_amd.encoders import HCCFEncoder
     from hypergraph_diffusion_for_recommendation_amd.plugins import HCCF
     U, I, nnz = shape
@@ -132,14 +131,14 @@ def _hccf_case(dev, shape, d, n_layers, seed, batch=4096, temp=1.0, cl_rate=0.01
         got[f"gcn[{layer}]"], got[f"hyper[{layer}]"] = gcns[layer], hyps[layer]
     got.update((f"d {k}", p.grad) for k, p in enc.named_parameters())
     r64 = reference(torch.float64)
-    r32 = reference(torch.float32) if fp32_bound else None
+    r32 = reference(torch.float32) if fp32_record else None
     ratios = {}
     for k in r64:
         # (tol 1e-2: the fp32 reference must be the same computation — e.g. the same InfoNCE
         # node lists — or the bound it sets would be vacuous)
         own = None if r32 is None else R.check_rows(r32[k], r64[k], f"reference fp32 {k}",
                                                     tol=1e-2)
-        ours = R.check_rows(got[k], r64[k], k, tol=R.TOL if own is None else max(R.TOL, own))
+        ours = R.check_rows(got[k], r64[k], k)
         ratios[k] = (ours, own)
     worst = max(v[0] for v in ratios.values())
     print(f"HCCF {shape} d={d} L={n_layers} seed={seed} view={capture_safe}: worst row ratio "
@@ -160,17 +159,18 @@ def test_hccf_yelp_3layer_d64_infonce_train_step(dev):
 
 @pytest.mark.parametrize("view", [False, True], ids=["compacted", "view"])
 @pytest.mark.parametrize("seed", range(10, 20))
-def test_hccf_lastfm_seeds_no_worse_than_reference_fp32(dev, seed, view):
+def test_hccf_lastfm_seeds_row_bound(dev, seed, view):
     """configs[0] (LastFM HCCF, 1 layer, d = 32) over seeds 10-19 on both drop-edge paths (the
     compacted children and the plugins' default masked views; the drops are bit-exact either
-    way). The batch's InfoNCE node lists are torch.unique(emb.long()) (HCCF.py:65-66): small
-    integers, sometimes just [0], so a few gradient rows are sums with heavy cancellation. E.g.
-    at seed 13 the lists are [0], a one-node softmax whose loss is 0 in fp32 and 2e-10 in
-    float64, and the reference's own torch calls evaluated in float32 miss row 0 of the item /
-    user gradients by 6.1e-4 / 2.5e-5 of its scale. The row bound cannot hold for ANY fp32
-    evaluation of such a row; every tensor of our step is held to max(1e-5, the reference's own
-    fp32 deviation from float64) — no seed is dropped (DESIGN.md §7 lists the ratios)."""
-    _hccf_case(dev, LASTFM, 32, 1, seed=seed, capture_safe=view, fp32_bound=True)
+    way), every tensor at the 1e-5 row bound outright — no seed dropped. The batch's InfoNCE
+    node lists are torch.unique(emb.long()) (HCCF.py:65-66): small integers, often just [0], a
+    one-node softmax whose diagonal weight 1 − p = 1e-8/(e^s + 1e-8) rounds to 0 in fp32 when
+    formed as 1 − e/deno: the reference's own torch calls evaluated in float32 miss row 0 of
+    the item gradient by up to 6.1e-4 of its scale (seed 13; over 1e-5 on 8 of the 10 seeds).
+    The fused InfoNCE forms that weight from the off-diagonal mass (csrc/infonce.hip), so ours
+    holds 1e-5 where the reference's fp32 cannot; the reference-fp32 ratios are printed beside
+    ours (DESIGN.md §7 lists them)."""
+    _hccf_case(dev, LASTFM, 32, 1, seed=seed, capture_safe=view, fp32_record=True)
 
 
 @pytest.mark.parametrize("shape,d,layers,seed", [("LASTFM", 32, 1, 10), ("YELP", 64, 3, 20)])

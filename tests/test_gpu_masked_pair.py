@@ -1,5 +1,6 @@
-"""The masked hop's two-batch walk (hgd_spmm_masked, HGD_TUNE_MASK_PAIR = 1, the default) against
-the one-batch walk (0) and the compacted child (Incidence.drop): the same sums in the same edge
+"""The masked hop's two-batch walk (hgd_spmm_masked, HGD_TUNE_MASK_PAIR = 2, the default: kept
+entries packed by forward permutes; 1: by set-bit searches and pulls) against the one-batch walk
+(0) and the compacted child (Incidence.drop): the same sums in the same edge
 order, so bitwise — at every lane-group width (d = 16 … 256, including the one-batch fallback
 below 8 lanes), keep rates from sparse to dense, rows longer than the split threshold (the split
 plan's chunks walked the same way) and empty / fully dropped rows."""
@@ -41,13 +42,14 @@ def test_masked_pair_walk_bitwise(dev, d, keep, heavy):
     view = inc.masked(mask, keep)
     outs = {}
     try:
-        for pair in (1, 0):
+        for pair in (2, 1, 0):
             nat.check(lib.hgd_set_tuning(15, pair), "hgd_set_tuning")
             outs[pair] = (spmm_csr(view.csr, X, view.val), spmm_csr(view.csc, Xt, view.val_t))
     finally:
-        nat.check(lib.hgd_set_tuning(15, 1), "hgd_set_tuning")
-    assert torch.equal(outs[1][0], outs[0][0]) and torch.equal(outs[1][1], outs[0][1])
+        nat.check(lib.hgd_set_tuning(15, 2), "hgd_set_tuning")
+    for pair in (1, 0):
+        assert torch.equal(outs[2][0], outs[pair][0]) and torch.equal(outs[2][1], outs[pair][1])
     if not heavy:  # no split rows: the compacted child's hop is the same sums
         child = inc.drop(mask, keep)
-        assert torch.equal(outs[1][0], spmm_csr(child.csr, X, child.val))
-        assert torch.equal(outs[1][1], spmm_csr(child.csc, Xt, child.val_t))
+        assert torch.equal(outs[2][0], spmm_csr(child.csr, X, child.val))
+        assert torch.equal(outs[2][1], spmm_csr(child.csc, Xt, child.val_t))

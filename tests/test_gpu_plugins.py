@@ -79,7 +79,9 @@ def _setup(tmp_path, monkeypatch, model="HCCF", **over):
                                          ("HGCN", {}), ("HCCF_diffusion", {}), ("DHCF", {}),
                                          ("HCCF", {"hgd_device_rng": True}),
                                          ("HCCF", {"hgd_graph": True}),
-                                         ("HCCF_diffusion", {"hgd_graph": True})])
+                                         ("HCCF_diffusion", {"hgd_graph": True}),
+                                         ("HCCF", {"hgd_graph": False}),
+                                         ("HCCF_diffusion", {"hgd_graph": False})])
 def test_selfrec_execute_end_to_end(dev, tmp_path, monkeypatch, model, extra):
     from hypergraph_diffusion_for_recommendation_amd.selfrec import SELFRec
     conf, kwargs = _setup(tmp_path, monkeypatch, model, **extra)
