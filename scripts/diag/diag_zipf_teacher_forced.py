@@ -82,8 +82,21 @@ def main():
                 self.masks.append((y != 0).cpu())
             return y
 
+    class ChildRecorder(R.DropRecorder):
+        """R.DropRecorder that also keeps each output's device Incidence (the compacted child
+        the hops run over) for the hop-level checks of analyze()."""
+
+        def __init__(self, inner):
+            super().__init__(inner)
+            self.children = []
+
+        def forward(self, adj, keep):
+            out = super().forward(adj, keep)
+            self.children.append(getattr(out, "_hgd_incidence", None))
+            return out
+
     enc.drop_out = DropoutRecorder(enc.drop_out)
-    enc.edgeDropper = R.DropRecorder(dropper)
+    enc.edgeDropper = ChildRecorder(dropper)
     captured = {}
     ssl_loss = rec.ssl_loss
 
@@ -150,6 +163,24 @@ def main():
         against float64, and whether the re-run's total gradient is bitwise the step's."""
         params = dict(enc.named_parameters())
         step_grads = {n: p.grad.detach().clone() for n, p in params.items()}
+        # each layer's compacted child, both orientations, against the recorded COO in float64
+        from hypergraph_diffusion_for_recommendation_amd.incidence import spmm_csr
+        hops = {}
+        gX = torch.Generator(device=rec.device).manual_seed(b)
+        for layer, ch in enumerate(list(enc.edgeDropper.children[:L])):
+            if ch is None:
+                continue
+            di, dv = drops[layer]
+            A64 = torch.sparse_coo_tensor(di, dv.double(), (N, N)).coalesce()
+            X = torch.randn(N, 64, device=rec.device, generator=gX)
+            Yr = spmm_csr(ch.csr, X, ch.val)
+            Yc = spmm_csr(ch.csc, X, ch.val_t)
+            Xh = X.cpu().double()
+            hops[f"layer{layer}"] = {
+                "csr": worst_row(Yr, torch.sparse.mm(A64, Xh)),
+                "csc": worst_row(Yc, torch.sparse.mm(A64.t().coalesce(), Xh)),
+                "n_heavy_csr": ch.csr.n_heavy, "n_heavy_csc": ch.csc.n_heavy,
+                "nnz": ch.nnz}
         post = {n: p.detach().clone() for n, p in params.items()}
         post_rng = (torch.get_rng_state(), torch.cuda.get_rng_state())
         with torch.no_grad():
@@ -174,7 +205,7 @@ def main():
         P64 = {n: v.clone().requires_grad_(True) for n, v in before.items()}
         (ueR, ieR, gR, hR), gbR, gsR = reference(P64, torch.float64, drops, masks, u.cpu(),
                                                  i.cpu(), j.cpu(), parts=True)
-        rep = {"batch": b, "analysis": True, "same_draws_on_rerun": same_draws,
+        rep = {"batch": b, "analysis": True, "same_draws_on_rerun": same_draws, "hops": hops,
                "forward": {"user_emb": worst_row(ue, ueR), "item_emb": worst_row(ie, ieR)}}
         for layer in range(L):
             rep["forward"][f"gcn[{layer}]"] = worst_row(gcn[layer], gR[layer])
@@ -218,6 +249,7 @@ def main():
             forced = ep == 1 and args.start <= b < args.stop
             enc.drop_out.masks.clear()
             enc.edgeDropper.outputs.clear()
+            enc.edgeDropper.children.clear()
             before = ({n: p.detach().cpu().double() for n, p in enc.named_parameters()}
                       if forced else None)
             pre_rng = (torch.get_rng_state(), torch.cuda.get_rng_state()) if forced else None
