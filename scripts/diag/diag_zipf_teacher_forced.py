@@ -88,11 +88,11 @@ def main():
 
         def __init__(self, inner):
             super().__init__(inner)
-            self.children = []
+            self.incs = []
 
         def forward(self, adj, keep):
             out = super().forward(adj, keep)
-            self.children.append(getattr(out, "_hgd_incidence", None))
+            self.incs.append(getattr(out, "_hgd_incidence", None))
             return out
 
     enc.drop_out = DropoutRecorder(enc.drop_out)
@@ -167,7 +167,7 @@ def main():
         from hypergraph_diffusion_for_recommendation_amd.incidence import spmm_csr
         hops = {}
         gX = torch.Generator(device=rec.device).manual_seed(b)
-        for layer, ch in enumerate(list(enc.edgeDropper.children[:L])):
+        for layer, ch in enumerate(list(enc.edgeDropper.incs[:L])):
             if ch is None:
                 continue
             di, dv = drops[layer]
@@ -249,7 +249,7 @@ def main():
             forced = ep == 1 and args.start <= b < args.stop
             enc.drop_out.masks.clear()
             enc.edgeDropper.outputs.clear()
-            enc.edgeDropper.children.clear()
+            enc.edgeDropper.incs.clear()
             before = ({n: p.detach().cpu().double() for n, p in enc.named_parameters()}
                       if forced else None)
             pre_rng = (torch.get_rng_state(), torch.cuda.get_rng_state()) if forced else None
