@@ -206,7 +206,6 @@ def main():
         (ueR, ieR, gR, hR), gbR, gsR = reference(P64, torch.float64, drops, masks, u.cpu(),
                                                  i.cpu(), j.cpu(), parts=True)
         rep = {"batch": b, "analysis": True, "same_draws_on_rerun": same_draws, "hops": hops,
-               "op_swaps": configs,
                "forward": {"user_emb": worst_row(ue, ueR), "item_emb": worst_row(ie, ieR)}}
         for layer in range(L):
             rep["forward"][f"gcn[{layer}]"] = worst_row(gcn[layer], gR[layer])
@@ -250,6 +249,7 @@ def main():
                 ENC.dense_two_hop_pair, ENC.linear = saved_ops[0], saved_ops[1]
                 type(enc.gcnlayer).forward = saved_ops[2]
                 enc.fused_layers = True
+        rep["op_swaps"] = configs
         rep["rerun_total_equals_step"] = {n: bool(torch.equal(rerun[n], step_grads[n]))
                                           for n in names}
         rep["rerun_vs_step_max_abs"] = {n: float((rerun[n] - step_grads[n]).abs().max())
