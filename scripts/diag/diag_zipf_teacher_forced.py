@@ -69,17 +69,26 @@ def main():
     keep_h = 1 - enc.drop_rate
 
     class DropoutRecorder(torch.nn.Module):
-        """The encoder's own nn.Dropout, its keep-masks read off its output (an element the mask
-        kept is nonzero unless its input was 0, where the mask does not matter)."""
+        """The encoder's own nn.Dropout and its exact keep-mask: the same draw applied to ones
+        (the device generator's state restored in between), so the mask is known where the
+        input is 0 too — reading it off the output (y != 0) would drop those elements, and an
+        exact-zero input element still passes its gradient through a kept mask entry."""
 
         def __init__(self, inner):
             super().__init__()
             self.inner, self.masks = inner, []
+            self.zero_inputs = 0
 
         def forward(self, x):
+            if not self.training:
+                return self.inner(x)
+            st = torch.cuda.get_rng_state(x.device)
+            m = self.inner(torch.ones_like(x)) != 0
+            torch.cuda.set_rng_state(st, x.device)
             y = self.inner(x)
-            if self.training:
-                self.masks.append((y != 0).cpu())
+            assert torch.equal(y != 0, m & (x != 0)), "dropout replay drew another mask"
+            self.zero_inputs += int((x == 0).sum())
+            self.masks.append(m.cpu())
             return y
 
     class ChildRecorder(R.DropRecorder):
@@ -320,6 +329,7 @@ def main():
             over = max(over, loss_rel / max(R.TOL, loss_rel32))
             worst_all = max(worst_all, over)
             print(json.dumps({"epoch": ep, "batch": b, "mode": mode, "loss": got,
+                              "dropout_zero_inputs_so_far": enc.drop_out.zero_inputs,
                               "loss_ref64": l64, "loss_rel": loss_rel, "loss_rel_ref32": loss_rel32,
                               "grad_row_ratio": rows, "ratio_over_bound": over,
                               "within_bound": over <= 1.0, "node_list_gaps": gaps,
