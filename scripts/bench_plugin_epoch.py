@@ -3,12 +3,14 @@
 Yelp2018 shape of BASELINE configs[2] (31,668 users × 38,048 items, ≈1.17 M training and
 ≈0.39 M test interactions, 3 layers, d = 64, batch 4096, InfoNCE SSL), wall clock:
 
-* ours:        sampler.next_batch_pairwise (native, bit-identical batches) + HCCF.train_step
-               (libhgd hops, fused InfoNCE, the reference's CPU drop-edge stream drawn natively)
-               for every batch of the epoch; again with capture-safe drop-edge views on
-               the same mask stream, with the device drop-edge mask (hgd_device_rng) and
-               replayed from a HIP graph (hgd_graph) — each from the same fresh model; then
-               fast_evaluation over all test users (device lists + metrics);
+* ours:        sampler.next_batch_pairwise (native, bit-identical batches) + the plugin's
+               default step (HCCF.graph_step: forward + backward replayed from a HIP graph,
+               libhgd hops, fused InfoNCE, the reference's CPU drop-edge stream drawn natively,
+               the reference's Adam) for every batch of the epoch, then the same model through
+               a second epoch (finite?); the eager loop (hgd_graph=False) on drop-edge views,
+               on compacted children (hgd_compact_drop) and with the device drop-edge mask
+               (hgd_device_rng) — each from the same fresh model; then fast_evaluation over
+               all test users (device lists + metrics);
 * reference ops: the restated Python sampler (oracle) + the reference's torch calls
                (oracle/ref_cpu.HCCFEncoderRef, torch.unique, contrastLoss) for the same epoch.
 
@@ -95,11 +97,9 @@ def main():
     out["load_s"] = round(time.perf_counter() - t, 3)
 
     def fresh(**extra):
-        # every timed epoch starts from the same fresh model: continuing one model through a
-        # second epoch diverges on this Zipf-1.2 set (the reference's step clips nothing —
-        # clip_grad_norm_ runs before backward, HCCF.py:94-95 — and the hypergraph layers'
-        # outputs grow until torch.unique(pos_emb.long()) indexes past the item table, which
-        # raises in the reference as here; scripts/diag/diag_epoch_nan.py)
+        # every variant starts from the same fresh model (round 4 also did this because a
+        # second epoch of one model diverged on this set; with round 5's InfoNCE the default
+        # model trains through both epochs below)
         torch.manual_seed(0)
         r = HCCF(conf, train, test, None, **dict(kw, **extra))
         torch.cuda.synchronize()
@@ -124,21 +124,31 @@ def main():
     rec = fresh()
     out["build_s"] = round(time.perf_counter() - t, 3)
     dev = rec.device
-    # ours: the plugin's default eager step (the reference's CPU drop-edge stream, compacted
-    # children)
-    out["ours_epoch_s"], n_batches = epoch(rec, rec.train_step)
+    # ours: the plugin's default step — forward + backward replayed from a HIP graph on the
+    # reference's CPU drop-edge stream, the reference's Adam after each replay
+    out["ours_epoch_s"], n_batches = epoch(rec, rec.graph_step, warm=4)
     out["batches"] = n_batches
-    # eager, capture-safe drop-edge views on the same CPU mask stream (per-call slots),
-    # device-side InfoNCE node counts: no host read inside a step
-    r = fresh()
-    r.model.edgeDropper.capture_safe = True
-    out["ours_epoch_capture_safe_s"], _ = epoch(r, r.train_step)
-    # hgd_device_rng: device drop-edge masks (a different stream), capture-safe views
-    r = fresh(hgd_device_rng=True)
+    # the same model through a second epoch (the run round 4 saw diverge): every parameter
+    # finite at its end, and its mean batch loss
+    losses = []
+    t = time.perf_counter()
+    for u, i, j in next_batch_pairwise(rec.data, rec.batchSize, device=dev):
+        losses.append(rec.graph_step(u, i, j))
+    torch.cuda.synchronize()
+    out["ours_second_epoch_s"] = round(time.perf_counter() - t, 3)
+    out["second_epoch_mean_loss"] = round(float(torch.stack(losses).mean()), 6)
+    out["two_epochs_finite"] = all(bool(torch.isfinite(p).all())
+                                   for p in rec.model.parameters())
+    # the eager loop (hgd_graph=False): capture-safe drop-edge views on the same CPU mask
+    # stream (per-call slots), device-side InfoNCE node counts: no host read inside a step
+    r = fresh(hgd_graph=False)
+    out["ours_epoch_eager_s"], _ = epoch(r, r.train_step)
+    # the eager loop on the reference's compacted sparse children (hgd_compact_drop)
+    r = fresh(hgd_compact_drop=True)
+    out["ours_epoch_eager_compacted_s"], _ = epoch(r, r.train_step)
+    # hgd_device_rng: device drop-edge masks (a different stream), capture-safe views, eager
+    r = fresh(hgd_device_rng=True, hgd_graph=False)
     out["ours_epoch_device_rng_s"], _ = epoch(r, r.train_step)
-    # hgd_graph: full-size batches replayed from one HIP graph, the reference's CPU mask stream
-    r = fresh(hgd_graph=True)
-    out["ours_epoch_graph_s"], _ = epoch(r, r.graph_step, warm=4)
     del r
     rec.model.eval()
     with torch.no_grad():
