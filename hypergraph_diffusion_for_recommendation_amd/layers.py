@@ -130,7 +130,18 @@ def _draw_keep_mask(state: torch.Tensor, n: int, keep: float, threads: int = 0):
 
 def _draw_step_masks(state: torch.Tensor, spec, threads: int = 0):
     """The masks of one step's drop calls ((n, keep) each, in order) from one generator state,
-    advanced in place: [mask], state."""
+    advanced in place: [mask], state. Calls at one rate are ONE draw of Σn words split into
+    views: ``torch.rand(n)`` takes exactly one generator word per element, so consecutive
+    calls are consecutive stretches of one stream, and one split draw pays the threads'
+    jump-ahead once instead of per call (HCCF: three 2.47 M masks per step)."""
+    if len(spec) > 1 and len({keep for _, keep in spec}) == 1:
+        total = sum(n for n, _ in spec)
+        mask, _, state = _draw_keep_mask(state, total, spec[0][1], threads)
+        masks, off = [], 0
+        for n, _ in spec:
+            masks.append(mask[off:off + n])
+            off += n
+        return masks, state
     masks = []
     for n, keep in spec:
         mask, _, state = _draw_keep_mask(state, n, keep, threads)

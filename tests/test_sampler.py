@@ -150,3 +150,31 @@ def test_torch_cpu_keep_mask_prefetch_keeps_the_stream():
         elif between == "seed":
             torch.manual_seed(7)
     assert torch.equal(torch.rand(8), want_next)
+
+
+@pytest.mark.parametrize("spec", [[(2_470_000, 0.5)] * 3, [(1000, 0.7), (5, 0.7), (70_000, 0.7)],
+                                  [(3000, 0.5), (3000, 0.9)]])
+def test_step_masks_one_draw_equals_per_call_draws(spec):
+    """SpAdjDropEdge.refill's step draw: calls at one rate come from ONE split draw of Σn words,
+    bit-identical to the per-call draws (torch.rand(n) and the native draw take one generator
+    word per element) and leaving the generator in the same state."""
+    import torch
+
+    from hypergraph_diffusion_for_recommendation_amd.layers import (_draw_keep_mask,
+                                                                    _draw_step_masks,
+                                                                    _native_cpu_mask_ok)
+    if not _native_cpu_mask_ok():
+        pytest.skip("native torch CPU generator layout not recognised")
+    torch.manual_seed(123)
+    torch.rand(17)  # start mid-block
+    st = torch.get_rng_state()
+    got, end = _draw_step_masks(st.clone(), spec)
+    state = st.clone()
+    for (n, keep), g in zip(spec, got):
+        ref, _, state = _draw_keep_mask(state, n, keep)
+        assert torch.equal(g, ref), (n, keep)
+    assert torch.equal(end, state)
+    torch.set_rng_state(st)
+    for (n, keep), g in zip(spec, got):  # and the reference's own calls
+        assert torch.equal(g.bool(), ((torch.rand(n) + keep).floor()).type(torch.bool))
+    assert torch.equal(torch.get_rng_state(), end)
