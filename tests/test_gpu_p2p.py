@@ -291,7 +291,9 @@ def _free_bytes(dev):
 
 def test_p2p_segments_freed_when_dropped_without_close(dev):
     """A ShardedIncidence dropped without close() frees its exported segments (hipMemGetInfo
-    back to where it was): no global keeps the exchange alive through its cached slot views."""
+    gains back the slots' 1 GiB): no global keeps the exchange alive through its cached slot
+    views. (Deltas at 0.8 of the slot bytes: other tests' garbage collected in between moves
+    the absolute free figure by tens of MB.)"""
     from hypergraph_diffusion_for_recommendation_amd import _native as nat
     items, d = 1 << 20, 64
     slots_bytes = 4 * items * d * 4  # 2 send + 2 reduced slots of 256 MB
@@ -300,10 +302,10 @@ def test_p2p_segments_freed_when_dropped_without_close(dev):
     sh, ex = _sharded_with_p2p(dev, items, d)
     ex.slot(0, items, d).fill_(1.0)
     free1 = _free_bytes(dev)
-    assert free0 - free1 >= slots_bytes, (free0, free1)
+    assert free0 - free1 >= 0.8 * slots_bytes, (free0, free1)
     del sh, ex
     free2 = _free_bytes(dev)
-    assert free0 - free2 < slots_bytes // 8, (free0, free2)
+    assert free2 - free1 >= 0.8 * slots_bytes, (free1, free2)
     assert nat.live_views() == live0
 
 
@@ -312,15 +314,16 @@ def test_p2p_slot_view_held_past_close_stays_valid(dev):
     alive (never a view of freed memory); the memory goes with the last view's storage."""
     items, d = 1 << 20, 64
     slots_bytes = 4 * items * d * 4
-    free0 = _free_bytes(dev)
     sh, ex = _sharded_with_p2p(dev, items, d)
     v = ex.slot(1, items, d)[10:20]  # a view of the view: the storage outlives the slot tensor
+    free_open = _free_bytes(dev)
     sh.close()
     with pytest.raises(RuntimeError, match="closed"):
         ex.slot(1, items, d)
-    assert free0 - _free_bytes(dev) >= slots_bytes  # still mapped: v points at live memory
+    free_closed = _free_bytes(dev)
+    assert free_closed - free_open < 0.2 * slots_bytes  # still mapped: v points at live memory
     v.fill_(3.0)
     assert bool((v == 3.0).all())
     del v
-    assert free0 - _free_bytes(dev) < slots_bytes // 8
+    assert _free_bytes(dev) - free_closed >= 0.8 * slots_bytes
     del sh, ex
