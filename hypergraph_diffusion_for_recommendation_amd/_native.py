@@ -177,6 +177,13 @@ class InfonceTerm(ctypes.Structure):
     ]
 
 
+class AdamTensor(ctypes.Structure):
+    """Mirror of ``hgd_adam_tensor`` (include/hgd.h)."""
+
+    _fields_ = [("param", c_void_p), ("grad", c_void_p), ("exp_avg", c_void_p),
+                ("exp_avg_sq", c_void_p), ("n", c_i64)]
+
+
 class IncidenceView(ctypes.Structure):
     """Mirror of ``hgd_incidence_view`` (include/hgd.h)."""
 
@@ -331,6 +338,7 @@ _SIGNATURES = {
                                       c_void_p]),
     "hgd_sum_slices": (c_i32, [c_void_p, c_i64, c_i64, c_i64, c_void_p, c_void_p]),
     "hgd_sum_arrays": (c_i32, [c_void_p, c_i32, c_i64, c_void_p, c_void_p]),
+    "hgd_adam_step": (c_i32, [c_void_p, c_i32, c_void_p, c_i32, c_void_p]),
     "hgd_dropout_apply": (c_i32, [c_void_p, c_i64, c_void_p, c_f32, c_f32, c_void_p, c_void_p]),
     "hgd_bpr_workspace_size": (c_size, [c_i64, c_i64]),
     "hgd_bpr_forward": (c_i32, [c_void_p, c_i64, c_i64, c_i64, c_i32, c_void_p, c_void_p,

@@ -43,6 +43,8 @@ import torch
 import torch.nn as nn
 from torch.optim.lr_scheduler import ReduceLROnPlateau
 
+from .optim import ReferenceAdam, calibrated_variant
+
 from .encoders import (HCCFDiffusionEncoder, HCCFEncoder, LocalAwareEncoder,
                        LocalAwareEncoderHD3, sparse_tensor_of)
 from .functional import (bpr_index_errors, bpr_loss_rows, contrast_loss, contrast_loss_layers,
@@ -102,15 +104,18 @@ class HCCF(GraphRecommender):
     def _init_optimizer(self, kwargs):
         # hgd_graph: the training step replayed from one HIP graph (graphs.CapturedStep) — the
         # drop-edge masks as views filled before each replay, device-side InfoNCE node counts.
-        # The optimizer is the reference's torch.optim.Adam(lr=float) (HCCF.py:33), stepping
-        # eagerly after each replay of the forward + backward, so replayed steps are bitwise the
-        # eager steps; hgd_capturable_adam=True puts a capturable fused Adam inside the graph
-        # instead (one launch less per step, but not the reference's rounding of the bias
-        # corrections: scripts/diag/diag_adam_bitwise.py)
+        # The optimizer is the reference's torch.optim.Adam(lr=float) (HCCF.py:33): inside the
+        # graph as optim.ReferenceAdam (one kernel, its per-step scalars refilled before each
+        # replay; bitwise torch's Adam — calibrated on the device, optim.calibrated_variant), or,
+        # if no kernel variant is bitwise torch's on this build, torch's own Adam stepping eagerly
+        # after each replay. Replayed steps are bitwise the eager steps either way.
+        # hgd_capturable_adam=True puts torch's capturable fused Adam in the graph instead (not
+        # the reference's rounding of the bias corrections: scripts/diag/diag_adam_bitwise.py)
         default = self._graph_default and not kwargs.get('hgd_compact_drop', False)
         self.graph_mode = bool(kwargs.get('hgd_graph', default))
         self._captured = None
         self._adam_in_graph = self.graph_mode and bool(kwargs.get('hgd_capturable_adam', False))
+        self._adam_kernel = False
         if self.graph_mode:
             # the drop-edge masks stay the reference's CPU torch.rand stream (drawn on the host
             # before each replay into the buffers the graph reads) unless hgd_device_rng asks
@@ -122,6 +127,9 @@ class HCCF(GraphRecommender):
             # fused: one multi-tensor kernel per step instead of the ~15 foreach passes
             self.optimizer = torch.optim.Adam(self.model.parameters(), lr=lr, capturable=True,
                                               fused=True)
+        elif self.graph_mode and calibrated_variant(self.device) is not None:
+            self.optimizer = ReferenceAdam(self.model.parameters(), lr=self.lRate)
+            self._adam_in_graph = self._adam_kernel = True
         else:
             self.optimizer = torch.optim.Adam(self.model.parameters(), lr=self.lRate)
         self.scheduler = ReduceLROnPlateau(self.optimizer, 'min', factor=self.lr_decay,
@@ -214,9 +222,22 @@ class HCCF(GraphRecommender):
             dropper = self.model.edgeDropper
             host_fed = not dropper.device_rng
             dropper.host_fed(host_fed)  # the capture records the slots; refill() fills them
-            body = self.train_step if self._adam_in_graph else self.forward_backward
+            opt = self.optimizer
+            if self._adam_kernel:  # the graph holds the Adam kernel; its scalars come per replay
+                def body(u, i, j):
+                    loss = self.forward_backward(u, i, j)
+                    opt.launch()
+                    return loss
+
+                def before():
+                    if host_fed:
+                        dropper.refill()
+                    opt.prepare()
+            else:
+                body = self.train_step if self._adam_in_graph else self.forward_backward
+                before = dropper.refill if host_fed else None
             self._captured = CapturedStep(body, (user_idx, pos_idx, neg_idx),
-                                          before_replay=dropper.refill if host_fed else None)
+                                          before_replay=before)
             # the gradient buffers the replays write (an eager short batch rebinds .grad)
             self._graph_grads = [p.grad for p in self.model.parameters()]
             return self._replay(user_idx, pos_idx, neg_idx)

@@ -14,6 +14,8 @@ reference calls it) and Adam. Variants:
                      drawn on the host before each replay (SpAdjDropEdge.refill);
 * hgd_graph_ref_adam — the hgd_graph_cpu_mask replay holding only the forward + backward, the
                      reference's Adam (torch.optim.Adam(lr=float)) stepping eagerly after it;
+* hgd_graph_kernel_adam — the same replay with the reference's Adam as one captured kernel
+                     (optim.ReferenceAdam: bitwise torch's Adam), the plugins' graph default;
 * hgd_capture_safe_eager — the graph variant's ops (device mask), launched eagerly;
 * hgd_cs_eager_cpu_mask — eager, capture-safe drop-edge views (the reference's CPU mask stream
                      through the per-call slots), device-side InfoNCE counts, fused BPR, the
@@ -72,12 +74,15 @@ def main():
                 torch.randint(0, ni, (args.batch,), device=dev, generator=g)) for _ in range(8)]
 
     def make_step(model, loss_fn, unique, hoist=True, graph=False, counted=None, host_fed=None,
-                  fused_adam=None, adam_after_replay=False):
+                  fused_adam=None, adam_after_replay=False, kernel_adam=False):
         # adam_after_replay: the graph holds the forward + backward only; the reference's Adam
         # (torch.optim.Adam(lr=float), non-capturable) steps eagerly after each replay
         counted = graph if counted is None else counted
         fused_adam = (counted and not adam_after_replay) if fused_adam is None else fused_adam
-        if fused_adam:
+        if kernel_adam:  # the reference's Adam as one capturable kernel (optim.ReferenceAdam)
+            from hypergraph_diffusion_for_recommendation_amd.optim import ReferenceAdam
+            opt = ReferenceAdam(model.parameters(), lr=conf["lrate"])
+        elif fused_adam:
             lr = torch.tensor(conf["lrate"], dtype=torch.float32, device=dev)
             opt = torch.optim.Adam(model.parameters(), lr=lr, capturable=True, fused=True)
         else:
@@ -109,7 +114,9 @@ def main():
             opt.zero_grad()
             torch.nn.utils.clip_grad_norm_(model.parameters(), 4)  # before backward, as HCCF.py:95
             loss.backward()
-            if not adam_after_replay:
+            if kernel_adam:
+                opt.launch()  # its scalars: opt.prepare() before the call / replay
+            elif not adam_after_replay:
                 opt.step()
             return loss
 
@@ -117,21 +124,29 @@ def main():
             uid, pid, nid = batches[state["k"] % len(batches)]
             state["k"] += 1
             if not graph:
+                if kernel_adam:
+                    opt.prepare()
                 out = body(uid, pid, nid)
                 if adam_after_replay:
                     opt.step()
                 return out
             if state["cap"] is None:
                 if state["k"] == 1:
+                    if kernel_adam:
+                        opt.prepare()
                     out = body(uid, pid, nid)  # one eager step: optimizer state, handles
                     if adam_after_replay:
                         opt.step()
                     return out
                 if host_fed is not None:  # the reference's CPU mask stream, drawn per replay
                     host_fed.host_fed(True)
-                state["cap"] = CapturedStep(body, (uid, pid, nid),
-                                            before_replay=None if host_fed is None
-                                            else host_fed.refill)
+
+                def before():
+                    if host_fed is not None:
+                        host_fed.refill()
+                    if kernel_adam:
+                        opt.prepare()
+                state["cap"] = CapturedStep(body, (uid, pid, nid), before_replay=before)
             out = state["cap"](uid, pid, nid)
             if adam_after_replay:
                 opt.step()
@@ -191,6 +206,16 @@ def main():
                                                           graph=True,
                                                           host_fed=a_model.edgeDropper,
                                                           adam_after_replay=True))))
+    if "hgd_graph_kernel_adam" in want:  # replayed step incl. the reference's Adam as one
+        torch.manual_seed(0)               # captured kernel (the plugins' graph default)
+        k_model = HCCFEncoder(conf, data, dev)
+        k_model.load_state_dict(ours.state_dict())
+        k_model.edgeDropper.device_rng = False
+        k_model.edgeDropper.capture_safe = True
+        out.append(("hgd_graph_kernel_adam", timed(make_step(k_model, contrast_loss,
+                                                             unique_long_n, graph=True,
+                                                             host_fed=k_model.edgeDropper,
+                                                             kernel_adam=True))))
     if "hgd_capture_safe_eager" in want:  # the graph variant's ops, launched eagerly
         torch.manual_seed(0)
         e_model = HCCFEncoder(conf, data, dev)
