@@ -3,7 +3,7 @@
 // per-step scalars are Python doubles computed on the host (bias corrections of the step count):
 //
 //   m ← lerp(m, g, 1 − β1)                    torch._foreach_lerp_ (weight < 0.5: m + w·(g − m))
-//   v ← v·β2 ; v ← v + (1 − β2)·g·g           torch._foreach_mul_ / _foreach_addcmul_
+//   v ← v·β2 ; v ← v + (1 − β2)·(g·g)         torch._foreach_mul_ / _foreach_addcmul_
 //   d ← sqrt(v) / sqrt(1 − β2^t) + eps        torch._foreach_sqrt / _foreach_div_ / _foreach_add_
 //   p ← p + (−lr / (1 − β1^t))·(m / d)        torch._foreach_addcdiv_
 //
@@ -63,9 +63,9 @@ __global__ __launch_bounds__(256) void k_adam(AdamList L, const float* __restric
     float v = L.v[t][e];
     // lerp(m, g, w), w = 1 − β1 < 0.5 (ATen Lerp.h: self + weight·(end − self))
     m = mul_add(s[0], g - m, m, f_lerp);
-    // v·β2, then addcmul: v + value·g·g evaluated as (value·g)·g + v
+    // v·β2, then addcmul as torch's foreach pointwise functor: v + value·(g·g)
     v = v * s[1];
-    v = mul_add(s[2] * g, g, v, f_cmul);
+    v = mul_add(s[2], g * g, v, f_cmul);
     float d = sqrt_of(v, fast_sqrt);
     d = div_of(d, s[3], fast_div);
     d = d + s[4];

@@ -790,7 +790,7 @@ hgd_status hgd_sum_arrays(const float* const* arrays, int32_t n_arrays, int64_t 
  * buffer `scalars` ([count, 6] floats: 1 − β1, β2, 1 − β2, sqrt(1 − β2^t), eps,
  * −lr / (1 − β1^t), each the float of the double torch computes on the host) that the caller
  * fills before every launch or graph replay. Per element, in torch's op order and rounding:
- * m ← m + w·(g − m); v ← v·β2; v ← (value·g)·g + v; d ← sqrt(v)/c2 + eps; p ← p + s·(m/d).
+ * m ← m + w·(g − m); v ← v·β2; v ← v + value·(g·g); d ← sqrt(v)/c2 + eps; p ← p + s·(m/d).
  * `variant` (0..31) selects the fused multiply-adds (bits 0–2: lerp, addcmul, addcdiv) and the
  * approximate sqrt / division (bits 3, 4) the torch build on the image matches bit for bit
  * (tests/test_gpu_adam.py). `tensors` is a HOST array. */

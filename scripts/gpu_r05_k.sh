@@ -10,6 +10,8 @@ export TMPDIR=/tmp
 ( while sleep 45; do echo "[r05 k] $(date +%T) $(ls -t $O | head -1)"; done ) &
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
+timeout -k 10 120 python -u scripts/diag/diag_adam_ops.py > $O/adam_ops.json 2> $O/adam_ops.err && \
+cat $O/adam_ops.json && \
 timeout -k 10 600 python -u -m pytest tests/test_gpu_adam.py tests/test_gpu_graph_step.py \
     tests/test_gpu_plugins.py -x -v -s --timeout 300 --timeout-method thread -p no:cacheprovider \
     > $O/pytest.txt 2>&1 && tail -1 $O/pytest.txt && \
