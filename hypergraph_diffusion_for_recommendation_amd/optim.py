@@ -100,6 +100,8 @@ class ReferenceAdam(torch.optim.Adam):
         foreach kernels would receive, written to the device buffer the kernel reads (ordered
         on the current stream before the launch / replay)."""
         params = self._params()
+        if not params:
+            return
         self._init_state(params)
         rows = []
         for group in self.param_groups:

@@ -87,7 +87,7 @@ def main():
             opt = torch.optim.Adam(model.parameters(), lr=lr, capturable=True, fused=True)
         else:
             opt = torch.optim.Adam(model.parameters(), lr=conf["lrate"])
-        state = {"k": 0, "cap": None}
+        state = {"k": 0, "cap": None, "capturing": False}
 
         def body(uid, pid, nid):
             ue, ie, gcn, hyp = model(keep_rate=keep)
@@ -114,8 +114,8 @@ def main():
             opt.zero_grad()
             torch.nn.utils.clip_grad_norm_(model.parameters(), 4)  # before backward, as HCCF.py:95
             loss.backward()
-            if kernel_adam:
-                opt.launch()  # its scalars: opt.prepare() before the call / replay
+            if kernel_adam and state["capturing"]:
+                opt.launch()  # the graph's half; opt.prepare() runs before each replay
             elif not adam_after_replay:
                 opt.step()
             return loss
@@ -124,16 +124,12 @@ def main():
             uid, pid, nid = batches[state["k"] % len(batches)]
             state["k"] += 1
             if not graph:
-                if kernel_adam:
-                    opt.prepare()
                 out = body(uid, pid, nid)
                 if adam_after_replay:
                     opt.step()
                 return out
             if state["cap"] is None:
                 if state["k"] == 1:
-                    if kernel_adam:
-                        opt.prepare()
                     out = body(uid, pid, nid)  # one eager step: optimizer state, handles
                     if adam_after_replay:
                         opt.step()
@@ -146,7 +142,9 @@ def main():
                         host_fed.refill()
                     if kernel_adam:
                         opt.prepare()
+                state["capturing"] = True
                 state["cap"] = CapturedStep(body, (uid, pid, nid), before_replay=before)
+                state["capturing"] = False
             out = state["cap"](uid, pid, nid)
             if adam_after_replay:
                 opt.step()
