@@ -338,7 +338,7 @@ _SIGNATURES = {
                                       c_void_p]),
     "hgd_sum_slices": (c_i32, [c_void_p, c_i64, c_i64, c_i64, c_void_p, c_void_p]),
     "hgd_sum_arrays": (c_i32, [c_void_p, c_i32, c_i64, c_void_p, c_void_p]),
-    "hgd_adam_step": (c_i32, [c_void_p, c_i32, c_void_p, c_i32, c_void_p]),
+    "hgd_adam_step": (c_i32, [c_void_p, c_i32, c_void_p, c_void_p, c_i32, c_void_p]),
     "hgd_dropout_apply": (c_i32, [c_void_p, c_i64, c_void_p, c_f32, c_f32, c_void_p, c_void_p]),
     "hgd_bpr_workspace_size": (c_size, [c_i64, c_i64]),
     "hgd_bpr_forward": (c_i32, [c_void_p, c_i64, c_i64, c_i64, c_i32, c_void_p, c_void_p,

@@ -787,9 +787,11 @@ hgd_status hgd_sum_arrays(const float* const* arrays, int32_t n_arrays, int64_t 
 /* The reference's optimizer step, torch.optim.Adam(params, lr=…) (model/graph/HCCF.py:33; the
  * multi-tensor non-capturable form torch runs on the device, no weight decay / amsgrad), as ONE
  * kernel over up to 16 tensors — capturable, since its per-step scalars are read from the device
- * buffer `scalars` ([count, 6] floats: 1 − β1, β2, 1 − β2, sqrt(1 − β2^t), eps,
- * −lr / (1 − β1^t), each the float of the double torch computes on the host) that the caller
- * fills before every launch or graph replay. Per element, in torch's op order and rounding:
+ * table `scalars` ([rows, count, 6] floats: 1 − β1, β2, 1 − β2, sqrt(1 − β2^t), eps,
+ * −lr / (1 − β1^t), each the float of the double torch computes on the host, one row per step):
+ * row *step_row is used and then step_row is advanced on the device (a second, one-thread
+ * launch on the same stream), so a graph holding the call steps through the table by itself;
+ * step_row NULL reads row 0 and advances nothing. Per element, in torch's op order and rounding:
  * m ← m + w·(g − m); v ← v·β2; v ← v + value·(g·g); d ← sqrt(v)/c2 + eps; p ← p + s·(m/d).
  * `variant` (0..31) selects the fused multiply-adds (bits 0–2: lerp, addcmul, addcdiv) and the
  * approximate sqrt / division (bits 3, 4) the torch build on the image matches bit for bit
@@ -802,7 +804,7 @@ typedef struct hgd_adam_tensor {
   int64_t n;
 } hgd_adam_tensor;
 hgd_status hgd_adam_step(const hgd_adam_tensor* tensors, int32_t count, const float* scalars,
-                         int32_t variant, void* stream);
+                         int32_t* step_row, int32_t variant, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Incidence objects (SURVEY.md §8b "C ABI libhgd"): the library-owned form of the structure the

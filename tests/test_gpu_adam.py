@@ -27,9 +27,14 @@ def test_a_kernel_variant_is_bitwise_torch_adam(dev):
     assert v is not None
 
 
+@pytest.mark.parametrize("rows", [512, 8], ids=["table512", "table8"])
 @pytest.mark.parametrize("graph", [False, True], ids=["eager", "graph"])
-def test_reference_adam_equals_torch_adam(dev, graph):
+def test_reference_adam_equals_torch_adam(dev, graph, rows, monkeypatch):
+    """60 steps, an lr change at step 25 (the table rebuilt), and with an 8-row table its
+    rebuilds every 8 steps (the graph keeps reading the same device table and row index)."""
+    from hypergraph_diffusion_for_recommendation_amd import optim
     from hypergraph_diffusion_for_recommendation_amd.optim import ReferenceAdam
+    monkeypatch.setattr(optim, "_TABLE_ROWS", rows)
     p0 = _params(dev)
     steps = 60
     grads = _grads(dev, p0, steps)
