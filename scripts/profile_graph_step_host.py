@@ -1,0 +1,100 @@
+#!/usr/bin/env python3
+"""Where the host time of the HCCF plugin's replayed step goes (HCCF.graph_step, the default):
+per step, wall time of the before-replay work (SpAdjDropEdge.refill: the reference's CPU mask
+stream; ReferenceAdam.prepare: step counters), of the replay call, and of the whole step with a
+device sync (as the plugin's loop syncs on batch_loss.item()), beside the replay's device time
+(HIP events). Yelp2018-shaped synthetic graph (SURVEY.md §8d generator), batch 4096, 3 layers,
+d = 64. Prints one JSON line of medians (µs)."""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+import types
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(ROOT))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=60)
+    args = ap.parse_args()
+    import torch
+
+    import refops as R
+    from hypergraph_diffusion_for_recommendation_amd.encoders import HCCFEncoder
+    from hypergraph_diffusion_for_recommendation_amd.functional import (bpr_loss_rows,
+                                                                         contrast_loss_layers,
+                                                                         unique_long_n_group)
+    from hypergraph_diffusion_for_recommendation_amd.graphs import CapturedStep
+    from hypergraph_diffusion_for_recommendation_amd.optim import ReferenceAdam
+    dev = torch.device("cuda")
+    nu, ni = 31_668, 38_048
+    u, i = R.synthetic_incidence(nu, ni, 1_237_259, seed=0)
+    A = R.normalize_graph_mat(R.bipartite_adjacency(u, i, nu, ni))
+    data = types.SimpleNamespace(n_users=nu, n_items=ni, norm_adj=A)
+    conf = dict(lrate=0.001, lr_decay=0.7, max_epoch=1, batch_size=4096, reg=0.1,
+                embedding_size=64, hyper_dim=32, drop_rate=0.5, p=0.1, n_layers=3)
+    torch.manual_seed(0)
+    model = HCCFEncoder(conf, data, dev)
+    model.edgeDropper.capture_safe = True
+    opt = ReferenceAdam(model.parameters(), lr=1e-3)
+    g = torch.Generator(device=dev).manual_seed(0)
+    batches = [tuple(torch.randint(0, n, (4096,), device=dev, generator=g) for n in (nu, ni, ni))
+               for _ in range(8)]
+    capturing = [False]
+
+    def body(uid, pid, nid):
+        ue, ie, gcn, hyp = model(keep_rate=0.5)
+        bpr, anc, pos = bpr_loss_rows(ue, ie, uid, pid, nid)
+        (un, uc), (pn, pc) = unique_long_n_group([anc, pos], [nu, ni])
+        ssl = contrast_loss_layers([t.detach() for t in gcn], hyp, nu, un, pn, 0.2, uc, pc)
+        loss = bpr + 1e-4 * ssl
+        opt.zero_grad()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 4)
+        loss.backward()
+        if capturing[0]:
+            opt.launch()
+        else:
+            opt.step()
+        return loss
+
+    body(*batches[0])
+    dropper = model.edgeDropper
+    dropper.host_fed(True)
+    capturing[0] = True
+    cap = CapturedStep(body, batches[1], before_replay=None)
+    capturing[0] = False
+    rec = {"refill": [], "prepare": [], "copy_inputs": [], "replay_call": [], "step_synced": [],
+           "device_replay": []}
+    for k in range(args.steps):
+        b = batches[k % len(batches)]
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        dropper.refill()
+        t1 = time.perf_counter()
+        opt.prepare()
+        t2 = time.perf_counter()
+        for dst, src in zip(cap.static, b):
+            dst.copy_(src)
+        t3 = time.perf_counter()
+        e0.record()
+        cap.graph.replay()
+        e1.record()
+        t4 = time.perf_counter()
+        float(cap.out.sum()) if hasattr(cap.out, "sum") else None
+        torch.cuda.synchronize()
+        t5 = time.perf_counter()
+        if k >= 5:
+            for name, v in (("refill", t1 - t0), ("prepare", t2 - t1), ("copy_inputs", t3 - t2),
+                            ("replay_call", t4 - t3), ("step_synced", t5 - t0),
+                            ("device_replay", e0.elapsed_time(e1) * 1e-3)):
+                rec[name].append(v * 1e6)
+    print(json.dumps({k: round(statistics.median(v), 1) for k, v in rec.items()}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
