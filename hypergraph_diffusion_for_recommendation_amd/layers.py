@@ -276,14 +276,17 @@ class _MaskStager:
             done.record(self.side)
         return masks, end, (k, done, flat)  # flat: the pinned source stays alive until done
 
-    def into_slots(self, staged, slots) -> None:
+    def into_slots(self, staged, slots, flat=None) -> None:
         k, done, _flat = staged
         cur = torch.cuda.current_stream(self.device)
         cur.wait_event(done)
-        off = 0
-        for n, _, buf in slots:
-            buf.copy_(self.bufs[k][off:off + n])
-            off += n
+        if flat is not None and flat.numel() == self.total:  # the slots are views of one buffer
+            flat.copy_(self.bufs[k])
+        else:
+            off = 0
+            for n, _, buf in slots:
+                buf.copy_(self.bufs[k][off:off + n])
+                off += n
         ev = torch.cuda.Event()
         ev.record(cur)
         self.free[k] = ev
@@ -326,8 +329,22 @@ class SpAdjDropEdge(nn.Module):
 
     def host_fed(self, on: bool = True):
         """capture_safe masks on the reference's CPU stream drawn ahead by :meth:`refill` (for a
-        captured step, whose replays do not run Python) instead of inside the step."""
+        captured step, whose replays do not run Python) instead of inside the step. Turning it
+        on (before the step is captured) also lays the step's slots out as consecutive views of
+        one buffer, so a refill moves them with one device copy."""
         self._prefilled = bool(on)
+        if on and len(self._slots) > 1:
+            flat = getattr(self, "_slot_flat", None)
+            total = sum(n for n, _, _ in self._slots)
+            if flat is None or flat.numel() != total:
+                flat = torch.empty(total, dtype=torch.uint8, device=self._slots[0][2].device)
+                slots, off = [], 0
+                for n, keep, buf in self._slots:
+                    view = flat[off:off + n]
+                    view.copy_(buf)
+                    slots.append((n, keep, view))
+                    off += n
+                self._slots, self._slot_flat = slots, flat
 
     def refill(self):
         """Draws the next step's masks from the CPU generator — the same draws, in the same
@@ -354,7 +371,7 @@ class SpAdjDropEdge(nn.Module):
             self._step_job = (end.clone(), spec,
                               _step_pool().submit(stager.draw_and_stage, end.clone(), spec))
         if staged is not None:  # already on the device: one D2D pass into the slots
-            self._stage.into_slots(staged, self._slots)
+            self._stage.into_slots(staged, self._slots, getattr(self, "_slot_flat", None))
         else:
             for (n, keep, buf), mask in zip(self._slots, masks):
                 buf.copy_(mask, non_blocking=True)
