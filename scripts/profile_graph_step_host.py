@@ -68,6 +68,26 @@ def main():
     capturing[0] = True
     cap = CapturedStep(body, batches[1], before_replay=None)
     capturing[0] = False
+    # the draw the worker makes per step (one split draw of the step's three masks), alone
+    from hypergraph_diffusion_for_recommendation_amd import layers as LY
+    spec = tuple((n, keep) for n, keep, _ in dropper._slots)
+    draws = []
+    for _ in range(12):
+        t0 = time.perf_counter()
+        LY._draw_step_masks(torch.get_rng_state(), spec)
+        draws.append((time.perf_counter() - t0) * 1e6)
+    # how long refill waits for the worker's job
+    waits = []
+    orig_result = None
+
+    def timed_result(fut):
+        t0 = time.perf_counter()
+        out = orig_result(fut)
+        waits.append((time.perf_counter() - t0) * 1e6)
+        return out
+    import concurrent.futures as cf
+    orig_result = cf.Future.result
+    cf.Future.result = timed_result
     rec = {"refill": [], "prepare": [], "copy_inputs": [], "replay_call": [], "step_synced": [],
            "device_replay": []}
     for k in range(args.steps):
@@ -93,7 +113,12 @@ def main():
                             ("replay_call", t4 - t3), ("step_synced", t5 - t0),
                             ("device_replay", e0.elapsed_time(e1) * 1e-3)):
                 rec[name].append(v * 1e6)
-    print(json.dumps({k: round(statistics.median(v), 1) for k, v in rec.items()}), flush=True)
+    cf.Future.result = orig_result
+    out = {k: round(statistics.median(v), 1) for k, v in rec.items()}
+    out["draw_step_masks_alone"] = round(statistics.median(draws[2:]), 1)
+    out["refill_wait_for_worker"] = round(statistics.median(waits[5:]), 1) if waits else None
+    out["spec"] = spec
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":
