@@ -261,11 +261,15 @@ class HCCF(GraphRecommender):
         lst_performances = []
         for ep in range(self.maxEpoch):
             s_train = time.time()
+            step_losses = []
             for n, batch in enumerate(next_batch_pairwise(self.data, self.batchSize,
                                                           device=self.device)):
                 user_idx, pos_idx, neg_idx = batch
-                batch_loss = self.graph_step(user_idx, pos_idx, neg_idx)
-                train_losses.append(batch_loss.item())
+                step_losses.append(self.graph_step(user_idx, pos_idx, neg_idx).detach())
+            # the batch losses (HCCF.py:91) feed only the epoch's mean (:115): read once here
+            # instead of per batch, so the host prepares batch n+1 while the device runs batch n
+            if step_losses:
+                train_losses.extend(torch.stack(step_losses).tolist())
             # the fused BPR clamps out-of-range ids where the reference's gather raises: one
             # read of its device count per epoch
             bad = bpr_index_errors(self.device)

@@ -26,11 +26,11 @@ from . import _native as nat
 
 def _mt_in() -> Tuple[tuple, np.ndarray]:
     st = random.getstate()
-    return st, np.array(st[1], dtype=np.uint32)
+    return st, np.fromiter(st[1], dtype=np.uint32, count=len(st[1]))
 
 
 def _mt_out(st: tuple, mt: np.ndarray) -> None:
-    random.setstate((st[0], tuple(int(x) for x in mt), st[2]))
+    random.setstate((st[0], tuple(mt.tolist()), st[2]))
 
 
 class _SamplerState:
@@ -100,6 +100,17 @@ def next_batch_pairwise(data, batch_size: int, n_negs: int = 1,
             u.ctypes.data, i.ctypes.data, j.ctypes.data), "hgd_sample_pairwise")
         _mt_out(st, mt)
         ptr = end
+        if device is not None and torch.device(device).type == "cuda":
+            # one pinned staging block and one asynchronous copy: a pageable .to(device) waits
+            # for the stream's queued work, which would stop the host from preparing the next
+            # batch while the device still runs this one (segments start 16-byte aligned)
+            s2 = b + (b & 1)
+            host = torch.empty(2 * s2 + b * n_negs, dtype=torch.int64, pin_memory=True)
+            hv = host.numpy()
+            hv[:b], hv[s2:s2 + b], hv[2 * s2:] = u, i, j[:b * n_negs]
+            dev = host.to(device, non_blocking=True)
+            yield dev[:b], dev[s2:s2 + b], dev[2 * s2:]
+            continue
         yield (torch.from_numpy(u.astype(np.int64)).to(device),
                torch.from_numpy(i.astype(np.int64)).to(device),
                torch.from_numpy(j[:b * n_negs].astype(np.int64)).to(device))

@@ -3,8 +3,10 @@
 per step, wall time of the before-replay work (SpAdjDropEdge.refill: the reference's CPU mask
 stream; ReferenceAdam.prepare: step counters), of the replay call, and of the whole step with a
 device sync (as the plugin's loop syncs on batch_loss.item()), beside the replay's device time
-(HIP events). Yelp2018-shaped synthetic graph (SURVEY.md §8d generator), batch 4096, 3 layers,
-d = 64. Prints one JSON line of medians (µs)."""
+(HIP events); then the same steps back to back with no host read between them
+(step_pipelined: wall time per step; host_issue_per_step: the host's time to issue one).
+Yelp2018-shaped synthetic graph (SURVEY.md §8d generator), batch 4096, 3 layers, d = 64.
+Prints one JSON line of medians (µs)."""
 import argparse
 import json
 import os
@@ -114,7 +116,25 @@ def main():
                             ("device_replay", e0.elapsed_time(e1) * 1e-3)):
                 rec[name].append(v * 1e6)
     cf.Future.result = orig_result
+    # the same steps with no host read between them (the plugin's loop reads the losses once
+    # per epoch): the host prepares step k+1 while the device runs step k
+    losses = []
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        b = batches[k % len(batches)]
+        dropper.refill()
+        opt.prepare()
+        for dst, src in zip(cap.static, b):
+            dst.copy_(src)
+        cap.graph.replay()
+        losses.append(cap.out.detach().clone())
+    t_host = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    out_pipe = {"step_pipelined": round((time.perf_counter() - t0) / args.steps * 1e6, 1),
+                "host_issue_per_step": round(t_host / args.steps * 1e6, 1)}
     out = {k: round(statistics.median(v), 1) for k, v in rec.items()}
+    out.update(out_pipe)
     out["draw_step_masks_alone"] = round(statistics.median(draws[2:]), 1)
     out["refill_wait_for_worker"] = round(statistics.median(waits[5:]), 1) if waits else None
     out["spec"] = spec
