@@ -6,9 +6,12 @@
 // neg and mean forward, and the same chain backward ending in three sort-based index_put
 // scatters (~40 small launches per step). Here: forward = one row kernel (gather, both dots,
 // per-row term and backward coefficient) + one fixed-order reduction; backward = zero/init,
-// one pass linking every position into its destination row's list (integer atomics), and one
-// row kernel in which one position per destination sums the contributions of all the row's
-// positions in ascending position order — deterministic, no float atomics, no sort.
+// one pass linking every position into its destination row's list and counting the row
+// (integer atomics), one row kernel in which one position per destination sums the
+// contributions of a row's (at most kWalkMax) positions in ascending position order, and one
+// kernel for the rows with more positions (one workgroup per row, fixed contiguous ranges of
+// its ascending positions, partials combined in range order) — deterministic, no float
+// atomics, no sort.
 #include <algorithm>
 
 #include "device_util.h"
@@ -94,7 +97,16 @@ __global__ __launch_bounds__(1024) void k_bpr_mean(const float* term, int64_t B,
   if (threadIdx.x == 0) *loss = s[0] / static_cast<float>(B);
 }
 
-__global__ void k_bpr_bwd_init(float* dE, int64_t lde, int64_t n_rows, int32_t d, int* head) {
+constexpr int kWalkMax = 8;          // rows with at most this many positions walk their list
+constexpr int kHeavyGrid = 256;       // blocks of the heavy-row kernel (they loop over the rows)
+constexpr int kWin = 16 * kBlock;     // positions one heavy-row window scans (16 per thread)
+
+__device__ __forceinline__ int64_t batch_row(const BprArgs& a, int64_t j) {
+  return j < a.B ? j : (j < 2 * a.B ? j - a.B : j - 2 * a.B);
+}
+
+__global__ void k_bpr_bwd_init(float* dE, int64_t lde, int64_t n_rows, int32_t d, int* head,
+                               int* cnt, int* n_heavy) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   const int64_t per = d / 4;
   if (i < n_rows * per) {
@@ -102,46 +114,47 @@ __global__ void k_bpr_bwd_init(float* dE, int64_t lde, int64_t n_rows, int32_t d
     const float z[4] = {0.f, 0.f, 0.f, 0.f};
     store_vec<4>(dE + r * lde + c, z);
   }
-  if (i < n_rows) head[i] = -1;
+  if (i < n_rows) {
+    head[i] = -1;
+    cnt[i] = 0;
+  }
+  if (i == 0) *n_heavy = 0;
 }
 
 // Every position pushes itself onto its destination row's list (integer atomics; the list
-// ORDER depends on timing, the set does not — the row kernel sorts it).
-__global__ void k_bpr_bwd_link(BprArgs a, int* head, int* next, int* dst) {
+// ORDER depends on timing, the set does not — the row kernel sorts it) and counts itself; the
+// position that takes a row past kWalkMax enters the row in the heavy list (exactly once).
+__global__ void k_bpr_bwd_link(BprArgs a, int* head, int* next, int* dst, int* cnt, int* heavy,
+                               int* n_heavy) {
   const int64_t q = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (q >= 3 * a.B) return;
   const int r = static_cast<int>(dest_row(a, q));
   dst[q] = r;
   next[q] = atomicExch(head + r, static_cast<int>(q));
+  if (atomicAdd(cnt + r, 1) == kWalkMax) heavy[atomicAdd(n_heavy, 1)] = r;
 }
 
 // One lane group per position; the position left at the head of each destination row's list
-// writes that row: the contributions of all its positions, summed in ascending position order.
-// The list is walked ONCE into the group's LDS slots (up to CAP positions), ranked there (each
-// lane counts the smaller entries of its slots) and added in rank order. Repeats are routine in
-// real batches — a popular item is the positive of tens of batch rows, and at d = 32 a group is
-// 4 lanes — so the ranking must not chase the list per element. A list longer than CAP (a
-// skewed catalogue's head item: under Zipf(1.2) popularity one item is the positive of ~740 of
-// 4,096 rows) stops being walked at CAP + 1 — a dependent load per entry — and the group scans
-// the destination array instead, K positions per lane per step (independent loads), taking its
-// row's positions in ascending order from the lanes' hit masks. That scan is ≤ 3B/(K·G) steps
-// for the few such rows; the round-3 fallback (repeated minimum walks over the list, quadratic
-// in dependent loads) took 45 ms per call on that batch.
+// writes that row when the row has at most kWalkMax positions (the heavy kernel writes the
+// others): the contributions of all its positions, summed in ascending position order — the
+// list walked once into the group's LDS slots, ranked there (each lane counts the smaller
+// entries of its slots), added in rank order.
 template <int G>
 __global__ __launch_bounds__(kBlock) void k_bpr_bwd_rows(BprArgs a, const float* coef,
                                                         const float* grad, const int* head,
                                                         const int* next, const int* dst,
-                                                        float* dE, int64_t ldd) {
+                                                        const int* cnt, float* dE, int64_t ldd) {
   constexpr int GPB = kBlock / G;
   const int l = threadIdx.x % G;
   const int64_t q = static_cast<int64_t>(blockIdx.x) * GPB + threadIdx.x / G;
   if (q >= 3 * a.B) return;
-  constexpr int CAP = G >= 4 ? 64 : 16;
-  __shared__ int s_list[GPB][CAP];
-  __shared__ int s_sorted[GPB][CAP];
+  __shared__ int s_list[GPB][kWalkMax];
+  __shared__ int s_sorted[GPB][kWalkMax];
   const int grp = threadIdx.x / G;
   const int r = dst[q];
   if (head[r] != static_cast<int>(q)) return;  // group-uniform
+  const int n_pos = cnt[r];
+  if (n_pos > kWalkMax) return;  // the heavy kernel's row
   const float gB = -(*grad) / static_cast<float>(a.B);
   constexpr int NV = 4;  // float4 column blocks per lane: d / 4 <= NV·G for every group_for(d)
   float acc[NV][4];
@@ -150,7 +163,7 @@ __global__ __launch_bounds__(kBlock) void k_bpr_bwd_rows(BprArgs a, const float*
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[v][i] = 0.f;
   auto add = [&](int64_t j) {
-    const int64_t k = j < a.B ? j : (j < 2 * a.B ? j - a.B : j - 2 * a.B);
+    const int64_t k = batch_row(a, j);
     const float t = gB * coef[k];
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
@@ -171,55 +184,12 @@ __global__ __launch_bounds__(kBlock) void k_bpr_bwd_rows(BprArgs a, const float*
       }
     }
   };
-  // add(js[0]) … add(js[cnt-1]) in that order, the rows of all of them loaded first
-  auto add4 = [&](const int64_t (&js)[4], int cnt) {
-    float t4[4];
-    int64_t k4[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int64_t j = js[u];
-      k4[u] = j < a.B ? j : (j < 2 * a.B ? j - a.B : j - 2 * a.B);
-      t4[u] = u < cnt ? gB * coef[k4[u]] : 0.f;
-    }
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      const int c = 4 * (l + v * G);
-      if (c >= a.d) break;
-      float r1[4][4], r2[4][4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (u >= cnt) continue;
-        if (js[u] < a.B) {
-          load_vec<4>(a.E + static_cast<int64_t>(dst[a.B + k4[u]]) * a.lde + c, r1[u]);
-          load_vec<4>(a.E + static_cast<int64_t>(dst[2 * a.B + k4[u]]) * a.lde + c, r2[u]);
-        } else {
-          load_vec<4>(a.E + static_cast<int64_t>(dst[k4[u]]) * a.lde + c, r1[u]);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (u >= cnt) continue;
-        if (js[u] < a.B) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) acc[v][i] += t4[u] * (r1[u][i] - r2[u][i]);
-        } else {
-          const float sg = js[u] < 2 * a.B ? t4[u] : -t4[u];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) acc[v][i] += sg * r1[u][i];
-        }
-      }
-    }
-  };
-  // walk the list once: its length (up to CAP + 1), and entry t in slot t (written by lane
-  // t mod G)
-  int n_pos = 0;
-  for (int e = static_cast<int>(q); e >= 0; e = next[e]) {
-    if (n_pos < CAP && n_pos % G == l) s_list[grp][n_pos] = e;
-    if (++n_pos > CAP) break;
-  }
   if (n_pos == 1) {
     add(q);
-  } else if (n_pos <= CAP) {
+  } else {
+    int e = static_cast<int>(q);
+    for (int t = 0; t < n_pos; ++t, e = next[e])
+      if (t % G == l) s_list[grp][t] = e;
     // the group's lanes are one wave's: order the LDS writes before the other lanes' reads
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -234,48 +204,143 @@ __global__ __launch_bounds__(kBlock) void k_bpr_bwd_rows(BprArgs a, const float*
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     for (int t = 0; t < n_pos; ++t) add(s_sorted[grp][t]);
-  } else {
-    // ascending scan of dst[]: lane l tests positions base + l·K + [0, K); the group's lanes
-    // with hits are taken in lane order (ballot), each lane's hits in k order (its mask,
-    // broadcast) — i.e. ascending positions, the order of the other paths
-    constexpr int K = 16;
-    const int P = static_cast<int>(3 * a.B);
-    const int g0 = static_cast<int>(threadIdx.x & 63) - l;  // the group's first lane in the wave
-    for (int base = 0; base < P; base += K * G) {
-      unsigned hits = 0;
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const int e = base + l * K + k;
-        if (e < P && dst[e] == r) hits |= 1u << k;
-      }
-      unsigned long long lanes = __ballot(hits != 0u);
-      if (G < 64) lanes = (lanes >> g0) & ((1ull << G) - 1ull);
-      while (lanes) {
-        const int src = __ffsll(static_cast<unsigned long long>(lanes)) - 1;
-        lanes &= lanes - 1ull;
-        unsigned m = static_cast<unsigned>(__shfl(static_cast<int>(hits), g0 + src));
-        while (m) {  // up to four positions at a time: their loads in flight together
-          int64_t js[4];
-          int cnt = 0;
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            js[u] = 0;
-            if (m) {
-              js[u] = base + src * K + (__ffs(m) - 1);
-              m &= m - 1u;
-              ++cnt;
-            }
-          }
-          add4(js, cnt);
-        }
-      }
-    }
   }
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const int c = 4 * (l + v * G);
     if (c >= a.d) break;
     store_vec<4>(dE + static_cast<int64_t>(r) * ldd + c, acc[v]);
+  }
+}
+
+// The rows with more than kWalkMax positions (a skewed catalogue's popular items: under
+// Zipf(1.2) popularity one item is the positive of ~740 of 4,096 rows), one workgroup per row
+// (the blocks loop over the heavy list). Per window of kWin positions: every thread tests its
+// 16 consecutive positions against the row, a block scan of the hit counts writes the row's
+// positions to LDS in ascending order, the GPB lane groups sum contiguous ranges of them (U rows
+// loaded before they are added) and group 0 adds the group partials in group order to the row.
+// The order is fixed by (batch, d), so the result is deterministic; every load of a window is
+// independent, where one lane group walking the row's list — or scanning the batch alone — paid
+// a dependent load per position (the round-4 scan path took ~0.5 ms on that batch).
+template <int G>
+__global__ __launch_bounds__(kBlock) void k_bpr_bwd_heavy(BprArgs a, const float* coef,
+                                                         const float* grad, const int* dst,
+                                                         const int* heavy, const int* n_heavy,
+                                                         float* dE, int64_t ldd) {
+  constexpr int GPB = kBlock / G;
+  constexpr int NV = 4;
+  constexpr int U = 8;
+  __shared__ int s_hits[kWin];
+  __shared__ int s_wave[kBlock / 64];
+  __shared__ float s_part[GPB][NV * G * 4];
+  const int tid = threadIdx.x, l = tid % G, grp = tid / G;
+  const int lane = tid & 63, wave = tid >> 6;
+  const float gB = -(*grad) / static_cast<float>(a.B);
+  const int P = static_cast<int>(3 * a.B);
+  const int nh = *n_heavy;
+  for (int h = blockIdx.x; h < nh; h += gridDim.x) {
+    const int r = heavy[h];
+    float acc[NV][4];
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[v][i] = 0.f;
+    for (int base = 0; base < P; base += kWin) {
+      const int p0 = base + 16 * tid;
+      unsigned m = 0;
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (p0 + k < P && dst[p0 + k] == r) m |= 1u << k;
+      const int c = __popc(m);
+      int incl = c;  // inclusive scan over the wave, then the waves in order
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+      }
+      if (lane == 63) s_wave[wave] = incl;
+      __syncthreads();
+      int off = 0, n = 0;
+#pragma unroll
+      for (int w = 0; w < kBlock / 64; ++w) {
+        const int t = s_wave[w];
+        off += w < wave ? t : 0;
+        n += t;
+      }
+      int pos = off + incl - c;
+      while (m) {
+        s_hits[pos++] = p0 + __ffs(m) - 1;
+        m &= m - 1u;
+      }
+      __syncthreads();
+      if (n == 0) continue;  // block-uniform
+      const int lo = static_cast<int>(static_cast<int64_t>(n) * grp / GPB);
+      const int hi = static_cast<int>(static_cast<int64_t>(n) * (grp + 1) / GPB);
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        const int cc = 4 * (l + v * G);
+        if (cc >= a.d) break;
+        float part[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int t0 = lo; t0 < hi; t0 += U) {
+          float r1[U][4], r2[U][4], tt[U];
+          bool anc[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            anc[u] = false;
+            tt[u] = 0.f;
+            if (t0 + u < hi) {
+              const int64_t j = s_hits[t0 + u];
+              const int64_t k = batch_row(a, j);
+              const float t = gB * coef[k];
+              anc[u] = j < a.B;
+              if (anc[u]) {
+                tt[u] = t;
+                load_vec<4>(a.E + static_cast<int64_t>(dst[a.B + k]) * a.lde + cc, r1[u]);
+                load_vec<4>(a.E + static_cast<int64_t>(dst[2 * a.B + k]) * a.lde + cc, r2[u]);
+              } else {
+                tt[u] = j < 2 * a.B ? t : -t;
+                load_vec<4>(a.E + static_cast<int64_t>(dst[k]) * a.lde + cc, r1[u]);
+              }
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            if (t0 + u < hi) {
+              if (anc[u]) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) part[i] += tt[u] * (r1[u][i] - r2[u][i]);
+              } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) part[i] += tt[u] * r1[u][i];
+              }
+            }
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s_part[grp][4 * (l + v * G) + i] = part[i];
+      }
+      __syncthreads();
+      if (grp == 0) {
+        for (int s = 0; s < GPB; ++s) {
+#pragma unroll
+          for (int v = 0; v < NV; ++v) {
+            const int cc = 4 * (l + v * G);
+            if (cc >= a.d) break;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[v][i] += s_part[s][cc + i];
+          }
+        }
+      }
+      __syncthreads();  // s_hits / s_part are refilled by the next window
+    }
+    if (grp == 0) {
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        const int cc = 4 * (l + v * G);
+        if (cc >= a.d) break;
+        store_vec<4>(dE + static_cast<int64_t>(r) * ldd + cc, acc[v]);
+      }
+    }
   }
 }
 
@@ -305,8 +370,10 @@ using namespace hgd;
 
 extern "C" size_t hgd_bpr_workspace_size(int64_t batch, int64_t n_rows) {
   const size_t b = static_cast<size_t>(batch > 0 ? batch : 0);
-  return align_up(b * 4) + align_up(static_cast<size_t>(n_rows > 0 ? n_rows : 0) * 4) +
-         2 * align_up(3 * b * 4);
+  const size_t n = static_cast<size_t>(n_rows > 0 ? n_rows : 0);
+  // term | head | next | dst | cnt | n_heavy | heavy rows
+  return align_up(b * 4) + align_up(n * 4) + 2 * align_up(3 * b * 4) + align_up(n * 4) +
+         align_up(4) + align_up((3 * b / (kWalkMax + 1) + 1) * 4);
 }
 
 extern "C" hgd_status hgd_bpr_forward(const float* E, int64_t lde, int64_t n_users,
@@ -364,20 +431,32 @@ extern "C" hgd_status hgd_bpr_backward(const float* E, int64_t lde, int64_t n_us
   int* head = reinterpret_cast<int*>(w);
   w += align_up(static_cast<size_t>(N) * 4);
   int* next = reinterpret_cast<int*>(w);
-  int* dst = reinterpret_cast<int*>(w + align_up(static_cast<size_t>(3 * batch) * 4));
+  w += align_up(static_cast<size_t>(3 * batch) * 4);
+  int* dst = reinterpret_cast<int*>(w);
+  w += align_up(static_cast<size_t>(3 * batch) * 4);
+  int* cnt = reinterpret_cast<int*>(w);
+  w += align_up(static_cast<size_t>(N) * 4);
+  int* n_heavy = reinterpret_cast<int*>(w);
+  int* heavy = reinterpret_cast<int*>(w + align_up(4));
   hipStream_t st = as_stream(stream);
   const int64_t init_n = std::max<int64_t>(N * (d / 4), N);
   hipLaunchKernelGGL(k_bpr_bwd_init, dim3(grid_for(init_n)), dim3(kBlock), 0, st, dE, ldd, N, d,
-                     head);
+                     head, cnt, n_heavy);
   hipLaunchKernelGGL(k_bpr_bwd_link, dim3(grid_for(3 * batch)), dim3(kBlock), 0, st, a, head,
-                     next, dst);
+                     next, dst, cnt, heavy, n_heavy);
   const int G = group_for(d);
   const unsigned blocks = static_cast<unsigned>((3 * batch + kBlock / G - 1) / (kBlock / G));
+#define HGD_BPR_ROWS(GG)                                                                        \
+  hipLaunchKernelGGL(k_bpr_bwd_rows<GG>, dim3(blocks), dim3(kBlock), 0, st, a, coef, grad, head, \
+                     next, dst, cnt, dE, ldd);                                                   \
+  hipLaunchKernelGGL(k_bpr_bwd_heavy<GG>, dim3(kHeavyGrid), dim3(kBlock), 0, st, a, coef, grad, \
+                     dst, heavy, n_heavy, dE, ldd)
   switch (G) {
-    case 64: hipLaunchKernelGGL(k_bpr_bwd_rows<64>, dim3(blocks), dim3(kBlock), 0, st, a, coef, grad, head, next, dst, dE, ldd); break;
-    case 16: hipLaunchKernelGGL(k_bpr_bwd_rows<16>, dim3(blocks), dim3(kBlock), 0, st, a, coef, grad, head, next, dst, dE, ldd); break;
-    case 4: hipLaunchKernelGGL(k_bpr_bwd_rows<4>, dim3(blocks), dim3(kBlock), 0, st, a, coef, grad, head, next, dst, dE, ldd); break;
-    default: hipLaunchKernelGGL(k_bpr_bwd_rows<1>, dim3(blocks), dim3(kBlock), 0, st, a, coef, grad, head, next, dst, dE, ldd); break;
+    case 64: HGD_BPR_ROWS(64); break;
+    case 16: HGD_BPR_ROWS(16); break;
+    case 4: HGD_BPR_ROWS(4); break;
+    default: HGD_BPR_ROWS(1); break;
   }
+#undef HGD_BPR_ROWS
   return check_launch("hgd_bpr_backward");
 }

@@ -32,17 +32,26 @@
 namespace hgd {
 namespace {
 
-// Split-plan defaults, the same policy as incidence.auto_split (Python): large structures split
-// only rows above 2048 nonzeros into 512-nonzero chunks; a structure with fewer rows than the
-// lane-group tasks that fill the chip (256 CUs × 16 waves × 4 groups) is cut finer.
+// Split-plan defaults, the same policy as incidence.auto_split (Python). A row walked by one
+// lane group costs about 1.4 µs per 16 nonzeros of dependent index → gather round trips, so an
+// unsplit row of T nonzeros ends the hop no sooner than ~T/11 µs: large structures split rows
+// above pow2_floor(nnz / 8192) nonzeros (clamped to [128, 2048]) into chunks of half that (at most
+// 512) — the longest walk stays a fraction of the whole hop's streaming time (a skewed catalogue's hop,
+// scripts/bench_skewed_hop.py: 180 µs at 2048 / 512, 43 µs at 128 / 64); a structure with fewer
+// rows than the lane-group tasks that fill the chip (256 CUs × 16 waves × 4 groups) is cut
+// finer.
 constexpr int64_t kSplitThreshold = 2048;
 constexpr int32_t kSplitChunk = 512;
+constexpr int64_t kSplitThresholdMin = 128;
+constexpr int64_t kSplitNnzPerThreshold = 8192;
 constexpr int64_t kTargetGroups = 16384;
 
 void auto_split(int64_t n_rows, int64_t nnz, int64_t* threshold, int32_t* chunk) {
   if (n_rows >= kTargetGroups || nnz == 0) {
-    *threshold = kSplitThreshold;
-    *chunk = kSplitChunk;
+    int64_t t = kSplitThresholdMin;
+    while (2 * t <= nnz / kSplitNnzPerThreshold && t < kSplitThreshold) t *= 2;
+    *threshold = t;
+    *chunk = static_cast<int32_t>(std::min<int64_t>(t / 2, kSplitChunk));
     return;
   }
   const int64_t want = std::max<int64_t>(1, nnz / kTargetGroups);

@@ -28,18 +28,29 @@ from . import profiling
 
 DEFAULT_SPLIT_THRESHOLD = 2048
 DEFAULT_SPLIT_CHUNK = 512
+SPLIT_THRESHOLD_MIN = 128
+SPLIT_NNZ_PER_THRESHOLD = 8192
 SEGMENTED_MAX_AVG_DEGREE = 32
 # lane-group tasks needed to fill MI355X: 256 CUs × 16 waves × 4 groups of 16 lanes (d = 64)
 TARGET_GROUPS = 16384
 
 
 def auto_split(n_rows: int, nnz: int) -> Tuple[int, int]:
-    """(threshold, chunk) for the long-row split. Large structures keep 2048 / 512 (split only
-    the popular outliers). A structure with fewer rows than TARGET_GROUPS (e.g. ML-1M's 3,706
-    items × ~200 nonzeros) would leave most CUs idle with one group per row, so its rows are cut
-    into chunks of ≈ nnz / TARGET_GROUPS nonzeros (power of two in [32, 512])."""
+    """(threshold, chunk) for the long-row split. A row walked by one lane group costs ~1.4 µs
+    per 16 nonzeros (dependent index → gather round trips), so one unsplit row of T nonzeros
+    ends the hop no sooner than ~T/11 µs: large structures split rows above
+    pow2_floor(nnz / 8192) nonzeros, clamped to [128, 2048], into chunks of half that (at most
+    512) — the longest walk stays a fraction of the hop's streaming time. (A skewed catalogue's hop,
+    scripts/bench_skewed_hop.py: 180 µs at 2048 / 512, 43 µs at 128 / 64; uniform graphs keep
+    their rows whole — their degrees stay far below the threshold.) A structure with fewer
+    rows than TARGET_GROUPS (e.g. ML-1M's 3,706 items × ~200 nonzeros) would leave most CUs idle
+    with one group per row, so its rows are cut into chunks of ≈ nnz / TARGET_GROUPS nonzeros
+    (power of two in [32, 512])."""
     if n_rows >= TARGET_GROUPS or nnz == 0:
-        return DEFAULT_SPLIT_THRESHOLD, DEFAULT_SPLIT_CHUNK
+        t = SPLIT_THRESHOLD_MIN
+        while 2 * t <= nnz // SPLIT_NNZ_PER_THRESHOLD and t < DEFAULT_SPLIT_THRESHOLD:
+            t *= 2
+        return t, min(t // 2, DEFAULT_SPLIT_CHUNK)
     want = max(1, nnz // TARGET_GROUPS)
     chunk = 32
     while chunk < want and chunk < DEFAULT_SPLIT_CHUNK:

@@ -737,8 +737,11 @@ hgd_status hgd_unique_dev_group(const hgd_unique_job* jobs, int32_t count, void*
  *   loss = mean_k −log(1e-5 + σ(⟨anc_k,pos_k⟩ − ⟨anc_k,neg_k⟩)), coef_k = σ(1−σ)/(1e-5+σ).
  * anc_out / pos_out ([batch, d], optional) receive the gathered rows (HCCF's InfoNCE node lists
  * are taken from them). Backward: dE = ∂(grad·loss)/∂E written in full (zero rows included;
- * `grad` a device scalar), every touched row summed over its positions in position order
- * (deterministic; integer atomics only). Workspace: hgd_bpr_workspace_size(batch, n_rows). */
+ * `grad` a device scalar), every touched row summed over its positions in a fixed order
+ * (position order for rows with at most 8 positions; rows with more — a skewed catalogue's
+ * popular items — by one workgroup in fixed contiguous ranges of their ascending positions,
+ * combined in range order): deterministic, integer atomics only.
+ * Workspace: hgd_bpr_workspace_size(batch, n_rows). */
 size_t hgd_bpr_workspace_size(int64_t batch, int64_t n_rows);
 hgd_status hgd_bpr_forward(const float* E, int64_t lde, int64_t n_users, int64_t n_items,
                            int32_t d, const int64_t* uid, const int64_t* pid, const int64_t* nid,

@@ -85,6 +85,24 @@ def main():
         rec.graph_step(*b)
     torch.cuda.synchronize()
     out["epoch_s"] = round(time.perf_counter() - t, 4)
+    # the epoch with fewer host threads for the drop-edge draw (HGD_TUNE_CPU_RNG_THREADS = 12):
+    # the draw's threads and the loop's own thread share the box's cores
+    from hypergraph_diffusion_for_recommendation_amd import _native as nat
+    lib = nat.load()
+    by_threads = {}
+    try:
+        for th in (16, 12, 8, 4):
+            nat.check(lib.hgd_set_tuning(12, th), "hgd_set_tuning")
+            t = time.perf_counter()
+            for b in next_batch_pairwise(rec.data, rec.batchSize, device=dev):
+                rec.graph_step(*b)
+            torch.cuda.synchronize()
+            by_threads[str(th)] = round(time.perf_counter() - t, 4)
+    finally:
+        nat.check(lib.hgd_set_tuning(12, 0), "hgd_set_tuning")
+    out["epoch_s_by_rng_threads"] = by_threads
+    out["cpu_count"] = os.cpu_count()
+    out["affinity"] = len(os.sched_getaffinity(0))
     print(json.dumps(out), flush=True)
 
 
