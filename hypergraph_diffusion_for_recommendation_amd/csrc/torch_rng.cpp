@@ -16,7 +16,8 @@
 // so the caller hands it back with torch.set_rng_state; the Python side checks the layout once
 // against torch.rand itself before using this path.
 #include <algorithm>
-#include <condition_variable>
+#include <atomic>
+#include <climits>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -26,6 +27,10 @@
 #include <mutex>
 #include <thread>
 #include <vector>
+
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include "../../include/hgd.h"
 #include "hgd_internal.h"
@@ -77,7 +82,10 @@ __attribute__((always_inline)) inline uint32_t temper(uint32_t y) {
 
 // The draw loop, shared by the AVX2 and the baseline build of it (selected at run time): the
 // tempering / compare loop and both halves of the state refill auto-vectorise.
-struct Draws {
+// One cache-line-aligned object per drawing thread: the split draw keeps the threads' states
+// side by side, and an unpadded state's counters shared a line with its neighbour's first words
+// (rewritten every refill) — a line bouncing between two cores every 624 draws.
+struct alignas(64) Draws {
   uint32_t s[kN];
   int left;
   uint32_t next;
@@ -87,18 +95,20 @@ __attribute__((always_inline)) inline int64_t draw_mask(Draws& g, int64_t n, flo
                                                         uint8_t* mask) {
   int64_t cnt = 0;
   int64_t k = 0;
+  int left = g.left;  // in registers: the byte stores below may not alias them
+  uint32_t next = g.next;
   while (k < n) {
     // at::mt19937::operator(): if (--left == 0) next_state(); y = state[next++]
-    if (--g.left == 0) {
+    if (--left == 0) {
       next_state(g.s);
-      g.left = kN;
-      g.next = 0;
+      left = kN;
+      next = 0;
     }
     // calls that succeed before the next refill: `left` of them (this one included), each
     // consuming s[next++]
-    const int64_t run = std::min<int64_t>(n - k, g.left);
-    const uint32_t* src = g.s + g.next;
-    uint8_t* dst = mask + k;
+    const int64_t run = std::min<int64_t>(n - k, left);
+    const uint32_t* __restrict__ src = g.s + next;
+    uint8_t* __restrict__ dst = mask + k;
     int64_t c = 0;
     for (int64_t t = 0; t < run; ++t) {
       const uint32_t y = temper(src[t]);
@@ -109,10 +119,12 @@ __attribute__((always_inline)) inline int64_t draw_mask(Draws& g, int64_t n, flo
       c += m;
     }
     cnt += c;
-    g.next += static_cast<uint32_t>(run);
-    g.left -= static_cast<int>(run - 1);  // the first call of the run already decremented
+    next += static_cast<uint32_t>(run);
+    left -= static_cast<int>(run - 1);  // the first call of the run already decremented
     k += run;
   }
+  g.left = left;
+  g.next = next;
   return cnt;
 }
 
@@ -361,7 +373,21 @@ __attribute__((target("avx2"))) void jump_array_avx2(const uint32_t* cur,
   }
 }
 
-// A small persistent pool for the split draws (one call at a time).
+// Futex waits on one 32-bit word (private to the process).
+inline void futex_wait(std::atomic<uint32_t>* w, uint32_t seen) {
+  syscall(SYS_futex, reinterpret_cast<uint32_t*>(w), FUTEX_WAIT_PRIVATE, seen, nullptr, nullptr,
+          0);
+}
+inline void futex_wake(std::atomic<uint32_t>* w, int n) {
+  syscall(SYS_futex, reinterpret_cast<uint32_t*>(w), FUTEX_WAKE_PRIVATE, n, nullptr, nullptr, 0);
+}
+
+// A small persistent pool for the split draws (one call at a time). A call bumps the wake word
+// of each worker it needs (one futex wake per worker; the others sleep on), each of them runs
+// its task and counts itself off, and the caller runs task 0 and then waits for the count to
+// reach zero. No mutex on either path: a condition variable's notify_all woke every worker and
+// made them re-take one mutex in turn on the way in and again on the way out — a convoy that
+// cost more than the draws' jumps at 16 threads (scripts/diag/diag_cpu_mask_threads.py).
 class Pool {
  public:
   static Pool& get() {  // never destroyed: its detached workers wait on it until the process ends
@@ -371,50 +397,54 @@ class Pool {
   std::mutex call_mu;  // serialises whole calls
   void run(int n_tasks, const std::function<void(int)>& fn) {
     ensure(n_tasks - 1);
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      fn_ = &fn;
-      n_tasks_ = n_tasks;
-      pending_ = n_tasks - 1;
-      ++gen_;
+    fn_ = &fn;
+    pending_.store(static_cast<uint32_t>(n_tasks - 1), std::memory_order_relaxed);
+    for (int i = 1; i < n_tasks; ++i) {
+      slots_[i].go.fetch_add(1, std::memory_order_release);  // publishes fn_ / pending_
+      futex_wake(&slots_[i].go, 1);
     }
-    cv_.notify_all();
     fn(0);
-    std::unique_lock<std::mutex> lk(mu_);
-    done_cv_.wait(lk, [&] { return pending_ == 0; });
+    for (int spin = 0;; ++spin) {  // a short spin, then sleep on the count
+      const uint32_t p = pending_.load(std::memory_order_acquire);
+      if (p == 0) break;
+      if (spin < 256)
+        _mm_pause();
+      else
+        futex_wait(&pending_, p);
+    }
     fn_ = nullptr;
   }
 
  private:
+  static constexpr int kMaxWorkers = 64;
+  struct alignas(64) Slot {
+    std::atomic<uint32_t> go{0};
+  };
   void ensure(int workers) {
-    while (static_cast<int>(threads_.size()) < workers) {
-      const int idx = static_cast<int>(threads_.size()) + 1;
-      threads_.emplace_back([this, idx] { loop(idx); });
-      threads_.back().detach();
+    while (threads_ < workers && threads_ < kMaxWorkers - 1) {
+      const int idx = ++threads_;
+      std::thread([this, idx] { loop(idx); }).detach();
     }
   }
   void loop(int idx) {
-    uint64_t seen = 0;
+    uint32_t seen = 0;  // the slot's word starts at 0 and only this worker's calls bump it
     for (;;) {
-      const std::function<void(int)>* fn = nullptr;
-      {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return gen_ != seen; });
-        seen = gen_;
-        if (idx < n_tasks_) fn = fn_;
+      uint32_t g;
+      for (int spin = 0; (g = slots_[idx].go.load(std::memory_order_acquire)) == seen; ++spin) {
+        if (spin < 256)
+          _mm_pause();
+        else
+          futex_wait(&slots_[idx].go, seen);
       }
-      if (!fn) continue;
-      (*fn)(idx);
-      std::lock_guard<std::mutex> lk(mu_);
-      if (--pending_ == 0) done_cv_.notify_all();
+      seen = g;
+      (*fn_)(idx);
+      if (pending_.fetch_sub(1, std::memory_order_acq_rel) == 1) futex_wake(&pending_, 1);
     }
   }
-  std::mutex mu_;
-  std::condition_variable cv_, done_cv_;
-  std::vector<std::thread> threads_;
+  Slot slots_[kMaxWorkers];
+  std::atomic<uint32_t> pending_{0};
   const std::function<void(int)>* fn_ = nullptr;
-  int n_tasks_ = 0, pending_ = 0;
-  uint64_t gen_ = 0;
+  int threads_ = 0;  // workers started (indices 1 .. threads_); only run() starts them
 };
 
 int g_rng_threads = 0;  // HGD_TUNE_CPU_RNG_THREADS: 0 = auto, 1 = serial
