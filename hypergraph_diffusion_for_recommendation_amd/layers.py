@@ -114,13 +114,19 @@ def _native_cpu_mask_ok() -> bool:
 _EAGER_RNG_THREADS = int(os.environ.get("HGD_EAGER_RNG_THREADS", "8"))
 
 
-def _draw_keep_mask(state: torch.Tensor, n: int, keep: float, threads: int = 0):
+def _draw_keep_mask(state: torch.Tensor, n: int, keep: float, threads: int = 0,
+                    out: Optional[torch.Tensor] = None):
     """hgd_torch_cpu_keep_mask on a private copy of the generator state (advanced in place);
-    ctypes drops the GIL for the call, so it can run on the prefetch thread."""
+    ctypes drops the GIL for the call, so it can run on the prefetch thread. ``out``: a uint8
+    host buffer of n bytes to draw into (else a new pinned one)."""
     import ctypes
 
     from . import _native as nat
-    mask = torch.empty(n, dtype=torch.uint8, pin_memory=torch.cuda.is_available())
+    if out is not None and (out.dtype != torch.uint8 or out.numel() != n or out.is_cuda
+                            or not out.is_contiguous()):
+        raise ValueError("_draw_keep_mask: out must be a contiguous host uint8 buffer of n bytes")
+    mask = out if out is not None else torch.empty(n, dtype=torch.uint8,
+                                                   pin_memory=torch.cuda.is_available())
     kept = ctypes.c_int64(0)
     nat.check(nat.load().hgd_torch_cpu_keep_mask_threads(
         state.data_ptr(), state.numel(), n, float(keep), mask.data_ptr() if n else None,
@@ -243,41 +249,56 @@ def torch_cpu_keep_mask(n: int, keep: float, prefetch: bool = True):
 
 class _MaskStager:
     """The next step's drop-edge masks on the device before its replay starts: the worker thread
-    that draws them (SpAdjDropEdge.refill) also copies them host → device into one of two
-    staging buffers on a side stream, so the transfer (7.4 MB per HCCF step, ~0.15 ms over PCIe)
-    runs under the current replay instead of in front of the next one; the replay's stream then
-    waits for that copy and moves the masks into the slots with one device-to-device pass. A
-    staging buffer is refilled only after the slot copies that read it (an event per buffer)."""
+    that draws them (SpAdjDropEdge.refill) draws into one of two pinned host buffers and copies
+    it host → device into the matching device staging buffer on a side stream, so the transfer
+    (7.4 MB per HCCF step, ~0.15 ms over PCIe) runs under the current replay instead of in front
+    of the next one; the replay's stream then waits for that copy and moves the masks into the
+    slots with one device-to-device pass. A pair of buffers is refilled only after the copies
+    that read it (an event per buffer for each direction). The host buffers are the stager's own:
+    a fresh pinned block per step left the caching host allocator allocating whenever the host
+    ran a few steps ahead of the device (multi-millisecond stalls)."""
 
     def __init__(self, device, total: int):
         self.device = torch.device(device)
         self.total = int(total)
         self.bufs = [torch.empty(self.total, dtype=torch.uint8, device=self.device)
                      for _ in range(2)]
-        self.free = [None, None]   # event: the slot copies that last read buffer k are done
+        self.host = [torch.empty(self.total, dtype=torch.uint8, pin_memory=True)
+                     for _ in range(2)]
+        self.free = [None, None]    # event: the slot copies that last read device buffer k
+        self.copied = [None, None]  # event: the H2D copy that last read host buffer k
         self.next = 0
         self.side = torch.cuda.Stream(self.device)
 
     def draw_and_stage(self, state: torch.Tensor, spec):
         """(masks, end state, staged) on the worker thread: the step's masks drawn as one
-        split draw and queued host → device on the side stream."""
-        masks, end = _draw_step_masks(state, spec)
-        flat = masks[0]._base if len(masks) > 1 and masks[0]._base is not None else None
-        if flat is None or flat.numel() != self.total or not flat.is_pinned():
-            return masks, end, None  # rates differ: the per-call masks, copied in refill
+        split draw into a host buffer and queued host → device on the side stream."""
+        if not (len(spec) > 1 and len({keep for _, keep in spec}) == 1
+                and sum(n for n, _ in spec) == self.total):
+            masks, end = _draw_step_masks(state, spec)  # rates differ: per-call masks, copied
+            return masks, end, None                     # in refill
         k = self.next
         self.next ^= 1
+        if self.copied[k] is not None:
+            self.copied[k].synchronize()  # its previous H2D copy has read it (long done)
+        host = self.host[k]
+        _, _, end = _draw_keep_mask(state, self.total, spec[0][1], out=host)
+        masks, off = [], 0
+        for n, _ in spec:
+            masks.append(host[off:off + n])
+            off += n
         torch.cuda.set_device(self.device)
         with torch.cuda.stream(self.side):
             if self.free[k] is not None:
                 self.side.wait_event(self.free[k])
-            self.bufs[k].copy_(flat, non_blocking=True)
+            self.bufs[k].copy_(host, non_blocking=True)
             done = torch.cuda.Event()
             done.record(self.side)
-        return masks, end, (k, done, flat)  # flat: the pinned source stays alive until done
+        self.copied[k] = done
+        return masks, end, (k, done, host)
 
     def into_slots(self, staged, slots, flat=None) -> None:
-        k, done, _flat = staged
+        k, done, _host = staged
         cur = torch.cuda.current_stream(self.device)
         cur.wait_event(done)
         if flat is not None and flat.numel() == self.total:  # the slots are views of one buffer

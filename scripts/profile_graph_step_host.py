@@ -119,20 +119,33 @@ def main():
     # the same steps with no host read between them (the plugin's loop reads the losses once
     # per epoch): the host prepares step k+1 while the device runs step k
     losses = []
+    pipe = {"refill": [], "prepare": [], "copy_inputs": [], "replay_call": [], "loss_clone": []}
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
         b = batches[k % len(batches)]
+        ta = time.perf_counter()
         dropper.refill()
+        tb = time.perf_counter()
         opt.prepare()
+        tc = time.perf_counter()
         for dst, src in zip(cap.static, b):
             dst.copy_(src)
+        td = time.perf_counter()
         cap.graph.replay()
+        te = time.perf_counter()
         losses.append(cap.out.detach().clone())
+        tf = time.perf_counter()
+        for name, v in (("refill", tb - ta), ("prepare", tc - tb), ("copy_inputs", td - tc),
+                        ("replay_call", te - td), ("loss_clone", tf - te)):
+            pipe[name].append(v * 1e6)
     t_host = time.perf_counter() - t0
     torch.cuda.synchronize()
     out_pipe = {"step_pipelined": round((time.perf_counter() - t0) / args.steps * 1e6, 1),
-                "host_issue_per_step": round(t_host / args.steps * 1e6, 1)}
+                "host_issue_per_step": round(t_host / args.steps * 1e6, 1),
+                "pipelined_host_us": {k: round(statistics.median(v[5:]), 1)
+                                      for k, v in pipe.items()},
+                "pipelined_host_max_us": {k: round(max(v[5:]), 1) for k, v in pipe.items()}}
     out = {k: round(statistics.median(v), 1) for k, v in rec.items()}
     out.update(out_pipe)
     out["draw_step_masks_alone"] = round(statistics.median(draws[2:]), 1)
