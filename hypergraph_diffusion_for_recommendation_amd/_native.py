@@ -184,6 +184,13 @@ class AdamTensor(ctypes.Structure):
                 ("exp_avg_sq", c_void_p), ("n", c_i64)]
 
 
+class MaskedSum(ctypes.Structure):
+    """Mirror of ``hgd_masked_sum`` (include/hgd.h)."""
+
+    _fields_ = [("dy", c_void_p * 8), ("mask", c_void_p * 8), ("out", c_void_p), ("n", c_i64),
+                ("count", c_i32), ("scale", c_f32)]
+
+
 class IncidenceView(ctypes.Structure):
     """Mirror of ``hgd_incidence_view`` (include/hgd.h)."""
 
@@ -340,6 +347,7 @@ _SIGNATURES = {
     "hgd_sum_arrays": (c_i32, [c_void_p, c_i32, c_i64, c_void_p, c_void_p]),
     "hgd_adam_step": (c_i32, [c_void_p, c_i32, c_void_p, c_void_p, c_i32, c_void_p]),
     "hgd_dropout_apply": (c_i32, [c_void_p, c_i64, c_void_p, c_f32, c_f32, c_void_p, c_void_p]),
+    "hgd_masked_scale_sum": (c_i32, [c_void_p, c_i32, c_void_p]),
     "hgd_bpr_workspace_size": (c_size, [c_i64, c_i64]),
     "hgd_bpr_forward": (c_i32, [c_void_p, c_i64, c_i64, c_i64, c_i32, c_void_p, c_void_p,
                                 c_void_p, c_i64, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -215,7 +215,8 @@ __global__ __launch_bounds__(kBlock) void k_bpr_bwd_rows(BprArgs a, const float*
 
 // The rows with more than kWalkMax positions (a skewed catalogue's popular items: under
 // Zipf(1.2) popularity one item is the positive of ~740 of 4,096 rows), one workgroup per row
-// (the blocks loop over the heavy list). Per window of kWin positions: every thread tests its
+// (the blocks loop over the heavy list). Per window of kWin positions (of the anchors for a user
+// row, of the positives and negatives for an item row): every thread tests its
 // 16 consecutive positions against the row, a block scan of the hit counts writes the row's
 // positions to LDS in ascending order, the GPB lane groups sum contiguous ranges of them (U rows
 // loaded before they are added) and group 0 adds the group partials in group order to the row.
@@ -245,12 +246,16 @@ __global__ __launch_bounds__(kBlock) void k_bpr_bwd_heavy(BprArgs a, const float
     for (int v = 0; v < NV; ++v)
 #pragma unroll
       for (int i = 0; i < 4; ++i) acc[v][i] = 0.f;
-    for (int base = 0; base < P; base += kWin) {
+    // a user row is only ever an anchor's destination, an item row a positive's or a
+    // negative's: scan that part of the batch
+    const int p_lo = r < a.nu ? 0 : static_cast<int>(a.B);
+    const int p_hi = r < a.nu ? static_cast<int>(a.B) : P;
+    for (int base = p_lo; base < p_hi; base += kWin) {
       const int p0 = base + 16 * tid;
       unsigned m = 0;
 #pragma unroll
       for (int k = 0; k < 16; ++k)
-        if (p0 + k < P && dst[p0 + k] == r) m |= 1u << k;
+        if (p0 + k < p_hi && dst[p0 + k] == r) m |= 1u << k;
       const int c = __popc(m);
       int incl = c;  // inclusive scan over the wave, then the waves in order
 #pragma unroll

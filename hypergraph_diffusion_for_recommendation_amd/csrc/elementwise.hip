@@ -6,6 +6,8 @@
 //             pre-activation, or on the output when slope >= 0 (same sign).
 //   sum_slices: the layer sum of HCCF's encoder, sum(hidden) (model/graph/HCCF.py:188), over
 //             the hidden tables stored as slices of one buffer — one pass instead of L adds.
+#include <algorithm>
+
 #include "device_util.h"
 #include "hgd_internal.h"
 
@@ -125,6 +127,61 @@ __global__ void k_dropout(const float* __restrict__ x, int64_t n, const uint64_t
   }
 }
 
+// The backward of L dropouts of one tensor (torch's native_dropout_backward per call,
+// g_k = ((float)mask_k · dy_k) · scale, then autograd's accumulation of the L gradients as they
+// arrive, the last call's first): out = ((g_{L-1} + g_{L-2}) + …) + g_0, one pass. Up to
+// kMaxMaskedSum calls per tensor and kMaxMaskedJobs tensors per launch (blockIdx.y). No
+// contraction: torch rounds the product and the sums separately.
+constexpr int kMaxMaskedSum = 8;
+constexpr int kMaxMaskedJobs = 4;
+struct MaskedSumJob {
+  const float* dy[kMaxMaskedSum];
+  const uint8_t* mask[kMaxMaskedSum];
+  float* out;
+  int64_t n;
+  int32_t count;
+  float scale;
+};
+struct MaskedSumJobs {
+  MaskedSumJob j[kMaxMaskedJobs];
+};
+
+#pragma clang fp contract(off)
+__global__ void k_masked_scale_sum(MaskedSumJobs J) {
+  const MaskedSumJob& b = J.j[blockIdx.y];
+  const int64_t i4 = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) * 4;
+  if (i4 >= b.n) return;
+  const int L = b.count;
+  if (i4 + 3 < b.n) {
+    float acc[4];
+    for (int k = L - 1; k >= 0; --k) {
+      const f32x4 d = *reinterpret_cast<const f32x4*>(b.dy[k] + i4);
+      const uint32_t m = *reinterpret_cast<const uint32_t*>(b.mask[k] + i4);
+      float g[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float mf = ((m >> (8 * t)) & 0xffu) ? 1.f : 0.f;
+        g[t] = (mf * d[t]) * b.scale;
+        acc[t] = k == L - 1 ? g[t] : acc[t] + g[t];
+      }
+    }
+    f32x4 o;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) o[t] = acc[t];
+    *reinterpret_cast<f32x4*>(b.out + i4) = o;
+  } else {
+    for (int64_t i = i4; i < b.n; ++i) {
+      float acc = 0.f;
+      for (int k = L - 1; k >= 0; --k) {
+        const float g = ((b.mask[k][i] ? 1.f : 0.f) * b.dy[k][i]) * b.scale;
+        acc = k == L - 1 ? g : acc + g;
+      }
+      b.out[i] = acc;
+    }
+  }
+}
+#pragma clang fp contract(on)
+
 inline bool aligned16(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
 
 }  // namespace hgd
@@ -196,4 +253,36 @@ extern "C" hgd_status hgd_dropout_apply(const float* x, int64_t n, const uint64_
   hipLaunchKernelGGL(k_dropout, dim3(grid_for((n + 3) / 4)), dim3(kBlock), 0, as_stream(stream),
                      x, n, seed, keep, scale, y);
   return check_launch("hgd_dropout_apply");
+}
+
+extern "C" hgd_status hgd_masked_scale_sum(const hgd_masked_sum* jobs, int32_t n_jobs,
+                                           void* stream) {
+  clear_error();
+  HGD_REQUIRE(jobs && n_jobs >= 1 && n_jobs <= kMaxMaskedJobs,
+              "hgd_masked_scale_sum: 1..%d jobs", kMaxMaskedJobs);
+  MaskedSumJobs J{};
+  int64_t n_max = 0;
+  for (int q = 0; q < n_jobs; ++q) {
+    const hgd_masked_sum& d = jobs[q];
+    HGD_REQUIRE(d.count >= 1 && d.count <= kMaxMaskedSum && d.n >= 0,
+                "hgd_masked_scale_sum: job %d: 1..%d gradients, n >= 0", q, kMaxMaskedSum);
+    HGD_REQUIRE(d.out && aligned16(d.out), "hgd_masked_scale_sum: job %d: out null/unaligned", q);
+    MaskedSumJob& b = J.j[q];
+    for (int k = 0; k < d.count; ++k) {
+      HGD_REQUIRE(d.dy[k] && d.mask[k] && aligned16(d.dy[k]) &&
+                      reinterpret_cast<uintptr_t>(d.mask[k]) % 4 == 0,
+                  "hgd_masked_scale_sum: job %d: dy / mask %d null or unaligned", q, k);
+      b.dy[k] = d.dy[k];
+      b.mask[k] = d.mask[k];
+    }
+    b.out = d.out;
+    b.n = d.n;
+    b.count = d.count;
+    b.scale = d.scale;
+    n_max = std::max<int64_t>(n_max, d.n);
+  }
+  if (n_max == 0) return HGD_OK;
+  hipLaunchKernelGGL(k_masked_scale_sum, dim3(grid_for((n_max + 3) / 4), n_jobs), dim3(kBlock), 0,
+                     as_stream(stream), J);
+  return check_launch("hgd_masked_scale_sum");
 }

@@ -24,7 +24,8 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from .functional import (dense_two_hop_pair, fan, hccf_layers, hccf_layers_supported, linear,
+from .functional import (dense_two_hop_pair, fan, hccf_layers, hccf_layers_supported,
+                         hyper_dropouts, linear,
                          split_rows, sum_n, two_hop_fused)
 from .incidence import Incidence, incidence_of
 from .layers import EquivSetGNN, GCNLayer, HGCNConv, HGNNLayer, LayerNorm, SpAdjDropEdge
@@ -68,6 +69,8 @@ class HCCFEncoder(nn.Module):
         self.edgeDropper = SpAdjDropEdge()
         # False: the per-layer module graph below (GCNLayer / dense_two_hop_pair and torch adds)
         self.fused_layers = True
+        # False: one nn.Dropout node per layer and table (bitwise the same results)
+        self.fused_dropouts = True
 
     def _parse_config(self, config):
         self.lRate = float(config['lrate'])
@@ -103,11 +106,22 @@ class HCCFEncoder(nn.Module):
             # the whole loop as one op (functional.hccf_layers): the layer sum, the layer adds
             # and autograd's accumulations ride in the hop / product stores. Same draws in the
             # same order as the loop below (drop-edge, then the two dropouts, per layer).
-            adjs, hus, his = [], [], []
-            for _ in range(self.n_layers):
-                adjs.append(incidence_of(self.edgeDropper(self.sparse_norm_adj, keep_rate)))
-                hus.append(self.drop_out(hyper_uu))
-                his.append(self.drop_out(hyper_ii))
+            # (the drop-edge draws use the CPU generator, the dropouts the device's: drawing
+            # the layers' drop-edges first leaves both streams as the reference's loop does)
+            adjs = [incidence_of(self.edgeDropper(self.sparse_norm_adj, keep_rate))
+                    for _ in range(self.n_layers)]
+            if (self.fused_dropouts and type(self.drop_out) is nn.Dropout
+                    and self.drop_out.training and not self.drop_out.inplace):
+                # the 2L dropouts as one autograd node (functional.hyper_dropouts: the same
+                # masks, the backward summed in one launch in autograd's order); a module put in
+                # drop_out's place is called as it is
+                drops = hyper_dropouts([hyper_uu, hyper_ii], self.drop_out.p, self.n_layers)
+                hus, his = [d[0] for d in drops], [d[1] for d in drops]
+            else:
+                hus, his = [], []
+                for _ in range(self.n_layers):
+                    hus.append(self.drop_out(hyper_uu))
+                    his.append(self.drop_out(hyper_ii))
             embeddings, gcn_hidden, hgnn_hidden = hccf_layers(
                 adjs, self.embedding_dict['user_emb'], self.embedding_dict['item_emb'], hus, his)
             user_emb, item_emb = torch.split(embeddings, [nu, embeddings.shape[0] - nu])

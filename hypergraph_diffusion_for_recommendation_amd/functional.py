@@ -27,6 +27,7 @@ import ctypes
 from typing import List, Optional, Tuple
 
 import torch
+import torch.nn.functional as F
 
 from . import _native as nat
 from .incidence import Incidence, spmm_csr
@@ -1356,6 +1357,71 @@ def hccf_layers(adjs, user_emb: torch.Tensor, item_emb: torch.Tensor, hypers_u, 
         Hs += [Hu, Hi]
     out = _HCCFLayers.apply(list(adjs), int(nu), user_emb, item_emb, *Hs)
     return out[0], list(out[1:1 + L]), list(out[1 + L:])
+
+
+class _HyperDropouts(torch.autograd.Function):
+    """``nn.Dropout(p)`` applied to each of ``tables`` once per layer, in the reference's call
+    order (HCCF.py:182-186: layer 0's user then item table, then layer 1's, …: the device
+    generator's stream), as ONE autograd node: the forward is torch's own ``native_dropout`` per
+    call (the same masks and outputs as the module), the backward one ``hgd_masked_scale_sum``
+    launch for all tables — per table the L masked gradients summed as autograd sums L separate
+    dropout nodes (the last call's first, each ((float)mask · dy) · scale), where the separate
+    nodes cost 2L masked-scale kernels and 2(L − 1) accumulation adds per step."""
+
+    @staticmethod
+    def forward(ctx, p, L, *tables):
+        outs, masks = [], []
+        for _ in range(L):
+            for t in tables:
+                o, m = torch.native_dropout(t, p, True)
+                outs.append(o)
+                masks.append(m)
+        ctx.save_for_backward(*masks)
+        ctx.p, ctx.L, ctx.T = p, L, len(tables)
+        ctx.shapes = [t.shape for t in tables]
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        masks = ctx.saved_tensors
+        L, T = ctx.L, ctx.T
+        dev = masks[0].device
+        scale = float(torch.tensor(1.0 / (1.0 - ctx.p), dtype=torch.float32))
+        outs, jobs, keep = [], [], []
+        for t in range(T):
+            out = torch.empty(ctx.shapes[t], dtype=torch.float32, device=dev)
+            job = nat.MaskedSum()
+            live = 0
+            for k in range(L):
+                g = grads[k * T + t]
+                if g is None:
+                    g = torch.zeros(ctx.shapes[t], dtype=torch.float32, device=dev)
+                g = g.contiguous()
+                keep.append(g)
+                job.dy[k] = g.data_ptr()
+                job.mask[k] = masks[k * T + t].data_ptr()
+                live += 1
+            job.out, job.n, job.count, job.scale = out.data_ptr(), out.numel(), live, scale
+            jobs.append(job)
+            outs.append(out)
+        arr = (nat.MaskedSum * len(jobs))(*jobs)
+        nat.check(nat.load().hgd_masked_scale_sum(arr, len(jobs), nat.stream_handle(dev)),
+                  "hgd_masked_scale_sum")
+        return (None, None, *outs)
+
+
+def hyper_dropouts(tables, p: float, L: int):
+    """``[[dropout(t) for t in tables] for _ in range(L)]`` with HCCF's module order and masks
+    (see :class:`_HyperDropouts`); falls back to the plain calls outside 0 < p < 1, for tables
+    that are not device fp32 with 16-byte-aligned rows, or for more than 8 layers / 4 tables."""
+    ok = (0.0 < p < 1.0 and 1 <= L <= 8 and 1 <= len(tables) <= 4
+          and all(t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()
+                  and t.data_ptr() % 16 == 0 and t.numel() % 4 == 0 for t in tables))
+    if not ok:
+        return [[F.dropout(t, p, True) for t in tables] for _ in range(L)]
+    outs = _HyperDropouts.apply(float(p), int(L), *tables)
+    T = len(tables)
+    return [list(outs[k * T:(k + 1) * T]) for k in range(L)]
 
 
 _BPR_BAD = {}

@@ -772,6 +772,22 @@ hgd_status hgd_epilogue_backward(const float* ref, const float* dy, int64_t n, i
  * first, is below floor(keep·65536 + 0.5) (f32). keep = 1 - p, scale = 1 / (1 - p). The
  * backward is the same call on the gradient with the same seed (no mask is stored). x, y
  * 16-byte aligned; y may alias x. */
+/* The backward of `count` nn.Dropout calls on one tensor (torch's native_dropout_backward per
+ * call, g_k = ((float)mask_k · dy_k) · scale, then autograd's accumulation of the calls'
+ * gradients as they arrive, the last call's first): out = ((g_{count-1} + g_{count-2}) + …) + g_0
+ * in one pass, products and sums rounded separately (bitwise torch's kernels). Up to 8 calls per
+ * job, up to 4 jobs (tensors) per launch; dy / out 16-byte aligned, masks (bool bytes) 4-byte
+ * aligned. HCCF's hypergraph dropouts (HCCF.py:182-186, one per layer on each of E_u·W_u and
+ * E_i·W_i) are two such jobs. */
+typedef struct hgd_masked_sum {
+  const float* dy[8];
+  const uint8_t* mask[8];
+  float* out;
+  int64_t n;
+  int32_t count;
+  float scale;
+} hgd_masked_sum;
+hgd_status hgd_masked_scale_sum(const hgd_masked_sum* jobs, int32_t n_jobs, void* stream);
 hgd_status hgd_dropout_apply(const float* x, int64_t n, const uint64_t* seed, float keep,
                              float scale, float* y, void* stream);
 /* out[i] = Σ_s P[s·slice_stride + i] over s = 0..n_slices-1, summed in slice order (bitwise the

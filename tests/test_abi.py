@@ -89,7 +89,8 @@ def test_struct_layouts_match_header(tmp_path):
     structs = {"hgd_split_plan": _native.SplitPlan, "hgd_row_epilogue": _native.RowEpilogue,
                "hgd_incidence_view": _native.IncidenceView,
                "hgd_gemm_rows_desc": _native.GemmRowsDesc, "hgd_gemm_tn_desc": _native.GemmTnDesc,
-               "hgd_infonce_term": _native.InfonceTerm, "hgd_adam_tensor": _native.AdamTensor}
+               "hgd_infonce_term": _native.InfonceTerm, "hgd_adam_tensor": _native.AdamTensor,
+               "hgd_masked_sum": _native.MaskedSum}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "hgd.h"', 'int main(void) {']
     for cname, py in structs.items():
         lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')

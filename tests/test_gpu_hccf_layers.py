@@ -129,6 +129,28 @@ def test_fused_layers_match_module_graph(dev, capture_safe, L):
         assert err <= 1e-5 * scale, (k, err, scale)
 
 
+@pytest.mark.parametrize("capture_safe", [True, False])
+@pytest.mark.parametrize("L", [1, 3])
+def test_fused_hyper_dropouts_are_the_module_dropouts(dev, capture_safe, L):
+    """functional.hyper_dropouts (the 2L hypergraph dropouts as one node, the backward summed in
+    one hgd_masked_scale_sum launch) against one nn.Dropout node per layer and table: outputs,
+    loss and every parameter gradient bitwise equal — the same masks from the device generator,
+    and the same sums in autograd's accumulation order."""
+    U, I, d = 1500, 2200, 64
+    A = _norm_adj(U, I, 40_000, seed=12)
+    outs = {}
+    for fused in (False, True):
+        enc = _encoder(dev, A, U, I, d, L, capture_safe, True)
+        enc.fused_dropouts = fused
+        outs[fused] = _run(enc, dev, U, I, seed=9)
+    (o0, l0, g0), (o1, l1, g1) = outs[False], outs[True]
+    for a, b in zip(o0, o1):
+        assert torch.equal(a, b)
+    assert l0 == l1
+    for k in g0:
+        assert torch.equal(g0[k], g1[k]), (k, float((g0[k] - g1[k]).abs().max()))
+
+
 def test_fused_layers_eval_and_no_grad(dev):
     """keep_rate 1 (the eval forward, HCCF.py:103) under no_grad: same tables as the loop."""
     U, I, d = 700, 900, 32
