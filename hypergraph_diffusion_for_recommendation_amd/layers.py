@@ -24,6 +24,7 @@ device :class:`~.incidence.Incidence` (also accepted directly).
 from __future__ import annotations
 
 import os
+import time
 import weakref
 from typing import Optional
 
@@ -269,6 +270,7 @@ class _MaskStager:
         self.copied = [None, None]  # event: the H2D copy that last read host buffer k
         self.next = 0
         self.side = torch.cuda.Stream(self.device)
+        self.trace = None  # a list: per-job timings appended (scripts/profile_graph_step_host.py)
 
     def draw_and_stage(self, state: torch.Tensor, spec):
         """(masks, end state, staged) on the worker thread: the step's masks drawn as one
@@ -277,12 +279,16 @@ class _MaskStager:
                 and sum(n for n, _ in spec) == self.total):
             masks, end = _draw_step_masks(state, spec)  # rates differ: per-call masks, copied
             return masks, end, None                     # in refill
+        trace = self.trace
+        t0 = time.perf_counter() if trace is not None else 0.0
         k = self.next
         self.next ^= 1
         if self.copied[k] is not None:
             self.copied[k].synchronize()  # its previous H2D copy has read it (long done)
+        t1 = time.perf_counter() if trace is not None else 0.0
         host = self.host[k]
         _, _, end = _draw_keep_mask(state, self.total, spec[0][1], out=host)
+        t2 = time.perf_counter() if trace is not None else 0.0
         masks, off = [], 0
         for n, _ in spec:
             masks.append(host[off:off + n])
@@ -295,6 +301,8 @@ class _MaskStager:
             done = torch.cuda.Event()
             done.record(self.side)
         self.copied[k] = done
+        if trace is not None:  # (host_wait, draw, stage) µs per job, for the profile scripts
+            trace.append(((t1 - t0) * 1e6, (t2 - t1) * 1e6, (time.perf_counter() - t2) * 1e6))
         return masks, end, (k, done, host)
 
     def into_slots(self, staged, slots, flat=None) -> None:

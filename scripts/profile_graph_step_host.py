@@ -23,7 +23,12 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--switch-interval", type=float, default=None,
+                    help="sys.setswitchinterval for the run (seconds; the interpreter's GIL "
+                         "hand-off period, 0.005 by default)")
     args = ap.parse_args()
+    if args.switch_interval:
+        sys.setswitchinterval(args.switch_interval)
     import torch
 
     import refops as R
@@ -118,6 +123,8 @@ def main():
     cf.Future.result = orig_result
     # the same steps with no host read between them (the plugin's loop reads the losses once
     # per epoch): the host prepares step k+1 while the device runs step k
+    stager = dropper._stager()
+    stager.trace = []
     losses = []
     pipe = {"refill": [], "prepare": [], "copy_inputs": [], "replay_call": [], "loss_clone": []}
     torch.cuda.synchronize()
@@ -151,6 +158,12 @@ def main():
     out["draw_step_masks_alone"] = round(statistics.median(draws[2:]), 1)
     out["refill_wait_for_worker"] = round(statistics.median(waits[5:]), 1) if waits else None
     out["spec"] = spec
+    out["switch_interval"] = sys.getswitchinterval()
+    jobs = stager.trace[5:]
+    if jobs:
+        out["pipelined_worker_job_us"] = {
+            name: round(statistics.median(j[i] for j in jobs), 1)
+            for i, name in enumerate(("wait_host_buffer", "draw", "stage_h2d_issue"))}
     print(json.dumps(out), flush=True)
 
 
