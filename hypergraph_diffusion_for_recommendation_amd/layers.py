@@ -272,9 +272,12 @@ class _MaskStager:
         self.side = torch.cuda.Stream(self.device)
         self.trace = None  # a list: per-job timings appended (scripts/profile_graph_step_host.py)
 
-    def draw_and_stage(self, state: torch.Tensor, spec):
+    def draw_and_stage(self, state: torch.Tensor, spec, target: Optional[torch.Tensor] = None,
+                       target_free: Optional[torch.cuda.Event] = None):
         """(masks, end state, staged) on the worker thread: the step's masks drawn as one
-        split draw into a host buffer and queued host → device on the side stream."""
+        split draw into a host buffer and queued host → device on the side stream — into this
+        stager's device buffer, or straight into ``target`` (a slot bank's buffer) once
+        ``target_free`` (its last reader) has passed."""
         if not (len(spec) > 1 and len({keep for _, keep in spec}) == 1
                 and sum(n for n, _ in spec) == self.total):
             masks, end = _draw_step_masks(state, spec)  # rates differ: per-call masks, copied
@@ -295,9 +298,14 @@ class _MaskStager:
             off += n
         torch.cuda.set_device(self.device)
         with torch.cuda.stream(self.side):
-            if self.free[k] is not None:
-                self.side.wait_event(self.free[k])
-            self.bufs[k].copy_(host, non_blocking=True)
+            if target is not None:
+                if target_free is not None:
+                    self.side.wait_event(target_free)
+                target.copy_(host, non_blocking=True)
+            else:
+                if self.free[k] is not None:
+                    self.side.wait_event(self.free[k])
+                self.bufs[k].copy_(host, non_blocking=True)
             done = torch.cuda.Event()
             done.record(self.side)
         self.copied[k] = done
@@ -351,16 +359,23 @@ class SpAdjDropEdge(nn.Module):
         self._prefilled = False
         self._step_job = None  # (start state, spec, future) of the next step's masks
         self._stage = None     # device staging of the next step's masks (refill)
+        self._banks = []       # host_fed(banks=2): [(slots, flat buffer)] the refills alternate
+        self._refills = 0      # refills so far (a step's bank is refills % len(banks))
+        self._bank = 0         # the bank the slots are (0 without banks)
 
     def begin_step(self):
         """A step boundary: the next drop uses the first slot (encoders call it per forward)."""
         self._slot_i = 0
 
-    def host_fed(self, on: bool = True):
+    def host_fed(self, on: bool = True, banks: int = 1):
         """capture_safe masks on the reference's CPU stream drawn ahead by :meth:`refill` (for a
         captured step, whose replays do not run Python) instead of inside the step. Turning it
         on (before the step is captured) also lays the step's slots out as consecutive views of
-        one buffer, so a refill moves them with one device copy."""
+        one buffer, so a refill moves them with one device copy. ``banks=2`` keeps two such
+        buffers that the refills alternate between (:meth:`use_bank` selects one for a capture):
+        the draw worker copies a step's masks host → device straight into its bank while the
+        previous step — on the other bank — runs, so no device-to-device pass is left between
+        two replays (one captured step per bank)."""
         self._prefilled = bool(on)
         if on and len(self._slots) > 1:
             flat = getattr(self, "_slot_flat", None)
@@ -374,6 +389,24 @@ class SpAdjDropEdge(nn.Module):
                     slots.append((n, keep, view))
                     off += n
                 self._slots, self._slot_flat = slots, flat
+                self._banks = []
+            if banks == 2 and len(self._banks) != 2:
+                flat2 = flat.clone()
+                slots2, off = [], 0
+                for n, keep, _ in self._slots:
+                    slots2.append((n, keep, flat2[off:off + n]))
+                    off += n
+                self._banks = [(self._slots, flat), (slots2, flat2)]
+                self._bank = 0
+
+    def use_bank(self, b: int) -> None:
+        """The slot bank the next drop calls read (a capture records that bank's buffers)."""
+        self._slots, self._slot_flat = self._banks[b]
+        self._bank = b
+
+    def upcoming_bank(self) -> int:
+        """The bank the next :meth:`refill` fills (0 without banks)."""
+        return self._refills % len(self._banks) if self._banks else 0
 
     def refill(self):
         """Draws the next step's masks from the CPU generator — the same draws, in the same
@@ -382,14 +415,20 @@ class SpAdjDropEdge(nn.Module):
         after are then drawn on a worker thread while this one runs (all library threads: a
         replayed step leaves the host idle), and used only if nothing else moved the generator
         in between — the stream stays the reference's either way."""
+        banked = len(self._banks) == 2
+        if banked:
+            self.use_bank(self._refills % 2)
+        self._refills += 1
         spec = tuple((n, keep) for n, keep, _ in self._slots)
         staged = None
+        cur = torch.cuda.current_stream(self._slots[0][2].device)
         if not _native_cpu_mask_ok():
             masks = [torch_cpu_keep_mask(n, keep, prefetch=False)[0] for n, keep in spec]
         else:
             st = torch.get_rng_state()
             job, self._step_job = getattr(self, "_step_job", None), None
-            if job is not None and job[1] == spec and torch.equal(job[0], st):
+            if job is not None and job[1] == spec and torch.equal(job[0], st) and (
+                    not banked or job[3] == self._bank):
                 masks, end, staged = job[2].result()
             else:
                 if job is not None:
@@ -397,11 +436,25 @@ class SpAdjDropEdge(nn.Module):
                 masks, end = _draw_step_masks(st, spec)
             torch.set_rng_state(end)
             stager = self._stager()
-            self._step_job = (end.clone(), spec,
-                              _step_pool().submit(stager.draw_and_stage, end.clone(), spec))
-        if staged is not None:  # already on the device: one D2D pass into the slots
-            self._stage.into_slots(staged, self._slots, getattr(self, "_slot_flat", None))
+            target = free = None
+            nxt = self._bank
+            if banked:
+                # the next step's bank was last read by the replay issued before this refill:
+                # an event recorded now orders the worker's copy into it after that replay
+                nxt = self._bank ^ 1
+                target = self._banks[nxt][1]
+                free = torch.cuda.Event()
+                free.record(cur)
+            self._step_job = (end.clone(), spec, _step_pool().submit(
+                stager.draw_and_stage, end.clone(), spec, target, free), nxt)
+        if staged is not None:
+            if banked:  # already in this step's bank: the replay only waits for the copy
+                cur.wait_event(staged[1])
+            else:  # in the staging buffer: one D2D pass into the slots
+                self._stage.into_slots(staged, self._slots, getattr(self, "_slot_flat", None))
         else:
+            if banked and self._stage is not None:
+                cur.wait_stream(self._stage.side)  # a discarded job's copy may target this bank
             for (n, keep, buf), mask in zip(self._slots, masks):
                 buf.copy_(mask, non_blocking=True)
         self._slot_i = 0

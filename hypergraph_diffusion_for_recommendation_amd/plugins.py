@@ -221,7 +221,10 @@ class HCCF(GraphRecommender):
             from .graphs import CapturedStep
             dropper = self.model.edgeDropper
             host_fed = not dropper.device_rng
-            dropper.host_fed(host_fed)  # the capture records the slots; refill() fills them
+            # the capture records the slots; refill() fills them — two slot banks and one
+            # captured step per bank on the reference's stream, so the draw worker's copy of
+            # the next step's masks goes straight into the bank the current replay does not read
+            dropper.host_fed(host_fed, banks=2 if host_fed else 1)
             opt = self.optimizer
             if self._adam_kernel:  # the graph holds the Adam kernel; its scalars come per replay
                 def body(u, i, j):
@@ -236,10 +239,15 @@ class HCCF(GraphRecommender):
             else:
                 body = self.train_step if self._adam_in_graph else self.forward_backward
                 before = dropper.refill if host_fed else None
-            self._captured = CapturedStep(body, (user_idx, pos_idx, neg_idx),
-                                          before_replay=before)
-            # the gradient buffers the replays write (an eager short batch rebinds .grad)
-            self._graph_grads = [p.grad for p in self.model.parameters()]
+            self._captured, self._graph_grads = [], []
+            for b in range(2 if host_fed and dropper._banks else 1):
+                if host_fed and dropper._banks:
+                    dropper.use_bank(b)
+                self._captured.append(CapturedStep(body, (user_idx, pos_idx, neg_idx),
+                                                   before_replay=before))
+                # the gradient buffers this graph's replays write (an eager short batch
+                # rebinds .grad)
+                self._graph_grads.append([p.grad for p in self.model.parameters()])
             return self._replay(user_idx, pos_idx, neg_idx)
         self._eager_steps = getattr(self, "_eager_steps", 0) + 1
         # detached: a caller holding the loss would keep the eager autograd graph — and with it
@@ -247,9 +255,10 @@ class HCCF(GraphRecommender):
         return self.train_step(user_idx, pos_idx, neg_idx).detach()
 
     def _replay(self, user_idx, pos_idx, neg_idx) -> torch.Tensor:
-        out = self._captured(user_idx, pos_idx, neg_idx).detach().clone()
+        b = self.model.edgeDropper.upcoming_bank() if len(self._captured) > 1 else 0
+        out = self._captured[b](user_idx, pos_idx, neg_idx).detach().clone()
         if not self._adam_in_graph:  # the reference's Adam on the replay's gradients
-            for p, g in zip(self.model.parameters(), self._graph_grads):
+            for p, g in zip(self.model.parameters(), self._graph_grads[b]):
                 p.grad = g
             self.optimizer.step()
         return out

@@ -153,6 +153,30 @@ def main():
                 "pipelined_host_us": {k: round(statistics.median(v[5:]), 1)
                                       for k, v in pipe.items()},
                 "pipelined_host_max_us": {k: round(max(v[5:]), 1) for k, v in pipe.items()}}
+    # two slot banks and one captured step per bank (the plugins' default): the worker copies
+    # the next step's masks straight into the bank the running replay does not read
+    dropper.host_fed(True, banks=2)
+    caps = []
+    for bank in range(2):
+        dropper.use_bank(bank)
+        capturing[0] = True
+        caps.append(CapturedStep(body, batches[1], before_replay=None))
+        capturing[0] = False
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        b = batches[k % len(batches)]
+        c = caps[dropper.upcoming_bank()]
+        dropper.refill()
+        opt.prepare()
+        for dst, src in zip(c.static, b):
+            dst.copy_(src)
+        c.graph.replay()
+        losses.append(c.out.detach().clone())
+    t_host = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    out_pipe["step_pipelined_banked"] = round((time.perf_counter() - t0) / args.steps * 1e6, 1)
+    out_pipe["host_issue_per_step_banked"] = round(t_host / args.steps * 1e6, 1)
     out = {k: round(statistics.median(v), 1) for k, v in rec.items()}
     out.update(out_pipe)
     out["draw_step_masks_alone"] = round(statistics.median(draws[2:]), 1)
