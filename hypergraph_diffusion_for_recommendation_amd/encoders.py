@@ -25,8 +25,8 @@ import torch
 import torch.nn as nn
 
 from .functional import (dense_two_hop_pair, fan, hccf_layers, hccf_layers_supported,
-                         hyper_dropouts, linear,
-                         split_rows, sum_n, two_hop_fused)
+                         hyper_dropouts, linear, split_rows, sum_n, table_projections,
+                         two_hop_fused)
 from .incidence import Incidence, incidence_of
 from .layers import EquivSetGNN, GCNLayer, HGCNConv, HGNNLayer, LayerNorm, SpAdjDropEdge
 
@@ -98,9 +98,11 @@ class HCCFEncoder(nn.Module):
     def forward(self, keep_rate=0.5):
         nu = self.data.n_users
         _begin_step(self.edgeDropper)
-        # E·W [n, d]·[d, K] on the skinny MFMA Linear (functional.linear takes W as [out, in])
-        hyper_uu = linear(self.embedding_dict['user_emb'], self.embedding_dict['user_w'].t())
-        hyper_ii = linear(self.embedding_dict['item_emb'], self.embedding_dict['item_w'].t())
+        # E·W [n, d]·[d, K] for both tables as one grouped op (functional.table_projections:
+        # W read in its own layout, the gradients in grouped launches)
+        hyper_uu, hyper_ii = table_projections(
+            [self.embedding_dict['user_emb'], self.embedding_dict['item_emb']],
+            [self.embedding_dict['user_w'], self.embedding_dict['item_w']])
         if self.fused_layers and hccf_layers_supported(self.embedding_dict['user_emb'],
                                                        self.embedding_dict['item_emb'], hyper_uu):
             # the whole loop as one op (functional.hccf_layers): the layer sum, the layer adds

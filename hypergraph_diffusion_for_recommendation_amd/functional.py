@@ -1359,6 +1359,65 @@ def hccf_layers(adjs, user_emb: torch.Tensor, item_emb: torch.Tensor, hypers_u, 
     return out[0], list(out[1:1 + L]), list(out[1 + L:])
 
 
+class _TableProjections(torch.autograd.Function):
+    """HCCF's learned hypergraphs ``[E_u·W_u, E_i·W_i]`` (HCCF.py:178-179; E [n, d], W [d, K]
+    as the parameters are stored) in grouped launches: the forward one row-GEMM launch for both
+    tables (W read in place — no transposed copy), the backward one row-GEMM launch for both
+    dE = dH·Wᵀ and one split-K launch for both dW = Eᵀ·dH, written in W's own layout. The
+    ``F.linear(E, W.t())`` form cost a contiguous copy of each Wᵀ, two launches per table each
+    way and a transposing copy of each weight gradient."""
+
+    @staticmethod
+    def forward(ctx, *EW):
+        T = len(EW) // 2
+        Es, Ws = [e.contiguous() for e in EW[:T]], [w.contiguous() for w in EW[T:]]
+        dev = Es[0].device
+        outs, descs = [], []
+        for E, W in zip(Es, Ws):
+            Y = torch.empty((E.shape[0], W.shape[1]), dtype=torch.float32, device=dev)
+            descs.append(_rows_desc(E, W, W.stride(0), 1, E.shape[1], W.shape[1], Y))
+            outs.append(Y)
+        _gemm_rows(descs, dev)
+        ctx.save_for_backward(*Es, *Ws)
+        ctx.T = T
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *dHs):
+        T = ctx.T
+        saved = ctx.saved_tensors
+        Es, Ws = saved[:T], saved[T:]
+        dev = Es[0].device
+        dHs = [torch.zeros((E.shape[0], W.shape[1]), dtype=torch.float32, device=dev)
+               if g is None else g.contiguous() for g, E, W in zip(dHs, Es, Ws)]
+        dEs = [None] * T
+        if any(ctx.needs_input_grad[:T]):
+            descs = []
+            for t in range(T):
+                dE = torch.empty_like(Es[t])
+                W = Ws[t]
+                descs.append(_rows_desc(dHs[t], W, 1, W.stride(0), W.shape[1], W.shape[0], dE))
+                dEs[t] = dE
+            _gemm_rows(descs, dev)
+        dWs = [None] * T
+        if any(ctx.needs_input_grad[T:]):
+            dWs = _gemm_tn_pair(list(zip(Es, dHs)), dev)
+        return (*dEs, *dWs)
+
+
+def table_projections(tables, weights):
+    """``[E @ W for E, W in zip(tables, weights)]`` (HCCF's E_u·W_u, E_i·W_i) as one grouped op
+    (:class:`_TableProjections`) for device fp32 operands whose feature sizes are multiples of 16
+    up to 128 (the row GEMM's K and N); ``torch.mm`` otherwise."""
+    ok = all(E.is_cuda and W.is_cuda and E.dtype == W.dtype == torch.float32 and E.dim() == 2
+             and W.dim() == 2 and E.shape[1] == W.shape[0] and E.shape[0] > 0
+             and all(x % 16 == 0 and 16 <= x <= 128 for x in W.shape)
+             for E, W in zip(tables, weights))
+    if not ok or len(tables) != len(weights) or not 1 <= len(tables) <= 4:
+        return [torch.mm(E, W) for E, W in zip(tables, weights)]
+    return list(_TableProjections.apply(*tables, *weights))
+
+
 class _HyperDropouts(torch.autograd.Function):
     """``nn.Dropout(p)`` applied to each of ``tables`` once per layer, in the reference's call
     order (HCCF.py:182-186: layer 0's user then item table, then layer 1's, …: the device

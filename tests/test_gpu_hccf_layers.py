@@ -151,6 +151,39 @@ def test_fused_hyper_dropouts_are_the_module_dropouts(dev, capture_safe, L):
         assert torch.equal(g0[k], g1[k]), (k, float((g0[k] - g1[k]).abs().max()))
 
 
+@pytest.mark.parametrize("d,K", [(64, 32), (32, 32), (128, 64)])
+def test_table_projections_match_float64(dev, d, K):
+    """functional.table_projections ([E_u·W_u, E_i·W_i] grouped, HCCF.py:178-179) against
+    float64: outputs and every gradient within 1e-5 of each row's scale (Σ|terms|), and two runs
+    bitwise equal."""
+    from hypergraph_diffusion_for_recommendation_amd.functional import table_projections
+    shapes = ((31_668, d), (38_048, d))
+    runs = []
+    for _ in range(2):
+        g = torch.Generator(device=dev).manual_seed(d + K)
+        Es = [torch.randn(s, device=dev, generator=torch.Generator(device=dev).manual_seed(s[0]))
+              .requires_grad_(True) for s in shapes]
+        Ws = [(0.1 * torch.randn(d, K, device=dev, generator=torch.Generator(device=dev)
+                                 .manual_seed(s[0] + 1))).requires_grad_(True) for s in shapes]
+        Hs = table_projections(Es, Ws)
+        dHs = [torch.randn(H.shape, device=dev, generator=g) for H in Hs]
+        torch.autograd.backward(Hs, dHs)
+        runs.append((Es, Ws, Hs, dHs))
+    (E0, W0, H0, _), (E1, W1, H1, dH1) = runs
+    for a, b in zip(H0 + [e.grad for e in E0] + [w.grad for w in W0],
+                    H1 + [e.grad for e in E1] + [w.grad for w in W1]):
+        assert torch.equal(a, b)
+    for E, W, H, dH in zip(E1, W1, H1, dH1):
+        E64, W64, dH64 = E.detach().double(), W.detach().double(), dH.double()
+        checks = ((H, E64 @ W64, E64.abs() @ W64.abs()),
+                  (E.grad, dH64 @ W64.t(), dH64.abs() @ W64.abs().t()),
+                  (W.grad, E64.t() @ dH64, E64.abs().t() @ dH64.abs()))
+        for got, ref, mag in checks:
+            err = (got.double() - ref).abs()
+            assert bool((err <= 1e-5 * mag.max(1, keepdim=True).values + 1e-30).all()), \
+                float((err / (mag + 1e-30)).max())
+
+
 def test_fused_layers_eval_and_no_grad(dev):
     """keep_rate 1 (the eval forward, HCCF.py:103) under no_grad: same tables as the loop."""
     U, I, d = 700, 900, 32
