@@ -357,7 +357,7 @@ class SpAdjDropEdge(nn.Module):
         self._slots = []       # [(nnz, keep, device uint8 buffer)] per call of a step
         self._slot_i = 0
         self._prefilled = False
-        self._step_job = None  # (start state, spec, future) of the next step's masks
+        self._step_job = None  # (start state, spec, future, bank) of the next step's masks
         self._stage = None     # device staging of the next step's masks (refill)
         self._banks = []       # host_fed(banks=2): [(slots, flat buffer)] the refills alternate
         self._refills = 0      # refills so far (a step's bank is refills % len(banks))
