@@ -25,7 +25,7 @@ import torch
 import torch.nn as nn
 
 from .functional import (dense_two_hop_pair, fan, hccf_layers, hccf_layers_supported,
-                         hyper_dropouts, linear, split_rows, sum_n, table_projections,
+                         hyper_dropouts, split_rows, sum_n, table_projections,
                          two_hop_fused)
 from .incidence import Incidence, incidence_of
 from .layers import EquivSetGNN, GCNLayer, HGCNConv, HGNNLayer, LayerNorm, SpAdjDropEdge
@@ -236,8 +236,8 @@ class HCCFDiffusionEncoder(HCCFEncoder):
         e = self.embedding_dict
         hidden = [torch.cat([e['user_emb'], e['item_emb']], 0)]
         gcn_hidden, hgnn_hidden = [], []
-        hyper_uu = linear(e['user_emb'], e['user_w'].t())
-        hyper_ii = linear(e['item_emb'], e['item_w'].t())
+        hyper_uu, hyper_ii = table_projections([e['user_emb'], e['item_emb']],
+                                               [e['user_w'], e['item_w']])
         blk = self.edhnnlayer
         terms = []  # the sum(hidden) operands
         for _ in range(self.n_layers):
