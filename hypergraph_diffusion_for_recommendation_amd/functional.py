@@ -811,7 +811,16 @@ class _ContrastLossLayers(torch.autograd.Function):
         g = g.to(dtype=torch.float32).reshape(1).contiguous()
         f = dict(dtype=torch.float32, device=dev)
         need = ctx.needs_input_grad[6:]
-        grads = [torch.zeros((N, d), **f) if need[j] else None for j in range(2 * L)]
+        # the needed gradients as slices of ONE zeroed block (one fill launch, not one per layer)
+        n_need = sum(1 for j in range(2 * L) if need[j])
+        block = torch.zeros((max(n_need, 1), N, d), **f) if n_need else None
+        grads, taken = [], 0
+        for j in range(2 * L):
+            if need[j]:
+                grads.append(block[taken])
+                taken += 1
+            else:
+                grads.append(None)
         none = (None,) * 6
         if all(x is None for x in grads):
             return none + tuple(grads)
