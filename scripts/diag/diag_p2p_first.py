@@ -1,0 +1,126 @@
+"""Is the FIRST peer exchange after its set-up ever wrong? (round 5: one N = 8 rehearsal of
+bench.py on one device saw the transport probe's first p2p step differ from RCCL by max |Y| on
+every rank; reruns, and diag_p2p_stress.py's 720 exchanges per rank on a standing exchange, did
+not.)
+
+Replays bench.py's probe sequence ``--cycles`` times on the headline graph sharded over N ranks
+(gloo stands in for RCCL, as in the rehearsal): one step over the all-reduce (the reference
+result), three more, a barrier, then ONE step over a freshly created peer exchange compared with
+the reference, and the exchange closed so the next cycle creates a new one. Prints one JSON line
+per cycle from rank 0 (max over ranks of the relative difference, and which ranks failed) and a
+summary.
+
+    python scripts/diag/diag_p2p_first.py --world 8 --cycles 12
+"""
+import argparse
+import json
+import os
+import socket
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+
+
+def worker(rank, world, port, args):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    from hypergraph_diffusion_for_recommendation_amd.sharded import (ShardedIncidence,
+                                                                       sharded_two_hop)
+    U, I, E, d = args.users, args.items, args.edges, args.dim
+    for turn in range(world):  # one graph build at a time on the shared device
+        if turn == rank:
+            idx = bench.make_graph(U, I, E, seed=0, zipf=None, device=dev)
+            torch.cuda.synchronize()
+        dist.barrier()
+    sh, u0, u1 = ShardedIncidence.from_global(idx, U, I, device=dev, n_chunks=4, P="sym",
+                                              Q="mean", R="sym", slice_width=None,
+                                              transport="rccl")
+    del idx
+    X = bench.table_rows(u0, u1, d, 1000, dev, (6.0 / (U + d)) ** 0.5)
+    dY = bench.table_rows(u0, u1, d, 1001, dev)
+    X.requires_grad_(True)
+
+    def step():
+        Y = sharded_two_hop(sh, X)
+        (dX,) = torch.autograd.grad(Y, X, dY)
+        return Y.detach(), dX
+
+    for _ in range(3):  # the bench's warm-up
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    bad = 0
+    t0 = time.perf_counter()
+    for c in range(args.cycles):
+        sh.transport = "rccl"
+        Y_r, dX_r = step()
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize()
+        dist.barrier()
+        err = None
+        rel = float("nan")
+        try:
+            sh.transport = "p2p"
+            Y_p, dX_p = step()
+            sh._p2p.wait()
+            sh._p2p.check()
+            rel = max(float((Y_p - Y_r).abs().max() / Y_r.abs().max().clamp_min(1e-30)),
+                      float((dX_p - dX_r).abs().max() / dX_r.abs().max().clamp_min(1e-30)))
+            # where a wrong Y sits: the fraction of rows off, and of them the share that is 0
+            off = (Y_p - Y_r).abs().amax(1) > 1e-5 * Y_r.abs().max()
+            frac_off = float(off.float().mean())
+            zero_rows = float((Y_p[off].abs().amax(1) == 0).float().mean()) if bool(off.any()) \
+                else 0.0
+        except Exception as e:  # noqa: BLE001 — reported
+            err = repr(e)[:300]
+            frac_off = zero_rows = float("nan")
+        res = torch.tensor([rel if rel == rel else 1e30, frac_off if frac_off == frac_off else 1.0,
+                            zero_rows if zero_rows == zero_rows else 0.0,
+                            1.0 if (err is not None or not rel <= 1e-5) else 0.0],
+                           dtype=torch.float64)
+        allres = [torch.zeros_like(res) for _ in range(world)]
+        dist.all_gather(allres, res)
+        failed = [q for q in range(world) if allres[q][3] > 0]
+        bad += bool(failed)
+        if rank == 0:
+            print(json.dumps({"cycle": c, "max_rel_diff": max(float(r[0]) for r in allres),
+                              "failed_ranks": failed,
+                              "frac_rows_off": [round(float(r[1]), 6) for r in allres],
+                              "zero_share_of_off_rows": [round(float(r[2]), 4) for r in allres],
+                              "error_rank0": err}), flush=True)
+        sh.close()  # collective; the next cycle's first p2p step creates a new exchange
+        torch.cuda.synchronize()
+        dist.barrier()
+    if rank == 0:
+        print(json.dumps({"summary": True, "world": world, "cycles": args.cycles,
+                          "cycles_with_a_wrong_first_exchange": bad,
+                          "seconds": round(time.perf_counter() - t0, 1)}), flush=True)
+    dist.destroy_process_group()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--cycles", type=int, default=12)
+    ap.add_argument("--users", type=int, default=10_000_000)
+    ap.add_argument("--items", type=int, default=1_000_000)
+    ap.add_argument("--edges", type=int, default=100_000_000)
+    ap.add_argument("--dim", type=int, default=64)
+    args = ap.parse_args()
+    import torch.multiprocessing as mp
+    with socket.socket() as sck:
+        sck.bind(("127.0.0.1", 0))
+        port = sck.getsockname()[1]
+    mp.spawn(worker, args=(args.world, port, args), nprocs=args.world, join=True)
+
+
+if __name__ == "__main__":
+    main()
