@@ -305,17 +305,19 @@ def choose_transport(sh, eager_step, device, phase, n=3):
     import torch.distributed as dist
 
     def timed():
-        """n steps between a barrier pair, max over ranks: (ms per step, error or None). A
-        failure on this rank alone (a poll that sees the error flag, a timed-out wait) is
-        recorded, never raised: every rank still reaches the same barrier and all-reduce, so
-        the collectives stay paired and agree() below decides on all ranks at once."""
+        """n steps between a barrier pair, max over ranks: (ms per step, error or None, the last
+        step's (Y, dX)). A failure on this rank alone (a poll that sees the error flag, a
+        timed-out wait) is recorded, never raised: every rank still reaches the same barrier and
+        all-reduce, so the collectives stay paired and agree() below decides on all ranks at
+        once."""
         err = None
+        last = None
         torch.cuda.synchronize()
         dist.barrier()
         t0 = time.perf_counter()
         try:
             for _ in range(n):
-                eager_step()
+                last = eager_step()
             if sh.transport == "p2p":
                 sh._p2p.wait()
                 sh._p2p.check()
@@ -329,7 +331,7 @@ def choose_transport(sh, eager_step, device, phase, n=3):
         t = torch.tensor([(time.perf_counter() - t0) / n * 1e3], dtype=torch.float64,
                          device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item()), err
+        return float(t.item()), err, last
 
     out = {"steps_each": n}
 
@@ -340,13 +342,23 @@ def choose_transport(sh, eager_step, device, phase, n=3):
             out[key] = err
         return int(flag.item()) == 0
 
+    def rel_diff(a, b):
+        return max(float((a[0].detach() - b[0]).abs().max() / b[0].abs().max().clamp_min(1e-30)),
+                   float((a[1] - b[1]).abs().max() / b[1].abs().max().clamp_min(1e-30)))
+
     sh.transport = "rccl"
-    Y_r, dX_r = eager_step()
-    Y_r, dX_r = Y_r.detach(), dX_r.detach()
-    ms, rccl_err = timed()
+    first = eager_step()
+    ms, rccl_err, last = timed()
     if not agree(rccl_err, "rccl_error"):  # the all-reduce path itself failed: no fallback
         raise RuntimeError(f"RCCL steps failed on some rank: {out.get('rccl_error')}")
     out["rccl_ms_per_step"] = round(ms, 4)
+    # The reference for the peer exchange is the LAST all-reduce step, not the first: in the
+    # one-device gloo rehearsal the first gloo step after the warm-up's barrier came out wrong
+    # in about a third of the cases while the back-to-back steps after it agreed bitwise
+    # (scripts/diag/diag_p2p_first.py, profiles/r05_scale/p2p_first/). Both are reported.
+    Y_r, dX_r = last[0].detach(), last[1].detach()
+    out["rccl_first_vs_last_rel_diff"] = rel_diff(first, (Y_r, dX_r))
+    del first, last
 
     err = None
     try:  # one step, checked against RCCL's, before any collective timing
@@ -354,8 +366,7 @@ def choose_transport(sh, eager_step, device, phase, n=3):
         Y_p, dX_p = eager_step()
         sh._p2p.wait()
         sh._p2p.check()
-        rel = max(float((Y_p.detach() - Y_r).abs().max() / Y_r.abs().max().clamp_min(1e-30)),
-                  float((dX_p - dX_r).abs().max() / dX_r.abs().max().clamp_min(1e-30)))
+        rel = rel_diff((Y_p, dX_p), (Y_r, dX_r))
         out["p2p_vs_rccl_max_rel_diff"] = rel
         if not rel <= 1e-5:
             raise RuntimeError(f"peer exchange differs from RCCL by {rel:.3e} of max |Y|")
@@ -363,7 +374,7 @@ def choose_transport(sh, eager_step, device, phase, n=3):
         err = repr(e)[:400]
     ok = agree(err)
     if ok:
-        ms, err = timed()
+        ms, err, _ = timed()
         ok = agree(err)
         if ok:
             out["p2p_ms_per_step"] = round(ms, 4)

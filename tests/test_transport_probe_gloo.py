@@ -52,6 +52,7 @@ def _worker(rank, world, port, case, q):
         Y = torch.linspace(-1.0, 1.0, 64).reshape(8, 8)
 
         p2p_steps = [0]
+        rccl_steps = [0]
 
         def eager_step():
             if sh.transport == "p2p":
@@ -66,9 +67,16 @@ def _worker(rank, world, port, case, q):
                 y = Y * (1.0 + 1e-3) if case == "mismatch" and rank == 0 else Y
                 return y, Y.clone()
             time.sleep(0.01)
+            rccl_steps[0] += 1
+            if case == "first_rccl_off" and rccl_steps[0] == 1:
+                # the one-device gloo rehearsal's flake: the first all-reduce step after the
+                # warm-up barrier is off; the reference is the last timed all-reduce step
+                return Y * 1.5, Y.clone()
             return Y.clone(), Y.clone()
 
         out = bench.choose_transport(sh, eager_step, torch.device("cpu"), lambda m: None, n=2)
+        if case == "first_rccl_off":
+            assert out["rccl_first_vs_last_rel_diff"] > 0.4, out
         q.put((rank, out["chosen"], out.get("p2p_failed_on_some_rank", False),
                "p2p_error" in out, sh.transport))
     finally:
@@ -78,7 +86,8 @@ def _worker(rank, world, port, case, q):
 @pytest.mark.parametrize("case,chosen,failed", [("ok", "p2p", False), ("slower", "rccl", False),
                                                 ("raise", "rccl", True), ("check", "rccl", True),
                                                 ("mismatch", "rccl", True),
-                                                ("raise_timed", "rccl", True)])
+                                                ("raise_timed", "rccl", True),
+                                                ("first_rccl_off", "p2p", False)])
 def test_auto_transport_decision_is_agreed(case, chosen, failed):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
