@@ -10,6 +10,11 @@ the reference, and the exchange closed so the next cycle creates a new one. Prin
 per cycle from rank 0 (max over ranks of the relative difference, and which ranks failed) and a
 summary.
 
+Finding (profiles/r05_scale/p2p_first/): the peer step was right every time — bitwise equal to
+the last all-reduce step, its send slots equal to the hop recomputed, a second exchange of them
+equal to gloo's sum — and the FIRST gloo step after the barrier was the one that was off, in
+about a third of the cycles. bench.py's probe now takes its reference from the last step.
+
     python scripts/diag/diag_p2p_first.py --world 8 --cycles 12
 """
 import argparse
