@@ -14,6 +14,8 @@
 //   * rows longer than the split plan's threshold are cut into fixed-size chunks handled by extra
 //     blocks placed FIRST in the grid (they are the longest work items); a fix-up kernel sums the
 //     chunk partials in chunk order — no float atomics anywhere.
+#include <cmath>
+
 #include "device_util.h"
 #include "hgd_internal.h"
 
@@ -50,8 +52,17 @@ struct SpmmArgs {
   // val[e] / keep (IEEE, as the dropped COO's values)
   const uint8_t* mask;
   float keep;
+  // 1 / keep when keep is a power of two (HCCF's 0.5), else 0: then w·inv_keep is w / keep bit
+  // for bit (one exact real value, rounded once either way) at one multiply instead of the
+  // IEEE division's ~10-instruction sequence per kept entry
+  float inv_keep;
   int32_t mask_pair;  // two-batch masked walk (HGD_TUNE_MASK_PAIR)
 };
+
+// vals[mask] / keepRate (HCCF.py:224)
+__device__ __forceinline__ float scale_kept(const SpmmArgs& a, float w) {
+  return a.inv_keep != 0.f ? w * a.inv_keep : __fdiv_rn(w, a.keep);
+}
 
 __device__ __forceinline__ float epilogue(float y, int epi, float slope) {
   if (epi == HGD_EPI_LEAKY_RELU) return y > 0.f ? y : y * slope;
@@ -175,7 +186,7 @@ __device__ __forceinline__ int compact_kept(const SpmmArgs& a, int l, int keep, 
   const unsigned long long gm =
       G == 64 ? bal : (bal >> base) & ((1ull << (G == 64 ? 0 : G)) - 1ull);
   const int src = nth_set_bit<G>(gm, l);
-  if constexpr (HAS_VAL) w = __fdiv_rn(w, a.keep);  // vals[mask] / keepRate (HCCF.py:224)
+  if constexpr (HAS_VAL) w = scale_kept(a, w);
   c = __shfl(c, src, G);
   if constexpr (HAS_VAL) w = __shfl(w, src, G);
   return __popcll(gm);
@@ -244,7 +255,7 @@ __device__ __forceinline__ void gather_sum_mask2(const SpmmArgs& a, int64_t e0, 
       cb = x2;
       if constexpr (HAS_VAL) {
         // vals[mask] / keepRate (HCCF.py:224), divided before the move (same IEEE quotient)
-        const float v1 = __fdiv_rn(w1, a.keep), v2 = __fdiv_rn(w2, a.keep);
+        const float v1 = scale_kept(a, w1), v2 = scale_kept(a, w2);
         const float y1 = __int_as_float(__builtin_amdgcn_ds_permute(a1, __float_as_int(v1)));
         const float y2 = __int_as_float(__builtin_amdgcn_ds_permute(a2, __float_as_int(v2)));
         wa = l < n1 ? y1 : y2;
@@ -259,8 +270,8 @@ __device__ __forceinline__ void gather_sum_mask2(const SpmmArgs& a, int64_t e0, 
       ca = l < n1 ? ca1 : ca2;
       if constexpr (HAS_VAL) {
         const float wa1 = __shfl(w1, s1, G), wa2 = __shfl(w2, s2a, G);
-        wa = __fdiv_rn(l < n1 ? wa1 : wa2, a.keep);  // vals[mask] / keepRate (HCCF.py:224)
-        wb = __fdiv_rn(__shfl(w2, s2b, G), a.keep);
+        wa = scale_kept(a, l < n1 ? wa1 : wa2);
+        wb = scale_kept(a, __shfl(w2, s2b, G));
       }
     }
     for (int k = 0; k < n; k += U) {
@@ -363,6 +374,7 @@ __device__ __forceinline__ void gather_sum(const SpmmArgs& a, int64_t e0, int64_
 }
 
 int g_mask_pair = 2;  // HGD_TUNE_MASK_PAIR: the masked hop walks two index batches per step
+int g_mask_div = 0;   // HGD_TUNE_MASK_DIV: 1 = divide by keep even when it is a power of two
 
 // MASK with G >= 8 lanes (U | G): the two-batch masked walk unless HGD_TUNE_MASK_PAIR is 0.
 template <int G, int VEC, int U, bool HAS_VAL, int POL, bool MASK>
@@ -739,6 +751,10 @@ hgd_status spmm_impl(const int64_t* rowptr, const int32_t* col, const float* val
   if (ex) a.ex = *ex;
   a.mask = mask;
   a.keep = keep;
+  {
+    int e2 = 0;
+    a.inv_keep = (!g_mask_div && keep > 0.f && std::frexp(keep, &e2) == 0.5f) ? 1.f / keep : 0.f;
+  }
   a.mask_pair = g_mask_pair;
   if (plan && plan->threshold > 0 && plan->n_heavy > 0) {
     HGD_REQUIRE(plan->chunk > 0 && plan->heavy_rows && plan->heavy_cptr && plan->chunk_heavy,
@@ -925,6 +941,10 @@ extern "C" hgd_status hgd_set_tuning(int32_t key, int32_t value) {
     case HGD_TUNE_MASK_PAIR:
       HGD_REQUIRE(value >= 0 && value <= 2, "hgd_set_tuning: mask pair must be 0, 1 or 2");
       g_mask_pair = value;
+      return HGD_OK;
+    case HGD_TUNE_MASK_DIV:
+      HGD_REQUIRE(value == 0 || value == 1, "hgd_set_tuning: mask div must be 0 or 1");
+      g_mask_div = value;
       return HGD_OK;
     case HGD_TUNE_CPU_RNG_THREADS:
       HGD_REQUIRE(value >= 0 && value <= 64, "hgd_set_tuning: cpu rng threads must be 0..64");

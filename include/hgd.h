@@ -105,7 +105,10 @@ typedef enum hgd_epilogue {
  *   HGD_TUNE_MASK_PAIR:   the masked hop (hgd_spmm_masked*) walks two index batches per step,
  *                         their kept entries packed by forward permutes (2, default) or by
  *                         set-bit searches and pulls (1), or one batch per step (0); the sums
- *                         are the same bits every way */
+ *                         are the same bits every way
+ *   HGD_TUNE_MASK_DIV:    the masked hop's kept weights val / keep: 0 (default) = one multiply by
+ *                         1 / keep when keep is a power of two (the same bits: one real value,
+ *                         rounded once), else the IEEE division; 1 = always the division */
 typedef enum hgd_tune_key {
   HGD_TUNE_SPMM_UNROLL = 1,
   HGD_TUNE_SPMM_POLICY = 2,
@@ -121,7 +124,8 @@ typedef enum hgd_tune_key {
   HGD_TUNE_CPU_RNG_THREADS = 12,
   HGD_TUNE_X3P_QUEUE = 13,
   HGD_TUNE_P2P_GRID = 14,
-  HGD_TUNE_MASK_PAIR = 15
+  HGD_TUNE_MASK_PAIR = 15,
+  HGD_TUNE_MASK_DIV = 16
 } hgd_tune_key;
 hgd_status hgd_set_tuning(int32_t key, int32_t value);
 

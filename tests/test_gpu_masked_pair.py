@@ -53,3 +53,37 @@ def test_masked_pair_walk_bitwise(dev, d, keep, heavy):
         child = inc.drop(mask, keep)
         assert torch.equal(outs[2][0], spmm_csr(child.csr, X, child.val))
         assert torch.equal(outs[2][1], spmm_csr(child.csc, Xt, child.val_t))
+
+
+@pytest.mark.parametrize("keep", [0.5, 0.25, 0.125, 0.3])
+@pytest.mark.parametrize("pair", [2, 1, 0])
+def test_masked_keep_reciprocal_is_the_division(dev, keep, pair):
+    """HGD_TUNE_MASK_DIV: with keep a power of two the kept weight is val · (1 / keep), one
+    multiply, instead of the IEEE val / keep — the same bits (one real value, rounded once), here
+    over values from subnormal to near the float32 top; 0.3 takes the division either way."""
+    from hypergraph_diffusion_for_recommendation_amd import _native as nat
+    from hypergraph_diffusion_for_recommendation_amd.incidence import Incidence, spmm_csr
+    lib = nat.load()
+    rng = np.random.default_rng(7)
+    n_rows, n_cols, nnz = 2000, 1500, 60_000
+    key = np.unique(rng.integers(0, n_rows, nnz) * n_cols + rng.integers(0, n_cols, nnz))
+    r, c = key // n_cols, key % n_cols
+    v = (rng.random(len(r)) * 2.0 ** rng.integers(-140, 100, len(r))).astype(np.float32)
+    inc = Incidence.from_coo(torch.from_numpy(np.stack([r, c])), torch.from_numpy(v),
+                             (n_rows, n_cols), device=dev)
+    g = torch.Generator(device=dev).manual_seed(11)
+    mask = (torch.rand(inc.nnz, device=dev, generator=g) < keep).to(torch.uint8)
+    X = torch.randn(n_cols, 64, device=dev, generator=g) * 1e-20
+    view = inc.masked(mask, keep)
+    outs = {}
+    try:
+        nat.check(lib.hgd_set_tuning(15, pair), "hgd_set_tuning")
+        for div in (0, 1):
+            nat.check(lib.hgd_set_tuning(16, div), "hgd_set_tuning")
+            outs[div] = spmm_csr(view.csr, X, view.val)
+    finally:
+        nat.check(lib.hgd_set_tuning(16, 0), "hgd_set_tuning")
+        nat.check(lib.hgd_set_tuning(15, 2), "hgd_set_tuning")
+    assert torch.equal(outs[0], outs[1])
+    child = inc.drop(mask, keep)  # the dropped COO's values divided on their own
+    assert torch.equal(outs[0], spmm_csr(child.csr, X, child.val))
