@@ -40,6 +40,16 @@ def worker(rank, world, port, args):
     from hypergraph_diffusion_for_recommendation_amd.sharded import (ShardedIncidence,
                                                                        sharded_two_hop)
     U, I, E, d = args.users, args.items, args.edges, args.dim
+    if args.sync_before_allreduce:
+        # every all-reduce issued only once the current stream has drained: the producing hop is
+        # complete before gloo records its event and stages the tensor to the host
+        plain = dist.all_reduce
+
+        def synced(t, *a, **k):
+            if t.is_cuda:
+                torch.cuda.current_stream(t.device).synchronize()
+            return plain(t, *a, **k)
+        dist.all_reduce = synced
     for turn in range(world):  # one graph build at a time on the shared device
         if turn == rank:
             idx = bench.make_graph(U, I, E, seed=0, zipf=None, device=dev)
@@ -184,6 +194,8 @@ def main():
     ap.add_argument("--items", type=int, default=1_000_000)
     ap.add_argument("--edges", type=int, default=100_000_000)
     ap.add_argument("--dim", type=int, default=64)
+    ap.add_argument("--sync-before-allreduce", action="store_true",
+                    help="drain the current stream before every all-reduce call")
     ap.add_argument("--warm", type=int, default=0,
                     help="with --precreate: rounds of known-pattern exchanges through every slot")
     ap.add_argument("--precreate", default="none", choices=["none", "odd", "all"],
