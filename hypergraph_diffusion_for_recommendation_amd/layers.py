@@ -297,15 +297,19 @@ class _MaskStager:
             masks.append(host[off:off + n])
             off += n
         torch.cuda.set_device(self.device)
+        # the destination's last reader is waited for on this (worker) thread before the copy is
+        # issued, not only by the side stream: on this stack gloo's staging copies, queued behind
+        # a stream wait on a still-pending event, did not reliably see their producer's output
+        # (the one-device rehearsals); here that order keeps a copy from overwriting
+        # masks a queued replay still reads. The wait is for the step before last, so the copy
+        # still runs under the next replay.
+        free = target_free if target is not None else self.free[k]
+        if free is not None:
+            free.synchronize()
         with torch.cuda.stream(self.side):
-            if target is not None:
-                if target_free is not None:
-                    self.side.wait_event(target_free)
-                target.copy_(host, non_blocking=True)
-            else:
-                if self.free[k] is not None:
-                    self.side.wait_event(self.free[k])
-                self.bufs[k].copy_(host, non_blocking=True)
+            if free is not None:
+                self.side.wait_event(free)
+            (target if target is not None else self.bufs[k]).copy_(host, non_blocking=True)
             done = torch.cuda.Event()
             done.record(self.side)
         self.copied[k] = done
