@@ -26,7 +26,9 @@ oracle/ref_cpu.py) run once on the FULL graph and tables of the GPU run (copied 
 ``parity`` compares one more GPU step with them row by row (the 1e-5 row bound; the script exits
 non-zero if it fails), and ``cpu_baseline`` times the same calls on a bounded prefix sample of
 the graph (median of 5 after 2 warm-ups) on this box's host cores. At N > 1 ``check`` compares
-every rank's rows with the single-GPU conv of the global graph (on by default).
+every rank's rows with the single-GPU conv of the global graph (on by default). Both gates also
+hold the FIRST timed step — the one straight after the pre-timing barrier, its outputs kept — to
+the same rule (``parity.first_step`` / ``check.first_step``); either failing fails the run.
 """
 from __future__ import annotations
 
@@ -152,33 +154,79 @@ def row_parity(got, ref, block=1 << 20):
     return worst, where, over, zero_bad
 
 
-def parity_gate(Y, dX, Y_ref, dX_ref, cpu_s):
+def parity_gate(Y, dX, Y_ref, dX_ref, cpu_s, first=None):
     """The GPU step's (Y, dX) — one eager step after timing, the same code the timed steps ran —
-    against the reference's torch.sparse.mm (Y, dX) on the same full-size inputs."""
+    against the reference's torch.sparse.mm (Y, dX) on the same full-size inputs. ``first``: the
+    FIRST timed step's (Y, dX) (the step straight after the pre-timing barrier), held to the same
+    rule under ``first_step``; the gate fails if either fails."""
     out = {"ok": True, "bound": "per row: max|err| <= 1e-5 * max|ref| (tests/_ref64.check_rows)",
            "reference": "oracle/ref_cpu.py torch.sparse.mm fwd+bwd, full graph, same X/dY",
            "reference_s": round(cpu_s, 2)}
-    for name, got, ref in (("Y", Y, Y_ref), ("dX", dX, dX_ref)):
-        worst, row, over, zero_bad = row_parity(got, ref)
-        out[f"max_row_ratio_{name}"] = worst
-        out[f"rows_over_{name}"] = over + zero_bad
-        if over or zero_bad or got.shape != ref.shape:
-            out["ok"] = False
-            out[f"worst_row_{name}"] = row
+
+    def rule(dst, got_Y, got_dX):
+        for name, got, ref in (("Y", got_Y, Y_ref), ("dX", got_dX, dX_ref)):
+            worst, row, over, zero_bad = row_parity(got, ref)
+            dst[f"max_row_ratio_{name}"] = worst
+            dst[f"rows_over_{name}"] = over + zero_bad
+            if over or zero_bad or got.shape != ref.shape:
+                dst["ok"] = False
+                dst[f"worst_row_{name}"] = row
+
+    rule(out, Y, dX)
+    if first is not None:
+        fs = {"ok": True, "what": "the first timed step (straight after the pre-timing barrier)"}
+        rule(fs, *first)
+        out["first_step"] = fs
+        out["ok"] = out["ok"] and fs["ok"]
     out["rows"] = int(Y_ref.shape[0])
     return out
 
 
-def cpu_baseline(idx, X, dY, U, I, d, label, full_s, frac=0.1):
+def host_cpus():
+    """The host the CPU baseline runs on: os.cpu_count() (the whole machine), this process's
+    affinity set, the cgroup CPU quota (cpu.max / cfs_quota_us, None when unlimited) and
+    OMP_NUM_THREADS. ``threads`` = the affinity count, capped by the quota — on
+    the GPU box the affinity set spans the whole machine while the box's share is its quota."""
+    cpu_count = os.cpu_count()
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = cpu_count
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, p = fh.read().split()[:2]
+            if q != "max":
+                quota = -(-int(q) // int(p))
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as fh:
+                q = int(fh.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as fh:
+                p = int(fh.read())
+            if q > 0:
+                quota = -(-q // p)
+        except (OSError, ValueError):
+            pass
+    threads = max(1, min(affinity, quota) if quota else affinity)
+    return {"os_cpu_count": cpu_count, "affinity": affinity, "cgroup_cpu_quota": quota,
+            "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS"), "threads": threads}
+
+
+def cpu_baseline(idx, X, dY, U, I, d, label, full_s, frac=0.1, host=None):
     """The CPU baseline's timing: the reference's calls
     (oracle/ref_cpu.py) on a BOUNDED sample of the same workload — the users [0, U·frac) of the
     GPU run's graph (a prefix of its row-sorted COO, every item kept) with their X / dY rows —
-    median of 5 runs after 2 warm-ups at torch's host threads, then one run at one thread. The
-    full-size run the parity gate made is reported beside it (``full_size``)."""
+    median of 5 runs after 2 warm-ups at the host's thread count (:func:`host_cpus`), then one
+    run at one thread. The sample is NOT the headline graph (its X table is a tenth as large);
+    the full-size run the parity gate made is reported beside it (``full_size``)."""
     import psutil
     import torch
 
     from oracle import ref_cpu
+    host = host or host_cpus()
+    prev_threads = torch.get_num_threads()
+    torch.set_num_threads(host["threads"])
     nnz_full = int(idx.shape[1])
     Us = max(1, int(U * frac))
     n = int(torch.searchsorted(idx[0].contiguous(), torch.tensor([Us])).item())
@@ -198,9 +246,15 @@ def cpu_baseline(idx, X, dY, U, I, d, label, full_s, frac=0.1):
         "unit": "M-edges/s",
         "cores": torch.get_num_threads(),
         "kind": "port",
-        "sample": (f"users [0, {Us}) of the headline graph ({label}): {Us}x{I}, {n} edges, d={d}, "
-                   f"the GPU run's X / dY rows; torch.sparse.mm fwd+bwd (oracle/ref_cpu.py), "
-                   f"median of 5 after 2 warm-ups, {t:.2f} s/run; host RAM {ram:.0f} GiB"),
+        "sample": (f"a {frac:g} prefix SAMPLE, not the headline graph (the full graph is "
+                   f"full_size): users [0, {Us}) of {label}: {Us}x{I}, {n} edges, d={d}, the GPU "
+                   f"run's X / dY rows; torch.sparse.mm fwd+bwd (oracle/ref_cpu.py), median of 5 "
+                   f"after 2 warm-ups, {t:.2f} s/run; host RAM {ram:.0f} GiB"),
+        "host": host,
+        "threads_note": ("threads = the affinity count capped by the cgroup CPU quota. 1 thread "
+                         "~ N threads: aten::addmm (sparse COO x dense, torch.sparse.mm's CPU "
+                         "kernel) walks the nonzeros in one serial loop and takes >90% of the "
+                         "time (profiles/r06_cpu/cpu_reference_profile.txt)"),
     }
     threads = torch.get_num_threads()
     torch.set_num_threads(1)
@@ -209,7 +263,7 @@ def cpu_baseline(idx, X, dY, U, I, d, label, full_s, frac=0.1):
         ref_cpu.hgconv2_fwd_bwd(H, Xs, dYs)
         t1 = time.perf_counter() - t0
     finally:
-        torch.set_num_threads(threads)
+        torch.set_num_threads(prev_threads)
     out["single_thread"] = {"value": round(n / t1 / 1e6, 3), "cores": 1,
                             "sample": f"the same sample, one run, {t1:.2f} s"}
     out["full_size"] = {"value": round(nnz_full / full_s / 1e6, 3), "cores": threads,
@@ -425,9 +479,20 @@ def table_rows(u0, u1, d, seed, device, bound=None):
     return out
 
 
-def check_against_single_gpu(idx, U, I, X_global, dY_global, Y, dX, u0, u1):
+def compare_elementwise(got, ref, mag):
+    """|got − ref| <= 1e-5 · mag per element (mag = the conv of |X|, so a near-cancelling element
+    is held to its terms' scale): {max_abs_err, max_rel_err, ok}."""
+    err = (got - ref).abs()
+    return {"max_abs_err": float(err.max()) if err.numel() else 0.0,
+            "max_rel_err": float((err / (mag + 1e-30)).max()) if err.numel() else 0.0,
+            "ok": bool((err <= 1e-5 * mag + 1e-30).all())}
+
+
+def check_against_single_gpu(idx, U, I, X_global, dY_global, Y, dX, u0, u1, first=None):
     """Strong scaling: this rank's sharded Y / dX rows against the single-GPU hgconv2 of the
-    global graph (functional.hgconv2, no exchange) at |err| <= 1e-5 · (the same conv of |X|)."""
+    global graph (functional.hgconv2, no exchange) at |err| <= 1e-5 · (the same conv of |X|).
+    ``(Y, dX)`` is one step after timing; ``first`` the FIRST timed step (straight after the
+    pre-timing barrier), checked against the same reference under ``first_step``."""
     import torch
 
     from hypergraph_diffusion_for_recommendation_amd import Incidence, hgconv2
@@ -438,14 +503,37 @@ def check_against_single_gpu(idx, U, I, X_global, dY_global, Y, dX, u0, u1):
     with torch.no_grad():
         mag = hgconv2(inc, X_global.abs())
         dmag = hgconv2(inc, dY_global.abs())  # the conv is self-adjoint: dX = conv(dY)
-        out = {}
-        for name, got, ref, m in (("Y", Y, Yg[u0:u1], mag[u0:u1]),
-                                  ("dX", dX, dXg[u0:u1], dmag[u0:u1])):
-            err = (got - ref).abs()
-            out[name] = {"max_abs_err": float(err.max()) if err.numel() else 0.0,
-                         "max_rel_err": float((err / (m + 1e-30)).max()) if err.numel() else 0.0,
-                         "ok": bool((err <= 1e-5 * m + 1e-30).all())}
+        return check_rows(Y, dX, Yg[u0:u1], dXg[u0:u1], mag[u0:u1], dmag[u0:u1], first)
+
+
+def check_rows(Y, dX, Y_ref, dX_ref, mag_Y, mag_dX, first=None):
+    """This rank's check record: the checked step's Y / dX and, when kept, the first timed
+    step's (``first_step``) against the same reference rows (:func:`compare_elementwise`)."""
+    out = {"Y": compare_elementwise(Y, Y_ref, mag_Y),
+           "dX": compare_elementwise(dX, dX_ref, mag_dX)}
+    if first is not None:
+        out["first_step"] = {"Y": compare_elementwise(first[0], Y_ref, mag_Y),
+                             "dX": compare_elementwise(first[1], dX_ref, mag_dX)}
     return out
+
+
+def line_status(check, parity) -> int:
+    """Exit status of the run: 1 if the N > 1 check (either step) or the N = 1 parity gate (either
+    step) failed, else 0."""
+    bad = (check is not None and not check["ok"]) or (parity is not None and not parity["ok"])
+    return 1 if bad else 0
+
+
+def corrupt_first_step(first, rank):
+    """Rehearsal hook: HGD_BENCH_CORRUPT_FIRST_STEP=<rank> adds max|Y| + 1 to element 0 of that
+    rank's kept first-step Y (after the timed region), so the first-step check must fail the
+    line on hardware where the exchange is right."""
+    if first is None or os.environ.get("HGD_BENCH_CORRUPT_FIRST_STEP") != str(rank):
+        return first
+    Y, dX = first
+    if Y.numel():
+        Y.view(-1)[0] += float(Y.abs().max()) + 1.0
+    return Y, dX
 
 
 def check_enabled(args, world) -> bool:
@@ -458,13 +546,28 @@ def gather_checks(check, world, shared_device):
     import torch.distributed as dist
     checks = [None] * world
     dist.all_gather_object(checks, check)
-    return {"ok": all(c["Y"]["ok"] and c["dX"]["ok"] for c in checks),
-            "max_rel_err_Y": max(c["Y"]["max_rel_err"] for c in checks),
-            "max_rel_err_dX": max(c["dX"]["max_rel_err"] for c in checks),
-            "bound": "|err| <= 1e-5 * conv(|x|), per element",
-            "ranks_checked": world,
-            "wall_s": max(c.get("wall_s", 0.0) for c in checks),
-            "ranks_in_parallel": not shared_device}
+    out = {"ok": all(c["Y"]["ok"] and c["dX"]["ok"] for c in checks),
+           "max_rel_err_Y": max(c["Y"]["max_rel_err"] for c in checks),
+           "max_rel_err_dX": max(c["dX"]["max_rel_err"] for c in checks),
+           "bound": "|err| <= 1e-5 * conv(|x|), per element",
+           "what": "one step after the timed steps",
+           "ranks_checked": world,
+           "wall_s": max(c.get("wall_s", 0.0) for c in checks),
+           "ranks_in_parallel": not shared_device}
+    firsts = [c.get("first_step") for c in checks]
+    if all(f is None for f in firsts):
+        out["first_step"] = None
+    else:
+        fs = [f for f in firsts if f is not None]
+        bad = [q for q, f in enumerate(firsts)
+               if f is None or not (f["Y"]["ok"] and f["dX"]["ok"])]
+        out["first_step"] = {"ok": not bad, "failed_ranks": bad,
+                             "max_rel_err_Y": max(f["Y"]["max_rel_err"] for f in fs),
+                             "max_rel_err_dX": max(f["dX"]["max_rel_err"] for f in fs),
+                             "what": "the first timed step, straight after the pre-timing "
+                                     "barrier, on every rank"}
+        out["ok"] = out["ok"] and not bad
+    return out
 
 
 def main():
@@ -603,12 +706,22 @@ def main():
             graph.replay()
             return static_out
 
+    # the first timed step's (Y, dX) are kept for the checks (an eager step's outputs; a graph
+    # replay overwrites its static outputs)
+    keep_first = (args.check or want_cpu) and not use_graph and not args.pmc_child
+    prev = None
     for k in range(args.warmup):
-        step()
+        # each warm-up step's outputs live until the next one's exist, so the allocator caches
+        # the blocks of two steps' outputs: holding the first timed step's costs no allocation
+        # inside the timed region
+        out_k = step()
+        prev = out_k if keep_first else None
+        del out_k
         phase(f"warm-up step {k} issued")
         if sh.transport == "p2p" and world > 1:
             sh._p2p.wait()  # bounded: a stalled exchange raises here instead of hanging
             sh._p2p.check()
+    del prev
     torch.cuda.synchronize()
     phase("warm")
     if world > 1:
@@ -619,16 +732,18 @@ def main():
         phase(f"transport: {probe}")
     def timed_and_checked():
         """The timed steps (barrier + sync both sides), then — with --check — one more step
-        compared with the single-GPU conv of the global graph. Returns (elapsed s, hop summary,
-        hop ms / step, exposed exchange ms / step, this rank's check or None, error or None);
-        a failure of the peer exchange on this rank is returned, never raised, so every rank
-        reaches the same collectives."""
+        compared with the single-GPU conv of the global graph, and the FIRST timed step (the
+        one straight after the barrier, kept) compared with it too. Returns (elapsed s, hop
+        summary, hop ms / step, exposed exchange ms / step, this rank's check or None, error or
+        None, the first step's (Y, dX) or None); a failure of the peer exchange on this rank is
+        returned, never raised, so every rank reaches the same collectives."""
         # roofline: HIP events around every hop launch on its stream, recorded inside the timed
         # region (two event records per hop, a few µs on a ~16 ms step); a captured graph cannot
         # record them, so with --graph on the same steps are re-run eagerly afterwards for them
         timer = profiling.HopTimer()
         xtimer = ExchangeTimer()
         failure = None
+        first = None
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -639,8 +754,11 @@ def main():
                     step()
             else:
                 with timer, xtimer:
-                    for _ in range(args.steps):
-                        step()
+                    for k in range(args.steps):
+                        out_k = step()
+                        if k == 0 and keep_first:
+                            first = (out_k[0].detach(), out_k[1])
+                        del out_k
         except Exception as e:  # noqa: BLE001 — a bounded p2p wait; agreed on below
             if sh.transport != "p2p":
                 raise
@@ -665,6 +783,7 @@ def main():
                 sh._p2p.check()  # no exchange timed out
             except Exception as e:  # noqa: BLE001
                 failure = repr(e)[:400]
+        first = corrupt_first_step(first, rank)
         check = None
         if args.check and not args.pmc_child and failure is None:
             t_check = time.perf_counter()
@@ -680,7 +799,7 @@ def main():
                         X_global = table_rows(0, U, d, seed_x, device, bound)
                         dY_global = table_rows(0, U, d, seed_x + 1, device)
                         check = check_against_single_gpu(idx, U, I, X_global, dY_global, Y, dX,
-                                                         u0, u1)
+                                                         u0, u1, first=first)
                         del X_global, dY_global
                         torch.cuda.synchronize()
                         torch.cuda.empty_cache()
@@ -689,9 +808,9 @@ def main():
                         dist.barrier()
                 check["wall_s"] = round(time.perf_counter() - t_check, 2)
         return (elapsed, hop, hop["total_ms"] / args.steps, xtimer.total_ms() / args.steps,
-                check, failure)
+                check, failure, first)
 
-    elapsed, hop, hop_ms_step, exposed_ms_step, check, failure = timed_and_checked()
+    elapsed, hop, hop_ms_step, exposed_ms_step, check, failure, first = timed_and_checked()
     fallback = None
     if world > 1 and sh.transport == "p2p":
         # the peer exchange chose by the probe must also pass the timed run's own check on
@@ -712,7 +831,9 @@ def main():
             for k in range(args.warmup):
                 step()
             torch.cuda.synchronize()
-            elapsed, hop, hop_ms_step, exposed_ms_step, check, failure = timed_and_checked()
+            del first
+            (elapsed, hop, hop_ms_step, exposed_ms_step, check, failure,
+             first) = timed_and_checked()
             if failure is not None:
                 raise RuntimeError(f"RCCL timed steps failed: {failure}")
     if keep_global:
@@ -795,14 +916,21 @@ def main():
         # torch.sparse.mm fwd+bwd on the same full graph and tables, compared row by row
         Yg, dXg = eager_step()
         Yh, dXh = Yg.detach().cpu(), dXg.cpu()
+        first_h = None if first is None else (first[0].cpu(), first[1].cpu())
         Xh, dYh = X.detach().cpu(), dY.cpu()
-        del X, dY, Yg, dXg
+        del X, dY, Yg, dXg, first
         torch.cuda.empty_cache()
-        Y_ref, dX_ref, full_s = cpu_reference(idx_host, Xh, dYh, U, I)
-        parity = parity_gate(Yh, dXh, Y_ref, dX_ref, full_s)
-        del Yh, dXh, Y_ref, dX_ref
+        host = host_cpus()
+        threads0 = torch.get_num_threads()
+        torch.set_num_threads(host["threads"])
+        try:
+            Y_ref, dX_ref, full_s = cpu_reference(idx_host, Xh, dYh, U, I)
+        finally:
+            torch.set_num_threads(threads0)
+        parity = parity_gate(Yh, dXh, Y_ref, dX_ref, full_s, first=first_h)
+        del Yh, dXh, Y_ref, dX_ref, first_h
         cpu = cpu_baseline(idx_host, Xh, dYh, U, I, d, f"{args.workload}-{U}x{I}x{E}-d{d}",
-                           full_s, args.cpu_sample_frac)
+                           full_s, args.cpu_sample_frac, host=host)
         del idx_host, Xh, dYh
 
     if world == 1:
@@ -867,8 +995,10 @@ def main():
         dist.barrier()
         sh.close()
         dist.destroy_process_group()
-    bad = (check is not None and not check["ok"]) or (parity is not None and not parity["ok"])
-    finish(1 if bad else 0)
+    if check is not None and not check["ok"]:
+        print(f"bench.py: CHECK FAILED against the single-GPU conv of the global graph: {check}",
+              file=sys.stderr, flush=True)
+    finish(line_status(check, parity))
 
 
 def finish(rc: int):

@@ -571,6 +571,13 @@ def _DL_DELETER(address, _live=_LIVE_RECORDS):
         pass
 
 
+# torch may release a view's storage during interpreter teardown, after this module's globals
+# are gone: one extra reference keeps the thunk (and, through its default, the record table)
+# alive for the life of the process, so the deleter is never a freed callback. The callbacks it
+# runs only do bookkeeping (sharded._P2PHandle.view_gone): no HIP call inside torch's release.
+ctypes.pythonapi.Py_IncRef(ctypes.py_object(_DL_DELETER))
+
+
 def live_views() -> int:
     """float_view storages torch has not released yet (tests)."""
     return len(_LIVE_RECORDS)

@@ -90,6 +90,7 @@ class ReferenceAdam(torch.optim.Adam):
         self._row = 0          # the same, as the host counts it
         self._key = None       # (params, hyper-parameters, first step) the table was built for
         self._stage = None     # (pinned source of the last table copy, its event)
+        self._captured = False  # a HIP graph holds a launch(): the table must not move
 
     def _params(self):
         return [p for group in self.param_groups for p in group["params"] if p.grad is not None]
@@ -125,6 +126,10 @@ class ReferenceAdam(torch.optim.Adam):
         src = torch.tensor(rows, dtype=torch.float64).to(torch.float32).reshape(
             _TABLE_ROWS, len(params), 6).pin_memory()
         if self._table is None or self._table.shape[1] != len(params):
+            if self._captured:
+                raise RuntimeError("ReferenceAdam: the set of parameters with a gradient changed "
+                                   "after a HIP graph captured launch(); the graph would read a "
+                                   "freed scalar table")
             self._table = torch.empty((_TABLE_ROWS, len(params), 6), dtype=torch.float32,
                                       device=dev)
             self._row_dev = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -162,6 +167,11 @@ class ReferenceAdam(torch.optim.Adam):
         pointers of the parameters' current .grad and moments), reading and advancing the device
         row of the scalar table."""
         params = self._params()
+        if self._key is None or self._key[0] != tuple(id(p) for p in params):
+            raise RuntimeError("ReferenceAdam.launch: the parameters with a gradient are not the "
+                               "ones prepare() built the scalar table for")
+        if torch.cuda.is_current_stream_capturing():
+            self._captured = True
         arr = (nat.AdamTensor * len(params))()
         for k, p in enumerate(params):
             st = self.state[p]

@@ -634,7 +634,8 @@ class _ShardedPlugin:
             1, t.numel() + 1, device=t.device)).sum() for k, t in enumerate(idx))
         v = torch.stack([c, -c]).to(torch.int64)
         m = v.clone()
-        self._dist.all_reduce(m, op=self._dist.ReduceOp.MAX)
+        from .sharded import ordered_all_reduce
+        ordered_all_reduce(m, op=self._dist.ReduceOp.MAX)
         if not torch.equal(m, v):
             raise RuntimeError(f"{type(self).__name__}: ranks drew different batches (the "
                                "Python random state diverged); the sharded loss would be wrong")
@@ -662,7 +663,8 @@ class _ShardedPlugin:
     def _full_user_table(self, user_local: torch.Tensor) -> torch.Tensor:
         full = torch.zeros(self.data.n_users, user_local.shape[1], device=user_local.device)
         full[self.u0:self.u1] = user_local
-        self._dist.all_reduce(full)
+        from .sharded import ordered_all_reduce
+        ordered_all_reduce(full)
         return full
 
 
@@ -724,9 +726,10 @@ class HCCF_sharded(_ShardedPlugin, HCCF):
         self.model = ShardedHCCFEncoder(kwargs, self.data, self.u0, self.u1, device=self.device,
                                         device_rng=bool(kwargs.get('hgd_device_rng', False)),
                                         seed=self.seed)
+        from .sharded import ordered_broadcast
         with torch.no_grad():  # replicated parameters start equal on every rank
             for p in self.model.replicated_parameters():
-                dist.broadcast(p.data, 0)
+                ordered_broadcast(p.data, 0)
         self.optimizer = torch.optim.Adam(self.model.parameters(), lr=self.lRate)
         self.scheduler = ReduceLROnPlateau(self.optimizer, 'min', factor=self.lr_decay,
                                            patience=5)
@@ -849,9 +852,10 @@ class HGNN_HD4_sharded(_ShardedPlugin, HGNN_HD4):
         self.model = ShardedHGNNModel(self.data, kwargs, self.device, self.u0, self.u1,
                                       bool(kwargs.get('hgd_device_rng', False)),
                                       self.sharded_encoder())
+        from .sharded import ordered_broadcast
         with torch.no_grad():
             for p in self.model.replicated_parameters():
-                self._dist.broadcast(p.data, 0)
+                ordered_broadcast(p.data, 0)
         self.optimizer = torch.optim.Adam(self.model.parameters(), lr=self.lRate,
                                           weight_decay=self.weight_decay)
         self.scheduler = ReduceLROnPlateau(self.optimizer, 'min', factor=self.lr_decay,

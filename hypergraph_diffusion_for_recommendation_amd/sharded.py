@@ -25,6 +25,7 @@ The reference has no distributed code at all; this is new desi
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
 import threading
@@ -51,6 +52,32 @@ def init_process_group(device: torch.device, backend: str = "nccl", **kw) -> Non
         dist.init_process_group("nccl", device_id=device, pg_options=opts, **kw)
     else:
         dist.init_process_group(backend, **kw)
+
+
+def _host_staged(t: torch.Tensor, group) -> bool:
+    """True when ``group``'s backend reduces a device tensor through host memory (gloo)."""
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
+def ordered_all_reduce(t: torch.Tensor, group=None, op=dist.ReduceOp.SUM,
+                       async_op: bool = False):
+    """``dist.all_reduce`` of a tensor the current stream is still producing, ordered after that
+    work on every backend. RCCL ('nccl') enqueues on its own stream behind an event of the
+    current stream. gloo stages a device tensor to pinned host memory on a pool stream behind such
+    an event; in the one-device gloo rehearsals that copy sometimes read the tensor before the
+    kernel producing it had written it (profiles/r05_scale/p2p_first/), so for gloo
+    the current stream is drained on the host first. gloo's sum runs on the host anyway: the wait
+    costs it nothing it would not pay."""
+    if _host_staged(t, group):
+        torch.cuda.current_stream(t.device).synchronize()
+    return dist.all_reduce(t, op=op, group=group, async_op=async_op)
+
+
+def ordered_broadcast(t: torch.Tensor, src: int, group=None, async_op: bool = False):
+    """``dist.broadcast`` with :func:`ordered_all_reduce`'s ordering on gloo."""
+    if _host_staged(t, group):
+        torch.cuda.current_stream(t.device).synchronize()
+    return dist.broadcast(t, src, group=group, async_op=async_op)
 
 
 def shard_bounds(n_users: int, world: int, rank: int, degrees=None):
@@ -123,17 +150,27 @@ def p2p_setup_stuck() -> int:
     return _P2P_STUCK
 
 
+# Lifetime of the exported peer segments. A segment may be freed only when (1) no peer can still
+# be reading it — every rank has synchronised its device and passed the barrier of a COLLECTIVE
+# close() — and (2) no slot view's storage is alive in this process. The destruction itself
+# (hgd_p2p_destroy synchronises the device) never runs inside torch's storage release (a DLPack
+# deleter can fire inside a graph capture or at interpreter teardown): a handle that becomes due
+# there waits in _PENDING for the next safe point (P2PExchange set-up or close(),
+# release_pending_p2p(), exit). An exchange dropped or released WITHOUT the collective close()
+# goes to _ABANDONED and stays mapped — a peer's exchange kernel may still read it — until a
+# collective close() in this process covers it too, or the process ends.
+_PENDING: List["_P2PHandle"] = []
+_ABANDONED: List["_P2PHandle"] = []
+_PLOCK = threading.Lock()
+
+
 class _P2PHandle:
-    """Owns one ``hgd_p2p`` handle (its exported send / reduced slots). The handle is destroyed
-    once BOTH a release was requested (:meth:`P2PExchange.close` / ``release``, or the exchange
-    was garbage-collected) AND no slot view's storage is alive (nat.float_view's deleter reports
-    each one's release, whenever torch gets to it): a slot view held past close() keeps pointing
-    at live memory, and an exchange dropped without close() still frees its segments."""
+    """Owns one ``hgd_p2p`` handle (its exported send / reduced slots); see the rules above."""
 
     def __init__(self, lib, h):
         self.lib, self.h = lib, h
         self.live = 0
-        self.wanted = False
+        self.closed = False  # a collective close() covered it: no peer reads it any more
         self.lock = threading.Lock()
 
     def view_born(self):
@@ -141,25 +178,74 @@ class _P2PHandle:
             self.live += 1
 
     def view_gone(self):
+        """nat.float_view's deleter: bookkeeping only, never a HIP call."""
         with self.lock:
             self.live -= 1
-        self._maybe_destroy()
+            due = self.closed and self.live == 0 and self.h is not None
+        if due:
+            with _PLOCK:
+                _PENDING.append(self)
 
-    def release(self):
+    def close_collective(self):
+        """After a collective close's barrier: destroy now, or when the last view goes."""
         with self.lock:
-            self.wanted = True
-        self._maybe_destroy()
+            self.closed = True
+            due = self.live == 0
+        if due:
+            self.destroy()
 
-    def _maybe_destroy(self):
+    def abandon(self):
+        """Dropped or released without the collective close: keep it mapped for now."""
         with self.lock:
-            if not (self.wanted and self.live == 0 and self.h is not None):
+            if self.closed or self.h is None:
                 return
+        with _PLOCK:
+            _ABANDONED.append(self)
+
+    def destroy(self):
+        with self.lock:
             h, self.h = self.h, None
-        self.lib.hgd_p2p_destroy(h)  # synchronises the device, closes the peers' mappings
+        if h is not None:
+            self.lib.hgd_p2p_destroy(h)  # synchronises the device, closes the peers' mappings
 
     @property
     def alive(self) -> bool:
         return self.h is not None
+
+
+def release_pending_p2p() -> int:
+    """Destroys the peer-exchange handles whose last slot view went after their collective
+    close() (a safe point: not inside a graph capture). Returns how many were destroyed."""
+    with _PLOCK:
+        due = list(_PENDING)
+        _PENDING.clear()
+    for hd in due:
+        hd.destroy()
+    return len(due)
+
+
+def _close_abandoned():
+    """Inside a collective close(), after its barrier: every rank's device has drained, so the
+    segments of exchanges this process dropped earlier can go too."""
+    with _PLOCK:
+        dropped = list(_ABANDONED)
+        _ABANDONED.clear()
+    for hd in dropped:
+        hd.close_collective()
+
+
+def abandoned_p2p() -> int:
+    """Handles of exchanges dropped without close() that are still mapped (tests)."""
+    with _PLOCK:
+        return sum(1 for hd in _ABANDONED if hd.alive)
+
+
+@atexit.register
+def _p2p_at_exit():
+    try:
+        release_pending_p2p()
+    except Exception:  # noqa: BLE001 — the runtime may already be going down
+        pass
 
 
 class P2PExchange:
@@ -188,6 +274,7 @@ class P2PExchange:
         trace = trace or (lambda msg: None)
         self.h = None
         self._handle = None  # _P2PHandle: the handle's lifetime (slot views may outlive close)
+        release_pending_p2p()  # a safe point: handles whose last view went since
         self._views = {}
         # every step that can fail locally is followed by an agreement among the ranks, so a
         # failure on one rank raises on all of them (none is left waiting in a collective)
@@ -253,7 +340,7 @@ class P2PExchange:
         bad = [(q, e) for q, e in enumerate(errs) if e is not None]
         if bad:
             if self._handle is not None and not self._stuck:
-                self._handle.release()
+                self._handle.destroy()  # set-up failed on some rank: no exchange ever ran
             self._handle = None
             self.h = None
             raise nat.HGDNativeError("P2PExchange: " + "; ".join(f"rank {q}: {e}"
@@ -309,22 +396,31 @@ class P2PExchange:
             pause = min(2 * pause, 0.05)
 
     def close(self) -> None:
-        """Collective: every rank's peers stop reading before the buffers go. The exchange is
-        unusable afterwards; its memory is freed as soon as no slot view handed out is alive."""
+        """Collective: every rank synchronises its device and passes a barrier, so no peer reads
+        this exchange's segments (nor those of exchanges this process dropped earlier) any more.
+        The exchange is unusable afterwards; its memory is freed now, or — if a slot view handed
+        out is still alive — at the first safe point after the last one goes."""
         if self.h is None:
             return
         torch.cuda.synchronize(self.device)
         if self.world > 1:
             dist.barrier(group=self.group)
-        self.release()
-
-    def release(self) -> None:
-        """Non-collective close (no barrier): the exchange stops being usable, and the handle
-        goes once every slot view's storage is released. What a dropped exchange does."""
         self.h = None
         self._views.clear()
         if self._handle is not None and not self._stuck:
-            self._handle.release()
+            self._handle.close_collective()
+        self._handle = None
+        _close_abandoned()
+        release_pending_p2p()
+
+    def release(self) -> None:
+        """Non-collective close (no barrier): the exchange stops being usable, but its segments
+        stay mapped — a peer's exchange kernel may still be reading them — until a collective
+        close() in this process covers them, or the process ends. What a dropped exchange does."""
+        self.h = None
+        self._views.clear()
+        if self._handle is not None and not self._stuck:
+            self._handle.abandon()
         self._handle = None
 
     def __enter__(self):
@@ -446,7 +542,7 @@ class ShardedIncidence:
         if kind not in ("mean", "sym"):
             raise ValueError(f"sharded: unsupported item scale {kind!r}")
         deg = (self.inc.csc.rowptr[1:] - self.inc.csc.rowptr[:-1]).to(torch.float64)
-        dist.all_reduce(deg, group=self.group)
+        ordered_all_reduce(deg, group=self.group)
         return _scale_of_degrees(deg, kind)
 
     def p2p(self, d: int) -> P2PExchange:
@@ -477,8 +573,8 @@ class ShardedIncidence:
         return False
 
     def __del__(self):
-        # dropped without close(): free the peer segments without a collective (the exchange's
-        # own finalizer would too; releasing here does not wait for the GC to reach it)
+        # dropped without close(): the exchange is released without a collective, its segments
+        # kept mapped until a collective close() (P2PExchange.release)
         try:
             if getattr(self, "_p2p", None) is not None:
                 self._p2p.release()
@@ -528,7 +624,8 @@ class ShardedIncidence:
                     spmm_csr(inc.csc, Xs, val=val_t, row_scale=self.q, out=Ms, row_begin=a,
                              row_end=b)
                     if self.world > 1:
-                        works.append(dist.all_reduce(Ms[a:b], group=self.group, async_op=True))
+                        works.append(ordered_all_reduce(Ms[a:b], group=self.group,
+                                                        async_op=True))
             pieces.append((c0, c1, Ms, works))
         xt = _XTIMER if self.world > 1 else None
         for c0, c1, Ms, works in pieces:
@@ -583,13 +680,13 @@ class _AllReduceSum(torch.autograd.Function):
     def forward(ctx, x, group):
         ctx.group = group
         y = x.contiguous().clone()
-        dist.all_reduce(y, group=group)
+        ordered_all_reduce(y, group=group)
         return y
 
     @staticmethod
     def backward(ctx, g):
         g = g.contiguous().clone()
-        dist.all_reduce(g, group=ctx.group)
+        ordered_all_reduce(g, group=ctx.group)
         return g, None
 
 
@@ -606,7 +703,7 @@ def allreduce_replicated_grads(params, group=None) -> None:
         return
     for p in params:
         if p.grad is not None:
-            dist.all_reduce(p.grad, group=group)
+            ordered_all_reduce(p.grad, group=group)
 
 
 def block_coo(indices: torch.Tensor, values: Optional[torch.Tensor], n_users: int, u0: int,
@@ -747,7 +844,7 @@ class ShardedBipartite:
         o = self.B.csr if side == "user" else self.C.csr
         deg = (o.rowptr[1:] - o.rowptr[:-1]).to(torch.float64)
         if side == "item" and self.world > 1:
-            dist.all_reduce(deg, group=self.group)
+            ordered_all_reduce(deg, group=self.group)
         s = _scale_of_degrees(deg, kind)
         self._scales[key] = s
         return s
@@ -821,7 +918,7 @@ class _BipartiteHop(torch.autograd.Function):
                 spmm_csr(sh.C.csr, X[:n], val=sh.C.val, row_scale=sh.scale("item", kind),
                          out=Yi, row_begin=a, row_end=b)
             if sh.world > 1:
-                works.append(dist.all_reduce(Yi[a:b], group=sh.group, async_op=True))
+                works.append(ordered_all_reduce(Yi[a:b], group=sh.group, async_op=True))
         spmm_csr(sh.B.csr, X[n:], val=sh.B.val, row_scale=sh.scale("user", kind), out=Y[:n])
         for w in works:
             w.wait()
@@ -842,7 +939,7 @@ def _bipartite_backward(sh: "ShardedBipartite", kind, dY: torch.Tensor) -> torch
     work = None
     if sh.world > 1:
         dYi = dYi.clone()
-        work = dist.all_reduce(dYi, group=sh.group, async_op=True)
+        work = ordered_all_reduce(dYi, group=sh.group, async_op=True)
     dX = torch.empty_like(dY)
     # partial dX_i = B_gᵀ·S_u·dY_u while the item gradient is summed
     spmm_csr(sh.B.csc, dY[:n], val=w_b, out=dX[n:])
@@ -894,7 +991,7 @@ class _BipartiteHopFused(torch.autograd.Function):
                 if b > a:
                     spmm_csr(sh.C.csr, X[:n], val=sh.C.val, row_scale=si, out=Zi, row_begin=a,
                              row_end=b)
-                works.append(dist.all_reduce(Zi[a:b], group=sh.group, async_op=True))
+                works.append(ordered_all_reduce(Zi[a:b], group=sh.group, async_op=True))
         else:
             spmm_csr(sh.C.csr, X[:n], val=sh.C.val, row_scale=si, out=Y[n:], ex=ex_rows(n))
         spmm_csr(sh.B.csr, X[n:], val=sh.B.val, row_scale=su, out=Y[:n], ex=ex_rows(0))
@@ -1025,7 +1122,7 @@ class _ShardedDenseTwoHop(torch.autograd.Function):
         H = H.contiguous()
         X = X.contiguous()
         M = _tn(H, X)                      # this rank's Hᵀ·X [K, d]
-        dist.all_reduce(M, group=group)    # K·d·4 bytes: 8 KB at K = 32, d = 64
+        ordered_all_reduce(M, group=group)    # K·d·4 bytes: 8 KB at K = 32, d = 64
         ctx.save_for_backward(H, X, M)
         ctx.group = group
         return _nn(H, M)
@@ -1035,7 +1132,7 @@ class _ShardedDenseTwoHop(torch.autograd.Function):
         H, X, M = ctx.saved_tensors
         dY = dY.contiguous()
         dM = _tn(H, dY)
-        dist.all_reduce(dM, group=ctx.group)
+        ordered_all_reduce(dM, group=ctx.group)
         dH = dX = None
         if ctx.needs_input_grad[1]:
             dX = _nn(H, dM)
@@ -1096,7 +1193,7 @@ class _ShardedHCCFLayers(torch.autograd.Function):
             h = hid[k]
             M_u, M_i = _gemm_tn_pair([(H_u, h[:nl]), (H_i, h[nl:])], dev)
             if world > 1:
-                dist.all_reduce(M_u, group=group)
+                ordered_all_reduce(M_u, group=group)
             Hh = torch.empty((N, d), **f)
             _gemm_rows([_rows_desc(H_u, M_u, d, 1, K, d, Hh[:nl]),
                         _rows_desc(H_i, M_i, d, 1, K, d, Hh[nl:])], dev)
@@ -1108,7 +1205,7 @@ class _ShardedHCCFLayers(torch.autograd.Function):
                     if b > a:
                         spmm_csr(sh.C.csr, h[:nl], val=sh.C.val, out=G[nl:], row_begin=a,
                                  row_end=b)
-                    works.append(dist.all_reduce(G[nl:][a:b], group=group, async_op=True))
+                    works.append(ordered_all_reduce(G[nl:][a:b], group=group, async_op=True))
             else:
                 spmm_csr(sh.C.csr, h[:nl], val=sh.C.val,
                          ex=_res_epilogue(Hh[nl:], act_out=G[nl:]), out=out[nl:])
@@ -1156,7 +1253,7 @@ class _ShardedHCCFLayers(torch.autograd.Function):
             dG = dG.contiguous()
             dM_u, dM_i = _gemm_tn_pair([(H_u, dHh[:nl]), (H_i, dHh[nl:])], dev)
             if world > 1:  # M_u was all-reduced: its gradient is summed too
-                dist.all_reduce(dM_u, group=group)
+                ordered_all_reduce(dM_u, group=group)
             if ctx.needs_input_grad[4 + 2 * k] or ctx.needs_input_grad[5 + 2 * k]:
                 dH_u, dH_i = torch.empty_like(H_u), torch.empty_like(H_i)
                 _gemm_rows([_rows_desc(dHh[:nl], M_u, 1, d, d, K, dH_u),
@@ -1180,7 +1277,7 @@ class _ShardedHCCFLayers(torch.autograd.Function):
             dZi, work = dG[nl:], None
             if world > 1:  # the items' gradient summed while the into-items hop runs
                 dZi = dZi.clone()
-                work = dist.all_reduce(dZi, group=group, async_op=True)
+                work = ordered_all_reduce(dZi, group=group, async_op=True)
             spmm_csr(sh.B.csc, dG[:nl], val=sh.B.val_t, ex=ex(nl, N), out=dh_new[nl:])
             if work is not None:
                 work.wait()

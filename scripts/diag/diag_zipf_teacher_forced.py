@@ -22,6 +22,8 @@ import random
 import sys
 import tempfile
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "scripts"))
@@ -35,6 +37,10 @@ def main():
     ap.add_argument("--items", type=int, default=38_048)
     ap.add_argument("--train", type=int, default=1_170_000)
     ap.add_argument("--test", type=int, default=390_000)
+    ap.add_argument("--orders", type=int, default=0,
+                    help="at every step where ours exceeds max(1e-5, the reference-fp32 "
+                         "deviation): the reference's fp32 calls again with each drop-edge COO's "
+                         "entries in this many other orders, and the worst rows named")
     ap.add_argument("--analyze", type=int, default=4,
                     help="decompose the first N steps over the bound (forward outputs, the BPR "
                          "and InfoNCE gradients apart, a bitwise re-run of the step)")
@@ -116,8 +122,21 @@ def main():
     rec.ssl_loss = ssl_capture
     print(json.dumps({"n_users": nu, "n_items": ni, "start": args.start}), flush=True)
 
-    def reference(P, dtype, drops, masks, u, i, j, parts=False):
-        adjs = [R.sparse(di, dv, (N, N), dtype) for di, dv in drops]
+    def permuted(di, dv, dtype, seed):
+        """The same dropped matrix with its entries listed in another order (an uncoalesced COO:
+        torch.sparse.mm's CPU kernel sums each row in storage order, so this is the reference's
+        own calls on the same matrix with a different, equally valid fp32 summation order)."""
+        ii = torch.as_tensor(np.asarray(di), dtype=torch.int64)
+        vv = torch.as_tensor(np.asarray(dv)).to(dtype)
+        p = torch.randperm(ii.shape[1], generator=torch.Generator().manual_seed(seed))
+        return torch.sparse_coo_tensor(ii[:, p], vv[p], (N, N))
+
+    def reference(P, dtype, drops, masks, u, i, j, parts=False, order_seed=None):
+        if order_seed is None:
+            adjs = [R.sparse(di, dv, (N, N), dtype) for di, dv in drops]
+        else:
+            adjs = [permuted(di, dv, dtype, order_seed * 97 + k)
+                    for k, (di, dv) in enumerate(drops)]
         ueR, ieR, gR, hR = R.hccf_encoder(P, adjs, [m.to(dtype) for m in masks], keep_h, nu, L)
         anc, pos, neg = ueR[u], ieR[i], ieR[j]
         nodes = []
@@ -328,12 +347,38 @@ def main():
             loss_rel32 = abs(l32 - l64) / abs(l64)
             over = max(over, loss_rel / max(R.TOL, loss_rel32))
             worst_all = max(worst_all, over)
+            orders = None
+            if args.orders and over > 1.0:
+                # the excess tensors: the reference's fp32 deviation under other entry orders,
+                # and where the worst rows of ours sit (which node, its degree, its batch count)
+                orders = {}
+                for n, (ours, own) in rows.items():
+                    if ours <= max(R.TOL, own):
+                        continue
+                    devs = []
+                    for o in range(args.orders):
+                        Po = {k: v.float().requires_grad_(True) for k, v in before.items()}
+                        _, go, _, _ = reference(Po, torch.float32, drops, masks, uc, ic, jc,
+                                                order_seed=1000 * b + o)
+                        devs.append(R.check_rows(go[n], g64[n], f"ref32 order {o} {n}",
+                                                 tol=1e9))
+                    off = nu if "item" in n else 0
+                    w = worst_row(params[n].grad, g64[n])
+                    w32 = worst_row(g32[n], g64[n])
+                    k = w["row"]
+                    ids = (ic, jc) if "item" in n else (uc,)
+                    orders[n] = {"ours": ours, "ref32": own, "ref32_other_orders": devs,
+                                 "max_ref32_any_order": max([own] + devs),
+                                 "ours_over_max_ref32_any_order": ours / max([own] + devs),
+                                 "worst_row": k, "ref32_worst_row": w32["row"],
+                                 "node_degree": int(node_deg[off + k]),
+                                 "times_in_batch": [int((t == k).sum()) for t in ids]}
             print(json.dumps({"epoch": ep, "batch": b, "mode": mode, "loss": got,
                               "dropout_zero_inputs_so_far": enc.drop_out.zero_inputs,
                               "loss_ref64": l64, "loss_rel": loss_rel, "loss_rel_ref32": loss_rel32,
                               "grad_row_ratio": rows, "ratio_over_bound": over,
                               "within_bound": over <= 1.0, "node_list_gaps": gaps,
-                              "max_abs_ref64": mags}), flush=True)
+                              "max_abs_ref64": mags, "orders": orders}), flush=True)
             if over > 10.0 and analyzed < args.analyze:
                 analyzed += 1
                 analyze(b, u, i, j, before, pre_rng, drops, masks)

@@ -106,3 +106,66 @@ def test_gather_checks_over_gloo_fails_if_any_rank_fails():
     for c in got:
         assert c["ok"] is False and c["ranks_checked"] == 2 and c["ranks_in_parallel"]
         assert c["max_rel_err_Y"] == pytest.approx(2e-7) and c["wall_s"] == 4.0
+
+
+def _first_step_worker(rank, world, port, corrupt, q):
+    """One rank of a CPU rehearsal of bench.py's N > 1 check: this rank's checked step and first
+    timed step against the same reference rows, the rehearsal hook applied, gathered."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if corrupt is not None:
+        os.environ["HGD_BENCH_CORRUPT_FIRST_STEP"] = str(corrupt)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = torch.Generator().manual_seed(10 + rank)
+        Y_ref, dX_ref = torch.randn(50, 8, generator=g), torch.randn(50, 8, generator=g)
+        mag_Y, mag_dX = Y_ref.abs() + 1.0, dX_ref.abs() + 1.0
+        Y, dX = Y_ref * (1 + 1e-7), dX_ref.clone()  # the checked step: within the bound
+        first = bench.corrupt_first_step((Y_ref.clone(), dX_ref.clone()), rank)
+        check = bench.check_rows(Y, dX, Y_ref, dX_ref, mag_Y, mag_dX, first)
+        got = bench.gather_checks(check, world, shared_device=False)
+        q.put((rank, got, bench.line_status(got, None)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("corrupt", [None, 1])
+def test_corrupted_first_step_fails_the_line_over_gloo(corrupt):
+    """VERDICT r05 'Next' 1: a first timed step that is wrong on ONE rank (rank 1, by the
+    HGD_BENCH_CORRUPT_FIRST_STEP hook) fails the gathered check on every rank and the run's exit
+    status, while the step after timing alone would have passed."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    mp.start_processes(_first_step_worker, args=(2, _free_port(), corrupt, q), nprocs=2,
+                       join=True, start_method="spawn")
+    got = [q.get(timeout=60) for _ in range(2)]
+    for rank, c, rc in got:
+        assert c["max_rel_err_Y"] < 1e-5 and c["max_rel_err_dX"] == 0.0
+        fs = c["first_step"]
+        if corrupt is None:
+            assert c["ok"] and fs["ok"] and fs["failed_ranks"] == [] and rc == 0
+        else:
+            assert not c["ok"] and not fs["ok"] and fs["failed_ranks"] == [1] and rc == 1
+            assert fs["max_rel_err_Y"] > 0.5
+
+
+def test_parity_gate_holds_the_first_step_too():
+    U, I, d = 300, 40, 16
+    idx = _graph(U, I)
+    g = torch.Generator().manual_seed(3)
+    X, dY = torch.randn(U, d, generator=g), torch.randn(U, d, generator=g)
+    Y, dX, s = bench.cpu_reference(idx, X, dY, U, I)
+    ok = bench.parity_gate(Y.clone(), dX.clone(), Y, dX, s, first=(Y.clone(), dX.clone()))
+    assert ok["ok"] and ok["first_step"]["ok"] and bench.line_status(None, ok) == 0
+    Yf = Y.clone()
+    Yf[5] += 1.0
+    bad = bench.parity_gate(Y.clone(), dX.clone(), Y, dX, s, first=(Yf, dX.clone()))
+    assert not bad["ok"] and not bad["first_step"]["ok"] and bad["first_step"]["worst_row_Y"] == 5
+    assert bad["rows_over_Y"] == 0 and bench.line_status(None, bad) == 1
+
+
+def test_host_cpus_reports_the_thread_choice():
+    h = bench.host_cpus()
+    assert h["os_cpu_count"] >= 1 and 1 <= h["affinity"] <= h["os_cpu_count"]
+    assert 1 <= h["threads"] <= h["affinity"]
+    if h["cgroup_cpu_quota"]:
+        assert h["threads"] <= h["cgroup_cpu_quota"]

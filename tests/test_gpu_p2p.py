@@ -289,29 +289,39 @@ def _free_bytes(dev):
     return torch.cuda.mem_get_info(dev)[0]
 
 
-def test_p2p_segments_freed_when_dropped_without_close(dev):
-    """A ShardedIncidence dropped without close() frees its exported segments (hipMemGetInfo
-    gains back the slots' 1 GiB): no global keeps the exchange alive through its cached slot
-    views. (Deltas at 0.8 of the slot bytes: other tests' garbage collected in between moves
-    the absolute free figure by tens of MB.)"""
+def test_p2p_segments_of_a_dropped_exchange_go_with_the_next_collective_close(dev):
+    """A ShardedIncidence dropped without close() keeps its exported segments mapped (a peer's
+    exchange kernel may still read them), and the next collective close() in the process frees
+    them with its own: hipMemGetInfo gains back both exchanges' slots. No global keeps the
+    dropped exchange's Python objects alive. (Deltas at 0.8 of the slot bytes: other tests'
+    garbage collected in between moves the absolute free figure by tens of MB.)"""
     from hypergraph_diffusion_for_recommendation_amd import _native as nat
+    from hypergraph_diffusion_for_recommendation_amd import sharded
     items, d = 1 << 20, 64
     slots_bytes = 4 * items * d * 4  # 2 send + 2 reduced slots of 256 MB
     free0 = _free_bytes(dev)
     live0 = nat.live_views()
+    a0 = sharded.abandoned_p2p()
     sh, ex = _sharded_with_p2p(dev, items, d)
     ex.slot(0, items, d).fill_(1.0)
     free1 = _free_bytes(dev)
     assert free0 - free1 >= 0.8 * slots_bytes, (free0, free1)
     del sh, ex
     free2 = _free_bytes(dev)
-    assert free2 - free1 >= 0.8 * slots_bytes, (free1, free2)
-    assert nat.live_views() == live0
+    assert abs(free2 - free1) < 0.2 * slots_bytes, (free1, free2)  # still mapped
+    assert sharded.abandoned_p2p() == a0 + 1 and nat.live_views() == live0
+    sh2, _ = _sharded_with_p2p(dev, items, d)
+    free3 = _free_bytes(dev)
+    sh2.close()  # collective (one rank): frees its own segments and the dropped exchange's
+    free4 = _free_bytes(dev)
+    assert free4 - free3 >= 1.6 * slots_bytes, (free3, free4)
+    assert sharded.abandoned_p2p() == 0
 
 
 def test_p2p_slot_view_held_past_close_stays_valid(dev):
     """close() makes the exchange unusable, but a slot view handed out before it keeps its memory
-    alive (never a view of freed memory); the memory goes with the last view's storage."""
+    alive (never a view of freed memory); the memory goes at the first safe point after the last
+    view's storage (never inside torch's storage release)."""
     items, d = 1 << 20, 64
     slots_bytes = 4 * items * d * 4
     sh, ex = _sharded_with_p2p(dev, items, d)
@@ -325,5 +335,7 @@ def test_p2p_slot_view_held_past_close_stays_valid(dev):
     v.fill_(3.0)
     assert bool((v == 3.0).all())
     del v
+    from hypergraph_diffusion_for_recommendation_amd import sharded
+    assert sharded.release_pending_p2p() >= 1  # the deleter only queued it: a safe point frees
     assert _free_bytes(dev) - free_closed >= 0.8 * slots_bytes
     del sh, ex

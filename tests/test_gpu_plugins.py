@@ -133,6 +133,7 @@ def _teacher_forced_hccf_steps(dev, tmp_path, monkeypatch, n_steps, zipf=None, f
     batches = list(next_batch_pairwise(rec.data, 256, device=dev))
     batches = (batches * (1 + n_steps // len(batches)))[:n_steps]
     worst = 0.0
+    relaxed = []
 
     def reference(before, dtype, adjs, masks, u, i, j):
         P = {n: v.to(dtype).clone().requires_grad_(True) for n, v in before.items()}
@@ -170,8 +171,16 @@ def _teacher_forced_hccf_steps(dev, tmp_path, monkeypatch, n_steps, zipf=None, f
         params = dict(enc.named_parameters())
         for n, g in g64.items():
             own = R.check_rows(g32[n], g, f"step {k} ref32 d {n}", tol=1e-2) if fp32 else 0.0
-            worst = max(worst, R.check_rows(params[n].grad, g, f"step {k} d {n}",
-                                            tol=max(R.TOL, own)))
+            ours = R.check_rows(params[n].grad, g, f"step {k} d {n}", tol=max(R.TOL, own))
+            worst = max(worst, ours)
+            if ours > R.TOL:  # a relaxed step: recorded for DESIGN.md §8's exceptions list
+                relaxed.append((k, n, ours, own))
+    if fp32:
+        over = max(relaxed, key=lambda t: t[2] / t[3], default=None)
+        print(f"relaxed-bound record: {len(relaxed)} tensor-steps over 1e-5 of "
+              f"{n_steps * len(g64)}; worst row {worst:.3e} ({worst / R.TOL:.2f}x 1e-5); "
+              f"largest ours / reference-fp32 among them: "
+              f"{'none' if over is None else f'{over[2] / over[3]:.3f} (step {over[0]}, {over[1]})'}")
     return worst
 
 
