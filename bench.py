@@ -412,6 +412,9 @@ def choose_transport(sh, eager_step, device, phase, n=3):
     # (scripts/diag/diag_p2p_first.py, profiles/r05_scale/p2p_first/). Both are reported.
     Y_r, dX_r = last[0].detach(), last[1].detach()
     out["rccl_first_vs_last_rel_diff"] = rel_diff(first, (Y_r, dX_r))
+    # the probe's first step came straight after the warm-up's barrier: if it differs from the
+    # back-to-back steps after it, the run fails (line_status), whichever transport is chosen
+    out["rccl_first_step_ok"] = out["rccl_first_vs_last_rel_diff"] <= 1e-5
     del first, last
 
     err = None
@@ -517,10 +520,12 @@ def check_rows(Y, dX, Y_ref, dX_ref, mag_Y, mag_dX, first=None):
     return out
 
 
-def line_status(check, parity) -> int:
-    """Exit status of the run: 1 if the N > 1 check (either step) or the N = 1 parity gate (either
-    step) failed, else 0."""
+def line_status(check, parity, probe=None) -> int:
+    """Exit status of the run: 1 if the N > 1 check (either step), the N = 1 parity gate (either
+    step) or the transport probe's first all-reduce step after the warm-up barrier failed, else
+    0."""
     bad = (check is not None and not check["ok"]) or (parity is not None and not parity["ok"])
+    bad = bad or (probe is not None and probe.get("rccl_first_step_ok") is False)
     return 1 if bad else 0
 
 
@@ -891,7 +896,7 @@ def main():
         roofline["per_hop"] = per
         # the hop into items gathers the user table (U·d·4 bytes, far beyond any cache) at random:
         # its rate is the HBM-efficiency figure; the hop into users gathers the item table, which
-        # is partly Infinity-Cache resident, so the mean over both is cache-assisted (DESIGN §5)
+        # is partly Infinity-Cache resident, so the mean over both is cache-assisted (DESIGN §6)
         items = [per[nm]["GBps"] for nm in ("fwd_items", "bwd_items")]
         roofline["frac_uncached_hop"] = round(statistics.mean(items) / HBM_PEAK_GBPS, 4)
         roofline["frac_note"] = ("frac is the mean over all four hops; the hops into users read "
@@ -998,7 +1003,11 @@ def main():
     if check is not None and not check["ok"]:
         print(f"bench.py: CHECK FAILED against the single-GPU conv of the global graph: {check}",
               file=sys.stderr, flush=True)
-    finish(line_status(check, parity))
+    if probe is not None and probe.get("rccl_first_step_ok") is False:
+        print(f"bench.py: the transport probe's first all-reduce step after the barrier differs "
+              f"from the steps after it by {probe['rccl_first_vs_last_rel_diff']:.3e} of max |Y|",
+              file=sys.stderr, flush=True)
+    finish(line_status(check, parity, probe))
 
 
 def finish(rc: int):

@@ -6,7 +6,7 @@
 // (util/algorithm.py:143-173). find_k_largest seeds its list with candidates[:K] sorted
 // descending (stable), then streams ALL candidates again (iid = 0..n-1), inserting a candidate
 // when it is strictly larger than the current K-th score, after every entry with an equal or
-// larger score. Closed form (DESIGN.md §4.4): the result is the first K entries of
+// larger score. Closed form (DESIGN.md §4.7): the result is the first K entries of
 //     seed = {(c_j, j) : j < K}  ∪  stream = {(c_i, i) : i < n}
 // ordered by score descending, then seed before stream, then index ascending — which is why an
 // item among the first K with a top score is listed twice by the reference, and is here too.

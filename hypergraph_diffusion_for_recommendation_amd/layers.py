@@ -300,7 +300,7 @@ class _MaskStager:
         # the destination's last reader is waited for on this (worker) thread before the copy is
         # issued, not only by the side stream: on this stack gloo's staging copies, queued behind
         # a stream wait on a still-pending event, did not reliably see their producer's output
-        # (the one-device rehearsals, DESIGN §6); here that order keeps a copy from overwriting
+        # (the one-device rehearsals, DESIGN §7); here that order keeps a copy from overwriting
         # masks a queued replay still reads. The wait is for the step before last, so the copy
         # still runs under the next replay.
         free = target_free if target is not None else self.free[k]

@@ -90,7 +90,7 @@ class HCCF(GraphRecommender):
 
     # the training loop replays its steps from a HIP graph unless hgd_graph=False (or the
     # compacted drop-edge children are asked for): bitwise the eager steps, ~1.3 vs ~1.9 ms per
-    # Yelp-shaped step (DESIGN.md §4.11)
+    # Yelp-shaped step (DESIGN.md §5)
     _graph_default = True
 
     def __init__(self, conf, training_set, test_set, knowledge_set, **kwargs):

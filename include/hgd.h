@@ -992,7 +992,7 @@ hgd_status hgd_p2p_poll(const hgd_p2p* p2p);
 /* Pricing hook: k_reduce (rank 0's block over nranks sources) and k_gather (the other blocks) of
  * a `count`-float exchange with every peer slot a separate LOCAL allocation (uncached unless
  * `cached`), mean ms per launch over `iters` launches; synchronises `stream`. Prices the
- * kernels, not xGMI (profiles/r04_scale, DESIGN.md §6). */
+ * kernels, not xGMI (profiles/r04_scale, DESIGN.md §7). */
 hgd_status hgd_p2p_price_local(int32_t nranks, int64_t count, int32_t cached, int32_t iters,
                                float* ms_reduce, float* ms_gather, void* stream);
 /* The block arithmetic of hgd_p2p_allreduce (host only, no device calls): rank q reduces floats

@@ -99,7 +99,7 @@ def main():
     def fresh(**extra):
         # every variant starts from the same fresh model (round 4 also did this because a
         # second epoch of one model diverged on this set; with round 5's InfoNCE the default
-        # model trains through both epochs below, DESIGN.md §4.11)
+        # model trains through both epochs below, DESIGN.md §5)
         torch.manual_seed(0)
         r = HCCF(conf, train, test, None, **dict(kw, **extra))
         torch.cuda.synchronize()

@@ -54,6 +54,8 @@ def worker(rank, world, port, args):
     mm_a = torch.randn(args.mm, args.mm, device=dev, generator=g)
     mm_c = torch.empty_like(mm_a)
     tail_buf = torch.ones(64, device=dev)
+    perm = torch.randperm(I, device=dev, generator=g)
+    Bs = [B[:, c:c + w].contiguous() for c in range(0, d, w)]
     step_ = (I + n_chunks - 1) // n_chunks
     bounds = [(k * step_, min((k + 1) * step_, I)) for k in range(n_chunks)]
     slices = [(c, min(c + w, d)) for c in range(0, d, w)]
@@ -62,9 +64,40 @@ def worker(rank, world, port, args):
     row_scale = inc.scale("row", "sym")
     tri = world * (world + 1) // 2
 
+    pool = [torch.cuda.Stream(dev, priority=-1) for _ in range(32)]
+    pool_next = [0]
+
+    class _Staged:
+        """--reduce emul: gloo's CUDA all-reduce restated with torch calls (ProcessGroupGloo's
+        AsyncAllreduceCUDAWork): an event on the current stream, a high-priority pool stream
+        waiting for it and copying the tensor to pinned host memory at once; at wait() the pool
+        stream is synchronised, the host copy summed over the ranks (gloo on CPU tensors) and
+        copied back on the pool stream, which the current stream then waits for."""
+
+        def __init__(self, t):
+            self.t = t
+            cur = torch.cuda.current_stream(dev)
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            self.st = pool[pool_next[0] % len(pool)]
+            pool_next[0] += 1
+            self.st.wait_event(ev)
+            with torch.cuda.stream(self.st):
+                self.host = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+                self.host.copy_(t, non_blocking=True)
+
+        def wait(self):
+            self.st.synchronize()
+            dist.all_reduce(self.host)
+            with torch.cuda.stream(self.st):
+                self.t.copy_(self.host, non_blocking=True)
+            torch.cuda.current_stream(dev).wait_stream(self.st)
+
     def all_reduce(t):
         if args.sync:
             torch.cuda.current_stream(dev).synchronize()
+        if args.reduce == "emul":
+            return _Staged(t)
         return dist.all_reduce(t, async_op=True)
 
     def two_hop(Xin, mult):
@@ -78,6 +111,9 @@ def worker(rank, world, port, args):
                 if args.hop1 == "hgd":
                     spmm_csr(inc.csc, Xs, val=val_t, row_scale=q, out=Ms, row_begin=a,
                              row_end=b)
+                elif args.hop1 == "gather":  # a memory-bound torch gather of the same rows
+                    torch.index_select(Bs[c0 // w], 0, perm[a:b], out=Ms[a:b])
+                    Ms[a:b].mul_(float((rank + 1) * mult))
                 else:
                     if args.mm:
                         torch.mm(mm_a, mm_a, out=mm_c)
@@ -101,6 +137,8 @@ def worker(rank, world, port, args):
     closed = None
     if args.hop1 == "torch" and args.hop2 == "torch":
         closed = (B[gather] * tri, B[gather] * 2 * tri)
+    elif args.hop1 == "gather" and args.hop2 == "torch":
+        closed = (B[perm][gather] * tri, B[perm][gather] * 2 * tri)
 
     for _ in range(3):
         step()
@@ -143,7 +181,7 @@ def worker(rank, world, port, args):
         dist.barrier()
     if rank == 0:
         print(json.dumps({"summary": True, "world": world, "hop1": args.hop1,
-                          "hop2": args.hop2, "sync": args.sync, "mm": args.mm, "tail": args.tail,
+                          "hop2": args.hop2, "sync": args.sync, "mm": args.mm, "tail": args.tail, "reduce": args.reduce,
                           "cycles": args.cycles, "cycles_first_step_off": bad_first,
                           "cycles_later_step_off": bad_other,
                           "seconds": round(time.perf_counter() - t0, 1)}), flush=True)
@@ -160,13 +198,16 @@ def main():
     ap.add_argument("--dim", type=int, default=64)
     ap.add_argument("--width", type=int, default=32)
     ap.add_argument("--chunks", type=int, default=4)
-    ap.add_argument("--hop1", default="torch", choices=["torch", "hgd"])
+    ap.add_argument("--hop1", default="torch", choices=["torch", "hgd", "gather"])
     ap.add_argument("--hop2", default="torch", choices=["torch", "hgd"])
     ap.add_argument("--mm", type=int, default=1024,
                     help="side of the matmul before each torch hop-1 chunk (0: none)")
     ap.add_argument("--tail", action="store_true",
                     help="launch one tiny torch kernel between each hop-1 chunk and its "
                          "all_reduce (the event gloo records then follows a torch kernel)")
+    ap.add_argument("--reduce", default="gloo", choices=["gloo", "emul"],
+                    help="gloo: dist.all_reduce of the device tensor; emul: its staging restated "
+                         "with torch calls (pool stream, pinned copy, CPU all-reduce, copy back)")
     ap.add_argument("--sync", action="store_true",
                     help="drain the current stream before every all_reduce")
     args = ap.parse_args()

@@ -67,7 +67,7 @@ def _hccf_case(dev, shape, d, n_layers, seed, batch=4096, temp=1.0, cl_rate=0.01
 
     Every output, the loss and every parameter gradient are held to the row bound against the
     reference's torch calls in float64. ``fp32_record``: the reference's own torch calls are also
-    evaluated in float32 and their deviation from the same float64 is recorded beside ours (§7 of
+    evaluated in float32 and their deviation from the same float64 is recorded beside ours (§8 of
     DESIGN.md). Returns {tensor: (ours, reference fp32 or None)} worst row ratios."""
     from hypergraph_diffusion_for_recommendation_amd.encoders import HCCFEncoder
     from hypergraph_diffusion_for_recommendation_amd.plugins import HCCF
@@ -169,7 +169,7 @@ def test_hccf_lastfm_seeds_row_bound(dev, seed, view):
     the item gradient by up to 6.1e-4 of its scale (seed 13; over 1e-5 on 8 of the 10 seeds).
     The fused InfoNCE forms that weight from the off-diagonal mass (csrc/infonce.hip), so ours
     holds 1e-5 where the reference's fp32 cannot; the reference-fp32 ratios are printed beside
-    ours (DESIGN.md §7 lists them)."""
+    ours (DESIGN.md §8 lists them)."""
     _hccf_case(dev, LASTFM, 32, 1, seed=seed, capture_safe=view, fp32_record=True)
 
 

@@ -75,8 +75,11 @@ def _worker(rank, world, port, case, q):
             return Y.clone(), Y.clone()
 
         out = bench.choose_transport(sh, eager_step, torch.device("cpu"), lambda m: None, n=2)
-        if case == "first_rccl_off":
+        if case == "first_rccl_off":  # reported, and it fails the run whatever is chosen
             assert out["rccl_first_vs_last_rel_diff"] > 0.4, out
+            assert out["rccl_first_step_ok"] is False and bench.line_status(None, None, out) == 1
+        else:
+            assert out["rccl_first_step_ok"] is True and bench.line_status(None, None, out) == 0
         q.put((rank, out["chosen"], out.get("p2p_failed_on_some_rank", False),
                "p2p_error" in out, sh.transport))
     finally:
