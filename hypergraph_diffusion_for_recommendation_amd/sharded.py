@@ -167,8 +167,9 @@ _PLOCK = threading.Lock()
 class _P2PHandle:
     """Owns one ``hgd_p2p`` handle (its exported send / reduced slots); see the rules above."""
 
-    def __init__(self, lib, h):
+    def __init__(self, lib, h, group=None):
         self.lib, self.h = lib, h
+        self.group = group   # the process group whose ranks map these segments
         self.live = 0
         self.closed = False  # a collective close() covered it: no peer reads it any more
         self.lock = threading.Lock()
@@ -224,12 +225,13 @@ def release_pending_p2p() -> int:
     return len(due)
 
 
-def _close_abandoned():
-    """Inside a collective close(), after its barrier: every rank's device has drained, so the
-    segments of exchanges this process dropped earlier can go too."""
+def _close_abandoned(group):
+    """Inside a collective close() over ``group``, after its barrier: every rank of the group has
+    drained its device, so the segments of exchanges this process dropped earlier over the SAME
+    group can go too (those of another group wait for a close over theirs)."""
     with _PLOCK:
-        dropped = list(_ABANDONED)
-        _ABANDONED.clear()
+        dropped = [hd for hd in _ABANDONED if hd.group is group]
+        _ABANDONED[:] = [hd for hd in _ABANDONED if hd.group is not group]
     for hd in dropped:
         hd.close_collective()
 
@@ -285,7 +287,7 @@ class P2PExchange:
                         "hgd_p2p_create")
         if err is None:
             self.h = h
-            self._handle = _P2PHandle(self.lib, h)
+            self._handle = _P2PHandle(self.lib, h, group)
             err = self._try(lambda: self.lib.hgd_p2p_set_timeout(h, self.timeout_s),
                             "hgd_p2p_set_timeout") or self._try(
                 lambda: self.lib.hgd_p2p_export(h, mine), "hgd_p2p_export")
@@ -410,7 +412,7 @@ class P2PExchange:
         if self._handle is not None and not self._stuck:
             self._handle.close_collective()
         self._handle = None
-        _close_abandoned()
+        _close_abandoned(self.group)
         release_pending_p2p()
 
     def release(self) -> None:

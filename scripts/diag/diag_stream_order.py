@@ -256,8 +256,10 @@ def roundtrip(args, inc, X, q, val_t, bounds, slices, perm, Xi, streams, cur, ou
                 torch.cuda.synchronize()
                 time.sleep(args.sleep_ms * 1e-3)
                 staged = []
+                prior = {}
                 for s, (c0, c1) in enumerate(slices):
                     Ms = torch.empty((n_items, c1 - c0), device=dev)
+                    prior[s] = Ms.clone() if args.prior else None  # what the block held before
                     for k, (a, b) in enumerate(bounds):
                         hop(kind, c0, c1, Ms, a, b)
                         if args.drain:  # the library's gloo ordering: drain on the host first
@@ -290,7 +292,7 @@ def roundtrip(args, inc, X, q, val_t, bounds, slices, perm, Xi, streams, cur, ou
                         results.append((c0, c1, spmm_csr(inc.csr, Ms, val=inc.val)))
                 torch.cuda.synchronize()
                 wrong = 0
-                for c0, c1, got in results:
+                for si, (c0, c1, got) in enumerate(results):
                     ref = torch.empty((n_items, c1 - c0), device=dev)
                     for a, b in bounds:
                         hop(kind, c0, c1, ref, a, b)
@@ -315,6 +317,13 @@ def roundtrip(args, inc, X, q, val_t, bounds, slices, perm, Xi, streams, cur, ou
                             "got_equals_unscaled_partial": float((g_b == p_b).all(1).float()
                                                                  .mean()),
                             "got_is_zero": float((g_b == 0).all(1).float().mean())})
+                        pr = prior.get(si)
+                        if pr is not None:
+                            p_r = pr[rows]
+                            details[-1]["got_equals_prior_times_factor"] = float(
+                                (g_b == p_r * args.host_factor).all(1).float().mean())
+                            details[-1]["got_equals_prior"] = float((g_b == p_r).all(1).float()
+                                                                    .mean())
                 bad_steps += wrong > 0
                 bad_rows += wrong
                 del staged, results
@@ -403,6 +412,9 @@ def main():
                     help="--roundtrip: what the host multiplies the staged chunk by (8: an exact "
                          "stand-in for a sum of 8 equal partials; 1: identity)")
     ap.add_argument("--rt-consumers", default="clone,hgd")
+    ap.add_argument("--prior", action="store_true",
+                    help="--roundtrip: snapshot each Ms block before its producer runs, to tell "
+                         "whether a wrong chunk holds the block's earlier content")
     ap.add_argument("--drain", action="store_true",
                     help="--roundtrip: synchronise the current stream on the host after each "
                          "chunk's producer, before its event (what sharded.ordered_all_reduce "

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 6: the torch-only reproducer of the first-step fault at a firmer count — the staging round
+# Round 6: the torch-only reproducer of the first-step fault (8 processes, staging round trip):
 # trip in 8 processes with a torch matmul producer (no libhgd call), then the same with the
 # producing stream drained on the host (the library's gloo ordering), and libhgd's hop drained.
 # Records under gpurun_out/r06_seq/<tag>.
@@ -28,10 +28,9 @@ for l in open(sys.argv[1]):
 print(sys.argv[1], {k: f"{w} wrong of {n} process-steps" for k, (n, w) in tot.items()})
 PY
 }
-rt mm_100 --producer mm --trials 100 && \
-rt mm_100_drained --producer mm --trials 100 --drain && \
-rt hgd_50_drained --producer hgd --trials 50 --drain && \
-rt hgd_50 --producer hgd --trials 50
+rt mm_prior --producer mm --trials 60 --prior && \
+rt hgd_prior --producer hgd --trials 60 --prior && \
+rt hgd_prior_drained --producer hgd --trials 60 --prior --drain
 rc=$?
 echo "rc=$rc"
 exit $rc

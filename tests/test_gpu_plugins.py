@@ -109,8 +109,8 @@ def _teacher_forced_hccf_steps(dev, tmp_path, monkeypatch, n_steps, zipf=None, f
     holds before it and with the same drop-edge and dropout draws, the float64 reference
     (tests/_ref64.py, the reference's torch calls) gives the batch loss and the gradient of every
     parameter that the plugin's optimizer then applies; held to 1e-5 (relative loss, every
-    gradient row against its scale) or, with ``fp32``, per tensor to max(1e-5, the same torch
-    calls' own deviation in float32). Returns the worst row ratio."""
+    gradient row against its scale); with ``fp32`` the same torch calls' own deviation in float32
+    is recorded beside. Returns the worst row ratio."""
     from hypergraph_diffusion_for_recommendation_amd.plugins import HCCF
     from hypergraph_diffusion_for_recommendation_amd.sampler import next_batch_pairwise
     from hypergraph_diffusion_for_recommendation_amd.selfrec import FileIO
@@ -132,8 +132,7 @@ def _teacher_forced_hccf_steps(dev, tmp_path, monkeypatch, n_steps, zipf=None, f
     random.seed(11)
     batches = list(next_batch_pairwise(rec.data, 256, device=dev))
     batches = (batches * (1 + n_steps // len(batches)))[:n_steps]
-    worst = 0.0
-    relaxed = []
+    worst = worst32 = 0.0
 
     def reference(before, dtype, adjs, masks, u, i, j):
         P = {n: v.to(dtype).clone().requires_grad_(True) for n, v in before.items()}
@@ -166,21 +165,16 @@ def _teacher_forced_hccf_steps(dev, tmp_path, monkeypatch, n_steps, zipf=None, f
         uc, ic, jc = u.cpu(), i.cpu(), j.cpu()
         l64, g64 = reference(before, torch.float64, adjs, masks, uc, ic, jc)
         l32, g32 = reference(before, torch.float32, adjs, masks, uc, ic, jc) if fp32 else (l64, None)
-        tol_l = max(R.TOL, abs(l32 - l64) / abs(l64)) if fp32 else R.TOL
-        assert abs(got - l64) <= tol_l * abs(l64), (k, got, l64)
+        assert abs(got - l64) <= R.TOL * abs(l64), (k, got, l64)
         params = dict(enc.named_parameters())
         for n, g in g64.items():
             own = R.check_rows(g32[n], g, f"step {k} ref32 d {n}", tol=1e-2) if fp32 else 0.0
-            ours = R.check_rows(params[n].grad, g, f"step {k} d {n}", tol=max(R.TOL, own))
-            worst = max(worst, ours)
-            if ours > R.TOL:  # a relaxed step: recorded for DESIGN.md §8's exceptions list
-                relaxed.append((k, n, ours, own))
-    if fp32:
-        over = max(relaxed, key=lambda t: t[2] / t[3], default=None)
-        print(f"relaxed-bound record: {len(relaxed)} tensor-steps over 1e-5 of "
-              f"{n_steps * len(g64)}; worst row {worst:.3e} ({worst / R.TOL:.2f}x 1e-5); "
-              f"largest ours / reference-fp32 among them: "
-              f"{'none' if over is None else f'{over[2] / over[3]:.3f} (step {over[0]}, {over[1]})'}")
+            worst = max(worst, R.check_rows(params[n].grad, g, f"step {k} d {n}"))
+            worst32 = max(worst32, own)
+    if fp32:  # the reference's own float32 deviation, recorded beside ours
+        print(f"skewed-catalogue record: worst gradient row {worst:.3e} of its scale over "
+              f"{n_steps} steps x {len(g64)} tensors (1e-5 outright); the reference's torch "
+              f"calls in float32: {worst32:.3e}")
     return worst
 
 
@@ -197,8 +191,9 @@ def test_hccf_skewed_catalogue_steps_match_reference_ops(dev, tmp_path, monkeypa
     """A skewed catalogue (Zipf(1.1) over 300 items: the head item is the positive of a large
     share of every batch — the fused BPR backward's list-scan path, heavy split rows in the
     item orientation) for one and a half epochs of teacher-forced plugin steps, every tensor
-    held to max(1e-5, the reference's own fp32 deviation) (the Yelp-shaped Zipf
-    record is scripts/diag/diag_zipf_teacher_forced.py)."""
+    held to 1e-5 outright (round 5 allowed max(1e-5, the reference's own fp32 deviation); the
+    round-6 record, worst 2.8e-6, never needed it), the reference's own fp32 deviation printed
+    beside (the Yelp-shaped Zipf record is scripts/diag/diag_zipf_teacher_forced.py)."""
     worst = _teacher_forced_hccf_steps(dev, tmp_path, monkeypatch, 36, zipf=1.1, fp32=True)
     print(f"HCCF plugin steps, skewed catalogue: worst gradient row ratio {worst:.2e}")
 

@@ -113,6 +113,19 @@ def test_dropped_sharded_incidence_keeps_its_exchange_mapped(fake):
     assert fake.destroyed == 2
 
 
+def test_a_close_over_another_group_leaves_a_dropped_exchange_mapped(fake):
+    ex = _exchange()
+    ex.slot(0, 8, 8)
+    del ex
+    gc.collect()
+    other = sharded.P2PExchange(64, 2, "cpu", group=object(), setup_timeout_s=10.0)
+    other.world = 1  # the stand-in group has one rank: no barrier
+    other.close()
+    assert fake.destroyed == 1 and sharded.abandoned_p2p() == 1  # only `other`'s own
+    _exchange().close()  # a close over the default group covers it
+    assert fake.destroyed == 3 and sharded.abandoned_p2p() == 0
+
+
 def test_context_manager_closes(fake):
     with _exchange() as ex:
         ex.slot(0, 8, 8)
