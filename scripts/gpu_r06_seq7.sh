@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round 6: the torch-only reproducer of the first-step fault (8 processes, staging round trip):
-# trip in 8 processes with a torch matmul producer (no libhgd call), then the same with the
-# producing stream drained on the host (the library's gloo ordering), and libhgd's hop drained.
+# Round 6: the staging round trip of the first-step fault in 8 processes, each Ms block
+# snapshotted before its producer: a torch matmul producer (no libhgd call), libhgd's hop,
+# and the hop with the producing stream drained on the host (the library's gloo ordering).
 # Records under gpurun_out/r06_seq/<tag>.
 #   gpurun --timeout 900 -- 'bash scripts/gpu_r06_seq7.sh <tag>'
 set -o pipefail
