@@ -57,6 +57,10 @@ struct SpmmArgs {
   // IEEE division's ~10-instruction sequence per kept entry
   float inv_keep;
   int32_t mask_pair;  // two-batch masked walk (HGD_TUNE_MASK_PAIR)
+  // XCD-interleaved column passes (HGD_TUNE_SPMM_PASS_INTERLEAVE): all n_pass column passes of a
+  // wide row in ONE launch, the passes of a row block on consecutive workgroups of the same XCD
+  int32_t n_pass;     // > 1: interleaved; else the launch covers the one pass at col0
+  int32_t pass_cols;  // columns per pass when interleaved
 };
 
 // vals[mask] / keepRate (HCCF.py:224)
@@ -205,10 +209,11 @@ __device__ __forceinline__ int compact_kept(const SpmmArgs& a, int l, int keep, 
 // (nth_set_bit, three per step: ~4 dependent popcount rounds each). Same slots, same sums.
 template <int G, int VEC, int U, bool HAS_VAL, int POL, bool PUSH>
 __device__ __forceinline__ void gather_sum_mask2(const SpmmArgs& a, int64_t e0, int64_t e1,
-                                                 int l, bool col_ok, float (&acc)[VEC]) {
+                                                 int l, bool col_ok, float (&acc)[VEC],
+                                                 int32_t col0) {
 #pragma unroll
   for (int i = 0; i < VEC; ++i) acc[i] = 0.f;
-  const int64_t coff = static_cast<int64_t>(a.col0) + static_cast<int64_t>(l) * VEC;
+  const int64_t coff = static_cast<int64_t>(col0) + static_cast<int64_t>(l) * VEC;
   const int base = (static_cast<int>(threadIdx.x) & 63) & ~(G - 1);
   auto group_bits = [&](int keep) {
     const unsigned long long bal = __ballot(keep != 0);
@@ -313,10 +318,10 @@ __device__ __forceinline__ void gather_sum_mask2(const SpmmArgs& a, int64_t e0, 
 // With MASK only the kept edges are summed (same order as over the compacted matrix).
 template <int G, int VEC, int U, bool HAS_VAL, int POL, bool MASK = false>
 __device__ __forceinline__ void gather_sum(const SpmmArgs& a, int64_t e0, int64_t e1, int l,
-                                           bool col_ok, float (&acc)[VEC]) {
+                                           bool col_ok, float (&acc)[VEC], int32_t col0) {
 #pragma unroll
   for (int i = 0; i < VEC; ++i) acc[i] = 0.f;
-  const int64_t coff = static_cast<int64_t>(a.col0) + static_cast<int64_t>(l) * VEC;
+  const int64_t coff = static_cast<int64_t>(col0) + static_cast<int64_t>(l) * VEC;
   constexpr bool PF = (POL & kPolPrefetch) != 0;
   int nxc = 0, nxk = 0;
   float nxw = 1.f;
@@ -379,18 +384,19 @@ int g_mask_div = 0;   // HGD_TUNE_MASK_DIV: 1 = divide by keep even when it is a
 // MASK with G >= 8 lanes (U | G): the two-batch masked walk unless HGD_TUNE_MASK_PAIR is 0.
 template <int G, int VEC, int U, bool HAS_VAL, int POL, bool MASK>
 __device__ __forceinline__ void masked_or_plain_sum(const SpmmArgs& a, int64_t e0, int64_t e1,
-                                                    int l, bool col_ok, float (&acc)[VEC]) {
+                                                    int l, bool col_ok, float (&acc)[VEC],
+                                                    int32_t col0) {
   if constexpr (MASK && G >= 8 && G % U == 0) {
     if (a.mask_pair == 2) {
-      gather_sum_mask2<G, VEC, U, HAS_VAL, POL, true>(a, e0, e1, l, col_ok, acc);
+      gather_sum_mask2<G, VEC, U, HAS_VAL, POL, true>(a, e0, e1, l, col_ok, acc, col0);
       return;
     }
     if (a.mask_pair) {
-      gather_sum_mask2<G, VEC, U, HAS_VAL, POL, false>(a, e0, e1, l, col_ok, acc);
+      gather_sum_mask2<G, VEC, U, HAS_VAL, POL, false>(a, e0, e1, l, col_ok, acc, col0);
       return;
     }
   }
-  gather_sum<G, VEC, U, HAS_VAL, POL, MASK>(a, e0, e1, l, col_ok, acc);
+  gather_sum<G, VEC, U, HAS_VAL, POL, MASK>(a, e0, e1, l, col_ok, acc, col0);
 }
 
 template <int G, int VEC, int U, bool HAS_VAL, int POL, bool EX, bool MASK = false>
@@ -398,11 +404,22 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
   constexpr int GPB = kBlock / G;
   const int g = threadIdx.x / G;
   const int l = threadIdx.x % G;
-  const int64_t coff = static_cast<int64_t>(a.col0) + static_cast<int64_t>(l) * VEC;
+  int64_t bid = static_cast<int64_t>(blockIdx.x) - a.heavy_blocks;
+  int32_t col0 = a.col0;
+  if (a.n_pass > 1) {
+    // workgroups are dispatched to the 8 XCDs round-robin (blockIdx mod 8): the n_pass passes of
+    // row block (k / n_pass)·8 + x run back to back on XCD x, so the later passes find the row
+    // pointers and index stream in that XCD's L2 and fetch the other quarters of the same
+    // gathered rows while the DRAM pages are open (no split rows here: heavy_blocks is 0)
+    const int64_t x = bid & 7, k = bid >> 3;
+    col0 = static_cast<int32_t>((k % a.n_pass) * a.pass_cols);
+    bid = (k / a.n_pass) * 8 + x;
+  }
+  const int64_t coff = static_cast<int64_t>(col0) + static_cast<int64_t>(l) * VEC;
   const bool col_ok = coff < a.d;
   float acc[VEC];
 
-  if (static_cast<int64_t>(blockIdx.x) < a.heavy_blocks) {
+  if (bid < 0) {
     const int64_t t = static_cast<int64_t>(blockIdx.x) * GPB + g;
     if (t >= a.n_chunks) return;
     const int h = a.chunk_heavy[t];
@@ -412,18 +429,17 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
     const int64_t re = a.rowptr[r + 1];
     const int64_t e0 = a.rowptr[r] + k * a.chunk;
     const int64_t e1 = min(e0 + static_cast<int64_t>(a.chunk), re);
-    masked_or_plain_sum<G, VEC, U, HAS_VAL, POL, MASK>(a, e0, e1, l, col_ok, acc);
+    masked_or_plain_sum<G, VEC, U, HAS_VAL, POL, MASK>(a, e0, e1, l, col_ok, acc, col0);
     if (col_ok) store_vec<VEC>(a.partial + t * a.d + coff, acc);
     return;
   }
 
-  const int64_t r =
-      a.row_begin + (static_cast<int64_t>(blockIdx.x) - a.heavy_blocks) * GPB + g;
+  const int64_t r = a.row_begin + bid * GPB + g;
   if (r >= a.row_end) return;
   const int64_t e0 = a.rowptr[r];
   const int64_t e1 = a.rowptr[r + 1];
   if (a.heavy_threshold > 0 && e1 - e0 > a.heavy_threshold) return;  // split-plan row
-  masked_or_plain_sum<G, VEC, U, HAS_VAL, POL, MASK>(a, e0, e1, l, col_ok, acc);
+  masked_or_plain_sum<G, VEC, U, HAS_VAL, POL, MASK>(a, e0, e1, l, col_ok, acc, col0);
   const float s = a.row_scale ? a.row_scale[r] : 1.f;
   finish_row<G, VEC, EX, (POL & kPolNtStore) != 0>(a, r, s, l, coff, col_ok, acc);
 }
@@ -591,6 +607,9 @@ int g_policy = kDefaultPolicy;
 // floats in one pass, wider rows in 64-column passes (measured on MI355X at 100 M edges, d = 256:
 // 64-column passes 64.9 ms per fwd+bwd, 128: 66.3 ms, one 256-wide pass of 64 lanes: 69.4 ms)
 int g_pass_cols = 0;
+// HGD_TUNE_SPMM_PASS_INTERLEAVE: 1 = a wide row's column passes as ONE launch, interleaved so the
+// passes of a row block run back to back on one XCD (see spmm_kernel); 0 = a launch per pass
+int g_pass_interleave = 0;
 
 template <int G, int VEC, int U, int POL, bool EX = false>
 void launch_kernel(const SpmmArgs& a, bool has_val, bool seg, int64_t blocks, hipStream_t st) {
@@ -660,8 +679,9 @@ hgd_status launch_g(SpmmArgs a, bool has_val, hipStream_t st) {
       return check_launch("hgd_spmm segmented kernel");
     }
   }
-  const int64_t light_blocks = (rows + GPB - 1) / GPB;
+  int64_t light_blocks = (rows + GPB - 1) / GPB;
   a.heavy_blocks = (a.n_chunks + GPB - 1) / GPB;
+  if (a.n_pass > 1) light_blocks = (light_blocks + 7) / 8 * 8 * a.n_pass;  // (no split rows)
   const int64_t blocks = light_blocks + a.heavy_blocks;
   if (blocks > 0) {
     if (blocks > 0x7fffffffLL) return fail(HGD_ERR_UNSUPPORTED, "hgd_spmm: grid too large");
@@ -796,6 +816,13 @@ hgd_status spmm_impl(const int64_t* rowptr, const int32_t* col, const float* val
     int G = lanes >= 64 ? 64 : next_pow2(lanes);
     const int pass_cols = g_pass_cols ? g_pass_cols : (d <= 128 ? 256 : 64);
     if (!ex && 4 * G > pass_cols) G = pass_cols / 4;
+    const int n_pass = (d + 4 * G - 1) / (4 * G);
+    if (g_pass_interleave && n_pass > 1 && !ex && !mask && a.n_chunks == 0 && !a.seg) {
+      a.col0 = 0;
+      a.n_pass = n_pass;
+      a.pass_cols = 4 * G;
+      return launch_vec<4>(G, a, has_val, st);
+    }
     for (int c0 = 0; c0 < d; c0 += 4 * G) {
       a.col0 = c0;
       hgd_status s = ex ? launch_vec<4, true>(G, a, has_val, st)
@@ -945,6 +972,10 @@ extern "C" hgd_status hgd_set_tuning(int32_t key, int32_t value) {
     case HGD_TUNE_MASK_DIV:
       HGD_REQUIRE(value == 0 || value == 1, "hgd_set_tuning: mask div must be 0 or 1");
       g_mask_div = value;
+      return HGD_OK;
+    case HGD_TUNE_SPMM_PASS_INTERLEAVE:
+      HGD_REQUIRE(value == 0 || value == 1, "hgd_set_tuning: pass interleave must be 0 or 1");
+      g_pass_interleave = value;
       return HGD_OK;
     case HGD_TUNE_CPU_RNG_THREADS:
       HGD_REQUIRE(value >= 0 && value <= 64, "hgd_set_tuning: cpu rng threads must be 0..64");

@@ -108,7 +108,11 @@ typedef enum hgd_epilogue {
  *                         are the same bits every way
  *   HGD_TUNE_MASK_DIV:    the masked hop's kept weights val / keep: 0 (default) = one multiply by
  *                         1 / keep when keep is a power of two (the same bits: one real value,
- *                         rounded once), else the IEEE division; 1 = always the division */
+ *                         rounded once), else the IEEE division; 1 = always the division
+ *   HGD_TUNE_SPMM_PASS_INTERLEAVE: rows wider than one column pass (d > 128 by default, unfused,
+ *                         no split rows): 0 = one launch per pass; 1 = all passes in one launch,
+ *                         a row block's passes on consecutive workgroups of one XCD (the same
+ *                         bits either way) */
 typedef enum hgd_tune_key {
   HGD_TUNE_SPMM_UNROLL = 1,
   HGD_TUNE_SPMM_POLICY = 2,
@@ -125,7 +129,8 @@ typedef enum hgd_tune_key {
   HGD_TUNE_X3P_QUEUE = 13,
   HGD_TUNE_P2P_GRID = 14,
   HGD_TUNE_MASK_PAIR = 15,
-  HGD_TUNE_MASK_DIV = 16
+  HGD_TUNE_MASK_DIV = 16,
+  HGD_TUNE_SPMM_PASS_INTERLEAVE = 17
 } hgd_tune_key;
 hgd_status hgd_set_tuning(int32_t key, int32_t value);
 

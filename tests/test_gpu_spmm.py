@@ -197,3 +197,40 @@ def test_segmented_only_for_short_rows(dev):
     inc.csr.configure_kernel(True)
     inc.csc.configure_kernel(True)
     assert inc.csr.segmented and not inc.csc.segmented
+
+
+@pytest.mark.parametrize("d", [192, 256, 320, 512])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_spmm_interleaved_column_passes_are_bitwise_the_pass_loop(dev, d, weighted):
+    """HGD_TUNE_SPMM_PASS_INTERLEAVE: a row wider than one column pass as ONE launch whose
+    workgroups walk the passes of a row block back to back on one XCD — the same sums in the
+    same order as one launch per pass, so bitwise equal; over a row range, with row scales, and
+    against the float64 oracle."""
+    from hypergraph_diffusion_for_recommendation_amd import _native as nat
+    from hypergraph_diffusion_for_recommendation_amd import spmm_csr
+    lib = nat.load()
+    rng = np.random.default_rng(d + 3 * weighted)
+    R, C = 3001, 517
+    r, c = random_coo(rng, R, C, 40000)
+    vals = rng.standard_normal(len(r)).astype(np.float32) if weighted else None
+    inc = _build(r, c, vals, (R, C), dev)
+    X = torch.from_numpy(rng.standard_normal((C, d)).astype(np.float32)).to(dev)
+    scale = torch.from_numpy(rng.random(R).astype(np.float32)).to(dev)
+    outs = []
+    try:
+        for inter in (0, 1):
+            nat.check(lib.hgd_set_tuning(17, inter), "interleave")
+            Y = torch.full((R, d), float("nan"), device=dev)
+            spmm_csr(inc.csr, X, val=inc.val, row_scale=scale, out=Y, row_begin=37, row_end=2900)
+            outs.append(Y)
+    finally:
+        nat.check(lib.hgd_set_tuning(17, 0), "interleave off")
+    assert torch.equal(outs[0][37:2900], outs[1][37:2900])
+    assert bool(outs[1][:37].isnan().all()) and bool(outs[1][2900:].isnan().all())
+    rowptr, col, v, _ = O.csr_from_coo(r, c, R, vals)
+    Xn = X.cpu().numpy()
+    sn = scale.cpu().numpy()
+    ref = O.spmm_csr(rowptr, col, Xn, v, sn)
+    mag = O.spmm_csr(rowptr, col, Xn, v, sn, absolute=True)
+    assert_close(outs[1][37:2900].cpu().numpy(), ref[37:2900], mag[37:2900],
+                 what=f"interleaved d={d}")
