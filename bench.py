@@ -884,6 +884,18 @@ def main():
         "avg_launch_ms": round(hop["avg_ms"], 4),
         "launches_timed": hop["launches"],
     }
+    # a "launch" above is one hop (one spmm_csr call); rocprofv3 lists spmm_kernel per dispatch:
+    # a row wider than 128 runs as 64-column passes, and the hop into items runs as
+    # hgd_spmm_blocked in `blocks` dispatches per pass when its gathered
+    # user table exceeds the Infinity Cache (incidence.spmm_blocks)
+    from hypergraph_diffusion_for_recommendation_amd.incidence import spmm_blocks
+    blocks = spmm_blocks(sh.inc.csc, args.dim)
+    passes = 1 if args.dim <= 128 else -(-args.dim // 64)  # hgd_spmm's 64-column passes
+    roofline["dispatches_per_hop"] = {"into_items": passes * max(1, blocks),
+                                      "into_users": passes}
+    if blocks:
+        roofline["kernel"] = ("hgd::spmm_kernel (hgd_spmm hop; into items: hgd_spmm_blocked, "
+                              f"{blocks} source blocks)")
     # per-hop breakdown: launches cycle fwd-CSC (into items), fwd-CSR (into users), bwd-CSC, bwd-CSR
     names = ["fwd_items", "fwd_users", "bwd_items", "bwd_users"]
     if world == 1 and hop["launches"] % 4 == 0:

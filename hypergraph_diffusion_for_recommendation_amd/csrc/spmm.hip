@@ -16,6 +16,8 @@
 //     chunk partials in chunk order — no float atomics anywhere.
 #include <cmath>
 
+#include <hipcub/hipcub.hpp>
+
 #include "device_util.h"
 #include "hgd_internal.h"
 
@@ -61,6 +63,14 @@ struct SpmmArgs {
   // wide row in ONE launch, the passes of a row block on consecutive workgroups of the same XCD
   int32_t n_pass;     // > 1: interleaved; else the launch covers the one pass at col0
   int32_t pass_cols;  // columns per pass when interleaved
+  // source-blocked hop (hgd_spmm_blocked): col / val are the block-major copy of the structure
+  // (hgd_spmm_col_blocks) and this launch sums, for every row r, its nonzeros of source block
+  // blk, blk_seg[blk·blk_rows + r] .. blk_seg[blk·blk_rows + r + 1]; with blk_accum it adds s·Σ
+  // to the Y row the blocks before it wrote
+  const int64_t* blk_seg;
+  int64_t blk_rows;
+  int32_t blk;
+  int32_t blk_accum;
 };
 
 // vals[mask] / keepRate (HCCF.py:224)
@@ -86,6 +96,21 @@ constexpr int kPolPrefetch = 8;  // software-pipelined index batches (see gather
 template <int G, int VEC, bool EX, bool NT_STORE>
 __device__ __forceinline__ void finish_row(const SpmmArgs& a, int64_t r, float s, int l,
                                            int64_t coff, bool col_ok, float (&acc)[VEC]) {
+  if constexpr (!EX) {
+    if (a.blk_accum) {  // a later block of a column-blocked hop: Y = epi(s·Σ_block + Y)
+      float prev[VEC];
+      if (col_ok) {
+        load_vec<VEC>(a.Y + r * a.ldy + coff, prev);
+      } else {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) prev[i] = 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) acc[i] = epilogue(acc[i] * s + prev[i], a.epi, a.slope);
+      if (col_ok) store_vec<VEC, NT_STORE>(a.Y + r * a.ldy + coff, acc);
+      return;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < VEC; ++i) acc[i] = epilogue(acc[i] * s, a.epi, a.slope);
   if constexpr (EX) {
@@ -436,9 +461,16 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
 
   const int64_t r = a.row_begin + bid * GPB + g;
   if (r >= a.row_end) return;
-  const int64_t e0 = a.rowptr[r];
-  const int64_t e1 = a.rowptr[r + 1];
-  if (a.heavy_threshold > 0 && e1 - e0 > a.heavy_threshold) return;  // split-plan row
+  int64_t e0, e1;
+  if (a.blk_seg) {  // source-blocked hop: this block's nonzeros of the row (no split rows)
+    const int64_t* sp = a.blk_seg + a.blk * a.blk_rows + r;
+    e0 = sp[0];
+    e1 = sp[1];
+  } else {
+    e0 = a.rowptr[r];
+    e1 = a.rowptr[r + 1];
+    if (a.heavy_threshold > 0 && e1 - e0 > a.heavy_threshold) return;  // split-plan row
+  }
   masked_or_plain_sum<G, VEC, U, HAS_VAL, POL, MASK>(a, e0, e1, l, col_ok, acc, col0);
   const float s = a.row_scale ? a.row_scale[r] : 1.f;
   finish_row<G, VEC, EX, (POL & kPolNtStore) != 0>(a, r, s, l, coff, col_ok, acc);
@@ -728,7 +760,9 @@ hgd_status spmm_impl(const int64_t* rowptr, const int32_t* col, const float* val
                      int64_t row_end, const float* X, int64_t ldx, float* Y, int64_t ldy,
                      int32_t d, int32_t epilogue, float slope, const hgd_row_epilogue* ex,
                      const uint8_t* mask, float keep, const hgd_split_plan* plan,
-                     void* workspace, size_t workspace_bytes, void* stream, const char* fn) {
+                     void* workspace, size_t workspace_bytes, void* stream, const char* fn,
+                     const int64_t* blk_seg = nullptr, int32_t n_blk = 0) {
+  // blk_seg (hgd_spmm_blocked): rowptr is unused, col / val are the block-major arrays
   HGD_REQUIRE(d > 0, "%s: d must be > 0 (got %d)", fn, d);
   HGD_REQUIRE(n_rows >= 0 && n_src_rows >= 0, "%s: negative sizes", fn);
   HGD_REQUIRE(row_begin >= 0 && row_begin <= row_end && row_end <= n_rows,
@@ -817,6 +851,21 @@ hgd_status spmm_impl(const int64_t* rowptr, const int32_t* col, const float* val
     const int pass_cols = g_pass_cols ? g_pass_cols : (d <= 128 ? 256 : 64);
     if (!ex && 4 * G > pass_cols) G = pass_cols / 4;
     const int n_pass = (d + 4 * G - 1) / (4 * G);
+    if (blk_seg) {  // column-blocked: every pass runs the blocks in order, the later ones adding
+      for (int c0 = 0; c0 < d; c0 += 4 * G) {
+        a.col0 = c0;
+        for (int k = 0; k < n_blk; ++k) {
+          a.blk_seg = blk_seg;
+          a.blk_rows = n_rows;
+          a.blk = k;
+          a.blk_accum = k > 0;
+          a.epi = k + 1 == n_blk ? epilogue : HGD_EPI_NONE;  // the activation after the last
+          hgd_status s = launch_vec<4>(G, a, has_val, st);
+          if (s != HGD_OK) return s;
+        }
+      }
+      return HGD_OK;
+    }
     if (g_pass_interleave && n_pass > 1 && !ex && !mask && a.n_chunks == 0 && !a.seg) {
       a.col0 = 0;
       a.n_pass = n_pass;
@@ -833,12 +882,80 @@ hgd_status spmm_impl(const int64_t* rowptr, const int32_t* col, const float* val
     const int G = d >= 64 ? 64 : next_pow2(d);
     for (int c0 = 0; c0 < d; c0 += G) {
       a.col0 = c0;
-      hgd_status s = ex ? launch_vec<1, true>(G, a, has_val, st)
-                        : launch_vec<1>(G, a, has_val, st);
-      if (s != HGD_OK) return s;
+      for (int k = 0; k < (blk_seg ? n_blk : 1); ++k) {
+        if (blk_seg) {
+          a.blk_seg = blk_seg;
+          a.blk_rows = n_rows;
+          a.blk = k;
+          a.blk_accum = k > 0;
+          a.epi = k + 1 == n_blk ? epilogue : HGD_EPI_NONE;
+        }
+        hgd_status s = ex ? launch_vec<1, true>(G, a, has_val, st)
+                          : launch_vec<1>(G, a, has_val, st);
+        if (s != HGD_OK) return s;
+      }
     }
   }
   return HGD_OK;
+}
+
+// Source block of column c among n_blk ranges [⌊n_cols·k/n_blk⌋, ⌊n_cols·(k+1)/n_blk⌋), stepping
+// k up from the previous nonzero's block (the columns of a row ascend).
+__device__ __forceinline__ int32_t advance_block(int64_t c, int32_t k, int64_t n_cols,
+                                                 int32_t n_blk) {
+  while (k + 1 < n_blk && c >= n_cols * (k + 1) / n_blk) ++k;
+  return k;
+}
+
+// cnt[k·n_rows + r] = nonzeros of row r in source block k (block-major, the order of the blocked
+// copy); one thread per row walks it once. cnt[n_blk·n_rows] = 0 closes the scan.
+__global__ void col_block_count_kernel(const int64_t* __restrict__ rowptr,
+                                       const int32_t* __restrict__ col, int64_t n_rows,
+                                       int64_t n_cols, int32_t n_blk, int64_t* __restrict__ cnt) {
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (r == 0) cnt[static_cast<int64_t>(n_blk) * n_rows] = 0;
+  if (r >= n_rows) return;
+  const int64_t b = rowptr[r], e = rowptr[r + 1];
+  int32_t k = 0;
+  int64_t start = b;
+  for (int64_t i = b; i < e; ++i) {
+    const int32_t kk = advance_block(col[i], k, n_cols, n_blk);
+    if (kk != k) {
+      cnt[static_cast<int64_t>(k) * n_rows + r] = i - start;
+      for (int32_t j = k + 1; j < kk; ++j) cnt[static_cast<int64_t>(j) * n_rows + r] = 0;
+      k = kk;
+      start = i;
+    }
+  }
+  cnt[static_cast<int64_t>(k) * n_rows + r] = e - start;
+  for (int32_t j = k + 1; j < n_blk; ++j) cnt[static_cast<int64_t>(j) * n_rows + r] = 0;
+}
+
+// Moves every nonzero to its block-major position blk_start[k·n_rows + r] + (its rank inside the
+// row's block k): blk_col gets the column, blk_perm (optional) the source position, with which
+// any per-nonzero array of the structure is gathered into the same order.
+__global__ void col_block_scatter_kernel(const int64_t* __restrict__ rowptr,
+                                         const int32_t* __restrict__ col, int64_t n_rows,
+                                         int64_t n_cols, int32_t n_blk,
+                                         const int64_t* __restrict__ blk_start,
+                                         int32_t* __restrict__ blk_col,
+                                         int32_t* __restrict__ blk_perm) {
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (r >= n_rows) return;
+  const int64_t b = rowptr[r], e = rowptr[r + 1];
+  int32_t k = 0;
+  int64_t start = b, out = blk_start[r];
+  for (int64_t i = b; i < e; ++i) {
+    const int32_t c = col[i];
+    const int32_t kk = advance_block(c, k, n_cols, n_blk);
+    if (kk != k) {
+      k = kk;
+      start = i;
+      out = blk_start[static_cast<int64_t>(k) * n_rows + r];
+    }
+    blk_col[out + (i - start)] = c;
+    if (blk_perm) blk_perm[out + (i - start)] = static_cast<int32_t>(i);
+  }
 }
 
 }  // namespace
@@ -854,6 +971,65 @@ extern "C" hgd_status hgd_spmm(const int64_t* rowptr, const int32_t* col, const 
   return hgd::spmm_impl(rowptr, col, val, row_scale, n_rows, n_src_rows, row_begin, row_end, X,
                         ldx, Y, ldy, d, epilogue, slope, nullptr, nullptr, 1.f, plan, workspace,
                         workspace_bytes, stream, "hgd_spmm");
+}
+
+extern "C" size_t hgd_spmm_col_blocks_workspace_size(int64_t n_rows, int32_t n_blocks) {
+  if (n_rows <= 0 || n_blocks <= 0) return 0;
+  const int64_t n = static_cast<int64_t>(n_blocks) * n_rows + 1;
+  size_t scan = 0;
+  if (hipcub::DeviceScan::ExclusiveSum(nullptr, scan, static_cast<const int64_t*>(nullptr),
+                                       static_cast<int64_t*>(nullptr), n) != hipSuccess)
+    return 0;
+  return hgd::align_up(static_cast<size_t>(n) * sizeof(int64_t)) + hgd::align_up(scan);
+}
+
+extern "C" hgd_status hgd_spmm_col_blocks(const int64_t* rowptr, const int32_t* col,
+                                          int64_t n_rows, int64_t n_cols, int32_t n_blocks,
+                                          int64_t* blk_start, int32_t* blk_col,
+                                          int32_t* blk_perm, void* workspace,
+                                          size_t workspace_bytes, void* stream) {
+  using namespace hgd;
+  clear_error();
+  HGD_REQUIRE(n_rows >= 0 && n_cols >= 0, "hgd_spmm_col_blocks: negative sizes");
+  HGD_REQUIRE(n_blocks >= 1 && n_blocks <= 64, "hgd_spmm_col_blocks: blocks must be 1..64");
+  HGD_REQUIRE(n_cols < (int64_t(1) << 31), "hgd_spmm_col_blocks: n_cols >= 2^31");
+  if (n_rows == 0) return HGD_OK;
+  HGD_REQUIRE(rowptr && blk_start, "hgd_spmm_col_blocks: null rowptr / blk_start");
+  const size_t need = hgd_spmm_col_blocks_workspace_size(n_rows, n_blocks);
+  if (!workspace || workspace_bytes < need)
+    return fail(HGD_ERR_WORKSPACE, "hgd_spmm_col_blocks: workspace %zu < %zu", workspace_bytes,
+                need);
+  const int64_t grid = (n_rows + 255) / 256;
+  HGD_REQUIRE(grid <= 0x7fffffffLL, "hgd_spmm_col_blocks: too many rows");
+  hipStream_t st = as_stream(stream);
+  const int64_t n = static_cast<int64_t>(n_blocks) * n_rows + 1;
+  int64_t* cnt = static_cast<int64_t*>(workspace);
+  char* tmp = static_cast<char*>(workspace) + align_up(static_cast<size_t>(n) * sizeof(int64_t));
+  size_t tmp_bytes = workspace_bytes - align_up(static_cast<size_t>(n) * sizeof(int64_t));
+  hipLaunchKernelGGL(col_block_count_kernel, dim3(grid), dim3(256), 0, st, rowptr, col, n_rows,
+                     n_cols, n_blocks, cnt);
+  hgd_status s = check_launch("hgd_spmm_col_blocks count");
+  if (s != HGD_OK) return s;
+  HGD_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, blk_start, n, st));
+  hipLaunchKernelGGL(col_block_scatter_kernel, dim3(grid), dim3(256), 0, st, rowptr, col, n_rows,
+                     n_cols, n_blocks, blk_start, blk_col, blk_perm);
+  return check_launch("hgd_spmm_col_blocks scatter");
+}
+
+extern "C" hgd_status hgd_spmm_blocked(const int64_t* blk_start, const int32_t* blk_col,
+                                       const float* blk_val, const float* row_scale,
+                                       int64_t n_rows,
+                                       int64_t n_src_rows, int64_t row_begin, int64_t row_end,
+                                       const float* X, int64_t ldx, float* Y, int64_t ldy,
+                                       int32_t d, int32_t epilogue, float slope,
+                                       int32_t n_blocks, void* stream) {
+  hgd::clear_error();
+  HGD_REQUIRE(n_blocks >= 1 && n_blocks <= 64, "hgd_spmm_blocked: blocks must be 1..64");
+  HGD_REQUIRE(row_end <= row_begin || blk_start, "hgd_spmm_blocked: null blk_start");
+  // spmm_impl's rowptr argument is only checked for NULL on this path
+  return hgd::spmm_impl(blk_start, blk_col, blk_val, row_scale, n_rows, n_src_rows, row_begin,
+                        row_end, X, ldx, Y, ldy, d, epilogue, slope, nullptr, nullptr, 1.f,
+                        nullptr, nullptr, 0, stream, "hgd_spmm_blocked", blk_start, n_blocks);
 }
 
 extern "C" hgd_status hgd_spmm_fused(const int64_t* rowptr, const int32_t* col, const float* val,

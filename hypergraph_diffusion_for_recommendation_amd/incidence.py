@@ -19,6 +19,7 @@ from __future__ import annotations
 import copy
 import ctypes
 import os
+import weakref
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -31,6 +32,11 @@ DEFAULT_SPLIT_CHUNK = 512
 SPLIT_THRESHOLD_MIN = 128
 SPLIT_NNZ_PER_THRESHOLD = 8192
 SEGMENTED_MAX_AVG_DEGREE = 32
+# source-blocked hop (hgd_spmm_blocked): a gathered table of at least SPMM_BLOCK_MIN_BYTES is
+# cut into about one block per SPMM_BLOCK_BYTES (2..16 blocks), see spmm_blocks()
+SPMM_BLOCK_MIN_BYTES = 1 << 30
+SPMM_BLOCK_BYTES = 640 << 20
+SPMM_BLOCK_MAX = 16
 # lane-group tasks needed to fill MI355X: 256 CUs × 16 waves × 4 groups of 16 lanes (d = 64)
 TARGET_GROUPS = 16384
 
@@ -82,6 +88,11 @@ class CSR:
         self.device = rowptr.device
         self.split_threshold = int(split_threshold)
         self.split_chunk = int(split_chunk)
+        # the columns of every row ascending (the CSC built by Incidence._from_sorted): required
+        # by the source-blocked hop, whose block starts are binary searches inside each row
+        self.cols_ascending = False
+        self._col_blocks: Dict[int, Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = {}
+        self._blk_vals: Dict[Tuple[int, int], tuple] = {}
         self._plan_arrays = ()
         self.plan = nat.SplitPlan()
         self.plan.threshold = 0
@@ -149,12 +160,87 @@ class CSR:
         # holding raw device pointers cannot be pickled or duplicated meaningfully)
         return self
 
+    def col_blocks(self, n_blocks: int) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        """The block-major copy of this structure for the source-blocked hop
+        (hgd_spmm_col_blocks): ``(blk_start [n_blocks·n_rows+1] int64, blk_col [nnz] int32,
+        blk_perm [nnz] int32)``, built once per block count on the current stream."""
+        got = self._col_blocks.get(n_blocks)
+        if got is None:
+            if not self.cols_ascending:
+                raise RuntimeError("col_blocks: the rows' columns are not known to be ascending")
+            dev = self.device
+            lib = nat.load()
+            start = torch.empty(n_blocks * self.n_rows + 1, dtype=torch.int64, device=dev)
+            bcol = torch.empty(self.nnz, dtype=torch.int32, device=dev)
+            perm = torch.empty(self.nnz, dtype=torch.int32, device=dev)
+            if self.n_rows:
+                ws = _ws(lib.hgd_spmm_col_blocks_workspace_size(self.n_rows, n_blocks), dev)
+                nat.check(lib.hgd_spmm_col_blocks(
+                    self.rowptr.data_ptr(), self.col.data_ptr() if self.nnz else None,
+                    self.n_rows, self.n_cols, n_blocks, start.data_ptr(),
+                    bcol.data_ptr() if self.nnz else None, perm.data_ptr() if self.nnz else None,
+                    ws.data_ptr(), ws.numel(), _stream(dev)), "hgd_spmm_col_blocks")
+            else:
+                start.zero_()
+            got = self._col_blocks[n_blocks] = (start, bcol, perm)
+        return got
+
+    def blocked_values(self, n_blocks: int, val: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+        """``val`` (per-nonzero weights in this structure's order) gathered into the block-major
+        order of :meth:`col_blocks`. Cached per tensor while it is alive and unmodified (its
+        version counter), e.g. the cached ``Incidence.edge_values`` a training step passes to
+        every hop; the last few are kept."""
+        if val is None:
+            return None
+        key = (n_blocks, id(val))
+        hit = self._blk_vals.get(key)
+        if hit is not None and hit[0]() is val and hit[1] == val._version:
+            return hit[2]
+        bval = _gather32(val, self.col_blocks(n_blocks)[2])
+        if len(self._blk_vals) >= 4:
+            self._blk_vals.pop(next(iter(self._blk_vals)))
+        self._blk_vals[key] = (weakref.ref(val), val._version, bval)
+        return bval
+
     @property
     def n_heavy(self) -> int:
         return int(self.plan.n_heavy) if self.plan.threshold > 0 else 0
 
     def degrees(self) -> torch.Tensor:
         return self.rowptr[1:] - self.rowptr[:-1]
+
+
+def spmm_blocks(csr: CSR, d: int) -> int:
+    """How many source blocks the hop over ``csr`` at width ``d`` runs in (0 = one pass).
+
+    The hop gathers one d-wide row of X per nonzero at random. When X is small enough for the
+    256 MB Infinity Cache (the item table a hop into users reads: 256 MB at d = 64) the gathers
+    run at ~7.5 TB/s; a larger table (the 2.56 GB user table the hop into items reads) runs at the
+    random-gather rate of HBM, ~5.9 TB/s. hgd_spmm_blocked cuts the source rows into P ranges
+    and sums a row's nonzeros of one range per pass, so each pass gathers from a slice 1/P as
+    large, for P−1 extra read+write passes over Y. Measured on MI355X at 10 M users × 1 M items
+    × 100 M edges (scripts/bench_mall_blocked.py): d = 64 −13 % at P = 4,
+    d = 128 −7 % at P = 8; hence about one block per 640 MiB of table, from 1 GiB. Rows wider
+    than 128 run as 64-column passes (1 KB row stride, 256 B gathered per row) and gained
+    nothing at any P (d = 256: −1 % … +2 % for P = 3…6), so they keep one pass.
+
+    Only for a structure whose rows' columns ascend (the CSC of an Incidence), without split
+    rows or the segmented walk. ``HGD_SPMM_BLOCKS``: ``0`` turns it off, an integer P forces P
+    blocks (1 = off) wherever it applies, unset = the size rule."""
+    if not csr.cols_ascending or csr.n_heavy or csr.segmented or csr.nnz == 0:
+        return 0
+    env = os.environ.get("HGD_SPMM_BLOCKS", "")
+    if env not in ("", "auto"):
+        p = int(env)
+        if p < 0 or p > 64:
+            raise ValueError(f"HGD_SPMM_BLOCKS must be 0..64, got {env!r}")
+        return p if p > 1 else 0
+    if d > 128:
+        return 0
+    table = csr.n_cols * d * 4
+    if table < SPMM_BLOCK_MIN_BYTES:
+        return 0
+    return max(2, min(SPMM_BLOCK_MAX, round(table / SPMM_BLOCK_BYTES)))
 
 
 def spmm_csr(csr: CSR, X: torch.Tensor, val: Optional[torch.Tensor] = None,
@@ -198,6 +284,7 @@ def spmm_csr(csr: CSR, X: torch.Tensor, val: Optional[torch.Tensor] = None,
     if timer is not None:
         t0 = timer.begin()
     mask = getattr(csr, "mask", None)
+    blocks = spmm_blocks(csr, d) if mask is None and ex is None else 0
     if mask is not None and ex is not None:
         nat.check(lib.hgd_spmm_masked_fused(
             csr.rowptr.data_ptr(), csr.col.data_ptr() if csr.nnz else None, nat.ptr(val),
@@ -212,6 +299,14 @@ def spmm_csr(csr: CSR, X: torch.Tensor, val: Optional[torch.Tensor] = None,
             csr.n_rows, csr.n_cols, int(row_begin), int(row_end), X.data_ptr(), X.stride(0),
             out.data_ptr(), out.stride(0), d, int(epilogue), float(slope), plan_ptr, nat.ptr(ws),
             wsb, _stream(X.device)), "hgd_spmm_masked")
+    elif ex is None and blocks:
+        start, bcol, _ = csr.col_blocks(blocks)
+        bval = csr.blocked_values(blocks, val)
+        nat.check(lib.hgd_spmm_blocked(
+            start.data_ptr(), bcol.data_ptr(), nat.ptr(bval), nat.ptr(row_scale), csr.n_rows,
+            csr.n_cols, int(row_begin), int(row_end), X.data_ptr(), X.stride(0), out.data_ptr(),
+            out.stride(0), d, int(epilogue), float(slope), blocks, _stream(X.device)),
+            "hgd_spmm_blocked")
     elif ex is None:
         nat.check(lib.hgd_spmm(
             csr.rowptr.data_ptr(), csr.col.data_ptr() if csr.nnz else None, nat.ptr(val),
@@ -229,10 +324,10 @@ def spmm_csr(csr: CSR, X: torch.Tensor, val: Optional[torch.Tensor] = None,
         full = rb == 0 and re_ == csr.n_rows
 
         def nbytes(csr=csr, rb=rb, re_=re_, full=full, d=d, hv=val is not None,
-                   hs=row_scale is not None):
+                   hs=row_scale is not None, blocks=blocks):
             nnz = csr.nnz if full else int(csr.rowptr[re_].item() - csr.rowptr[rb].item())
             return (profiling.hop_bytes(nnz, re_ - rb, d),
-                    profiling.impl_bytes(nnz, re_ - rb, d, hv, hs))
+                    profiling.impl_bytes(nnz, re_ - rb, d, hv, hs, blocks))
 
         timer.end(t0, nbytes)
     return out
@@ -366,6 +461,7 @@ class Incidence:
 
         csr = CSR(rowptr, cols, n_rows, n_cols, *split(n_rows))
         csc = CSR(colptr, csc_col, n_cols, n_rows, *split(n_cols))
+        csc.cols_ascending = True
         c1, c2 = csr.plan_count_async(), csc.plan_count_async()
         if c1 is not None:
             csr._build_plan(*c1.tolist())

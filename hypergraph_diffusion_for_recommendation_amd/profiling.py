@@ -31,8 +31,16 @@ def hop_bytes(nnz: int, rows: int, d: int, weighted: bool = False) -> int:
     return nnz * (4 + (4 if weighted else 0) + 4 * d) + rows * (4 * d + 4) + (rows + 1) * 4
 
 
-def impl_bytes(nnz: int, rows: int, d: int, has_val: bool, has_scale: bool) -> int:
-    """Bytes the hgd_spmm launch streams at minimum as implemented (int64 rowptr, weights)."""
+def impl_bytes(nnz: int, rows: int, d: int, has_val: bool, has_scale: bool,
+               blocks: int = 0) -> int:
+    """Bytes the hgd_spmm launch streams at minimum as implemented (int64 rowptr, weights).
+    A source-blocked hop (hgd_spmm_blocked, ``blocks`` = P > 1) reads the [R × (P+1)] int64
+    block starts instead of the rowptr, writes every Y row P times, reads it back P−1 times and
+    applies the row scale in every pass."""
+    if blocks > 1:
+        return (nnz * (4 + (4 if has_val else 0) + 4 * d)
+                + rows * (4 * d * (2 * blocks - 1) + (4 * blocks if has_scale else 0))
+                + rows * (blocks + 1) * 8)
     return (nnz * (4 + (4 if has_val else 0) + 4 * d)
             + rows * (4 * d + (4 if has_scale else 0)) + (rows + 1) * 8)
 

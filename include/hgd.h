@@ -185,6 +185,36 @@ hgd_status hgd_spmm(const int64_t* rowptr, const int32_t* col, const float* val,
                     const hgd_split_plan* plan, void* workspace, size_t workspace_bytes,
                     void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * The same hop (rows [row_begin,row_end), no split plan) run in n_blocks passes over SOURCE-ROW
+ * ranges [⌊n_src_rows·k/n_blocks⌋, ⌊n_src_rows·(k+1)/n_blocks⌋): pass k sums only a row's
+ * nonzeros whose column lies in block k and adds that partial to Y (pass 0 writes it; the
+ * activation runs after the last). Replaces the same call sites as hgd_spmm
+ * (torch.sparse.mm(adj.t(), X), model/graph/HGNN_HD4.py:459-462) when the gathered table is too
+ * large for the 256 MB Infinity Cache: each pass gathers from a 1/n_blocks slice of X, for
+ * (n_blocks−1) extra read+write passes over Y. The sum is a different fp32 association of the same
+ * terms (blockwise partials, each scaled by row_scale), so it is not bitwise hgd_spmm's.
+ *
+ * hgd_spmm_col_blocks builds the BLOCK-MAJOR copy of a structure whose rows' columns ascend (the
+ * CSC of an incidence): all rows' block-0 nonzeros, then all rows' block-1 nonzeros, …
+ *   blk_start: int64 [n_blocks·n_rows + 1], row r's block-k nonzeros are
+ *              [blk_start[k·n_rows + r], blk_start[k·n_rows + r + 1]) of
+ *   blk_col:   int32 [nnz], their columns, and
+ *   blk_perm:  int32 [nnz] (may be NULL), their positions in the source structure — gather any
+ *              per-nonzero weights through it (hgd_gather32) to get hgd_spmm_blocked's blk_val.
+ * Workspace: hgd_spmm_col_blocks_workspace_size.
+ * ---------------------------------------------------------------------------------------- */
+size_t hgd_spmm_col_blocks_workspace_size(int64_t n_rows, int32_t n_blocks);
+hgd_status hgd_spmm_col_blocks(const int64_t* rowptr, const int32_t* col, int64_t n_rows,
+                               int64_t n_cols, int32_t n_blocks, int64_t* blk_start,
+                               int32_t* blk_col, int32_t* blk_perm, void* workspace,
+                               size_t workspace_bytes, void* stream);
+hgd_status hgd_spmm_blocked(const int64_t* blk_start, const int32_t* blk_col,
+                            const float* blk_val, const float* row_scale, int64_t n_rows,
+                            int64_t n_src_rows, int64_t row_begin, int64_t row_end,
+                            const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t d,
+                            int32_t epilogue, float slope, int32_t n_blocks, void* stream);
+
 /* The same hop over the EDGE-DROPPED matrix of SpAdjDropEdge (model/graph/HCCF.py:213-226:
  * mask = floor(rand + keepRate), idxs[:, mask], vals[mask] / keepRate) without building it: the
  * structure is the parent's, `mask` (uint8, this orientation's edge order; for the CSC of the

@@ -1,0 +1,87 @@
+#!/usr/bin/env python3
+"""Does blocking the into-items hop by USER range pay on MI355X? The hop Hᵀ·X gathers 256-B rows
+of the 2.56 GB user table at random (5.9–6.4 TB/s, the random-gather ceiling), while the
+into-users hop, whose 256 MB item table the 256 MB Infinity Cache (MALL) mostly holds, runs at
+7.5 TB/s. Here the item hop is split into P phases, phase k summing only the neighbours in user
+block k (a CSC of H's rows [u_k, u_k+1)), so each phase gathers from a U/P-row slice of X that
+the MALL can hold; the phases accumulate into Y (Y = s·acc_k + Y). The price is P−1 extra read+write passes over Y.
+Round 6 first emulated this with one sub-CSC per block and the fused residual epilogue; it now
+times the library's hgd_spmm_blocked (one launch per block over the block-major copy of the CSC,
+hgd_spmm_col_blocks, selected through HGD_SPMM_BLOCKS) against hgd_spmm in interleaved rounds and reports
+the worst relative difference (a different fp32 summation order, so not bitwise).
+
+    python scripts/bench_mall_blocked.py [--dim 64 --rounds 5]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--users", type=int, default=10_000_000)
+    ap.add_argument("--items", type=int, default=1_000_000)
+    ap.add_argument("--edges", type=int, default=100_000_000)
+    ap.add_argument("--dim", type=int, default=64)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--blocks", default="2,4,8,10,16")
+    args = ap.parse_args()
+
+    import torch
+
+    import bench
+    from hypergraph_diffusion_for_recommendation_amd import Incidence
+    from hypergraph_diffusion_for_recommendation_amd.incidence import spmm_csr
+
+    dev = torch.device("cuda:0")
+    U, I, d = args.users, args.items, args.dim
+    idx = bench.make_graph(U, I, args.edges, 0, None, dev)
+    inc = Incidence.from_coo(idx, None, (U, I), device=dev, validate=False, rows_sorted=True)
+    del idx
+    nnz = inc.nnz
+    X = torch.randn(U, d, device=dev)
+    q = inc.scale("col", "mean")
+    w_full = inc.edge_values("csc", "sym")
+    blocks = [int(p) for p in args.blocks.split(",")]
+    for P in blocks:  # block-major copies built outside the timed rounds
+        inc.csc.col_blocks(P)
+        inc.csc.blocked_values(P, w_full)
+
+    def run(P):
+        # HGD_SPMM_BLOCKS=0: hgd_spmm; =P: hgd_spmm_blocked over P user ranges (spmm_blocks)
+        os.environ["HGD_SPMM_BLOCKS"] = str(P)
+        return spmm_csr(inc.csc, X, val=w_full, row_scale=q)
+
+    ref = run(0)
+    res = {"dim": d, "nnz": nnz, "bytes_algorithmic": nnz * (4 + 4 * d) + I * (4 * d + 4)
+           + (I + 1) * 4, "variants": {}}
+    times = {"plain": []}
+    times.update({P: [] for P in blocks})
+    diffs = {}
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    for rnd in range(args.rounds + 1):
+        for key in ["plain"] + blocks:
+            ev[0].record()
+            Y = run(0 if key == "plain" else key)
+            ev[1].record()
+            torch.cuda.synchronize()
+            if rnd:
+                times[key].append(ev[0].elapsed_time(ev[1]))
+            elif key != "plain":
+                diffs[key] = float((Y - ref).abs().max() / ref.abs().max())
+    for key, ts in times.items():
+        ms = statistics.median(ts)
+        res["variants"][str(key)] = {"ms": round(ms, 4),
+                                     "GBps_algorithmic": round(res["bytes_algorithmic"] / ms / 1e6,
+                                                               1),
+                                     "max_rel_diff_vs_plain": diffs.get(key, 0.0)}
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

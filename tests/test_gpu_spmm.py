@@ -234,3 +234,120 @@ def test_spmm_interleaved_column_passes_are_bitwise_the_pass_loop(dev, d, weight
     mag = O.spmm_csr(rowptr, col, Xn, v, sn, absolute=True)
     assert_close(outs[1][37:2900].cpu().numpy(), ref[37:2900], mag[37:2900],
                  what=f"interleaved d={d}")
+
+
+def _blocked_case(dev, seed, R=2001, C=613, nnz=30000, weighted=True, sorted_cols=True):
+    rng = np.random.default_rng(seed)
+    r, c = random_coo(rng, R, C, nnz)
+    vals = rng.standard_normal(len(r)).astype(np.float32) if weighted else None
+    # the CSC of this incidence: rows = items (C), sources = users (R), rows' columns ascending
+    inc = _build(r, c, vals, (R, C), dev, split_threshold=0)
+    return rng, r, c, vals, inc
+
+
+@pytest.mark.parametrize("n_blocks", [1, 2, 3, 7, 64])
+def test_spmm_col_blocks_is_the_block_major_copy(dev, n_blocks):
+    """hgd_spmm_col_blocks: all rows' nonzeros of source block 0, then of block 1, … (block k =
+    columns [⌊n_cols·k/P⌋, ⌊n_cols·(k+1)/P⌋)), each row's in its original order — bit-exact
+    against a numpy restatement, rows with no nonzeros included; blk_perm maps back."""
+    _, r, c, _, inc = _blocked_case(dev, 40 + n_blocks, nnz=9000)
+    csc = inc.csc
+    assert csc.cols_ascending and not inc.csr.cols_ascending
+    start, bcol, perm = (t.cpu().numpy() for t in csc.col_blocks(n_blocks))
+    rp = csc.rowptr.cpu().numpy()
+    col = csc.col.cpu().numpy()
+    R = csc.n_rows
+    cuts = np.array([csc.n_cols * k // n_blocks for k in range(n_blocks + 1)])
+    blk = np.searchsorted(cuts, col, side="right") - 1  # block of every nonzero
+    row = np.repeat(np.arange(R), np.diff(rp))
+    order = np.lexsort((np.arange(len(col)), row, blk))  # block, then row, then position
+    np.testing.assert_array_equal(perm, order)
+    np.testing.assert_array_equal(bcol, col[order])
+    cnt = np.zeros(n_blocks * R, np.int64)
+    np.add.at(cnt, blk * R + row, 1)
+    np.testing.assert_array_equal(start, np.concatenate([[0], np.cumsum(cnt)]))
+    assert csc.col_blocks(n_blocks) is csc.col_blocks(n_blocks)  # cached per block count
+
+
+@pytest.mark.parametrize("d", [7, 16, 64, 128, 256])
+@pytest.mark.parametrize("n_blocks", [2, 3, 5])
+@pytest.mark.parametrize("epi", [None, "leaky_relu"])
+def test_spmm_blocked_matches_the_oracle(dev, monkeypatch, d, n_blocks, epi):
+    """The source-blocked hop (hgd_spmm_blocked through spmm_csr, forced by HGD_SPMM_BLOCKS)
+    over the CSC of an incidence: blockwise partial sums, so a different fp32 association —
+    element-wise within 1e-5·Σ|terms| of the float64 oracle, over a row range, with row scales,
+    per-nonzero weights and the activation applied once after the last block; rows outside the
+    range untouched."""
+    from hypergraph_diffusion_for_recommendation_amd import _native as nat
+    from hypergraph_diffusion_for_recommendation_amd import spmm_csr
+    from hypergraph_diffusion_for_recommendation_amd.incidence import spmm_blocks
+    monkeypatch.setenv("HGD_SPMM_BLOCKS", str(n_blocks))
+    rng, r, c, vals, inc = _blocked_case(dev, d * 13 + n_blocks)
+    assert spmm_blocks(inc.csc, d) == n_blocks
+    R, C = 2001, 613
+    X = torch.from_numpy(rng.standard_normal((R, d)).astype(np.float32)).to(dev)
+    q = torch.from_numpy(rng.random(C).astype(np.float32)).to(dev)
+    code = {None: nat.EPI_NONE, "leaky_relu": nat.EPI_LEAKY_RELU}[epi]
+    Y = torch.full((C, d), float("nan"), device=dev)
+    spmm_csr(inc.csc, X, val=inc.val_t, row_scale=q, out=Y, row_begin=11, row_end=600,
+             epilogue=code, slope=0.2)
+    assert bool(Y[:11].isnan().all()) and bool(Y[600:].isnan().all())
+    rowptr, col, v, _ = O.csr_from_coo(c, r, C, vals)
+    Xn, qn = X.cpu().numpy(), q.cpu().numpy()
+    ref = O.spmm_csr(rowptr, col, Xn, v, qn, epi=epi, slope=0.2)
+    mag = O.spmm_csr(rowptr, col, Xn, v, qn, absolute=True)
+    assert_close(Y[11:600].cpu().numpy(), ref[11:600], mag[11:600],
+                 what=f"blocked d={d} P={n_blocks} epi={epi}")
+
+
+@pytest.mark.parametrize("d", [16, 64, 256])
+def test_spmm_one_block_is_bitwise_the_plain_hop(dev, d):
+    """With one block the block-major copy IS the structure and hgd_spmm_blocked walks
+    [rowptr[r], rowptr[r+1]) exactly as hgd_spmm: bitwise equal."""
+    from hypergraph_diffusion_for_recommendation_amd import _native as nat
+    from hypergraph_diffusion_for_recommendation_amd import spmm_csr
+    from hypergraph_diffusion_for_recommendation_amd.incidence import _stream
+    rng, r, c, vals, inc = _blocked_case(dev, 77 + d)
+    csc = inc.csc
+    X = torch.from_numpy(rng.standard_normal((2001, d)).astype(np.float32)).to(dev)
+    q = torch.from_numpy(rng.random(613).astype(np.float32)).to(dev)
+    plain = spmm_csr(csc, X, val=inc.val_t, row_scale=q)
+    start, bcol, perm = csc.col_blocks(1)
+    assert torch.equal(start, csc.rowptr) and torch.equal(bcol, csc.col)
+    bval = csc.blocked_values(1, inc.val_t)
+    assert csc.blocked_values(1, inc.val_t) is bval  # cached while the tensor lives unmodified
+    Y = torch.empty_like(plain)
+    nat.check(nat.load().hgd_spmm_blocked(
+        start.data_ptr(), bcol.data_ptr(), bval.data_ptr(), q.data_ptr(), csc.n_rows,
+        csc.n_cols, 0, csc.n_rows, X.data_ptr(), d, Y.data_ptr(), d, d, 0, 0.0, 1,
+        _stream(X.device)), "hgd_spmm_blocked")
+    assert torch.equal(Y, plain)
+    v2 = inc.val_t.clone()
+    b1 = csc.blocked_values(1, v2)
+    v2.mul_(2.0)  # modified in place: gathered again
+    b2 = csc.blocked_values(1, v2)
+    assert b2 is not b1 and torch.equal(b2, 2.0 * bval)
+
+
+def test_spmm_blocked_two_hop_fwd_bwd(dev, monkeypatch):
+    """hgconv2 fwd + bwd with the hops into items blocked (HGD_SPMM_BLOCKS=4) against the
+    float64 oracle of the two-hop and its backward, and the blocked backward of the symmetric
+    operator bitwise its blocked forward (the same hops)."""
+    from hypergraph_diffusion_for_recommendation_amd import hgconv2
+    from hypergraph_diffusion_for_recommendation_amd.incidence import spmm_blocks
+    monkeypatch.setenv("HGD_SPMM_BLOCKS", "4")
+    rng = np.random.default_rng(123)
+    U, I, d = 3000, 400, 64
+    r, c = random_coo(rng, U, I, 40000)
+    inc = _build(r, c, None, (U, I), dev, split_threshold=0)
+    assert spmm_blocks(inc.csc, d) == 4 and spmm_blocks(inc.csr, d) == 0
+    X = torch.from_numpy(rng.standard_normal((U, d)).astype(np.float32)).to(dev)
+    W = torch.from_numpy(rng.standard_normal((U, d)).astype(np.float32)).to(dev)
+    Xr = X.clone().requires_grad_(True)
+    Y = hgconv2(inc, Xr)
+    (dX,) = torch.autograd.grad(Y, Xr, W)
+    assert torch.equal(dX, hgconv2(inc, W))
+    Xn = X.cpu().numpy()
+    ref = O.two_hop(r, c, None, (U, I), Xn, P="sym", Q="mean", R="sym")
+    mag = O.two_hop(r, c, None, (U, I), np.abs(Xn), P="sym", Q="mean", R="sym")
+    assert_close(Y.detach().cpu().numpy(), ref, mag, what="blocked hgconv2")

@@ -1,0 +1,74 @@
+"""Host logic of the source-blocked hop selection (incidence.spmm_blocks): which hops run as
+hgd_spmm_blocked and in how many blocks. No GPU: the structures are CPU tensors that are never
+launched on."""
+import pytest
+import torch
+
+from hypergraph_diffusion_for_recommendation_amd.incidence import CSR, spmm_blocks
+
+
+def _csr(n_rows, n_cols, nnz=10, ascending=True):
+    rowptr = torch.zeros(n_rows + 1, dtype=torch.int64)
+    rowptr[-1] = nnz
+    s = CSR(rowptr, torch.zeros(nnz, dtype=torch.int32), n_rows, n_cols, split_threshold=0)
+    s.cols_ascending = ascending
+    return s
+
+
+@pytest.fixture(autouse=True)
+def _no_env(monkeypatch):
+    monkeypatch.delenv("HGD_SPMM_BLOCKS", raising=False)
+
+
+def test_size_rule_follows_the_gathered_table():
+    # the bench's hop into items gathers the 10 M-row user table
+    assert spmm_blocks(_csr(1_000_000, 10_000_000), 64) == 4     # 2.56 GB
+    assert spmm_blocks(_csr(1_000_000, 10_000_000), 128) == 8    # 5.12 GB
+    # rows wider than 128 (64-column passes) measured no gain: never blocked by the size rule
+    assert spmm_blocks(_csr(1_000_000, 10_000_000), 256) == 0
+    assert spmm_blocks(_csr(1_000_000, 10_000_000), 129) == 0
+    assert spmm_blocks(_csr(1_000_000, 100_000_000), 64) == 16  # clamped
+    # the hop into users gathers the 256 MB item table: one pass
+    assert spmm_blocks(_csr(10_000_000, 1_000_000), 64) == 0
+    # just below / at the 1 GiB floor
+    assert spmm_blocks(_csr(10, (1 << 30) // 256 - 1), 64) == 0
+    assert spmm_blocks(_csr(10, (1 << 30) // 256), 64) == 2
+
+
+def test_only_for_ascending_unsplit_plain_structures(monkeypatch):
+    big = 10_000_000
+    assert spmm_blocks(_csr(1000, big, ascending=False), 64) == 0
+    assert spmm_blocks(_csr(1000, big, nnz=0), 64) == 0
+    s = _csr(1000, big)
+    s.plan.flags = 1  # the segmented walk
+    assert spmm_blocks(s, 64) == 0
+    s = _csr(1000, big)
+    s.plan.threshold, s.plan.n_heavy = 16, 3  # split rows
+    assert spmm_blocks(s, 64) == 0
+    monkeypatch.setenv("HGD_SPMM_BLOCKS", "5")  # forcing never overrides the structure rules
+    assert spmm_blocks(_csr(1000, big, ascending=False), 64) == 0
+
+
+def test_environment_override(monkeypatch):
+    small = _csr(100, 1000)
+    monkeypatch.setenv("HGD_SPMM_BLOCKS", "3")
+    assert spmm_blocks(small, 8) == 3
+    monkeypatch.setenv("HGD_SPMM_BLOCKS", "1")
+    assert spmm_blocks(small, 8) == 0
+    monkeypatch.setenv("HGD_SPMM_BLOCKS", "0")
+    assert spmm_blocks(_csr(1_000_000, 10_000_000), 64) == 0
+    monkeypatch.setenv("HGD_SPMM_BLOCKS", "auto")
+    assert spmm_blocks(_csr(1_000_000, 10_000_000), 64) == 4
+    monkeypatch.setenv("HGD_SPMM_BLOCKS", "65")
+    with pytest.raises(ValueError):
+        spmm_blocks(small, 8)
+
+
+def test_blocked_implementation_bytes():
+    from hypergraph_diffusion_for_recommendation_amd import profiling
+    nnz, R, d = 1000, 100, 64
+    plain = profiling.impl_bytes(nnz, R, d, True, True)
+    assert profiling.impl_bytes(nnz, R, d, True, True, blocks=1) == plain
+    four = profiling.impl_bytes(nnz, R, d, True, True, blocks=4)
+    # + 3 Y writes and 3 Y reads, + 3 row-scale reads, block starts (R·5·8) for rowptr (R+1)·8
+    assert four - plain == 6 * R * 4 * d + 3 * R * 4 + R * 5 * 8 - (R + 1) * 8
