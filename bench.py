@@ -913,7 +913,9 @@ def main():
         roofline["frac_uncached_hop"] = round(statistics.mean(items) / HBM_PEAK_GBPS, 4)
         roofline["frac_note"] = ("frac is the mean over all four hops; the hops into users read "
                                  "a partly cache-resident item table, frac_uncached_hop is the "
-                                 "into-items hops alone")
+                                 "into-items hops alone (gathering the user table; when blocked, "
+                                 "dispatches_per_hop.into_items > 1, each dispatch's user slice "
+                                 "is partly cache-resident too)")
     if world == 1:
         # also report a measured stream-copy peak on this box (read + write bytes)
         cp, cp_detail = copy_peak_gbps(device)

@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -144,6 +145,16 @@ struct hgd_incidence {
   // per-nonzero CSC weights val_t[e]·S[row_t[e]] for source kind S (lazily built)
   mutable std::mutex mu;
   mutable float* ev_csc[5] = {};
+  // block-major copies of the CSC for the source-blocked hop (hgd_spmm_blocked), one per block
+  // count in use, with the CSC weights of each source kind gathered into their order (lazily)
+  struct BlockCopy {
+    int32_t P = 0;
+    int64_t* start = nullptr;
+    int32_t* col = nullptr;
+    int32_t* perm = nullptr;
+    float* w[5] = {};  // [source kind]; HGD_SCALE_NONE = val_t (weighted objects only)
+  };
+  mutable BlockCopy blk[4];
   mutable std::vector<void*> owned;
 
   template <class T>
@@ -353,6 +364,92 @@ hgd_status csc_weights(const hgd_incidence* o, int k, const float** out, hipStre
 
 bool valid_kind(int32_t k) { return k >= HGD_SCALE_NONE && k <= HGD_SCALE_WSYM; }
 
+// Source blocks of the hop over the CSC at width d: the rule of incidence.spmm_blocks (the
+// Python host), so both hosts sum in the same order. 0 = one pass.
+int32_t csc_blocks(const hgd_incidence* o, int32_t d) {
+  const hgd_split_plan& pl = o->plan[1];
+  if (o->nnz == 0 || (pl.threshold > 0 && pl.n_heavy > 0) || (pl.flags & HGD_PLAN_SEGMENTED))
+    return 0;
+  const char* env = std::getenv("HGD_SPMM_BLOCKS");
+  if (env && *env && std::strcmp(env, "auto") != 0) {
+    const long p = std::strtol(env, nullptr, 10);
+    return (p > 1 && p <= 64) ? static_cast<int32_t>(p) : 0;
+  }
+  if (d > 128) return 0;
+  const double table = static_cast<double>(o->n_rows) * d * 4.0;
+  if (table < 1073741824.0) return 0;
+  const double x = table / (640.0 * 1048576.0);
+  double p = std::floor(x);  // Python's round(): half to even
+  const double frac = x - p;
+  if (frac > 0.5 || (frac == 0.5 && std::fmod(p, 2.0) != 0.0)) p += 1.0;
+  return static_cast<int32_t>(std::min(16.0, std::max(2.0, p)));
+}
+
+// The block-major copy for P blocks and the CSC weights `w` of source kind k in its order.
+hgd_status block_copy(const hgd_incidence* o, int32_t P, int32_t k, const float* w,
+                      const hgd_incidence::BlockCopy** out, const float** out_w, hipStream_t st) {
+  std::lock_guard<std::mutex> g(o->mu);
+  hgd_incidence::BlockCopy* b = nullptr;
+  for (auto& c : o->blk)
+    if (c.P == P) b = &c;
+  auto grab = [&](void** q, size_t bytes) -> hgd_status {
+    HGD_HIP(hipMalloc(q, bytes));
+    o->owned.push_back(*q);
+    return HGD_OK;
+  };
+  if (!b) {
+    for (auto& c : o->blk)
+      if (c.P == 0 && !b) b = &c;
+    HGD_REQUIRE(b, "hgd_incidence: more than 4 block counts in use");
+    void *a = nullptr, *c = nullptr, *pm = nullptr, *ws = nullptr;
+    const size_t wsb = hgd_spmm_col_blocks_workspace_size(o->n_cols, P);
+    hgd_status r = grab(&a, (static_cast<size_t>(P) * o->n_cols + 1) * 8);
+    if (r == HGD_OK) r = grab(&c, static_cast<size_t>(o->nnz) * 4);
+    if (r == HGD_OK) r = grab(&pm, static_cast<size_t>(o->nnz) * 4);
+    if (r != HGD_OK) return r;
+    HGD_HIP(hipMalloc(&ws, wsb));
+    r = hgd_spmm_col_blocks(o->colptr, o->row_t, o->n_cols, o->n_rows, P,
+                            static_cast<int64_t*>(a), static_cast<int32_t*>(c),
+                            static_cast<int32_t*>(pm), ws, wsb, st);
+    const hipError_t e = hipStreamSynchronize(st);  // the workspace is freed here
+    (void)hipFree(ws);
+    if (r != HGD_OK) return r;
+    if (e != hipSuccess) return fail(HGD_ERR_HIP, "hgd_incidence block copy: %s", hipGetErrorString(e));
+    b->P = P;
+    b->start = static_cast<int64_t*>(a);
+    b->col = static_cast<int32_t*>(c);
+    b->perm = static_cast<int32_t*>(pm);
+  }
+  if (w && !b->w[k]) {
+    void* q = nullptr;
+    hgd_status r = grab(&q, static_cast<size_t>(o->nnz) * 4);
+    if (r != HGD_OK) return r;
+    if ((r = hgd_gather32(w, b->perm, o->nnz, q, st)) != HGD_OK) return r;
+    b->w[k] = static_cast<float*>(q);
+  }
+  *out = b;
+  *out_w = w ? b->w[k] : nullptr;
+  return HGD_OK;
+}
+
+// One hop over the CSC (rows [a, b) of Aᵀ) with the CSC weights w of source kind k: the
+// source-blocked hop when csc_blocks says so, else hgd_spmm.
+hgd_status csc_hop(const hgd_incidence* o, int32_t k, const float* w, const float* q, int64_t a,
+                   int64_t b, const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t d,
+                   int32_t epilogue, float slope, void* ws, size_t wsb, hipStream_t st) {
+  const int32_t P = csc_blocks(o, d);
+  if (P > 1) {
+    const hgd_incidence::BlockCopy* bc = nullptr;
+    const float* bw = nullptr;
+    hgd_status r = block_copy(o, P, k, w, &bc, &bw, st);
+    if (r != HGD_OK) return r;
+    return hgd_spmm_blocked(bc->start, bc->col, bw, q, o->n_cols, o->n_rows, a, b, X, ldx, Y, ldy,
+                            d, epilogue, slope, P, st);
+  }
+  return hgd_spmm(o->colptr, o->row_t, w, q, o->n_cols, o->n_rows, a, b, X, ldx, Y, ldy, d,
+                  epilogue, slope, &o->plan[1], ws, wsb, st);
+}
+
 size_t spmm_ws(const hgd_incidence* o, int32_t d) {
   return std::max(hgd_spmm_workspace_size(&o->plan[0], d), hgd_spmm_workspace_size(&o->plan[1], d));
 }
@@ -366,10 +463,7 @@ hgd_status hop_to_items(const hgd_incidence* o, int32_t Q, int32_t S, const floa
   if (r != HGD_OK) return r;
   const float* q = Q == HGD_SCALE_NONE ? nullptr : o->scale[HGD_SIDE_COLS][Q];
   const int64_t n = o->n_cols;
-  if (!comm) {
-    return hgd_spmm(o->colptr, o->row_t, w, q, n, o->n_rows, 0, n, X, ldx, M, d, d, HGD_EPI_NONE,
-                    0.f, &o->plan[1], ws, wsb, st);
-  }
+  if (!comm) return csc_hop(o, S, w, q, 0, n, X, ldx, M, d, d, HGD_EPI_NONE, 0.f, ws, wsb, st);
   HGD_REQUIRE(comm->device == o->device, "%s: communicator and incidence on different devices",
               fn);
   const int64_t chunks = std::max<int64_t>(1, std::min<int64_t>(comm->n_chunks, n));
@@ -377,8 +471,7 @@ hgd_status hop_to_items(const hgd_incidence* o, int32_t Q, int32_t S, const floa
   int used = 0;
   for (int64_t a = 0; a < n; a += step) {
     const int64_t b = std::min(n, a + step);
-    r = hgd_spmm(o->colptr, o->row_t, w, q, n, o->n_rows, a, b, X, ldx, M, d, d, HGD_EPI_NONE,
-                 0.f, &o->plan[1], ws, wsb, st);
+    r = csc_hop(o, S, w, q, a, b, X, ldx, M, d, d, HGD_EPI_NONE, 0.f, ws, wsb, st);
     if (r != HGD_OK) return r;
     HGD_HIP(hipEventRecord(comm->ev[used], st));
     HGD_HIP(hipStreamWaitEvent(comm->side, comm->ev[used], 0));
@@ -444,8 +537,8 @@ hgd_status two_hop_p2p(const hgd_incidence* o, int32_t Q, int32_t S_src, const f
     const int c0 = s * w, ws_ = std::min(w, d - c0);
     const int slot = parity * n_sl + s;
     float* send = hgd_p2p_slot(c->p2p, slot);
-    if (I > 0 && (r = hgd_spmm(o->colptr, o->row_t, wt, q, I, o->n_rows, 0, I, X + c0, ldx, send,
-                               ws_, ws_, HGD_EPI_NONE, 0.f, &o->plan[1], ws, wsb, st)) != HGD_OK)
+    if (I > 0 && (r = csc_hop(o, S_src, wt, q, 0, I, X + c0, ldx, send, ws_, ws_, HGD_EPI_NONE,
+                              0.f, ws, wsb, st)) != HGD_OK)
       return r;
     HGD_HIP(hipEventRecord(c->ev[s], st));
     HGD_HIP(hipStreamWaitEvent(c->side, c->ev[s], 0));
@@ -692,8 +785,8 @@ extern "C" hgd_status hgd_incidence_spmm(const hgd_incidence* o, int32_t transpo
   clear_error();
   HGD_REQUIRE(o, "hgd_incidence_spmm: null incidence");
   if (transpose)
-    return hgd_spmm(o->colptr, o->row_t, o->val_t, row_scale, o->n_cols, o->n_rows, 0, o->n_cols,
-                    X, ldx, Y, ldy, d, epilogue, slope, &o->plan[1], ws, wsb, stream);
+    return csc_hop(o, HGD_SCALE_NONE, o->val_t, row_scale, 0, o->n_cols, X, ldx, Y, ldy, d,
+                   epilogue, slope, ws, wsb, as_stream(stream));
   return hgd_spmm(o->rowptr, o->col, o->val, row_scale, o->n_rows, o->n_cols, 0, o->n_rows, X,
                   ldx, Y, ldy, d, epilogue, slope, &o->plan[0], ws, wsb, stream);
 }

@@ -359,3 +359,52 @@ def test_one_rank_comm_matches_local(dev):
         assert torch.equal(buf, ref)
     finally:
         lib.hgd_comm_destroy(comm)
+
+
+@pytest.mark.parametrize("case", [CASES[0], CASES[3]], ids=[CASES[0][0], CASES[3][0]])
+def test_conv2hop_source_blocked_matches_python(dev, monkeypatch, case):
+    """With HGD_SPMM_BLOCKS forcing the source-blocked hop (hgd_spmm_blocked; the size rule
+    picks it only for ≥ 1 GiB tables), the object path blocks its CSC hops exactly as the Python
+    Incidence does: conv2hop fwd/bwd and hgd_incidence_spmm(transpose) bitwise equal to
+    functional.two_hop / spmm_csr, and the forward within the oracle bound."""
+    from hypergraph_diffusion_for_recommendation_amd import Incidence, spmm_csr, two_hop
+    from hypergraph_diffusion_for_recommendation_amd.incidence import spmm_blocks
+    nat, lib = _lib()
+    monkeypatch.setenv("HGD_SPMM_BLOCKS", "3")
+    name, weighted, P, Q, R, epi, slope = case
+    rng = np.random.default_rng(71)
+    Nv, Ne, d = 3000, 800, 64
+    r, c = random_coo(rng, Nv, Ne, 20000)
+    vals = (rng.random(len(r)).astype(np.float32) + 0.1) if weighted else None
+    rowptr, col, _, _ = _csr_of(r, c, Nv, dev)
+    obj = _create(rowptr, col, None if vals is None else torch.from_numpy(vals).to(dev), Nv, Ne,
+                  dev)
+    inc = Incidence.from_coo(torch.from_numpy(np.stack([r, c])),
+                             None if vals is None else torch.from_numpy(vals), (Nv, Ne),
+                             device=dev)
+    assert inc.csc.n_heavy == 0 and spmm_blocks(inc.csc, d) == 3
+    X = rng.standard_normal((Nv, d)).astype(np.float32)
+    Xt = torch.from_numpy(X).to(dev)
+    dYt = torch.from_numpy(rng.standard_normal((Nv, d)).astype(np.float32)).to(dev)
+    Y, M, pre, ws = _conv(obj, P, Q, R, Xt, epi, slope, dev)
+    dX = _conv_bwd(obj, P, Q, R, dYt, (pre if pre is not None else Y) if epi else None, epi,
+                   slope, dev, ws)
+    Xg = Xt.clone().requires_grad_(True)
+    Yp = two_hop(inc, Xg, P=P, Q=Q, R=R, epilogue=epi, slope=slope)
+    (dXp,) = torch.autograd.grad(Yp, Xg, dYt)
+    assert torch.equal(Y, Yp.detach()) and torch.equal(dX, dXp), name
+    monkeypatch.setenv("HGD_SPMM_BLOCKS", "0")  # the blocked sums are not the plain ones bitwise
+    Y0, _, _, _ = _conv(obj, P, Q, R, Xt, epi, slope, dev)
+    assert not torch.equal(Y, Y0)
+    monkeypatch.setenv("HGD_SPMM_BLOCKS", "3")
+    ref = O.two_hop(r, c, vals, (Nv, Ne), X, P, Q, R, epi, slope)
+    w = None if vals is None else np.abs(vals)
+    mag = O.two_hop(r, c, w, (Nv, Ne), np.abs(X), P=P, Q=Q, R=R)
+    assert_close(Y.cpu().numpy(), ref, mag, what=f"{name} blocked fwd")
+    # the transposed plain hop of hgd_incidence_spmm
+    Yt = torch.empty(Ne, d, device=dev)
+    wsb = lib.hgd_incidence_workspace_size(obj.h, d)
+    ws2 = torch.empty(max(1, wsb), dtype=torch.uint8, device=dev)
+    nat.check(lib.hgd_incidence_spmm(obj.h, 1, Xt.data_ptr(), d, Yt.data_ptr(), d, d, None, 0,
+                                     0.0, ws2.data_ptr(), wsb, _st(dev)), "hgd_incidence_spmm")
+    assert torch.equal(Yt, spmm_csr(inc.csc, Xt, val=inc.val_t))
