@@ -885,13 +885,14 @@ def main():
         "launches_timed": hop["launches"],
     }
     # a "launch" above is one hop (one spmm_csr call); rocprofv3 lists spmm_kernel per dispatch:
-    # a row wider than 128 runs as 64-column passes, and the hop into items runs as
-    # hgd_spmm_blocked in `blocks` dispatches per pass when its gathered
+    # hgd_spmm runs a row wider than 128 as 64-column passes, and the hop into items runs as
+    # hgd_spmm_blocked (128-column passes) in `blocks` dispatches per pass when its gathered
     # user table exceeds the Infinity Cache (incidence.spmm_blocks)
     from hypergraph_diffusion_for_recommendation_amd.incidence import spmm_blocks
     blocks = spmm_blocks(sh.inc.csc, args.dim)
     passes = 1 if args.dim <= 128 else -(-args.dim // 64)  # hgd_spmm's 64-column passes
-    roofline["dispatches_per_hop"] = {"into_items": passes * max(1, blocks),
+    bpasses = -(-args.dim // 128)  # hgd_spmm_blocked's 128-column passes
+    roofline["dispatches_per_hop"] = {"into_items": bpasses * blocks if blocks else passes,
                                       "into_users": passes}
     if blocks:
         roofline["kernel"] = ("hgd::spmm_kernel (hgd_spmm hop; into items: hgd_spmm_blocked, "

@@ -375,8 +375,8 @@ int32_t csc_blocks(const hgd_incidence* o, int32_t d) {
     const long p = std::strtol(env, nullptr, 10);
     return (p > 1 && p <= 64) ? static_cast<int32_t>(p) : 0;
   }
-  if (d > 128) return 0;
-  const double table = static_cast<double>(o->n_rows) * d * 4.0;
+  // a blocked hop runs rows wider than 128 as 128-column passes
+  const double table = static_cast<double>(o->n_rows) * std::min<int32_t>(d, 128) * 4.0;
   if (table < 1073741824.0) return 0;
   const double x = table / (640.0 * 1048576.0);
   double p = std::floor(x);  // Python's round(): half to even

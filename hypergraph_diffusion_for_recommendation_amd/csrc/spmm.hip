@@ -851,7 +851,13 @@ hgd_status spmm_impl(const int64_t* rowptr, const int32_t* col, const float* val
     const int pass_cols = g_pass_cols ? g_pass_cols : (d <= 128 ? 256 : 64);
     if (!ex && 4 * G > pass_cols) G = pass_cols / 4;
     const int n_pass = (d + 4 * G - 1) / (4 * G);
-    if (blk_seg) {  // column-blocked: every pass runs the blocks in order, the later ones adding
+    if (blk_seg) {  // source-blocked: every pass runs the blocks in order, the later ones adding
+      // passes of up to 128 columns (unless tuned): at d = 256 the blocked hop into items takes
+      // 16.99 ms in 128-column passes, 18.04 in 64-column ones and 19.54 in one 256-wide pass
+      // (scripts/bench_mall_blocked.py --pass-cols, profiles/r06_round/wide/)
+      const int bcols = g_pass_cols ? g_pass_cols : 128;
+      G = lanes >= 64 ? 64 : next_pow2(lanes);
+      if (4 * G > bcols) G = bcols / 4;
       for (int c0 = 0; c0 < d; c0 += 4 * G) {
         a.col0 = c0;
         for (int k = 0; k < n_blk; ++k) {

@@ -220,9 +220,10 @@ def spmm_blocks(csr: CSR, d: int) -> int:
     and sums a row's nonzeros of one range per pass, so each pass gathers from a slice 1/P as
     large, for P−1 extra read+write passes over Y. Measured on MI355X at 10 M users × 1 M items
     × 100 M edges (scripts/bench_mall_blocked.py): d = 64 −13 % at P = 4,
-    d = 128 −7 % at P = 8; hence about one block per 640 MiB of table, from 1 GiB. Rows wider
-    than 128 run as 64-column passes (1 KB row stride, 256 B gathered per row) and gained
-    nothing at any P (d = 256: −1 % … +2 % for P = 3…6), so they keep one pass.
+    d = 128 −7 % at P = 8; hence about one block per 640 MiB of the table a pass gathers from,
+    from 1 GiB. A blocked hop runs rows wider than 128 as 128-column passes (d = 256: −6 % at
+    P = 8; in the plain hop's 64-column passes blocking gained nothing, 256 B gathered from
+    every 1 KB row).
 
     Only for a structure whose rows' columns ascend (the CSC of an Incidence), without split
     rows or the segmented walk. ``HGD_SPMM_BLOCKS``: ``0`` turns it off, an integer P forces P
@@ -235,9 +236,7 @@ def spmm_blocks(csr: CSR, d: int) -> int:
         if p < 0 or p > 64:
             raise ValueError(f"HGD_SPMM_BLOCKS must be 0..64, got {env!r}")
         return p if p > 1 else 0
-    if d > 128:
-        return 0
-    table = csr.n_cols * d * 4
+    table = csr.n_cols * min(d, 128) * 4  # a blocked hop runs wider rows as 128-column passes
     if table < SPMM_BLOCK_MIN_BYTES:
         return 0
     return max(2, min(SPMM_BLOCK_MAX, round(table / SPMM_BLOCK_BYTES)))

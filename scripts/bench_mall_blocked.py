@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--dim", type=int, default=64)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--blocks", default="2,4,8,10,16")
+    ap.add_argument("--pass-cols", type=int, default=0,
+                    help="HGD_TUNE_SPMM_PASS_COLS for every variant (0 = the default passes)")
     args = ap.parse_args()
 
     import torch
@@ -38,6 +40,8 @@ def main():
     from hypergraph_diffusion_for_recommendation_amd import Incidence
     from hypergraph_diffusion_for_recommendation_amd.incidence import spmm_csr
 
+    from hypergraph_diffusion_for_recommendation_amd import _native as nat
+    nat.check(nat.load().hgd_set_tuning(3, args.pass_cols), "pass cols")
     dev = torch.device("cuda:0")
     U, I, d = args.users, args.items, args.dim
     idx = bench.make_graph(U, I, args.edges, 0, None, dev)
@@ -58,7 +62,7 @@ def main():
         return spmm_csr(inc.csc, X, val=w_full, row_scale=q)
 
     ref = run(0)
-    res = {"dim": d, "nnz": nnz, "bytes_algorithmic": nnz * (4 + 4 * d) + I * (4 * d + 4)
+    res = {"dim": d, "pass_cols": args.pass_cols, "nnz": nnz, "bytes_algorithmic": nnz * (4 + 4 * d) + I * (4 * d + 4)
            + (I + 1) * 4, "variants": {}}
     times = {"plain": []}
     times.update({P: [] for P in blocks})

@@ -24,9 +24,10 @@ def test_size_rule_follows_the_gathered_table():
     # the bench's hop into items gathers the 10 M-row user table
     assert spmm_blocks(_csr(1_000_000, 10_000_000), 64) == 4     # 2.56 GB
     assert spmm_blocks(_csr(1_000_000, 10_000_000), 128) == 8    # 5.12 GB
-    # rows wider than 128 (64-column passes) measured no gain: never blocked by the size rule
-    assert spmm_blocks(_csr(1_000_000, 10_000_000), 256) == 0
-    assert spmm_blocks(_csr(1_000_000, 10_000_000), 129) == 0
+    # rows wider than 128 run blocked as 128-column passes: the table of one pass decides
+    assert spmm_blocks(_csr(1_000_000, 10_000_000), 256) == 8
+    assert spmm_blocks(_csr(1_000_000, 10_000_000), 1024) == 8
+    assert spmm_blocks(_csr(1_000_000, 2_000_000), 256) == 0  # 1.02 GB < 1 GiB
     assert spmm_blocks(_csr(1_000_000, 100_000_000), 64) == 16  # clamped
     # the hop into users gathers the 256 MB item table: one pass
     assert spmm_blocks(_csr(10_000_000, 1_000_000), 64) == 0
