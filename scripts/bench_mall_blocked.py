@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--dim", type=int, default=64)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--blocks", default="2,4,8,10,16")
+    ap.add_argument("--hop", choices=("items", "users"), default="items",
+                    help="items: Hᵀ·X over the CSC (gathers the user table); users: H·M over the "
+                         "CSR (gathers the item table)")
     ap.add_argument("--pass-cols", type=int, default=0,
                     help="HGD_TUNE_SPMM_PASS_COLS for every variant (0 = the default passes)")
     args = ap.parse_args()
@@ -48,22 +51,35 @@ def main():
     inc = Incidence.from_coo(idx, None, (U, I), device=dev, validate=False, rows_sorted=True)
     del idx
     nnz = inc.nnz
-    X = torch.randn(U, d, device=dev)
-    q = inc.scale("col", "mean")
-    w_full = inc.edge_values("csc", "sym")
+    if args.hop == "items":
+        S, R = inc.csc, I
+        X = torch.randn(U, d, device=dev)
+        q = inc.scale("col", "mean")
+        w_full = inc.edge_values("csc", "sym")
+    else:
+        # make_graph's COO is sorted by (user, item): every CSR row's columns ascend
+        S, R = inc.csr, U
+        rows = torch.repeat_interleave(torch.arange(U, device=dev), S.degrees())
+        same = rows[1:] == rows[:-1]
+        assert bool((S.col[1:][same] >= S.col[:-1][same]).all()), "CSR columns not ascending"
+        del rows, same
+        S.cols_ascending = True
+        X = torch.randn(I, d, device=dev)
+        q = inc.scale("row", "sym")
+        w_full = None
     blocks = [int(p) for p in args.blocks.split(",")]
     for P in blocks:  # block-major copies built outside the timed rounds
-        inc.csc.col_blocks(P)
-        inc.csc.blocked_values(P, w_full)
+        S.col_blocks(P)
+        S.blocked_values(P, w_full)
 
     def run(P):
-        # HGD_SPMM_BLOCKS=0: hgd_spmm; =P: hgd_spmm_blocked over P user ranges (spmm_blocks)
+        # HGD_SPMM_BLOCKS=0: hgd_spmm; =P: hgd_spmm_blocked over P source ranges (spmm_blocks)
         os.environ["HGD_SPMM_BLOCKS"] = str(P)
-        return spmm_csr(inc.csc, X, val=w_full, row_scale=q)
+        return spmm_csr(S, X, val=w_full, row_scale=q)
 
     ref = run(0)
-    res = {"dim": d, "pass_cols": args.pass_cols, "nnz": nnz, "bytes_algorithmic": nnz * (4 + 4 * d) + I * (4 * d + 4)
-           + (I + 1) * 4, "variants": {}}
+    res = {"dim": d, "hop": args.hop, "pass_cols": args.pass_cols, "nnz": nnz,
+           "bytes_algorithmic": nnz * (4 + 4 * d) + R * (4 * d + 4) + (R + 1) * 4, "variants": {}}
     times = {"plain": []}
     times.update({P: [] for P in blocks})
     diffs = {}
