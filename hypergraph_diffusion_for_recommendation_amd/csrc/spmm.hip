@@ -682,12 +682,15 @@ void launch_tuned(const SpmmArgs& a, bool has_val, bool seg, int64_t blocks, hip
   } else if constexpr (EX) {
     launch_kernel<G, VEC, 8, kDefaultPolicy, true>(a, has_val, seg, blocks, st);
   } else if constexpr (G == 16 && VEC == 4) {
-    // the d = 64 path carries the tuning matrix (unroll × {plain, nt-store, prefetch, both})
+    // the d = 64 path carries the tuning matrix (unroll × {plain, nt-store, prefetch, both,
+    // prefetch + nt-index, prefetch + nt-index + nt-store})
 #define HGD_POL_CASES(U)                                                            \
     switch (g_policy) {                                                             \
       case 0: return launch_kernel<G, VEC, U, 0>(a, has_val, seg, blocks, st);      \
       case 1: return launch_kernel<G, VEC, U, 1>(a, has_val, seg, blocks, st);      \
       case 9: return launch_kernel<G, VEC, U, 9>(a, has_val, seg, blocks, st);      \
+      case 10: return launch_kernel<G, VEC, U, 10>(a, has_val, seg, blocks, st);    \
+      case 11: return launch_kernel<G, VEC, U, 11>(a, has_val, seg, blocks, st);    \
       default: return launch_kernel<G, VEC, U, 8>(a, has_val, seg, blocks, st);     \
     }
     if (g_unroll >= 16) { HGD_POL_CASES(16) }
@@ -1093,8 +1096,9 @@ extern "C" hgd_status hgd_set_tuning(int32_t key, int32_t value) {
       g_unroll = value;
       return HGD_OK;
     case HGD_TUNE_SPMM_POLICY:
-      HGD_REQUIRE(value == 0 || value == 1 || value == 8 || value == 9,
-                  "hgd_set_tuning: policy must be 0, 1 (nt stores), 8 (index prefetch) or 9");
+      HGD_REQUIRE(value == 0 || value == 1 || (value >= 8 && value <= 11),
+                  "hgd_set_tuning: policy must be 0, 1 (nt stores), 8 (index prefetch), 9, 10 "
+                  "(prefetch + nt index loads) or 11");
       g_policy = value;
       return HGD_OK;
     case HGD_TUNE_SPMM_PASS_COLS:

@@ -59,7 +59,8 @@ typedef enum hgd_epilogue {
 /* Tuning knobs of the SpMM hop (process-wide; defaults are the measured best on MI355X).
  *   HGD_TUNE_SPMM_UNROLL: independent row gathers in flight per lane (8 or 16)
  *   HGD_TUNE_SPMM_POLICY: 0 plain, 1 non-temporal Y stores, 8 software-pipelined index
- *                         batches (default), 9 both
+ *                         batches (default), 9 both, 10 prefetch + non-temporal index/weight
+ *                         loads, 11 all three (d = 64 float4 path only)
  *   HGD_TUNE_SPMM_PASS_COLS: widest column pass of a hop without a fused row epilogue
  *                         (64, 128 or 256 fp32 columns; wider rows run as several passes;
  *                         0 = auto, the default: one pass up to 128 columns, else 64)
