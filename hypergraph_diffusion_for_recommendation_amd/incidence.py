@@ -192,14 +192,18 @@ class CSR:
         every hop; the last few are kept."""
         if val is None:
             return None
+        try:
+            version = val._version
+        except RuntimeError:  # an inference tensor tracks no version: gathered every call
+            return _gather32(val, self.col_blocks(n_blocks)[2])
         key = (n_blocks, id(val))
         hit = self._blk_vals.get(key)
-        if hit is not None and hit[0]() is val and hit[1] == val._version:
+        if hit is not None and hit[0]() is val and hit[1] == version:
             return hit[2]
         bval = _gather32(val, self.col_blocks(n_blocks)[2])
         if len(self._blk_vals) >= 4:
             self._blk_vals.pop(next(iter(self._blk_vals)))
-        self._blk_vals[key] = (weakref.ref(val), val._version, bval)
+        self._blk_vals[key] = (weakref.ref(val), version, bval)
         return bval
 
     @property

@@ -327,6 +327,9 @@ def test_spmm_one_block_is_bitwise_the_plain_hop(dev, d):
     v2.mul_(2.0)  # modified in place: gathered again
     b2 = csc.blocked_values(1, v2)
     assert b2 is not b1 and torch.equal(b2, 2.0 * bval)
+    with torch.inference_mode():  # no version counter: gathered every call, still right
+        v3 = inc.val_t * 3.0
+        assert torch.equal(csc.blocked_values(1, v3), 3.0 * bval)
 
 
 def test_spmm_blocked_two_hop_fwd_bwd(dev, monkeypatch):
