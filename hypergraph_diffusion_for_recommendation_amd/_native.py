@@ -443,7 +443,7 @@ def load() -> ctypes.CDLL:
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        # optional process-wide tuning overrides (hgd_set_tuning keys 1 .. 17)
+        # optional process-wide tuning overrides (hgd_set_tuning keys 1 .. 18)
         for key, env in ((1, "HGD_SPMM_UNROLL"), (2, "HGD_SPMM_POLICY"),
                          (3, "HGD_SPMM_PASS_COLS"), (4, "HGD_ROWGEMM_BLOCKS"),
                          (5, "HGD_SPLITK_ROWS"), (6, "HGD_GEMM_EXACT"),
@@ -451,7 +451,7 @@ def load() -> ctypes.CDLL:
                          (10, "HGD_P2P_SEGMENT_MB"), (11, "HGD_P2P_CACHED"),
                          (12, "HGD_CPU_RNG_THREADS"), (13, "HGD_X3P_QUEUE"),
                          (14, "HGD_P2P_GRID"), (15, "HGD_MASK_PAIR"), (16, "HGD_MASK_DIV"),
-                         (17, "HGD_SPMM_PASS_INTERLEAVE")):
+                         (17, "HGD_SPMM_PASS_INTERLEAVE"), (18, "HGD_SPMM_BLOCKED_SEG")):
             if os.environ.get(env):
                 st = lib.hgd_set_tuning(key, int(os.environ[env]))
                 if st != HGD_OK:

@@ -63,13 +63,9 @@ struct SpmmArgs {
   // wide row in ONE launch, the passes of a row block on consecutive workgroups of the same XCD
   int32_t n_pass;     // > 1: interleaved; else the launch covers the one pass at col0
   int32_t pass_cols;  // columns per pass when interleaved
-  // source-blocked hop (hgd_spmm_blocked): col / val are the block-major copy of the structure
-  // (hgd_spmm_col_blocks) and this launch sums, for every row r, its nonzeros of source block
-  // blk, blk_seg[blk·blk_rows + r] .. blk_seg[blk·blk_rows + r + 1]; with blk_accum it adds s·Σ
-  // to the Y row the blocks before it wrote
-  const int64_t* blk_seg;
-  int64_t blk_rows;
-  int32_t blk;
+  // source-blocked hop (hgd_spmm_blocked): a launch per source block k over the block-major
+  // copy (hgd_spmm_col_blocks), whose rows of block k are a CSR of their own (rowptr =
+  // blk_start + k·n_rows); with blk_accum the row adds s·Σ to the Y row the blocks before wrote
   int32_t blk_accum;
 };
 
@@ -461,16 +457,9 @@ __global__ __launch_bounds__(kBlock) void spmm_kernel(SpmmArgs a) {
 
   const int64_t r = a.row_begin + bid * GPB + g;
   if (r >= a.row_end) return;
-  int64_t e0, e1;
-  if (a.blk_seg) {  // source-blocked hop: this block's nonzeros of the row (no split rows)
-    const int64_t* sp = a.blk_seg + a.blk * a.blk_rows + r;
-    e0 = sp[0];
-    e1 = sp[1];
-  } else {
-    e0 = a.rowptr[r];
-    e1 = a.rowptr[r + 1];
-    if (a.heavy_threshold > 0 && e1 - e0 > a.heavy_threshold) return;  // split-plan row
-  }
+  const int64_t e0 = a.rowptr[r];
+  const int64_t e1 = a.rowptr[r + 1];
+  if (a.heavy_threshold > 0 && e1 - e0 > a.heavy_threshold) return;  // split-plan row
   masked_or_plain_sum<G, VEC, U, HAS_VAL, POL, MASK>(a, e0, e1, l, col_ok, acc, col0);
   const float s = a.row_scale ? a.row_scale[r] : 1.f;
   finish_row<G, VEC, EX, (POL & kPolNtStore) != 0>(a, r, s, l, coff, col_ok, acc);
@@ -642,6 +631,9 @@ int g_pass_cols = 0;
 // HGD_TUNE_SPMM_PASS_INTERLEAVE: 1 = a wide row's column passes as ONE launch, interleaved so the
 // passes of a row block run back to back on one XCD (see spmm_kernel); 0 = a launch per pass
 int g_pass_interleave = 0;
+// HGD_TUNE_SPMM_BLOCKED_SEG: 1 = the source-blocked hop walks each block's short rows with the
+// segmented kernel (a group owns G consecutive rows as one nonzero stream); 0 = a row per group
+int g_blocked_seg = 0;
 
 template <int G, int VEC, int U, int POL, bool EX = false>
 void launch_kernel(const SpmmArgs& a, bool has_val, bool seg, int64_t blocks, hipStream_t st) {
@@ -765,7 +757,8 @@ hgd_status spmm_impl(const int64_t* rowptr, const int32_t* col, const float* val
                      const uint8_t* mask, float keep, const hgd_split_plan* plan,
                      void* workspace, size_t workspace_bytes, void* stream, const char* fn,
                      const int64_t* blk_seg = nullptr, int32_t n_blk = 0) {
-  // blk_seg (hgd_spmm_blocked): rowptr is unused, col / val are the block-major arrays
+  // blk_seg (hgd_spmm_blocked): the block-major blk_start (rowptr is the same pointer), col / val
+  // the block-major arrays
   HGD_REQUIRE(d > 0, "%s: d must be > 0 (got %d)", fn, d);
   HGD_REQUIRE(n_rows >= 0 && n_src_rows >= 0, "%s: negative sizes", fn);
   HGD_REQUIRE(row_begin >= 0 && row_begin <= row_end && row_end <= n_rows,
@@ -864,9 +857,8 @@ hgd_status spmm_impl(const int64_t* rowptr, const int32_t* col, const float* val
       for (int c0 = 0; c0 < d; c0 += 4 * G) {
         a.col0 = c0;
         for (int k = 0; k < n_blk; ++k) {
-          a.blk_seg = blk_seg;
-          a.blk_rows = n_rows;
-          a.blk = k;
+          a.rowptr = blk_seg + static_cast<int64_t>(k) * n_rows;  // block k's own CSR
+          a.seg = g_blocked_seg;
           a.blk_accum = k > 0;
           a.epi = k + 1 == n_blk ? epilogue : HGD_EPI_NONE;  // the activation after the last
           hgd_status s = launch_vec<4>(G, a, has_val, st);
@@ -893,9 +885,7 @@ hgd_status spmm_impl(const int64_t* rowptr, const int32_t* col, const float* val
       a.col0 = c0;
       for (int k = 0; k < (blk_seg ? n_blk : 1); ++k) {
         if (blk_seg) {
-          a.blk_seg = blk_seg;
-          a.blk_rows = n_rows;
-          a.blk = k;
+          a.rowptr = blk_seg + static_cast<int64_t>(k) * n_rows;
           a.blk_accum = k > 0;
           a.epi = k + 1 == n_blk ? epilogue : HGD_EPI_NONE;
         }
@@ -1162,6 +1152,10 @@ extern "C" hgd_status hgd_set_tuning(int32_t key, int32_t value) {
     case HGD_TUNE_SPMM_PASS_INTERLEAVE:
       HGD_REQUIRE(value == 0 || value == 1, "hgd_set_tuning: pass interleave must be 0 or 1");
       g_pass_interleave = value;
+      return HGD_OK;
+    case HGD_TUNE_SPMM_BLOCKED_SEG:
+      HGD_REQUIRE(value == 0 || value == 1, "hgd_set_tuning: blocked seg must be 0 or 1");
+      g_blocked_seg = value;
       return HGD_OK;
     case HGD_TUNE_CPU_RNG_THREADS:
       HGD_REQUIRE(value >= 0 && value <= 64, "hgd_set_tuning: cpu rng threads must be 0..64");

@@ -113,7 +113,10 @@ typedef enum hgd_epilogue {
  *   HGD_TUNE_SPMM_PASS_INTERLEAVE: rows wider than one column pass (d > 128 by default, unfused,
  *                         no split rows): 0 = one launch per pass; 1 = all passes in one launch,
  *                         a row block's passes on consecutive workgroups of one XCD (the same
- *                         bits either way) */
+ *                         bits either way)
+ *   HGD_TUNE_SPMM_BLOCKED_SEG: hgd_spmm_blocked walks each source block's (short) rows with
+ *                         0 = a lane group per row (default), 1 = the segmented kernel (a group
+ *                         owns G consecutive rows as one nonzero stream; the same bits) */
 typedef enum hgd_tune_key {
   HGD_TUNE_SPMM_UNROLL = 1,
   HGD_TUNE_SPMM_POLICY = 2,
@@ -131,7 +134,8 @@ typedef enum hgd_tune_key {
   HGD_TUNE_P2P_GRID = 14,
   HGD_TUNE_MASK_PAIR = 15,
   HGD_TUNE_MASK_DIV = 16,
-  HGD_TUNE_SPMM_PASS_INTERLEAVE = 17
+  HGD_TUNE_SPMM_PASS_INTERLEAVE = 17,
+  HGD_TUNE_SPMM_BLOCKED_SEG = 18
 } hgd_tune_key;
 hgd_status hgd_set_tuning(int32_t key, int32_t value);
 

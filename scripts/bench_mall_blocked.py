@@ -35,6 +35,8 @@ def main():
                          "CSR (gathers the item table)")
     ap.add_argument("--policy", type=int, default=8,
                     help="HGD_TUNE_SPMM_POLICY for every variant (8 = the default)")
+    ap.add_argument("--seg", type=int, default=0,
+                    help="HGD_TUNE_SPMM_BLOCKED_SEG for the blocked variants (1 = segmented walk)")
     ap.add_argument("--pass-cols", type=int, default=0,
                     help="HGD_TUNE_SPMM_PASS_COLS for every variant (0 = the default passes)")
     args = ap.parse_args()
@@ -48,6 +50,7 @@ def main():
     from hypergraph_diffusion_for_recommendation_amd import _native as nat
     nat.check(nat.load().hgd_set_tuning(3, args.pass_cols), "pass cols")
     nat.check(nat.load().hgd_set_tuning(2, args.policy), "policy")
+    nat.check(nat.load().hgd_set_tuning(18, args.seg), "blocked seg")
     dev = torch.device("cuda:0")
     U, I, d = args.users, args.items, args.dim
     idx = bench.make_graph(U, I, args.edges, 0, None, dev)
@@ -81,7 +84,7 @@ def main():
         return spmm_csr(S, X, val=w_full, row_scale=q)
 
     ref = run(0)
-    res = {"dim": d, "hop": args.hop, "pass_cols": args.pass_cols, "policy": args.policy, "nnz": nnz,
+    res = {"dim": d, "hop": args.hop, "pass_cols": args.pass_cols, "policy": args.policy, "seg": args.seg, "nnz": nnz,
            "bytes_algorithmic": nnz * (4 + 4 * d) + R * (4 * d + 4) + (R + 1) * 4, "variants": {}}
     times = {"plain": []}
     times.update({P: [] for P in blocks})

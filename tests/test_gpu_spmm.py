@@ -354,3 +354,30 @@ def test_spmm_blocked_two_hop_fwd_bwd(dev, monkeypatch):
     ref = O.two_hop(r, c, None, (U, I), Xn, P="sym", Q="mean", R="sym")
     mag = O.two_hop(r, c, None, (U, I), np.abs(Xn), P="sym", Q="mean", R="sym")
     assert_close(Y.detach().cpu().numpy(), ref, mag, what="blocked hgconv2")
+
+
+@pytest.mark.parametrize("d", [16, 64, 128, 256])
+@pytest.mark.parametrize("n_blocks", [2, 5])
+def test_spmm_blocked_segmented_walk_is_bitwise_the_row_walk(dev, monkeypatch, d, n_blocks):
+    """HGD_TUNE_SPMM_BLOCKED_SEG: each source block's short rows walked by the segmented kernel
+    sum the same nonzeros in the same order as a lane group per row — bitwise equal, over a row
+    range with weights, row scales and the activation."""
+    from hypergraph_diffusion_for_recommendation_amd import _native as nat
+    from hypergraph_diffusion_for_recommendation_amd import spmm_csr
+    lib = nat.load()
+    monkeypatch.setenv("HGD_SPMM_BLOCKS", str(n_blocks))
+    rng, r, c, vals, inc = _blocked_case(dev, 500 + d + n_blocks)
+    X = torch.from_numpy(rng.standard_normal((2001, d)).astype(np.float32)).to(dev)
+    q = torch.from_numpy(rng.random(613).astype(np.float32)).to(dev)
+    outs = []
+    try:
+        for seg in (0, 1):
+            nat.check(lib.hgd_set_tuning(18, seg), "blocked seg")
+            Y = torch.full((613, d), float("nan"), device=dev)
+            spmm_csr(inc.csc, X, val=inc.val_t, row_scale=q, out=Y, row_begin=5, row_end=601,
+                     epilogue=nat.EPI_LEAKY_RELU, slope=0.2)
+            outs.append(Y)
+    finally:
+        nat.check(lib.hgd_set_tuning(18, 0), "blocked seg off")
+    assert torch.equal(outs[0][5:601], outs[1][5:601])
+    assert bool(outs[1][:5].isnan().all()) and bool(outs[1][601:].isnan().all())
