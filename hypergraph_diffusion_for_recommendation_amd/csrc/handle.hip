@@ -382,7 +382,7 @@ int32_t csc_blocks(const hgd_incidence* o, int32_t d) {
   double p = std::floor(x);  // Python's round(): half to even
   const double frac = x - p;
   if (frac > 0.5 || (frac == 0.5 && std::fmod(p, 2.0) != 0.0)) p += 1.0;
-  return static_cast<int32_t>(std::min(16.0, std::max(2.0, p)));
+  return static_cast<int32_t>(std::min(16.0, std::max(4.0, p)));
 }
 
 // The block-major copy for P blocks and the CSC weights `w` of source kind k in its order.

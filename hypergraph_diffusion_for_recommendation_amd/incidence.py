@@ -33,9 +33,10 @@ SPLIT_THRESHOLD_MIN = 128
 SPLIT_NNZ_PER_THRESHOLD = 8192
 SEGMENTED_MAX_AVG_DEGREE = 32
 # source-blocked hop (hgd_spmm_blocked): a gathered table of at least SPMM_BLOCK_MIN_BYTES is
-# cut into about one block per SPMM_BLOCK_BYTES (2..16 blocks), see spmm_blocks()
+# cut into about one block per SPMM_BLOCK_BYTES (4..16 blocks), see spmm_blocks()
 SPMM_BLOCK_MIN_BYTES = 1 << 30
 SPMM_BLOCK_BYTES = 640 << 20
+SPMM_BLOCK_MIN = 4
 SPMM_BLOCK_MAX = 16
 # lane-group tasks needed to fill MI355X: 256 CUs × 16 waves × 4 groups of 16 lanes (d = 64)
 TARGET_GROUPS = 16384
@@ -189,7 +190,7 @@ class CSR:
         """``val`` (per-nonzero weights in this structure's order) gathered into the block-major
         order of :meth:`col_blocks`. Cached per tensor while it is alive and unmodified (its
         version counter), e.g. the cached ``Incidence.edge_values`` a training step passes to
-        every hop; the last few are kept."""
+        every hop; the last 8 are kept."""
         if val is None:
             return None
         try:
@@ -201,7 +202,7 @@ class CSR:
         if hit is not None and hit[0]() is val and hit[1] == version:
             return hit[2]
         bval = _gather32(val, self.col_blocks(n_blocks)[2])
-        if len(self._blk_vals) >= 4:
+        if len(self._blk_vals) >= 8:
             self._blk_vals.pop(next(iter(self._blk_vals)))
         self._blk_vals[key] = (weakref.ref(val), version, bval)
         return bval
@@ -224,8 +225,8 @@ def spmm_blocks(csr: CSR, d: int) -> int:
     and sums a row's nonzeros of one range per pass, so each pass gathers from a slice 1/P as
     large, for P−1 extra read+write passes over Y. Measured on MI355X at 10 M users × 1 M items
     × 100 M edges (scripts/bench_mall_blocked.py): d = 64 −13 % at P = 4,
-    d = 128 −7 % at P = 8; hence about one block per 640 MiB of the table a pass gathers from,
-    from 1 GiB. A blocked hop runs rows wider than 128 as 128-column passes (d = 256: −6 % at
+    d = 128 −7 % at P = 8, d = 32 −4 % at P = 4 (−1 % at P = 2); hence about one block per
+    640 MiB of the table a pass gathers from, at least 4, from 1 GiB. A blocked hop runs rows wider than 128 as 128-column passes (d = 256: −6 % at
     P = 8; in the plain hop's 64-column passes blocking gained nothing, 256 B gathered from
     every 1 KB row).
 
@@ -243,7 +244,7 @@ def spmm_blocks(csr: CSR, d: int) -> int:
     table = csr.n_cols * min(d, 128) * 4  # a blocked hop runs wider rows as 128-column passes
     if table < SPMM_BLOCK_MIN_BYTES:
         return 0
-    return max(2, min(SPMM_BLOCK_MAX, round(table / SPMM_BLOCK_BYTES)))
+    return max(SPMM_BLOCK_MIN, min(SPMM_BLOCK_MAX, round(table / SPMM_BLOCK_BYTES)))
 
 
 def spmm_csr(csr: CSR, X: torch.Tensor, val: Optional[torch.Tensor] = None,

@@ -33,7 +33,8 @@ def test_size_rule_follows_the_gathered_table():
     assert spmm_blocks(_csr(10_000_000, 1_000_000), 64) == 0
     # just below / at the 1 GiB floor
     assert spmm_blocks(_csr(10, (1 << 30) // 256 - 1), 64) == 0
-    assert spmm_blocks(_csr(10, (1 << 30) // 256), 64) == 2
+    assert spmm_blocks(_csr(10, (1 << 30) // 256), 64) == 4  # at least 4 blocks
+    assert spmm_blocks(_csr(1_000_000, 10_000_000), 32) == 4   # 1.28 GB: measured best at 4
 
 
 def test_only_for_ascending_unsplit_plain_structures(monkeypatch):
