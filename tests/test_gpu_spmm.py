@@ -381,3 +381,38 @@ def test_spmm_blocked_segmented_walk_is_bitwise_the_row_walk(dev, monkeypatch, d
         nat.check(lib.hgd_set_tuning(18, 0), "blocked seg off")
     assert torch.equal(outs[0][5:601], outs[1][5:601])
     assert bool(outs[1][:5].isnan().all()) and bool(outs[1][601:].isnan().all())
+
+
+def test_spmm_blocked_two_hop_replays_in_a_hip_graph(dev, monkeypatch):
+    """bench.py --graph on's pattern with the blocked hop into items: eager warm-up steps (they
+    build the block-major copy and the blocked weights), then fwd + autograd bwd captured in one
+    HIP graph; every replay is bitwise the eager step."""
+    from hypergraph_diffusion_for_recommendation_amd import hgconv2
+    monkeypatch.setenv("HGD_SPMM_BLOCKS", "4")
+    rng = np.random.default_rng(321)
+    U, I, d = 5000, 700, 64
+    r, c = random_coo(rng, U, I, 60000)
+    inc = _build(r, c, None, (U, I), dev, split_threshold=0)
+    X = torch.from_numpy(rng.standard_normal((U, d)).astype(np.float32)).to(dev)
+    dY = torch.from_numpy(rng.standard_normal((U, d)).astype(np.float32)).to(dev)
+    X.requires_grad_(True)
+
+    def step():
+        Y = hgconv2(inc, X)
+        (dX,) = torch.autograd.grad(Y, X, dY)
+        return Y, dX
+
+    Y0, dX0 = step()
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        for _ in range(2):
+            step()
+    torch.cuda.current_stream(dev).wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        Yg, dXg = step()
+    for _ in range(3):
+        graph.replay()
+        torch.cuda.synchronize(dev)
+        assert torch.equal(Yg, Y0.detach()) and torch.equal(dXg, dX0)
