@@ -703,8 +703,13 @@ def main():
             for _ in range(3):
                 eager_step()
         torch.cuda.current_stream(device).wait_stream(side)
+        import gc
+        gc.collect()  # no eager autograd graph (its nodes bound to another stream) may survive
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        # thread-local capture: the autograd engine runs the backward on its device thread, and
+        # under this build's default ("global") mode the capture then ends in a crash
+        # (scripts/diag/diag_graph_capture.py: torch ops alone crash the same way)
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             static_out = eager_step()
 
         def step():

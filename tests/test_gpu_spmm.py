@@ -3,6 +3,8 @@
 Every case goes through the C ABI (libhgd.so via ctypes). Tolerance: |got - ref| <= 1e-5·Σ|terms|
 element-wise (tests/_util.py).
 """
+import gc
+
 import numpy as np
 import pytest
 import torch
@@ -403,16 +405,19 @@ def test_spmm_blocked_two_hop_replays_in_a_hip_graph(dev, monkeypatch):
         return Y, dX
 
     Y0, dX0 = step()
+    Y0 = Y0.detach()  # an eager output holding its autograd graph would break the capture
     side = torch.cuda.Stream(dev)
     side.wait_stream(torch.cuda.current_stream(dev))
     with torch.cuda.stream(side):
         for _ in range(2):
             step()
     torch.cuda.current_stream(dev).wait_stream(side)
+    gc.collect()
     graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
+    # thread-local, as bench.py: autograd's device thread runs the backward during the capture
+    with torch.cuda.graph(graph, capture_error_mode="thread_local"):
         Yg, dXg = step()
     for _ in range(3):
         graph.replay()
         torch.cuda.synchronize(dev)
-        assert torch.equal(Yg, Y0.detach()) and torch.equal(dXg, dX0)
+        assert torch.equal(Yg, Y0) and torch.equal(dXg, dX0)
