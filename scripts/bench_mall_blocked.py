@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--hop", choices=("items", "users"), default="items",
                     help="items: Hᵀ·X over the CSC (gathers the user table); users: H·M over the "
                          "CSR (gathers the item table)")
+    ap.add_argument("--unroll", type=int, default=8,
+                    help="HGD_TUNE_SPMM_UNROLL for every variant (gathers in flight per lane)")
     ap.add_argument("--policy", type=int, default=8,
                     help="HGD_TUNE_SPMM_POLICY for every variant (8 = the default)")
     ap.add_argument("--seg", type=int, default=0,
@@ -50,6 +52,7 @@ def main():
     from hypergraph_diffusion_for_recommendation_amd import _native as nat
     nat.check(nat.load().hgd_set_tuning(3, args.pass_cols), "pass cols")
     nat.check(nat.load().hgd_set_tuning(2, args.policy), "policy")
+    nat.check(nat.load().hgd_set_tuning(1, args.unroll), "unroll")
     nat.check(nat.load().hgd_set_tuning(18, args.seg), "blocked seg")
     dev = torch.device("cuda:0")
     U, I, d = args.users, args.items, args.dim
@@ -84,7 +87,7 @@ def main():
         return spmm_csr(S, X, val=w_full, row_scale=q)
 
     ref = run(0)
-    res = {"dim": d, "hop": args.hop, "pass_cols": args.pass_cols, "policy": args.policy, "seg": args.seg, "nnz": nnz,
+    res = {"dim": d, "hop": args.hop, "pass_cols": args.pass_cols, "policy": args.policy, "unroll": args.unroll, "seg": args.seg, "nnz": nnz,
            "bytes_algorithmic": nnz * (4 + 4 * d) + R * (4 * d + 4) + (R + 1) * 4, "variants": {}}
     times = {"plain": []}
     times.update({P: [] for P in blocks})
