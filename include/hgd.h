@@ -12,6 +12,9 @@
  *                                                               model/graph/HGCN.py:173-175,
  *                            torch_scatter.scatter(.., 'mean')  model/layers/layers2/EquivSetConv2.py:88-93
  *                            (row_scale = 1/count is the scatter-mean; val = per-nonzero weight)
+ *   hgd_spmm_blocked         the same torch.sparse.mm(adj.t(), X) hop for a gathered table larger
+ *                            than the Infinity Cache (source-blocked; hgd_spmm_col_blocks builds
+ *                            its block-major copy of the CSC)
  *   hgd_sort_perm            COO→CSR / CSR→CSC ordering that cuSPARSE re-derives per call
  *                            (`adj.t()` in HGCNConv.forward, HGNN_HD4.py:459; coalesce in torch.sparse.mm)
  *   hgd_rowptr_from_sorted   row pointer of a row-sorted COO  base/torch_interface.py:8-12
