@@ -377,7 +377,8 @@ int32_t csc_blocks(const hgd_incidence* o, int32_t d) {
   }
   // a blocked hop runs rows wider than 128 as 128-column passes
   const double table = static_cast<double>(o->n_rows) * std::min<int32_t>(d, 128) * 4.0;
-  if (table < 1073741824.0) return 0;
+  if (table < 536870912.0) return 0;  // < 512 MiB: one pass
+  if (table < 1073741824.0) return 2;
   const double x = table / (640.0 * 1048576.0);
   double p = std::floor(x);  // Python's round(): half to even
   const double frac = x - p;
@@ -537,8 +538,9 @@ hgd_status two_hop_p2p(const hgd_incidence* o, int32_t Q, int32_t S_src, const f
     const int c0 = s * w, ws_ = std::min(w, d - c0);
     const int slot = parity * n_sl + s;
     float* send = hgd_p2p_slot(c->p2p, slot);
-    if (I > 0 && (r = csc_hop(o, S_src, wt, q, 0, I, X + c0, ldx, send, ws_, ws_, HGD_EPI_NONE,
-                              0.f, ws, wsb, st)) != HGD_OK)
+    // never source-blocked here: the send slot is uncached exchange memory (as sharded.py)
+    if (I > 0 && (r = hgd_spmm(o->colptr, o->row_t, wt, q, I, o->n_rows, 0, I, X + c0, ldx, send,
+                               ws_, ws_, HGD_EPI_NONE, 0.f, &o->plan[1], ws, wsb, st)) != HGD_OK)
       return r;
     HGD_HIP(hipEventRecord(c->ev[s], st));
     HGD_HIP(hipStreamWaitEvent(c->side, c->ev[s], 0));

@@ -32,8 +32,10 @@ DEFAULT_SPLIT_CHUNK = 512
 SPLIT_THRESHOLD_MIN = 128
 SPLIT_NNZ_PER_THRESHOLD = 8192
 SEGMENTED_MAX_AVG_DEGREE = 32
-# source-blocked hop (hgd_spmm_blocked): a gathered table of at least SPMM_BLOCK_MIN_BYTES is
-# cut into about one block per SPMM_BLOCK_BYTES (4..16 blocks), see spmm_blocks()
+# source-blocked hop (hgd_spmm_blocked): a gathered table of SPMM_BLOCK_TWO_BYTES up to
+# SPMM_BLOCK_MIN_BYTES runs in 2 blocks; from SPMM_BLOCK_MIN_BYTES, in about one block per
+# SPMM_BLOCK_BYTES (4..16 blocks), see spmm_blocks()
+SPMM_BLOCK_TWO_BYTES = 512 << 20
 SPMM_BLOCK_MIN_BYTES = 1 << 30
 SPMM_BLOCK_BYTES = 640 << 20
 SPMM_BLOCK_MIN = 4
@@ -226,7 +228,9 @@ def spmm_blocks(csr: CSR, d: int) -> int:
     large, for P−1 extra read+write passes over Y. Measured on MI355X at 10 M users × 1 M items
     × 100 M edges (scripts/bench_mall_blocked.py): d = 64 −13 % at P = 4,
     d = 128 −7 % at P = 8, d = 32 −4 % at P = 4 (−1 % at P = 2); hence about one block per
-    640 MiB of the table a pass gathers from, at least 4, from 1 GiB. A blocked hop runs rows wider than 128 as 128-column passes (d = 256: −6 % at
+    640 MiB of the table a pass gathers from, at least 4, from 1 GiB. Between 512 MiB and 1 GiB
+    two blocks: the 32-column slices of a 5 M-user shard (the sharded hop at N = 2, 640 MB)
+    −4 % at P = 2; a 320 MB table (N = 4) is 3 % slower blocked. A blocked hop runs rows wider than 128 as 128-column passes (d = 256: −6 % at
     P = 8; in the plain hop's 64-column passes blocking gained nothing, 256 B gathered from
     every 1 KB row).
 
@@ -242,8 +246,10 @@ def spmm_blocks(csr: CSR, d: int) -> int:
             raise ValueError(f"HGD_SPMM_BLOCKS must be 0..64, got {env!r}")
         return p if p > 1 else 0
     table = csr.n_cols * min(d, 128) * 4  # a blocked hop runs wider rows as 128-column passes
-    if table < SPMM_BLOCK_MIN_BYTES:
+    if table < SPMM_BLOCK_TWO_BYTES:
         return 0
+    if table < SPMM_BLOCK_MIN_BYTES:
+        return 2
     return max(SPMM_BLOCK_MIN, min(SPMM_BLOCK_MAX, round(table / SPMM_BLOCK_BYTES)))
 
 
@@ -251,11 +257,14 @@ def spmm_csr(csr: CSR, X: torch.Tensor, val: Optional[torch.Tensor] = None,
              row_scale: Optional[torch.Tensor] = None, epilogue: int = nat.EPI_NONE,
              slope: float = 0.0, out: Optional[torch.Tensor] = None,
              row_begin: int = 0, row_end: Optional[int] = None,
-             ex: Optional[nat.RowEpilogue] = None) -> torch.Tensor:
+             ex: Optional[nat.RowEpilogue] = None, blocks: Optional[int] = None) -> torch.Tensor:
     """``Y[r] = epi(row_scale[r] * Σ_e val[e] * X[col[e]])`` for r in [row_begin, row_end).
 
     With ``ex`` (an ``hgd_row_epilogue``) the call is ``hgd_spmm_fused``: ``ex.act``/``ex.slope``
-    replace ``epilogue``/``slope`` and the LayerNorm / residual epilogue runs in the store."""
+    replace ``epilogue``/``slope`` and the LayerNorm / residual epilogue runs in the store.
+    ``blocks``: None = :func:`spmm_blocks` decides whether the hop runs source-blocked
+    (hgd_spmm_blocked); 0 = never (e.g. into uncached exchange memory, which the blocked hop
+    would read back P−1 times)."""
     if X.dim() != 2:
         raise ValueError(f"spmm: X must be 2-D, got {tuple(X.shape)}")
     if X.dtype != torch.float32:
@@ -288,7 +297,10 @@ def spmm_csr(csr: CSR, X: torch.Tensor, val: Optional[torch.Tensor] = None,
     if timer is not None:
         t0 = timer.begin()
     mask = getattr(csr, "mask", None)
-    blocks = spmm_blocks(csr, d) if mask is None and ex is None else 0
+    if mask is not None or ex is not None or blocks == 0:
+        blocks = 0
+    else:
+        blocks = spmm_blocks(csr, d)
     if mask is not None and ex is not None:
         nat.check(lib.hgd_spmm_masked_fused(
             csr.rowptr.data_ptr(), csr.col.data_ptr() if csr.nnz else None, nat.ptr(val),

@@ -611,7 +611,9 @@ class ShardedIncidence:
             if use_p2p:
                 k = parity * len(sl) + s
                 send = ex.slot(k, inc.n_cols, w)
-                spmm_csr(inc.csc, Xs, val=val_t, row_scale=self.q, out=send)
+                # never source-blocked: the send slot is uncached exchange memory, which the
+                # blocked hop would read back once per extra block
+                spmm_csr(inc.csc, Xs, val=val_t, row_scale=self.q, out=send, blocks=0)
                 Ms = torch.empty((inc.n_cols, w), dtype=torch.float32, device=X.device)
                 ready = torch.cuda.Event()
                 ready.record(cur)

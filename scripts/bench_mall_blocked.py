@@ -33,6 +33,9 @@ def main():
     ap.add_argument("--hop", choices=("items", "users"), default="items",
                     help="items: Hᵀ·X over the CSC (gathers the user table); users: H·M over the "
                          "CSR (gathers the item table)")
+    ap.add_argument("--ld", type=int, default=0,
+                    help="row stride of X (0 = dim): a column slice of a wider table, as the "
+                         "sharded hop's 32-column slices of a d = 64 table")
     ap.add_argument("--unroll", type=int, default=8,
                     help="HGD_TUNE_SPMM_UNROLL for every variant (gathers in flight per lane)")
     ap.add_argument("--policy", type=int, default=8,
@@ -62,7 +65,7 @@ def main():
     nnz = inc.nnz
     if args.hop == "items":
         S, R = inc.csc, I
-        X = torch.randn(U, d, device=dev)
+        X = torch.randn(U, max(d, args.ld), device=dev)[:, :d]
         q = inc.scale("col", "mean")
         w_full = inc.edge_values("csc", "sym")
     else:
@@ -87,7 +90,7 @@ def main():
         return spmm_csr(S, X, val=w_full, row_scale=q)
 
     ref = run(0)
-    res = {"dim": d, "hop": args.hop, "pass_cols": args.pass_cols, "policy": args.policy, "unroll": args.unroll, "seg": args.seg, "nnz": nnz,
+    res = {"dim": d, "hop": args.hop, "pass_cols": args.pass_cols, "policy": args.policy, "unroll": args.unroll, "seg": args.seg, "ld": args.ld, "nnz": nnz,
            "bytes_algorithmic": nnz * (4 + 4 * d) + R * (4 * d + 4) + (R + 1) * 4, "variants": {}}
     times = {"plain": []}
     times.update({P: [] for P in blocks})

@@ -421,3 +421,17 @@ def test_spmm_blocked_two_hop_replays_in_a_hip_graph(dev, monkeypatch):
         graph.replay()
         torch.cuda.synchronize(dev)
         assert torch.equal(Yg, Y0) and torch.equal(dXg, dX0)
+
+
+def test_spmm_blocks_zero_keeps_the_plain_hop(dev, monkeypatch):
+    """``spmm_csr(..., blocks=0)`` (the sharded hop's uncached exchange slots) runs hgd_spmm even
+    where the rule (here forced by HGD_SPMM_BLOCKS) would block: bitwise the plain hop."""
+    from hypergraph_diffusion_for_recommendation_amd import spmm_csr
+    rng, r, c, vals, inc = _blocked_case(dev, 909)
+    X = torch.from_numpy(rng.standard_normal((2001, 64)).astype(np.float32)).to(dev)
+    monkeypatch.setenv("HGD_SPMM_BLOCKS", "0")
+    plain = spmm_csr(inc.csc, X, val=inc.val_t)
+    monkeypatch.setenv("HGD_SPMM_BLOCKS", "3")
+    blocked = spmm_csr(inc.csc, X, val=inc.val_t)
+    kept = spmm_csr(inc.csc, X, val=inc.val_t, blocks=0)
+    assert torch.equal(kept, plain) and not torch.equal(blocked, plain)

@@ -27,13 +27,19 @@ def test_size_rule_follows_the_gathered_table():
     # rows wider than 128 run blocked as 128-column passes: the table of one pass decides
     assert spmm_blocks(_csr(1_000_000, 10_000_000), 256) == 8
     assert spmm_blocks(_csr(1_000_000, 10_000_000), 1024) == 8
-    assert spmm_blocks(_csr(1_000_000, 2_000_000), 256) == 0  # 1.02 GB < 1 GiB
+    assert spmm_blocks(_csr(1_000_000, 2_000_000), 256) == 2  # 1.02 GB < 1 GiB
+    assert spmm_blocks(_csr(1_000_000, 1_000_000), 256) == 0  # 512 MB < 512 MiB
     assert spmm_blocks(_csr(1_000_000, 100_000_000), 64) == 16  # clamped
     # the hop into users gathers the 256 MB item table: one pass
     assert spmm_blocks(_csr(10_000_000, 1_000_000), 64) == 0
-    # just below / at the 1 GiB floor
-    assert spmm_blocks(_csr(10, (1 << 30) // 256 - 1), 64) == 0
+    # the 512 MiB and 1 GiB steps
+    assert spmm_blocks(_csr(10, (1 << 29) // 256 - 1), 64) == 0
+    assert spmm_blocks(_csr(10, (1 << 29) // 256), 64) == 2
+    assert spmm_blocks(_csr(10, (1 << 30) // 256 - 1), 64) == 2
     assert spmm_blocks(_csr(10, (1 << 30) // 256), 64) == 4  # at least 4 blocks
+    # the sharded hop's 32-column slices: a 5 M-user shard (N = 2) 2 blocks, 2.5 M (N = 4) none
+    assert spmm_blocks(_csr(1_000_000, 5_000_000), 32) == 2
+    assert spmm_blocks(_csr(1_000_000, 2_500_000), 32) == 0
     assert spmm_blocks(_csr(1_000_000, 10_000_000), 32) == 4   # 1.28 GB: measured best at 4
 
 
