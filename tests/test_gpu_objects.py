@@ -320,13 +320,19 @@ def test_create_rejects_malformed(dev):
     assert (Y == 0).all() and (M == 0).all()
 
 
-def test_one_rank_comm_matches_local(dev):
+@pytest.mark.parametrize("blocks", ["0", "3"])
+def test_one_rank_comm_matches_local(dev, monkeypatch, blocks):
     """hgd_comm over one rank: globalize leaves the item scales as they were (to rounding of
-    the float64 pow), chunked + all-reduced hop 1 equals the local conv."""
+    the float64 pow), chunked + all-reduced hop 1 equals the local conv — also with the
+    source-blocked hop forced (HGD_SPMM_BLOCKS=3: every chunk's rows blocked as the local
+    hop's, so still bitwise)."""
     nat, lib = _lib()
+    monkeypatch.setenv("HGD_SPMM_BLOCKS", blocks)
     rng = np.random.default_rng(9)
-    Nv, Ne, d = 800, 300, 64
-    r, c = random_coo(rng, Nv, Ne, 10000)
+    Nv, Ne, d = 3000, 800, 64
+    r, c = random_coo(rng, Nv, Ne, 20000)
+    # no CSC row above the auto split threshold (2·32 at this size): the blocked hop applies
+    assert np.bincount(c, minlength=Ne).max() <= 64
     rowptr, col, _, _ = _csr_of(r, c, Nv, dev)
     obj = _create(rowptr, col, None, Nv, Ne, dev)
     X = torch.randn(Nv, d, device=dev)
@@ -334,6 +340,11 @@ def test_one_rank_comm_matches_local(dev):
     Y0, M0, _, ws = _conv(obj, "sym", "mean", "sym", X, None, 0.0, dev)
     dX0 = _conv_bwd(obj, "sym", "mean", "sym", dY, None, None, 0.0, dev, ws)
     q0 = _dev_array(obj.scale(1, "mean"), Ne, torch.float32, dev)
+    if blocks != "0":  # the blocked hop was taken: its M differs from the plain hop's in bits
+        monkeypatch.setenv("HGD_SPMM_BLOCKS", "0")
+        _, Mp, _, _ = _conv(obj, "sym", "mean", "sym", X, None, 0.0, dev)
+        assert not torch.equal(Mp, M0)
+        monkeypatch.setenv("HGD_SPMM_BLOCKS", blocks)
     uid = ctypes.create_string_buffer(nat.COMM_ID_BYTES)
     nat.check(lib.hgd_comm_get_unique_id(uid), "unique id")
     comm = ctypes.c_void_p()
