@@ -893,12 +893,15 @@ def main():
     # hgd_spmm runs a row wider than 128 as 64-column passes, and the hop into items runs as
     # hgd_spmm_blocked (128-column passes) in `blocks` dispatches per pass when its gathered
     # user table exceeds the Infinity Cache (incidence.spmm_blocks)
+    # (N = 1 only: the sharded hop at N > 1 runs column slices, blocked by their own width,
+    # and never blocks into the peer exchange's slots)
     from hypergraph_diffusion_for_recommendation_amd.incidence import spmm_blocks
-    blocks = spmm_blocks(sh.inc.csc, args.dim)
+    blocks = spmm_blocks(sh.inc.csc, args.dim) if world == 1 else 0
     passes = 1 if args.dim <= 128 else -(-args.dim // 64)  # hgd_spmm's 64-column passes
     bpasses = -(-args.dim // 128)  # hgd_spmm_blocked's 128-column passes
-    roofline["dispatches_per_hop"] = {"into_items": bpasses * blocks if blocks else passes,
-                                      "into_users": passes}
+    if world == 1:
+        roofline["dispatches_per_hop"] = {"into_items": bpasses * blocks if blocks else passes,
+                                          "into_users": passes}
     if blocks:
         roofline["kernel"] = ("hgd::spmm_kernel (hgd_spmm hop; into items: hgd_spmm_blocked, "
                               f"{blocks} source blocks)")
