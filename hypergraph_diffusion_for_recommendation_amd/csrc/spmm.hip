@@ -1017,10 +1017,9 @@ extern "C" hgd_status hgd_spmm_col_blocks(const int64_t* rowptr, const int32_t* 
 
 extern "C" hgd_status hgd_spmm_blocked(const int64_t* blk_start, const int32_t* blk_col,
                                        const float* blk_val, const float* row_scale,
-                                       int64_t n_rows,
-                                       int64_t n_src_rows, int64_t row_begin, int64_t row_end,
-                                       const float* X, int64_t ldx, float* Y, int64_t ldy,
-                                       int32_t d, int32_t epilogue, float slope,
+                                       int64_t n_rows, int64_t n_src_rows, int64_t row_begin,
+                                       int64_t row_end, const float* X, int64_t ldx, float* Y,
+                                       int64_t ldy, int32_t d, int32_t epilogue, float slope,
                                        int32_t n_blocks, void* stream) {
   hgd::clear_error();
   HGD_REQUIRE(n_blocks >= 1 && n_blocks <= 64, "hgd_spmm_blocked: blocks must be 1..64");

@@ -209,7 +209,8 @@ hgd_status hgd_spmm(const int64_t* rowptr, const int32_t* col, const float* val,
  *              [blk_start[k·n_rows + r], blk_start[k·n_rows + r + 1]) of
  *   blk_col:   int32 [nnz], their columns, and
  *   blk_perm:  int32 [nnz] (may be NULL), their positions in the source structure — gather any
- *              per-nonzero weights through it (hgd_gather32) to get hgd_spmm_blocked's blk_val.
+ *              per-nonzero weights through it (hgd_gather32) to get hgd_spmm_blocked's blk_val
+ *              (int32 positions: nnz < 2^31, the library's limit for permutations, as perm_t).
  * Workspace: hgd_spmm_col_blocks_workspace_size.
  * ---------------------------------------------------------------------------------------- */
 size_t hgd_spmm_col_blocks_workspace_size(int64_t n_rows, int32_t n_blocks);
