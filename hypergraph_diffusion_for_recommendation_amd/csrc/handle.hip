@@ -415,7 +415,8 @@ hgd_status block_copy(const hgd_incidence* o, int32_t P, int32_t k, const float*
     const hipError_t e = hipStreamSynchronize(st);  // the workspace is freed here
     (void)hipFree(ws);
     if (r != HGD_OK) return r;
-    if (e != hipSuccess) return fail(HGD_ERR_HIP, "hgd_incidence block copy: %s", hipGetErrorString(e));
+    if (e != hipSuccess)
+      return fail(HGD_ERR_HIP, "hgd_incidence block copy: %s", hipGetErrorString(e));
     b->P = P;
     b->start = static_cast<int64_t*>(a);
     b->col = static_cast<int32_t*>(c);
