@@ -230,9 +230,9 @@ def spmm_blocks(csr: CSR, d: int) -> int:
     d = 128 −7 % at P = 8, d = 32 −4 % at P = 4 (−1 % at P = 2); hence about one block per
     640 MiB of the table a pass gathers from, at least 4, from 1 GiB. Between 512 MiB and 1 GiB
     two blocks: the 32-column slices of a 5 M-user shard (the sharded hop at N = 2, 640 MB)
-    −4 % at P = 2; a 320 MB table (N = 4) is 3 % slower blocked. A blocked hop runs rows wider than 128 as 128-column passes (d = 256: −6 % at
-    P = 8; in the plain hop's 64-column passes blocking gained nothing, 256 B gathered from
-    every 1 KB row).
+    −4 % at P = 2; a 320 MB table (N = 4) is 3 % slower blocked. A blocked hop runs rows wider
+    than 128 as 128-column passes (d = 256: −6 % at P = 8; in the plain hop's 64-column passes
+    blocking gained nothing, 256 B gathered from every 1 KB row).
 
     Only for a structure whose rows' columns ascend (the CSC of an Incidence), without split
     rows or the segmented walk. ``HGD_SPMM_BLOCKS``: ``0`` turns it off, an integer P forces P

@@ -4,11 +4,12 @@ of the 2.56 GB user table at random (5.9–6.4 TB/s, the random-gather ceiling),
 into-users hop, whose 256 MB item table the 256 MB Infinity Cache (MALL) mostly holds, runs at
 7.5 TB/s. Here the item hop is split into P phases, phase k summing only the neighbours in user
 block k (a CSC of H's rows [u_k, u_k+1)), so each phase gathers from a U/P-row slice of X that
-the MALL can hold; the phases accumulate into Y (Y = s·acc_k + Y). The price is P−1 extra read+write passes over Y.
-Round 6 first emulated this with one sub-CSC per block and the fused residual epilogue; it now
-times the library's hgd_spmm_blocked (one launch per block over the block-major copy of the CSC,
-hgd_spmm_col_blocks, selected through HGD_SPMM_BLOCKS) against hgd_spmm in interleaved rounds and reports
-the worst relative difference (a different fp32 summation order, so not bitwise).
+the MALL can hold; the phases accumulate into Y (Y = s·acc_k + Y). The price is P−1 extra
+read+write passes over Y. Round 6 first emulated this with one sub-CSC per block and the fused
+residual epilogue; it now times the library's hgd_spmm_blocked (one launch per block over the
+block-major copy of the CSC, hgd_spmm_col_blocks, selected through HGD_SPMM_BLOCKS) against
+hgd_spmm in interleaved rounds and reports the worst relative difference (a different fp32
+summation order, so not bitwise).
 
     python scripts/bench_mall_blocked.py [--dim 64 --rounds 5]
 """
