@@ -26,6 +26,9 @@ def main():
     ap.add_argument("--dim", type=int, default=64)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--blocks", default="2,4,8")
+    ap.add_argument("--parent-split", type=int, default=0,
+                    help="1: every block's sub-incidence takes the parent CSC's split threshold "
+                         "and chunk (as a per-block plan of the block-major copy would)")
     args = ap.parse_args()
 
     import torch
@@ -56,8 +59,10 @@ def main():
             u0, u1 = cuts[k], cuts[k + 1]
             loc = idx[:, lo[k]:lo[k + 1]].clone()
             loc[0] -= u0
+            kw = ({"split_threshold": inc.csc.split_threshold,
+                   "split_chunk": inc.csc.split_chunk} if args.parent_split else {})
             sub = Incidence.from_coo(loc, None, (u1 - u0, I), device=dev, validate=False,
-                                     rows_sorted=True)
+                                     rows_sorted=True, **kw)
             w = torch.empty(sub.nnz, device=dev)
             nat.check(lib.hgd_edge_values(None, None, dv[u0:u1].contiguous().data_ptr(),
                                           sub.csc.col.data_ptr(), sub.nnz, w.data_ptr(),
@@ -77,7 +82,9 @@ def main():
         return Y
 
     ref = plain()
-    res = {"dim": d, "zipf": args.zipf, "nnz": nnz, "csc_split_rows": inc.csc.n_heavy,
+    res = {"dim": d, "zipf": args.zipf, "parent_split": args.parent_split, "nnz": nnz,
+           "csc_split_rows": inc.csc.n_heavy, "split": [inc.csc.split_threshold,
+                                                        inc.csc.split_chunk],
            "max_item_degree": int(inc.csc.degrees().max()),
            "bytes_algorithmic": nnz * (4 + 4 * d) + I * (4 * d + 4) + (I + 1) * 4,
            "variants": {}}
