@@ -303,12 +303,13 @@ def test_spmm_blocked_matches_the_oracle(dev, monkeypatch, d, n_blocks, epi):
 
 
 @pytest.mark.parametrize("d", [16, 64, 256])
-def test_spmm_one_block_is_bitwise_the_plain_hop(dev, d):
+def test_spmm_one_block_is_bitwise_the_plain_hop(dev, monkeypatch, d):
     """With one block the block-major copy IS the structure and hgd_spmm_blocked walks
     [rowptr[r], rowptr[r+1]) exactly as hgd_spmm: bitwise equal."""
     from hypergraph_diffusion_for_recommendation_amd import _native as nat
     from hypergraph_diffusion_for_recommendation_amd import spmm_csr
     from hypergraph_diffusion_for_recommendation_amd.incidence import _stream
+    monkeypatch.setenv("HGD_SPMM_BLOCKS", "0")  # the plain hop, whatever the environment says
     rng, r, c, vals, inc = _blocked_case(dev, 77 + d)
     csc = inc.csc
     X = torch.from_numpy(rng.standard_normal((2001, d)).astype(np.float32)).to(dev)
