@@ -229,6 +229,7 @@ _SIGNATURES = {
     "hgd_spmm": (c_i32, [c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_i64, c_i64, c_i64,
                          c_void_p, c_i64, c_void_p, c_i64, c_i32, c_i32, c_f32,
                          ctypes.POINTER(SplitPlan), c_void_p, c_size, c_void_p]),
+    "hgd_spmm_blocks_for": (c_i32, [c_i64, c_i32]),
     "hgd_spmm_col_blocks_workspace_size": (c_size, [c_i64, c_i32]),
     "hgd_spmm_col_blocks": (c_i32, [c_void_p, c_void_p, c_i64, c_i64, c_i32, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_size, c_void_p]),

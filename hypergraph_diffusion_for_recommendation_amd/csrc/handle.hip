@@ -364,8 +364,9 @@ hgd_status csc_weights(const hgd_incidence* o, int k, const float** out, hipStre
 
 bool valid_kind(int32_t k) { return k >= HGD_SCALE_NONE && k <= HGD_SCALE_WSYM; }
 
-// Source blocks of the hop over the CSC at width d: the rule of incidence.spmm_blocks (the
-// Python host), so both hosts sum in the same order. 0 = one pass.
+// Source blocks of the hop over the CSC at width d: the structure and environment checks of
+// incidence.spmm_blocks (the Python host) and the library's size rule hgd_spmm_blocks_for, so both
+// hosts sum in the same order. 0 = one pass.
 int32_t csc_blocks(const hgd_incidence* o, int32_t d) {
   const hgd_split_plan& pl = o->plan[1];
   if (o->nnz == 0 || (pl.threshold > 0 && pl.n_heavy > 0) || (pl.flags & HGD_PLAN_SEGMENTED))
@@ -375,15 +376,7 @@ int32_t csc_blocks(const hgd_incidence* o, int32_t d) {
     const long p = std::strtol(env, nullptr, 10);
     return (p > 1 && p <= 64) ? static_cast<int32_t>(p) : 0;
   }
-  // a blocked hop runs rows wider than 128 as 128-column passes
-  const double table = static_cast<double>(o->n_rows) * std::min<int32_t>(d, 128) * 4.0;
-  if (table < 536870912.0) return 0;  // < 512 MiB: one pass
-  if (table < 1073741824.0) return 2;
-  const double x = table / (640.0 * 1048576.0);
-  double p = std::floor(x);  // Python's round(): half to even
-  const double frac = x - p;
-  if (frac > 0.5 || (frac == 0.5 && std::fmod(p, 2.0) != 0.0)) p += 1.0;
-  return static_cast<int32_t>(std::min(16.0, std::max(4.0, p)));
+  return hgd_spmm_blocks_for(o->n_rows, d);
 }
 
 // The block-major copy for P blocks and the CSC weights `w` of source kind k in its order.

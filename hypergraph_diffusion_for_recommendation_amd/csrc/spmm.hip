@@ -972,6 +972,18 @@ extern "C" hgd_status hgd_spmm(const int64_t* rowptr, const int32_t* col, const 
                         workspace_bytes, stream, "hgd_spmm");
 }
 
+extern "C" int32_t hgd_spmm_blocks_for(int64_t n_src_rows, int32_t d) {
+  // one pass's gathered table: a blocked hop runs rows wider than 128 as 128-column passes
+  const double table = static_cast<double>(n_src_rows) * (d < 128 ? d : 128) * 4.0;
+  if (n_src_rows <= 0 || d <= 0 || table < 536870912.0) return 0;  // < 512 MiB: one pass
+  if (table < 1073741824.0) return 2;                               // < 1 GiB: two blocks
+  const double x = table / (640.0 * 1048576.0);                     // ~ one per 640 MiB
+  double p = std::floor(x);  // rounded half to even
+  const double frac = x - p;
+  if (frac > 0.5 || (frac == 0.5 && std::fmod(p, 2.0) != 0.0)) p += 1.0;
+  return static_cast<int32_t>(p < 4.0 ? 4.0 : (p > 16.0 ? 16.0 : p));
+}
+
 extern "C" size_t hgd_spmm_col_blocks_workspace_size(int64_t n_rows, int32_t n_blocks) {
   if (n_rows <= 0 || n_blocks <= 0) return 0;
   const int64_t n = static_cast<int64_t>(n_blocks) * n_rows + 1;

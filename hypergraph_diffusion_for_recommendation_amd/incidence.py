@@ -32,14 +32,6 @@ DEFAULT_SPLIT_CHUNK = 512
 SPLIT_THRESHOLD_MIN = 128
 SPLIT_NNZ_PER_THRESHOLD = 8192
 SEGMENTED_MAX_AVG_DEGREE = 32
-# source-blocked hop (hgd_spmm_blocked): a gathered table of SPMM_BLOCK_TWO_BYTES up to
-# SPMM_BLOCK_MIN_BYTES runs in 2 blocks; from SPMM_BLOCK_MIN_BYTES, in about one block per
-# SPMM_BLOCK_BYTES (4..16 blocks), see spmm_blocks()
-SPMM_BLOCK_TWO_BYTES = 512 << 20
-SPMM_BLOCK_MIN_BYTES = 1 << 30
-SPMM_BLOCK_BYTES = 640 << 20
-SPMM_BLOCK_MIN = 4
-SPMM_BLOCK_MAX = 16
 # lane-group tasks needed to fill MI355X: 256 CUs × 16 waves × 4 groups of 16 lanes (d = 64)
 TARGET_GROUPS = 16384
 
@@ -245,12 +237,8 @@ def spmm_blocks(csr: CSR, d: int) -> int:
         if p < 0 or p > 64:
             raise ValueError(f"HGD_SPMM_BLOCKS must be 0..64, got {env!r}")
         return p if p > 1 else 0
-    table = csr.n_cols * min(d, 128) * 4  # a blocked hop runs wider rows as 128-column passes
-    if table < SPMM_BLOCK_TWO_BYTES:
-        return 0
-    if table < SPMM_BLOCK_MIN_BYTES:
-        return 2
-    return max(SPMM_BLOCK_MIN, min(SPMM_BLOCK_MAX, round(table / SPMM_BLOCK_BYTES)))
+    # the library's size rule (hgd_spmm_blocks_for), shared with the native incidence objects
+    return int(nat.load().hgd_spmm_blocks_for(csr.n_cols, int(d)))
 
 
 def spmm_csr(csr: CSR, X: torch.Tensor, val: Optional[torch.Tensor] = None,

@@ -213,6 +213,10 @@ hgd_status hgd_spmm(const int64_t* rowptr, const int32_t* col, const float* val,
  *              (int32 positions: nnz < 2^31, the library's limit for permutations, as perm_t).
  * Workspace: hgd_spmm_col_blocks_workspace_size.
  * ---------------------------------------------------------------------------------------- */
+/* The size rule both hosts use (measured on MI355X): the number of source
+ * blocks for a hop gathering n_src_rows rows at width d (a pass of at most 128 columns):
+ * 0 (one pass) under 512 MiB, 2 under 1 GiB, else about one per 640 MiB, 4..16. */
+int32_t hgd_spmm_blocks_for(int64_t n_src_rows, int32_t d);
 size_t hgd_spmm_col_blocks_workspace_size(int64_t n_rows, int32_t n_blocks);
 hgd_status hgd_spmm_col_blocks(const int64_t* rowptr, const int32_t* col, int64_t n_rows,
                                int64_t n_cols, int32_t n_blocks, int64_t* blk_start,

@@ -80,3 +80,16 @@ def test_blocked_implementation_bytes():
     four = profiling.impl_bytes(nnz, R, d, True, True, blocks=4)
     # + 3 Y writes and 3 Y reads, + 3 row-scale reads, block starts (R·5·8) for rowptr (R+1)·8
     assert four - plain == 6 * R * 4 * d + 3 * R * 4 + R * 5 * 8 - (R + 1) * 8
+
+
+def test_library_size_rule():
+    """hgd_spmm_blocks_for, the one size rule both hosts use (host-only, no device)."""
+    from hypergraph_diffusion_for_recommendation_amd import _native as nat
+    f = nat.load().hgd_spmm_blocks_for
+    assert f(0, 64) == 0 and f(10_000_000, 0) == 0
+    assert f(10_000_000, 64) == 4 and f(10_000_000, 128) == 8 and f(10_000_000, 512) == 8
+    # table / 640 MiB exactly halfway: rounded half to even (4.5 -> 4, 5.5 -> 6)
+    assert f(int(4.5 * (640 << 20)) // 256, 64) == 4
+    assert f(int(5.5 * (640 << 20)) // 256, 64) == 6
+    assert f(int(6.4 * (640 << 20)) // 256, 64) == 6
+    assert f(int(6.6 * (640 << 20)) // 256, 64) == 7
